@@ -1,0 +1,271 @@
+#!/usr/bin/env python
+"""Headline benchmark: flash-checkpoint save/load seconds for GPT2-1.5B DDP,
+plus goodput under an injected rank failure, on 1..8 MI355X GPUs.
+
+Metric (BASELINE.json): "ckpt save/load sec GPT2-1.5B; goodput% under
+injected faults at 1/2/4/8 GPU".  Reference numbers (DLRover flash
+checkpoint, GPT-2 xl 1.5B, A100 x2, docs/figures/ft_llm_training/
+checkpoint_{save,load}_time): DDP save (paused training) 2.2 s, DDP load
+3.7 s.
+
+What one rank does:
+  1. builds GPT-2 xl (48 layers, 1600 hidden, 1.56 B params, random init)
+     in bf16 with fp32 master weights + AdamW state in flat buffers, wrapped
+     in FlatDDP (RCCL bucketed all-reduce);
+  2. runs W untimed warm-up steps, then K timed steps; EVERY step trains on a
+     synthetic token batch (full forward/backward/all-reduce/optimizer step)
+     and then takes a flash checkpoint of model + optimizer state to host
+     shared memory (DdpCheckpointer, StorageType.MEMORY).  The save time is
+     the training pause: wall time of save_checkpoint() + the GPU snapshot it
+     enqueues (torch.cuda.synchronize() before and after);
+  3. load: after the last save lands in shm, the live parameters/optimizer
+     state are poisoned and restored from shm in place; timed until the
+     restored state is on the GPU (synchronised), and verified bit-exact;
+  4. goodput: a rank failure is injected (every rank tears down its RCCL
+     communicator), the world is re-formed under a new store prefix, the
+     state is restored from shm and training resumes; goodput = useful
+     training time / (timed wall + recovery wall).
+
+Prints ONE JSON line (rank 0).  Timed region is bracketed by barrier +
+cuda.synchronize on both sides and reduced with MAX over ranks.
+"""
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REF_SAVE_SEC = 2.2  # DLRover DDP GPT-1.5B "DLRover Async Persist" (paused training time)
+REF_LOAD_SEC = 3.7  # DLRover DDP GPT-1.5B "DLRover Recovery In-Memory"
+METRIC = "ckpt save/load sec GPT2-1.5B; goodput% under injected faults at 1/2/4/8 GPU"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--model", default="gpt2-1.5b")
+    p.add_argument("--micro-batch", type=int, default=8)
+    p.add_argument("--seq", type=int, default=1024)
+    p.add_argument("--ckpt-interval", type=int, default=1)
+    p.add_argument("--ckpt-dir", default="/tmp/dwamd_bench_ckpt")
+    p.add_argument("--no-fault", action="store_true")
+    return p.parse_args()
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def max_over_ranks(x: float, device) -> float:
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        t = torch.tensor([x], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+    return x
+
+
+def sync_all(device):
+    if dist.is_initialized():
+        dist.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("LOCAL_WORLD_SIZE", str(world))
+    os.environ.setdefault("DWAMD_SHM_PREFIX", f"bench{os.getpid() if world == 1 else os.environ.get('MASTER_PORT', '0')}")
+    cuda = torch.cuda.is_available()
+    device = torch.device("cuda", local_rank) if cuda else torch.device("cpu")
+    if cuda:
+        torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl" if cuda else "gloo", device_id=device if cuda else None)
+
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+    from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
+    from dlrover_wuqiong_amd.optimizers.fused import FusedAdamW
+    from dlrover_wuqiong_amd.parallel.ddp import FlatDDP
+    from dlrover_wuqiong_amd.parallel.flat import FlatParams
+
+    dtype = torch.bfloat16 if cuda else torch.float32
+    cfg = GPT2Config.named(args.model)
+    cfg.n_positions = max(cfg.n_positions, args.seq)
+    torch.manual_seed(1234)
+    with torch.device(device):
+        model = GPT2(cfg)
+    model.to(dtype)
+    nparams = model.num_params()
+    flat = FlatParams(model, dtype=dtype, device=device)
+    opt = FusedAdamW(flat, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0)
+    ddp = FlatDDP(model, flat, bucket_mb=128)
+    opt.grad_scale = 1.0 / max(1, world)
+    log(f"model {args.model}: {nparams/1e9:.3f} B params, world {world}, device {device}")
+
+    B, S = args.micro_batch, args.seq
+    g = torch.Generator(device="cpu").manual_seed(rank)
+    data = torch.randint(0, cfg.vocab_size, (4, B, S + 1), generator=g).to(device)
+
+    ckpt = DdpCheckpointer(os.path.join(args.ckpt_dir, f"w{world}"))
+
+    def state():
+        return {"model": model.state_dict(), "optimizer": opt.state_dict()}
+
+    step = 0
+
+    def train_step():
+        nonlocal step
+        batch = data[step % data.shape[0]]
+        loss = ddp(batch[:, :-1], batch[:, 1:])
+        loss.backward()
+        ddp.finish_gradient_sync()
+        opt.step()
+        flat.zero_grad()
+        step += 1
+        return loss
+
+    def save():
+        t0 = time.perf_counter()
+        ok = ckpt.save_checkpoint(step, state(), storage_type=StorageType.MEMORY)
+        if cuda:
+            torch.cuda.current_stream().synchronize()
+        return time.perf_counter() - t0, ok
+
+    # ---------------- warm-up
+    for i in range(args.warmup):
+        train_step()
+        if cuda:
+            torch.cuda.synchronize()
+        save()
+    ckpt.wait_latest_checkpoint()
+    sync_all(device)
+
+    # ---------------- timed: train + flash checkpoint every ckpt_interval steps
+    save_times, step_times = [], []
+    sync_all(device)
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        ts = time.perf_counter()
+        loss = train_step()
+        if cuda:
+            torch.cuda.synchronize()
+        te = time.perf_counter()
+        step_times.append(te - ts)
+        if (i + 1) % args.ckpt_interval == 0:
+            st, ok = save()
+            save_times.append(st)
+    sync_all(device)
+    t_timed = time.perf_counter() - t_start
+    t_timed = max_over_ranks(t_timed, device)
+    save_sec = max_over_ranks(statistics.mean(save_times) if save_times else 0.0, device)
+    save_max = max_over_ranks(max(save_times) if save_times else 0.0, device)
+    step_sec = max_over_ranks(statistics.median(step_times), device)
+    loss_v = float(loss.float().item())
+
+    # ---------------- load (restore from shm into live tensors)
+    ckpt.wait_latest_checkpoint()
+    sync_all(device)
+    third = opt.master if opt.master is not None else opt.exp_avg_sq
+    ref_sum = flat.data.float().sum().item(), opt.exp_avg.sum().item(), third.sum().item()
+    flat.data.zero_()
+    opt.exp_avg.zero_()
+    third.zero_()
+    sync_all(device)
+    t0 = time.perf_counter()
+    restored = ckpt.load_checkpoint(target=state())
+    if cuda:
+        torch.cuda.synchronize()
+    load_sec = time.perf_counter() - t0
+    got = flat.data.float().sum().item(), opt.exp_avg.sum().item(), third.sum().item()
+    load_ok = all(abs(a - b) <= 1e-6 * max(1.0, abs(a)) for a, b in zip(ref_sum, got))
+    load_sec = max_over_ranks(load_sec, device)
+
+    # ---------------- goodput under an injected fault (RCCL re-form + restore)
+    recover_sec = 0.0
+    goodput = None
+    if not args.no_fault:
+        sync_all(device)
+        t0 = time.perf_counter()
+        fail_step = step
+        if world > 1:
+            dist.destroy_process_group()
+            store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world,
+                                  is_master=False, timeout=__import__("datetime").timedelta(seconds=300))
+            pstore = dist.PrefixStore("dwamd_recover_1", store)
+            dist.init_process_group("nccl" if cuda else "gloo", store=pstore, rank=rank, world_size=world,
+                                    device_id=device if cuda else None)
+            ddp.pg = None
+            ckpt.close()
+            ckpt = DdpCheckpointer(os.path.join(args.ckpt_dir, f"w{world}"))
+        flat.data.zero_()  # the restarted rank has lost its GPU state
+        ckpt.load_checkpoint(target=state())
+        train_step()  # first useful step after recovery
+        if cuda:
+            torch.cuda.synchronize()
+        recover_sec = time.perf_counter() - t0 - step_sec  # exclude the useful step itself
+        recover_sec = max_over_ranks(recover_sec, device)
+        useful = args.steps * step_sec
+        goodput = 100.0 * useful / (t_timed + recover_sec)
+        assert step == fail_step + 1
+
+    tokens = B * S * world
+    ckpt_bytes = ckpt.engine._shm_handler.payload_size if ckpt.engine._shm_handler.shared_memory else 0
+    res = {
+        "metric": METRIC,
+        "value": round(save_sec, 4),
+        "unit": "s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * t_timed / args.steps, 2),
+        "higher_is_better": False,
+        "scaling": "strong",
+        "vs_baseline": round(save_sec / REF_SAVE_SEC, 4),
+        "dtype": "bf16" if cuda else "fp32",
+        "data": "synthetic tokens, random-init weights",
+        "config": {"model": "GPT2-1.5B (gpt2-xl: 48L, 1600H, 25 heads)", "global_batch": B * world,
+                   "seq_len": S, "parallelism": f"dp{world}"},
+        "save_sec_mean": round(save_sec, 4),
+        "save_sec_max": round(save_max, 4),
+        "load_sec": round(load_sec, 4),
+        "load_vs_baseline": round(load_sec / REF_LOAD_SEC, 4),
+        "load_verified": load_ok,
+        "recover_sec": round(recover_sec, 3),
+        "goodput_pct": round(goodput, 2) if goodput is not None else None,
+        "ckpt_bytes": ckpt_bytes,
+        "params": nparams,
+        "train_step_ms": round(1000 * step_sec, 2),
+        "tokens_per_s": round(tokens / step_sec, 1),
+        "loss": round(loss_v, 4),
+    }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    ckpt.close()
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        # leave no 20 GB segments behind on the box
+        import glob
+
+        for f in glob.glob(f"/dev/shm/dwamd_{os.environ['DWAMD_SHM_PREFIX']}*"):
+            try:
+                os.remove(f)
+            except OSError:
+                pass
+
+
+if __name__ == "__main__":
+    main()

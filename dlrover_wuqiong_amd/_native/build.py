@@ -1,0 +1,118 @@
+"""In-tree build of the native libraries (gfx950 only).
+
+``python -m dlrover_wuqiong_amd._native.build`` builds both libraries.
+Every ``csrc/kernels/*.hip`` translation unit is compiled separately (in
+parallel) with ``hipcc --offload-arch=gfx950`` and linked into
+``libdw_kernels.so``; ``csrc/runtime/*.cpp`` is compiled with the host
+compiler into ``libdw_runtime.so``.
+"""
+
+import glob
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+CSRC = os.path.join(PKG, "csrc")
+BUILD_DIR = os.path.join(HERE, "_build")
+ARCH = os.environ.get("DWAMD_OFFLOAD_ARCH", "gfx950")
+
+
+def runtime_lib_path():
+    return os.path.join(HERE, "libdw_runtime.so")
+
+
+def kernels_lib_path():
+    return os.path.join(HERE, "libdw_kernels.so")
+
+
+def sources_for(which):
+    if which == "runtime":
+        return sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))) + sorted(
+            glob.glob(os.path.join(CSRC, "runtime", "*.h")))
+    return sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))) + sorted(
+        glob.glob(os.path.join(CSRC, "kernels", "*.h")))
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"command failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}")
+    return r.stdout
+
+
+def _atomic_replace(tmp, dst):
+    os.replace(tmp, dst)
+
+
+def build_runtime(verbose=False):
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    srcs = [s for s in sources_for("runtime") if s.endswith(".cpp")]
+    out = runtime_lib_path()
+    tmp = out + f".tmp{os.getpid()}"
+    cxx = os.environ.get("CXX", "g++")
+    cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-msse4.2", "-pthread",
+           "-Wall", "-Wno-unused-result", "-o", tmp] + srcs + ["-lrt"]
+    o = _run(cmd)
+    if verbose and o:
+        print(o)
+    _atomic_replace(tmp, out)
+    return out
+
+
+def _compile_hip(src):
+    obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
+    deps = [src] + glob.glob(os.path.join(CSRC, "kernels", "*.h"))
+    if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
+        return obj
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+           "-mcode-object-version=5", "-munsafe-fp-atomics", "-ffp-contract=fast",
+           "-Wno-unused-result", "-I", os.path.join(CSRC, "kernels"), "-c", src,
+           "-o", obj + ".tmp"]
+    _run(cmd)
+    os.replace(obj + ".tmp", obj)
+    return obj
+
+
+def build_kernels(verbose=False, jobs=None):
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    srcs = [s for s in sources_for("kernels") if s.endswith(".hip")]
+    jobs = jobs or min(8, max(1, len(srcs)))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(_compile_hip, srcs))
+    out = kernels_lib_path()
+    tmp = out + f".tmp{os.getpid()}"
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+    o = _run(cmd)
+    if verbose and o:
+        print(o)
+    _atomic_replace(tmp, out)
+    return out
+
+
+def build_all(verbose=True):
+    r = build_runtime(verbose)
+    k = build_kernels(verbose)
+    if verbose:
+        print(f"built {r}\nbuilt {k}")
+    return r, k
+
+
+if __name__ == "__main__":
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which == "runtime":
+        build_runtime(True)
+    elif which == "kernels":
+        build_kernels(True)
+    else:
+        build_all(True)

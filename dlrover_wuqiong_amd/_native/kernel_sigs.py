@@ -1,0 +1,62 @@
+"""ctypes signatures of ``libdw_kernels.so`` (one place, checked at load)."""
+
+import ctypes as c
+
+vp, i64, i32, u32, u64, f32, cp = (c.c_void_p, c.c_int64, c.c_int, c.c_uint32, c.c_uint64,
+                                   c.c_float, c.c_char_p)
+
+SIGS = {
+    # ckpt_copy.hip
+    "dw_multi_copy": (i32, [vp, i64, vp]),
+    "dw_fill_u32": (i32, [vp, i64, u32, vp]),
+    "dw_host_register": (i32, [vp, u64]),
+    "dw_host_unregister": (i32, [vp]),
+    "dw_host_registered": (i32, [vp]),
+    "dw_memcpy_async": (i32, [vp, vp, u64, i32, vp]),
+    "dw_stream_sync": (i32, [vp]),
+    "dw_hip_error_string": (cp, [i32]),
+    "dw_kernels_abi_version": (i32, []),
+    # optim.hip
+    "dw_adam_flat": (i32, [vp, i32, vp, vp, i32, vp, vp, vp, i64, i64, f32, f32, f32, f32, f32,
+                           f32, f32, i32, vp, vp]),
+    "dw_agd_flat": (i32, [vp, i32, vp, vp, i32, vp, vp, vp, i64, i64, f32, f32, f32, f32, f32,
+                          f32, f32, f32, f32, vp, vp]),
+    "dw_sumsq_flat": (i32, [vp, i32, i64, vp, vp]),
+    "dw_clip_coef": (i32, [vp, f32, f32, vp, vp, vp]),
+    "dw_scale_flat": (i32, [vp, i32, i64, vp, vp]),
+    # norm.hip
+    "dw_norm_fwd": (i32, [vp, vp, vp, vp, vp, vp, i64, i32, f32, i32, vp]),
+    "dw_norm_bwd_blocks": (i32, [i64]),
+    "dw_norm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, vp]),
+    # elementwise.hip
+    "dw_bias_gelu_fwd": (i32, [vp, vp, vp, vp, i64, i32, vp]),
+    "dw_gelu_bwd": (i32, [vp, vp, vp, i64, vp]),
+    "dw_colsum_parts": (i32, [i64]),
+    "dw_colsum": (i32, [vp, i64, i32, vp, vp, i32, vp]),
+    "dw_swiglu_fwd": (i32, [vp, vp, i64, i32, vp]),
+    "dw_swiglu_bwd": (i32, [vp, vp, vp, i64, i32, vp]),
+    "dw_rope": (i32, [vp, vp, vp, vp, i64, i32, i32, i32, i32, vp, vp]),
+    # xent.hip
+    "dw_xent_fwd": (i32, [vp, vp, vp, vp, vp, vp, i64, i32, i64, i64, f32, vp]),
+    "dw_xent_bwd": (i32, [vp, vp, vp, vp, i32, vp, i64, i32, i64, i64, f32, vp]),
+}
+
+OPTIONAL = {
+    # attention kernels (attn_fwd.hip / attn_bwd.hip)
+    "dw_attn_fwd": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, i32, vp]),
+    "dw_attn_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32,
+                          i32, f32, i32, vp]),
+    "dw_attn_bwd_workspace": (i64, [i32, i32, i32, i32]),
+}
+
+
+def declare(lib):
+    for name, (res, args) in SIGS.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    for name, (res, args) in OPTIONAL.items():
+        f = getattr(lib, name, None)
+        if f is not None:
+            f.restype = res
+            f.argtypes = args

@@ -1,0 +1,97 @@
+// Shared device helpers for the gfx950 kernels of dlrover_wuqiong_amd.
+//
+// Conventions used by every kernel TU:
+//  * wave64 everywhere (CDNA4): lane = threadIdx.x & 63, reductions use
+//    __shfl_xor over 64 lanes;
+//  * bf16 tensors are moved as 16-byte vectors (8 x bf16) — hipcc does not
+//    auto-vectorise 2-byte loads (guide G13);
+//  * conversions use the native __bf16 type so hipcc emits
+//    v_cvt_pk_bf16_f32 (round-to-nearest-even, NaN preserving);
+//  * every launcher is `extern "C" int dw_xxx(..., void* stream)` returning
+//    the hipError_t of the launch, operating on PyTorch's current stream.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef unsigned short bf16_t;  // storage type
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+
+#define DW_LAUNCH_RET return (int)hipGetLastError()
+
+__device__ __forceinline__ float bf2f(bf16_t u) {
+  return __uint_as_float(((unsigned int)u) << 16);
+}
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+// unpack / pack 8 bf16 held in a 16-byte vector
+__device__ __forceinline__ void unpack8(const u32x4& v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    unsigned int w = v[i];
+    f[2 * i] = __uint_as_float(w << 16);
+    f[2 * i + 1] = __uint_as_float(w & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ u32x4 pack8(const float* f) {
+  u32x4 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    unsigned int lo = f2bf(f[2 * i]);
+    unsigned int hi = f2bf(f[2 * i + 1]);
+    v[i] = lo | (hi << 16);
+  }
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x = NT (multiple of 64). `red` must hold
+// NT/64 floats of LDS. Result broadcast to every thread.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t += red[i];
+  __syncthreads();
+  return t;
+}
+template <int NT>
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t = fmaxf(t, red[i]);
+  __syncthreads();
+  return t;
+}
+
+// Grid size for memory-bound grid-stride kernels (guide G11): enough blocks
+// to fill 256 CUs several times, capped.
+static inline int dw_grid_for(int64_t work_items, int per_block, int cap = 2048) {
+  int64_t g = (work_items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}

@@ -1,0 +1,559 @@
+// dw_runtime: node-local native runtime for dlrover_wuqiong_amd.
+//
+// What lives here (all host-side, no GPU dependency so it also serves CPU/gloo
+// jobs and the CPU test-suite):
+//   * POSIX shared-memory segments that survive a worker crash (the flash
+//     checkpoint buffer lives in one), with parallel pre-faulting so the first
+//     checkpoint does not pay page-fault cost inside the training loop.
+//   * Process-shared, *robust* primitives living in small named shm control
+//     blocks: a lock (pthread robust mutex: a worker that dies while holding it
+//     does not wedge the agent), a bounded message queue (mutex + 2 condvars,
+//     variable-size messages in a ring), and a versioned blob "dict".
+//     The reference implements SharedLock/SharedQueue/SharedDict as Python
+//     socket servers with pickle framing (reference
+//     dlrover/python/common/multi_process.py:162-534); here they are lock-free
+//     of any server thread: every process maps the control block directly.
+//   * Parallel file IO used by the asynchronous persister: pwrite/pread of a
+//     large buffer with N threads, optional fsync, and a parallel memcpy.
+//
+// C ABI only (loaded through ctypes) so it has no Python/PyTorch ABI coupling.
+
+#include <errno.h>
+#include <fcntl.h>
+#include <pthread.h>
+#include <signal.h>
+#include <stdint.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <string>
+#include <thread>
+#include <vector>
+
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23
+#endif
+
+extern "C" {
+
+// ---------------------------------------------------------------------------
+// Error reporting
+// ---------------------------------------------------------------------------
+static thread_local char g_err[512];
+static void set_err(const char* what) {
+  snprintf(g_err, sizeof(g_err), "%s: %s", what, strerror(errno));
+}
+const char* dw_last_error() { return g_err; }
+
+static std::string shm_path_name(const char* name) {
+  std::string n(name);
+  if (n.empty() || n[0] != '/') n = "/" + n;
+  return n;
+}
+
+// ---------------------------------------------------------------------------
+// Shared memory segments
+// ---------------------------------------------------------------------------
+// Create (or re-create with a different size) a named segment and map it.
+// Returns the mapped address or nullptr.
+void* dw_shm_create(const char* name, uint64_t size, int exclusive) {
+  std::string n = shm_path_name(name);
+  int flags = O_CREAT | O_RDWR | (exclusive ? O_EXCL : 0);
+  int fd = shm_open(n.c_str(), flags, 0600);
+  if (fd < 0) { set_err("shm_open(create)"); return nullptr; }
+  struct stat st;
+  if (fstat(fd, &st) != 0) { set_err("fstat"); close(fd); return nullptr; }
+  if ((uint64_t)st.st_size != size) {
+    if (ftruncate(fd, (off_t)size) != 0) { set_err("ftruncate"); close(fd); return nullptr; }
+  }
+  void* p = mmap(nullptr, size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) { set_err("mmap"); return nullptr; }
+  return p;
+}
+
+// Open an existing segment; *size receives its length. nullptr if absent.
+void* dw_shm_open(const char* name, uint64_t* size) {
+  std::string n = shm_path_name(name);
+  int fd = shm_open(n.c_str(), O_RDWR, 0600);
+  if (fd < 0) { set_err("shm_open"); return nullptr; }
+  struct stat st;
+  if (fstat(fd, &st) != 0) { set_err("fstat"); close(fd); return nullptr; }
+  *size = (uint64_t)st.st_size;
+  if (st.st_size == 0) { close(fd); return nullptr; }
+  void* p = mmap(nullptr, (size_t)st.st_size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) { set_err("mmap"); return nullptr; }
+  return p;
+}
+
+int dw_shm_exists(const char* name) {
+  std::string n = "/dev/shm" + shm_path_name(name);
+  struct stat st;
+  return stat(n.c_str(), &st) == 0 ? 1 : 0;
+}
+
+int64_t dw_shm_size(const char* name) {
+  std::string n = "/dev/shm" + shm_path_name(name);
+  struct stat st;
+  if (stat(n.c_str(), &st) != 0) return -1;
+  return (int64_t)st.st_size;
+}
+
+int dw_shm_close(void* p, uint64_t size) { return munmap(p, size); }
+
+int dw_shm_unlink(const char* name) {
+  std::string n = shm_path_name(name);
+  int r = shm_unlink(n.c_str());
+  if (r != 0 && errno == ENOENT) return 0;
+  return r;
+}
+
+// Touch every page of [p, p+size) with nthreads so the kernel allocates and
+// zeroes them now rather than inside a later (timed) copy.
+int dw_prefault(void* p, uint64_t size, int nthreads) {
+  if (size == 0) return 0;
+  if (madvise(p, size, MADV_POPULATE_WRITE) == 0 && nthreads <= 1) return 0;
+  nthreads = std::max(1, nthreads);
+  const uint64_t page = 4096;
+  uint64_t per = ((size / nthreads) + page - 1) / page * page;
+  std::vector<std::thread> ts;
+  for (int t = 0; t < nthreads; ++t) {
+    uint64_t b = t * per, e = std::min(size, b + per);
+    if (b >= e) break;
+    ts.emplace_back([=]() {
+      char* base = (char*)p;
+      if (madvise(base + b, e - b, MADV_POPULATE_WRITE) == 0) return;
+      for (uint64_t o = b; o < e; o += page) {
+        volatile char* c = base + o;
+        *c = *c;
+      }
+    });
+  }
+  for (auto& t : ts) t.join();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Parallel memcpy / file IO (persist path)
+// ---------------------------------------------------------------------------
+int dw_memcpy_parallel(void* dst, const void* src, uint64_t n, int nthreads) {
+  nthreads = std::max(1, nthreads);
+  if (n < (8ull << 20) || nthreads == 1) { memcpy(dst, src, n); return 0; }
+  uint64_t per = (n + nthreads - 1) / nthreads;
+  per = (per + 4095) / 4096 * 4096;
+  std::vector<std::thread> ts;
+  for (int t = 0; t < nthreads; ++t) {
+    uint64_t b = t * per, e = std::min(n, b + per);
+    if (b >= e) break;
+    ts.emplace_back([=]() { memcpy((char*)dst + b, (const char*)src + b, e - b); });
+  }
+  for (auto& t : ts) t.join();
+  return 0;
+}
+
+static int pwrite_all(int fd, const char* buf, uint64_t n, uint64_t off) {
+  while (n > 0) {
+    size_t chunk = (size_t)std::min<uint64_t>(n, 1ull << 30);
+    ssize_t w = pwrite(fd, buf, chunk, (off_t)off);
+    if (w < 0) { if (errno == EINTR) continue; return -1; }
+    buf += w; n -= (uint64_t)w; off += (uint64_t)w;
+  }
+  return 0;
+}
+
+static int pread_all(int fd, char* buf, uint64_t n, uint64_t off) {
+  while (n > 0) {
+    size_t chunk = (size_t)std::min<uint64_t>(n, 1ull << 30);
+    ssize_t r = pread(fd, buf, chunk, (off_t)off);
+    if (r < 0) { if (errno == EINTR) continue; return -1; }
+    if (r == 0) { errno = EIO; return -1; }
+    buf += r; n -= (uint64_t)r; off += (uint64_t)r;
+  }
+  return 0;
+}
+
+// Write buf[0:n] at file offset `file_off` of `path` with nthreads concurrent
+// pwrite streams. mode: bit0 = truncate/create, bit1 = fsync at the end.
+int dw_write_file(const char* path, const void* buf, uint64_t n, uint64_t file_off,
+                  int nthreads, int mode) {
+  int flags = O_WRONLY | O_CREAT | ((mode & 1) ? O_TRUNC : 0);
+  int fd = open(path, flags, 0644);
+  if (fd < 0) { set_err("open(write)"); return -1; }
+  nthreads = std::max(1, nthreads);
+  std::atomic<int> failed{0};
+  if (n < (16ull << 20)) nthreads = 1;
+  uint64_t per = (n + nthreads - 1) / nthreads;
+  per = (per + 4095) / 4096 * 4096;
+  std::vector<std::thread> ts;
+  for (int t = 0; t < nthreads; ++t) {
+    uint64_t b = t * per, e = std::min(n, b + per);
+    if (b >= e) break;
+    ts.emplace_back([&, b, e]() {
+      if (pwrite_all(fd, (const char*)buf + b, e - b, file_off + b) != 0) failed = 1;
+    });
+  }
+  for (auto& t : ts) t.join();
+  if (failed) { set_err("pwrite"); close(fd); return -1; }
+  if ((mode & 2) && fsync(fd) != 0) { set_err("fsync"); close(fd); return -1; }
+  close(fd);
+  return 0;
+}
+
+int dw_read_file(const char* path, void* buf, uint64_t n, uint64_t file_off, int nthreads) {
+  int fd = open(path, O_RDONLY);
+  if (fd < 0) { set_err("open(read)"); return -1; }
+  nthreads = std::max(1, nthreads);
+  if (n < (16ull << 20)) nthreads = 1;
+  std::atomic<int> failed{0};
+  uint64_t per = (n + nthreads - 1) / nthreads;
+  per = (per + 4095) / 4096 * 4096;
+  std::vector<std::thread> ts;
+  for (int t = 0; t < nthreads; ++t) {
+    uint64_t b = t * per, e = std::min(n, b + per);
+    if (b >= e) break;
+    ts.emplace_back([&, b, e]() {
+      if (pread_all(fd, (char*)buf + b, e - b, file_off + b) != 0) failed = 1;
+    });
+  }
+  for (auto& t : ts) t.join();
+  close(fd);
+  if (failed) { set_err("pread"); return -1; }
+  return 0;
+}
+
+// CRC32C (Castagnoli), slicing-by-1 table; used to verify persisted shards.
+static uint32_t g_crc_table[256];
+static std::atomic<int> g_crc_init{0};
+static void crc_init() {
+  if (g_crc_init.load()) return;
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = (c & 1) ? (0x82F63B78u ^ (c >> 1)) : (c >> 1);
+    g_crc_table[i] = c;
+  }
+  g_crc_init = 1;
+}
+uint32_t dw_crc32c(const void* data, uint64_t n, uint32_t seed) {
+  crc_init();
+  const uint8_t* p = (const uint8_t*)data;
+  uint32_t c = ~seed;
+#if defined(__SSE4_2__)
+  while (n >= 8) { c = (uint32_t)__builtin_ia32_crc32di(c, *(const uint64_t*)p); p += 8; n -= 8; }
+  while (n--) c = __builtin_ia32_crc32qi(c, *p++);
+#else
+  while (n--) c = g_crc_table[(c ^ *p++) & 0xFF] ^ (c >> 8);
+#endif
+  return ~c;
+}
+
+// ---------------------------------------------------------------------------
+// Control blocks: robust lock, queue, blob dict
+// ---------------------------------------------------------------------------
+static const uint64_t kMagic = 0x44574d4443544c31ull;  // "DWMDCTL1"
+
+struct CtlHeader {
+  std::atomic<uint64_t> magic;
+  pthread_mutex_t mu;
+  pthread_cond_t not_empty;
+  pthread_cond_t not_full;
+  uint32_t kind;       // 1 lock, 2 queue, 3 dict
+  uint32_t pad0;
+  uint64_t capacity;   // queue: max messages
+  uint64_t data_size;  // bytes of payload area
+  // queue ring state
+  uint64_t head;       // byte offset of the oldest message
+  uint64_t tail;       // byte offset where the next message goes
+  uint64_t count;      // messages in the queue
+  uint64_t used;       // bytes used in ring (incl. 8-byte length prefixes)
+  // dict state
+  uint64_t version;
+  uint64_t blob_len;
+  // lock state
+  int32_t held;
+  int32_t holder_pid;
+};
+
+static uint64_t ctl_total(uint64_t data_size) {
+  return (sizeof(CtlHeader) + 63) / 64 * 64 + data_size;
+}
+static char* ctl_data(CtlHeader* h) { return (char*)h + (sizeof(CtlHeader) + 63) / 64 * 64; }
+
+static int robust_lock(CtlHeader* h) {
+  int r = pthread_mutex_lock(&h->mu);
+  if (r == EOWNERDEAD) { pthread_mutex_consistent(&h->mu); r = 0; }
+  return r;
+}
+
+static void abs_deadline(struct timespec* ts, double timeout_s) {
+  clock_gettime(CLOCK_MONOTONIC, ts);
+  long sec = (long)timeout_s;
+  long nsec = (long)((timeout_s - (double)sec) * 1e9);
+  ts->tv_sec += sec;
+  ts->tv_nsec += nsec;
+  if (ts->tv_nsec >= 1000000000L) { ts->tv_sec += 1; ts->tv_nsec -= 1000000000L; }
+}
+
+// Returns the mapped control block. create=1 initialises it (idempotent if a
+// live block with the same kind already exists).
+void* dw_ctl_open(const char* name, int create, uint32_t kind, uint64_t capacity,
+                  uint64_t data_size) {
+  std::string n = shm_path_name(name);
+  uint64_t total = ctl_total(data_size);
+  if (create) {
+    int fd = shm_open(n.c_str(), O_CREAT | O_RDWR | O_EXCL, 0600);
+    bool fresh = fd >= 0;
+    if (!fresh) {
+      // Exists already: attach (e.g. agent restarted while workers alive).
+      uint64_t sz = 0;
+      void* p = nullptr;
+      // The creator may still be initialising the block: give it up to 2 s.
+      for (int spin = 0; spin < 200; ++spin) {
+        p = dw_shm_open(name, &sz);
+        if (p && sz >= sizeof(CtlHeader) && ((CtlHeader*)p)->magic.load() == kMagic) break;
+        if (p) { munmap(p, sz); p = nullptr; }
+        usleep(10000);
+      }
+      if (p && sz >= sizeof(CtlHeader)) {
+        CtlHeader* h = (CtlHeader*)p;
+        if (h->magic.load() == kMagic && h->kind == kind && sz == total) return p;
+        munmap(p, sz);
+      }
+      shm_unlink(n.c_str());
+      fd = shm_open(n.c_str(), O_CREAT | O_RDWR | O_EXCL, 0600);
+      if (fd < 0) { set_err("shm_open(ctl)"); return nullptr; }
+    }
+    if (ftruncate(fd, (off_t)total) != 0) { set_err("ftruncate(ctl)"); close(fd); return nullptr; }
+    void* p = mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) { set_err("mmap(ctl)"); return nullptr; }
+    CtlHeader* h = (CtlHeader*)p;
+    memset((void*)h, 0, sizeof(CtlHeader));
+    pthread_mutexattr_t ma;
+    pthread_mutexattr_init(&ma);
+    pthread_mutexattr_setpshared(&ma, PTHREAD_PROCESS_SHARED);
+    pthread_mutexattr_setrobust(&ma, PTHREAD_MUTEX_ROBUST);
+    pthread_mutex_init(&h->mu, &ma);
+    pthread_mutexattr_destroy(&ma);
+    pthread_condattr_t ca;
+    pthread_condattr_init(&ca);
+    pthread_condattr_setpshared(&ca, PTHREAD_PROCESS_SHARED);
+    pthread_condattr_setclock(&ca, CLOCK_MONOTONIC);
+    pthread_cond_init(&h->not_empty, &ca);
+    pthread_cond_init(&h->not_full, &ca);
+    pthread_condattr_destroy(&ca);
+    h->kind = kind;
+    h->capacity = capacity;
+    h->data_size = data_size;
+    h->magic.store(kMagic);
+    return p;
+  }
+  uint64_t sz = 0;
+  void* p = dw_shm_open(name, &sz);
+  if (!p) return nullptr;
+  CtlHeader* h = (CtlHeader*)p;
+  if (sz < sizeof(CtlHeader) || h->magic.load() != kMagic || h->kind != kind) {
+    munmap(p, sz);
+    errno = EINVAL;
+    set_err("ctl block not initialised");
+    return nullptr;
+  }
+  return p;
+}
+
+int dw_ctl_close(void* p) {
+  CtlHeader* h = (CtlHeader*)p;
+  return munmap(p, ctl_total(h->data_size));
+}
+
+// ---- lock -----------------------------------------------------------------
+// The "held" flag is separate from the pthread mutex so that acquire/release
+// may happen from different threads (the reference's SharedLock semantics).
+// timeout < 0 blocks forever; returns 1 acquired, 0 not acquired.
+int dw_lock_acquire(void* p, int blocking, double timeout) {
+  CtlHeader* h = (CtlHeader*)p;
+  if (robust_lock(h) != 0) return 0;
+  if (h->held && h->holder_pid > 0 && kill(h->holder_pid, 0) != 0 && errno == ESRCH) {
+    h->held = 0;  // holder died without releasing
+  }
+  if (!blocking) {
+    int ok = !h->held;
+    if (ok) { h->held = 1; h->holder_pid = getpid(); }
+    pthread_mutex_unlock(&h->mu);
+    return ok;
+  }
+  struct timespec dl;
+  if (timeout >= 0) abs_deadline(&dl, timeout);
+  while (h->held) {
+    int r;
+    if (timeout >= 0) {
+      r = pthread_cond_timedwait(&h->not_full, &h->mu, &dl);
+    } else {
+      struct timespec slice;
+      abs_deadline(&slice, 1.0);  // wake periodically to detect dead holders
+      r = pthread_cond_timedwait(&h->not_full, &h->mu, &slice);
+      if (r == ETIMEDOUT) r = 0;
+    }
+    if (r == EOWNERDEAD) { pthread_mutex_consistent(&h->mu); r = 0; }
+    if (h->held && h->holder_pid > 0 && kill(h->holder_pid, 0) != 0 && errno == ESRCH) h->held = 0;
+    if (r == ETIMEDOUT && h->held) { pthread_mutex_unlock(&h->mu); return 0; }
+  }
+  h->held = 1;
+  h->holder_pid = getpid();
+  pthread_mutex_unlock(&h->mu);
+  return 1;
+}
+
+int dw_lock_release(void* p) {
+  CtlHeader* h = (CtlHeader*)p;
+  if (robust_lock(h) != 0) return -1;
+  h->held = 0;
+  h->holder_pid = 0;
+  pthread_cond_broadcast(&h->not_full);
+  pthread_mutex_unlock(&h->mu);
+  return 0;
+}
+
+int dw_lock_locked(void* p) {
+  CtlHeader* h = (CtlHeader*)p;
+  if (robust_lock(h) != 0) return 0;
+  if (h->held && h->holder_pid > 0 && kill(h->holder_pid, 0) != 0 && errno == ESRCH) h->held = 0;
+  int r = h->held;
+  pthread_mutex_unlock(&h->mu);
+  return r;
+}
+
+// ---- queue ----------------------------------------------------------------
+// Messages are stored contiguously as [u64 len][bytes...] padded to 8 bytes,
+// wrapping with a zero-length "skip" marker when a message does not fit the
+// tail of the ring.
+static uint64_t pad8(uint64_t x) { return (x + 7) & ~7ull; }
+
+// returns 0 ok, 1 timeout/full, -1 error (message too large)
+int dw_queue_put(void* p, const void* msg, uint64_t len, int blocking, double timeout) {
+  CtlHeader* h = (CtlHeader*)p;
+  uint64_t need = 8 + pad8(len);
+  if (need + 8 > h->data_size) return -1;
+  if (robust_lock(h) != 0) return -1;
+  struct timespec dl;
+  if (timeout >= 0) abs_deadline(&dl, timeout);
+  for (;;) {
+    bool has_slot = h->count < h->capacity;
+    // space check (conservative: need + possible wrap waste)
+    uint64_t tail_room = h->data_size - h->tail;
+    uint64_t waste = (tail_room < need) ? tail_room : 0;
+    bool has_space = h->used + need + waste <= h->data_size;
+    if (has_slot && has_space) {
+      char* d = ctl_data(h);
+      if (waste) {
+        if (tail_room >= 8) *(uint64_t*)(d + h->tail) = ~0ull;  // wrap marker
+        h->used += waste;
+        h->tail = 0;
+      }
+      *(uint64_t*)(d + h->tail) = len;
+      memcpy(d + h->tail + 8, msg, len);
+      h->tail += need;
+      if (h->tail >= h->data_size) h->tail = 0;
+      h->used += need;
+      h->count += 1;
+      pthread_cond_signal(&h->not_empty);
+      pthread_mutex_unlock(&h->mu);
+      return 0;
+    }
+    if (!blocking) { pthread_mutex_unlock(&h->mu); return 1; }
+    int r = (timeout >= 0) ? pthread_cond_timedwait(&h->not_full, &h->mu, &dl)
+                           : pthread_cond_wait(&h->not_full, &h->mu);
+    if (r == EOWNERDEAD) { pthread_mutex_consistent(&h->mu); r = 0; }
+    if (r == ETIMEDOUT) { pthread_mutex_unlock(&h->mu); return 1; }
+  }
+}
+
+// Pops a message into buf (cap bytes). Returns message length (>=0),
+// -1 timeout/empty, -2 buffer too small (message kept; required size in *need).
+int64_t dw_queue_get(void* p, void* buf, uint64_t cap, int blocking, double timeout,
+                     uint64_t* need_out) {
+  CtlHeader* h = (CtlHeader*)p;
+  if (robust_lock(h) != 0) return -1;
+  struct timespec dl;
+  if (timeout >= 0) abs_deadline(&dl, timeout);
+  while (h->count == 0) {
+    if (!blocking) { pthread_mutex_unlock(&h->mu); return -1; }
+    int r = (timeout >= 0) ? pthread_cond_timedwait(&h->not_empty, &h->mu, &dl)
+                           : pthread_cond_wait(&h->not_empty, &h->mu);
+    if (r == EOWNERDEAD) { pthread_mutex_consistent(&h->mu); r = 0; }
+    if (r == ETIMEDOUT && h->count == 0) { pthread_mutex_unlock(&h->mu); return -1; }
+  }
+  char* d = ctl_data(h);
+  uint64_t tail_room = h->data_size - h->head;
+  if (tail_room < 8 || *(uint64_t*)(d + h->head) == ~0ull) {
+    h->used -= tail_room;
+    h->head = 0;
+  }
+  uint64_t len = *(uint64_t*)(d + h->head);
+  if (len > cap) {
+    if (need_out) *need_out = len;
+    pthread_mutex_unlock(&h->mu);
+    return -2;
+  }
+  memcpy(buf, d + h->head + 8, len);
+  uint64_t sz = 8 + pad8(len);
+  h->head += sz;
+  if (h->head >= h->data_size) h->head = 0;
+  h->used -= sz;
+  h->count -= 1;
+  if (h->count == 0) { h->head = h->tail = 0; h->used = 0; }
+  pthread_cond_signal(&h->not_full);
+  pthread_mutex_unlock(&h->mu);
+  return (int64_t)len;
+}
+
+int64_t dw_queue_size(void* p) {
+  CtlHeader* h = (CtlHeader*)p;
+  if (robust_lock(h) != 0) return -1;
+  int64_t c = (int64_t)h->count;
+  pthread_mutex_unlock(&h->mu);
+  return c;
+}
+
+// ---- dict (versioned blob) -----------------------------------------------
+int dw_blob_set(void* p, const void* data, uint64_t len) {
+  CtlHeader* h = (CtlHeader*)p;
+  if (len > h->data_size) return -1;
+  if (robust_lock(h) != 0) return -1;
+  memcpy(ctl_data(h), data, len);
+  h->blob_len = len;
+  h->version += 1;
+  pthread_cond_broadcast(&h->not_empty);
+  pthread_mutex_unlock(&h->mu);
+  return 0;
+}
+
+// Returns length, or -2 if cap too small (*need set), or -1 on error.
+int64_t dw_blob_get(void* p, void* buf, uint64_t cap, uint64_t* need_out, uint64_t* version) {
+  CtlHeader* h = (CtlHeader*)p;
+  if (robust_lock(h) != 0) return -1;
+  uint64_t len = h->blob_len;
+  if (version) *version = h->version;
+  if (len > cap) {
+    if (need_out) *need_out = len;
+    pthread_mutex_unlock(&h->mu);
+    return -2;
+  }
+  memcpy(buf, ctl_data(h), len);
+  pthread_mutex_unlock(&h->mu);
+  return (int64_t)len;
+}
+
+uint64_t dw_blob_version(void* p) {
+  CtlHeader* h = (CtlHeader*)p;
+  return __atomic_load_n(&h->version, __ATOMIC_ACQUIRE);
+}
+
+int dw_runtime_abi_version() { return 1; }
+
+}  // extern "C"

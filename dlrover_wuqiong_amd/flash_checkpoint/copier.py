@@ -1,0 +1,248 @@
+"""Byte movement between live tensors and the shm payload.
+
+GPU save path (what the training loop pays for):
+  1. ONE ``dw_multi_copy`` launch on the compute stream snapshots this
+     process's payload slice (HBM -> HBM staging buffer, 16-byte vector
+     streams, all 256 CUs).  Training may mutate parameters right after: the
+     snapshot is ordered before them on the same stream.
+  2. A background thread makes a side HIP stream wait on the snapshot event
+     and issues ``hipMemcpyAsync`` staging -> *pinned* shm (the segment is
+     registered with ``hipHostRegister``), then stamps the slice step in the
+     shm header.  PCIe time is hidden behind the next training steps.
+
+GPU load path: H2D of this process's slice from pinned shm, then (for a
+replicated checkpoint split across the node's local ranks) an RCCL
+``all_gather_into_tensor`` over xGMI re-assembles the full payload on every
+GPU, and ONE ``dw_multi_copy`` scatters it into the live tensors.
+
+Reference behaviour being replaced: per-tensor synchronous
+``torch.frombuffer(...).copy_(gpu_tensor)`` into pageable memory
+(``ckpt_saver.py:197-206``) and per-tensor H2D on load.
+"""
+
+import ctypes
+import threading
+from concurrent.futures import Future, ThreadPoolExecutor
+from typing import Callable, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..common.log import logger
+from .._native import runtime
+from .layout import Extent, Layout, TensorMeta, intersect_extents, iter_leaves
+
+CHUNK = 1 << 20  # descriptor granularity for the multi-copy kernel
+
+
+def _kern():
+    from .._native import kernels
+
+    return kernels(required=True)
+
+
+def _check(err, what):
+    if err != 0:
+        msg = _kern().dw_hip_error_string(err)
+        raise RuntimeError(f"{what}: hip error {err} ({msg.decode() if msg else ''})")
+
+
+def build_descs(pieces: List[Tuple[int, int, int]], device) -> torch.Tensor:
+    """pieces: (src_addr, dst_addr, nbytes) -> device int64 [n, 3] chunked."""
+    rows = []
+    for s, d, n in pieces:
+        o = 0
+        while o < n:
+            c = min(CHUNK, n - o)
+            rows.append((s + o, d + o, c))
+            o += c
+    if not rows:
+        return torch.empty(0, 3, dtype=torch.int64, device=device)
+    arr = np.asarray(rows, dtype=np.uint64).view(np.int64)
+    return torch.from_numpy(arr).to(device, non_blocking=False)
+
+
+def launch_multi_copy(descs: torch.Tensor, stream=None):
+    if descs.numel() == 0:
+        return
+    s = stream if stream is not None else torch.cuda.current_stream()
+    _check(_kern().dw_multi_copy(ctypes.c_void_p(descs.data_ptr()), descs.shape[0],
+                                 ctypes.c_void_p(s.cuda_stream)), "multi_copy")
+
+
+class PinnedRegistry:
+    """Tracks hipHostRegister'ed ranges of shm mappings."""
+
+    def __init__(self):
+        self._ranges: List[Tuple[int, int]] = []
+        self._lock = threading.Lock()
+
+    def ensure(self, addr: int, nbytes: int) -> bool:
+        if nbytes <= 0:
+            return True
+        page = 4096
+        a = addr // page * page
+        e = (addr + nbytes + page - 1) // page * page
+        with self._lock:
+            for (ra, re) in self._ranges:
+                if ra <= a and e <= re:
+                    return True
+            err = _kern().dw_host_register(ctypes.c_void_p(a), e - a)
+            if err != 0:
+                logger.warning(f"hipHostRegister({e - a} B) failed with {err}; using pageable copies")
+                return False
+            self._ranges.append((a, e))
+            return True
+
+    def release_all(self):
+        with self._lock:
+            for (a, _e) in self._ranges:
+                _kern().dw_host_unregister(ctypes.c_void_p(a))
+            self._ranges.clear()
+
+
+class GpuCopier:
+    """Per-process GPU <-> shm mover with a persistent staging buffer."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.side_stream = torch.cuda.Stream(device=device)
+        self.pinned = PinnedRegistry()
+        self._staging: Optional[torch.Tensor] = None
+        self._executor = ThreadPoolExecutor(max_workers=1, thread_name_prefix="dwamd-d2h")
+        self._inflight: Optional[Future] = None
+        self._desc_cache = {}
+
+    def staging(self, nbytes: int) -> torch.Tensor:
+        if self._staging is None or self._staging.numel() < nbytes:
+            self._staging = None
+            self._staging = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.device)
+        return self._staging
+
+    def wait(self):
+        f = self._inflight
+        if f is not None:
+            f.result()
+            self._inflight = None
+
+    def busy(self) -> bool:
+        return self._inflight is not None and not self._inflight.done()
+
+    # ----------------------------------------------------------------- save
+    def save_slice(self, layout: Layout, shm_payload_addr: int, lo: int, hi: int,
+                   on_done: Callable[[], None], sync: bool = False):
+        """Snapshot payload bytes [lo, hi) of ``layout`` and flush to shm."""
+        self.wait()  # the staging buffer is reused
+        n = hi - lo
+        cur = torch.cuda.current_stream(self.device)
+        if n > 0:
+            stg = self.staging(n)
+            base = stg.data_ptr()
+            key = (layout.signature, lo, hi, base, tuple(e.src_ptr for e in layout.extents))
+            descs = self._desc_cache.get(key)
+            if descs is None:
+                pieces = [(e.src_ptr + (a - e.offset), base + (a - lo), b - a)
+                          for e, a, b in intersect_extents(layout.gpu_extents(), lo, hi)]
+                descs = build_descs(pieces, self.device)
+                self._desc_cache = {key: descs}
+            launch_multi_copy(descs, cur)
+            # CPU tensors go straight to shm (small: counters, rng state...)
+            for e, a, b in intersect_extents(layout.cpu_extents(), lo, hi):
+                runtime().dw_memcpy_parallel(ctypes.c_void_p(shm_payload_addr + a),
+                                             ctypes.c_void_p(e.src_ptr + (a - e.offset)), b - a, 4)
+            pinned = self.pinned.ensure(shm_payload_addr + lo, n)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+
+        def flush():
+            if n > 0:
+                with torch.cuda.stream(self.side_stream):
+                    self.side_stream.wait_event(ev)
+                    err = _kern().dw_memcpy_async(ctypes.c_void_p(shm_payload_addr + lo),
+                                                  ctypes.c_void_p(self._staging.data_ptr()), n,
+                                                  1 if pinned else 3,
+                                                  ctypes.c_void_p(self.side_stream.cuda_stream))
+                    _check(err, "D2H flush")
+                self.side_stream.synchronize()
+            else:
+                ev.synchronize()
+            on_done()
+
+        if sync:
+            flush()
+        else:
+            self._inflight = self._executor.submit(flush)
+
+    # ----------------------------------------------------------------- load
+    def restore(self, pieces_gpu: List[Tuple[int, int, int]], shm_payload_addr: int, payload_bytes: int,
+                lo: int, hi: int, gather_group=None, world: int = 1):
+        """Restore GPU targets.
+
+        pieces_gpu: (payload_off, dst_addr, nbytes) for every GPU target.
+        If ``gather_group`` is None this process copies every piece itself
+        (H2D straight into the targets).  Otherwise this process H2D's only
+        its slice [lo, hi) into a full-size staging buffer, the group
+        all-gathers, and one kernel scatters into the targets.
+        """
+        cur = torch.cuda.current_stream(self.device)
+        if gather_group is None or world <= 1:
+            merged = _merge_pieces(pieces_gpu)
+            for off, dst, n in merged:
+                self.pinned.ensure(shm_payload_addr + off, n)
+            for off, dst, n in merged:
+                _check(_kern().dw_memcpy_async(ctypes.c_void_p(dst), ctypes.c_void_p(shm_payload_addr + off), n,
+                                               0, ctypes.c_void_p(cur.cuda_stream)), "H2D restore")
+            return
+        import torch.distributed as dist
+
+        per = hi - lo
+        stg = self.staging(per * world)
+        # every rank's slice has the same size `per` (last one may be short in
+        # payload terms but is padded): copy what exists.
+        real = max(0, min(hi, payload_bytes) - lo)
+        if real > 0:
+            self.pinned.ensure(shm_payload_addr + lo, real)
+            _check(_kern().dw_memcpy_async(ctypes.c_void_p(stg.data_ptr() + lo),
+                                           ctypes.c_void_p(shm_payload_addr + lo), real, 0,
+                                           ctypes.c_void_p(cur.cuda_stream)), "H2D slice")
+        full = stg[: per * world]
+        mine = full[lo: lo + per]
+        dist.all_gather_into_tensor(full, mine, group=gather_group)
+        base = stg.data_ptr()
+        descs = build_descs([(base + off, dst, n) for off, dst, n in _merge_pieces(pieces_gpu)], self.device)
+        launch_multi_copy(descs, cur)
+
+    def close(self):
+        try:
+            self.wait()
+        finally:
+            self._executor.shutdown(wait=True)
+            self.pinned.release_all()
+            self._staging = None
+
+
+def _merge_pieces(pieces: List[Tuple[int, int, int]]) -> List[Tuple[int, int, int]]:
+    ps = sorted(pieces)
+    out: List[List[int]] = []
+    for off, dst, n in ps:
+        if out and out[-1][0] + out[-1][2] == off and out[-1][1] + out[-1][2] == dst:
+            out[-1][2] += n
+        else:
+            out.append([off, dst, n])
+    return [tuple(x) for x in out]
+
+
+def match_targets(meta_tree, target) -> Tuple[List[Tuple[TensorMeta, torch.Tensor]], bool]:
+    """Pair TensorMeta leaves with same-shaped tensors of ``target`` (same
+    tree structure).  Returns (pairs, structure_ok)."""
+    metas = iter_leaves(meta_tree)
+    tgts = iter_leaves(target)
+    if len(metas) != len(tgts):
+        return [], False
+    pairs = []
+    for m, t in zip(metas, tgts):
+        if isinstance(m, TensorMeta):
+            if not torch.is_tensor(t) or t.numel() != m.numel or t.dtype != m.dtype:
+                return [], False
+            pairs.append((m, t))
+    return pairs, True

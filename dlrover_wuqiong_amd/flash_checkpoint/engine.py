@@ -1,0 +1,534 @@
+"""Trainer-side flash-checkpoint engine.
+
+Runs inside every training process.  ``save_to_memory`` snapshots the state
+dict into the node's shared memory (see ``copier.py`` for the GPU data path)
+and returns as soon as the GPU snapshot kernel is enqueued; the agent (or a
+local saver thread when not launched by ``dwamd-run``) persists shm to
+storage asynchronously.  ``load`` restores from shm when every rank holds the
+same complete step, otherwise from storage.
+
+Parity: reference ``dlrover/trainer/torch/flash_checkpoint/engine.py``
+(``CheckpointEngine`` :136-435, ``check_all_rank_ready`` :53,
+``verify_all_rank_step_consistent`` :70, ``start_saver_process`` :114) and
+``full_ckpt_engine.py`` (``FullCheckpointEngine``).
+
+Replicated vs sharded state:
+ * ``replicated=True`` (DDP): the node holds ONE copy; each of the L local
+   ranks snapshots and flushes 1/L of it (parallel PCIe links), and restore
+   H2D's 1/L per rank + RCCL all-gather over xGMI.
+ * ``replicated=False`` (FSDP/ZeRO/Megatron shards): one segment per local
+   rank, each rank moves its own shard.
+"""
+
+import os
+import threading
+import time
+from abc import ABC, abstractmethod
+from datetime import timedelta
+from typing import Any, Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..common import env_utils
+from ..common.constants import CheckpointConstant
+from ..common.log import logger
+from ..common.multi_process import SharedLock, SharedQueue
+from ..common.serialize import ClassMeta
+from ..common.storage import CheckpointStorage, get_checkpoint_storage
+from .layout import Layout, TensorMeta, iter_leaves, plan_layout, split_ranges, traverse
+from .shm_handler import (DLROVER_CKPT_CONFIG_KEY, EVENT_QUEUE_SIZE, CheckpointConfig,
+                          CheckpointSharedObjPrefix, SharedMemoryHandler)
+
+
+class CheckpointEventType:
+    SAVE = 1
+    UPDATE_SHARD = 2
+    EXIT = 3
+
+
+class CheckpointEvent:
+    def __init__(self, type=CheckpointEventType.SAVE, step=0, global_shard_num=0):
+        self.type = type
+        self.step = step
+        self.global_shard_num = global_shard_num
+
+    def __repr__(self):
+        return f"CheckpointEvent(type={self.type}, step={self.step}, shards={self.global_shard_num})"
+
+
+def _ctl_reduce_min(group, value: int) -> int:
+    if not dist.is_available() or not dist.is_initialized():
+        return value
+    t = torch.tensor([value], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return int(t.item())
+
+
+def check_all_rank_ready(group, ready: bool) -> bool:
+    """True iff every rank of ``group`` is ready (CPU/gloo collective: no GPU
+    stream sync is needed to take the decision)."""
+    return _ctl_reduce_min(group, 1 if ready else 0) == 1
+
+
+def verify_all_rank_step_consistent(group, step: int) -> bool:
+    if not dist.is_available() or not dist.is_initialized():
+        return True
+    t = torch.tensor([step, -step], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return int(t[0]) == step and -int(t[1]) == step
+
+
+class _LocalSaverThread:
+    """When the training process was not launched by the agent, local rank 0
+    hosts the asynchronous saver in a daemon thread (reference
+    ``start_saver_process`` forks a process instead; a thread avoids forking
+    a GPU-initialised process)."""
+
+    started_for = None  # shm namespace the saver listens on
+
+    @classmethod
+    def ensure(cls):
+        from ..common.multi_process import shm_name
+
+        ns = shm_name("", "")
+        if cls.started_for == ns or env_utils.is_under_agent():
+            return
+        if env_utils.get_local_rank() != 0:
+            return
+        from ..elastic_agent.ckpt_saver import AsyncCheckpointSaver
+
+        AsyncCheckpointSaver.start_async_saving_ckpt()
+        cls.started_for = ns
+
+
+class CheckpointEngine(ABC):
+    def __init__(self, checkpoint_dir: str, storage: Optional[CheckpointStorage] = None,
+                 comm_backend: str = "", save_timeout: int = CheckpointConstant.SAVE_TIMEOUT,
+                 replica_count: int = 0, replicated: bool = False):
+        _LocalSaverThread.ensure()
+        self.checkpoint_dir = checkpoint_dir
+        self.storage = storage or get_checkpoint_storage()
+        self._save_timeout = save_timeout
+        self._replicated = replicated
+        self._local_rank = env_utils.get_local_rank()
+        self._local_world = env_utils.get_local_world_size()
+        self._rank = 0
+        self._world = 1
+        self._group_rank = env_utils.get_group_rank()
+        if dist.is_available() and dist.is_initialized():
+            self._rank = dist.get_rank()
+            self._world = dist.get_world_size()
+            self._local_world = min(self._local_world, self._world) or 1
+        self._cached_step = 0
+        self._restart_count = env_utils.get_torch_restart_count()
+        self.local_shard_num = self.get_local_shard_num()
+        self.local_shard_id = 0 if self._replicated else self._local_rank % max(1, self.local_shard_num)
+        self._num_slices = self._local_world if self._replicated else 1
+        self._slice_idx = self._local_rank if self._replicated else 0
+        self._is_shard_owner = (self._local_rank == self.local_shard_id) if not self._replicated else (
+            self._local_rank == 0)
+
+        self._shm_handler = SharedMemoryHandler(self.local_shard_id, host=False)
+        self._shm_lock = SharedLock(CheckpointSharedObjPrefix.SHM_LOCK_NAME + str(self.local_shard_id),
+                                    create=True)
+        self._event_queue = (SharedQueue(CheckpointSharedObjPrefix.SAVE_STEP_QNAME + "0", create=True,
+                                         maxsize=EVENT_QUEUE_SIZE)
+                             if self._local_rank == 0 else None)
+        self._ctl_group = None
+        self._gather_group = None
+        self._init_groups(comm_backend)
+        self._copier = None
+        self._layout: Optional[Layout] = None
+        self._layout_key = None
+        self._lock_held = False
+        self._generation = 0
+        self._last_save_blocking = 0.0
+        self._notify_agent_to_create_saver()
+        self._update_saver_config()
+        from .replica import CkptReplicaManager
+
+        self._replica_manager = CkptReplicaManager.create(self, replica_count)
+
+    # ------------------------------------------------------------ groups
+    def _init_groups(self, comm_backend: str):
+        if not (dist.is_available() and dist.is_initialized()):
+            return
+        backend = dist.get_backend()
+        # control collectives on CPU (gloo) so decisions never sync the GPU
+        if backend == "gloo":
+            self._ctl_group = None
+        else:
+            self._ctl_group = dist.new_group(backend="gloo", timeout=timedelta(seconds=120))
+        # intra-node group for the replicated all-gather restore
+        if self._replicated and self._local_world > 1:
+            n_nodes = self._world // self._local_world
+            if n_nodes <= 1:
+                self._gather_group = dist.group.WORLD if backend != "gloo" else None
+            else:
+                for node in range(n_nodes):
+                    ranks = list(range(node * self._local_world, (node + 1) * self._local_world))
+                    g = dist.new_group(ranks=ranks, backend=comm_backend or backend)
+                    if self._rank in ranks:
+                        self._gather_group = g
+
+    def _ctl_barrier(self):
+        if dist.is_available() and dist.is_initialized():
+            dist.barrier(group=self._ctl_group)
+
+    # -------------------------------------------------------- agent notify
+    def _notify_agent_to_create_saver(self):
+        if self._local_rank != 0:
+            return
+        queue = SharedQueue("factory", create=True, maxsize=4)
+        clazz = self.get_saver_class()
+        meta = ClassMeta(module_path=clazz.__module__, class_name=clazz.__name__, kwargs={
+            "checkpoint_dir": self.checkpoint_dir,
+            "storage_meta": self.storage.get_class_meta(),
+            "local_shard_num": self.local_shard_num,
+            "global_shard_num": self.get_global_shard_num(),
+            "save_timeout": self._save_timeout,
+        })
+        try:
+            queue.put(meta, timeout=5)
+        except Exception:
+            logger.warning("saver factory queue is full; the agent already has a saver")
+
+    def _update_saver_config(self):
+        if self._local_rank == 0 and self._event_queue is not None:
+            ev = CheckpointEvent(type=CheckpointEventType.UPDATE_SHARD,
+                                 global_shard_num=self.get_global_shard_num())
+            try:
+                self._event_queue.put(ev, timeout=5)
+            except Exception:
+                logger.warning("checkpoint event queue full; UPDATE_SHARD dropped")
+
+    # ------------------------------------------------------------ helpers
+    def _device_copier(self):
+        if self._copier is None and torch.cuda.is_available():
+            from .copier import GpuCopier
+
+            self._copier = GpuCopier(torch.device("cuda", torch.cuda.current_device()))
+        return self._copier
+
+    def _plan(self, state_dict) -> Layout:
+        layout, tensors = plan_layout(state_dict)
+        self._keepalive = tensors
+        return layout
+
+    def _ensure_shm(self, total: int):
+        """(Re)create the segment when the payload size changes."""
+        h = self._shm_handler
+        cur = h.payload_size if h.shared_memory is not None else -1
+        need_resize = cur != total
+        if self._replicated:
+            # every local rank plans the same layout -> same decision
+            if need_resize:
+                self._ctl_barrier()
+                if self._local_rank == 0:
+                    h.close()
+                    h.init_shared_memory(create=True, size=total)
+                    h.shared_memory.prefault(8)
+                self._ctl_barrier()
+                if self._local_rank != 0:
+                    h.close()
+                    h.init_shared_memory(create=False)
+                self._generation += 1
+        elif need_resize:
+            h.close()
+            h.init_shared_memory(create=True, size=total)
+            h.shared_memory.prefault(8)
+            self._generation += 1
+
+    # ----------------------------------------------------------- core save
+    def save_state_dict_to_memory(self, state_dict: Dict, conf: CheckpointConfig) -> bool:
+        if not self._replicated and self._local_rank != self.local_shard_id:
+            return False
+        t0 = time.perf_counter()
+        copier = self._device_copier()
+        if copier is not None:
+            copier.wait()  # previous flush must land before the staging buffer is reused
+        self._wait_own_lock_release()
+
+        acquired = False
+        if self._is_shard_owner:
+            acquired = self._shm_lock.acquire(blocking=False)
+        owner_ok = acquired if self._is_shard_owner else True
+        if not check_all_rank_ready(self._ctl_group, owner_ok and bool(state_dict)):
+            if acquired:
+                self._shm_lock.release()
+            logger.info(f"rank {self._rank} skips the memory checkpoint of step {conf.step}: "
+                        "the agent is persisting the previous one")
+            return False
+        self._lock_held = acquired
+
+        layout = self._plan(state_dict)
+        self._ensure_shm(layout.total_bytes)
+        h = self._shm_handler
+        conf.rank = self._rank
+        conf.group_rank = self._group_rank
+        conf.world_size = self._world
+        conf.num_slices = self._num_slices
+        conf.generation = self._generation
+        if self._is_shard_owner:
+            h.set_metadata(layout.meta_tree, conf)
+        lo, hi = split_ranges(layout.total_bytes, self._num_slices)[self._slice_idx]
+        step = conf.step
+
+        def on_done():
+            h.set_slice_step(self._slice_idx, step)
+            if self._is_shard_owner:
+                self._release_when_complete(step)
+
+        has_gpu = any(e.device == "cuda" for e in layout.extents)
+        if has_gpu and copier is not None:
+            copier.save_slice(layout, h.payload_addr, lo, hi, on_done)
+        else:
+            self._cpu_save_slice(layout, lo, hi)
+            on_done()
+        self._cached_step = step
+        self._last_save_blocking = time.perf_counter() - t0
+        self._replica_manager.backup(self._shm_handler)
+        return True
+
+    def _cpu_save_slice(self, layout: Layout, lo: int, hi: int):
+        import ctypes
+
+        from .._native import runtime
+        from .layout import intersect_extents
+
+        base = self._shm_handler.payload_addr
+        for e, a, b in intersect_extents(layout.extents, lo, hi):
+            if e.device == "cuda":
+                # no copier (should not happen on a GPU host): go through torch
+                t = e.keepalive
+                raise RuntimeError("GPU tensors in state dict but no GPU copier available")
+            runtime().dw_memcpy_parallel(ctypes.c_void_p(base + a), ctypes.c_void_p(e.src_ptr + (a - e.offset)),
+                                         b - a, 8)
+
+    def _release_when_complete(self, step: int):
+        """Shard owner: keep the shm lock until every slice holds ``step``."""
+        if not self._lock_held:
+            return
+        h = self._shm_handler
+        deadline = time.time() + self._save_timeout
+
+        def _wait():
+            while time.time() < deadline:
+                if all(s == step for s in h.slice_steps(self._num_slices)):
+                    break
+                time.sleep(0.0005)
+            self._lock_held = False
+            self._shm_lock.release()
+
+        if self._num_slices <= 1:
+            _wait()
+        else:
+            threading.Thread(target=_wait, daemon=True, name="dwamd-ckpt-unlock").start()
+
+    def _wait_own_lock_release(self, timeout: float = 600.0):
+        deadline = time.time() + timeout
+        while self._lock_held and time.time() < deadline:
+            time.sleep(0.0005)
+
+    def wait_for_memory_save(self):
+        """Block until this process's last snapshot is in shm."""
+        if self._copier is not None:
+            self._copier.wait()
+        self._wait_own_lock_release()
+
+    # ----------------------------------------------------------- core load
+    def get_state_dict_from_memory(self, target: Any = None):
+        """Returns (step, state_dict) from shm, or (0, {})."""
+        self._restore_memory_from_replica()
+        h = self._shm_handler
+        step = h.complete_step() if (self._replicated or self._local_rank == self.local_shard_id) else 0
+        if not verify_all_rank_step_consistent(self._ctl_group, step) or step <= 0:
+            return 0, {}
+        meta = h.metadata.get()
+        tree = meta["tree"]
+        if target is not None:
+            sd = self._restore_into(tree, target)
+            if sd is not None:
+                return step, sd
+        sd = h.load_state_dict()
+        if isinstance(sd, dict):
+            sd.pop(DLROVER_CKPT_CONFIG_KEY, None)
+        return step, sd
+
+    def _restore_into(self, tree, target):
+        """Fast path: H2D (sliced + all-gather for replicated) straight into
+        the live tensors of ``target`` (same structure as the saved dict)."""
+        from .copier import match_targets
+
+        pairs, ok = match_targets(tree, target)
+        ok_all = check_all_rank_ready(self._ctl_group, ok)
+        if not ok_all:
+            return None
+        h = self._shm_handler
+        gpu_pieces = []
+        for m, t in pairs:
+            if m.numel == 0:
+                continue
+            if t.is_cuda and t.is_contiguous():
+                gpu_pieces.append((m.offset, t.data_ptr(), m.numel * m.element_size))
+            else:
+                src = torch.frombuffer(h.shared_memory.buf, dtype=m.dtype, count=m.numel,
+                                       offset=m.offset + h.payload_addr - h.shared_memory.addr)
+                with torch.no_grad():
+                    t.copy_(src.view(t.shape))
+        total = h.payload_size
+        copier = self._device_copier() if gpu_pieces else None
+        if copier is None:
+            it = iter([t for _, t in pairs])
+            return traverse(tree, lambda v: next(it) if isinstance(v, TensorMeta) else v)
+        if self._replicated and self._num_slices > 1 and self._gather_group is not None:
+            per = split_ranges(total, self._num_slices)[0][1]
+            lo = self._slice_idx * per
+            copier.restore(gpu_pieces, h.payload_addr, total, lo, lo + per, self._gather_group, self._num_slices)
+        else:
+            copier.restore(gpu_pieces, h.payload_addr, total, 0, total)
+        it = iter([t for _, t in pairs])
+
+        def pick(v):
+            if isinstance(v, TensorMeta):
+                return next(it)
+            return v
+
+        return traverse(tree, pick)
+
+    def _restore_memory_from_replica(self):
+        if self._replica_manager.has_replica():
+            self._replica_manager.gather(self._shm_handler)
+
+    # --------------------------------------------------------- properties
+    @property
+    def last_save_blocking_sec(self) -> float:
+        return self._last_save_blocking
+
+    def close(self):
+        try:
+            if self._copier is not None:
+                self._copier.wait()
+                self._wait_own_lock_release(timeout=30)
+                self._copier.close()
+        finally:
+            self._copier = None
+            self._shm_handler.close()
+
+    # ------------------------------------------------------- abstract API
+    @abstractmethod
+    def get_saving_ranks(self) -> Optional[List[int]]:
+        ...
+
+    @abstractmethod
+    def get_saver_class(self):
+        ...
+
+    @abstractmethod
+    def get_local_shard_num(self) -> int:
+        ...
+
+    @abstractmethod
+    def get_global_shard_num(self) -> int:
+        ...
+
+    @abstractmethod
+    def save_to_memory(self, step, state_dict, paths: Dict[str, str]) -> bool:
+        ...
+
+    @abstractmethod
+    def save_to_storage(self, step, state_dict, paths: Dict[str, str]) -> bool:
+        ...
+
+    @abstractmethod
+    def load(self, resume_path: str = "", target: Any = None):
+        ...
+
+    def _notify_persist(self, step: int):
+        if self._rank == 0 and self._event_queue is not None:
+            self._event_queue.put(CheckpointEvent(type=CheckpointEventType.SAVE, step=step), timeout=60)
+
+
+class FullCheckpointEngine(CheckpointEngine):
+    """Replicated (DDP) state.  ``local_shard_num == 1``: one node copy split
+    across local ranks; ``local_shard_num == local_world``: per-rank copies
+    (reference semantics for partitioned models)."""
+
+    def __init__(self, checkpoint_dir, storage=None, local_shard_num=1, global_shard_num=1,
+                 comm_backend="", save_timeout=CheckpointConstant.SAVE_TIMEOUT, replica_count=0):
+        self._local_shard_num = max(1, local_shard_num)
+        self._global_shard_num = max(global_shard_num, self._local_shard_num)
+        super().__init__(checkpoint_dir, storage, comm_backend, save_timeout, replica_count,
+                         replicated=(self._local_shard_num == 1))
+
+    def get_saving_ranks(self):
+        return None  # every rank participates (slices)
+
+    def get_local_shard_num(self):
+        return self._local_shard_num
+
+    def get_global_shard_num(self):
+        return self._global_shard_num
+
+    def get_saver_class(self):
+        from ..elastic_agent.ckpt_saver import DdpCheckpointSaver
+
+        return DdpCheckpointSaver
+
+    def save_to_memory(self, step, state_dict, paths):
+        conf = CheckpointConfig(step=step, paths=dict(paths))
+        return self.save_state_dict_to_memory(state_dict, conf)
+
+    def save_to_storage(self, step, state_dict, paths):
+        ok = True
+        if step > self._cached_step:
+            ok = self.save_to_memory(step, state_dict, paths)
+        if dist.is_available() and dist.is_initialized():
+            dist.barrier(group=self._ctl_group)
+        if ok:
+            self._notify_persist(step)
+        return ok
+
+    def load(self, resume_path="", target=None):
+        step, sd = self.get_state_dict_from_memory(target=target)
+        if sd:
+            keys = list(sd.keys())
+            if len(keys) == 1:
+                return sd[keys[0]]
+            return sd
+        return self._load_from_storage(resume_path)
+
+    def _load_from_storage(self, resume_path=""):
+        read = lambda p: torch.load(p, map_location="cpu", weights_only=True)  # noqa: E731
+        if resume_path:
+            return self.storage.read_state_dict(resume_path, read)
+        tracker = os.path.join(self.checkpoint_dir, CheckpointConstant.TRACER_FILE_NAME)
+        content = self.storage.read(tracker)
+        if not content:
+            return {}
+        it = int(str(content).strip())
+        name = "rank_0.pt" if self._global_shard_num == 1 else f"rank_{self._rank}.pt"
+        return self.storage.read_state_dict(os.path.join(self.checkpoint_dir, str(it), name), read)
+
+
+class ShardCheckpointEngine(FullCheckpointEngine):
+    """Every rank owns a distinct shard (FSDP / ZeRO / TP-PP)."""
+
+    def __init__(self, checkpoint_dir, storage=None, comm_backend="",
+                 save_timeout=CheckpointConstant.SAVE_TIMEOUT, replica_count=0):
+        lw = env_utils.get_local_world_size()
+        ws = dist.get_world_size() if dist.is_available() and dist.is_initialized() else lw
+        super().__init__(checkpoint_dir, storage, local_shard_num=max(lw, 1), global_shard_num=max(ws, 1),
+                         comm_backend=comm_backend, save_timeout=save_timeout, replica_count=replica_count)
+
+    def get_saver_class(self):
+        from ..elastic_agent.ckpt_saver import CommonDirCheckpointSaver
+
+        return CommonDirCheckpointSaver
+
+    def load(self, resume_path="", target=None):
+        step, sd = self.get_state_dict_from_memory(target=target)
+        if sd:
+            return sd
+        return {}

@@ -1,0 +1,55 @@
+"""Glue between PyTorch tensors and the HIP kernel library.
+
+Tensors on a GPU always run the hand-written gfx950 kernels; if the kernel
+library cannot be loaded on a GPU host this raises (no silent eager
+fallback).  CPU tensors run the PyTorch reference math - that is the CPU/gloo
+execution path of the framework, also used as the numerics oracle in tests.
+"""
+
+import ctypes
+
+import torch
+
+from .._native import kernels
+
+
+class HipKernelError(RuntimeError):
+    pass
+
+
+def lib():
+    return kernels(required=True)
+
+
+def stream() -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t) -> ctypes.c_void_p:
+    if t is None:
+        return ctypes.c_void_p(0)
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def check(err: int, what: str = "kernel"):
+    if err != 0:
+        msg = lib().dw_hip_error_string(err)
+        raise HipKernelError(f"{what} failed: hip error {err} ({msg.decode() if msg else '?'})")
+
+
+def use_hip(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return 0
+    if t.dtype == torch.bfloat16:
+        return 1
+    raise HipKernelError(f"unsupported dtype {t.dtype} for HIP kernel")
+
+
+def require_bf16(*ts):
+    for t in ts:
+        if t is not None and t.dtype != torch.bfloat16:
+            raise HipKernelError(f"HIP kernel expects bf16 tensors, got {t.dtype}")

@@ -1,0 +1,94 @@
+"""Fused activations: bias+GeLU(tanh) and SwiGLU (``csrc/kernels/elementwise.hip``)."""
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import _hip
+
+
+def _colsum(x2: torch.Tensor, out_dtype) -> torch.Tensor:
+    R, C = x2.shape
+    L = _hip.lib()
+    P = L.dw_colsum_parts(R)
+    partial = torch.empty(P * C, device=x2.device, dtype=torch.float32)
+    out = torch.empty(C, device=x2.device, dtype=out_dtype)
+    _hip.check(L.dw_colsum(_hip.ptr(x2), R, C, _hip.ptr(partial), _hip.ptr(out),
+                           int(out_dtype == torch.float32), _hip.stream()), "colsum")
+    return out
+
+
+class _BiasGeluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bias):
+        C = x.shape[-1]
+        x = x.contiguous()
+        _hip.require_bf16(x, bias)
+        y = torch.empty_like(x)
+        pre = torch.empty_like(x) if bias is not None else None
+        _hip.check(_hip.lib().dw_bias_gelu_fwd(_hip.ptr(x), _hip.ptr(bias), _hip.ptr(y), _hip.ptr(pre),
+                                               x.numel(), C, _hip.stream()), "bias_gelu_fwd")
+        ctx.save_for_backward(pre if pre is not None else x)
+        ctx.has_bias = bias is not None
+        ctx.bias_dtype = bias.dtype if bias is not None else None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (pre,) = ctx.saved_tensors
+        dy = dy.contiguous().to(torch.bfloat16)
+        dx = torch.empty_like(pre)
+        _hip.check(_hip.lib().dw_gelu_bwd(_hip.ptr(dy), _hip.ptr(pre), _hip.ptr(dx), pre.numel(),
+                                          _hip.stream()), "gelu_bwd")
+        db = None
+        if ctx.has_bias:
+            C = pre.shape[-1]
+            db = _colsum(dx.view(-1, C), ctx.bias_dtype)
+        return dx, db
+
+
+def _gelu_tanh_ref(x):
+    return 0.5 * x * (1.0 + torch.tanh(math.sqrt(2.0 / math.pi) * (x + 0.044715 * x.pow(3))))
+
+
+def bias_gelu(x, bias=None):
+    """gelu_tanh(x + bias) — GPT-2's MLP activation."""
+    if _hip.use_hip(x):
+        return _BiasGeluFn.apply(x, bias)
+    y = x + bias if bias is not None else x
+    return F.gelu(y, approximate="tanh")
+
+
+class _SwiGLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        _hip.require_bf16(x)
+        C2 = x.shape[-1]
+        C = C2 // 2
+        R = x.numel() // C2
+        y = torch.empty(*x.shape[:-1], C, device=x.device, dtype=x.dtype)
+        _hip.check(_hip.lib().dw_swiglu_fwd(_hip.ptr(x), _hip.ptr(y), R, C, _hip.stream()), "swiglu_fwd")
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = dy.contiguous().to(torch.bfloat16)
+        C2 = x.shape[-1]
+        C = C2 // 2
+        R = x.numel() // C2
+        dx = torch.empty_like(x)
+        _hip.check(_hip.lib().dw_swiglu_bwd(_hip.ptr(dy), _hip.ptr(x), _hip.ptr(dx), R, C, _hip.stream()),
+                   "swiglu_bwd")
+        return dx
+
+
+def swiglu(x):
+    """silu(x[..., :C]) * x[..., C:] for x of last dim 2C (fused gate|up)."""
+    if _hip.use_hip(x):
+        return _SwiGLUFn.apply(x)
+    a, b = x.chunk(2, dim=-1)
+    return F.silu(a) * b

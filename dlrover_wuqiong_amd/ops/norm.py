@@ -1,0 +1,93 @@
+"""Fused LayerNorm / RMSNorm (HIP kernels in ``csrc/kernels/norm.hip``).
+
+Parity: reference ``atorch/atorch/normalization/layernorm.py``
+(``AtorchLayerNorm``) and the RMSNorm of its Llama modules.
+"""
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _hip
+
+
+class _NormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps, rms):
+        H = x.shape[-1]
+        x2 = x.contiguous().view(-1, H)
+        R = x2.shape[0]
+        _hip.require_bf16(x2, weight, bias)
+        y = torch.empty_like(x2)
+        mean = None if rms else torch.empty(R, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(R, device=x.device, dtype=torch.float32)
+        _hip.check(_hip.lib().dw_norm_fwd(_hip.ptr(x2), _hip.ptr(weight), _hip.ptr(bias), _hip.ptr(y),
+                                          _hip.ptr(mean), _hip.ptr(rstd), R, H, float(eps), int(rms),
+                                          _hip.stream()), "norm_fwd")
+        ctx.save_for_backward(x2, weight, mean, rstd)
+        ctx.rms = rms
+        ctx.has_bias = bias is not None
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight, mean, rstd = ctx.saved_tensors
+        H = x2.shape[-1]
+        R = x2.shape[0]
+        dy2 = dy.contiguous().view(-1, H)
+        if dy2.dtype != torch.bfloat16:
+            dy2 = dy2.to(torch.bfloat16)
+        L = _hip.lib()
+        nblk = L.dw_norm_bwd_blocks(R)
+        partial = torch.empty(nblk * 2 * H, device=x2.device, dtype=torch.float32)
+        dx = torch.empty_like(x2)
+        dgamma = torch.empty(H, device=x2.device, dtype=weight.dtype)
+        dbeta = torch.empty(H, device=x2.device, dtype=weight.dtype) if ctx.has_bias else None
+        _hip.check(L.dw_norm_bwd(_hip.ptr(dy2), _hip.ptr(x2), _hip.ptr(weight), _hip.ptr(mean),
+                                 _hip.ptr(rstd), _hip.ptr(dx), _hip.ptr(dgamma), _hip.ptr(dbeta),
+                                 _hip.ptr(partial), R, H, int(ctx.rms),
+                                 int(weight.dtype == torch.float32), _hip.stream()), "norm_bwd")
+        return dx.view(dy.shape), dgamma, dbeta, None, None
+
+
+def layer_norm(x, weight, bias, eps: float = 1e-5):
+    if _hip.use_hip(x):
+        return _NormFn.apply(x, weight, bias, eps, False)
+    return F.layer_norm(x, (x.shape[-1],), weight, bias, eps)
+
+
+def rms_norm(x, weight, eps: float = 1e-6):
+    if _hip.use_hip(x):
+        return _NormFn.apply(x, weight, None, eps, True)
+    xf = x.float()
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    return (y * weight.float()).to(x.dtype)
+
+
+class LayerNorm(nn.Module):
+    """Drop-in for ``nn.LayerNorm`` (last-dim only) on the fused kernel."""
+
+    def __init__(self, hidden, eps=1e-5, bias=True, device=None, dtype=None):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(hidden, device=device, dtype=dtype))
+        self.bias = nn.Parameter(torch.zeros(hidden, device=device, dtype=dtype)) if bias else None
+
+    def forward(self, x):
+        if self.bias is None and _hip.use_hip(x):
+            zeros = torch.zeros_like(self.weight)
+            return _NormFn.apply(x, self.weight, zeros, self.eps, False)
+        return layer_norm(x, self.weight, self.bias, self.eps)
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, hidden, eps=1e-6, device=None, dtype=None):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(hidden, device=device, dtype=dtype))
+
+    def forward(self, x):
+        return rms_norm(x, self.weight, self.eps)
+
+
+AtorchLayerNorm = LayerNorm  # reference-compatible name

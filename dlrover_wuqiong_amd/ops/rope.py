@@ -1,0 +1,70 @@
+"""Rotary position embedding (rotate-half convention) on a host-built
+cos/sin table (``csrc/kernels/elementwise.hip:dw_rope``)."""
+
+import torch
+
+from . import _hip
+
+_TABLES = {}
+
+
+def rope_table(seq_len: int, head_dim: int, base: float = 10000.0, device="cpu"):
+    key = (seq_len, head_dim, base, str(device))
+    t = _TABLES.get(key)
+    if t is None:
+        inv = 1.0 / (base ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+        pos = torch.arange(seq_len, dtype=torch.float64)
+        freqs = torch.outer(pos, inv)
+        t = (freqs.cos().float().to(device).contiguous(), freqs.sin().float().to(device).contiguous())
+        _TABLES[key] = t
+    return t
+
+
+def _rope_ref(x, cos, sin, sign=1.0, pos_ids=None):
+    # x: [B, S, NH, D]
+    D = x.shape[-1]
+    h = D // 2
+    S = x.shape[1]
+    c = cos[:S] if pos_ids is None else cos[pos_ids]
+    s = sin[:S] if pos_ids is None else sin[pos_ids]
+    if pos_ids is None:
+        c = c[None, :, None, :]
+        s = s[None, :, None, :]
+    else:
+        c = c.view(x.shape[0], S, 1, h)
+        s = s.view(x.shape[0], S, 1, h)
+    s = s * sign
+    xf = x.float()
+    a, b = xf[..., :h], xf[..., h:]
+    return torch.cat([a * c - b * s, b * c + a * s], dim=-1).to(x.dtype)
+
+
+class _RopeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cos, sin, pos_ids):
+        x = x.contiguous()
+        _hip.require_bf16(x)
+        B, S, NH, D = x.shape
+        y = torch.empty_like(x)
+        pid = pos_ids.to(torch.int32).contiguous() if pos_ids is not None else None
+        _hip.check(_hip.lib().dw_rope(_hip.ptr(x), _hip.ptr(y), _hip.ptr(cos), _hip.ptr(sin), B, S, NH, D, 0,
+                                      _hip.ptr(pid), _hip.stream()), "rope")
+        ctx.save_for_backward(cos, sin, pid)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        cos, sin, pid = ctx.saved_tensors
+        dy = dy.contiguous().to(torch.bfloat16)
+        B, S, NH, D = dy.shape
+        dx = torch.empty_like(dy)
+        _hip.check(_hip.lib().dw_rope(_hip.ptr(dy), _hip.ptr(dx), _hip.ptr(cos), _hip.ptr(sin), B, S, NH, D, 1,
+                                      _hip.ptr(pid), _hip.stream()), "rope_bwd")
+        return dx, None, None, None
+
+
+def apply_rope(x, cos, sin, pos_ids=None):
+    """x: [B, S, NH, D]; cos/sin: [>=S, D/2] fp32."""
+    if _hip.use_hip(x):
+        return _RopeFn.apply(x, cos, sin, pos_ids)
+    return _rope_ref(x, cos, sin, 1.0, pos_ids)

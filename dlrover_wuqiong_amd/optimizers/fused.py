@@ -1,0 +1,203 @@
+"""Fused optimizers over :class:`FlatParams` (``csrc/kernels/optim.hip``).
+
+``FusedAdamW`` / ``FusedAGD`` keep fp32 master weights (when the model is
+bf16), exp_avg and exp_avg_sq as three flat fp32 buffers.  ``step()`` is one
+kernel launch (plus two tiny ones for global-norm clipping, which never sync
+the host: the clip coefficient stays on the device).
+
+``state_dict()`` is torch-optimizer shaped ({"state": {idx: {...}},
+"param_groups": [...]}) but every tensor in it is a view into a flat buffer,
+so a flash checkpoint of the optimizer is three contiguous extents.
+
+Parity: ATorch optimizers (atorch/atorch/optimizers/agd.py, bf16_optimizer.py,
+adam_offload.py) and the fused Adam they use.
+"""
+
+import math
+from typing import Optional
+
+import torch
+
+from ..ops import _hip
+from ..parallel.flat import FlatParams
+
+
+class _FlatOptimizer(torch.optim.Optimizer):
+    def __init__(self, flat: FlatParams, defaults: dict, master_weights: Optional[bool] = None,
+                 max_grad_norm: float = 0.0):
+        self.flat = flat
+        super().__init__(flat.params, defaults)
+        dev = flat.device
+        self.master_weights = (flat.dtype != torch.float32) if master_weights is None else master_weights
+        n = flat.numel
+        self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.master = flat.data.float().clone() if self.master_weights else None
+        self.step_count = 0
+        self.max_grad_norm = max_grad_norm
+        self.grad_scale = 1.0  # e.g. 1/world for summed DDP gradients
+        self._scalars = torch.zeros(4, dtype=torch.float32, device=dev)  # sumsq, coef, norm, pad
+        self.last_grad_norm = None
+
+    # ------------------------------------------------------------ helpers
+    def _gscale_ptr(self):
+        """Device scalar = grad_scale * clip coefficient (None if trivial)."""
+        on_gpu = self.flat.data.is_cuda
+        if self.max_grad_norm <= 0 and self.grad_scale == 1.0:
+            return None
+        if not on_gpu:
+            return None
+        L = _hip.lib()
+        s = self._scalars
+        if self.max_grad_norm > 0:
+            s[0].zero_()
+            _hip.check(L.dw_sumsq_flat(_hip.ptr(self.flat.grad), _hip.dtype_code(self.flat.grad), self.flat.numel,
+                                       _hip.ptr(s[0:1]), _hip.stream()), "sumsq")
+            _hip.check(L.dw_clip_coef(_hip.ptr(s[0:1]), float(self.max_grad_norm), float(self.grad_scale),
+                                      _hip.ptr(s[1:2]), _hip.ptr(s[2:3]), _hip.stream()), "clip_coef")
+            self.last_grad_norm = s[2]
+        else:
+            s[1].fill_(self.grad_scale)
+        return s[1:2]
+
+    def _cpu_gscale(self) -> float:
+        g = self.flat.grad.float()
+        scale = self.grad_scale
+        if self.max_grad_norm > 0:
+            nrm = float(g.norm()) * self.grad_scale
+            self.last_grad_norm = torch.tensor(nrm)
+            scale *= min(1.0, self.max_grad_norm / (nrm + 1e-6))
+        return scale
+
+    def _decay_vec(self):
+        m = self.flat.decay_mask.cpu().repeat_interleave(64)[: self.flat.numel].to(self.flat.device)
+        return m.bool()
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.flat.zero_grad()
+
+    # -------------------------------------------------------- state dict
+    def state_dict(self):
+        state = {}
+        for i, (o, c) in enumerate(self.flat.offsets):
+            p = self.flat.params[i]
+            st = {"step": torch.tensor(float(self.step_count)),
+                  "exp_avg": self.exp_avg[o:o + c].view(p.shape),
+                  "exp_avg_sq": self.exp_avg_sq[o:o + c].view(p.shape)}
+            if self.master is not None:
+                st["master_param"] = self.master[o:o + c].view(p.shape)
+            state[i] = st
+        groups = []
+        for g in self.param_groups:
+            d = {k: v for k, v in g.items() if k != "params"}
+            d["params"] = list(range(len(self.flat.params)))
+            groups.append(d)
+        return {"state": state, "param_groups": groups}
+
+    def load_state_dict(self, sd):
+        st = sd["state"]
+        with torch.no_grad():
+            for i, (o, c) in enumerate(self.flat.offsets):
+                if i not in st:
+                    continue
+                s = st[i]
+                self.exp_avg[o:o + c].copy_(s["exp_avg"].reshape(-1))
+                self.exp_avg_sq[o:o + c].copy_(s["exp_avg_sq"].reshape(-1))
+                if self.master is not None and "master_param" in s:
+                    self.master[o:o + c].copy_(s["master_param"].reshape(-1))
+                self.step_count = int(float(s["step"]))
+        for g, sg in zip(self.param_groups, sd.get("param_groups", [])):
+            for k, v in sg.items():
+                if k != "params":
+                    g[k] = v
+
+
+class FusedAdamW(_FlatOptimizer):
+    def __init__(self, flat: FlatParams, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
+                 adamw=True, master_weights=None, max_grad_norm=0.0):
+        super().__init__(flat, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay), master_weights,
+                         max_grad_norm)
+        self.adamw = adamw
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        self.step_count += 1
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        bc1 = 1.0 - b1 ** self.step_count
+        bc2 = 1.0 - b2 ** self.step_count
+        f = self.flat
+        if f.data.is_cuda:
+            gs = self._gscale_ptr()
+            _hip.check(_hip.lib().dw_adam_flat(
+                _hip.ptr(f.data), _hip.dtype_code(f.data), _hip.ptr(self.master), _hip.ptr(f.grad),
+                _hip.dtype_code(f.grad), _hip.ptr(self.exp_avg), _hip.ptr(self.exp_avg_sq), _hip.ptr(gs),
+                f.numel, 0, float(g["lr"]), float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]),
+                float(bc1), float(bc2), int(self.adamw), _hip.ptr(f.decay_mask), _hip.stream()), "adam")
+            return loss
+        # CPU path (reference math)
+        scale = self._cpu_gscale()
+        grad = f.grad.float() * scale
+        w = self.master if self.master is not None else f.data
+        decay = self._decay_vec()
+        lr, wd, eps = g["lr"], g["weight_decay"], g["eps"]
+        if not self.adamw and wd:
+            grad = grad + wd * w * decay
+        self.exp_avg.mul_(b1).add_(grad, alpha=1 - b1)
+        self.exp_avg_sq.mul_(b2).addcmul_(grad, grad, value=1 - b2)
+        denom = self.exp_avg_sq.sqrt() / math.sqrt(bc2) + eps
+        if self.adamw and wd:
+            w.sub_(lr * wd * w * decay)
+        w.addcdiv_(self.exp_avg, denom, value=-lr / bc1)
+        if self.master is not None:
+            f.data.copy_(w.to(f.data.dtype))
+        return loss
+
+
+class FusedAGD(_FlatOptimizer):
+    """AGD (reference atorch/atorch/optimizers/agd.py) on flat buffers."""
+
+    def __init__(self, flat: FlatParams, lr=1e-3, betas=(0.9, 0.999), delta=1e-5, weight_decay=0.0,
+                 clip=None, master_weights=None, max_grad_norm=0.0):
+        super().__init__(flat, dict(lr=lr, betas=betas, delta=delta, weight_decay=weight_decay, clip=clip),
+                         master_weights, max_grad_norm)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        self.step_count += 1
+        t = self.step_count
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        bc1, bc2 = 1.0 - b1 ** t, 1.0 - b2 ** t
+        bc1_prev = 1.0 - b1 ** (t - 1) if t > 1 else 0.0
+        clip = float(g["clip"]) if g["clip"] is not None else 0.0
+        f = self.flat
+        if f.data.is_cuda:
+            gs = self._gscale_ptr()
+            _hip.check(_hip.lib().dw_agd_flat(
+                _hip.ptr(f.data), _hip.dtype_code(f.data), _hip.ptr(self.master), _hip.ptr(f.grad),
+                _hip.dtype_code(f.grad), _hip.ptr(self.exp_avg), _hip.ptr(self.exp_avg_sq), _hip.ptr(gs),
+                f.numel, 0, float(g["lr"]), float(b1), float(b2), float(g["delta"]), float(g["weight_decay"]),
+                float(bc1), float(bc1_prev), float(bc2), clip, _hip.ptr(f.decay_mask), _hip.stream()), "agd")
+            return loss
+        scale = self._cpu_gscale()
+        grad = f.grad.float() * scale
+        w = self.master if self.master is not None else f.data
+        decay = self._decay_vec()
+        lr, wd = g["lr"], g["weight_decay"]
+        if wd:
+            w.mul_(torch.where(decay, 1.0 - lr * wd, 1.0))
+        m_old = self.exp_avg.clone()
+        self.exp_avg.mul_(b1).add_(grad, alpha=1 - b1)
+        upd = self.exp_avg / bc1 if t == 1 else self.exp_avg / bc1 - m_old / bc1_prev
+        self.exp_avg_sq.mul_(b2).addcmul_(upd, upd, value=1 - b2)
+        den = self.exp_avg_sq.sqrt().clamp(min=g["delta"] * math.sqrt(bc2))
+        u = self.exp_avg / den
+        if clip:
+            u.clamp_(-clip, clip)
+        w.add_(u, alpha=-lr * math.sqrt(bc2) / bc1)
+        if self.master is not None:
+            f.data.copy_(w.to(f.data.dtype))
+        return loss

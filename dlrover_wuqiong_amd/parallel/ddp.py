@@ -1,0 +1,98 @@
+"""Data parallelism over flat gradient buckets (RCCL over xGMI).
+
+Gradients live in one flat buffer (``FlatParams``); a bucket is a contiguous
+slice of it.  A post-accumulate-grad hook counts ready parameters per bucket
+and launches ``all_reduce`` on the slice as soon as the bucket is complete,
+so communication overlaps the rest of backward (RCCL runs on its own stream;
+``work.wait()`` only makes the compute stream wait, never the host).
+
+Bucket sizing for MI355X: an 8-GPU node is a fully connected xGMI mesh
+(7 links x ~153 GB/s per GPU); ring all-reduce is per-link bound, so a few
+large buckets (default 128 MiB) amortise the per-collective latency while
+still leaving several buckets to overlap with backward.
+
+Gradients are SUMMED; the optimizer divides by the world size inside its
+fused update (``grad_scale``), in fp32, instead of a separate scaling pass.
+
+Parity: reference trainers wrap models in torch DDP
+(dlrover/trainer/torch/elastic/trainer.py, atorch data_parallel/*); this is
+the framework's own replacement tuned for flat buffers.
+"""
+
+from contextlib import contextmanager
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from .flat import FlatParams
+
+
+class FlatDDP(nn.Module):
+    def __init__(self, module: nn.Module, flat: FlatParams, process_group=None, bucket_mb: int = 128,
+                 broadcast_params: bool = True):
+        super().__init__()
+        self.module = module
+        self.flat = flat
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.buckets = flat.grad_slices(bucket_mb << 20)
+        self._bucket_of = {}
+        for bi, (_s, _e, idxs) in enumerate(self.buckets):
+            for i in idxs:
+                self._bucket_of[i] = bi
+        self._pending: List[int] = []
+        self._works: List[Optional[object]] = []
+        self._sync = True
+        self._reset()
+        if self.world > 1:
+            if broadcast_params:
+                dist.broadcast(flat.data, src=self._global_src(), group=process_group)
+            for i, p in enumerate(flat.params):
+                p.register_post_accumulate_grad_hook(self._make_hook(i))
+
+    def _global_src(self):
+        if self.pg is None:
+            return 0
+        return dist.get_global_rank(self.pg, 0)
+
+    def _reset(self):
+        self._pending = [len(idxs) for (_s, _e, idxs) in self.buckets]
+        self._works = [None] * len(self.buckets)
+
+    def _make_hook(self, idx):
+        def hook(_p):
+            if not self._sync:
+                return
+            b = self._bucket_of[idx]
+            self._pending[b] -= 1
+            if self._pending[b] == 0:
+                s, e, _ = self.buckets[b]
+                self._works[b] = dist.all_reduce(self.flat.grad[s:e], group=self.pg, async_op=True)
+        return hook
+
+    def forward(self, *args, **kwargs):
+        self._reset()
+        return self.module(*args, **kwargs)
+
+    @contextmanager
+    def no_sync(self):
+        prev = self._sync
+        self._sync = False
+        try:
+            yield
+        finally:
+            self._sync = prev
+
+    def finish_gradient_sync(self):
+        """Wait for every bucket (launching any that never completed, e.g.
+        buckets holding unused parameters)."""
+        if self.world <= 1:
+            return
+        for b, (s, e, _) in enumerate(self.buckets):
+            if self._works[b] is None:
+                self._works[b] = dist.all_reduce(self.flat.grad[s:e], group=self.pg, async_op=True)
+        for w in self._works:
+            w.wait()
+        self._reset()

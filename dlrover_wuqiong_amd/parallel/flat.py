@@ -1,0 +1,97 @@
+"""Flat (contiguous) parameter and gradient buffers.
+
+Every trainable parameter of a module is re-pointed to a view of ONE flat
+buffer (``param.data``), and its ``.grad`` to a view of ONE flat gradient
+buffer.  Consequences, all deliberate for MI355X:
+
+* bucketed gradient all-reduce = contiguous slices of the flat grad buffer
+  (no pack/unpack copies before RCCL);
+* the optimizer update is one streaming kernel over the whole buffer
+  (``optim.hip``), HBM-bound at ~28 B/element;
+* a flash checkpoint of model + optimizer state is a handful of long
+  contiguous copies (``flash_checkpoint/layout.py`` coalesces by storage).
+
+Parameters are placed in *reverse* registration order so that backward
+(which produces gradients roughly from the last layer to the first) fills
+the buffer front to back and the first DDP bucket is ready first.  Every
+parameter starts on a 64-element boundary; the optimizer's weight-decay mask
+has one byte per 64-element block.
+"""
+
+from typing import Callable, Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+ALIGN = 64
+
+
+def default_no_decay(name: str, p: torch.Tensor) -> bool:
+    """GPT/Llama convention: no weight decay on biases, norms, 1-D params."""
+    return p.ndim < 2 or name.endswith(".bias") or "norm" in name.lower() or ".ln" in name
+
+
+class FlatParams:
+    def __init__(self, module: nn.Module, dtype: Optional[torch.dtype] = None, device=None,
+                 no_decay_fn: Callable[[str, torch.Tensor], bool] = default_no_decay,
+                 grad_dtype: Optional[torch.dtype] = None):
+        named = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
+        # tied weights appear once in named_parameters (dedup by identity)
+        named.reverse()
+        first = named[0][1] if named else None
+        self.dtype = dtype or (first.dtype if first is not None else torch.float32)
+        self.grad_dtype = grad_dtype or self.dtype
+        self.device = torch.device(device) if device is not None else (
+            first.device if first is not None else torch.device("cpu"))
+        self.names: List[str] = []
+        self.params: List[nn.Parameter] = []
+        self.offsets: List[Tuple[int, int]] = []  # (offset, numel)
+        off = 0
+        for n, p in named:
+            self.names.append(n)
+            self.params.append(p)
+            self.offsets.append((off, p.numel()))
+            off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+        self.numel = off
+        self.data = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
+        self.grad = torch.zeros(self.numel, dtype=self.grad_dtype, device=self.device)
+        mask = torch.ones(max(1, self.numel // ALIGN), dtype=torch.uint8)
+        for n, p, (o, c) in zip(self.names, self.params, self.offsets):
+            view = self.data[o:o + c].view_as(p)
+            with torch.no_grad():
+                view.copy_(p.data.to(self.device, self.dtype))
+            p.data = view
+            p.grad = self.grad[o:o + c].view_as(p)
+            if no_decay_fn(n, p):
+                mask[o // ALIGN:(o + c + ALIGN - 1) // ALIGN] = 0
+        self.decay_mask = mask.to(self.device)
+        self._index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
+
+    def index_of(self, p) -> int:
+        return self._index[id(p)]
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def reattach_grads(self):
+        """Re-point .grad views (e.g. after someone set grads to None)."""
+        for p, (o, c) in zip(self.params, self.offsets):
+            if p.grad is None or p.grad.data_ptr() != self.grad[o:o + c].data_ptr():
+                p.grad = self.grad[o:o + c].view_as(p)
+
+    def grad_slices(self, bucket_bytes: int) -> List[Tuple[int, int, List[int]]]:
+        """Partition [0, numel) into contiguous buckets of ~bucket_bytes
+        at parameter boundaries: (start, end, param indices)."""
+        esz = self.grad.element_size()
+        target = max(1, bucket_bytes // esz)
+        buckets = []
+        start, idxs = 0, []
+        for i, (o, c) in enumerate(self.offsets):
+            idxs.append(i)
+            end = o + (c + ALIGN - 1) // ALIGN * ALIGN
+            if end - start >= target:
+                buckets.append((start, end, idxs))
+                start, idxs = end, []
+        if idxs:
+            buckets.append((start, self.numel, idxs))
+        return buckets

@@ -1,0 +1,42 @@
+import glob
+import os
+import uuid
+
+import pytest
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) GPU")
+    config.addinivalue_line("markers", "slow: long-running test")
+
+
+@pytest.fixture(autouse=True)
+def _isolated_shm(monkeypatch):
+    """Every test gets its own shm namespace and cleans it up."""
+    prefix = "pt" + uuid.uuid4().hex[:8]
+    monkeypatch.setenv("DWAMD_SHM_PREFIX", prefix)
+    yield prefix
+    for f in glob.glob(f"/dev/shm/dwamd_{prefix}*"):
+        try:
+            os.remove(f)
+        except OSError:
+            pass
+
+
+def gpu_available():
+    try:
+        import torch
+
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+def free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p

@@ -1,0 +1,128 @@
+"""Flash checkpoint on CPU (gloo): layout, shm round trip, split (replicated)
+save across ranks, persistence format, deletion strategies."""
+
+import os
+import time
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import free_port
+
+
+def test_layout_coalesces_flat_views():
+    from dlrover_wuqiong_amd.flash_checkpoint.layout import plan_layout
+
+    flat = torch.arange(1000, dtype=torch.float32)
+    sd = {"a": flat[0:100].view(10, 10), "b": flat[100:300], "c": {"d": flat[300:1000]}, "n": 3,
+          "other": torch.ones(5)}
+    layout, _ = plan_layout(sd)
+    assert len(layout.extents) == 2  # one per storage
+    assert layout.meta_tree["n"] == 3
+    assert layout.meta_tree["c"]["d"].offset - layout.meta_tree["a"].offset == 300 * 4
+
+
+def test_single_process_memory_roundtrip(tmp_path):
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+
+    m = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.ReLU(), torch.nn.Linear(64, 8))
+    opt = torch.optim.AdamW(m.parameters())
+    m(torch.randn(2, 32)).sum().backward()
+    opt.step()
+    ck = DdpCheckpointer(str(tmp_path / "ck"))
+    sd = {"model": m.state_dict(), "optimizer": opt.state_dict(), "epoch": 3, "list": [1, torch.ones(2)]}
+    assert ck.save_checkpoint(10, sd, storage_type=StorageType.MEMORY)
+    out = ck.load_checkpoint()
+    assert out["epoch"] == 3
+    assert torch.equal(out["model"]["0.weight"], m[0].weight.detach())
+    assert torch.equal(out["optimizer"]["state"][0]["exp_avg"], opt.state[m[0].weight]["exp_avg"])
+    assert torch.equal(out["list"][1], torch.ones(2))
+    # a new state of different size re-creates the segment
+    sd2 = {"model": torch.nn.Linear(3, 3).state_dict()}
+    assert ck.save_checkpoint(11, sd2, storage_type=StorageType.MEMORY)
+    out2 = ck.load_checkpoint()
+    assert set(out2["model"].keys()) == {"weight", "bias"}
+    ck.close()
+
+
+def test_save_to_storage_and_reload(tmp_path):
+    from dlrover_wuqiong_amd.common.storage import KeepLatestStepStrategy
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+
+    d = tmp_path / "ck"
+    ck = DdpCheckpointer(str(d), deletion_strategy=KeepLatestStepStrategy(2, str(d)))
+    for step in (1, 2, 3):
+        sd = {"w": torch.full((100,), float(step))}
+        assert ck.save_checkpoint(step, sd, storage_type=StorageType.DISK)
+        deadline = time.time() + 30
+        while time.time() < deadline:
+            if (d / "dlrover_latest.txt").exists() and (d / "dlrover_latest.txt").read_text() == str(step):
+                break
+            time.sleep(0.05)
+    assert (d / "dlrover_latest.txt").read_text() == "3"
+    x = torch.load(d / "3" / "rank_0.pt", weights_only=True)
+    assert torch.equal(x["w"], torch.full((100,), 3.0))
+    # strategy keeps the newest 2 -> step 1 removed
+    assert not (d / "1").exists()
+    # fresh checkpointer with empty memory loads from storage
+    ck.close()
+    from dlrover_wuqiong_amd.flash_checkpoint.shm_handler import SharedMemoryHandler
+
+    SharedMemoryHandler(0).unlink()
+    ck2 = DdpCheckpointer(str(d))
+    out = ck2.load_checkpoint()
+    assert torch.equal(out["w"], torch.full((100,), 3.0))
+    ck2.close()
+
+
+def _split_worker(rank, world, port, root, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+        from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+
+        torch.manual_seed(0)  # replicated state on every rank
+        flat = torch.randn(3 << 20)
+        sd = {"a": flat[: 1 << 20], "b": flat[1 << 20:], "meta": {"k": "v"}}
+        ck = DdpCheckpointer(root)
+        assert ck.engine._num_slices == world
+        assert ck.save_checkpoint(4, sd, storage_type=StorageType.MEMORY)
+        dist.barrier()
+        h = ck.engine._shm_handler
+        assert h.complete_step() == 4, h.slice_steps(world)
+        out = ck.load_checkpoint()
+        ok = torch.equal(out["a"], sd["a"]) and torch.equal(out["b"], sd["b"]) and out["meta"] == {"k": "v"}
+        # persist through the saver of local rank 0
+        assert ck.save_checkpoint(5, sd, storage_type=StorageType.DISK)
+        dist.barrier()
+        if rank == 0:
+            deadline = time.time() + 60
+            f = os.path.join(root, "dlrover_latest.txt")
+            while time.time() < deadline and not os.path.exists(f):
+                time.sleep(0.05)
+            x = torch.load(os.path.join(root, "5", "rank_0.pt"), weights_only=False)
+            ok = ok and torch.equal(x["b"], sd["b"])
+        dist.barrier()
+        ck.close()
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_replicated_split_save_two_ranks(tmp_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_split_worker, args=(r, 2, port, str(tmp_path / "ck"), q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=180) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    assert sorted(res) == [(0, True), (1, True)]

@@ -1,0 +1,111 @@
+"""Native robust IPC primitives (parity: reference python/tests/test_multi_process.py)."""
+
+import multiprocessing as mp
+import os
+import queue
+import time
+
+import pytest
+
+from dlrover_wuqiong_amd.common.multi_process import SharedDict, SharedLock, SharedMemory, SharedQueue
+
+
+def test_queue_fifo_and_sizes():
+    q = SharedQueue("q1", create=True, maxsize=10, bytes_capacity=1 << 16)
+    q2 = SharedQueue("q1")
+    for i in range(10):
+        q.put({"i": i, "pad": "x" * (i * 500)})
+    with pytest.raises(queue.Full):
+        q.put(1, timeout=0.05)
+    assert q2.qsize() == 10
+    assert [q2.get()["i"] for _ in range(10)] == list(range(10))
+    assert q2.empty()
+    with pytest.raises(queue.Empty):
+        q2.get(timeout=0.05)
+    # wraparound with variable sizes
+    for r in range(50):
+        q.put(b"y" * (r * 97 % 3000))
+        assert len(q2.get()) == r * 97 % 3000
+    q.unlink()
+
+
+def test_lock_semantics():
+    a = SharedLock("l1", create=True)
+    b = SharedLock("l1")
+    assert a.acquire(blocking=False)
+    assert a.locked() and b.locked()
+    assert not b.acquire(blocking=False)
+    assert not b.acquire(blocking=True, timeout=0.1)
+    a.release()
+    assert b.acquire(blocking=False)
+    b.release()
+    a.unlink()
+
+
+def _hold_and_die(name):
+    lk = SharedLock(name)
+    lk.acquire()
+    os._exit(0)  # die while holding the lock
+
+
+def test_lock_reclaimed_from_dead_holder():
+    lk = SharedLock("l2", create=True)
+    p = mp.get_context("fork").Process(target=_hold_and_die, args=("l2",))
+    p.start()
+    p.join()
+    assert lk.acquire(blocking=True, timeout=3.0)
+    lk.release()
+    lk.unlink()
+
+
+def _producer(name, n):
+    q = SharedQueue(name)
+    for i in range(n):
+        q.put(i)
+
+
+def test_queue_cross_process():
+    q = SharedQueue("q3", create=True, maxsize=4)
+    p = mp.get_context("fork").Process(target=_producer, args=("q3", 100))
+    p.start()
+    got = [q.get(timeout=10) for _ in range(100)]
+    p.join()
+    assert got == list(range(100))
+    q.unlink()
+
+
+def test_dict_and_memory():
+    d = SharedDict("d1", create=True)
+    d2 = SharedDict("d1")
+    d.set({"a": 1, "b": [1, 2]})
+    assert d2.get() == {"a": 1, "b": [1, 2]}
+    v = d2.version()
+    d2.update({"c": 3})
+    assert d.get()["c"] == 3 and d.version() > v
+    assert d.get(local=True)["c"] == 3
+    d.unlink()
+    m = SharedMemory("m1", create=True, size=8192)
+    m.buf[100:105] = b"hello"
+    m2 = SharedMemory("m1")
+    assert bytes(m2.buf[100:105]) == b"hello"
+    assert SharedMemory.exists("m1")
+    m.unlink()
+    assert not SharedMemory.exists("m1")
+
+
+def test_storage_parallel_io(tmp_path):
+    import ctypes
+
+    from dlrover_wuqiong_amd.common.storage import PosixDiskStorage
+
+    data = os.urandom(40 << 20)
+    buf = ctypes.create_string_buffer(data, len(data))
+    st = PosixDiskStorage()
+    p = str(tmp_path / "x.bin")
+    st.write_bytes(ctypes.addressof(buf), len(data), p, threads=8)
+    out = ctypes.create_string_buffer(len(data))
+    st.read_into(p, ctypes.addressof(out), len(data), threads=8)
+    assert out.raw[: len(data)] == data
+    from dlrover_wuqiong_amd._native import runtime
+
+    assert runtime().dw_crc32c(buf, len(data), 0) == runtime().dw_crc32c(out, len(data), 0)

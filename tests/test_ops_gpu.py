@@ -1,0 +1,226 @@
+"""Numerics of every HIP kernel vs a plain PyTorch fp32 reference (GPU)."""
+
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.fixture(autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from dlrover_wuqiong_amd._native import kernels
+
+    kernels(required=True)
+
+
+@pytest.mark.parametrize("H", [256, 1600, 4096])
+@pytest.mark.parametrize("rms", [False, True])
+def test_norm_fwd_bwd(H, rms):
+    from dlrover_wuqiong_amd.ops.norm import layer_norm, rms_norm
+
+    torch.manual_seed(0)
+    x = torch.randn(777, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16).requires_grad_()
+    b = (0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16).requires_grad_()
+    dy = torch.randn(777, H, device=DEV, dtype=torch.bfloat16)
+    xf, wf, bf = x.detach().float().requires_grad_(), w.detach().float().requires_grad_(), b.detach().float().requires_grad_()
+    if rms:
+        y = rms_norm(x, w, 1e-6)
+        yr = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6) * wf
+    else:
+        y = layer_norm(x, w, b, 1e-5)
+        yr = F.layer_norm(xf, (H,), wf, bf, 1e-5)
+    assert _rel(y, yr) < 1e-2
+    y.backward(dy)
+    yr.backward(dy.float())
+    assert _rel(x.grad, xf.grad) < 2e-2
+    assert _rel(w.grad, wf.grad) < 2e-2
+    if not rms:
+        assert _rel(b.grad, bf.grad) < 2e-2
+
+
+def test_bias_gelu():
+    from dlrover_wuqiong_amd.ops.activation import bias_gelu
+
+    x = torch.randn(300, 6400, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    b = torch.randn(6400, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = bias_gelu(x, b)
+    xf, bf = x.detach().float().requires_grad_(), b.detach().float().requires_grad_()
+    yr = F.gelu(xf + bf, approximate="tanh")
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy.float())
+    assert _rel(x.grad, xf.grad) < 2e-2
+    assert _rel(b.grad, bf.grad) < 2e-2
+
+
+def test_swiglu():
+    from dlrover_wuqiong_amd.ops.activation import swiglu
+
+    x = torch.randn(257, 2 * 1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = swiglu(x)
+    xf = x.detach().float().requires_grad_()
+    a, c = xf.chunk(2, -1)
+    yr = F.silu(a) * c
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy.float())
+    assert _rel(x.grad, xf.grad) < 2e-2
+
+
+def test_rope():
+    from dlrover_wuqiong_amd.ops.rope import _rope_ref, apply_rope, rope_table
+
+    B, S, NH, D = 2, 128, 8, 128
+    cos, sin = rope_table(S, D, device=DEV)
+    x = torch.randn(B, S, NH, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = apply_rope(x, cos, sin)
+    xf = x.detach().float().requires_grad_()
+    yr = _rope_ref(xf, cos, sin)
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy.float())
+    assert _rel(x.grad, xf.grad) < 2e-2
+
+
+@pytest.mark.parametrize("V", [50304, 1000])
+def test_cross_entropy(V):
+    from dlrover_wuqiong_amd.ops.cross_entropy import cross_entropy
+
+    T = 513
+    logits = (3 * torch.randn(T, V, device=DEV)).to(torch.bfloat16).requires_grad_()
+    tgt = torch.randint(0, V, (T,), device=DEV)
+    tgt[::7] = -100
+    lf = logits.detach().float().requires_grad_()
+    loss = cross_entropy(logits, tgt)
+    ref = F.cross_entropy(lf, tgt, ignore_index=-100)
+    assert abs(loss.item() - ref.item()) < 1e-3 * max(1.0, abs(ref.item()))
+    loss.backward()
+    ref.backward()
+    assert _rel(logits.grad, lf.grad) < 2e-2
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("S,H,HKV", [(256, 4, 4), (333, 8, 2)])
+def test_flash_attention(D, causal, S, H, HKV):
+    from dlrover_wuqiong_amd.ops.attention import attention_reference, flash_attn_func
+
+    torch.manual_seed(1)
+    B = 2
+    q = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, HKV, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, HKV, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = flash_attn_func(q, k, v, causal=causal)
+    qf, kf, vf = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = attention_reference(qf, kf, vf, causal=causal)
+    assert _rel(o, orf) < 2e-2
+    do = torch.randn_like(o)
+    o.backward(do)
+    orf.backward(do.float())
+    assert _rel(q.grad, qf.grad) < 3e-2
+    assert _rel(k.grad, kf.grad) < 3e-2
+    assert _rel(v.grad, vf.grad) < 3e-2
+
+
+@pytest.mark.parametrize("n", [1000, 1 << 20, (1 << 20) + 13])
+def test_fused_adamw_matches_torch(n):
+    from dlrover_wuqiong_amd.optimizers.fused import FusedAdamW
+    from dlrover_wuqiong_amd.parallel.flat import FlatParams
+
+    torch.manual_seed(0)
+    m = torch.nn.Linear(n // 100 if n >= 1000 else 10, 100, bias=True).to(DEV)
+    ref = torch.nn.Linear(m.in_features, 100, bias=True).to(DEV)
+    ref.load_state_dict(m.state_dict())
+    flat = FlatParams(m, dtype=torch.float32)
+    opt = FusedAdamW(flat, lr=1e-2, weight_decay=0.1, max_grad_norm=0.0)
+    ropt = torch.optim.AdamW([{"params": [ref.weight], "weight_decay": 0.1},
+                              {"params": [ref.bias], "weight_decay": 0.0}], lr=1e-2)
+    for _ in range(3):
+        x = torch.randn(8, m.in_features, device=DEV)
+        m(x).square().sum().backward()
+        ref(x).square().sum().backward()
+        opt.step()
+        ropt.step()
+        flat.zero_grad()
+        ropt.zero_grad()
+    assert torch.allclose(m.weight, ref.weight, atol=1e-5, rtol=1e-4)
+    assert torch.allclose(m.bias, ref.bias, atol=1e-5, rtol=1e-4)
+
+
+def test_fused_agd_matches_reference():
+    from dlrover_wuqiong_amd.optimizers.agd import AGD
+    from dlrover_wuqiong_amd.optimizers.fused import FusedAGD
+    from dlrover_wuqiong_amd.parallel.flat import FlatParams
+
+    torch.manual_seed(0)
+    m = torch.nn.Linear(64, 32).to(DEV)
+    ref = torch.nn.Linear(64, 32).to(DEV)
+    ref.load_state_dict(m.state_dict())
+    flat = FlatParams(m, dtype=torch.float32, no_decay_fn=lambda n, p: False)
+    opt = FusedAGD(flat, lr=1e-2, weight_decay=0.01, clip=0.5)
+    ropt = AGD(ref.parameters(), lr=1e-2, weight_decay=0.01, clip=0.5)
+    for _ in range(4):
+        x = torch.randn(8, 64, device=DEV)
+        m(x).square().sum().backward()
+        ref(x).square().sum().backward()
+        opt.step()
+        ropt.step()
+        flat.zero_grad()
+        ropt.zero_grad()
+    assert torch.allclose(m.weight, ref.weight, atol=1e-5, rtol=1e-4)
+
+
+def test_multi_copy_kernel():
+    from dlrover_wuqiong_amd.flash_checkpoint.copier import build_descs, launch_multi_copy
+
+    src = torch.randint(0, 255, (5 << 20,), dtype=torch.uint8, device=DEV)
+    dst = torch.zeros_like(src)
+    pieces = [(src.data_ptr() + 3, dst.data_ptr() + 3, (3 << 20) + 5),
+              (src.data_ptr() + (4 << 20), dst.data_ptr() + (4 << 20), 777),
+              (src.data_ptr() + (4 << 20) + 1001, dst.data_ptr() + (4 << 20) + 1001, 64)]
+    launch_multi_copy(build_descs(pieces, src.device))
+    torch.cuda.synchronize()
+    for s, d, n in pieces:
+        so, do = s - src.data_ptr(), d - dst.data_ptr()
+        assert torch.equal(src[so:so + n], dst[do:do + n])
+    assert dst[:3].sum() == 0
+
+
+def test_gpt2_tiny_trains():
+    from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
+    from dlrover_wuqiong_amd.optimizers.fused import FusedAdamW
+    from dlrover_wuqiong_amd.parallel.flat import FlatParams
+
+    torch.manual_seed(0)
+    cfg = GPT2Config.named("gpt2-tiny")
+    with torch.device(DEV):
+        model = GPT2(cfg)
+    model.to(torch.bfloat16)
+    flat = FlatParams(model)
+    opt = FusedAdamW(flat, lr=3e-3)
+    x = torch.randint(0, cfg.vocab_size, (4, 65), device=DEV)
+    first = last = None
+    for i in range(30):
+        loss = model(x[:, :-1], x[:, 1:])
+        loss.backward()
+        opt.step()
+        flat.zero_grad()
+        first = first if first is not None else loss.item()
+        last = loss.item()
+    assert last < first - 1.0
