@@ -105,6 +105,69 @@ extern "C" int dw_memcpy_async(void* dst, const void* src, uint64_t bytes, int k
 
 extern "C" int dw_stream_sync(void* stream) { return (int)hipStreamSynchronize((hipStream_t)stream); }
 
+// A stream whose kernels (including the runtime's blit kernels that
+// implement hipMemcpyAsync to/from host memory) may only run on a subset of
+// the CUs: every `stride`-th CU.  The checkpoint flush runs on such a stream
+// so a multi-hundred-millisecond PCIe copy cannot occupy all 256 CUs and
+// stall the training kernels on the compute stream.
+extern "C" void* dw_stream_create_cumask(int stride, int* ncu_out) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return nullptr;
+  const int ncu = prop.multiProcessorCount;
+  const int words = (ncu + 31) / 32;
+  uint32_t mask[64] = {0};
+  int n = 0;
+  for (int cu = 0; cu < ncu && cu < 64 * 32; ++cu) {
+    if (stride <= 1 || cu % stride == 0) {
+      mask[cu / 32] |= 1u << (cu % 32);
+      ++n;
+    }
+  }
+  hipStream_t s = nullptr;
+  if (hipExtStreamCreateWithCUMask(&s, words, mask) != hipSuccess) return nullptr;
+  if (ncu_out) *ncu_out = n;
+  return (void*)s;
+}
+
+extern "C" int dw_stream_destroy(void* s) { return (int)hipStreamDestroy((hipStream_t)s); }
+
+// Non-blocking stream (no implicit sync with the legacy null stream) with a
+// priority: which = 0 lowest, 1 default, 2 highest of the device range.
+extern "C" void* dw_stream_create_prio(int which, int* prio_out) {
+  int lo = 0, hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&lo, &hi);  // lo = least, hi = greatest priority
+  const int p = which == 0 ? lo : which == 2 ? hi : (lo + hi) / 2;
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, p) != hipSuccess) return nullptr;
+  if (prio_out) *prio_out = p;
+  return (void*)s;
+}
+
+// Device-side pointer for registered host memory (zero-copy stores over PCIe).
+extern "C" void* dw_host_device_ptr(void* host) {
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, host, 0) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+  return d;
+}
+
+// Bounded-footprint copy kernel: `blocks` workgroups stream 16-byte vectors
+// (used for device->host-mapped copies where a full-chip blit would stall
+// training).
+__global__ void __launch_bounds__(256) stream_copy_kernel(const u32x4* __restrict__ s, u32x4* __restrict__ d,
+                                                          int64_t nv) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < nv; i += (int64_t)gridDim.x * 256) {
+    d[i] = __builtin_nontemporal_load(s + i);
+  }
+}
+extern "C" int dw_stream_copy(void* dst, const void* src, uint64_t bytes, int blocks, void* stream) {
+  if (((uintptr_t)dst | (uintptr_t)src | bytes) & 15) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(stream_copy_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const u32x4*)src,
+                     (u32x4*)dst, (int64_t)(bytes >> 4));
+  DW_LAUNCH_RET;
+}
+
 extern "C" const char* dw_hip_error_string(int e) { return hipGetErrorString((hipError_t)e); }
 
 extern "C" int dw_kernels_abi_version() { return 1; }

@@ -87,6 +87,16 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(const bf16_t* __restrict_
   float* acc_b = acc_g + H;        // [H]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nv = H >> 3;
+  // lane-owned column vectors c = lane + 64 j are the same for every row:
+  // accumulate dgamma/dbeta in registers when they fit (H <= 2048)
+  constexpr bool REG = VPL <= 4;
+  float rg[REG ? VPL : 1][8], rb[REG ? VPL : 1][8];
+  if constexpr (REG) {
+#pragma unroll
+    for (int j = 0; j < VPL; ++j)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) rg[j][k] = rb[j][k] = 0.f;
+  }
   for (int c = threadIdx.x; c < 2 * H; c += 256) acc_g[c] = 0.f;
   __syncthreads();
   for (int64_t row = (int64_t)blockIdx.x * 4 + wid; row < rows; row += (int64_t)gridDim.x * 4) {
@@ -95,7 +105,10 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(const bf16_t* __restrict_
     const bf16_t* xr = x + row * H;
     const bf16_t* dr = dy + row * H;
     float s1 = 0.f, s2 = 0.f;
-    for (int c = lane; c < nv; c += 64) {
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c >= nv) break;
       float xv[8], dv[8], gm[8];
       unpack8(*(const u32x4*)(xr + c * 8), xv);
       unpack8(*(const u32x4*)(dr + c * 8), dv);
@@ -106,8 +119,13 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(const bf16_t* __restrict_
         const float g = dv[k] * gm[k];
         s1 += g;
         s2 += g * xh;
-        atomicAdd(&acc_g[c * 8 + k], dv[k] * xh);
-        if (!RMS) atomicAdd(&acc_b[c * 8 + k], dv[k]);
+        if constexpr (REG) {
+          rg[j][k] += dv[k] * xh;
+          rb[j][k] += dv[k];
+        } else {
+          atomicAdd(&acc_g[c * 8 + k], dv[k] * xh);
+          if (!RMS) atomicAdd(&acc_b[c * 8 + k], dv[k]);
+        }
       }
     }
     const float m1 = RMS ? 0.f : wave_sum(s1) / (float)H;
@@ -125,6 +143,18 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(const bf16_t* __restrict_
       *(u32x4*)(dx + row * H + c * 8) = pack8(o);
     }
   }
+  if constexpr (REG) {
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c >= nv) break;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        atomicAdd(&acc_g[c * 8 + k], rg[j][k]);  // 4 waves per column: cheap
+        if (!RMS) atomicAdd(&acc_b[c * 8 + k], rb[j][k]);
+      }
+    }
+  }
   __syncthreads();
   for (int c = threadIdx.x; c < H; c += 256) {
     partial[((int64_t)blockIdx.x * 2) * H + c] = acc_g[c];
@@ -132,15 +162,22 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(const bf16_t* __restrict_
   }
 }
 
-// Sum partial rows -> dgamma/dbeta (bf16 or fp32 out). One thread per column.
+// Sum partial rows -> dgamma/dbeta (bf16 or fp32 out).  Block = 64 columns x
+// 4 row groups (each strides over the partial rows), combined through LDS.
 template <typename TO>
-__global__ void norm_bwd_reduce_kernel(const float* __restrict__ partial, int nblk, int H,
-                                       TO* __restrict__ dgamma, TO* __restrict__ dbeta) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(256) norm_bwd_reduce_kernel(const float* __restrict__ partial, int nblk, int H,
+                                                              TO* __restrict__ dgamma, TO* __restrict__ dbeta) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + cl;
   const int which = blockIdx.y;
-  if (col >= H) return;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += partial[((int64_t)b * 2 + which) * H + col];
+  if (col < H)
+    for (int b = rg; b < nblk; b += 4) s += partial[((int64_t)b * 2 + which) * H + col];
+  red[rg][cl] = s;
+  __syncthreads();
+  if (rg != 0 || col >= H) return;
+  s = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
   TO* out = which == 0 ? dgamma : dbeta;
   if (!out) return;
   if constexpr (sizeof(TO) == 2) out[col] = f2bf(s); else out[col] = s;
@@ -195,7 +232,7 @@ extern "C" int dw_norm_bwd(const void* dy, const void* x, const void* gamma, con
                          (const bf16_t*)x, (const bf16_t*)gamma, (const float*)mean, (const float*)rstd,
                          (bf16_t*)dx, (float*)partial, rows, H);
   });
-  dim3 rg((H + 255) / 256, rms ? 1 : 2);
+  dim3 rg((H + 63) / 64, rms ? 1 : 2);
   if (out_fp32)
     hipLaunchKernelGGL(norm_bwd_reduce_kernel<float>, rg, dim3(256), 0, s, (const float*)partial, nblk,
                        H, (float*)dgamma, (float*)dbeta);

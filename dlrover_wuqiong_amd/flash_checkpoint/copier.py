@@ -22,6 +22,7 @@ Reference behaviour being replaced: per-tensor synchronous
 
 import ctypes
 import threading
+import time
 from concurrent.futures import Future, ThreadPoolExecutor
 from typing import Callable, List, Optional, Tuple
 
@@ -104,9 +105,42 @@ class PinnedRegistry:
 class GpuCopier:
     """Per-process GPU <-> shm mover with a persistent staging buffer."""
 
-    def __init__(self, device: torch.device):
+    def __init__(self, device: torch.device, flush_cu_stride: Optional[int] = None):
+        import os
+
         self.device = device
-        self.side_stream = torch.cuda.Stream(device=device)
+        # The runtime implements D2H/H2D to pinned host memory with blit
+        # kernels; on a plain stream one 20 GB flush occupies every CU for
+        # ~0.4 s and stalls the training kernels.  Flush on a CU-masked stream
+        # (every `stride`-th CU) instead.
+        stride = flush_cu_stride if flush_cu_stride is not None else int(
+            os.environ.get("DWAMD_FLUSH_CU_STRIDE", "8"))
+        # lowprio (default): non-blocking, lowest-priority queue -> the flush
+        # never implicitly serialises with the legacy null stream and loses
+        # dispatch arbitration to training kernels.  cumask: restrict the
+        # flush blit to every `stride`-th CU (blocking stream type).
+        kind = os.environ.get("DWAMD_FLUSH_STREAM", "lowprio")  # lowprio | cumask | highprio | plain
+        self._cumask_ptr = None
+        self.flush_cus = 0
+        self.flush_stream_kind = kind
+        if kind == "cumask" and stride > 1:
+            n = ctypes.c_int(0)
+            p = _kern().dw_stream_create_cumask(stride, ctypes.byref(n))
+            if p:
+                self._cumask_ptr = p
+                self.flush_cus = n.value
+        elif kind in ("lowprio", "highprio"):
+            pr = ctypes.c_int(0)
+            p = _kern().dw_stream_create_prio(0 if kind == "lowprio" else 2, ctypes.byref(pr))
+            if p:
+                self._cumask_ptr = p
+        self.side_stream = (torch.cuda.ExternalStream(self._cumask_ptr, device=device)
+                            if self._cumask_ptr else torch.cuda.Stream(device=device))
+        # "memcpy": hipMemcpyAsync (runtime blit); "kernel": our bounded
+        # copy kernel storing through the device mapping of the pinned shm
+        self.flush_mode = os.environ.get("DWAMD_FLUSH_MODE", "memcpy")
+        self.flush_blocks = int(os.environ.get("DWAMD_FLUSH_BLOCKS", "64"))
+        self.flush_stats: List[Tuple[int, float]] = []
         self.pinned = PinnedRegistry()
         self._staging: Optional[torch.Tensor] = None
         self._executor = ThreadPoolExecutor(max_workers=1, thread_name_prefix="dwamd-d2h")
@@ -154,18 +188,32 @@ class GpuCopier:
         ev = torch.cuda.Event()
         ev.record(cur)
 
+        # NOTE: every host-side wait in this thread goes through ctypes (which
+        # drops the GIL); torch's Stream/Event.synchronize would hold the GIL
+        # for the whole PCIe transfer and stall the training thread's launches.
         def flush():
             if n > 0:
                 with torch.cuda.stream(self.side_stream):
-                    self.side_stream.wait_event(ev)
-                    err = _kern().dw_memcpy_async(ctypes.c_void_p(shm_payload_addr + lo),
-                                                  ctypes.c_void_p(self._staging.data_ptr()), n,
-                                                  1 if pinned else 3,
-                                                  ctypes.c_void_p(self.side_stream.cuda_stream))
+                    self.side_stream.wait_event(ev)  # device-side dependency only
+                    t0 = time.perf_counter()
+                    dst = shm_payload_addr + lo
+                    sp = ctypes.c_void_p(self.side_stream.cuda_stream)
+                    dptr = _kern().dw_host_device_ptr(ctypes.c_void_p(dst)) if (
+                        pinned and self.flush_mode == "kernel") else None
+                    if dptr and (n % 16 == 0):
+                        err = _kern().dw_stream_copy(ctypes.c_void_p(dptr), ctypes.c_void_p(self._staging.data_ptr()),
+                                                     n, self.flush_blocks, sp)
+                    else:
+                        err = _kern().dw_memcpy_async(ctypes.c_void_p(dst), ctypes.c_void_p(self._staging.data_ptr()),
+                                                      n, 1 if pinned else 3, sp)
                     _check(err, "D2H flush")
-                self.side_stream.synchronize()
+                _check(_kern().dw_stream_sync(ctypes.c_void_p(self.side_stream.cuda_stream)), "flush sync")
+                dt = time.perf_counter() - t0
+                self.flush_stats.append((n, dt))
             else:
-                ev.synchronize()
+                with torch.cuda.stream(self.side_stream):
+                    self.side_stream.wait_event(ev)
+                _check(_kern().dw_stream_sync(ctypes.c_void_p(self.side_stream.cuda_stream)), "flush sync")
             on_done()
 
         if sync:
@@ -219,6 +267,10 @@ class GpuCopier:
             self._executor.shutdown(wait=True)
             self.pinned.release_all()
             self._staging = None
+            if self._cumask_ptr:
+                self.side_stream.synchronize()
+                _kern().dw_stream_destroy(ctypes.c_void_p(self._cumask_ptr))
+                self._cumask_ptr = None
 
 
 def _merge_pieces(pieces: List[Tuple[int, int, int]]) -> List[Tuple[int, int, int]]:

@@ -212,7 +212,11 @@ class CheckpointEngine(ABC):
         return self._copier
 
     def _plan(self, state_dict) -> Layout:
-        layout, tensors = plan_layout(state_dict)
+        if not hasattr(self, "_layout_cache"):
+            from .layout import LayoutCache
+
+            self._layout_cache = LayoutCache()
+        layout, tensors = self._layout_cache.plan(state_dict)
         self._keepalive = tensors
         return layout
 

@@ -102,6 +102,50 @@ def _storage_key(t: torch.Tensor):
     return (t.device.type, t.device.index, st.data_ptr())
 
 
+MERGE_GAP = 1 << 20  # bridge gaps (alignment padding) up to 1 MiB inside one storage
+
+
+class LayoutCache:
+    """Re-plans only when the tensor set changes.
+
+    A training loop checkpoints the same tensors every time (same storages,
+    same addresses); only non-tensor leaves (step counters, lr, ...) change.
+    The cache key is the (address, numel, dtype) sequence of the tensor
+    leaves; on a hit the TensorMetas and extents are reused and only the
+    meta tree is rebuilt (cheap, no allocation per tensor).
+    """
+
+    def __init__(self):
+        self._key = None
+        self._layout: Optional[Layout] = None
+        self._metas: List[TensorMeta] = []
+
+    def plan(self, state_dict: Any) -> Tuple[Layout, List[torch.Tensor]]:
+        tensors: List[torch.Tensor] = []
+        key: List[Tuple] = []
+
+        def collect(v):
+            if torch.is_tensor(v):
+                key.append((v.data_ptr(), v.numel(), v.dtype, v.is_contiguous()))
+                tensors.append(v)
+            return v
+
+        traverse(state_dict, collect)
+        key_t = tuple(key)
+        all_contig = all(k[3] for k in key)  # temporaries of non-contiguous leaves are never cached
+        if all_contig and key_t == self._key and self._layout is not None:
+            it = iter(self._metas)
+            tree = traverse(state_dict, lambda v: next(it) if torch.is_tensor(v) else v)
+            lay = self._layout
+            return Layout(meta_tree=tree, extents=lay.extents, total_bytes=lay.total_bytes,
+                          signature=lay.signature), tensors
+        layout, tens = plan_layout(state_dict)
+        self._key = key_t
+        self._layout = layout
+        self._metas = [m for m in iter_leaves(layout.meta_tree) if isinstance(m, TensorMeta)]
+        return layout, tens
+
+
 def plan_layout(state_dict: Any) -> Tuple[Layout, List[torch.Tensor]]:
     """Plan where every tensor of ``state_dict`` lives in the payload.
 
@@ -139,7 +183,7 @@ def plan_layout(state_dict: Any) -> Tuple[Layout, List[torch.Tensor]]:
         ranges.sort()
         merged: List[List[int]] = []  # [start, end, [idx...]]
         for s, e, i in ranges:
-            if merged and s <= merged[-1][1]:
+            if merged and s <= merged[-1][1] + MERGE_GAP:
                 merged[-1][1] = max(merged[-1][1], e)
                 merged[-1][2].append(i)
             else:

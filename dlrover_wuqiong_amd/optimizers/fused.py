@@ -78,15 +78,21 @@ class _FlatOptimizer(torch.optim.Optimizer):
 
     # -------------------------------------------------------- state dict
     def state_dict(self):
-        state = {}
-        for i, (o, c) in enumerate(self.flat.offsets):
-            p = self.flat.params[i]
-            st = {"step": torch.tensor(float(self.step_count)),
-                  "exp_avg": self.exp_avg[o:o + c].view(p.shape),
-                  "exp_avg_sq": self.exp_avg_sq[o:o + c].view(p.shape)}
-            if self.master is not None:
-                st["master_param"] = self.master[o:o + c].view(p.shape)
-            state[i] = st
+        # The per-parameter views never change: build them once.  All params
+        # share one "step" tensor (same value), updated in place.
+        if getattr(self, "_sd_views", None) is None:
+            self._step_t = torch.zeros((), dtype=torch.float32)
+            views = {}
+            for i, (o, c) in enumerate(self.flat.offsets):
+                p = self.flat.params[i]
+                v = {"exp_avg": self.exp_avg[o:o + c].view(p.shape),
+                     "exp_avg_sq": self.exp_avg_sq[o:o + c].view(p.shape)}
+                if self.master is not None:
+                    v["master_param"] = self.master[o:o + c].view(p.shape)
+                views[i] = v
+            self._sd_views = views
+        self._step_t.fill_(float(self.step_count))
+        state = {i: {"step": self._step_t, **v} for i, v in self._sd_views.items()}
         groups = []
         for g in self.param_groups:
             d = {k: v for k, v in g.items() if k != "params"}

@@ -1,0 +1,93 @@
+"""Micro-benchmark: device->pinned-shm flush bandwidth and its interference
+with concurrent GEMMs, for the copy strategies the flash-checkpoint copier can
+use.  Results feed the choice in flash_checkpoint/copier.py."""
+
+import ctypes
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("DWAMD_SHM_PREFIX", f"d2h{os.getpid()}")
+from dlrover_wuqiong_amd._native import kernels  # noqa: E402
+from dlrover_wuqiong_amd.common.multi_process import SharedMemory  # noqa: E402
+
+GB = 1 << 30
+L = kernels()
+n = int(os.environ.get("D2H_GB", "8")) * GB
+seg = SharedMemory("d2hbench", create=True, size=n)
+t0 = time.time()
+seg.prefault(16)
+t_pf = time.time() - t0
+t0 = time.time()
+assert L.dw_host_register(ctypes.c_void_p(seg.addr), n) == 0
+t_reg = time.time() - t0
+dev = torch.empty(n, dtype=torch.uint8, device="cuda")
+dev.random_()
+a = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+b = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
+out = {"bytes": n, "prefault_s": round(t_pf, 3), "register_s": round(t_reg, 3)}
+
+
+def gemms(k=60):
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(k):
+        torch.matmul(a, b)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t
+
+
+gemms(10)  # warm up hipBLASLt
+out["gemm_alone_s"] = round(gemms(), 4)
+
+
+def run_copy(kind, stream, **kw):
+    s_ptr = ctypes.c_void_p(stream.cuda_stream)
+    if kind == "memcpy":
+        e = L.dw_memcpy_async(ctypes.c_void_p(seg.addr), ctypes.c_void_p(dev.data_ptr()), n, 1, s_ptr)
+    elif kind == "h2d":
+        e = L.dw_memcpy_async(ctypes.c_void_p(dev.data_ptr()), ctypes.c_void_p(seg.addr), n, 0, s_ptr)
+    else:
+        dptr = L.dw_host_device_ptr(ctypes.c_void_p(seg.addr))
+        e = L.dw_stream_copy(ctypes.c_void_p(dptr), ctypes.c_void_p(dev.data_ptr()), n, kw["blocks"], s_ptr)
+    assert e == 0, e
+
+
+def measure(name, kind, stream, **kw):
+    # alone
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    run_copy(kind, stream, **kw)
+    stream.synchronize()
+    alone = time.perf_counter() - t
+    # concurrent with GEMMs on the default stream
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    run_copy(kind, stream, **kw)
+    g = gemms()
+    stream.synchronize()
+    both = time.perf_counter() - t
+    out[name] = {"copy_GBps_alone": round(n / alone / 1e9, 1), "gemm_s_concurrent": round(g, 4),
+                 "gemm_slowdown": round(g / out["gemm_alone_s"], 3), "total_s": round(both, 3)}
+
+
+plain = torch.cuda.Stream()
+measure("memcpy_plain_stream", "memcpy", plain)
+measure("h2d_plain_stream", "h2d", plain)
+for stride in (8, 16):
+    ncu = ctypes.c_int(0)
+    sp = L.dw_stream_create_cumask(stride, ctypes.byref(ncu))
+    if sp:
+        ext = torch.cuda.ExternalStream(sp)
+        measure(f"memcpy_cumask_{ncu.value}cu", "memcpy", ext)
+        measure(f"h2d_cumask_{ncu.value}cu", "h2d", ext)
+for blocks in (16, 32, 64):
+    measure(f"kernel_copy_{blocks}blk", "kernel", plain, blocks=blocks)
+print(json.dumps(out))
+L.dw_host_unregister(ctypes.c_void_p(seg.addr))
+del dev
+seg.unlink()

@@ -1,0 +1,10 @@
+#!/bin/bash
+set -u
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+run() { local name=$1 secs=$2; shift 2; echo "=== $name"; timeout -k 10 "$secs" "$@" > gpurun_out/$name.log 2>&1; local rc=$?; echo "rc=$rc"; tail -3 gpurun_out/$name.log; [ $rc -ge 124 ] && exit $rc; return 0; }
+run build 300 python -c "import __graft_entry__ as g; g.build()"
+run d2h 300 python scripts/bench_d2h.py
+run pytest_gpu 600 python -m pytest tests -m gpu -q -p no:cacheprovider
+run bench_cu8 600 python bench.py --steps 8 --warmup 2
+DWAMD_FLUSH_CU_STRIDE=1 run bench_plain 600 python bench.py --steps 8 --warmup 2
