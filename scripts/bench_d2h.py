@@ -87,7 +87,33 @@ for stride in (8, 16):
         measure(f"h2d_cumask_{ncu.value}cu", "h2d", ext)
 for blocks in (16, 32, 64):
     measure(f"kernel_copy_{blocks}blk", "kernel", plain, blocks=blocks)
-print(json.dumps(out))
 L.dw_host_unregister(ctypes.c_void_p(seg.addr))
+# pageable (unregistered) H2D / D2H bandwidth
+for kind, k in (("h2d_pageable", 0), ("d2h_pageable", 1)):
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    if k == 0:
+        e = L.dw_memcpy_async(ctypes.c_void_p(dev.data_ptr()), ctypes.c_void_p(seg.addr), n, 0,
+                              ctypes.c_void_p(plain.cuda_stream))
+    else:
+        e = L.dw_memcpy_async(ctypes.c_void_p(seg.addr), ctypes.c_void_p(dev.data_ptr()), n, 1,
+                              ctypes.c_void_p(plain.cuda_stream))
+    L.dw_stream_sync(ctypes.c_void_p(plain.cuda_stream))
+    out[kind + "_GBps"] = round(n / (time.perf_counter() - t) / 1e9, 1)
+# registration with T threads over disjoint chunks
+from concurrent.futures import ThreadPoolExecutor  # noqa: E402
+
+for T in (1, 4, 8):
+    chunk = n // (4 * T) // 4096 * 4096
+    ranges = [(seg.addr + i * chunk, chunk) for i in range(n // chunk)]
+    t = time.perf_counter()
+    with ThreadPoolExecutor(T) as ex:
+        rs = list(ex.map(lambda r: L.dw_host_register(ctypes.c_void_p(r[0]), r[1]), ranges))
+    dt = time.perf_counter() - t
+    out[f"register_{T}thr_GBps"] = round(n / dt / 1e9, 1)
+    assert all(x == 0 for x in rs), rs
+    for a, _ in ranges:
+        L.dw_host_unregister(ctypes.c_void_p(a))
+print(json.dumps(out))
 del dev
 seg.unlink()
