@@ -191,6 +191,9 @@ def main():
     flat.data.zero_()
     opt.exp_avg.zero_()
     third.zero_()
+    if ckpt.engine._copier is not None:
+        # a restarted process has nothing pinned: measure the load cold
+        ckpt.engine._copier.pinned.release_all()
     sync_all(device)
     t0 = time.perf_counter()
     restored = ckpt.load_checkpoint(target=state())

@@ -85,14 +85,24 @@ class PinnedRegistry:
         a = addr // page * page
         e = (addr + nbytes + page - 1) // page * page
         with self._lock:
-            for (ra, re) in self._ranges:
-                if ra <= a and e <= re:
-                    return True
-            err = _kern().dw_host_register(ctypes.c_void_p(a), e - a)
-            if err != 0:
-                logger.warning(f"hipHostRegister({e - a} B) failed with {err}; using pageable copies")
-                return False
-            self._ranges.append((a, e))
+            # register only the parts of [a, e) not yet covered
+            gaps, cur = [], a
+            for (ra, re) in sorted(self._ranges):
+                if re <= cur or ra >= e:
+                    continue
+                if ra > cur:
+                    gaps.append((cur, ra))
+                cur = max(cur, re)
+                if cur >= e:
+                    break
+            if cur < e:
+                gaps.append((cur, e))
+            for ga, ge in gaps:
+                err = _kern().dw_host_register(ctypes.c_void_p(ga), ge - ga)
+                if err != 0:
+                    logger.warning(f"hipHostRegister({ge - ga} B) failed with {err}; using pageable copies")
+                    return False
+                self._ranges.append((ga, ge))
             return True
 
     def release_all(self):
@@ -234,12 +244,8 @@ class GpuCopier:
         """
         cur = torch.cuda.current_stream(self.device)
         if gather_group is None or world <= 1:
-            merged = _merge_pieces(pieces_gpu)
-            for off, dst, n in merged:
-                self.pinned.ensure(shm_payload_addr + off, n)
-            for off, dst, n in merged:
-                _check(_kern().dw_memcpy_async(ctypes.c_void_p(dst), ctypes.c_void_p(shm_payload_addr + off), n,
-                                               0, ctypes.c_void_p(cur.cuda_stream)), "H2D restore")
+            self._pipelined_h2d([(shm_payload_addr + off, dst, n) for off, dst, n in _merge_pieces(pieces_gpu)],
+                                cur)
             return
         import torch.distributed as dist
 
@@ -249,16 +255,34 @@ class GpuCopier:
         # payload terms but is padded): copy what exists.
         real = max(0, min(hi, payload_bytes) - lo)
         if real > 0:
-            self.pinned.ensure(shm_payload_addr + lo, real)
-            _check(_kern().dw_memcpy_async(ctypes.c_void_p(stg.data_ptr() + lo),
-                                           ctypes.c_void_p(shm_payload_addr + lo), real, 0,
-                                           ctypes.c_void_p(cur.cuda_stream)), "H2D slice")
+            self._pipelined_h2d([(shm_payload_addr + lo, stg.data_ptr() + lo, real)], cur)
         full = stg[: per * world]
         mine = full[lo: lo + per]
         dist.all_gather_into_tensor(full, mine, group=gather_group)
         base = stg.data_ptr()
         descs = build_descs([(base + off, dst, n) for off, dst, n in _merge_pieces(pieces_gpu)], self.device)
         launch_multi_copy(descs, cur)
+
+    def _pipelined_h2d(self, copies: List[Tuple[int, int, int]], stream, chunk: int = 512 << 20):
+        """H2D of (host_src, dev_dst, nbytes) ranges.  Pinning (hipHostRegister,
+        ~50 GB/s) of chunk k+1 overlaps the DMA (~57 GB/s) of chunk k, so a
+        freshly restarted process pays ~max(pin, copy) instead of the sum."""
+        pieces = []
+        for src, dst, n in copies:
+            o = 0
+            while o < n:
+                c = min(chunk, n - o)
+                pieces.append((src + o, dst + o, c))
+                o += c
+        if not pieces:
+            return
+        with ThreadPoolExecutor(max_workers=1, thread_name_prefix="dwamd-pin") as ex:
+            futs = [ex.submit(self.pinned.ensure, s, n) for s, _d, n in pieces]
+            sp = ctypes.c_void_p(stream.cuda_stream)
+            for (s, d, n), f in zip(pieces, futs):
+                pinned = f.result()
+                _check(_kern().dw_memcpy_async(ctypes.c_void_p(d), ctypes.c_void_p(s), n, 0 if pinned else 3, sp),
+                       "H2D restore")
 
     def close(self):
         try:

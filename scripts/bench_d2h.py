@@ -114,6 +114,35 @@ for T in (1, 4, 8):
     assert all(x == 0 for x in rs), rs
     for a, _ in ranges:
         L.dw_host_unregister(ctypes.c_void_p(a))
+
+# fresh (never registered) segments: one-shot vs chunked+threaded registration
+def fresh_reg(tag, chunk_mb, threads):
+    s2 = SharedMemory(f"d2hfresh{tag}", create=True, size=n)
+    s2.prefault(16)
+    chunk = chunk_mb << 20
+    ranges = [(s2.addr + o, min(chunk, n - o)) for o in range(0, n, chunk)]
+    t = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        rs = list(ex.map(lambda r: L.dw_host_register(ctypes.c_void_p(r[0]), r[1]), ranges))
+    dt = time.perf_counter() - t
+    assert all(x == 0 for x in rs)
+    # H2D from it to check the registration is effective
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for a, b in ranges:
+        L.dw_memcpy_async(ctypes.c_void_p(dev.data_ptr() + (a - s2.addr)), ctypes.c_void_p(a), b, 0,
+                          ctypes.c_void_p(plain.cuda_stream))
+    L.dw_stream_sync(ctypes.c_void_p(plain.cuda_stream))
+    h2d = n / (time.perf_counter() - t) / 1e9
+    for a, _ in ranges:
+        L.dw_host_unregister(ctypes.c_void_p(a))
+    s2.unlink()
+    out[f"fresh_register_{chunk_mb}MB_{threads}thr"] = {"GBps": round(n / dt / 1e9, 1), "h2d_GBps": round(h2d, 1)}
+
+
+fresh_reg("a", n >> 20, 1)
+fresh_reg("b", 256, 1)
+fresh_reg("c", 256, 8)
 print(json.dumps(out))
 del dev
 seg.unlink()
