@@ -1,0 +1,476 @@
+"""Per-node elastic training agent (runs inside ``dwamd-run``).
+
+Responsibilities (parity: reference
+``dlrover/python/elastic_agent/torch/training.py``: ``ElasticLaunchConfig``
+:116-168, ``MasterRendezvousHandler`` :179-359, ``ElasticTrainingAgent``
+:362-731, ``launch_agent`` :734-822, node check :864-1112):
+
+* rendezvous through the job master (join, poll the completed world),
+  global rank assignment (offset = sum of local world sizes of lower node
+  ranks), MASTER_ADDR/PORT published by node 0 through the master KV store;
+* spawn one process per GPU (plain ``subprocess``; this process never touches
+  the GPU, so no fork/exec of a GPU-initialised process ever happens);
+* monitor loop: success -> exit barrier; failure -> report to master, persist
+  the latest in-memory flash checkpoint ("save at breakpoint"), restart the
+  worker group (re-rendezvous so the RCCL world is re-formed) while restarts
+  remain; membership change (new/returning nodes waiting) -> restart without
+  consuming a retry;
+* host the asynchronous flash-checkpoint saver (shm -> storage) whose shm
+  outlives the worker processes, so restarted workers restore from memory;
+* heartbeats + resource reports; optional network check before training.
+"""
+
+import json
+import os
+import signal
+import socket
+import subprocess
+import sys
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+from ..common import env_utils
+from ..common.constants import (Accelerators, JobConstant, NodeEnv, NodeStatus, RendezvousName,
+                                TrainingExceptionLevel)
+from ..common.log import logger
+from ..common.rpc import find_free_port, find_free_port_in_range, find_free_port_in_set
+from .master_client import MasterClient
+
+
+class RendezvousTimeoutError(RuntimeError):
+    pass
+
+
+class NodeCheckFailedError(RuntimeError):
+    pass
+
+
+@dataclass
+class ElasticLaunchConfig:
+    min_nodes: int = 1
+    max_nodes: int = 1
+    nproc_per_node: int = 1
+    run_id: str = "dwamd"
+    max_restarts: int = JobConstant.MAX_RESTART_DEFAULT
+    monitor_interval: float = 0.5
+    join_timeout: float = JobConstant.RDZV_JOIN_TIMEOUT_DEFAULT
+    lastcall_timeout: float = 3.0
+    pend_timeout: float = float("inf")
+    node_unit: int = 1
+    network_check: bool = False
+    comm_perf_test: bool = False
+    exclude_straggler: bool = False
+    save_at_breakpoint: bool = True
+    auto_config: bool = False
+    auto_tunning: bool = False
+    accelerator: str = Accelerators.AMD_GPU
+    log_dir: str = ""
+    redirects: bool = False
+    node_rank: int = 0
+    local_addr: str = ""
+    heartbeat_interval: float = JobConstant.HEARTBEAT_INTERVAL
+    exit_barrier_timeout: float = 300.0
+    stop_timeout: float = 15.0
+    extra_env: Dict[str, str] = field(default_factory=dict)
+
+    def auto_configure_params(self):
+        """nnodes from NODE_NUM, nproc from the visible GPUs, network check
+        on for >= 4 nodes (reference training.py:140-168)."""
+        n = int(os.getenv(NodeEnv.NODE_NUM, "0") or 0)
+        if n > 0:
+            self.min_nodes = self.max_nodes = n
+        if self.accelerator == Accelerators.AMD_GPU:
+            ng = _visible_gpu_count()
+            if ng > 0:
+                self.nproc_per_node = ng
+        if self.max_nodes >= 4:
+            self.network_check = True
+
+
+def _visible_gpu_count() -> int:
+    """Count GPUs without initialising HIP in this process (sysfs / env)."""
+    vis = os.getenv("HIP_VISIBLE_DEVICES") or os.getenv("ROCR_VISIBLE_DEVICES") or os.getenv(
+        "CUDA_VISIBLE_DEVICES")
+    if vis:
+        return len([v for v in vis.split(",") if v.strip() != ""])
+    try:
+        import glob
+
+        n = 0
+        for p in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/gpu_id"):
+            with open(p) as f:
+                if int(f.read().strip() or 0) != 0:
+                    n += 1
+        return n
+    except Exception:
+        return 0
+
+
+@dataclass
+class WorkerProcess:
+    local_rank: int
+    global_rank: int
+    proc: subprocess.Popen
+    log_path: str = ""
+
+
+class RunResult:
+    SUCCEEDED = "SUCCEEDED"
+    FAILED = "FAILED"
+    HEALTHY = "HEALTHY"
+
+    def __init__(self, state: str, failures: Optional[Dict[int, dict]] = None):
+        self.state = state
+        self.failures = failures or {}
+
+
+class MasterRendezvousHandler:
+    """Join the master's rendezvous and wait for a world containing us."""
+
+    def __init__(self, client: MasterClient, config: ElasticLaunchConfig, rdzv_name=RendezvousName.ELASTIC_TRAINING):
+        self.client = client
+        self.config = config
+        self.name = rdzv_name
+        self.node_rank = config.node_rank
+
+    def next_rendezvous(self) -> Tuple[int, int, Dict[int, int]]:
+        self.client.join_rendezvous(self.node_rank, self.config.nproc_per_node, self.name)
+        start = time.time()
+        while True:
+            rnd, group, world = self.client.get_comm_world(self.name, self.node_rank)
+            if world and self.node_rank in world:
+                return rnd, group, world
+            if world and self.node_rank not in world and time.time() - start > self.config.pend_timeout:
+                raise RendezvousTimeoutError("node not admitted into the world")
+            if time.time() - start > self.config.join_timeout:
+                raise RendezvousTimeoutError(f"rendezvous {self.name} timed out after {self.config.join_timeout}s")
+            time.sleep(JobConstant.RDZV_POLL_INTERVAL if self.config.lastcall_timeout > 1 else 0.1)
+
+    def num_nodes_waiting(self) -> int:
+        return self.client.num_nodes_waiting(self.name)
+
+
+class ElasticTrainingAgent:
+    def __init__(self, config: ElasticLaunchConfig, entrypoint: str, args: List[str], client: MasterClient,
+                 is_module: bool = False):
+        self.config = config
+        self.entrypoint = entrypoint
+        self.args = list(args)
+        self.is_module = is_module
+        self.client = client
+        self.rdzv = MasterRendezvousHandler(client, config)
+        self.workers: List[WorkerProcess] = []
+        self.restart_count = 0
+        self.remaining_restarts = config.max_restarts
+        self.round = 0
+        self.world: Dict[int, int] = {}
+        self.group_rank = 0
+        self.master_addr = ""
+        self.master_port = 0
+        self._stop_hb = threading.Event()
+        self._hostname = config.local_addr or _local_ip()
+        self.events: List[Tuple[float, str]] = []  # (time, what) for goodput accounting
+
+    # ------------------------------------------------------------ ranks
+    @staticmethod
+    def assign_ranks(node_rank: int, world: Dict[int, int]) -> Tuple[int, int, List[int]]:
+        """(group_rank, world_size, global ranks of this node's workers)."""
+        nodes = sorted(world)
+        group_rank = nodes.index(node_rank)
+        offset = sum(world[n] for n in nodes[:group_rank])
+        return group_rank, sum(world.values()), list(range(offset, offset + world[node_rank]))
+
+    def _store_key(self, what: str) -> str:
+        return f"{self.config.run_id}/round{self.round}/{what}"
+
+    def _free_port(self) -> int:
+        hp = os.getenv("HOST_PORTS", "")
+        if hp:
+            try:
+                return find_free_port_in_set([int(p) for p in hp.split(",") if p])
+            except RuntimeError:
+                pass
+        try:
+            return find_free_port_in_range(20000, 30000)
+        except RuntimeError:
+            return find_free_port()
+
+    def _rendezvous(self):
+        t0 = time.time()
+        self.round, _group, self.world = self.rdzv.next_rendezvous()
+        self.group_rank, world_size, ranks = self.assign_ranks(self.config.node_rank, self.world)
+        if self.group_rank == 0:
+            self.master_addr = self._hostname
+            self.master_port = self._free_port()
+            self.client.kv_store_set(self._store_key("master"), f"{self.master_addr}:{self.master_port}".encode())
+        else:
+            deadline = time.time() + self.config.join_timeout
+            while True:
+                v = self.client.kv_store_get(self._store_key("master"))
+                if v:
+                    a, p = v.decode().rsplit(":", 1)
+                    self.master_addr, self.master_port = a, int(p)
+                    break
+                if time.time() > deadline:
+                    raise RendezvousTimeoutError("no MASTER_ADDR published")
+                time.sleep(0.05)
+        self.events.append((time.time(), "rendezvous"))
+        logger.info(f"rendezvous round {self.round} ({time.time() - t0:.2f}s): world={self.world} "
+                    f"group_rank={self.group_rank} ranks={ranks} master={self.master_addr}:{self.master_port}")
+        return ranks, world_size
+
+    # ----------------------------------------------------------- workers
+    def _worker_env(self, local_rank: int, global_rank: int, world_size: int) -> Dict[str, str]:
+        env = dict(os.environ)
+        env.update(self.config.extra_env)
+        env.update({
+            "LOCAL_RANK": str(local_rank),
+            "RANK": str(global_rank),
+            "GROUP_RANK": str(self.group_rank),
+            "ROLE_RANK": str(global_rank),
+            "ROLE_NAME": "dlrover-trainer",
+            "LOCAL_WORLD_SIZE": str(self.config.nproc_per_node),
+            "WORLD_SIZE": str(world_size),
+            "GROUP_WORLD_SIZE": str(len(self.world)),
+            "ROLE_WORLD_SIZE": str(world_size),
+            "MASTER_ADDR": self.master_addr,
+            "MASTER_PORT": str(self.master_port),
+            "TORCHELASTIC_RESTART_COUNT": str(self.restart_count),
+            "TORCHELASTIC_MAX_RESTARTS": str(self.config.max_restarts),
+            "TORCHELASTIC_RUN_ID": self.config.run_id,
+            "TORCHELASTIC_USE_AGENT_STORE": "False",
+            NodeEnv.NODE_RANK: str(self.config.node_rank),
+            NodeEnv.DLROVER_MASTER_ADDR: self.client.master_addr,
+            "HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
+        })
+        env.setdefault("OMP_NUM_THREADS", "1")
+        return env
+
+    def _start_workers(self):
+        ranks, world_size = self._rendezvous()
+        self.workers = []
+        for lr, gr in enumerate(ranks):
+            cmd = [sys.executable, "-u"] + (["-m", self.entrypoint] if self.is_module else [self.entrypoint]) + self.args
+            env = self._worker_env(lr, gr, world_size)
+            log_path, out, err = "", None, None
+            if self.config.log_dir:
+                os.makedirs(self.config.log_dir, exist_ok=True)
+                log_path = os.path.join(self.config.log_dir,
+                                        f"{self.config.run_id}_r{self.restart_count}_rank{gr}.log")
+                out = open(log_path, "w")
+                err = subprocess.STDOUT
+            p = subprocess.Popen(cmd, env=env, stdout=out, stderr=err, start_new_session=True)
+            if out is not None:
+                out.close()
+            self.workers.append(WorkerProcess(lr, gr, p, log_path))
+        self.events.append((time.time(), "workers_started"))
+        logger.info(f"started {len(self.workers)} workers (restart {self.restart_count})")
+
+    def _stop_workers(self, timeout: Optional[float] = None):
+        timeout = self.config.stop_timeout if timeout is None else timeout
+        for w in self.workers:
+            if w.proc.poll() is None:
+                try:
+                    os.killpg(w.proc.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+        deadline = time.time() + timeout
+        for w in self.workers:
+            while w.proc.poll() is None and time.time() < deadline:
+                time.sleep(0.05)
+            if w.proc.poll() is None:
+                try:
+                    os.killpg(w.proc.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                w.proc.wait()
+        self.workers = []
+
+    def _monitor_workers(self) -> RunResult:
+        codes = [(w, w.proc.poll()) for w in self.workers]
+        failed = {w.global_rank: self._failure(w, c) for w, c in codes if c not in (None, 0)}
+        if failed:
+            return RunResult(RunResult.FAILED, failed)
+        if all(c == 0 for _w, c in codes):
+            return RunResult(RunResult.SUCCEEDED)
+        return RunResult(RunResult.HEALTHY)
+
+    def _failure(self, w: WorkerProcess, code: int) -> dict:
+        msg = ""
+        if w.log_path and os.path.exists(w.log_path):
+            try:
+                with open(w.log_path, errors="replace") as f:
+                    msg = f.read()[-2000:]
+            except OSError:
+                pass
+        return {"local_rank": w.local_rank, "exitcode": code, "message": msg,
+                "timestamp": int(time.time())}
+
+    # ----------------------------------------------------- checkpointing
+    def _saver(self):
+        from .ckpt_saver import AsyncCheckpointSaver
+
+        return AsyncCheckpointSaver.get_ckpt_saver()
+
+    def _save_ckpt_to_storage(self):
+        if not self.config.save_at_breakpoint:
+            return
+        saver = self._saver()
+        if saver is not None:
+            try:
+                saver.save_shm_to_storage(60, self.client if len(self.world) > 1 else None)
+            except Exception as e:
+                logger.warning(f"breakpoint save failed: {e}")
+
+    # --------------------------------------------------------- main loop
+    def _heartbeat_loop(self):
+        from .monitor import ResourceMonitor
+
+        rm = ResourceMonitor()
+        while not self._stop_hb.wait(self.config.heartbeat_interval):
+            try:
+                self.client.report_heart_beat()
+                cpu, mem = rm.sample()
+                self.client.report_used_resource(mem, cpu, rm.gpu_stats())
+            except Exception as e:
+                logger.debug(f"heartbeat failed: {e}")
+
+    def run(self) -> int:
+        from .ckpt_saver import AsyncCheckpointSaver
+
+        AsyncCheckpointSaver.start_async_saving_ckpt()
+        self.client.report_rdzv_params(self.config.min_nodes, self.config.max_nodes, self.config.lastcall_timeout,
+                                       self.config.node_unit, int(self.config.join_timeout))
+        hb = threading.Thread(target=self._heartbeat_loop, daemon=True, name="dwamd-heartbeat")
+        hb.start()
+        try:
+            if self.config.network_check:
+                from .node_check import run_network_check
+
+                ok = run_network_check(self.config, self.client)
+                if not ok:
+                    raise NodeCheckFailedError(f"node {self.config.node_rank} failed the network check")
+            self._start_workers()
+            AsyncCheckpointSaver.register_signal_handler()
+            self._install_signal_handlers()
+            return self._invoke_run()
+        finally:
+            self._stop_hb.set()
+
+    def _invoke_run(self) -> int:
+        last_membership_check = 0.0
+        while True:
+            time.sleep(self.config.monitor_interval)
+            res = self._monitor_workers()
+            if res.state == RunResult.SUCCEEDED:
+                self.events.append((time.time(), "succeeded"))
+                self._exit_barrier()
+                self._wait_async_saver()
+                self._cleanup_shm()
+                self.client.report_node_event(NodeStatus.SUCCEEDED, "")
+                return 0
+            if res.state == RunResult.FAILED:
+                self.events.append((time.time(), "failed"))
+                logger.error(f"worker failure: { {r: (f['exitcode']) for r, f in res.failures.items()} }")
+                try:
+                    self.client.report_failures(json.dumps(res.failures), self.restart_count,
+                                                TrainingExceptionLevel.PROCESS_ERROR)
+                except Exception:
+                    pass
+                self._stop_workers()
+                self._save_ckpt_to_storage()
+                if self.remaining_restarts > 0:
+                    self.remaining_restarts -= 1
+                    self._restart_workers()
+                    continue
+                self.client.report_node_event(NodeStatus.FAILED, "max restarts reached")
+                return 1
+            # healthy: check membership change (rate limited)
+            now = time.time()
+            if now - last_membership_check > 2.0:
+                last_membership_check = now
+                if self.rdzv.num_nodes_waiting() > 0:
+                    logger.info("new/returning nodes are waiting: restart the worker group")
+                    self._stop_workers()
+                    self._save_ckpt_to_storage()
+                    self._restart_workers(count=False)
+
+    def _install_signal_handlers(self):
+        """SIGTERM/SIGINT: stop the worker processes first (they run in their
+        own sessions), then the saver's handler persists shm and exits."""
+        for sig in (signal.SIGTERM, signal.SIGINT):
+            prev = signal.getsignal(sig)
+
+            def handler(signum, frame, prev=prev):
+                self._stop_workers(timeout=5)
+                if callable(prev):
+                    prev(signum, frame)
+                raise SystemExit(128 + signum)
+
+            signal.signal(sig, handler)
+
+    def _restart_workers(self, count: bool = True):
+        from .ckpt_saver import AsyncCheckpointSaver
+
+        if count:
+            self.restart_count += 1
+        AsyncCheckpointSaver.reset()
+        self._start_workers()
+
+    def _exit_barrier(self):
+        key = f"{self.config.run_id}/exit_barrier"
+        try:
+            n = self.client.kv_store_add(key, 1)
+            deadline = time.time() + self.config.exit_barrier_timeout
+            while n < len(self.world) and time.time() < deadline:
+                time.sleep(0.2)
+                n = int(self.client.kv_store_add(key, 0))
+        except Exception:
+            pass
+
+    def _wait_async_saver(self):
+        saver = self._saver()
+        if saver is None:
+            return
+        t0 = time.time()
+        while saver.wait_saving_checkpoint() and time.time() - t0 < 600:
+            time.sleep(0.2)
+
+    def _cleanup_shm(self):
+        """The job finished: release the node's checkpoint memory."""
+        import glob
+
+        from ..common.multi_process import shm_name
+
+        ns = shm_name("", "").rstrip("_")
+        saver = self._saver()
+        if saver is not None:
+            saver.close()
+        for f in glob.glob(f"/dev/shm/{ns}*"):
+            try:
+                os.remove(f)
+            except OSError:
+                pass
+
+
+def _local_ip() -> str:
+    try:
+        s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        s.connect(("10.255.255.255", 1))
+        ip = s.getsockname()[0]
+        s.close()
+        return ip
+    except OSError:
+        return "127.0.0.1"
+
+
+def launch_agent(config: ElasticLaunchConfig, entrypoint: str, args: List[str], master_addr: str,
+                 is_module: bool = False) -> int:
+    client = MasterClient(master_addr, node_id=config.node_rank)
+    agent = ElasticTrainingAgent(config, entrypoint, args, client, is_module=is_module)
+    try:
+        return agent.run()
+    finally:
+        agent._stop_workers(timeout=5)

@@ -113,18 +113,26 @@ class AsyncCheckpointSaver:
         prev_int = signal.getsignal(signal.SIGINT)
         prev_term = signal.getsignal(signal.SIGTERM)
 
+        def chain(prev, signum, frame):
+            if callable(prev):
+                prev(signum, frame)
+            elif prev != signal.SIG_IGN:
+                # default disposition: terminate (via SystemExit so that the
+                # launcher's cleanup/finally blocks still run)
+                raise SystemExit(128 + signum)
+
         def on_int(signum, frame):
             if cls._saver_instance:
                 cls._saver_instance.close()
-            if callable(prev_int):
-                prev_int(signum, frame)
+            chain(prev_int, signum, frame)
 
         def on_term(signum, frame):
             if cls._saver_instance:
-                cls._saver_instance.save_shm_to_storage()
-                cls._saver_instance.close()
-            if callable(prev_term):
-                prev_term(signum, frame)
+                try:
+                    cls._saver_instance.save_shm_to_storage()
+                finally:
+                    cls._saver_instance.close()
+            chain(prev_term, signum, frame)
 
         signal.signal(signal.SIGINT, on_int)
         signal.signal(signal.SIGTERM, on_term)

@@ -1,0 +1,98 @@
+"""dwamd-run end to end on CPU/gloo: fault injection -> agent restart ->
+restore from the in-memory flash checkpoint; two simulated nodes; network
+check; rank assignment (parity: reference test_elastic_training_agent.py)."""
+
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+from conftest import free_port
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXAMPLE = os.path.join(REPO, "examples", "elastic_train.py")
+
+
+def _run(args, env_extra, timeout=240):
+    env = dict(os.environ)
+    env.update(env_extra)
+    env["PYTHONPATH"] = REPO + os.pathsep + env.get("PYTHONPATH", "")
+    return subprocess.Popen([sys.executable, "-m", "dlrover_wuqiong_amd.trainer.run"] + args, env=env,
+                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+
+
+def _results(path):
+    with open(path) as f:
+        return [json.loads(line) for line in f if line.strip()]
+
+
+def test_assign_ranks():
+    from dlrover_wuqiong_amd.elastic_agent.agent import ElasticTrainingAgent
+
+    world = {3: 8, 0: 8, 5: 4}
+    assert ElasticTrainingAgent.assign_ranks(0, world) == (0, 20, list(range(0, 8)))
+    assert ElasticTrainingAgent.assign_ranks(3, world) == (1, 20, list(range(8, 16)))
+    assert ElasticTrainingAgent.assign_ranks(5, world) == (2, 20, list(range(16, 20)))
+
+
+def test_single_node_fault_restart_restores_from_memory(tmp_path):
+    out = tmp_path / "out.jsonl"
+    p = _run(["--nnodes", "1", "--nproc-per-node", "2", "--max-restarts", "2", EXAMPLE, "--steps", "16",
+              "--out", str(out), "--ckpt-dir", str(tmp_path / "ck")],
+             {"DWAMD_FAULT_INJECT_STEP": "6", "DWAMD_FAULT_INJECT_RANK": "1"})
+    log, _ = p.communicate(timeout=240)
+    assert p.returncode == 0, log[-3000:]
+    res = _results(out)
+    assert len(res) == 1
+    assert res[0]["restart"] == 1 and res[0]["start_step"] == 6  # resumed from the in-memory step-6 checkpoint
+    # the agent persisted the breakpoint checkpoint before restarting
+    assert (tmp_path / "ck" / "dlrover_latest.txt").read_text() == "6"
+
+
+def test_max_restarts_exhausted_fails(tmp_path):
+    bad = tmp_path / "bad.py"
+    bad.write_text("import sys; sys.exit(3)\n")
+    p = _run(["--nnodes", "1", "--nproc-per-node", "1", "--max-restarts", "1", str(bad)], {})
+    log, _ = p.communicate(timeout=120)
+    assert p.returncode == 1, log[-2000:]
+    assert "max restarts" in log or "worker failure" in log
+
+
+def test_two_nodes_one_fails(tmp_path):
+    port = free_port()
+    out = tmp_path / "out.jsonl"
+
+    def args(node, ck):
+        return ["--node-rank", str(node), "--nnodes", "2", "--nproc-per-node", "1", "--max-restarts", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(port), "--rdzv-conf", "lastcall_timeout=1",
+                EXAMPLE, "--steps", "14", "--out", str(out), "--ckpt-dir", str(tmp_path / ck)]
+
+    inject = {"DWAMD_FAULT_INJECT_STEP": "5", "DWAMD_FAULT_INJECT_RANK": "1"}
+    n0 = _run(args(0, "ck0"), dict(inject, DWAMD_SHM_PREFIX=os.environ["DWAMD_SHM_PREFIX"] + "n0"))
+    time.sleep(1.0)
+    n1 = _run(args(1, "ck1"), dict(inject, DWAMD_SHM_PREFIX=os.environ["DWAMD_SHM_PREFIX"] + "n1"))
+    try:
+        l1, _ = n1.communicate(timeout=240)
+        l0, _ = n0.communicate(timeout=240)
+    finally:
+        for p in (n0, n1):
+            if p.poll() is None:
+                p.kill()
+    assert n0.returncode == 0, l0[-3000:]
+    assert n1.returncode == 0, l1[-3000:]
+    res = _results(out)
+    assert res and res[-1]["world"] == 2
+    assert res[-1]["restart"] >= 1 and res[-1]["start_step"] == 5
+
+
+def test_network_check_then_train(tmp_path):
+    out = tmp_path / "out.jsonl"
+    p = _run(["--nnodes", "1", "--nproc-per-node", "2", "--network-check", "--rdzv-conf", "lastcall_timeout=0.5",
+              EXAMPLE, "--steps", "4", "--out", str(out), "--ckpt-dir", str(tmp_path / "ck")], {})
+    log, _ = p.communicate(timeout=240)
+    assert p.returncode == 0, log[-3000:]
+    assert "network check round 0: ok=True" in log
+    assert _results(out)[0]["restart"] == 0
