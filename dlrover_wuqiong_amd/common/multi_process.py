@@ -66,6 +66,17 @@ class SharedMemory:
         self.addr = int(addr)
         self.buf = memoryview((ctypes.c_char * self.size).from_address(self.addr)).cast("B")
         self._closed = False
+        self.ino = self._inode()
+
+    def _inode(self) -> int:
+        try:
+            return os.stat("/dev/shm/" + self._name.lstrip("/")).st_ino
+        except OSError:
+            return -1
+
+    def stale(self) -> bool:
+        """True if the name now refers to a different (re-created) segment."""
+        return self._inode() != self.ino
 
     @property
     def name(self) -> str:

@@ -9,7 +9,9 @@ Responsibilities (parity: reference
   global rank assignment (offset = sum of local world sizes of lower node
   ranks), MASTER_ADDR/PORT published by node 0 through the master KV store;
 * spawn one process per GPU (plain ``subprocess``; this process never touches
-  the GPU, so no fork/exec of a GPU-initialised process ever happens);
+  the GPU, so no fork/exec of a GPU-initialised process ever happens); a
+  warm standby interpreter per local rank (``standby.py``) is kept ready so a
+  restart skips interpreter start + ``import torch``;
 * monitor loop: success -> exit barrier; failure -> report to master, persist
   the latest in-memory flash checkpoint ("save at breakpoint"), restart the
   worker group (re-rendezvous so the RCCL world is re-formed) while restarts
@@ -54,7 +56,7 @@ class ElasticLaunchConfig:
     nproc_per_node: int = 1
     run_id: str = "dwamd"
     max_restarts: int = JobConstant.MAX_RESTART_DEFAULT
-    monitor_interval: float = 0.5
+    monitor_interval: float = 0.1
     join_timeout: float = JobConstant.RDZV_JOIN_TIMEOUT_DEFAULT
     lastcall_timeout: float = 3.0
     pend_timeout: float = float("inf")
@@ -74,6 +76,11 @@ class ElasticLaunchConfig:
     exit_barrier_timeout: float = 300.0
     stop_timeout: float = 15.0
     extra_env: Dict[str, str] = field(default_factory=dict)
+    # pre-started interpreters (torch imported) that become the next workers
+    warm_standby: bool = field(default_factory=lambda: os.getenv("DWAMD_WARM_STANDBY", "1") == "1")
+    standby_delay: float = field(default_factory=lambda: float(os.getenv("DWAMD_STANDBY_DELAY", "3")))
+    # persist the breakpoint checkpoint while the new workers already start
+    async_breakpoint_save: bool = True
 
     def auto_configure_params(self):
         """nnodes from NODE_NUM, nproc from the visible GPUs, network check
@@ -172,6 +179,9 @@ class ElasticTrainingAgent:
         self._stop_hb = threading.Event()
         self._hostname = config.local_addr or _local_ip()
         self.events: List[Tuple[float, str]] = []  # (time, what) for goodput accounting
+        self._standby: Dict[int, subprocess.Popen] = {}
+        self._workers_started_at = 0.0
+        self._bp_thread: Optional[threading.Thread] = None
 
     # ------------------------------------------------------------ ranks
     @staticmethod
@@ -251,22 +261,79 @@ class ElasticTrainingAgent:
     def _start_workers(self):
         ranks, world_size = self._rendezvous()
         self.workers = []
+        warm = 0
         for lr, gr in enumerate(ranks):
-            cmd = [sys.executable, "-u"] + (["-m", self.entrypoint] if self.is_module else [self.entrypoint]) + self.args
             env = self._worker_env(lr, gr, world_size)
-            log_path, out, err = "", None, None
+            log_path = ""
             if self.config.log_dir:
                 os.makedirs(self.config.log_dir, exist_ok=True)
                 log_path = os.path.join(self.config.log_dir,
                                         f"{self.config.run_id}_r{self.restart_count}_rank{gr}.log")
-                out = open(log_path, "w")
-                err = subprocess.STDOUT
-            p = subprocess.Popen(cmd, env=env, stdout=out, stderr=err, start_new_session=True)
-            if out is not None:
-                out.close()
+            p = self._activate_standby(lr, env, log_path)
+            if p is None:
+                p = self._cold_start(env, log_path)
+            else:
+                warm += 1
             self.workers.append(WorkerProcess(lr, gr, p, log_path))
-        self.events.append((time.time(), "workers_started"))
-        logger.info(f"started {len(self.workers)} workers (restart {self.restart_count})")
+        self._workers_started_at = time.time()
+        self.events.append((self._workers_started_at, "workers_started"))
+        logger.info(f"started {len(self.workers)} workers (restart {self.restart_count}, "
+                    f"{warm} from warm standby)")
+
+    def _cold_start(self, env: Dict[str, str], log_path: str) -> subprocess.Popen:
+        cmd = [sys.executable, "-u"] + (["-m", self.entrypoint] if self.is_module else [self.entrypoint]) + self.args
+        out, err = None, None
+        if log_path:
+            out = open(log_path, "w")
+            err = subprocess.STDOUT
+        p = subprocess.Popen(cmd, env=env, stdout=out, stderr=err, start_new_session=True)
+        if out is not None:
+            out.close()
+        return p
+
+    # ------------------------------------------------------ warm standby
+    def _spawn_standbys(self):
+        """Start one idle interpreter per local rank for the next (re)start."""
+        if not self.config.warm_standby:
+            return
+        env = dict(os.environ)
+        env.update(self.config.extra_env)
+        env.setdefault("OMP_NUM_THREADS", "1")
+        for lr in range(self.config.nproc_per_node):
+            p = self._standby.get(lr)
+            if p is not None and p.poll() is None:
+                continue
+            self._standby[lr] = subprocess.Popen(
+                [sys.executable, "-u", "-m", "dlrover_wuqiong_amd.elastic_agent.standby"], env=env,
+                stdin=subprocess.PIPE, start_new_session=True, text=True)
+
+    def _activate_standby(self, local_rank: int, env: Dict[str, str], log_path: str):
+        p = self._standby.pop(local_rank, None)
+        if p is None:
+            return None
+        if p.poll() is not None:
+            return None
+        cmd = {"env": env, "entry": self.entrypoint, "args": self.args, "module": self.is_module,
+               "log": log_path, "cwd": os.getcwd()}
+        try:
+            p.stdin.write(json.dumps(cmd) + "\n")
+            p.stdin.close()
+        except (BrokenPipeError, OSError):
+            return None
+        return p
+
+    def _discard_standbys(self):
+        for p in self._standby.values():
+            try:
+                if p.poll() is None:
+                    p.stdin.close()  # the standby exits on EOF
+                    p.wait(timeout=5)
+            except Exception:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except (ProcessLookupError, PermissionError):
+                    pass
+        self._standby = {}
 
     def _stop_workers(self, timeout: Optional[float] = None):
         timeout = self.config.stop_timeout if timeout is None else timeout
@@ -315,14 +382,30 @@ class ElasticTrainingAgent:
         return AsyncCheckpointSaver.get_ckpt_saver()
 
     def _save_ckpt_to_storage(self):
+        """Persist the latest in-memory checkpoint after a failure.  The shm
+        outlives the workers and a save always writes the *other* slot, so
+        this runs concurrently with the restart (the new workers restore from
+        the same memory while it is written to storage)."""
         if not self.config.save_at_breakpoint:
             return
         saver = self._saver()
-        if saver is not None:
+        if saver is None:
+            return
+        client = self.client if len(self.world) > 1 else None
+
+        def run():
             try:
-                saver.save_shm_to_storage(60, self.client if len(self.world) > 1 else None)
+                saver.save_shm_to_storage(60, client)
             except Exception as e:
                 logger.warning(f"breakpoint save failed: {e}")
+
+        if self._bp_thread is not None and self._bp_thread.is_alive():
+            self._bp_thread.join()
+        if self.config.async_breakpoint_save:
+            self._bp_thread = threading.Thread(target=run, daemon=True, name="dwamd-breakpoint-save")
+            self._bp_thread.start()
+        else:
+            run()
 
     # --------------------------------------------------------- main loop
     def _heartbeat_loop(self):
@@ -358,14 +441,23 @@ class ElasticTrainingAgent:
             return self._invoke_run()
         finally:
             self._stop_hb.set()
+            self._discard_standbys()
+            if self._bp_thread is not None:
+                self._bp_thread.join(timeout=600)
 
     def _invoke_run(self) -> int:
         last_membership_check = 0.0
         while True:
             time.sleep(self.config.monitor_interval)
+            if (self.config.warm_standby and not self._standby
+                    and time.time() - self._workers_started_at > self.config.standby_delay):
+                self._spawn_standbys()
             res = self._monitor_workers()
             if res.state == RunResult.SUCCEEDED:
                 self.events.append((time.time(), "succeeded"))
+                self._discard_standbys()
+                if self._bp_thread is not None:
+                    self._bp_thread.join(timeout=600)
                 self._exit_barrier()
                 self._wait_async_saver()
                 self._cleanup_shm()
@@ -385,6 +477,7 @@ class ElasticTrainingAgent:
                     self.remaining_restarts -= 1
                     self._restart_workers()
                     continue
+                self._discard_standbys()
                 self.client.report_node_event(NodeStatus.FAILED, "max restarts reached")
                 return 1
             # healthy: check membership change (rate limited)

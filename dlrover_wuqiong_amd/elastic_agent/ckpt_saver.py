@@ -33,7 +33,7 @@ from ..common.multi_process import SharedLock, SharedQueue
 from ..common.serialize import ClassMeta
 from ..flash_checkpoint.engine import CheckpointEvent, CheckpointEventType
 from ..flash_checkpoint.shm_handler import (DLROVER_CKPT_CONFIG_KEY, EVENT_QUEUE_SIZE, CheckpointConfig,
-                                            CheckpointSharedObjPrefix, SharedMemoryHandler)
+                                            CheckpointSharedObjPrefix, SharedMemoryHandler, slot_lock_name)
 
 
 class AsyncCheckpointSaver:
@@ -57,10 +57,11 @@ class AsyncCheckpointSaver:
         self._event_queue = SharedQueue(CheckpointSharedObjPrefix.SAVE_STEP_QNAME + "0", create=True,
                                         maxsize=EVENT_QUEUE_SIZE)
         self._shm_handlers: List[SharedMemoryHandler] = []
-        self._shm_locks: List[SharedLock] = []
+        self._shm_locks: List[List[SharedLock]] = []  # [shard][slot]
         for i in range(local_shard_num):
-            self._shm_handlers.append(SharedMemoryHandler(i, host=True))
-            self._shm_locks.append(SharedLock(CheckpointSharedObjPrefix.SHM_LOCK_NAME + str(i), create=True))
+            h = SharedMemoryHandler(i, host=True)
+            self._shm_handlers.append(h)
+            self._shm_locks.append([SharedLock(slot_lock_name(i, s), create=True) for s in range(h.num_slots)])
         self._executor = ThreadPoolExecutor(max_workers=max(1, local_shard_num), thread_name_prefix="ckpt_saver")
         self.last_persist_sec = 0.0
         logger.info(f"{type(self).__name__}: dir={checkpoint_dir} local_shards={local_shard_num} "
@@ -143,7 +144,8 @@ class AsyncCheckpointSaver:
             cls._saver_instance.reset_shared_memory()
 
     def reset_shared_memory(self):
-        self._stop_commit = True
+        # workers restart: re-attach lazily (only if a segment was re-created);
+        # an in-flight breakpoint persist keeps running
         for h in self._shm_handlers:
             h.reset()
 
@@ -165,8 +167,9 @@ class AsyncCheckpointSaver:
     def unlink_all(self):
         for h in self._shm_handlers:
             h.unlink()
-        for lk in self._shm_locks:
-            lk.unlink()
+        for locks in self._shm_locks:
+            for lk in locks:
+                lk.unlink()
         self._event_queue.unlink()
 
     # ------------------------------------------------------------- loop
@@ -191,30 +194,33 @@ class AsyncCheckpointSaver:
     def _get_checkpoint_done_dir(self, step):
         return os.path.join(self.checkpoint_dir, self._STAGE_DIR, f"{step}.done")
 
-    def _wait_shard_complete(self, handler: SharedMemoryHandler, step: int, timeout: float) -> bool:
+    def _wait_shard_complete(self, handler: SharedMemoryHandler, step: int, timeout: float) -> int:
+        """Slot holding ``step`` complete, or -1 (timeout / overwritten by a newer step)."""
         deadline = time.time() + timeout
         while time.time() < deadline:
-            if handler.complete_step() == step:
-                return True
+            steps = handler.complete_steps()
+            if step in steps:
+                return steps[step]
+            if steps and min(steps) > step:
+                return -1
             time.sleep(0.01)
-        return False
+        return -1
 
     def _save_shard(self, step: int, shard_id: int, done_dir: str) -> bool:
         h = self._shm_handlers[shard_id]
-        lock = self._shm_locks[shard_id]
-        if h.shared_memory is None:
-            h.init_shared_memory(create=False)
-        if not self._wait_shard_complete(h, step, self._save_timeout):
-            logger.error(f"shard {shard_id} never completed step {step}")
+        slot = self._wait_shard_complete(h, step, self._save_timeout)
+        if slot < 0:
+            logger.error(f"shard {shard_id} does not hold a complete step {step}")
             return False
+        lock = self._shm_locks[shard_id][slot]
         if not lock.acquire(blocking=True, timeout=self._save_timeout):
             return False
         try:
-            cfg = h.get_checkpoint_config()
-            if h.complete_step() != step:
-                logger.error(f"shard {shard_id}: memory holds step {cfg.step}, event step {step}")
+            if h.slot_step(slot) != step:
+                logger.error(f"shard {shard_id}: slot {slot} was overwritten before step {step} was persisted")
                 return False
-            self.persist_to_storage(shard_id, cfg)
+            cfg = h.get_checkpoint_config(slot=slot)
+            self.persist_to_storage(shard_id, cfg, slot)
         finally:
             lock.release()
         self.storage.write("done", os.path.join(done_dir, str(cfg.rank)))
@@ -236,10 +242,10 @@ class AsyncCheckpointSaver:
         finally:
             self._writing_storage = False
 
-    def persist_to_storage(self, shard_id: int, cfg: CheckpointConfig):
+    def persist_to_storage(self, shard_id: int, cfg: CheckpointConfig, slot: int):
         """Write each category of the shard's state dict to its path."""
         h = self._shm_handlers[shard_id]
-        sd = h.load_state_dict()
+        sd = h.load_state_dict(slot)
         sd.pop(DLROVER_CKPT_CONFIG_KEY, None)
         for name, path in (cfg.paths or {}).items():
             if name in sd:
@@ -253,6 +259,9 @@ class AsyncCheckpointSaver:
                 return False
             n = len(self.storage.listdir(step_done_dir)) if self.storage.exists(step_done_dir) else 0
             if n >= self.global_shard_num:
+                if not self._finalize_step(step):
+                    self.storage.commit(step, False)
+                    return False
                 self.update_tracker_file(step)
                 self.storage.safe_rmtree(step_done_dir)
                 self.storage.commit(step, True)
@@ -262,6 +271,10 @@ class AsyncCheckpointSaver:
         self.storage.commit(step, False)
         return False
 
+    def _finalize_step(self, step: int) -> bool:
+        """Hook run on node 0 once every global shard is on storage."""
+        return True
+
     def update_tracker_file(self, step: int):
         self.storage.write(str(step), os.path.join(self.checkpoint_dir, CheckpointConstant.TRACER_FILE_NAME))
 
@@ -269,22 +282,20 @@ class AsyncCheckpointSaver:
     def save_shm_to_storage(self, timeout: int = 60, master_client=None):
         """Persist the latest complete in-memory checkpoint (e.g. after a
         worker failure, before restarting the workers)."""
-        steps = []
+        common = None
         for h in self._shm_handlers:
-            if h.shared_memory is None:
-                h.init_shared_memory(create=False)
-            steps.append(h.complete_step())
-        if not steps or any(s == 0 for s in steps):
+            steps = set(h.complete_steps())
+            common = steps if common is None else common & steps
+        if not common:
             logger.info("no complete in-memory checkpoint to persist")
             return False
-        if len(set(steps)) != 1:
-            logger.error(f"inconsistent shard steps {steps}; skip breakpoint save")
-            return False
-        step = steps[0]
+        step = max(common)
         if master_client is not None and not self._sync_node_checkpoint(master_client, step, timeout):
             self._stop_commit = True
             return False
-        if self._writing_storage or any(lk.locked() for lk in self._shm_locks):
+        busy = any(locks[h.slot_of(step)].locked() for h, locks in zip(self._shm_handlers, self._shm_locks)
+                   if h.slot_of(step) >= 0)
+        if self._writing_storage or busy:
             logger.info("saver busy; skip breakpoint save")
             return False
         if step > self._latest_step:
@@ -308,9 +319,9 @@ class CommonDirCheckpointSaver(AsyncCheckpointSaver):
 class TempDirCheckpointSaver(AsyncCheckpointSaver):
     """Persist into a staging dir, then move into place at commit."""
 
-    def persist_to_storage(self, shard_id, cfg):
+    def persist_to_storage(self, shard_id, cfg, slot):
         h = self._shm_handlers[shard_id]
-        sd = h.load_state_dict()
+        sd = h.load_state_dict(slot)
         sd.pop(DLROVER_CKPT_CONFIG_KEY, None)
         stage = os.path.join(self.checkpoint_dir, self._STAGE_DIR, str(cfg.step))
         for name, path in (cfg.paths or {}).items():
@@ -367,10 +378,22 @@ class FsdpDcpSaver(CommonDirCheckpointSaver):
     """Writes torch.distributed.checkpoint-compatible ``.distcp`` shards +
     ``.metadata`` (see flash_checkpoint/fsdp.py for the layout)."""
 
-    def persist_to_storage(self, shard_id, cfg):
+    def persist_to_storage(self, shard_id, cfg, slot):
         from ..flash_checkpoint.fsdp import persist_dcp_shard
 
         h = self._shm_handlers[shard_id]
-        sd = h.load_state_dict()
+        sd = h.load_state_dict(slot)
         sd.pop(DLROVER_CKPT_CONFIG_KEY, None)
-        persist_dcp_shard(self.storage, sd, cfg)
+        path = persist_dcp_shard(self.storage, sd, cfg)
+        if not hasattr(self, "_step_paths"):
+            self._step_paths = {}
+        self._step_paths[cfg.step] = (path, cfg.world_size)
+
+    def _finalize_step(self, step):
+        from ..flash_checkpoint.fsdp import finalize_dcp_checkpoint
+
+        path, world = getattr(self, "_step_paths", {}).pop(step, (None, 0))
+        if path is None:
+            logger.error(f"no DCP path recorded for step {step}")
+            return False
+        return finalize_dcp_checkpoint(self.storage, path, world)

@@ -38,7 +38,7 @@ from ..common.serialize import ClassMeta
 from ..common.storage import CheckpointStorage, get_checkpoint_storage
 from .layout import Layout, TensorMeta, iter_leaves, plan_layout, split_ranges, traverse
 from .shm_handler import (DLROVER_CKPT_CONFIG_KEY, EVENT_QUEUE_SIZE, CheckpointConfig,
-                          CheckpointSharedObjPrefix, SharedMemoryHandler)
+                          CheckpointSharedObjPrefix, SharedMemoryHandler, slot_lock_name)
 
 
 class CheckpointEventType:
@@ -77,6 +77,21 @@ def verify_all_rank_step_consistent(group, step: int) -> bool:
     t = torch.tensor([step, -step], dtype=torch.int64)
     dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
     return int(t[0]) == step and -int(t[1]) == step
+
+
+def agree_on_step(group, steps: Optional[List[int]]) -> int:
+    """Latest step every rank holds complete in memory (0 if none).
+    ``steps=None``: this rank holds no shard and accepts any step."""
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return max(steps) if steps else 0
+    allv: List[Optional[List[int]]] = [None] * dist.get_world_size(group)
+    dist.all_gather_object(allv, None if steps is None else sorted(steps), group=group)
+    common = None
+    for s in allv:
+        if s is None:
+            continue
+        common = set(s) if common is None else common & set(s)
+    return max(common) if common else 0
 
 
 class _LocalSaverThread:
@@ -130,8 +145,9 @@ class CheckpointEngine(ABC):
             self._local_rank == 0)
 
         self._shm_handler = SharedMemoryHandler(self.local_shard_id, host=False)
-        self._shm_lock = SharedLock(CheckpointSharedObjPrefix.SHM_LOCK_NAME + str(self.local_shard_id),
-                                    create=True)
+        self._shm_locks = [SharedLock(slot_lock_name(self.local_shard_id, s), create=True)
+                           for s in range(self._shm_handler.num_slots)]
+        self._next_slot: Optional[int] = None
         self._event_queue = (SharedQueue(CheckpointSharedObjPrefix.SAVE_STEP_QNAME + "0", create=True,
                                          maxsize=EVENT_QUEUE_SIZE)
                              if self._local_rank == 0 else None)
@@ -238,11 +254,13 @@ class CheckpointEngine(ABC):
                     h.close()
                     h.init_shared_memory(create=False)
                 self._generation += 1
+                self._next_slot = None
         elif need_resize:
             h.close()
             h.init_shared_memory(create=True, size=total)
             h.shared_memory.prefault(8)
             self._generation += 1
+            self._next_slot = None
 
     # ----------------------------------------------------------- core save
     def save_state_dict_to_memory(self, state_dict: Dict, conf: CheckpointConfig) -> bool:
@@ -254,54 +272,60 @@ class CheckpointEngine(ABC):
             copier.wait()  # previous flush must land before the staging buffer is reused
         self._wait_own_lock_release()
 
-        acquired = False
-        if self._is_shard_owner:
-            acquired = self._shm_lock.acquire(blocking=False)
-        owner_ok = acquired if self._is_shard_owner else True
-        if not check_all_rank_ready(self._ctl_group, owner_ok and bool(state_dict)):
-            if acquired:
-                self._shm_lock.release()
-            logger.info(f"rank {self._rank} skips the memory checkpoint of step {conf.step}: "
-                        "the agent is persisting the previous one")
-            return False
-        self._lock_held = acquired
-
         layout = self._plan(state_dict)
         self._ensure_shm(layout.total_bytes)
         h = self._shm_handler
+        if self._next_slot is None:
+            # first save of this process (nothing in flight): never the latest complete slot
+            self._next_slot = h.write_slot()
+        slot = self._next_slot
+        lock = self._shm_locks[slot]
+        acquired = False
+        if self._is_shard_owner:
+            acquired = lock.acquire(blocking=False)
+        owner_ok = acquired if self._is_shard_owner else True
+        if not check_all_rank_ready(self._ctl_group, owner_ok and bool(state_dict)):
+            if acquired:
+                lock.release()
+            logger.info(f"rank {self._rank} skips the memory checkpoint of step {conf.step}: "
+                        f"the agent is persisting slot {slot}")
+            return False
+        self._lock_held = acquired
+        self._next_slot = (slot + 1) % h.num_slots
+
         conf.rank = self._rank
         conf.group_rank = self._group_rank
         conf.world_size = self._world
         conf.num_slices = self._num_slices
         conf.generation = self._generation
+        h.set_slice_step(slot, self._slice_idx, 0)  # slot reads incomplete before any byte changes
         if self._is_shard_owner:
-            h.set_metadata(layout.meta_tree, conf)
+            h.set_metadata(slot, layout.meta_tree, conf)
         lo, hi = split_ranges(layout.total_bytes, self._num_slices)[self._slice_idx]
         step = conf.step
 
         def on_done():
-            h.set_slice_step(self._slice_idx, step)
+            h.set_slice_step(slot, self._slice_idx, step)
             if self._is_shard_owner:
-                self._release_when_complete(step)
+                self._release_when_complete(step, slot)
 
         has_gpu = any(e.device == "cuda" for e in layout.extents)
         if has_gpu and copier is not None:
-            copier.save_slice(layout, h.payload_addr, lo, hi, on_done)
+            copier.save_slice(layout, h.payload_addr(slot), lo, hi, on_done)
         else:
-            self._cpu_save_slice(layout, lo, hi)
+            self._cpu_save_slice(layout, h.payload_addr(slot), lo, hi)
             on_done()
         self._cached_step = step
         self._last_save_blocking = time.perf_counter() - t0
         self._replica_manager.backup(self._shm_handler)
         return True
 
-    def _cpu_save_slice(self, layout: Layout, lo: int, hi: int):
+    def _cpu_save_slice(self, layout: Layout, base: int, lo: int, hi: int):
         import ctypes
 
         from .._native import runtime
         from .layout import intersect_extents
 
-        base = self._shm_handler.payload_addr
         for e, a, b in intersect_extents(layout.extents, lo, hi):
             if e.device == "cuda":
                 # no copier (should not happen on a GPU host): go through torch
@@ -310,8 +334,8 @@ class CheckpointEngine(ABC):
             runtime().dw_memcpy_parallel(ctypes.c_void_p(base + a), ctypes.c_void_p(e.src_ptr + (a - e.offset)),
                                          b - a, 8)
 
-    def _release_when_complete(self, step: int):
-        """Shard owner: keep the shm lock until every slice holds ``step``."""
+    def _release_when_complete(self, step: int, slot: int):
+        """Shard owner: keep the slot lock until every slice holds ``step``."""
         if not self._lock_held:
             return
         h = self._shm_handler
@@ -319,11 +343,11 @@ class CheckpointEngine(ABC):
 
         def _wait():
             while time.time() < deadline:
-                if all(s == step for s in h.slice_steps(self._num_slices)):
+                if all(s == step for s in h.slice_steps(slot, self._num_slices)):
                     break
                 time.sleep(0.0005)
             self._lock_held = False
-            self._shm_lock.release()
+            self._shm_locks[slot].release()
 
         if self._num_slices <= 1:
             _wait()
@@ -346,21 +370,24 @@ class CheckpointEngine(ABC):
         """Returns (step, state_dict) from shm, or (0, {})."""
         self._restore_memory_from_replica()
         h = self._shm_handler
-        step = h.complete_step() if (self._replicated or self._local_rank == self.local_shard_id) else 0
-        if not verify_all_rank_step_consistent(self._ctl_group, step) or step <= 0:
+        holds = self._replicated or self._local_rank == self.local_shard_id
+        step = agree_on_step(self._ctl_group, list(h.complete_steps()) if holds else None)
+        slot = h.slot_of(step) if (step > 0 and holds) else -1
+        if step <= 0 or not check_all_rank_ready(self._ctl_group, slot >= 0 or not holds):
             return 0, {}
-        meta = h.metadata.get()
-        tree = meta["tree"]
+        if not holds:
+            return 0, {}
+        tree = h.get_meta(slot)["tree"]
         if target is not None:
-            sd = self._restore_into(tree, target)
+            sd = self._restore_into(tree, target, slot)
             if sd is not None:
                 return step, sd
-        sd = h.load_state_dict()
+        sd = h.load_state_dict(slot)
         if isinstance(sd, dict):
             sd.pop(DLROVER_CKPT_CONFIG_KEY, None)
         return step, sd
 
-    def _restore_into(self, tree, target):
+    def _restore_into(self, tree, target, slot: int):
         """Fast path: H2D (sliced + all-gather for replicated) straight into
         the live tensors of ``target`` (same structure as the saved dict)."""
         from .copier import match_targets
@@ -370,6 +397,7 @@ class CheckpointEngine(ABC):
         if not ok_all:
             return None
         h = self._shm_handler
+        base = h.payload_addr(slot)
         gpu_pieces = []
         for m, t in pairs:
             if m.numel == 0:
@@ -378,7 +406,7 @@ class CheckpointEngine(ABC):
                 gpu_pieces.append((m.offset, t.data_ptr(), m.numel * m.element_size))
             else:
                 src = torch.frombuffer(h.shared_memory.buf, dtype=m.dtype, count=m.numel,
-                                       offset=m.offset + h.payload_addr - h.shared_memory.addr)
+                                       offset=m.offset + h.payload_offset(slot))
                 with torch.no_grad():
                     t.copy_(src.view(t.shape))
         total = h.payload_size
@@ -389,9 +417,9 @@ class CheckpointEngine(ABC):
         if self._replicated and self._num_slices > 1 and self._gather_group is not None:
             per = split_ranges(total, self._num_slices)[0][1]
             lo = self._slice_idx * per
-            copier.restore(gpu_pieces, h.payload_addr, total, lo, lo + per, self._gather_group, self._num_slices)
+            copier.restore(gpu_pieces, base, total, lo, lo + per, self._gather_group, self._num_slices)
         else:
-            copier.restore(gpu_pieces, h.payload_addr, total, 0, total)
+            copier.restore(gpu_pieces, base, total, 0, total)
         it = iter([t for _, t in pairs])
 
         def pick(v):

@@ -9,6 +9,8 @@ Parity: reference ``dlrover/trainer/torch/flash_checkpoint/replica.py``
 gloo group of ``replica_count`` nodes; ``FullCkptReplicaManager`` :245-350
 broadcasts from any node holding a copy).
 
+Only the latest complete slot of the (double-buffered) shard is shipped.
+
 Backup groups: node n belongs to group n // replica_count; inside a group the
 ranks with the same local rank exchange shards.  Peer shards are kept in a
 separate shm segment per peer (``replica_{peer_rank}``) so a local restart
@@ -25,7 +27,7 @@ import torch.distributed as dist
 from ..common import env_utils
 from ..common.log import logger
 from ..common.multi_process import SharedMemory
-from .shm_handler import HEADER_BYTES, SharedMemoryHandler
+from .shm_handler import SharedMemoryHandler
 
 
 class CkptReplicaManager:
@@ -68,22 +70,24 @@ class CkptReplicaManager:
         if not self.has_replica():
             return
         self.engine.wait_for_memory_save()
-        if handler.shared_memory is None:
-            return
-        payload = np.frombuffer(handler.shared_memory.buf, dtype=np.uint8)
-        meta = handler.metadata.get()
+        slot = handler.latest_slot() if handler.shared_memory is not None else -1
+        if slot >= 0:
+            view, meta = handler.export_slot(slot)
+            payload = np.frombuffer(view, dtype=np.uint8)
+        else:
+            payload, meta = np.zeros(0, dtype=np.uint8), None
         size = torch.tensor([payload.size], dtype=torch.int64)
         sizes = [torch.zeros(1, dtype=torch.int64) for _ in self.backup_ranks]
         dist.all_gather(sizes, size, group=self._group)
         maxn = int(max(int(s) for s in sizes))
-        buf = torch.zeros(maxn, dtype=torch.uint8)
+        buf = torch.zeros(max(maxn, 1), dtype=torch.uint8)
         buf[: payload.size] = torch.from_numpy(payload)
-        outs = [torch.empty(maxn, dtype=torch.uint8) for _ in self.backup_ranks]
+        outs = [torch.empty(max(maxn, 1), dtype=torch.uint8) for _ in self.backup_ranks]
         dist.all_gather(outs, buf, group=self._group)
         metas: List[Optional[dict]] = [None] * len(self.backup_ranks)
         dist.all_gather_object(metas, meta, group=self._group)
         for r, t, m, n in zip(self.backup_ranks, outs, metas, sizes):
-            if r == self.rank:
+            if r == self.rank or m is None:
                 continue
             n = int(n)
             mb = pickle.dumps(m)
@@ -130,10 +134,7 @@ class CkptReplicaManager:
                 except FileNotFoundError:
                     obj = [None]
             dist.broadcast_object_list(obj, src=donor, group=self._group)
-            if self.rank == r and obj[0] is not None:
+            if self.rank == r and obj[0] is not None and obj[0][1]:
                 data, meta = obj[0]
-                handler.init_shared_memory(create=True, size=len(data) - HEADER_BYTES)
-                handler.shared_memory.buf[: len(data)] = data
-                if meta:
-                    handler.metadata.set(meta)
+                handler.import_slot(data, meta)
                 logger.info(f"rank {r} restored its checkpoint shard ({len(data)} B) from peer {donor}")

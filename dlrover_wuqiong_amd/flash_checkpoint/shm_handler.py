@@ -1,39 +1,57 @@
-"""The flash-checkpoint shared-memory shard: header + payload + metadata.
+"""The flash-checkpoint shared-memory shard: header + double-buffered payload.
 
 Segment layout (one segment per local checkpoint shard)::
 
-    [0, HEADER)        header: int64 words
-                         0 magic, 1 payload bytes, 2 layout generation,
-                         3 number of slices, 8+r  step of slice r complete
-    [HEADER, ...)      payload: the coalesced tensor extents (layout.py)
+    [0, HEADER)                   header: int64 words
+                                    0 magic, 1 payload bytes (per slot),
+                                    2 layout generation, 3 slot stride,
+                                    4 number of slots,
+                                    8 + s*MAX_SLICES + r: step of slice r of slot s
+    [HEADER + s*stride, ...)      payload slot s: the coalesced tensor extents
+
+Two payload *slots*: a save always writes the slot that does NOT hold the
+latest complete checkpoint, so a process that dies in the middle of a
+snapshot/flush (the D2H flush of a 1.5B-parameter state takes ~0.4 s, i.e.
+a large fraction of a short checkpoint interval) still leaves the previous
+complete checkpoint intact in memory, and the agent can persist slot A while
+training already snapshots into slot B.  (The reference keeps one buffer:
+a crash during a save loses the in-memory checkpoint.)  ``DWAMD_CKPT_SLOTS=1``
+restores the single-buffer behaviour to halve host memory.
 
 A *slice* is a page-aligned sub-range of the payload written by one process:
 for replicated (DDP) state every local rank writes 1/L of the payload in
 parallel, each over its own PCIe link; for sharded state there is one slice.
-A shard is complete for step ``s`` iff ``meta.config.step == s`` and every
-slice word equals ``s`` (8-byte aligned stores: atomic on x86-64).
+Slot ``s`` is complete for step ``t`` iff its metadata config has
+``step == t`` and every slice word of the slot equals ``t`` (8-byte aligned
+stores: atomic on x86-64).  A writer zeroes its slice word before touching
+the slot's bytes, so a partially written slot never reads as complete.
 
-Metadata (tree of TensorMeta + CheckpointConfig) lives in a SharedDict so the
-agent can rebuild the state dict after the worker is gone.
+Metadata (tree of TensorMeta + CheckpointConfig) lives in one SharedDict per
+slot so the agent can rebuild the state dict after the worker is gone.
 
 Parity: reference ``SharedMemoryHandler`` (``ckpt_saver.py:209-341``).
 """
 
 import os
 from dataclasses import dataclass, field
-from typing import Any, Dict, Optional
+from typing import Any, Dict, List, Optional
 
 import numpy as np
 
 from ..common.log import logger
 from ..common.multi_process import SharedDict, SharedMemory
-from .layout import TensorMeta, tensors_from_payload
+from .layout import TensorMeta, tensors_from_payload  # noqa: F401  (TensorMeta re-exported)
 
 HEADER_BYTES = 64 * 1024
-MAGIC = 0x44574B5053484D31  # "DWKPSHM1"
+MAGIC = 0x44574B5053484D32  # "DWKPSHM2"
 MAX_SLICES = 1024
+SLOT_ALIGN = 2 << 20
 DLROVER_CKPT_CONFIG_KEY = "_DLORVER_CKPT_CONFIG"
 EVENT_QUEUE_SIZE = 16  # checkpoint events buffered between workers and the saver
+
+
+def default_num_slots() -> int:
+    return max(1, min(2, int(os.environ.get("DWAMD_CKPT_SLOTS", "2"))))
 
 
 class CheckpointSharedObjPrefix:
@@ -57,11 +75,17 @@ class CheckpointConfig:
     generation: int = 0
 
 
+def slot_lock_name(local_shard_id: int, slot: int) -> str:
+    return f"{CheckpointSharedObjPrefix.SHM_LOCK_NAME}{local_shard_id}_{slot}"
+
+
 class SharedMemoryHandler:
-    def __init__(self, local_shard_id: int, host: bool = True):
+    def __init__(self, local_shard_id: int, host: bool = True, num_slots: Optional[int] = None):
         self.local_shard_id = local_shard_id
+        self.num_slots = num_slots or default_num_slots()
         self._shm_name = CheckpointSharedObjPrefix.SHM_NAME + str(local_shard_id)
-        self.metadata = SharedDict(CheckpointSharedObjPrefix.META_NAME + str(local_shard_id), create=True)
+        self.metas = [SharedDict(f"{CheckpointSharedObjPrefix.META_NAME}{local_shard_id}_{s}", create=True)
+                      for s in range(self.num_slots)]
         self.shared_memory: Optional[SharedMemory] = None
         self._header: Optional[np.ndarray] = None
         self._need_creation = True
@@ -71,15 +95,29 @@ class SharedMemoryHandler:
     def shm_name(self):
         return self._shm_name
 
+    @staticmethod
+    def _stride(size: int) -> int:
+        return (size + SLOT_ALIGN - 1) // SLOT_ALIGN * SLOT_ALIGN
+
     def init_shared_memory(self, create: bool = False, size: int = 0) -> bool:
-        """Create (payload ``size`` bytes) or attach the segment."""
+        """Create (``size`` payload bytes per slot) or attach the segment."""
+        if self.shared_memory is not None and self.shared_memory.stale():
+            self.close()  # re-created by a writer (resize): drop the old mapping
         if self.shared_memory is not None:
-            if not create or self.shared_memory.size == size + HEADER_BYTES:
+            if not create or (self._header is not None and int(self._header[1]) == size):
                 return True
             self.close()
+        if create and self.init_shared_memory(create=False) and int(self._header[1]) == size:
+            return True  # compatible segment (e.g. from before a restart): keep its checkpoints
+        self.close()
         try:
             if create:
-                self.shared_memory = SharedMemory(self._shm_name, create=True, size=size + HEADER_BYTES)
+                if self.exists():
+                    # never resize in place: a reader's mapping could fault (SIGBUS)
+                    SharedMemory(self._shm_name, create=False).unlink()
+                stride = self._stride(size)
+                self.shared_memory = SharedMemory(self._shm_name, create=True,
+                                                  size=HEADER_BYTES + stride * self.num_slots)
             else:
                 self.shared_memory = SharedMemory(self._shm_name, create=False)
         except FileNotFoundError:
@@ -87,83 +125,147 @@ class SharedMemoryHandler:
             return False
         self._header = np.frombuffer(self.shared_memory.buf, dtype=np.int64, count=HEADER_BYTES // 8)
         if create:
+            self._header[8:] = 0
             self._header[0] = MAGIC
             self._header[1] = size
+            self._header[3] = self._stride(size)
+            self._header[4] = self.num_slots
+            for m in self.metas:
+                m.set({})
+        elif int(self._header[0]) != MAGIC or int(self._header[4]) != self.num_slots:
+            logger.warning(f"shm {self._shm_name}: incompatible header; ignoring it")
+            self.close()
+            return False
         self._need_creation = False
         return True
 
     def exists(self) -> bool:
         return SharedMemory.exists(self._shm_name)
 
-    @property
-    def payload_addr(self) -> int:
-        return self.shared_memory.addr + HEADER_BYTES
+    def payload_addr(self, slot: int = 0) -> int:
+        return self.shared_memory.addr + self.payload_offset(slot)
+
+    def payload_offset(self, slot: int = 0) -> int:
+        return HEADER_BYTES + slot * int(self._header[3])
 
     @property
     def payload_size(self) -> int:
-        return self.shared_memory.size - HEADER_BYTES if self.shared_memory else 0
+        return int(self._header[1]) if self.shared_memory is not None and self._header is not None else 0
 
-    def payload_view(self):
-        return self.shared_memory.buf[HEADER_BYTES:]
+    def payload_view(self, slot: int = 0):
+        off = self.payload_offset(slot)
+        return self.shared_memory.buf[off: off + self.payload_size]
 
     # --------------------------------------------------------------- header
-    def set_slice_step(self, idx: int, step: int):
-        self._header[8 + idx] = step
+    def set_slice_step(self, slot: int, idx: int, step: int):
+        self._header[8 + slot * MAX_SLICES + idx] = step
 
-    def slice_steps(self, n: int):
+    def slice_steps(self, slot: int, n: int) -> List[int]:
         if self._header is None:
             return []
-        return [int(self._header[8 + i]) for i in range(n)]
+        base = 8 + slot * MAX_SLICES
+        return [int(self._header[base + i]) for i in range(n)]
 
-    def reset_slices(self, n: int):
+    def reset_slices(self, slot: int, n: int):
         if self._header is not None:
-            self._header[8:8 + max(n, 1)] = 0
+            base = 8 + slot * MAX_SLICES
+            self._header[base: base + max(n, 1)] = 0
 
     # ------------------------------------------------------------- metadata
-    def get_checkpoint_config(self, default_config: Optional[CheckpointConfig] = None) -> CheckpointConfig:
-        meta = self.metadata.get()
-        return meta.get(DLROVER_CKPT_CONFIG_KEY, default_config or CheckpointConfig())
+    def get_meta(self, slot: int) -> dict:
+        return self.metas[slot].get() or {}
 
-    def set_metadata(self, meta_tree: Any, config: CheckpointConfig):
-        d = {"tree": meta_tree, DLROVER_CKPT_CONFIG_KEY: config}
-        self.metadata.set(d)
+    def get_checkpoint_config(self, default_config: Optional[CheckpointConfig] = None,
+                              slot: Optional[int] = None) -> CheckpointConfig:
+        if slot is None:
+            slot = self.latest_slot()
+        if slot < 0:
+            return default_config or CheckpointConfig()
+        return self.get_meta(slot).get(DLROVER_CKPT_CONFIG_KEY, default_config or CheckpointConfig())
 
-    def update_config(self, config: CheckpointConfig):
-        d = self.metadata.get(local=True) or self.metadata.get()
-        d[DLROVER_CKPT_CONFIG_KEY] = config
-        self.metadata.set(d)
+    def set_metadata(self, slot: int, meta_tree: Any, config: CheckpointConfig):
+        self.metas[slot].set({"tree": meta_tree, DLROVER_CKPT_CONFIG_KEY: config})
 
-    def complete_step(self) -> int:
-        """Step of the complete checkpoint in memory, 0 if none/partial."""
-        meta = self.metadata.get()
-        cfg: CheckpointConfig = meta.get(DLROVER_CKPT_CONFIG_KEY)
-        if cfg is None or cfg.step <= 0:
+    def _attached(self) -> bool:
+        if self.shared_memory is not None and not self.shared_memory.stale():
+            self._need_creation = False
+            return True
+        self.close()
+        return self.init_shared_memory(create=False)
+
+    def slot_step(self, slot: int) -> int:
+        """Step of the complete checkpoint in ``slot``; 0 if none/partial."""
+        cfg = self.get_meta(slot).get(DLROVER_CKPT_CONFIG_KEY)
+        if cfg is None or cfg.step <= 0 or not self._attached():
             return 0
-        if self.shared_memory is None or self._need_creation:
-            if not self.init_shared_memory(create=False):
-                return 0
-        steps = self.slice_steps(cfg.num_slices)
+        steps = self.slice_steps(slot, cfg.num_slices)
         if steps and all(s == cfg.step for s in steps):
             return cfg.step
         return 0
+
+    def complete_steps(self) -> Dict[int, int]:
+        """{step: slot} of every complete in-memory checkpoint."""
+        out = {}
+        for s in range(self.num_slots):
+            st = self.slot_step(s)
+            if st > 0:
+                out[st] = s
+        return out
+
+    def complete_step(self) -> int:
+        """Step of the latest complete checkpoint in memory, 0 if none."""
+        steps = self.complete_steps()
+        return max(steps) if steps else 0
+
+    def latest_slot(self) -> int:
+        steps = self.complete_steps()
+        return steps[max(steps)] if steps else -1
+
+    def slot_of(self, step: int) -> int:
+        return self.complete_steps().get(step, -1)
+
+    def write_slot(self) -> int:
+        """The slot the next save writes: never the latest complete one."""
+        latest = self.latest_slot()
+        if latest < 0:
+            return 0
+        return (latest + 1) % self.num_slots
 
     def no_checkpoint_state(self) -> bool:
         return self.complete_step() == 0
 
     no_checkpint_state = no_checkpoint_state  # reference spelling
 
-    def load_state_dict(self) -> Dict:
-        """Zero-copy CPU view of the complete checkpoint ({} if none)."""
-        if self.complete_step() == 0:
+    def load_state_dict(self, slot: Optional[int] = None) -> Dict:
+        """Zero-copy CPU view of a complete checkpoint ({} if none)."""
+        if slot is None:
+            slot = self.latest_slot()
+        if slot < 0 or self.slot_step(slot) == 0:
             return {}
-        meta = self.metadata.get()
+        meta = self.get_meta(slot)
         tree = meta.get("tree")
         if tree is None:
             return {}
-        sd = tensors_from_payload(tree, self.shared_memory.buf, HEADER_BYTES)
+        sd = tensors_from_payload(tree, self.shared_memory.buf, self.payload_offset(slot))
         if isinstance(sd, dict):
             sd[DLROVER_CKPT_CONFIG_KEY] = meta.get(DLROVER_CKPT_CONFIG_KEY)
         return sd
+
+    # ---------------------------------------------------- replica transport
+    def export_slot(self, slot: int):
+        """(payload bytes view, metadata) of a complete slot, for replicas."""
+        return self.payload_view(slot), self.get_meta(slot)
+
+    def import_slot(self, data, meta: dict):
+        """Install a peer's copy as this shard's (only) complete checkpoint."""
+        self.close()
+        self.init_shared_memory(create=True, size=len(data))
+        off = self.payload_offset(0)
+        self.shared_memory.buf[off: off + len(data)] = data
+        cfg: CheckpointConfig = meta[DLROVER_CKPT_CONFIG_KEY]
+        self.metas[0].set(meta)
+        for r in range(cfg.num_slices):
+            self.set_slice_step(0, r, cfg.step)
 
     def reset(self):
         self._need_creation = True
@@ -186,4 +288,5 @@ class SharedMemoryHandler:
         except Exception as e:  # pragma: no cover
             logger.warning(f"unlink shm {self._shm_name}: {e}")
         self.close()
-        self.metadata.unlink()
+        for m in self.metas:
+            m.unlink()

@@ -42,9 +42,10 @@ def test_single_node_fault_restart_restores_from_memory(tmp_path):
     out = tmp_path / "out.jsonl"
     p = _run(["--nnodes", "1", "--nproc-per-node", "2", "--max-restarts", "2", EXAMPLE, "--steps", "16",
               "--out", str(out), "--ckpt-dir", str(tmp_path / "ck")],
-             {"DWAMD_FAULT_INJECT_STEP": "6", "DWAMD_FAULT_INJECT_RANK": "1"})
+             {"DWAMD_FAULT_INJECT_STEP": "6", "DWAMD_FAULT_INJECT_RANK": "1", "DWAMD_STANDBY_DELAY": "0"})
     log, _ = p.communicate(timeout=240)
     assert p.returncode == 0, log[-3000:]
+    assert "2 from warm standby" in log  # the restart reused the pre-started interpreters
     res = _results(out)
     assert len(res) == 1
     assert res[0]["restart"] == 1 and res[0]["start_step"] == 6  # resumed from the in-memory step-6 checkpoint

@@ -48,6 +48,34 @@ def test_single_process_memory_roundtrip(tmp_path):
     ck.close()
 
 
+def test_double_buffer_survives_torn_save(tmp_path):
+    """A process dying mid-snapshot must leave the previous checkpoint intact."""
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+    from dlrover_wuqiong_amd.flash_checkpoint.shm_handler import CheckpointConfig
+
+    ck = DdpCheckpointer(str(tmp_path / "ck"))
+    h = ck.engine._shm_handler
+    for step in (4, 8):
+        assert ck.save_checkpoint(step, {"w": torch.full((1000,), float(step))}, storage_type=StorageType.MEMORY)
+    assert h.complete_steps() == {4: 0, 8: 1}
+    # torn save of step 12: the writer invalidated its slot and died
+    slot = h.write_slot()
+    assert slot == 0
+    h.set_slice_step(slot, 0, 0)
+    h.set_metadata(slot, h.get_meta(1)["tree"], CheckpointConfig(step=12))
+    h.payload_view(slot)[:16] = b"\xff" * 16
+    assert h.complete_steps() == {8: 1}
+    ck.close()
+    # a restarted process restores step 8 and its first save goes to the other slot
+    ck2 = DdpCheckpointer(str(tmp_path / "ck"))
+    out = ck2.load_checkpoint()
+    assert torch.equal(out["w"], torch.full((1000,), 8.0))
+    assert ck2.save_checkpoint(16, {"w": torch.full((1000,), 16.0)}, storage_type=StorageType.MEMORY)
+    assert ck2.engine._shm_handler.complete_steps() == {16: 0, 8: 1}
+    ck2.close()
+
+
 def test_save_to_storage_and_reload(tmp_path):
     from dlrover_wuqiong_amd.common.storage import KeepLatestStepStrategy
     from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
@@ -95,7 +123,7 @@ def _split_worker(rank, world, port, root, q):
         assert ck.save_checkpoint(4, sd, storage_type=StorageType.MEMORY)
         dist.barrier()
         h = ck.engine._shm_handler
-        assert h.complete_step() == 4, h.slice_steps(world)
+        assert h.complete_step() == 4, h.complete_steps()
         out = ck.load_checkpoint()
         ok = torch.equal(out["a"], sd["a"]) and torch.equal(out["b"], sd["b"]) and out["meta"] == {"k": "v"}
         # persist through the saver of local rank 0

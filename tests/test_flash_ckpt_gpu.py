@@ -78,3 +78,54 @@ def test_gpu_save_to_disk_is_torch_loadable(tmp_path):
     sd = torch.load(d / "9" / "rank_0.pt", weights_only=True)
     assert torch.equal(sd["model"]["h.0.attn.c_attn.weight"], model.h[0].attn.c_attn.weight.cpu())
     ck.close()
+
+
+def test_gpu_fsdp2_shard_checkpoint(tmp_path, monkeypatch):
+    """FSDP2 (fully_shard) on one GPU over RCCL: memory snapshot, in-place
+    restore of DTensor shards + optimizer state, DCP-format persistence."""
+    import torch.distributed as dist
+    from torch.distributed.fsdp import fully_shard
+
+    from conftest import free_port
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.fsdp import FsdpShardCheckpointer, wait_for_persist
+
+    for k, v in dict(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1",
+                     LOCAL_RANK="0", LOCAL_WORLD_SIZE="1").items():
+        monkeypatch.setenv(k, v)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    try:
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Linear(256, 512), torch.nn.GELU(), torch.nn.Linear(512, 64)).cuda()
+        for m in model:
+            if isinstance(m, torch.nn.Linear):
+                fully_shard(m)
+        fully_shard(model)
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+
+        def train():
+            model(torch.randn(8, 256, device="cuda")).square().mean().backward()
+            opt.step()
+            opt.zero_grad()
+
+        train()
+        ck = FsdpShardCheckpointer(str(tmp_path / "ck"))
+        assert ck.save_checkpoint(3, model, opt, {"epoch": 1}, storage_type=StorageType.DISK)
+        ck.wait_latest_checkpoint()
+        want = {k: v.to_local().clone() for k, v in model.state_dict().items()}
+        assert wait_for_persist(str(tmp_path / "ck"), 3, timeout=60)
+        train()
+        extra = ck.load_checkpoint(model, opt, extra_sd={"epoch": 0})
+        torch.cuda.synchronize()
+        assert extra["step"] == 3 and extra["epoch"] == 1
+        for k, v in model.state_dict().items():
+            assert torch.equal(v.to_local(), want[k]), k
+        import torch.distributed.checkpoint as dist_cp
+
+        sd = {"model": {k: torch.zeros_like(v.full_tensor()).cpu() for k, v in model.state_dict().items()}}
+        dist_cp.load(sd, checkpoint_id=str(tmp_path / "ck" / "3"), no_dist=True)
+        for k, v in sd["model"].items():
+            assert torch.equal(v, want[k].cpu()), k
+        ck.close()
+    finally:
+        dist.destroy_process_group()
