@@ -36,6 +36,19 @@ from ..flash_checkpoint.shm_handler import (DLROVER_CKPT_CONFIG_KEY, EVENT_QUEUE
                                             CheckpointSharedObjPrefix, SharedMemoryHandler, slot_lock_name)
 
 
+def _writer_for(path: str):
+    """File format by extension: safetensors for ``*.safetensors`` (HF
+    weights), ``torch.save`` otherwise."""
+    if str(path).endswith(".safetensors"):
+        def write(sd, p):
+            from safetensors.torch import save_file
+
+            save_file({k: v.contiguous() for k, v in sd.items()}, p, metadata={"format": "pt"})
+
+        return write
+    return torch.save
+
+
 class AsyncCheckpointSaver:
     _saver_instance: Optional["AsyncCheckpointSaver"] = None
     _factory_started = False
@@ -249,7 +262,7 @@ class AsyncCheckpointSaver:
         sd.pop(DLROVER_CKPT_CONFIG_KEY, None)
         for name, path in (cfg.paths or {}).items():
             if name in sd:
-                self.storage.write_state_dict(sd[name], path, torch.save)
+                self.storage.write_state_dict(sd[name], path, _writer_for(path))
 
     def commit_checkpoint(self, step: int, step_done_dir: str, timeout=600):
         deadline = time.time() + timeout
@@ -283,9 +296,12 @@ class AsyncCheckpointSaver:
         """Persist the latest complete in-memory checkpoint (e.g. after a
         worker failure, before restarting the workers)."""
         common = None
+        per_shard = []
         for h in self._shm_handlers:
             steps = set(h.complete_steps())
+            per_shard.append(sorted(steps))
             common = steps if common is None else common & steps
+        logger.info(f"breakpoint save: complete in-memory steps per local shard: {per_shard}")
         if not common:
             logger.info("no complete in-memory checkpoint to persist")
             return False
@@ -327,7 +343,7 @@ class TempDirCheckpointSaver(AsyncCheckpointSaver):
         for name, path in (cfg.paths or {}).items():
             if name in sd:
                 rel = os.path.relpath(path, self.checkpoint_dir)
-                self.storage.write_state_dict(sd[name], os.path.join(stage, rel), torch.save)
+                self.storage.write_state_dict(sd[name], os.path.join(stage, rel), _writer_for(path))
 
     def commit_checkpoint(self, step, step_done_dir, timeout=600):
         stage = os.path.join(self.checkpoint_dir, self._STAGE_DIR, str(step))
@@ -364,14 +380,31 @@ class MegatronCheckpointSaver(CommonDirCheckpointSaver):
     TRACER_FILE = "latest_checkpointed_iteration.txt"
 
     def update_tracker_file(self, step):
+        super().update_tracker_file(step)
         self.storage.write(str(step), os.path.join(self.checkpoint_dir, self.TRACER_FILE))
 
 
 class DeepSpeedCheckpointSaver(CommonDirCheckpointSaver):
+    """Commits DeepSpeed's ``latest`` with the checkpoint's tag (free-form,
+    e.g. ``global_step100``); ``._dlrover_ds_tags/{step}`` remembers it so a
+    later memory-only save can restore ``latest``."""
+
     TRACER_FILE = "latest"
+    TAGS_DIR = "._dlrover_ds_tags"
+
+    def persist_to_storage(self, shard_id, cfg, slot):
+        super().persist_to_storage(shard_id, cfg, slot)
+        tag = (cfg.paths or {}).get("__tag__")
+        if tag:
+            if not hasattr(self, "_step_tags"):
+                self._step_tags = {}
+            self._step_tags[cfg.step] = tag
 
     def update_tracker_file(self, step):
-        self.storage.write(f"global_step{step}", os.path.join(self.checkpoint_dir, self.TRACER_FILE))
+        super().update_tracker_file(step)
+        tag = getattr(self, "_step_tags", {}).pop(step, str(step))
+        self.storage.write(tag, os.path.join(self.checkpoint_dir, self.TAGS_DIR, str(step)))
+        self.storage.write(tag, os.path.join(self.checkpoint_dir, self.TRACER_FILE))
 
 
 class FsdpDcpSaver(CommonDirCheckpointSaver):

@@ -105,6 +105,32 @@ class PinnedRegistry:
                 self._ranges.append((ga, ge))
             return True
 
+    def split(self, addr: int, nbytes: int) -> List[Tuple[int, int, bool]]:
+        """Cut [addr, addr+nbytes) at registration boundaries: HIP rejects a
+        pinned-kind copy whose host range spans two hipHostRegister'ed
+        allocations ("invalid argument").  Returns (addr, n, pinned)."""
+        end = addr + nbytes
+        out: List[Tuple[int, int, bool]] = []
+        cur = addr
+        with self._lock:
+            ranges = sorted(self._ranges)
+        for ra, re in ranges:
+            if re <= cur:
+                continue
+            if ra >= end:
+                break
+            if ra > cur:
+                out.append((cur, ra - cur, False))
+                cur = ra
+            e = min(re, end)
+            out.append((cur, e - cur, True))
+            cur = e
+            if cur >= end:
+                break
+        if cur < end:
+            out.append((cur, end - cur, False))
+        return out
+
     def release_all(self):
         with self._lock:
             for (a, _e) in self._ranges:
@@ -207,16 +233,18 @@ class GpuCopier:
                     self.side_stream.wait_event(ev)  # device-side dependency only
                     t0 = time.perf_counter()
                     dst = shm_payload_addr + lo
+                    src = self._staging.data_ptr()
                     sp = ctypes.c_void_p(self.side_stream.cuda_stream)
+                    segs = self.pinned.split(dst, n) if pinned else [(dst, n, False)]
                     dptr = _kern().dw_host_device_ptr(ctypes.c_void_p(dst)) if (
-                        pinned and self.flush_mode == "kernel") else None
+                        pinned and self.flush_mode == "kernel" and len(segs) == 1) else None
                     if dptr and (n % 16 == 0):
-                        err = _kern().dw_stream_copy(ctypes.c_void_p(dptr), ctypes.c_void_p(self._staging.data_ptr()),
-                                                     n, self.flush_blocks, sp)
+                        _check(_kern().dw_stream_copy(ctypes.c_void_p(dptr), ctypes.c_void_p(src), n,
+                                                      self.flush_blocks, sp), "D2H flush")
                     else:
-                        err = _kern().dw_memcpy_async(ctypes.c_void_p(dst), ctypes.c_void_p(self._staging.data_ptr()),
-                                                      n, 1 if pinned else 3, sp)
-                    _check(err, "D2H flush")
+                        for a, c, p in segs:
+                            _check(_kern().dw_memcpy_async(ctypes.c_void_p(a), ctypes.c_void_p(src + (a - dst)), c,
+                                                           1 if p else 3, sp), "D2H flush")
                 _check(_kern().dw_stream_sync(ctypes.c_void_p(self.side_stream.cuda_stream)), "flush sync")
                 dt = time.perf_counter() - t0
                 self.flush_stats.append((n, dt))
@@ -281,8 +309,9 @@ class GpuCopier:
             sp = ctypes.c_void_p(stream.cuda_stream)
             for (s, d, n), f in zip(pieces, futs):
                 pinned = f.result()
-                _check(_kern().dw_memcpy_async(ctypes.c_void_p(d), ctypes.c_void_p(s), n, 0 if pinned else 3, sp),
-                       "H2D restore")
+                for a, c, p in (self.pinned.split(s, n) if pinned else [(s, n, False)]):
+                    _check(_kern().dw_memcpy_async(ctypes.c_void_p(d + (a - s)), ctypes.c_void_p(a), c,
+                                                   0 if p else 3, sp), "H2D restore")
 
     def close(self):
         try:

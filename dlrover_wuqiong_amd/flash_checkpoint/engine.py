@@ -265,6 +265,11 @@ class CheckpointEngine(ABC):
     # ----------------------------------------------------------- core save
     def save_state_dict_to_memory(self, state_dict: Dict, conf: CheckpointConfig) -> bool:
         if not self._replicated and self._local_rank != self.local_shard_id:
+            # not a saving rank (e.g. a data-parallel replica of a TP/PP shard):
+            # still takes part in the slot vote of the saving ranks
+            if dist.is_available() and dist.is_initialized():
+                t = torch.ones(self._shm_handler.num_slots, dtype=torch.int64)
+                dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self._ctl_group)
             return False
         t0 = time.perf_counter()
         copier = self._device_copier()
@@ -278,19 +283,12 @@ class CheckpointEngine(ABC):
         if self._next_slot is None:
             # first save of this process (nothing in flight): never the latest complete slot
             self._next_slot = h.write_slot()
-        slot = self._next_slot
-        lock = self._shm_locks[slot]
-        acquired = False
-        if self._is_shard_owner:
-            acquired = lock.acquire(blocking=False)
-        owner_ok = acquired if self._is_shard_owner else True
-        if not check_all_rank_ready(self._ctl_group, owner_ok and bool(state_dict)):
-            if acquired:
-                lock.release()
+        slot = self._choose_slot(h, bool(state_dict))
+        if slot < 0:
             logger.info(f"rank {self._rank} skips the memory checkpoint of step {conf.step}: "
-                        f"the agent is persisting slot {slot}")
+                        "the agent is persisting the in-memory checkpoints")
             return False
-        self._lock_held = acquired
+        self._lock_held = self._is_shard_owner
         self._next_slot = (slot + 1) % h.num_slots
 
         conf.rank = self._rank
@@ -319,6 +317,38 @@ class CheckpointEngine(ABC):
         self._last_save_blocking = time.perf_counter() - t0
         self._replica_manager.backup(self._shm_handler)
         return True
+
+    def _choose_slot(self, h: SharedMemoryHandler, has_state: bool) -> int:
+        """Slot this save writes (same on every rank), its lock held by the
+        shard owner; -1 = skip.  Preferred: the alternating ``_next_slot``.
+        If the agent holds it (persisting), the other slot is used provided
+        an intact complete checkpoint remains (the one being persisted).
+        Shard owners vote with per-slot flags (gloo MIN) so all ranks agree."""
+        n = h.num_slots
+        order = [self._next_slot] + [s for s in range(n) if s != self._next_slot]
+        flags = [1] * n
+        acquired = {}
+        if self._is_shard_owner:
+            complete = h.complete_steps()
+            complete_slots = set(complete.values())
+            for s in order:
+                others_intact = any(c in complete_slots for c in range(n) if c != s)
+                allowed = s == self._next_slot or others_intact or not complete_slots
+                ok = allowed and has_state and self._shm_locks[s].acquire(blocking=False)
+                flags[s] = 1 if ok else 0
+                if ok:
+                    acquired[s] = True
+        elif not has_state:
+            flags = [0] * n
+        if dist.is_available() and dist.is_initialized():
+            t = torch.tensor(flags, dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self._ctl_group)
+            flags = [int(x) for x in t]
+        slot = next((s for s in order if flags[s]), -1)
+        for s in acquired:
+            if s != slot:
+                self._shm_locks[s].release()
+        return slot
 
     def _cpu_save_slice(self, layout: Layout, base: int, lo: int, hi: int):
         import ctypes
@@ -377,6 +407,8 @@ class CheckpointEngine(ABC):
             return 0, {}
         if not holds:
             return 0, {}
+        logger.info(f"rank {self._rank}: restoring step {step} from memory slot {slot} "
+                    f"(complete in memory: {sorted(h.complete_steps())})")
         tree = h.get_meta(slot)["tree"]
         if target is not None:
             sd = self._restore_into(tree, target, slot)
@@ -478,7 +510,8 @@ class CheckpointEngine(ABC):
         ...
 
     def _notify_persist(self, step: int):
-        if self._rank == 0 and self._event_queue is not None:
+        # every node's agent persists its own local shards (node 0 also commits)
+        if self._local_rank == 0 and self._event_queue is not None:
             self._event_queue.put(CheckpointEvent(type=CheckpointEventType.SAVE, step=step), timeout=60)
 
 
@@ -488,11 +521,14 @@ class FullCheckpointEngine(CheckpointEngine):
     (reference semantics for partitioned models)."""
 
     def __init__(self, checkpoint_dir, storage=None, local_shard_num=1, global_shard_num=1,
-                 comm_backend="", save_timeout=CheckpointConstant.SAVE_TIMEOUT, replica_count=0):
+                 comm_backend="", save_timeout=CheckpointConstant.SAVE_TIMEOUT, replica_count=0,
+                 replicated: Optional[bool] = None):
+        """``replicated=False`` with ``local_shard_num=1``: only local rank 0
+        holds the state (e.g. DeepSpeed ZeRO-0 saves on rank 0 only)."""
         self._local_shard_num = max(1, local_shard_num)
         self._global_shard_num = max(global_shard_num, self._local_shard_num)
         super().__init__(checkpoint_dir, storage, comm_backend, save_timeout, replica_count,
-                         replicated=(self._local_shard_num == 1))
+                         replicated=(self._local_shard_num == 1) if replicated is None else replicated)
 
     def get_saving_ranks(self):
         return None  # every rank participates (slices)

@@ -45,12 +45,15 @@ def main():
     lr = int(os.getenv("LOCAL_RANK", "0"))
     cuda = torch.cuda.is_available()
     dev = torch.device("cuda", lr) if cuda else torch.device("cpu")
+    tl = {}
     if cuda:
         torch.cuda.set_device(dev)
         torch.cuda.set_stream(torch.cuda.Stream(dev))
+    tl["cuda_init"] = time.time() - t_proc
     world = int(os.getenv("WORLD_SIZE", "1"))
     if world > 1:
         dist.init_process_group("nccl" if cuda else "gloo", device_id=dev if cuda else None)
+    tl["pg_init"] = time.time() - t_proc
     rank = int(os.getenv("RANK", "0"))
     dtype = torch.bfloat16 if cuda else torch.float32
     cfg = GPT2Config.named(a.model)
@@ -63,7 +66,9 @@ def main():
     opt = FusedAdamW(flat, lr=1e-4, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0)
     ddp = FlatDDP(model, flat)
     opt.grad_scale = 1.0 / world
+    tl["model_opt"] = time.time() - t_proc
     ckpt = DdpCheckpointer(a.ckpt_dir)
+    tl["ckpt_init"] = time.time() - t_proc
 
     def state(step_t):
         return {"model": model.state_dict(), "optimizer": opt.state_dict(), "step": step_t}
@@ -80,7 +85,7 @@ def main():
     if log:
         log.write(json.dumps({"event": "start", "restart": int(os.getenv("TORCHELASTIC_RESTART_COUNT", "0")),
                               "start_step": start, "t": time.time(), "proc_start": t_proc,
-                              "restore_sec": t_restore}) + "\n")
+                              "restore_sec": t_restore, "timeline": tl}) + "\n")
         log.flush()
     for step in range(start, a.steps):
         maybe_inject_fault(step)

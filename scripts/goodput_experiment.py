@@ -68,6 +68,7 @@ def main():
            "recovery_gap_s": round(gap, 3) if gap is not None else None,
            "restarts": len(starts) - 1, "resumed_from_step": starts[-1]["start_step"],
            "restore_sec_after_failure": round(starts[-1]["restore_sec"], 3),
+           "restart_timeline_s": {k: round(v, 3) for k, v in starts[-1].get("timeline", {}).items()},
            "process_start_to_first_step_s": round(
                next(e["t"] for e in steps if e["t"] > starts[-1]["t"]) - starts[-1]["proc_start"], 3),
            "launcher_wall_s": round(wall, 2), "model": a.model, "nproc": a.nproc,

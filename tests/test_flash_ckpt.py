@@ -76,6 +76,32 @@ def test_double_buffer_survives_torn_save(tmp_path):
     ck2.close()
 
 
+def test_slot_fallback_while_agent_persists(tmp_path):
+    from dlrover_wuqiong_amd.common.multi_process import SharedLock
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+    from dlrover_wuqiong_amd.flash_checkpoint.shm_handler import slot_lock_name
+
+    ck = DdpCheckpointer(str(tmp_path / "ck"))
+    h = ck.engine._shm_handler
+
+    def save(step):
+        return ck.save_checkpoint(step, {"w": torch.full((1000,), float(step))}, storage_type=StorageType.MEMORY)
+
+    assert save(4) and save(8)
+    assert h.complete_steps() == {4: 0, 8: 1}
+    agent_lock = SharedLock(slot_lock_name(0, 0), create=True)
+    assert agent_lock.acquire(blocking=False)  # the agent persists slot 0 (step 4)
+    assert save(12)  # slot 0 busy -> slot 1 (slot 0 stays an intact checkpoint)
+    assert h.complete_steps() == {4: 0, 12: 1}
+    assert save(16)
+    assert h.complete_steps() == {4: 0, 16: 1}
+    agent_lock.release()
+    assert save(20)
+    assert h.complete_steps() == {20: 0, 16: 1}
+    ck.close()
+
+
 def test_save_to_storage_and_reload(tmp_path):
     from dlrover_wuqiong_amd.common.storage import KeepLatestStepStrategy
     from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
