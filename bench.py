@@ -258,7 +258,9 @@ def main():
         "vs_baseline": round(save_sec / REF_SAVE_SEC, 4),
         "dtype": "bf16" if cuda else "fp32",
         "data": "synthetic tokens, random-init weights",
-        "config": {"model": "GPT2-1.5B (gpt2-xl: 48L, 1600H, 25 heads)", "global_batch": B * world,
+        "config": {"model": ("GPT2-1.5B (gpt2-xl: 48L, 1600H, 25 heads)" if args.model == "gpt2-1.5b" else
+                             f"{args.model} ({cfg.n_layer}L, {cfg.n_embd}H, {cfg.n_head} heads)"),
+                   "global_batch": B * world,
                    "seq_len": S, "parallelism": f"dp{world}"},
         "save_sec_mean": round(save_sec, 4),
         "save_sec_max": round(save_max, 4),

@@ -22,6 +22,9 @@
 #include <fcntl.h>
 #include <pthread.h>
 #include <signal.h>
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <climits>
 #include <stdint.h>
 #include <string.h>
 #include <sys/mman.h>
@@ -255,13 +258,18 @@ uint32_t dw_crc32c(const void* data, uint64_t n, uint32_t seed) {
 // ---------------------------------------------------------------------------
 // Control blocks: robust lock, queue, blob dict
 // ---------------------------------------------------------------------------
-static const uint64_t kMagic = 0x44574d4443544c31ull;  // "DWMDCTL1"
+// Waiting uses futexes on sequence words instead of process-shared condition
+// variables: a glibc condvar signal can block forever when one of its waiters
+// was SIGKILLed (it waits for the dead waiter to leave its group), and killed
+// agents/workers are exactly what this runtime must survive.  FUTEX_WAKE never
+// blocks, and a dead waiter simply never consumes its wake-up.
+static const uint64_t kMagic = 0x44574d4443544c32ull;  // "DWMDCTL2"
 
 struct CtlHeader {
   std::atomic<uint64_t> magic;
   pthread_mutex_t mu;
-  pthread_cond_t not_empty;
-  pthread_cond_t not_full;
+  std::atomic<uint32_t> seq_not_empty;
+  std::atomic<uint32_t> seq_not_full;
   uint32_t kind;       // 1 lock, 2 queue, 3 dict
   uint32_t pad0;
   uint64_t capacity;   // queue: max messages
@@ -288,6 +296,29 @@ static int robust_lock(CtlHeader* h) {
   int r = pthread_mutex_lock(&h->mu);
   if (r == EOWNERDEAD) { pthread_mutex_consistent(&h->mu); r = 0; }
   return r;
+}
+
+static void seq_notify(std::atomic<uint32_t>* w) {
+  w->fetch_add(1, std::memory_order_release);
+  syscall(SYS_futex, (uint32_t*)w, FUTEX_WAKE, INT32_MAX, nullptr, nullptr, 0);
+}
+
+// Called with h->mu held; releases it, sleeps until *w changes (or at most
+// `slice_s`), re-acquires it.  Spurious wake-ups are fine: callers re-check.
+static int seq_wait_unlocked(CtlHeader* h, std::atomic<uint32_t>* w, double slice_s) {
+  uint32_t seen = w->load(std::memory_order_acquire);
+  pthread_mutex_unlock(&h->mu);
+  struct timespec rel;
+  rel.tv_sec = (time_t)slice_s;
+  rel.tv_nsec = (long)((slice_s - (double)rel.tv_sec) * 1e9);
+  syscall(SYS_futex, (uint32_t*)w, FUTEX_WAIT, seen, &rel, nullptr, 0);
+  return robust_lock(h);
+}
+
+static double secs_left(const struct timespec* dl) {
+  struct timespec now;
+  clock_gettime(CLOCK_MONOTONIC, &now);
+  return (double)(dl->tv_sec - now.tv_sec) + 1e-9 * (double)(dl->tv_nsec - now.tv_nsec);
 }
 
 static void abs_deadline(struct timespec* ts, double timeout_s) {
@@ -340,13 +371,8 @@ void* dw_ctl_open(const char* name, int create, uint32_t kind, uint64_t capacity
     pthread_mutexattr_setrobust(&ma, PTHREAD_MUTEX_ROBUST);
     pthread_mutex_init(&h->mu, &ma);
     pthread_mutexattr_destroy(&ma);
-    pthread_condattr_t ca;
-    pthread_condattr_init(&ca);
-    pthread_condattr_setpshared(&ca, PTHREAD_PROCESS_SHARED);
-    pthread_condattr_setclock(&ca, CLOCK_MONOTONIC);
-    pthread_cond_init(&h->not_empty, &ca);
-    pthread_cond_init(&h->not_full, &ca);
-    pthread_condattr_destroy(&ca);
+    h->seq_not_empty.store(0);
+    h->seq_not_full.store(0);
     h->kind = kind;
     h->capacity = capacity;
     h->data_size = data_size;
@@ -390,18 +416,15 @@ int dw_lock_acquire(void* p, int blocking, double timeout) {
   struct timespec dl;
   if (timeout >= 0) abs_deadline(&dl, timeout);
   while (h->held) {
-    int r;
+    // wake at least every 100 ms to detect dead holders
+    double slice = 0.1;
     if (timeout >= 0) {
-      r = pthread_cond_timedwait(&h->not_full, &h->mu, &dl);
-    } else {
-      struct timespec slice;
-      abs_deadline(&slice, 1.0);  // wake periodically to detect dead holders
-      r = pthread_cond_timedwait(&h->not_full, &h->mu, &slice);
-      if (r == ETIMEDOUT) r = 0;
+      double left = secs_left(&dl);
+      if (left <= 0) { pthread_mutex_unlock(&h->mu); return 0; }
+      if (left < slice) slice = left;
     }
-    if (r == EOWNERDEAD) { pthread_mutex_consistent(&h->mu); r = 0; }
+    if (seq_wait_unlocked(h, &h->seq_not_full, slice) != 0) return 0;
     if (h->held && h->holder_pid > 0 && kill(h->holder_pid, 0) != 0 && errno == ESRCH) h->held = 0;
-    if (r == ETIMEDOUT && h->held) { pthread_mutex_unlock(&h->mu); return 0; }
   }
   h->held = 1;
   h->holder_pid = getpid();
@@ -414,8 +437,8 @@ int dw_lock_release(void* p) {
   if (robust_lock(h) != 0) return -1;
   h->held = 0;
   h->holder_pid = 0;
-  pthread_cond_broadcast(&h->not_full);
   pthread_mutex_unlock(&h->mu);
+  seq_notify(&h->seq_not_full);
   return 0;
 }
 
@@ -461,15 +484,18 @@ int dw_queue_put(void* p, const void* msg, uint64_t len, int blocking, double ti
       if (h->tail >= h->data_size) h->tail = 0;
       h->used += need;
       h->count += 1;
-      pthread_cond_signal(&h->not_empty);
       pthread_mutex_unlock(&h->mu);
+      seq_notify(&h->seq_not_empty);
       return 0;
     }
     if (!blocking) { pthread_mutex_unlock(&h->mu); return 1; }
-    int r = (timeout >= 0) ? pthread_cond_timedwait(&h->not_full, &h->mu, &dl)
-                           : pthread_cond_wait(&h->not_full, &h->mu);
-    if (r == EOWNERDEAD) { pthread_mutex_consistent(&h->mu); r = 0; }
-    if (r == ETIMEDOUT) { pthread_mutex_unlock(&h->mu); return 1; }
+    double slice = 0.1;
+    if (timeout >= 0) {
+      double left = secs_left(&dl);
+      if (left <= 0) { pthread_mutex_unlock(&h->mu); return 1; }
+      if (left < slice) slice = left;
+    }
+    if (seq_wait_unlocked(h, &h->seq_not_full, slice) != 0) return -1;
   }
 }
 
@@ -483,10 +509,13 @@ int64_t dw_queue_get(void* p, void* buf, uint64_t cap, int blocking, double time
   if (timeout >= 0) abs_deadline(&dl, timeout);
   while (h->count == 0) {
     if (!blocking) { pthread_mutex_unlock(&h->mu); return -1; }
-    int r = (timeout >= 0) ? pthread_cond_timedwait(&h->not_empty, &h->mu, &dl)
-                           : pthread_cond_wait(&h->not_empty, &h->mu);
-    if (r == EOWNERDEAD) { pthread_mutex_consistent(&h->mu); r = 0; }
-    if (r == ETIMEDOUT && h->count == 0) { pthread_mutex_unlock(&h->mu); return -1; }
+    double slice = 0.1;
+    if (timeout >= 0) {
+      double left = secs_left(&dl);
+      if (left <= 0) { pthread_mutex_unlock(&h->mu); return -1; }
+      if (left < slice) slice = left;
+    }
+    if (seq_wait_unlocked(h, &h->seq_not_empty, slice) != 0) return -1;
   }
   char* d = ctl_data(h);
   uint64_t tail_room = h->data_size - h->head;
@@ -507,8 +536,8 @@ int64_t dw_queue_get(void* p, void* buf, uint64_t cap, int blocking, double time
   h->used -= sz;
   h->count -= 1;
   if (h->count == 0) { h->head = h->tail = 0; h->used = 0; }
-  pthread_cond_signal(&h->not_full);
   pthread_mutex_unlock(&h->mu);
+  seq_notify(&h->seq_not_full);
   return (int64_t)len;
 }
 
@@ -528,8 +557,8 @@ int dw_blob_set(void* p, const void* data, uint64_t len) {
   memcpy(ctl_data(h), data, len);
   h->blob_len = len;
   h->version += 1;
-  pthread_cond_broadcast(&h->not_empty);
   pthread_mutex_unlock(&h->mu);
+  seq_notify(&h->seq_not_empty);
   return 0;
 }
 

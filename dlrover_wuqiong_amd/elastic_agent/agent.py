@@ -81,6 +81,8 @@ class ElasticLaunchConfig:
     standby_delay: float = field(default_factory=lambda: float(os.getenv("DWAMD_STANDBY_DELAY", "3")))
     # persist the breakpoint checkpoint while the new workers already start
     async_breakpoint_save: bool = True
+    # exit (and let the platform relaunch the node) on GPU/driver fault signatures
+    exit_on_node_error: bool = field(default_factory=lambda: os.getenv("DWAMD_EXIT_ON_NODE_ERROR", "0") == "1")
 
     def auto_configure_params(self):
         """nnodes from NODE_NUM, nproc from the visible GPUs, network check
@@ -428,6 +430,10 @@ class ElasticTrainingAgent:
                                        self.config.node_unit, int(self.config.join_timeout))
         hb = threading.Thread(target=self._heartbeat_loop, daemon=True, name="dwamd-heartbeat")
         hb.start()
+        if self.config.log_dir:
+            from .diagnosis import DiagnosisMonitor
+
+            DiagnosisMonitor(self.client, self.config.log_dir).start()
         try:
             if self.config.network_check:
                 from .node_check import run_network_check
@@ -466,13 +472,24 @@ class ElasticTrainingAgent:
             if res.state == RunResult.FAILED:
                 self.events.append((time.time(), "failed"))
                 logger.error(f"worker failure: { {r: (f['exitcode']) for r, f in res.failures.items()} }")
+                from .diagnosis import classify_failure
+
+                level = max((classify_failure(f.get("message", "")) for f in res.failures.values()),
+                            key=lambda lv: lv == TrainingExceptionLevel.NODE_ERROR)
                 try:
-                    self.client.report_failures(json.dumps(res.failures), self.restart_count,
-                                                TrainingExceptionLevel.PROCESS_ERROR)
+                    self.client.report_failures(json.dumps(res.failures), self.restart_count, level)
                 except Exception:
                     pass
                 self._stop_workers()
                 self._save_ckpt_to_storage()
+                if level == TrainingExceptionLevel.NODE_ERROR and self.config.exit_on_node_error:
+                    # hardware signature: let the platform replace this node
+                    logger.error("GPU/driver fault signature in the worker log: exiting for node relaunch")
+                    self._discard_standbys()
+                    if self._bp_thread is not None:
+                        self._bp_thread.join(timeout=600)
+                    self.client.report_node_event(NodeStatus.FAILED, "node error")
+                    return 2
                 if self.remaining_restarts > 0:
                     self.remaining_restarts -= 1
                     self._restart_workers()

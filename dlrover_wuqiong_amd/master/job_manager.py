@@ -13,12 +13,12 @@ no-op because ``dwamd-run`` agents restart their own worker processes.
 
 import threading
 import time
-from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Tuple
 
 from ..common.constants import (JobConstant, NodeExitReason, NodeStatus, NodeType,
                                 TrainingExceptionLevel)
 from ..common.log import logger
+from ..common.node import Node  # noqa: F401  (re-exported)
 
 # (from, to) -> should_relaunch
 _FLOW: Dict[Tuple[str, str], bool] = {
@@ -44,38 +44,6 @@ def get_node_state_flow(from_status: str, to_status: str) -> Optional[bool]:
     if from_status == to_status:
         return None
     return _FLOW.get((from_status, to_status))
-
-
-@dataclass
-class Node:
-    type: str = NodeType.WORKER
-    id: int = 0
-    rank_index: int = 0
-    name: str = ""
-    status: str = NodeStatus.INITIAL
-    host_addr: str = ""
-    start_time: float = 0.0
-    heartbeat_time: float = 0.0
-    relaunch_count: int = 0
-    max_relaunch_count: int = 3
-    exit_reason: str = ""
-    critical: bool = False
-    used_cpu: float = 0.0
-    used_memory: int = 0
-    gpu_stats: List = field(default_factory=list)
-    paral_config = None
-    restart_training: bool = False
-    reported_failures: List[Tuple[str, str]] = field(default_factory=list)
-
-    def update_status(self, status: str) -> bool:
-        if status == self.status:
-            return False
-        if get_node_state_flow(self.status, status) is None and self.status != NodeStatus.INITIAL:
-            logger.debug(f"node {self.id}: ignore transition {self.status} -> {status}")
-        self.status = status
-        if status == NodeStatus.RUNNING and not self.start_time:
-            self.start_time = time.time()
-        return True
 
 
 class NodeLauncher:

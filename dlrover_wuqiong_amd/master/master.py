@@ -22,12 +22,13 @@ from .shard import TaskManager
 class JobMaster:
     def __init__(self, port: int = 0, node_num: int = 1, launcher: Optional[NodeLauncher] = None,
                  loop_interval: float = 30.0, hang_secs: float = 1800.0,
-                 run_configs: Optional[Dict[str, str]] = None, max_relaunch_count: int = 3):
+                 run_configs: Optional[Dict[str, str]] = None, max_relaunch_count: int = 3,
+                 job_manager: Optional[JobManager] = None, speed_monitor: Optional[SpeedMonitor] = None):
         self.port = port or find_free_port()
         self.node_num = node_num
-        self.job_manager = JobManager(node_num, launcher, max_relaunch_count=max_relaunch_count)
+        self.job_manager = job_manager or JobManager(node_num, launcher, max_relaunch_count=max_relaunch_count)
         self.task_manager = TaskManager()
-        self.speed_monitor = SpeedMonitor()
+        self.speed_monitor = speed_monitor or SpeedMonitor()
         self.rdzv_managers = {
             RendezvousName.ELASTIC_TRAINING: ElasticTrainingRendezvousManager(),
             RendezvousName.NETWORK_CHECK: NetworkCheckRendezvousManager(),
@@ -87,7 +88,67 @@ class JobMaster:
 
 
 LocalJobMaster = JobMaster
-DistributedJobMaster = JobMaster
+
+
+class DistributedJobMaster(JobMaster):
+    """Master that also owns the nodes: launches them through a ``Scaler``,
+    watches them, relaunches failed ones (same rank) and stops the job on
+    unrecoverable failures (reference ``dist_master.py:81-304``)."""
+
+    def __init__(self, job_resource, scaler_factory, watcher_factory=None, port: int = 0,
+                 loop_interval: float = 5.0, hang_secs: float = 1800.0, max_relaunch_count: int = 3,
+                 heartbeat_timeout: float = 300.0, node_unit: int = 1, auto_worker: bool = False,
+                 stats_path: str = ""):
+        from .dist_job_manager import DistributedJobManager
+        from .event_callback import AllReduceNodeHandlingCallback, TaskRescheduleCallback
+        from .stats import JobMetricCollector, LocalStatsReporter
+        from .watcher import ProcessWatcher
+
+        port = port or find_free_port()
+        self.scaler = scaler_factory(f"127.0.0.1:{port}")
+        watcher = watcher_factory(self.scaler) if watcher_factory else ProcessWatcher(self.scaler)
+        speed = SpeedMonitor()
+        jm = DistributedJobManager(job_resource, self.scaler, watcher, max_relaunch_count=max_relaunch_count,
+                                   heartbeat_timeout=heartbeat_timeout, speed_monitor=speed, node_unit=node_unit,
+                                   auto_worker=auto_worker)
+        super().__init__(port=port, node_num=job_resource.worker_num, loop_interval=loop_interval,
+                         hang_secs=hang_secs, max_relaunch_count=max_relaunch_count, job_manager=jm,
+                         speed_monitor=speed)
+        self.rdzv_managers[RendezvousName.ELASTIC_TRAINING].update_rdzv_params(
+            job_resource.worker_num, job_resource.worker_num, 60, node_unit)
+        jm.add_node_event_callback(TaskRescheduleCallback(self.task_manager))
+        jm.add_node_event_callback(AllReduceNodeHandlingCallback(self))
+        self.metric_collector = JobMetricCollector(jm, speed, LocalStatsReporter(stats_path))
+        self._stop_request = None
+
+    def request_stop(self, success: bool, reason: str, msg: str = ""):
+        logger.info(f"job stop requested: success={success} reason={reason} {msg}")
+        self._stop_request = (success, reason, msg)
+        self._stop.set()
+
+    def prepare(self):
+        super().prepare()
+        self.job_manager.start()
+
+    def run(self) -> int:
+        while not self._stop.wait(self._loop_interval):
+            self.task_manager.reassign_timeout_tasks()
+            self.metric_collector.collect_runtime_stats()
+            if self.diagnosis.check_training_hang():
+                logger.error("training hang detected (no global step progress)")
+                self.exit_reason = JobExitReason.HANG_ERROR
+            if self.job_manager.all_workers_exited():
+                ok = self.job_manager.all_workers_succeeded()
+                self.exit_reason = JobExitReason.SUCCEEDED if ok else JobExitReason.WORKER_ERROR
+                logger.info(f"all workers exited (success={ok})")
+                self.metric_collector.collect_job_exit_reason(self.exit_reason)
+                return 0 if ok else 1
+        if self._stop_request is not None:
+            ok, reason, _ = self._stop_request
+            self.exit_reason = reason
+            self.metric_collector.collect_job_exit_reason(reason)
+            return 0 if ok else 1
+        return 0
 
 
 def main(argv=None) -> int:
@@ -101,8 +162,26 @@ def main(argv=None) -> int:
     p.add_argument("--platform", default="local")
     p.add_argument("--loop_interval", type=float, default=30.0)
     p.add_argument("--port_file", default="")
+    p.add_argument("--nproc_per_node", "--nproc-per-node", type=int, default=1)
+    p.add_argument("--max_relaunch_count", "--max-relaunch-count", type=int, default=3)
+    p.add_argument("--log_dir", "--log-dir", default="")
+    p.add_argument("--agent_args", "--agent-args", default="", help="extra dwamd-run flags (one string)")
+    p.add_argument("entry", nargs=argparse.REMAINDER, help="training script + args (platform=process)")
     a = p.parse_args(argv)
-    m = JobMaster(port=a.port, node_num=a.node_num, loop_interval=a.loop_interval)
+    if a.platform == "process":
+        import shlex
+
+        from ..common.node import JobResource
+        from .scaler import ProcessScaler
+
+        jr = JobResource()
+        jr.update_node_group_resource("worker", a.node_num)
+        m = DistributedJobMaster(
+            jr, lambda addr: ProcessScaler(a.job_name, addr, a.entry, a.nproc_per_node, str(a.node_num),
+                                           a.log_dir, agent_args=shlex.split(a.agent_args)),
+            port=a.port, loop_interval=min(a.loop_interval, 5.0), max_relaunch_count=a.max_relaunch_count)
+    else:
+        m = JobMaster(port=a.port, node_num=a.node_num, loop_interval=a.loop_interval)
     m.prepare()
     if a.port_file:
         with open(a.port_file, "w") as f:

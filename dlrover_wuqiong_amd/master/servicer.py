@@ -117,7 +117,7 @@ class MasterServicer:
         node_rank = m.node_rank if m.node_rank >= 0 else m.node_id
         self.job_manager.add_node(m.node_id, NodeType.WORKER, m.node_ip)
         for r in self.rdzv.values():
-            r.add_alive_node(m.node_id)
+            r.add_alive_node(node_rank)
         rnd = mgr.join_rendezvous(node_rank, m.local_world_size, m.node_ip)
         if name == RendezvousName.NETWORK_CHECK:
             # nodes re-checking the network leave the training waiting list

@@ -42,7 +42,7 @@ def parse_args(argv=None):
     p.add_argument("--master-addr", "--master_addr", default="127.0.0.1")
     p.add_argument("--master-port", "--master_port", type=int, default=0)
     p.add_argument("--max-restarts", "--max_restarts", type=int, default=3)
-    p.add_argument("--monitor-interval", "--monitor_interval", type=float, default=0.5)
+    p.add_argument("--monitor-interval", "--monitor_interval", type=float, default=0.1)
     p.add_argument("--rdzv-backend", "--rdzv_backend", default="dlrover-master")
     p.add_argument("--rdzv-endpoint", "--rdzv_endpoint", default="")
     p.add_argument("--rdzv-id", "--rdzv_id", default="")
@@ -137,6 +137,13 @@ def run(a) -> int:
     cfg = build_config(a)
     master_addr = os.getenv(NodeEnv.DLROVER_MASTER_ADDR, "")
     master_proc: Optional[subprocess.Popen] = None
+    if not master_addr and a.master_port and a.node_rank == 0 and not a.standalone:
+        # a job master is already serving there (e.g. started by the platform)
+        from ..common.rpc import addr_connected
+
+        if addr_connected(f"{a.master_addr}:{a.master_port}"):
+            master_addr = f"{a.master_addr}:{a.master_port}"
+            os.environ[NodeEnv.DLROVER_MASTER_ADDR] = master_addr
     if not master_addr:
         port = a.master_port or find_free_port()
         if a.node_rank == 0 or a.standalone:
@@ -163,6 +170,10 @@ def run(a) -> int:
 
 
 def main(argv=None) -> int:
+    import faulthandler
+    import signal
+
+    faulthandler.register(signal.SIGUSR2, all_threads=True)  # `kill -USR2 <agent pid>` dumps every stack
     a = parse_args(argv)
     return run(a)
 

@@ -33,6 +33,8 @@ def main():
     p.add_argument("--out", default="")
     p.add_argument("--hidden", type=int, default=256)
     p.add_argument("--disk-every", type=int, default=0)
+    p.add_argument("--step-sleep", type=float, default=0.0, help="slow steps down (fault-injection tests)")
+    p.add_argument("--progress", default="", help="rank 0 writes the last finished step here")
     a = p.parse_args()
     t_start = time.time()
     cuda = torch.cuda.is_available()
@@ -69,6 +71,11 @@ def main():
         sd = {"model": model.state_dict(), "optimizer": opt.state_dict(), "step": step + 1}
         st = StorageType.DISK if a.disk_every and (step + 1) % a.disk_every == 0 else StorageType.MEMORY
         ckpt.save_checkpoint(step + 1, sd, storage_type=st)
+        if a.progress and rank == 0:
+            with open(a.progress, "w") as f:
+                f.write(str(step + 1))
+        if a.step_sleep:
+            time.sleep(a.step_sleep)
     ckpt.wait_latest_checkpoint()
     dist.barrier()
     if a.out and rank == 0:

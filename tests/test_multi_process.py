@@ -109,3 +109,38 @@ def test_storage_parallel_io(tmp_path):
     from dlrover_wuqiong_amd._native import runtime
 
     assert runtime().dw_crc32c(buf, len(data), 0) == runtime().dw_crc32c(out, len(data), 0)
+
+
+def _blocked_getter(name, prefix):
+    import os
+
+    os.environ["DWAMD_SHM_PREFIX"] = prefix
+    from dlrover_wuqiong_amd.common.multi_process import SharedQueue
+
+    q = SharedQueue(name, create=False)
+    q.get(timeout=60)  # killed while waiting
+
+
+def test_queue_survives_killed_waiter(_isolated_shm):
+    """A waiter SIGKILLed inside get() must not wedge later put/get calls
+    (process-shared condvars can; the futex-based waits cannot)."""
+    import multiprocessing as mp
+    import os
+    import signal
+    import time
+
+    from dlrover_wuqiong_amd.common.multi_process import SharedQueue
+
+    q = SharedQueue("kq", create=True, maxsize=4)
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_blocked_getter, args=("kq", _isolated_shm)) for _ in range(2)]
+    for p in ps:
+        p.start()
+    time.sleep(1.5)
+    for p in ps:
+        os.kill(p.pid, signal.SIGKILL)
+        p.join()
+    t0 = time.time()
+    q.put({"x": 1}, timeout=5)
+    assert q.get(timeout=5) == {"x": 1}
+    assert time.time() - t0 < 2.0
