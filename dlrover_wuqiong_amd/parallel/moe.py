@@ -1,0 +1,176 @@
+"""Mixture-of-Experts layer with expert parallelism (dropless, top-k).
+
+Token path (per MoE layer):
+  1. router logits -> top-k experts + renormalised weights (aux load-balance
+     loss and router z-loss are recorded on the module);
+  2. the T*k (token, expert) assignments are sorted by expert -- one gather
+     builds a contiguous, expert-grouped activation buffer;
+  3. expert parallel: the buffer is exchanged with ONE variable-split
+     ``all_to_all_single`` over the EP group (RCCL; the per-expert counts go
+     first in a tiny all_to_all) and regrouped by local expert;
+  4. the local experts run as a grouped GEMM over the contiguous groups
+     (``grouped_mlp``: per-expert hipBLASLt GEMMs on views of one buffer --
+     no padding, no capacity drop);
+  5. the inverse exchange + un-permute + weighted sum over k.
+
+MI355X sizing: with 288 GB per GPU experts can stay resident at high EP
+degrees; keep EP within a node (xGMI all-to-all is per-link bound: every
+GPU talks to 7 peers over 7 links concurrently) and put DP across nodes.
+
+Parity: ATorch ``atorch/modules/moe`` (``MOELayer``, ``TopkGate``,
+``Experts``, ``_AllToAll``; grouped-GEMM experts) -- re-designed dropless.
+"""
+
+import math
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def _ws(group) -> int:
+    return dist.get_world_size(group) if (dist.is_initialized() and group is not None) else 1
+
+
+class _AllToAllV(torch.autograd.Function):
+    """Variable-split all_to_all_single along dim 0 (autograd: inverse split)."""
+
+    @staticmethod
+    def forward(ctx, x, out_splits: List[int], in_splits: List[int], group):
+        ctx.group, ctx.out_splits, ctx.in_splits = group, out_splits, in_splits
+        out = x.new_empty((sum(out_splits),) + tuple(x.shape[1:]))
+        dist.all_to_all_single(out, x.contiguous(), out_splits, in_splits, group=group)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        gin = g.new_empty((sum(ctx.in_splits),) + tuple(g.shape[1:]))
+        dist.all_to_all_single(gin, g.contiguous(), ctx.in_splits, ctx.out_splits, group=ctx.group)
+        return gin, None, None, None
+
+
+def all_to_all_v(x, out_splits, in_splits, group):
+    return _AllToAllV.apply(x, out_splits, in_splits, group)
+
+
+class TopKGate(nn.Module):
+    def __init__(self, hidden: int, num_experts: int, top_k: int = 2, z_loss_coef: float = 1e-3,
+                 aux_loss_coef: float = 1e-2, norm_topk: bool = True, dtype=None, device=None):
+        super().__init__()
+        self.num_experts, self.top_k = num_experts, top_k
+        self.z_loss_coef, self.aux_loss_coef = z_loss_coef, aux_loss_coef
+        self.norm_topk = norm_topk
+        self.wg = nn.Linear(hidden, num_experts, bias=False, dtype=dtype, device=device)
+
+    def forward(self, x):
+        logits = self.wg(x).float()
+        probs = logits.softmax(-1)
+        w, idx = probs.topk(self.top_k, dim=-1)
+        if self.norm_topk:
+            w = w / w.sum(-1, keepdim=True)
+        # Switch/GShard load balance: E * sum_e f_e * p_e
+        frac = torch.zeros(self.num_experts, device=x.device, dtype=torch.float32)
+        frac.scatter_add_(0, idx.reshape(-1), torch.ones(idx.numel(), device=x.device))
+        frac = frac / idx.numel()
+        aux = self.num_experts * (frac * probs.mean(0)).sum() * self.aux_loss_coef
+        z = torch.logsumexp(logits, -1).square().mean() * self.z_loss_coef
+        return w, idx, aux + z
+
+
+def grouped_mlp(x: torch.Tensor, counts: List[int], w1: torch.Tensor, w2: torch.Tensor,
+                w3: Optional[torch.Tensor] = None, activation: str = "silu") -> torch.Tensor:
+    """Expert FFN over contiguous groups: rows [off_e, off_e + counts[e]) go
+    through expert e.  w1/w3 [E, F, H] (w3: SwiGLU gate), w2 [E, H, F]."""
+    outs = []
+    off = 0
+    act = F.silu if activation == "silu" else F.gelu
+    for e, n in enumerate(counts):
+        if n == 0:
+            continue
+        xe = x[off:off + n]
+        h = F.linear(xe, w1[e])
+        h = act(h) * F.linear(xe, w3[e]) if w3 is not None else act(h)
+        outs.append(F.linear(h, w2[e]))
+        off += n
+    if not outs:
+        return x.new_zeros((0, w2.shape[1])) + 0 * (w1.sum() + w2.sum() + (w3.sum() if w3 is not None else 0))
+    return torch.cat(outs, 0)
+
+
+class Experts(nn.Module):
+    def __init__(self, num_local_experts: int, hidden: int, ffn: int, swiglu: bool = True, dtype=None, device=None):
+        super().__init__()
+        self.num_local_experts = num_local_experts
+        self.w1 = nn.Parameter(torch.empty(num_local_experts, ffn, hidden, dtype=dtype, device=device))
+        self.w2 = nn.Parameter(torch.empty(num_local_experts, hidden, ffn, dtype=dtype, device=device))
+        self.w3 = nn.Parameter(torch.empty(num_local_experts, ffn, hidden, dtype=dtype, device=device)) \
+            if swiglu else None
+        for p in (self.w1, self.w2, self.w3):
+            if p is not None:
+                nn.init.normal_(p, std=1.0 / math.sqrt(p.shape[-1]))
+                p.expert_parallel = True  # grads reduced over the expert-data-parallel group only
+
+    def forward(self, x, counts: List[int]):
+        return grouped_mlp(x, counts, self.w1, self.w2, self.w3, "silu" if self.w3 is not None else "gelu")
+
+
+class MoELayer(nn.Module):
+    """``num_experts`` global experts split evenly over ``ep_group``."""
+
+    def __init__(self, hidden: int, ffn: int, num_experts: int, top_k: int = 2, ep_group=None,
+                 swiglu: bool = True, dtype=None, device=None, aux_loss_coef: float = 1e-2):
+        super().__init__()
+        self.ep_group = ep_group
+        self.ep = _ws(ep_group)
+        assert num_experts % self.ep == 0, f"{num_experts} experts not divisible by EP {self.ep}"
+        self.num_experts, self.top_k = num_experts, top_k
+        self.num_local = num_experts // self.ep
+        self.gate = TopKGate(hidden, num_experts, top_k, aux_loss_coef=aux_loss_coef, dtype=dtype, device=device)
+        self.experts = Experts(self.num_local, hidden, ffn, swiglu, dtype=dtype, device=device)
+        self.aux_loss = torch.zeros(())
+
+    def forward(self, x):
+        shape = x.shape
+        x = x.reshape(-1, shape[-1])
+        T, k, E = x.shape[0], self.top_k, self.num_experts
+        w, idx, self.aux_loss = self.gate(x)
+        flat = idx.reshape(-1)
+        order = torch.argsort(flat, stable=True)
+        counts = torch.bincount(flat, minlength=E)
+        xs = x.index_select(0, order // k)
+        if self.ep > 1:
+            send_counts = counts.view(self.ep, self.num_local)  # [dst rank, local expert]
+            recv_counts = torch.empty_like(send_counts)
+            dist.all_to_all_single(recv_counts, send_counts.contiguous(), group=self.ep_group)
+            send_c = send_counts.tolist()
+            recv_c = recv_counts.tolist()  # [src rank, local expert]
+            in_splits = [sum(r) for r in send_c]
+            out_splits = [sum(r) for r in recv_c]
+            xr = all_to_all_v(xs, out_splits, in_splits, self.ep_group)
+            # received rows are (src rank, expert)-ordered: regroup by local expert
+            seg, off = [], 0
+            for src in range(self.ep):
+                for e in range(self.num_local):
+                    seg.append((e, src, off, recv_c[src][e]))
+                    off += recv_c[src][e]
+            perm = [torch.arange(o, o + n, device=x.device) for e, src, o, n in sorted(seg)]
+            perm = torch.cat(perm) if perm else torch.zeros(0, dtype=torch.long, device=x.device)
+            local_counts = [sum(recv_c[s][e] for s in range(self.ep)) for e in range(self.num_local)]
+            y = self.experts(xr.index_select(0, perm), local_counts)
+            inv = torch.empty_like(perm)
+            inv[perm] = torch.arange(perm.numel(), device=x.device)
+            y = all_to_all_v(y.index_select(0, inv), in_splits, out_splits, self.ep_group)
+        else:
+            y = self.experts(xs, counts.tolist())
+        # un-permute and combine the k expert outputs per token
+        out = torch.zeros(T * k, y.shape[-1], dtype=y.dtype, device=y.device)
+        out = out.index_copy(0, order, y)
+        out = (out.view(T, k, -1) * w.to(y.dtype).unsqueeze(-1)).sum(1)
+        return out.view(shape[:-1] + (out.shape[-1],))
+
+
+def moe_aux_loss(model: nn.Module) -> torch.Tensor:
+    losses = [m.aux_loss for m in model.modules() if isinstance(m, MoELayer)]
+    return sum(losses) if losses else torch.zeros(())
