@@ -1,0 +1,140 @@
+"""auto_accelerate strategies on CPU: single process (module_replace, amp,
+checkpoint, planner) and 2 ranks (ddp, fsdp, zero1, tensor_parallel)
+(parity: ATorch tests/auto/test_auto_accelerate.py)."""
+
+import os
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+import torch.nn as nn
+import torch.nn.functional as F
+
+from conftest import free_port
+
+
+class Block(nn.Module):
+    def __init__(self, h=32, heads=4):
+        super().__init__()
+        self.num_heads = heads
+        self.norm = nn.LayerNorm(h)
+        self.q_proj, self.k_proj, self.v_proj = nn.Linear(h, h), nn.Linear(h, h), nn.Linear(h, h)
+        self.o_proj = nn.Linear(h, h)
+        self.up_proj, self.down_proj = nn.Linear(h, 4 * h), nn.Linear(4 * h, h)
+
+    def forward(self, x):
+        B, S, H = x.shape
+        y = self.norm(x)
+        q, k, v = (p(y).view(B, S, self.num_heads, -1).transpose(1, 2) for p in (self.q_proj, self.k_proj, self.v_proj))
+        a = F.scaled_dot_product_attention(q, k, v, is_causal=True).transpose(1, 2).reshape(B, S, -1)
+        x = x + self.o_proj(a)
+        return x + self.down_proj(F.gelu(self.up_proj(x)))
+
+
+class Toy(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.emb = nn.Embedding(64, 32)
+        self.layers = nn.ModuleList([Block(), Block()])
+        self.head = nn.Linear(32, 64)
+
+    def forward(self, ids):
+        x = self.emb(ids)
+        for b in self.layers:
+            x = b(x)
+        return self.head(x)
+
+
+class DS(torch.utils.data.Dataset):
+    def __len__(self):
+        return 32
+
+    def __getitem__(self, i):
+        g = torch.Generator().manual_seed(i)
+        ids = torch.randint(0, 64, (9,), generator=g)
+        return {"ids": ids[:-1], "labels": ids[1:]}
+
+
+def loss_func(batch, out):
+    return F.cross_entropy(out.reshape(-1, 64).float(), batch["labels"].reshape(-1))
+
+
+def _train(result, steps=4):
+    import itertools
+
+    losses = []
+    it = itertools.cycle(result.dataloader)
+    for _ in range(steps):
+        b = result.prepare_input(next(it), result.args["device"])
+        loss = result.loss_func(b, result.model(b["ids"]))
+        result.optim.zero_grad()
+        loss.backward()
+        result.optim.step()
+        losses.append(float(loss.detach()))
+    return losses
+
+
+def test_single_process_strategies():
+    from dlrover_wuqiong_amd.atorch.auto_accelerate import auto_accelerate
+    from dlrover_wuqiong_amd.ops.norm import LayerNorm
+
+    torch.manual_seed(0)
+    ok, res, strat = auto_accelerate(
+        Toy(), torch.optim.AdamW, dataset=DS(), loss_func=loss_func, optim_args={"lr": 1e-2},
+        dataloader_args={"batch_size": 8},
+        load_strategy=["module_replace", ("amp_native", {"dtype": torch.bfloat16}), "checkpoint"])
+    assert ok and strat.names() == ["module_replace", "amp_native", "checkpoint"]
+    assert any(isinstance(m, LayerNorm) for m in res.model.modules())
+    losses = _train(res, 6)
+    assert losses[-1] < losses[0]
+    # semi-automatic planner
+    ok, res2, strat2 = auto_accelerate(Toy(), torch.optim.SGD, optim_args={"lr": 0.1})
+    assert "amp_native" in strat2.names() and res2.optim is not None
+
+
+def _worker(rank, world, port, strategy, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    try:
+        from dlrover_wuqiong_amd.atorch import distributed as adist
+        from dlrover_wuqiong_amd.atorch.auto_accelerate import auto_accelerate
+
+        adist.init_distributed("gloo")
+        torch.manual_seed(0)
+        ok, res, strat = auto_accelerate(Toy(), torch.optim.AdamW, dataset=DS(), loss_func=loss_func,
+                                         optim_args={"lr": 1e-2}, dataloader_args={"batch_size": 8},
+                                         load_strategy=strategy)
+        losses = _train(res, 5)
+        good = ok and losses[-1] < losses[0] and len(res.dataloader) == 32 // 8
+        q.put((rank, bool(good), strat.names()))
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        traceback.print_exc()
+        q.put((rank, repr(e), None))
+    finally:
+        adist.reset_distributed()
+
+
+def _run(strategy):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, strategy, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in ps), key=lambda x: x[0])
+    for p in ps:
+        p.join(timeout=30)
+    return res
+
+
+def test_two_rank_ddp_fsdp_zero1():
+    for strategy in (["parallel_mode", "ddp"], ["parallel_mode", "fsdp"], ["parallel_mode", "zero1"]):
+        res = _run(strategy)
+        assert [r[1] for r in res] == [True, True], (strategy, res)
+
+
+def test_two_rank_tensor_parallel():
+    res = _run([("parallel_mode", ([("tensor", 2)], None)), "tensor_parallel"])
+    assert [r[1] for r in res] == [True, True], res
