@@ -38,6 +38,12 @@ SIGS = {
     "dw_gelu_bwd": (i32, [vp, vp, vp, i64, vp]),
     "dw_colsum_parts": (i32, [i64]),
     "dw_colsum": (i32, [vp, i64, i32, vp, vp, i32, vp]),
+    # optim_lowbit.hip
+    "dw_qadamw": (i32, [vp, vp, vp, vp, vp, vp, i64, i64, i32, i32, i32, f32, f32, f32, f32, f32, f32, f32, f32,
+                        vp]),
+    # colred.hip
+    "dw_colsum_acc": (i32, [vp, i64, i32, vp, vp, i32, i32, vp]),
+    "dw_norm_bwd2": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp]),
     "dw_swiglu_fwd": (i32, [vp, vp, i64, i32, vp]),
     "dw_swiglu_bwd": (i32, [vp, vp, vp, i64, i32, vp]),
     "dw_rope": (i32, [vp, vp, vp, vp, i64, i32, i32, i32, i32, vp, vp]),
@@ -52,6 +58,9 @@ OPTIONAL = {
     "dw_attn_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32,
                           i32, f32, i32, vp]),
     "dw_attn_bwd_workspace": (i64, [i32, i32, i32, i32]),
+    "dw_attn_fwd_strided": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, f32, i32, vp]),
+    "dw_attn_bwd_strided": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, f32,
+                                  i32, vp]),
 }
 
 

@@ -47,34 +47,42 @@ __device__ __forceinline__ u32x4 tr_pair(const char* base, int off0, int off1) {
   return v;
 }
 
-// delta[b,h,q] = sum_d dO*O ; also zero dq_acc rows handled by memset
+// delta[b,h,q] = sum_d dO*O.  D/8 lanes per (b, s, h) row (16-byte loads),
+// 64/(D/8) rows per wave; rows are (b, s, h) in BSHD order.
 template <int D>
 __global__ void __launch_bounds__(256) attn_bwd_pre_kernel(const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
-                                                           float* __restrict__ delta, int B, int S, int H) {
-  const int64_t row = blockIdx.x * 4 + (threadIdx.x >> 6);  // (b, s, h) row
+                                                           float* __restrict__ delta, int B, int S, int H,
+                                                           AttnStrides st) {
+  constexpr int LPR = D / 8;            // lanes per row
+  constexpr int RPW = 64 / LPR;         // rows per wave
   const int lane = threadIdx.x & 63;
-  if (row >= (int64_t)B * S * H) return;
-  const int h = (int)(row % H);
-  const int64_t bs = row / H;
-  const int s = (int)(bs % S), b = (int)(bs / S);
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  const int c = lane % LPR;
+  const bool ok = row < (int64_t)B * S * H;
   float acc = 0.f;
-  for (int c = lane; c < D / 8; c += 64) {
+  int h = 0, s = 0, b = 0;
+  if (ok) {
+    h = (int)(row % H);
+    const int64_t bs = row / H;
+    s = (int)(bs % S);
+    b = (int)(bs / S);
     float a[8], d[8];
-    unpack8(*(const u32x4*)(O + row * D + c * 8), a);
-    unpack8(*(const u32x4*)(dO + row * D + c * 8), d);
+    unpack8(*(const u32x4*)(O + (int64_t)b * st.o_bs + (int64_t)s * st.o_rs + h * D + c * 8), a);
+    unpack8(*(const u32x4*)(dO + (int64_t)b * st.do_bs + (int64_t)s * st.do_rs + h * D + c * 8), d);
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc += a[k] * d[k];
   }
-  acc = wave_sum(acc);
-  if (lane == 0) delta[((int64_t)b * H + h) * S + s] = acc;
+#pragma unroll
+  for (int off = LPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if (ok && c == 0) delta[((int64_t)b * H + h) * S + s] = acc;
 }
 
 template <int D, bool CAUSAL>
-__global__ void __launch_bounds__(256, 1)
+__global__ void __launch_bounds__(256, (D <= 64 ? 2 : 1))  // D=64: keep 2 waves/SIMD (<= 256 VGPR+AGPR)
 attn_bwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
                 const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
                 float* __restrict__ dQacc, bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int S, int H, int HKV,
-                float scale, float scale_log2) {
+                float scale, float scale_log2, AttnStrides st) {
   constexpr int KS = D / 32;   // k-steps over d
   constexpr int DT = D / 16;   // d tiles
   constexpr int NCH = D / 8;
@@ -90,19 +98,20 @@ attn_bwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int b = blockIdx.z, hk = blockIdx.y;
-  const int kb0 = blockIdx.x * BKB;
+  // causal: the key blocks with the most queries (the first ones) go first
+  const int kb0 = blockIdx.x * BKB;  // causal: the first key blocks (most queries) dispatch first
   const int kw0 = kb0 + 32 * wid;  // this wave's first key
   const int group = H / HKV;
-  const int64_t q_rs = (int64_t)H * D, kv_rs = (int64_t)HKV * D;
-  const bf16_t* Kb = K + (int64_t)b * S * kv_rs + (int64_t)hk * D;
-  const bf16_t* Vb = V + (int64_t)b * S * kv_rs + (int64_t)hk * D;
+  const int64_t q_acc_rs = (int64_t)H * D;  // fp32 dQ workspace is contiguous BSHD
+  const bf16_t* Kb = K + (int64_t)b * st.k_bs + (int64_t)hk * D;
+  const bf16_t* Vb = V + (int64_t)b * st.v_bs + (int64_t)hk * D;
 
   // K block -> LDS (for the dQ transpose reads); K,V fragments -> registers
   for (int v = tid; v < BKB * NCH; v += 256) {
     const int r = v / NCH, c = v % NCH;
     const int key = kb0 + r;
     u32x4 x = (u32x4){0, 0, 0, 0};
-    if (key < S) x = *(const u32x4*)(Kb + (int64_t)key * kv_rs + c * 8);
+    if (key < S) x = *(const u32x4*)(Kb + (int64_t)key * st.k_rs + c * 8);
     *(u32x4*)(k_lds + swzb<D>(r, c)) = x;
   }
   u32x4 kf[2][KS], vf[2][KS];  // B operand frags: [key = li][d = 32kk + 8g..]
@@ -112,8 +121,8 @@ attn_bwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) {
       if (key < S) {
-        kf[kt][kk] = *(const u32x4*)(Kb + (int64_t)key * kv_rs + 32 * kk + 8 * g);
-        vf[kt][kk] = *(const u32x4*)(Vb + (int64_t)key * kv_rs + 32 * kk + 8 * g);
+        kf[kt][kk] = *(const u32x4*)(Kb + (int64_t)key * st.k_rs + 32 * kk + 8 * g);
+        vf[kt][kk] = *(const u32x4*)(Vb + (int64_t)key * st.v_rs + 32 * kk + 8 * g);
       } else {
         kf[kt][kk] = (u32x4){0, 0, 0, 0};
         vf[kt][kk] = (u32x4){0, 0, 0, 0};
@@ -132,11 +141,11 @@ attn_bwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   const int q_start = CAUSAL ? (kb0 / QI) * QI : 0;
   for (int hh = 0; hh < group; ++hh) {
     const int h = hk * group + hh;
-    const bf16_t* Qb = Q + (int64_t)b * S * q_rs + (int64_t)h * D;
-    const bf16_t* dOb = dO + (int64_t)b * S * q_rs + (int64_t)h * D;
+    const bf16_t* Qb = Q + (int64_t)b * st.q_bs + (int64_t)h * D;
+    const bf16_t* dOb = dO + (int64_t)b * st.do_bs + (int64_t)h * D;
     const float* lse_b = LSE + ((int64_t)b * H + h) * S;
     const float* del_b = DELTA + ((int64_t)b * H + h) * S;
-    float* dQb = dQacc + (int64_t)b * S * q_rs + (int64_t)h * D;
+    float* dQb = dQacc + (int64_t)b * S * q_acc_rs + (int64_t)h * D;
 
     for (int qb = q_start; qb < S; qb += QI) {
       __syncthreads();  // previous iteration's LDS reads done
@@ -145,8 +154,8 @@ attn_bwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
         const int q = qb + r;
         u32x4 x = (u32x4){0, 0, 0, 0}, y = (u32x4){0, 0, 0, 0};
         if (q < S) {
-          x = *(const u32x4*)(Qb + (int64_t)q * q_rs + c * 8);
-          y = *(const u32x4*)(dOb + (int64_t)q * q_rs + c * 8);
+          x = *(const u32x4*)(Qb + (int64_t)q * st.q_rs + c * 8);
+          y = *(const u32x4*)(dOb + (int64_t)q * st.do_rs + c * 8);
         }
         *(u32x4*)(q_lds + swzb<D>(r, c)) = x;
         *(u32x4*)(do_lds + swzb<D>(r, c)) = y;
@@ -268,14 +277,14 @@ attn_bwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int q = qb + 16 * qt + 4 * g + r;
-            if (q < S) atomicAdd(dQb + (int64_t)q * q_rs + 16 * (dt0 + i) + li, acc[i][r]);
+            if (q < S) atomicAdd(dQb + (int64_t)q * q_acc_rs + 16 * (dt0 + i) + li, acc[i][r]);
           }
       }
     }
   }
   // write dK, dV: lane holds [d = 16dt + 4g + r][key = kw0 + 16kt + li]
-  bf16_t* dKb = dK + (int64_t)b * S * kv_rs + (int64_t)hk * D;
-  bf16_t* dVb = dV + (int64_t)b * S * kv_rs + (int64_t)hk * D;
+  bf16_t* dKb = dK + (int64_t)b * st.dk_bs + (int64_t)hk * D;
+  bf16_t* dVb = dV + (int64_t)b * st.dv_bs + (int64_t)hk * D;
 #pragma unroll
   for (int kt = 0; kt < 2; ++kt) {
     const int key = kw0 + 16 * kt + li;
@@ -287,9 +296,24 @@ attn_bwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
       wk.y = pk2(dk[dt][kt][2], dk[dt][kt][3]);
       wv.x = pk2(dv[dt][kt][0], dv[dt][kt][1]);
       wv.y = pk2(dv[dt][kt][2], dv[dt][kt][3]);
-      *(uint2*)(dKb + (int64_t)key * kv_rs + 16 * dt + 4 * g) = wk;
-      *(uint2*)(dVb + (int64_t)key * kv_rs + 16 * dt + 4 * g) = wv;
+      *(uint2*)(dKb + (int64_t)key * st.dk_rs + 16 * dt + 4 * g) = wk;
+      *(uint2*)(dVb + (int64_t)key * st.dv_rs + 16 * dt + 4 * g) = wv;
     }
+  }
+}
+
+// dQ workspace (contiguous fp32 BSHD) -> bf16 dq with its own batch/row strides
+__global__ void dq_to_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t rows, int S, int HD,
+                                  long long bs, long long rs) {
+  const int per_row = HD / 8;
+  const int64_t nv = rows * per_row;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / per_row;  // (b, s)
+    const int c = (int)(i % per_row);
+    const int64_t b = row / S, sq = row % S;
+    const f32x4 a = *(const f32x4*)(x + i * 8), bb = *(const f32x4*)(x + i * 8 + 4);
+    const float f[8] = {a[0], a[1], a[2], a[3], bb[0], bb[1], bb[2], bb[3]};
+    *(u32x4*)(y + b * bs + sq * rs + c * 8) = pack8(f);
   }
 }
 
@@ -312,46 +336,58 @@ static size_t bwd_lds_bytes() {
   return 128 * D * 2 + 2 * 32 * D * 2 + 32 * 128 * 2 + 64 * 4;
 }
 
+template <int D>
+static void launch_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const void* lse,
+                       float* dq_acc, float* delta, void* dk, void* dv, int B, int S, int H, int HKV, int causal,
+                       float softmax_scale, const AttnStrides& st, hipStream_t s) {
+  const int64_t rows = (int64_t)B * S * H;
+  constexpr int RPB = 4 * (64 / (D / 8));  // rows per 256-thread block
+  hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3((unsigned)((rows + RPB - 1) / RPB)), dim3(256), 0, s,
+                     (const bf16_t*)o, (const bf16_t*)dout, delta, B, S, H, st);
+  const float scale_log2 = softmax_scale * 1.4426950408889634f;
+  dim3 grid((S + 127) / 128, HKV, B);
+  const size_t lds = bwd_lds_bytes<D>();
+  if (causal)
+    hipLaunchKernelGGL((attn_bwd_kernel<D, true>), grid, dim3(256), lds, s, (const bf16_t*)q, (const bf16_t*)k,
+                       (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta, dq_acc, (bf16_t*)dk,
+                       (bf16_t*)dv, S, H, HKV, softmax_scale, scale_log2, st);
+  else
+    hipLaunchKernelGGL((attn_bwd_kernel<D, false>), grid, dim3(256), lds, s, (const bf16_t*)q, (const bf16_t*)k,
+                       (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta, dq_acc, (bf16_t*)dk,
+                       (bf16_t*)dv, S, H, HKV, softmax_scale, scale_log2, st);
+}
+
+// strides: int64[16] = q, k, v, o, do, dq, dk, dv  x (batch, row) in elements
+extern "C" int dw_attn_bwd_strided(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                                   const void* lse, void* dq, void* dk, void* dv, void* workspace, int B, int S,
+                                   int H, int HKV, int D, const long long* strides, int causal, float softmax_scale,
+                                   int flags, void* stream) {
+  if (H % HKV != 0 || (D != 64 && D != 128)) return (int)hipErrorInvalidValue;
+  AttnStrides st;
+  long long* f = &st.q_bs;
+  for (int i = 0; i < 16; ++i) f[i] = strides[i];
+  hipStream_t s = (hipStream_t)stream;
+  float* dq_acc = (float*)workspace;
+  float* delta = dq_acc + (int64_t)B * S * H * D;
+  hipError_t e = hipMemsetAsync(dq_acc, 0, (size_t)B * S * H * D * 4, s);
+  if (e != hipSuccess) return (int)e;
+  if (D == 128) launch_bwd<128>(q, k, v, o, dout, lse, dq_acc, delta, dk, dv, B, S, H, HKV, causal, softmax_scale,
+                                st, s);
+  else launch_bwd<64>(q, k, v, o, dout, lse, dq_acc, delta, dk, dv, B, S, H, HKV, causal, softmax_scale, st, s);
+  const int64_t rows = (int64_t)B * S;
+  const int64_t nv = rows * H * D / 8;
+  hipLaunchKernelGGL(dq_to_bf16_kernel, dim3(dw_grid_for(nv, 256, 4096)), dim3(256), 0, s, dq_acc, (bf16_t*)dq,
+                     rows, S, H * D, st.dq_bs, st.dq_rs);
+  DW_LAUNCH_RET;
+}
+
 extern "C" int dw_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
                            const void* lse, void* dq, void* dk, void* dv, void* workspace, void* unused,
                            int B, int S, int H, int HKV, int D, int causal, float softmax_scale, int flags,
                            void* stream) {
-  if (H % HKV != 0 || (D != 64 && D != 128)) return (int)hipErrorInvalidValue;
-  hipStream_t st = (hipStream_t)stream;
-  float* dq_acc = (float*)workspace;
-  float* delta = dq_acc + (int64_t)B * S * H * D;
-  hipError_t e = hipMemsetAsync(dq_acc, 0, (size_t)B * S * H * D * 4, st);
-  if (e != hipSuccess) return (int)e;
-  const int64_t rows = (int64_t)B * S * H;
-  const float scale_log2 = softmax_scale * 1.4426950408889634f;
-  dim3 grid((S + 127) / 128, HKV, B);
-  if (D == 128) {
-    hipLaunchKernelGGL(attn_bwd_pre_kernel<128>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st,
-                       (const bf16_t*)o, (const bf16_t*)dout, delta, B, S, H);
-    const size_t lds = bwd_lds_bytes<128>();
-    if (causal)
-      hipLaunchKernelGGL((attn_bwd_kernel<128, true>), grid, dim3(256), lds, st, (const bf16_t*)q, (const bf16_t*)k,
-                         (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta, dq_acc, (bf16_t*)dk,
-                         (bf16_t*)dv, S, H, HKV, softmax_scale, scale_log2);
-    else
-      hipLaunchKernelGGL((attn_bwd_kernel<128, false>), grid, dim3(256), lds, st, (const bf16_t*)q, (const bf16_t*)k,
-                         (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta, dq_acc, (bf16_t*)dk,
-                         (bf16_t*)dv, S, H, HKV, softmax_scale, scale_log2);
-  } else {
-    hipLaunchKernelGGL(attn_bwd_pre_kernel<64>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st,
-                       (const bf16_t*)o, (const bf16_t*)dout, delta, B, S, H);
-    const size_t lds = bwd_lds_bytes<64>();
-    if (causal)
-      hipLaunchKernelGGL((attn_bwd_kernel<64, true>), grid, dim3(256), lds, st, (const bf16_t*)q, (const bf16_t*)k,
-                         (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta, dq_acc, (bf16_t*)dk,
-                         (bf16_t*)dv, S, H, HKV, softmax_scale, scale_log2);
-    else
-      hipLaunchKernelGGL((attn_bwd_kernel<64, false>), grid, dim3(256), lds, st, (const bf16_t*)q, (const bf16_t*)k,
-                         (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta, dq_acc, (bf16_t*)dk,
-                         (bf16_t*)dv, S, H, HKV, softmax_scale, scale_log2);
-  }
-  const int64_t n = (int64_t)B * S * H * D;
-  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(dw_grid_for(n / 8, 256, 4096)), dim3(256), 0, st, dq_acc,
-                     (bf16_t*)dq, n);
-  DW_LAUNCH_RET;
+  const long long qs = (long long)S * H * D, qr = (long long)H * D, ks = (long long)S * HKV * D,
+                  kr = (long long)HKV * D;
+  const long long st[16] = {qs, qr, ks, kr, ks, kr, qs, qr, qs, qr, qs, qr, ks, kr, ks, kr};
+  return dw_attn_bwd_strided(q, k, v, o, dout, lse, dq, dk, dv, workspace, B, S, H, HKV, D, st, causal,
+                             softmax_scale, flags, stream);
 }

@@ -55,7 +55,8 @@ __device__ __forceinline__ unsigned int pack2(float a, float b) {
 template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(256, (D <= 64 ? 2 : 1))
 attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
-                bf16_t* __restrict__ O, float* __restrict__ LSE, int S, int H, int HKV, float scale_log2) {
+                bf16_t* __restrict__ O, float* __restrict__ LSE, int S, int H, int HKV, float scale_log2,
+                AttnStrides st) {
   using C = AttnCfg<D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* k_lds = smem;
@@ -65,12 +66,15 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   const int g = lane >> 4, li = lane & 15;
   const int b = blockIdx.z, h = blockIdx.y;
   const int hk = h / (H / HKV);
-  const int q_blk0 = blockIdx.x * C::BQ;
+  // causal: the longest (last) query blocks are dispatched first so the
+  // short ones fill in the tail of the grid
+  const int qblk = CAUSAL ? (int)(gridDim.x - 1 - blockIdx.x) : (int)blockIdx.x;
+  const int q_blk0 = qblk * C::BQ;
   const int q0 = q_blk0 + wid * 32;
-  const int64_t q_rs = (int64_t)H * D, kv_rs = (int64_t)HKV * D;
-  const bf16_t* Qb = Q + (int64_t)b * S * q_rs + (int64_t)h * D;
-  const bf16_t* Kb = K + (int64_t)b * S * kv_rs + (int64_t)hk * D;
-  const bf16_t* Vb = V + (int64_t)b * S * kv_rs + (int64_t)hk * D;
+  const int64_t q_rs = st.q_rs, k_rs = st.k_rs, v_rs = st.v_rs;
+  const bf16_t* Qb = Q + (int64_t)b * st.q_bs + (int64_t)h * D;
+  const bf16_t* Kb = K + (int64_t)b * st.k_bs + (int64_t)hk * D;
+  const bf16_t* Vb = V + (int64_t)b * st.v_bs + (int64_t)hk * D;
 
   // ---- Q fragments (B operand): lane holds Q[q0+16qt+li][32kk + 8g .. +7]
   u32x4 qf[2][C::KSTEPS];
@@ -106,8 +110,8 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
       const int r = v / C::NCH, c = v % C::NCH;
       const int key = t * C::BK + r;
       if (key < S) {
-        kst[i] = *(const u32x4*)(Kb + (int64_t)key * kv_rs + c * 8);
-        vst[i] = *(const u32x4*)(Vb + (int64_t)key * kv_rs + c * 8);
+        kst[i] = *(const u32x4*)(Kb + (int64_t)key * k_rs + c * 8);
+        vst[i] = *(const u32x4*)(Vb + (int64_t)key * v_rs + c * 8);
       } else {
         kst[i] = (u32x4){0, 0, 0, 0};
         vst[i] = (u32x4){0, 0, 0, 0};
@@ -222,7 +226,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   }
 
   // ---- epilogue: O = O^T / l ; lse
-  bf16_t* Ob = O + (int64_t)b * S * q_rs + (int64_t)h * D;
+  bf16_t* Ob = O + (int64_t)b * st.o_bs + (int64_t)h * D;
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int q = q0 + 16 * qt + li;
@@ -234,7 +238,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
       uint2 w;
       w.x = pack2(a[0] * inv, a[1] * inv);
       w.y = pack2(a[2] * inv, a[3] * inv);
-      *(uint2*)(Ob + (int64_t)q * q_rs + 16 * dt + 4 * g) = w;
+      *(uint2*)(Ob + (int64_t)q * st.o_rs + 16 * dt + 4 * g) = w;
     }
     if (g == 0 && LSE) {
       const float lse = (l_i[qt] > 0.f) ? (m_i[qt] + log2f(l_i[qt])) * 0.6931471805599453f : -INFINITY;
@@ -243,30 +247,38 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   }
 }
 
+template <int D>
+static void launch_fwd(const void* q, const void* k, const void* v, void* o, void* lse, int B, int S, int H, int HKV,
+                       int causal, float scale_log2, const AttnStrides& st, hipStream_t s) {
+  dim3 grid((S + AttnCfg<D>::BQ - 1) / AttnCfg<D>::BQ, H, B), block(256);
+  const int lds = 2 * AttnCfg<D>::TILE_BYTES;
+  if (causal)
+    hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
+                       (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st);
+  else
+    hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
+                       (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st);
+}
+
+// strides: int64[8] = q_bs, q_rs, k_bs, k_rs, v_bs, v_rs, o_bs, o_rs (elements)
+extern "C" int dw_attn_fwd_strided(const void* q, const void* k, const void* v, void* o, void* lse, int B, int S,
+                                   int H, int HKV, int D, const long long* strides, int causal, float softmax_scale,
+                                   int flags, void* stream) {
+  if (H % HKV != 0) return (int)hipErrorInvalidValue;
+  AttnStrides st = {};
+  st.q_bs = strides[0]; st.q_rs = strides[1]; st.k_bs = strides[2]; st.k_rs = strides[3];
+  st.v_bs = strides[4]; st.v_rs = strides[5]; st.o_bs = strides[6]; st.o_rs = strides[7];
+  const float scale_log2 = softmax_scale * 1.4426950408889634f;
+  hipStream_t s = (hipStream_t)stream;
+  if (D == 128) launch_fwd<128>(q, k, v, o, lse, B, S, H, HKV, causal, scale_log2, st, s);
+  else if (D == 64) launch_fwd<64>(q, k, v, o, lse, B, S, H, HKV, causal, scale_log2, st, s);
+  else return (int)hipErrorInvalidValue;
+  DW_LAUNCH_RET;
+}
+
 extern "C" int dw_attn_fwd(const void* q, const void* k, const void* v, void* o, void* lse, int B, int S,
                            int H, int HKV, int D, int causal, float softmax_scale, int flags, void* stream) {
-  if (H % HKV != 0) return (int)hipErrorInvalidValue;
-  const float scale_log2 = softmax_scale * 1.4426950408889634f;
-  dim3 grid((S + 127) / 128, H, B), block(256);
-  hipStream_t s = (hipStream_t)stream;
-  if (D == 128) {
-    const int lds = 2 * AttnCfg<128>::TILE_BYTES;
-    if (causal)
-      hipLaunchKernelGGL((attn_fwd_kernel<128, true>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
-                         (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2);
-    else
-      hipLaunchKernelGGL((attn_fwd_kernel<128, false>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
-                         (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2);
-  } else if (D == 64) {
-    const int lds = 2 * AttnCfg<64>::TILE_BYTES;
-    if (causal)
-      hipLaunchKernelGGL((attn_fwd_kernel<64, true>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
-                         (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2);
-    else
-      hipLaunchKernelGGL((attn_fwd_kernel<64, false>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
-                         (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2);
-  } else {
-    return (int)hipErrorInvalidValue;
-  }
-  DW_LAUNCH_RET;
+  const long long st[8] = {(long long)S * H * D, (long long)H * D, (long long)S * HKV * D, (long long)HKV * D,
+                           (long long)S * HKV * D, (long long)HKV * D, (long long)S * H * D, (long long)H * D};
+  return dw_attn_fwd_strided(q, k, v, o, lse, B, S, H, HKV, D, st, causal, softmax_scale, flags, stream);
 }

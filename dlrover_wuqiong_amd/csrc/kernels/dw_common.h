@@ -19,6 +19,14 @@ typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 
+// Element strides (batch, sequence row) of the BSHD attention tensors, so
+// q/k/v can be views into one fused [B, S, 3, H, D] QKV projection output
+// and the gradients can be written straight into the packed dQKV buffer.
+struct AttnStrides {
+  long long q_bs, q_rs, k_bs, k_rs, v_bs, v_rs, o_bs, o_rs;
+  long long do_bs, do_rs, dq_bs, dq_rs, dk_bs, dk_rs, dv_bs, dv_rs;
+};
+
 #define DW_LAUNCH_RET return (int)hipGetLastError()
 
 __device__ __forceinline__ float bf2f(bf16_t u) {

@@ -18,8 +18,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.activation import bias_gelu
-from ..ops.attention import flash_attn_func
+from ..ops.attention import flash_attn_qkvpacked_func
 from ..ops.cross_entropy import cross_entropy
+from ..ops.linear import FusedLinear, linear
 from ..ops.norm import LayerNorm
 
 
@@ -53,25 +54,24 @@ class CausalSelfAttention(nn.Module):
         super().__init__()
         self.n_head = cfg.n_head
         self.head_dim = cfg.n_embd // cfg.n_head
-        self.c_attn = nn.Linear(cfg.n_embd, 3 * cfg.n_embd)
-        self.c_proj = nn.Linear(cfg.n_embd, cfg.n_embd)
+        self.c_attn = FusedLinear(cfg.n_embd, 3 * cfg.n_embd)
+        self.c_proj = FusedLinear(cfg.n_embd, cfg.n_embd)
 
     def forward(self, x):
         B, S, C = x.shape
         qkv = self.c_attn(x).view(B, S, 3, self.n_head, self.head_dim)
-        q, k, v = qkv.unbind(2)
-        y = flash_attn_func(q, k, v, causal=True)
+        y = flash_attn_qkvpacked_func(qkv, causal=True)
         return self.c_proj(y.reshape(B, S, C))
 
 
 class MLP(nn.Module):
     def __init__(self, cfg: GPT2Config):
         super().__init__()
-        self.c_fc = nn.Linear(cfg.n_embd, 4 * cfg.n_embd)
-        self.c_proj = nn.Linear(4 * cfg.n_embd, cfg.n_embd)
+        self.c_fc = FusedLinear(cfg.n_embd, 4 * cfg.n_embd)
+        self.c_proj = FusedLinear(4 * cfg.n_embd, cfg.n_embd)
 
     def forward(self, x):
-        h = F.linear(x, self.c_fc.weight)  # bias fused into the activation kernel
+        h = linear(x, self.c_fc.weight)  # bias fused into the activation kernel
         h = bias_gelu(h, self.c_fc.bias)
         return self.c_proj(h)
 

@@ -1,0 +1,34 @@
+"""Direct gradient accumulation into flat gradient buffers.
+
+Parameters managed by ``parallel.flat.FlatParams`` (with
+``direct_grads=True``) carry ``_dwamd_direct``: their ``.grad`` is a view of
+the flat gradient buffer, zeroed once per step.  The fused ops accumulate
+into it themselves -- weight GEMMs with ``addmm_`` (beta = 1: the hipBLASLt
+epilogue does the add), bias / norm-weight reductions with an accumulating
+finish kernel -- and return ``None`` to autograd.  That removes one
+elementwise ``grad += g`` pass per parameter per micro-batch (hundreds of
+kernels per step) and the temporary ``g``.  ``_dwamd_grad_ready`` (set by
+``FlatDDP``) is then invoked so bucketed all-reduce still starts as soon as
+a bucket's gradients are final.
+"""
+
+from typing import Optional
+
+import torch
+
+
+def direct_grad(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    if p is None or not getattr(p, "_dwamd_direct", False):
+        return None
+    g = p.grad
+    if g is None or not g.is_contiguous():
+        return None
+    return g
+
+
+def notify(p: Optional[torch.Tensor]):
+    if p is None:
+        return
+    cb = getattr(p, "_dwamd_grad_ready", None)
+    if cb is not None:
+        cb(p)

@@ -6,17 +6,22 @@ import torch
 import torch.nn.functional as F
 
 from . import _hip
+from ._grad import direct_grad, notify
 
 
-def _colsum(x2: torch.Tensor, out_dtype) -> torch.Tensor:
+def colsum(x2: torch.Tensor, out_dtype=None, out: torch.Tensor = None, accumulate: bool = False) -> torch.Tensor:
+    """Column sums of a [rows, C] bf16 tensor (bias gradients), fp32 math;
+    ``out`` (+)= result when given (direct flat-gradient accumulation)."""
     R, C = x2.shape
-    L = _hip.lib()
-    P = L.dw_colsum_parts(R)
-    partial = torch.empty(P * C, device=x2.device, dtype=torch.float32)
-    out = torch.empty(C, device=x2.device, dtype=out_dtype)
-    _hip.check(L.dw_colsum(_hip.ptr(x2), R, C, _hip.ptr(partial), _hip.ptr(out),
-                           int(out_dtype == torch.float32), _hip.stream()), "colsum")
+    if out is None:
+        out = torch.empty(C, device=x2.device, dtype=out_dtype or x2.dtype)
+    ws = torch.empty(C, device=x2.device, dtype=torch.float32)
+    _hip.check(_hip.lib().dw_colsum_acc(_hip.ptr(x2), R, C, _hip.ptr(ws), _hip.ptr(out),
+                                        int(out.dtype == torch.float32), int(accumulate), _hip.stream()), "colsum")
     return out
+
+
+_colsum = colsum
 
 
 class _BiasGeluFn(torch.autograd.Function):
@@ -32,6 +37,7 @@ class _BiasGeluFn(torch.autograd.Function):
         ctx.save_for_backward(pre if pre is not None else x)
         ctx.has_bias = bias is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
+        ctx.bias_param = bias
         return y
 
     @staticmethod
@@ -44,7 +50,12 @@ class _BiasGeluFn(torch.autograd.Function):
         db = None
         if ctx.has_bias:
             C = pre.shape[-1]
-            db = _colsum(dx.view(-1, C), ctx.bias_dtype)
+            g = direct_grad(ctx.bias_param)
+            if g is not None:
+                colsum(dx.view(-1, C), out=g, accumulate=True)
+                notify(ctx.bias_param)
+            else:
+                db = colsum(dx.view(-1, C), ctx.bias_dtype)
         return dx, db
 
 

@@ -9,6 +9,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _hip
+from ._grad import direct_grad, notify
 
 
 class _NormFn(torch.autograd.Function):
@@ -26,7 +27,8 @@ class _NormFn(torch.autograd.Function):
                                           _hip.stream()), "norm_fwd")
         ctx.save_for_backward(x2, weight, mean, rstd)
         ctx.rms = rms
-        ctx.has_bias = bias is not None
+        ctx.has_bias = bias is not None and bias.requires_grad
+        ctx.weight_param, ctx.bias_param = weight, (bias if ctx.has_bias else None)
         return y.view(x.shape)
 
     @staticmethod
@@ -38,15 +40,24 @@ class _NormFn(torch.autograd.Function):
         if dy2.dtype != torch.bfloat16:
             dy2 = dy2.to(torch.bfloat16)
         L = _hip.lib()
-        nblk = L.dw_norm_bwd_blocks(R)
-        partial = torch.empty(nblk * 2 * H, device=x2.device, dtype=torch.float32)
+        ws = torch.empty(2 * H, device=x2.device, dtype=torch.float32)
         dx = torch.empty_like(x2)
-        dgamma = torch.empty(H, device=x2.device, dtype=weight.dtype)
-        dbeta = torch.empty(H, device=x2.device, dtype=weight.dtype) if ctx.has_bias else None
-        _hip.check(L.dw_norm_bwd(_hip.ptr(dy2), _hip.ptr(x2), _hip.ptr(weight), _hip.ptr(mean),
-                                 _hip.ptr(rstd), _hip.ptr(dx), _hip.ptr(dgamma), _hip.ptr(dbeta),
-                                 _hip.ptr(partial), R, H, int(ctx.rms),
-                                 int(weight.dtype == torch.float32), _hip.stream()), "norm_bwd")
+        wp, bp = ctx.weight_param, ctx.bias_param
+        gd, bd = direct_grad(wp), direct_grad(bp) if ctx.has_bias else None
+        direct = gd is not None and (not ctx.has_bias or bd is not None)
+        if direct:
+            dgamma, dbeta = gd, bd
+        else:
+            dgamma = torch.empty(H, device=x2.device, dtype=weight.dtype)
+            dbeta = torch.empty(H, device=x2.device, dtype=weight.dtype) if ctx.has_bias else None
+        _hip.check(L.dw_norm_bwd2(_hip.ptr(dy2), _hip.ptr(x2), _hip.ptr(weight), _hip.ptr(mean),
+                                  _hip.ptr(rstd), _hip.ptr(dx), _hip.ptr(dgamma), _hip.ptr(dbeta),
+                                  _hip.ptr(ws), R, H, int(ctx.rms), int(dgamma.dtype == torch.float32),
+                                  int(direct), _hip.stream()), "norm_bwd")
+        if direct:
+            notify(wp)
+            notify(bp)
+            return dx.view(dy.shape), None, None, None, None
         return dx.view(dy.shape), dgamma, dbeta, None, None
 
 

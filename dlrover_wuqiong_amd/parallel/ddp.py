@@ -50,7 +50,9 @@ class FlatDDP(nn.Module):
             if broadcast_params:
                 dist.broadcast(flat.data, src=self._global_src(), group=process_group)
             for i, p in enumerate(flat.params):
-                p.register_post_accumulate_grad_hook(self._make_hook(i))
+                hook = self._make_hook(i)
+                p.register_post_accumulate_grad_hook(hook)
+                p._dwamd_grad_ready = hook  # fused ops that accumulate directly (ops/_grad.py)
 
     def _global_src(self):
         if self.pg is None:

@@ -34,7 +34,11 @@ def default_no_decay(name: str, p: torch.Tensor) -> bool:
 class FlatParams:
     def __init__(self, module: nn.Module, dtype: Optional[torch.dtype] = None, device=None,
                  no_decay_fn: Callable[[str, torch.Tensor], bool] = default_no_decay,
-                 grad_dtype: Optional[torch.dtype] = None):
+                 grad_dtype: Optional[torch.dtype] = None, direct_grads: bool = True):
+        """``direct_grads``: the fused ops (``ops/linear.py``, norms, bias
+        activations) accumulate straight into the flat ``.grad`` views
+        (``ops/_grad.py``); call ``zero_grad()`` (not ``set_to_none``) once
+        per optimizer step."""
         named = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
         # tied weights appear once in named_parameters (dedup by identity)
         named.reverse()
@@ -62,6 +66,7 @@ class FlatParams:
                 view.copy_(p.data.to(self.device, self.dtype))
             p.data = view
             p.grad = self.grad[o:o + c].view_as(p)
+            p._dwamd_direct = bool(direct_grads)
             if no_decay_fn(n, p):
                 mask[o // ALIGN:(o + c + ALIGN - 1) // ALIGN] = 0
         self.decay_mask = mask.to(self.device)

@@ -138,6 +138,26 @@ def test_flash_attention(D, causal, S, H, HKV):
     assert _rel(v.grad, vf.grad) < 3e-2
 
 
+@pytest.mark.parametrize("D,causal,S", [(64, True, 1024), (64, False, 200), (128, True, 384)])
+def test_flash_attention_qkvpacked(D, causal, S):
+    """Packed [B, S, 3, H, D] path: strided q/k/v reads, packed dQKV writes."""
+    from dlrover_wuqiong_amd.ops.attention import attention_reference, flash_attn_qkvpacked_func
+
+    torch.manual_seed(2)
+    B, H = 2, 5
+    lin = torch.randn(B, S, 3 * H * D + 8, device=DEV, dtype=torch.bfloat16)
+    qkv = lin[..., : 3 * H * D].view(B, S, 3, H, D).detach().requires_grad_()  # non-dense batch/row strides
+    o = flash_attn_qkvpacked_func(qkv, causal=causal)
+    qf = qkv.detach().float().requires_grad_()
+    orf = attention_reference(qf[:, :, 0], qf[:, :, 1], qf[:, :, 2], causal=causal)
+    assert _rel(o, orf) < 2e-2
+    do = torch.randn_like(o)
+    o.backward(do)
+    orf.backward(do.float())
+    for i in range(3):
+        assert _rel(qkv.grad[:, :, i], qf.grad[:, :, i]) < 3e-2, i
+
+
 @pytest.mark.parametrize("n", [1000, 1 << 20, (1 << 20) + 13])
 def test_fused_adamw_matches_torch(n):
     from dlrover_wuqiong_amd.optimizers.fused import FusedAdamW
@@ -227,3 +247,68 @@ def test_gpt2_tiny_trains():
         first = first if first is not None else loss.item()
         last = loss.item()
     assert last < first - 1.0
+
+
+def test_direct_flat_grads_match_autograd():
+    """Fused ops accumulating straight into the flat grad buffer (addmm_ /
+    colsum / norm finish kernels) == the autograd accumulation path."""
+    from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
+    from dlrover_wuqiong_amd.parallel.flat import FlatParams
+
+    grads = []
+    for direct in (True, False):
+        torch.manual_seed(0)
+        cfg = GPT2Config.named("gpt2-tiny")
+        with torch.device(DEV):
+            m = GPT2(cfg)
+        m.to(torch.bfloat16)
+        flat = FlatParams(m, direct_grads=direct)
+        x = torch.randint(0, cfg.vocab_size, (2, 65), device=DEV)
+        for _ in range(2):  # two micro-batches: accumulation
+            m(x[:, :-1], x[:, 1:]).backward()
+        grads.append(flat.grad.float().clone())
+    assert _rel(grads[0], grads[1]) < 1e-2
+
+
+def test_colsum_accumulate():
+    from dlrover_wuqiong_amd.ops.activation import colsum
+
+    x = torch.randn(4096, 1600, device=DEV, dtype=torch.bfloat16)
+    out = torch.ones(1600, device=DEV, dtype=torch.bfloat16)
+    colsum(x, out=out, accumulate=True)
+    ref = x.float().sum(0) + 1
+    assert _rel(out, ref) < 1e-2
+    assert _rel(colsum(x, torch.float32), x.float().sum(0)) < 1e-4
+
+
+@pytest.mark.parametrize("bits", [4, 8])
+def test_low_bit_adamw_kernel_matches_reference(bits):
+    """Fused 4/8-bit-state AdamW kernel == the PyTorch reference codec."""
+    from dlrover_wuqiong_amd.optimizers.low_bit import Q_AdamW, dequant_m, _unpack4
+
+    torch.manual_seed(0)
+    n = 128 * 40 + 77
+    p_gpu = torch.randn(n, device=DEV).to(torch.bfloat16).requires_grad_()
+    p_ref = p_gpu.detach().clone().requires_grad_()
+    og = Q_AdamW([p_gpu], lr=1e-2, q_bits=bits, threshold=1)
+    orf = Q_AdamW([p_ref], lr=1e-2, q_bits=bits, threshold=1)
+    for it in range(3):
+        g = torch.randn(n, device=DEV).to(torch.bfloat16)
+        p_gpu.grad = g.clone()
+        p_ref.grad = g.clone()
+        og.step()
+        st = orf.state.get(p_ref) or None
+        if st is None:
+            orf._init_state(p_ref, orf.param_groups[0])
+            orf.state[p_ref]["step"] = 0
+        orf.state[p_ref]["step"] += 1
+        t = orf.state[p_ref]["step"]
+        b1, b2 = orf.param_groups[0]["betas"]
+        with torch.no_grad():
+            orf._ref_step(p_ref, orf.state[p_ref], orf.param_groups[0], 1 - b1 ** t, 1 - b2 ** t)
+    assert _rel(p_gpu, p_ref) < 2e-3
+    sg, sr = og.state[p_gpu], orf.state[p_ref]
+    G = sg["ms"].numel()
+    mg = dequant_m((_unpack4(sg["mq"]) if bits == 4 else sg["mq"]).view(G, 128), sg["ms"], bits)
+    mr = dequant_m((_unpack4(sr["mq"]) if bits == 4 else sr["mq"]).view(G, 128), sr["ms"], bits)
+    assert _rel(mg, mr) < 2e-2

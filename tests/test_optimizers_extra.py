@@ -1,0 +1,96 @@
+"""WSAM and low-bit (4/8-bit state) AdamW on CPU (reference paths);
+GPU kernel parity lives in test_ops_gpu.py."""
+
+import torch
+
+
+def _problem(seed=0):
+    torch.manual_seed(seed)
+    model = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.Tanh(), torch.nn.Linear(64, 1))
+    x = torch.randn(256, 32)
+    y = (x[:, :4].sum(1, keepdim=True)).tanh()
+    return model, x, y
+
+
+def test_wsam_reduces_loss_and_matches_sam_when_gamma_half():
+    from dlrover_wuqiong_amd.optimizers.wsam import WeightedSAM
+
+    model, x, y = _problem()
+    base = torch.optim.SGD(model.parameters(), lr=0.1)
+    opt = WeightedSAM(model, base, rho=0.05, gamma=0.9)
+
+    def closure():
+        opt.zero_grad()
+        loss = torch.nn.functional.mse_loss(model(x), y)
+        loss.backward()
+        return loss
+
+    l0 = float(closure())
+    for _ in range(30):
+        opt.step(closure)
+    assert float(closure()) < l0 * 0.7
+    # coupled WSAM with gamma = 0.5 (alpha = 1) is plain SAM: step on g1
+    model, x, y = _problem(1)
+    ref = _problem(1)[0]
+    opt = WeightedSAM(model, torch.optim.SGD(model.parameters(), lr=0.1), rho=0.05, gamma=0.5, decouple=False)
+
+    def cl(m, o):
+        def f():
+            o.zero_grad()
+            loss = torch.nn.functional.mse_loss(m(x), y)
+            loss.backward()
+            return loss
+        return f
+
+    opt.step(cl(model, opt))
+    # manual SAM
+    rsgd = torch.optim.SGD(ref.parameters(), lr=0.1)
+    cl(ref, rsgd)()
+    gn = torch.norm(torch.stack([p.grad.norm() for p in ref.parameters()]))
+    with torch.no_grad():
+        eps = [0.05 * p.grad / (gn + 1e-12) for p in ref.parameters()]
+        for p, e in zip(ref.parameters(), eps):
+            p.add_(e)
+    cl(ref, rsgd)()
+    with torch.no_grad():
+        for p, e in zip(ref.parameters(), eps):
+            p.sub_(e)
+    rsgd.step()
+    for a, b in zip(model.parameters(), ref.parameters()):
+        assert torch.allclose(a, b, atol=1e-6)
+
+
+def test_low_bit_adamw_trains_close_to_adamw():
+    from dlrover_wuqiong_amd.optimizers.low_bit import Q_AdamW
+
+    for bits in (4, 8):
+        model, x, y = _problem()
+        ref_model = _problem()[0]
+        opt = Q_AdamW(model.parameters(), lr=1e-2, weight_decay=0.0, q_bits=bits, threshold=1000)
+        ref = torch.optim.AdamW(ref_model.parameters(), lr=1e-2, weight_decay=0.0)
+        for _ in range(60):
+            for m, o in ((model, opt), (ref_model, ref)):
+                o.zero_grad()
+                torch.nn.functional.mse_loss(m(x), y).backward()
+                o.step()
+        lq = float(torch.nn.functional.mse_loss(model(x), y))
+        lr_ = float(torch.nn.functional.mse_loss(ref_model(x), y))
+        assert lq < 0.05 and lq < 3 * lr_ + 0.01, (bits, lq, lr_)
+        # quantized states: 64x32 weight (2048 elems) -> 1 B/elem (8-bit) or 0.5 B (4-bit) per moment
+        st = opt.state[model[0].weight]
+        assert st["mq"].numel() == (2048 // 2 if bits == 4 else 2048)
+
+
+def test_codec_roundtrip():
+    from dlrover_wuqiong_amd.optimizers.low_bit import dequant_m, dequant_v, quant_m, quant_v
+
+    x = torch.randn(10, 128)
+    for bits in (4, 8):
+        c, s = quant_m(x, bits)
+        xr = dequant_m(c, s, bits)
+        assert (xr - x).abs().max() <= s.max() * (0.13 if bits == 4 else 0.005)
+        v = x.square()
+        cv, sv = quant_v(v, bits)
+        vr = dequant_v(cv, sv, bits)
+        assert (vr > 0).all()  # zero-point free
+        assert ((vr.sqrt() - v.sqrt()).abs() <= sv.sqrt()[:, None] * (1.0 / (16 if bits == 4 else 256))).all()
