@@ -21,6 +21,17 @@ SIGS = {
     "dw_stream_copy": (i32, [vp, vp, u64, i32, vp]),
     "dw_hip_error_string": (cp, [i32]),
     "dw_kernels_abi_version": (i32, []),
+    # xpu_timer.hip
+    "dw_xt_start": (i32, [c.c_double, i32]),
+    "dw_xt_stop": (i32, []),
+    "dw_xt_flush": (i32, [c.c_double]),
+    "dw_xt_key": (i32, [cp]),
+    "dw_xt_begin": (i64, [i32, vp]),
+    "dw_xt_end": (i32, [i64, c.c_double, vp]),
+    "dw_xt_snapshot": (i32, [c.c_char_p, i32]),
+    "dw_xt_hang": (i32, [c.c_char_p, i32, c.POINTER(c.c_double)]),
+    "dw_xt_reset": (None, []),
+    "dw_xt_pending": (i64, []),
     # optim.hip
     "dw_adam_flat": (i32, [vp, i32, vp, vp, i32, vp, vp, vp, i64, i64, f32, f32, f32, f32, f32,
                            f32, f32, i32, vp, vp]),
@@ -43,7 +54,8 @@ SIGS = {
                         vp]),
     # colred.hip
     "dw_colsum_acc": (i32, [vp, i64, i32, vp, vp, i32, i32, vp]),
-    "dw_norm_bwd2": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp]),
+    "dw_norm_bwd2": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp]),
+    "dw_add_norm_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, f32, i32, vp]),
     "dw_swiglu_fwd": (i32, [vp, vp, i64, i32, vp]),
     "dw_swiglu_bwd": (i32, [vp, vp, vp, i64, i32, vp]),
     "dw_rope": (i32, [vp, vp, vp, vp, i64, i32, i32, i32, i32, vp, vp]),

@@ -71,12 +71,17 @@ __global__ void __launch_bounds__(256) colred_kernel(const bf16_t* __restrict__ 
   }
 }
 
-// out[c] (+)= ws[c]; out dtype bf16 (is_fp32=0) or fp32
-__global__ void colred_finish_kernel(const float* __restrict__ ws, void* __restrict__ out, int C, int is_fp32,
+// out[c] (+)= ws[c]; out dtype bf16 (is_fp32=0) or fp32.  The workspace is
+// SELF-CLEANING: every reader zeroes the words it consumed, so ws is all-zero
+// between calls and no per-call hipMemsetAsync (a 5 us fill launch, ~340 per
+// GPT2-1.5B step) is needed.  out == nullptr only clears.
+__global__ void colred_finish_kernel(float* __restrict__ ws, void* __restrict__ out, int C, int is_fp32,
                                      int accumulate) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float v = ws[c];
+  ws[c] = 0.f;
+  if (!out) return;
   if (is_fp32) {
     float* o = (float*)out;
     o[c] = accumulate ? o[c] + v : v;
@@ -86,12 +91,13 @@ __global__ void colred_finish_kernel(const float* __restrict__ ws, void* __restr
   }
 }
 
-// dx = rstd * (dy*g - mean(dy*g) - xhat * mean(dy*g*xhat)); one wave per row
+// dx = rstd * (dy*g - mean(dy*g) - xhat * mean(dy*g*xhat)) [+ dres]; one wave per row
 template <int VPL, bool RMS>
 __global__ void __launch_bounds__(256) norm_dx_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                       const bf16_t* __restrict__ gamma,
                                                       const float* __restrict__ mean_in,
-                                                      const float* __restrict__ rstd_in, bf16_t* __restrict__ dx,
+                                                      const float* __restrict__ rstd_in,
+                                                      const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
                                                       int64_t rows, int H) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -139,6 +145,12 @@ __global__ void __launch_bounds__(256) norm_dx_kernel(const bf16_t* __restrict__
 #pragma unroll
         for (int k = 0; k < 8; ++k) o[k] = rstd * (dv[k] * gm[k] - m1 - (xv[k] - mu) * rstd * m2);
       }
+      if (dres) {  // fused residual-branch gradient (uniform branch)
+        float r[8];
+        unpack8(*(const u32x4*)(dres + row * H + c * 8), r);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] += r[k];
+      }
       *(u32x4*)(dx + row * H + c * 8) = pack8(o);
     }
   }
@@ -154,18 +166,16 @@ static int colred_rows_per_blk(int64_t rows, int C) {
   return (int)(per < 4 ? 4 : per);
 }
 
-// ws: fp32 [C] (zeroed here).  out (+)= column sums of dy [rows, C].
+// ws: fp32 [C], all-zero on entry, left all-zero.  out (+)= column sums of dy [rows, C].
 extern "C" int dw_colsum_acc(const void* dy, int64_t rows, int C, void* ws, void* out, int out_fp32, int accumulate,
                              void* stream) {
   if (C % 8 != 0) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  hipError_t e = hipMemsetAsync(ws, 0, (size_t)C * 4, s);
-  if (e != hipSuccess) return (int)e;
   const int per = colred_rows_per_blk(rows, C);
   dim3 grid((C + 511) / 512, (unsigned)((rows + per - 1) / per));
   hipLaunchKernelGGL(colred_kernel<0>, grid, dim3(256), 0, s, (const bf16_t*)dy, nullptr, nullptr, nullptr,
                      (float*)ws, rows, C, per);
-  hipLaunchKernelGGL(colred_finish_kernel, dim3((C + 255) / 256), dim3(256), 0, s, (const float*)ws, out, C, out_fp32,
+  hipLaunchKernelGGL(colred_finish_kernel, dim3((C + 255) / 256), dim3(256), 0, s, (float*)ws, out, C, out_fp32,
                      accumulate);
   DW_LAUNCH_RET;
 }
@@ -180,24 +190,26 @@ extern "C" int dw_colsum_acc(const void* dy, int64_t rows, int C, void* ws, void
     else { constexpr int VPL = 16; __VA_ARGS__; }     \
   } while (0)
 
-// Norm backward v2.  ws: fp32 [2H] scratch.  dgamma/dbeta (+)= (accumulate flag).
+// Norm backward v2.  ws: fp32 [2H], all-zero on entry, left all-zero.
+// dgamma/dbeta (+)= (accumulate flag).  dres (nullable): gradient of the
+// residual sum that this norm's input also feeds (fused add+norm) -> dx += dres.
 extern "C" int dw_norm_bwd2(const void* dy, const void* x, const void* gamma, const void* mean, const void* rstd,
-                            void* dx, void* dgamma, void* dbeta, void* ws, int64_t rows, int H, int rms,
-                            int out_fp32, int accumulate, void* stream) {
+                            const void* dres, void* dx, void* dgamma, void* dbeta, void* ws, int64_t rows, int H,
+                            int rms, int out_fp32, int accumulate, void* stream) {
   if (H % 8 != 0 || H > 8 * 64 * 16) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   DISPATCH_VPL2(H, {
     if (rms)
       hipLaunchKernelGGL((norm_dx_kernel<VPL, true>), grid, block, 0, s, (const bf16_t*)dy, (const bf16_t*)x,
-                         (const bf16_t*)gamma, nullptr, (const float*)rstd, (bf16_t*)dx, rows, H);
+                         (const bf16_t*)gamma, nullptr, (const float*)rstd, (const bf16_t*)dres, (bf16_t*)dx, rows,
+                         H);
     else
       hipLaunchKernelGGL((norm_dx_kernel<VPL, false>), grid, block, 0, s, (const bf16_t*)dy, (const bf16_t*)x,
-                         (const bf16_t*)gamma, (const float*)mean, (const float*)rstd, (bf16_t*)dx, rows, H);
+                         (const bf16_t*)gamma, (const float*)mean, (const float*)rstd, (const bf16_t*)dres,
+                         (bf16_t*)dx, rows, H);
   });
   if (!dgamma && !dbeta) { DW_LAUNCH_RET; }
-  hipError_t e = hipMemsetAsync(ws, 0, (size_t)2 * H * 4, s);
-  if (e != hipSuccess) return (int)e;
   const int per = colred_rows_per_blk(rows, H);
   dim3 cg((H + 511) / 512, (unsigned)((rows + per - 1) / per));
   if (rms)
@@ -206,11 +218,11 @@ extern "C" int dw_norm_bwd2(const void* dy, const void* x, const void* gamma, co
   else
     hipLaunchKernelGGL(colred_kernel<1>, cg, dim3(256), 0, s, (const bf16_t*)dy, (const bf16_t*)x,
                        (const float*)mean, (const float*)rstd, (float*)ws, rows, H, per);
-  if (dgamma)
-    hipLaunchKernelGGL(colred_finish_kernel, dim3((H + 255) / 256), dim3(256), 0, s, (const float*)ws, dgamma, H,
-                       out_fp32, accumulate);
-  if (dbeta && !rms)
-    hipLaunchKernelGGL(colred_finish_kernel, dim3((H + 255) / 256), dim3(256), 0, s, (const float*)ws + H, dbeta, H,
+  // both halves are consumed (and cleared) even if one output is absent
+  hipLaunchKernelGGL(colred_finish_kernel, dim3((H + 255) / 256), dim3(256), 0, s, (float*)ws, dgamma, H, out_fp32,
+                     accumulate);
+  if (!rms)
+    hipLaunchKernelGGL(colred_finish_kernel, dim3((H + 255) / 256), dim3(256), 0, s, (float*)ws + H, dbeta, H,
                        out_fp32, accumulate);
   DW_LAUNCH_RET;
 }

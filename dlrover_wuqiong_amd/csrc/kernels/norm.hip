@@ -13,11 +13,16 @@
 // fused LayerNorm) and the RMSNorm used by its Llama modules.
 #include "dw_common.h"
 
-template <int VPL, bool RMS>
+// ADD: fused residual add -- h = x + res is formed in registers, rounded to
+// bf16 (exactly what a separate bf16 add would store), written to h_out and
+// normalized; the residual stream is read once instead of three times.
+template <int VPL, bool RMS, bool ADD = false>
 __global__ void __launch_bounds__(256) norm_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ gamma,
                                                        const bf16_t* __restrict__ beta, bf16_t* __restrict__ y,
                                                        float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                       int64_t rows, int H, float eps) {
+                                                       int64_t rows, int H, float eps,
+                                                       const bf16_t* __restrict__ res = nullptr,
+                                                       bf16_t* __restrict__ h_out = nullptr) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -30,6 +35,16 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(const bf16_t* __restrict_
     const int c = lane + 64 * j;
     if (c < nv) {
       unpack8(*(const u32x4*)(xr + c * 8), v[j]);
+      if constexpr (ADD) {
+        float r[8];
+        unpack8(*(const u32x4*)(res + row * H + c * 8), r);
+        u32x4 hv;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] += v[j][k];
+        hv = pack8(r);
+        *(u32x4*)(h_out + row * H + c * 8) = hv;
+        unpack8(hv, v[j]);  // normalize the bf16-rounded sum
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) s += v[j][k];
     } else {
@@ -206,6 +221,26 @@ extern "C" int dw_norm_fwd(const void* x, const void* gamma, const void* beta, v
       hipLaunchKernelGGL((norm_fwd_kernel<VPL, false>), grid, block, 0, s, (const bf16_t*)x,
                          (const bf16_t*)gamma, (const bf16_t*)beta, (bf16_t*)y, (float*)mean,
                          (float*)rstd, rows, H, eps);
+  });
+  DW_LAUNCH_RET;
+}
+
+// y = norm(x + res), h_out = x + res (bf16).  Fused pre-norm residual add.
+extern "C" int dw_add_norm_fwd(const void* x, const void* res, const void* gamma, const void* beta, void* y,
+                               void* h_out, void* mean, void* rstd, int64_t rows, int H, float eps, int rms,
+                               void* stream) {
+  if (H % 8 != 0 || H > 8 * 64 * 16) return (int)hipErrorInvalidValue;
+  dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  hipStream_t s = (hipStream_t)stream;
+  DISPATCH_VPL(H, {
+    if (rms)
+      hipLaunchKernelGGL((norm_fwd_kernel<VPL, true, true>), grid, block, 0, s, (const bf16_t*)x,
+                         (const bf16_t*)gamma, nullptr, (bf16_t*)y, nullptr, (float*)rstd, rows, H, eps,
+                         (const bf16_t*)res, (bf16_t*)h_out);
+    else
+      hipLaunchKernelGGL((norm_fwd_kernel<VPL, false, true>), grid, block, 0, s, (const bf16_t*)x,
+                         (const bf16_t*)gamma, (const bf16_t*)beta, (bf16_t*)y, (float*)mean, (float*)rstd, rows,
+                         H, eps, (const bf16_t*)res, (bf16_t*)h_out);
   });
   DW_LAUNCH_RET;
 }

@@ -24,10 +24,12 @@ Responsibilities (parity: reference
 
 import json
 import os
+import shutil
 import signal
 import socket
 import subprocess
 import sys
+import tempfile
 import threading
 import time
 from dataclasses import dataclass, field
@@ -83,6 +85,9 @@ class ElasticLaunchConfig:
     async_breakpoint_save: bool = True
     # exit (and let the platform relaunch the node) on GPU/driver fault signatures
     exit_on_node_error: bool = field(default_factory=lambda: os.getenv("DWAMD_EXIT_ON_NODE_ERROR", "0") == "1")
+    # > 0: a worker whose heartbeat file (atorch.fault_tolerance.heartbeat) is
+    # older than this is treated as hung and the worker group is relaunched
+    hang_timeout: float = field(default_factory=lambda: float(os.getenv("DWAMD_HANG_TIMEOUT", "0")))
 
     def auto_configure_params(self):
         """nnodes from NODE_NUM, nproc from the visible GPUs, network check
@@ -184,6 +189,10 @@ class ElasticTrainingAgent:
         self._standby: Dict[int, subprocess.Popen] = {}
         self._workers_started_at = 0.0
         self._bp_thread: Optional[threading.Thread] = None
+        # worker <-> agent control files (heartbeats, relaunch requests)
+        self.ctl_dir = os.path.join(tempfile.gettempdir(), "dwamd_ctl",
+                                    f"{config.run_id}_n{config.node_rank}_{os.getpid()}")
+        os.makedirs(self.ctl_dir, exist_ok=True)
 
     # ------------------------------------------------------------ ranks
     @staticmethod
@@ -256,12 +265,53 @@ class ElasticTrainingAgent:
             NodeEnv.NODE_RANK: str(self.config.node_rank),
             NodeEnv.DLROVER_MASTER_ADDR: self.client.master_addr,
             "HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
+            "DWAMD_AGENT_CTL_DIR": self.ctl_dir,
         })
         env.setdefault("OMP_NUM_THREADS", "1")
         return env
 
+    def _clear_ctl(self):
+        for f in os.listdir(self.ctl_dir):
+            try:
+                os.unlink(os.path.join(self.ctl_dir, f))
+            except OSError:
+                pass
+
+    def _ctl_failures(self) -> Dict[int, dict]:
+        """Relaunch requests and stale heartbeats from the control dir."""
+        out = {}
+        now = time.time()
+        try:
+            entries = list(os.scandir(self.ctl_dir))
+        except OSError:
+            return out
+        by_lr = {w.local_rank: w for w in self.workers}
+        for e in entries:
+            kind, _, lr = e.name.partition(".")
+            if not lr.isdigit() or int(lr) not in by_lr:
+                continue
+            w = by_lr[int(lr)]
+            if kind == "relaunch":
+                try:
+                    with open(e.path) as f:
+                        reason = f.read()
+                except OSError:
+                    reason = "relaunch requested"
+                out[w.global_rank] = {"local_rank": w.local_rank, "exitcode": -1, "message": reason,
+                                      "timestamp": int(now)}
+            elif kind == "hb" and self.config.hang_timeout > 0:
+                try:
+                    age = now - e.stat().st_mtime
+                except OSError:
+                    continue
+                if age > self.config.hang_timeout:
+                    out[w.global_rank] = {"local_rank": w.local_rank, "exitcode": -1,
+                                          "message": f"hang: no heartbeat for {age:.0f}s", "timestamp": int(now)}
+        return out
+
     def _start_workers(self):
         ranks, world_size = self._rendezvous()
+        self._clear_ctl()
         self.workers = []
         warm = 0
         for lr, gr in enumerate(ranks):
@@ -364,6 +414,10 @@ class ElasticTrainingAgent:
             return RunResult(RunResult.FAILED, failed)
         if all(c == 0 for _w, c in codes):
             return RunResult(RunResult.SUCCEEDED)
+        hung = self._ctl_failures()
+        if hung:
+            logger.error(f"relaunch requested / hang detected: { {r: f['message'] for r, f in hung.items()} }")
+            return RunResult(RunResult.FAILED, hung)
         return RunResult(RunResult.HEALTHY)
 
     def _failure(self, w: WorkerProcess, code: int) -> dict:
@@ -467,7 +521,11 @@ class ElasticTrainingAgent:
                 self._exit_barrier()
                 self._wait_async_saver()
                 self._cleanup_shm()
-                self.client.report_node_event(NodeStatus.SUCCEEDED, "")
+                try:  # the master may already be going away (its host node finished first)
+                    self.client.report_node_event(NodeStatus.SUCCEEDED, "")
+                    self.client.kv_store_add(f"{self.config.run_id}/exit_done", 1)
+                except Exception as e:
+                    logger.warning(f"final success report not delivered: {e}")
                 return 0
             if res.state == RunResult.FAILED:
                 self.events.append((time.time(), "failed"))
@@ -584,3 +642,19 @@ def launch_agent(config: ElasticLaunchConfig, entrypoint: str, args: List[str], 
         return agent.run()
     finally:
         agent._stop_workers(timeout=5)
+        shutil.rmtree(agent.ctl_dir, ignore_errors=True)
+
+
+def wait_nodes_done(master_addr: str, run_id: str, nnodes: int, timeout: float = 15.0) -> bool:
+    """Used by the launcher that hosts the local master: keep the master up
+    until every node reported its final state (or ``timeout``)."""
+    client = MasterClient(master_addr, node_id=-1)
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        try:
+            if client.kv_store_add(f"{run_id}/exit_done", 0) >= nnodes:
+                return True
+        except Exception:
+            return False
+        time.sleep(0.1)
+    return False

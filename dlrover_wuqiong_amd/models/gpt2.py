@@ -84,10 +84,17 @@ class Block(nn.Module):
         self.ln_2 = LayerNorm(cfg.n_embd, eps=cfg.layer_norm_eps)
         self.mlp = MLP(cfg)
 
-    def forward(self, x):
-        x = x + self.attn(self.ln_1(x))
-        x = x + self.mlp(self.ln_2(x))
-        return x
+    def forward(self, x, r=None):
+        """Pre-norm block on the split residual stream: the stream value is
+        ``x + r`` (``r`` = previous block's MLP output, None for the first
+        block), and every residual add is fused into the following norm.
+        Returns ``(h, r2)`` with the block output = ``h + r2``."""
+        if r is None:
+            a, h = self.ln_1(x), x
+        else:
+            a, h = self.ln_1.add_forward(x, r)
+        b, h = self.ln_2.add_forward(h, self.attn(a))
+        return h, self.mlp(b)
 
 
 class GPT2(nn.Module):
@@ -119,12 +126,13 @@ class GPT2(nn.Module):
         B, S = idx.shape
         pos = torch.arange(S, device=idx.device)
         x = self.wte(idx) + self.wpe(pos)[None]
+        r = None
         for blk in self.h:
             if self.cfg.activation_checkpointing and self.training:
-                x = torch.utils.checkpoint.checkpoint(blk, x, use_reentrant=False)
+                x, r = torch.utils.checkpoint.checkpoint(blk, x, r, use_reentrant=False)
             else:
-                x = blk(x)
-        x = self.ln_f(x)
+                x, r = blk(x, r)
+        x = self.ln_f.add_forward(x, r)[0] if r is not None else self.ln_f(x)
         logits = F.linear(x, self.wte.weight)  # tied LM head
         if targets is None:
             return logits

@@ -161,9 +161,15 @@ class LlamaDecoderLayer(nn.Module):
         else:
             self.mlp = LlamaMLP(cfg, tp_group)
 
-    def forward(self, x, cos, sin):
-        x = x + self.self_attn(self.input_layernorm(x), cos, sin)
-        return x + self.mlp(self.post_attention_layernorm(x))
+    def forward(self, x, cos, sin, r=None):
+        """Split residual stream (value = x + r); the residual adds are fused
+        into the RMSNorms.  Returns (h, mlp_out)."""
+        if r is None:
+            a, h = self.input_layernorm(x), x
+        else:
+            a, h = self.input_layernorm.add_forward(x, r)
+        b, h = self.post_attention_layernorm.add_forward(h, self.self_attn(a, cos, sin))
+        return h, self.mlp(b)
 
 
 class Llama(nn.Module):
@@ -208,12 +214,13 @@ class Llama(nn.Module):
         sp = _ws(self.sp_group)
         x = self.embed_tokens(ids)
         cos, sin = rope_table(S * sp, self.cfg.head_dim, self.cfg.rope_theta, x.device)
+        r = None
         for layer in self.layers:
             if self.cfg.activation_checkpointing and self.training:
-                x = torch.utils.checkpoint.checkpoint(layer, x, cos, sin, use_reentrant=False)
+                x, r = torch.utils.checkpoint.checkpoint(layer, x, cos, sin, r, use_reentrant=False)
             else:
-                x = layer(x, cos, sin)
-        x = self.norm(x)
+                x, r = layer(x, cos, sin, r)
+        x = self.norm.add_forward(x, r)[0] if r is not None else self.norm(x)
         if self.lm_head is None:
             logits = F.linear(x, self.embed_tokens.weight)
         else:

@@ -53,3 +53,19 @@ def require_bf16(*ts):
     for t in ts:
         if t is not None and t.dtype != torch.bfloat16:
             raise HipKernelError(f"HIP kernel expects bf16 tensors, got {t.dtype}")
+
+
+_ZERO_WS = {}
+
+
+def zeroed_workspace(nfloats: int, device) -> torch.Tensor:
+    """fp32 scratch that is all-zero on entry to a kernel and left all-zero by
+    it (the column-reduction kernels clear what they consume).  One buffer per
+    (device, stream): stream order serializes its users, and no per-call
+    memset launch is needed."""
+    key = (torch.device(device).index, torch.cuda.current_stream(device).cuda_stream)
+    buf = _ZERO_WS.get(key)
+    if buf is None or buf.numel() < nfloats:
+        buf = torch.zeros(max(nfloats, 1 << 16), device=device, dtype=torch.float32)
+        _ZERO_WS[key] = buf
+    return buf

@@ -15,7 +15,7 @@ def colsum(x2: torch.Tensor, out_dtype=None, out: torch.Tensor = None, accumulat
     R, C = x2.shape
     if out is None:
         out = torch.empty(C, device=x2.device, dtype=out_dtype or x2.dtype)
-    ws = torch.empty(C, device=x2.device, dtype=torch.float32)
+    ws = _hip.zeroed_workspace(C, x2.device)
     _hip.check(_hip.lib().dw_colsum_acc(_hip.ptr(x2), R, C, _hip.ptr(ws), _hip.ptr(out),
                                         int(out.dtype == torch.float32), int(accumulate), _hip.stream()), "colsum")
     return out

@@ -12,6 +12,48 @@ from . import _hip
 from ._grad import direct_grad, notify
 
 
+def _norm_backward(ctx, dy, dres):
+    """Shared backward of the plain and the fused add+norm functions: dx
+    (+ dres, the residual-stream gradient, fused into the same row pass) and
+    dgamma/dbeta accumulated directly into flat gradient storage if present."""
+    x2, weight, mean, rstd = ctx.saved_tensors
+    H = x2.shape[-1]
+    R = x2.shape[0]
+    dy2 = dy.contiguous().view(-1, H)
+    if dy2.dtype != torch.bfloat16:
+        dy2 = dy2.to(torch.bfloat16)
+    if dres is not None:
+        dres = dres.contiguous().view(-1, H)
+        if dres.dtype != torch.bfloat16:
+            dres = dres.to(torch.bfloat16)
+    ws = _hip.zeroed_workspace(2 * H, x2.device)
+    dx = torch.empty_like(x2)
+    wp, bp = ctx.weight_param, ctx.bias_param
+    gd, bd = direct_grad(wp), direct_grad(bp) if ctx.has_bias else None
+    direct = gd is not None and (not ctx.has_bias or bd is not None)
+    if direct:
+        dgamma, dbeta = gd, bd
+    else:
+        dgamma = torch.empty(H, device=x2.device, dtype=weight.dtype)
+        dbeta = torch.empty(H, device=x2.device, dtype=weight.dtype) if ctx.has_bias else None
+    _hip.check(_hip.lib().dw_norm_bwd2(_hip.ptr(dy2), _hip.ptr(x2), _hip.ptr(weight), _hip.ptr(mean),
+                                       _hip.ptr(rstd), _hip.ptr(dres), _hip.ptr(dx), _hip.ptr(dgamma),
+                                       _hip.ptr(dbeta), _hip.ptr(ws), R, H, int(ctx.rms),
+                                       int(dgamma.dtype == torch.float32), int(direct), _hip.stream()), "norm_bwd")
+    if direct:
+        notify(wp)
+        notify(bp)
+        return dx.view(dy.shape), None, None
+    return dx.view(dy.shape), dgamma, dbeta
+
+
+def _save(ctx, x2, weight, bias, mean, rstd, rms):
+    ctx.save_for_backward(x2, weight, mean, rstd)
+    ctx.rms = rms
+    ctx.has_bias = bias is not None and bias.requires_grad
+    ctx.weight_param, ctx.bias_param = weight, (bias if ctx.has_bias else None)
+
+
 class _NormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, eps, rms):
@@ -25,40 +67,57 @@ class _NormFn(torch.autograd.Function):
         _hip.check(_hip.lib().dw_norm_fwd(_hip.ptr(x2), _hip.ptr(weight), _hip.ptr(bias), _hip.ptr(y),
                                           _hip.ptr(mean), _hip.ptr(rstd), R, H, float(eps), int(rms),
                                           _hip.stream()), "norm_fwd")
-        ctx.save_for_backward(x2, weight, mean, rstd)
-        ctx.rms = rms
-        ctx.has_bias = bias is not None and bias.requires_grad
-        ctx.weight_param, ctx.bias_param = weight, (bias if ctx.has_bias else None)
+        _save(ctx, x2, weight, bias, mean, rstd, rms)
         return y.view(x.shape)
 
     @staticmethod
     def backward(ctx, dy):
-        x2, weight, mean, rstd = ctx.saved_tensors
-        H = x2.shape[-1]
+        dx, dgamma, dbeta = _norm_backward(ctx, dy, None)
+        return dx, dgamma, dbeta, None, None
+
+
+class _AddNormFn(torch.autograd.Function):
+    """(y, h) = (norm(x + res), x + res): the pre-norm residual add fused into
+    the norm.  Backward: dh = norm_bwd(dy) + dh_out in one row pass; x and
+    res receive the same gradient."""
+
+    @staticmethod
+    def forward(ctx, x, res, weight, bias, eps, rms):
+        H = x.shape[-1]
+        x2 = x.contiguous().view(-1, H)
+        r2 = res.contiguous().view(-1, H)
         R = x2.shape[0]
-        dy2 = dy.contiguous().view(-1, H)
-        if dy2.dtype != torch.bfloat16:
-            dy2 = dy2.to(torch.bfloat16)
-        L = _hip.lib()
-        ws = torch.empty(2 * H, device=x2.device, dtype=torch.float32)
-        dx = torch.empty_like(x2)
-        wp, bp = ctx.weight_param, ctx.bias_param
-        gd, bd = direct_grad(wp), direct_grad(bp) if ctx.has_bias else None
-        direct = gd is not None and (not ctx.has_bias or bd is not None)
-        if direct:
-            dgamma, dbeta = gd, bd
-        else:
-            dgamma = torch.empty(H, device=x2.device, dtype=weight.dtype)
-            dbeta = torch.empty(H, device=x2.device, dtype=weight.dtype) if ctx.has_bias else None
-        _hip.check(L.dw_norm_bwd2(_hip.ptr(dy2), _hip.ptr(x2), _hip.ptr(weight), _hip.ptr(mean),
-                                  _hip.ptr(rstd), _hip.ptr(dx), _hip.ptr(dgamma), _hip.ptr(dbeta),
-                                  _hip.ptr(ws), R, H, int(ctx.rms), int(dgamma.dtype == torch.float32),
-                                  int(direct), _hip.stream()), "norm_bwd")
-        if direct:
-            notify(wp)
-            notify(bp)
-            return dx.view(dy.shape), None, None, None, None
-        return dx.view(dy.shape), dgamma, dbeta, None, None
+        _hip.require_bf16(x2, r2, weight, bias)
+        y = torch.empty_like(x2)
+        h = torch.empty_like(x2)
+        mean = None if rms else torch.empty(R, device=x.device, dtype=torch.float32)
+        rstd = torch.empty(R, device=x.device, dtype=torch.float32)
+        _hip.check(_hip.lib().dw_add_norm_fwd(_hip.ptr(x2), _hip.ptr(r2), _hip.ptr(weight), _hip.ptr(bias),
+                                              _hip.ptr(y), _hip.ptr(h), _hip.ptr(mean), _hip.ptr(rstd), R, H,
+                                              float(eps), int(rms), _hip.stream()), "add_norm_fwd")
+        _save(ctx, h, weight, bias, mean, rstd, rms)
+        return y.view(x.shape), h.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy, dh):
+        dx, dgamma, dbeta = _norm_backward(ctx, dy, dh)
+        return dx, dx, dgamma, dbeta, None, None
+
+
+def add_layer_norm(x, res, weight, bias, eps: float = 1e-5):
+    """Returns (layer_norm(x + res), x + res)."""
+    if _hip.use_hip(x):
+        return _AddNormFn.apply(x, res, weight, bias, eps, False)
+    h = x + res
+    return F.layer_norm(h, (h.shape[-1],), weight, bias, eps), h
+
+
+def add_rms_norm(x, res, weight, eps: float = 1e-6):
+    """Returns (rms_norm(x + res), x + res)."""
+    if _hip.use_hip(x):
+        return _AddNormFn.apply(x, res, weight, None, eps, True)
+    h = x + res
+    return rms_norm(h, weight, eps), h
 
 
 def layer_norm(x, weight, bias, eps: float = 1e-5):
@@ -90,6 +149,12 @@ class LayerNorm(nn.Module):
             return _NormFn.apply(x, self.weight, zeros, self.eps, False)
         return layer_norm(x, self.weight, self.bias, self.eps)
 
+    def add_forward(self, x, res):
+        """(norm(x + res), x + res) with the residual add fused in."""
+        if self.bias is None and _hip.use_hip(x):
+            return _AddNormFn.apply(x, res, self.weight, torch.zeros_like(self.weight), self.eps, False)
+        return add_layer_norm(x, res, self.weight, self.bias, self.eps)
+
 
 class RMSNorm(nn.Module):
     def __init__(self, hidden, eps=1e-6, device=None, dtype=None):
@@ -99,6 +164,9 @@ class RMSNorm(nn.Module):
 
     def forward(self, x):
         return rms_norm(x, self.weight, self.eps)
+
+    def add_forward(self, x, res):
+        return add_rms_norm(x, res, self.weight, self.eps)
 
 
 AtorchLayerNorm = LayerNorm  # reference-compatible name

@@ -24,6 +24,7 @@ import torch
 import torch.distributed as dist
 from torch.utils.data import DataLoader, Sampler
 
+from ..atorch.fault_tolerance import heartbeat
 from ..common.constants import ConfigPath, NodeEnv
 from ..common.log import logger
 
@@ -97,6 +98,9 @@ class ElasticTrainer:
         self.gradient_accumulation_steps = 1
         self._report_interval = report_interval
         self._last_report = 0.0
+        from ..utils.xpu_timer import maybe_install_from_env
+
+        maybe_install_from_env()
 
     def prepare(self, optimizer, lr_scheduler=None):
         self._set_gradient_accumulation_steps()
@@ -130,6 +134,7 @@ class ElasticTrainer:
             yield
         if gs.sync_gradients:
             gs.num_steps += 1
+            heartbeat()
             maybe_inject_fault(gs.num_steps)
             now = time.time()
             if now - self._last_report > self._report_interval:

@@ -61,6 +61,10 @@ def parse_args(argv=None):
     p.add_argument("--auto_tunning", "--auto-tunning", action="store_true")
     p.add_argument("--exclude-straggler", "--exclude_straggler", action="store_true")
     p.add_argument("--save_at_breakpoint", "--save-at-breakpoint", type=_bool, default=True)
+    p.add_argument("--relaunch-on-hang", "--relaunch_on_hanging", type=float, default=0.0, metavar="SECONDS",
+                   help="relaunch the worker group when a worker heartbeat is older than SECONDS")
+    p.add_argument("--xpu-timer", "--xpu_timer", action="store_true",
+                   help="install the xpu_timer (GEMM/collective timing + hang detection) in every worker")
     p.add_argument("--accelerator", default=Accelerators.AMD_GPU,
                    choices=[Accelerators.AMD_GPU, Accelerators.NVIDIA_GPU, Accelerators.ASCEND_NPU,
                             Accelerators.CPU])
@@ -112,6 +116,10 @@ def build_config(a) -> "ElasticLaunchConfig":
                               save_at_breakpoint=a.save_at_breakpoint, auto_config=a.auto_config,
                               auto_tunning=a.auto_tunning, accelerator=a.accelerator, log_dir=a.log_dir,
                               node_rank=a.node_rank, local_addr=a.local_addr)
+    if a.relaunch_on_hang > 0:
+        cfg.hang_timeout = a.relaunch_on_hang
+    if a.xpu_timer:
+        cfg.extra_env["DWAMD_XPU_TIMER"] = "1"
     if "join_timeout" in conf:
         cfg.join_timeout = float(conf["join_timeout"])
     if "lastcall_timeout" in conf:
@@ -158,10 +166,16 @@ def run(a) -> int:
     os.environ.setdefault(NodeEnv.TORCHELASTIC_RUN_ID, cfg.run_id)
     logger.info(f"dwamd-run: master={master_addr} nodes={cfg.min_nodes}:{cfg.max_nodes} nproc={cfg.nproc_per_node} "
                 f"node_rank={cfg.node_rank}")
+    rc = 1
     try:
-        return launch_agent(cfg, a.training_script, a.training_script_args, master_addr, is_module=a.module)
+        rc = launch_agent(cfg, a.training_script, a.training_script_args, master_addr, is_module=a.module)
+        return rc
     finally:
         if master_proc is not None:
+            if rc == 0 and cfg.max_nodes > 1:
+                from ..elastic_agent.agent import wait_nodes_done
+
+                wait_nodes_done(master_addr, cfg.run_id, cfg.min_nodes)
             master_proc.terminate()
             try:
                 master_proc.wait(timeout=10)

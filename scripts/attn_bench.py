@@ -5,6 +5,8 @@ import math
 
 import torch
 
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dlrover_wuqiong_amd.ops.attention import flash_attn_func, flash_attn_qkvpacked_func
 
 

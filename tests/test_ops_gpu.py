@@ -51,6 +51,41 @@ def test_norm_fwd_bwd(H, rms):
         assert _rel(b.grad, bf.grad) < 2e-2
 
 
+@pytest.mark.parametrize("H", [256, 1600])
+@pytest.mark.parametrize("rms", [False, True])
+def test_add_norm_fused(H, rms):
+    """(norm(x + r), x + r) with both outputs used downstream (as in the
+    split residual stream) vs fp32 autograd; also exercises the self-cleaning
+    workspace across repeated calls."""
+    from dlrover_wuqiong_amd.ops.norm import add_layer_norm, add_rms_norm
+
+    torch.manual_seed(1)
+    for _ in range(2):
+        x = torch.randn(513, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+        r = torch.randn(513, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+        w = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16).requires_grad_()
+        b = (0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16).requires_grad_()
+        dy = torch.randn(513, H, device=DEV, dtype=torch.bfloat16)
+        dh = torch.randn(513, H, device=DEV, dtype=torch.bfloat16)
+        xf, rf = x.detach().float().requires_grad_(), r.detach().float().requires_grad_()
+        wf, bf = w.detach().float().requires_grad_(), b.detach().float().requires_grad_()
+        if rms:
+            y, h = add_rms_norm(x, r, w, 1e-6)
+            hf = xf + rf
+            yr = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-6) * wf
+        else:
+            y, h = add_layer_norm(x, r, w, b, 1e-5)
+            hf = xf + rf
+            yr = F.layer_norm(hf, (H,), wf, bf, 1e-5)
+        assert _rel(h, hf) < 5e-3 and _rel(y, yr) < 1e-2
+        torch.autograd.backward([y, h], [dy, dh])
+        torch.autograd.backward([yr, hf], [dy.float(), dh.float()])
+        assert _rel(x.grad, xf.grad) < 2e-2 and _rel(r.grad, rf.grad) < 2e-2
+        assert _rel(w.grad, wf.grad) < 2e-2
+        if not rms:
+            assert _rel(b.grad, bf.grad) < 2e-2
+
+
 def test_bias_gelu():
     from dlrover_wuqiong_amd.ops.activation import bias_gelu
 

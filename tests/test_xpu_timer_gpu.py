@@ -1,0 +1,50 @@
+"""xpu_timer native HIP-event backend on the GPU: per-shape GEMM timing and
+device-hang detection (a calibrated ~2 s spin kernel vs a 0.5 s timeout)."""
+
+import time
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def test_gemm_timing_and_hang_detection():
+    from dlrover_wuqiong_amd.utils.xpu_timer import XpuTimer, _HipBackend
+
+    hangs = []
+    t = XpuTimer(hang_timeout=0.5, poll_ms=10, on_hang=[lambda d, s: hangs.append(d)]).install(collectives=False)
+    try:
+        assert isinstance(t.backend, _HipBackend)
+        a = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+        b = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+        for _ in range(20):
+            torch.mm(a, b)
+        torch.cuda.synchronize()
+        assert t.flush(10)
+        st = {s.key: s for s in t.stats()}["mm|4096_4096_4096"]
+        assert st.count == 20 and st.avg_us > 0
+        assert 50 < st.rate()["tflops"] < 2600, st  # plausible for MI355X bf16
+        # calibrate torch.cuda._sleep, then spin ~2 s inside a timed region
+        s0 = time.time()
+        torch.cuda._sleep(10_000_000)
+        torch.cuda.synchronize()
+        per_cycle = max(time.time() - s0, 1e-4) / 10_000_000
+        cycles = int(min(2.0 / per_cycle, 2e10))
+        with t.timed("spin|x", 0.0, a):
+            torch.cuda._sleep(cycles)
+        deadline = time.time() + 5
+        while not hangs and time.time() < deadline:
+            time.sleep(0.05)
+        torch.cuda.synchronize()
+        assert hangs and "spin|x" in hangs[0]
+        time.sleep(0.2)
+        assert t.hang_status()[0] == 0  # cleared once the op finished
+    finally:
+        t.uninstall()
