@@ -123,6 +123,22 @@ def _declare_runtime(lib):
         "dw_blob_get": (i64, [vp, vp, u64, c.POINTER(u64), c.POINTER(u64)]),
         "dw_blob_version": (u64, [vp]),
         "dw_runtime_abi_version": (i32, []),
+        "dw_ring_open": (vp, [cp, i32, u32, u64, u32, u32, u32, dbl]),
+        "dw_ring_close": (i32, [vp]),
+        "dw_ring_slot_bytes": (u64, [vp]),
+        "dw_ring_nslots": (u32, [vp]),
+        "dw_ring_epoch": (u32, [vp]),
+        "dw_ring_base": (vp, [vp]),
+        "dw_ring_total": (u64, [vp]),
+        "dw_ring_slot": (vp, [vp, i64]),
+        "dw_ring_write_acquire": (i64, [vp, dbl]),
+        "dw_ring_write_commit": (i32, [vp, i64, u64]),
+        "dw_ring_read_acquire": (i64, [vp, i32, dbl, c.POINTER(u64)]),
+        "dw_ring_read_release": (i32, [vp, i32, i64]),
+        "dw_ring_stop": (i32, [vp]),
+        "dw_ring_abort": (i32, [vp]),
+        "dw_ring_next_epoch": (i32, [vp, dbl]),
+        "dw_ring_wait_epoch": (i32, [vp, u32, dbl]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
