@@ -140,7 +140,8 @@ def test_shm_ring_direct_dma_to_gpu():
         for i in range(5):
             w.put({"a": torch.arange(100000) + i, "b": torch.full((7, 9), float(i), dtype=torch.bfloat16)})
             b = r.get(0, device="cuda")
-            assert b["a"].is_cuda and int(b["a"][0].item()) == i and float(b["b"].float().mean()) == i
+            assert b["a"].is_cuda and torch.equal(b["a"].cpu(), torch.arange(100000) + i)
+            assert torch.equal(b["b"].cpu(), torch.full((7, 9), float(i), dtype=torch.bfloat16))
         w.stop()
         assert r.get(0, device="cuda") is None
     finally:
