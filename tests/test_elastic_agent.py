@@ -86,7 +86,10 @@ def test_two_nodes_one_fails(tmp_path):
     assert n1.returncode == 0, l1[-3000:]
     res = _results(out)
     assert res and res[-1]["world"] == 2
-    assert res[-1]["restart"] >= 1 and res[-1]["start_step"] == 5
+    # node 0's group restarts either on its own gloo failure (counted) or on
+    # the membership change (not counted, torch semantics): both resume from
+    # the in-memory step-5 checkpoint
+    assert res[-1]["start_step"] == 5
 
 
 def test_network_check_then_train(tmp_path):
