@@ -21,6 +21,10 @@ Optimizations (applied in a fixed, dependency-respecting order):
   tensor_parallel    DTensor TP plan inferred from Llama/GPT-style layer names
                      (q/k/v/gate/up column-wise, o/down row-wise)
   checkpoint         activation checkpointing of the given (or decoder) layers
+  pipeline_parallel  split GPT2/Llama at decoder layers over the ``("pipeline", p)``
+                     dimension; {"chunks": micro-batches, "schedule": "1f1b" |
+                     "gpipe" | "interleaved", "virtual_stages": v}; train with
+                     ``result.model.train_step(ids, targets)`` (``parallel/pipeline.py``)
   fsdp / zero2       FSDP2 ``fully_shard`` per layer (zero2: no reshard after fwd)
   zero1              ZeroRedundancyOptimizer on top of DDP
   ddp                DistributedDataParallel (default when data parallel > 1)
@@ -50,8 +54,9 @@ from ..common.log import logger
 from . import distributed as adist
 
 ORDER = ["parallel_mode", "module_replace", "half", "amp_native", "tensor_parallel", "sequence_parallel",
-         "checkpoint", "fsdp", "zero2", "zero1", "ddp"]
-ALIASES = {"amp": "amp_native", "amp_native_bf16": "amp_native", "fsdp2": "fsdp", "zero3": "fsdp"}
+         "checkpoint", "pipeline_parallel", "fsdp", "zero2", "zero1", "ddp"]
+ALIASES = {"amp": "amp_native", "amp_native_bf16": "amp_native", "fsdp2": "fsdp", "zero3": "fsdp",
+           "pipe": "pipeline_parallel", "pipeline": "pipeline_parallel", "ds_3d_parallel": "pipeline_parallel"}
 
 
 @dataclass
@@ -273,6 +278,31 @@ def _apply_checkpoint(ctx, cfg):
         logger.info(f"checkpoint: activation checkpointing on {[c.__name__ for c in classes]}")
 
 
+def _apply_pipeline_parallel(ctx, cfg):
+    from ..parallel.pipeline import PipelineModule
+
+    cfg = cfg if isinstance(cfg, dict) else {}
+    group, ranks = adist.parallel_group_and_ranks("pipeline")
+    if not ranks or len(ranks) == 1:
+        return
+    me = dist.get_rank()
+    emb_group = None
+    # first + last stage of every pipeline group (created by every rank, same order)
+    for _g, rk in adist._DistributedContext.PARALLEL_GROUPS_AND_RANKS["pipeline"]:
+        eg = dist.new_group(sorted({rk[0], rk[-1]}))
+        if me in rk:
+            emb_group = eg
+    pipe = PipelineModule(ctx["model"], len(ranks), ranks.index(me),
+                          num_microbatches=cfg.get("chunks", cfg.get("num_microbatches", len(ranks))),
+                          schedule=cfg.get("schedule", "1f1b"), virtual_stages=cfg.get("virtual_stages", 1),
+                          group=group, embedding_group=emb_group)
+    pipe.amp_dtype = ctx.get("amp_dtype")
+    ctx["model"] = pipe
+    ctx["pipeline"] = True
+    logger.info(f"pipeline_parallel: stage {pipe.stage}/{len(ranks)} "
+                f"layers {[(c.start, c.end) for c in pipe.chunks]} schedule {pipe.schedule_name}")
+
+
 def _apply_fsdp(ctx, cfg, reshard=True):
     from torch.distributed.fsdp import MixedPrecisionPolicy, fully_shard
 
@@ -304,6 +334,11 @@ def _apply_ddp(ctx, cfg):
     if not dist.is_initialized() or ctx.get("fsdp"):
         return
     dpg = ctx.get("dp_group")
+    if ctx.get("pipeline"):
+        # the pipeline all-reduces stage gradients over the data dimension
+        if dpg is not None and dist.get_world_size(dpg) > 1:
+            ctx["model"].dp_group = dpg
+        return
     if adist.parallel_config() is not None and dpg is None:
         return  # the parallel config has no data-parallel dimension
     if dpg is not None and dist.get_world_size(dpg) == 1:
@@ -318,6 +353,7 @@ def _apply_ddp(ctx, cfg):
 APPLY = {"parallel_mode": _apply_parallel_mode, "module_replace": _apply_module_replace, "half": _apply_half,
          "amp_native": _apply_amp_native, "tensor_parallel": _apply_tensor_parallel,
          "sequence_parallel": _apply_sequence_parallel, "checkpoint": _apply_checkpoint,
+         "pipeline_parallel": _apply_pipeline_parallel,
          "fsdp": _apply_fsdp, "zero2": functools.partial(_apply_fsdp, reshard=False),
          "zero1": lambda ctx, cfg: ctx.__setitem__("zero1", True), "ddp": _apply_ddp}
 
@@ -347,16 +383,14 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
     for name, cfg in strategy.opts:
         if name == "parallel_mode":
             APPLY[name](ctx, cfg)
-            if dev.type == "cuda" and "fsdp" not in strategy.names():
-                ctx["model"] = ctx["model"].to(dev)
-            elif dev.type == "cuda":
-                ctx["model"] = ctx["model"].to(dev)
+            if dev.type == "cuda" and "pipeline_parallel" not in strategy.names():
+                ctx["model"] = ctx["model"].to(dev)  # a pipeline moves only its own stage later
             continue
         APPLY[name](ctx, cfg)
     model = ctx["model"]
     if dev.type == "cuda":
         model = model.to(dev)
-    if ctx.get("amp_dtype") is not None and not ctx.get("fsdp"):
+    if ctx.get("amp_dtype") is not None and not ctx.get("fsdp") and not ctx.get("pipeline"):
         model = _AutocastModule(model, ctx["amp_dtype"])
 
     optim = None

@@ -85,6 +85,8 @@ def initialize_model_parallel(tensor_model_parallel_size: int = 1, pipeline_mode
     build("dp_cp", lambda t, c, d, p: [rank_of(t, xc, xd, p) for xd in range(dp) for xc in range(cp)])
     build("pp", lambda t, c, d, p: [rank_of(t, c, d, x) for x in range(pp)])
     build("mp", lambda t, c, d, p: [rank_of(xt, c, d, xp) for xp in range(pp) for xt in range(tp)])
+    # first + last pipeline stage: tied input embedding / LM head gradients
+    build("embd", lambda t, c, d, p: sorted({rank_of(t, c, d, 0), rank_of(t, c, d, pp - 1)}))
 
     def ep_members(t, c, d, p):
         flat = c + cp * d  # position inside dp_cp
@@ -161,6 +163,10 @@ def get_expert_data_parallel_group():
 
 def get_model_parallel_group():
     return _group("mp")
+
+
+def get_embedding_group():
+    return _group("embd")
 
 
 def get_tensor_model_parallel_rank() -> int:

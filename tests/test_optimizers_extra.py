@@ -94,3 +94,44 @@ def test_codec_roundtrip():
         vr = dequant_v(cv, sv, bits)
         assert (vr > 0).all()  # zero-point free
         assert ((vr.sqrt() - v.sqrt()).abs() <= sv.sqrt()[:, None] * (1.0 / (16 if bits == 4 else 256))).all()
+
+
+def test_bf16_optimizer_keeps_fp32_masters_and_skips_nonfinite():
+    import torch
+
+    from dlrover_wuqiong_amd.optimizers.bf16 import BF16Optimizer
+
+    torch.manual_seed(0)
+    ref = torch.nn.Linear(16, 8)
+    lo = torch.nn.Linear(16, 8).to(torch.bfloat16)
+    lo.load_state_dict({k: v.to(torch.bfloat16) for k, v in ref.state_dict().items()})
+    ref.load_state_dict({k: v.float() for k, v in lo.state_dict().items()})
+    opt = BF16Optimizer(torch.optim.SGD(lo.parameters(), lr=1e-3))
+    ref_opt = torch.optim.SGD(ref.parameters(), lr=1e-3)
+    for _ in range(20):
+        x = torch.randn(4, 16)
+        lo(x.bfloat16()).float().square().mean().backward()
+        ref(x).square().mean().backward()
+        # feed the reference the same (bf16-rounded) gradient
+        for p, q in zip(ref.parameters(), lo.parameters()):
+            p.grad.copy_(q.grad.float())
+        opt.step()
+        ref_opt.step()
+        opt.zero_grad()
+        ref_opt.zero_grad()
+    # masters accumulate tiny updates that bf16 alone would round away
+    masters = opt.master_groups[0]
+    assert all(m.dtype == torch.float32 for m in masters)
+    for m, r in zip(masters, ref.parameters()):
+        assert torch.allclose(m, r, atol=1e-6)
+    for p, m in zip(lo.parameters(), masters):
+        assert torch.equal(p, m.to(torch.bfloat16))
+    # non-finite gradient -> step skipped
+    w0 = masters[0].clone()
+    lo.weight.grad = torch.full_like(lo.weight, float("inf"))
+    opt.step()
+    assert opt.skipped_steps == 1 and torch.equal(masters[0], w0)
+    sd = opt.state_dict()
+    opt2 = BF16Optimizer(torch.optim.SGD(lo.parameters(), lr=1e-3))
+    opt2.load_state_dict(sd)
+    assert torch.equal(opt2.master_groups[0][0], masters[0])
