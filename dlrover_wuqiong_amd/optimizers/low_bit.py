@@ -11,10 +11,12 @@ zero signed map for m and a zero-point-free quadratic map for v.
 On CPU the identical algorithm runs in PyTorch (``_ref_step``), which is also
 the fp32 reference the GPU test compares the kernel against.
 
-Parity: ATorch ``atorch/optimizers/low_bit/optim/q_adamw.py`` (``Q_AdamW``,
-``q_bits``, ``threshold``; ATorch also ships Q_AGD / Q_CAME / Q_Adafactor on
-the same quantizer -- ``Q_AGD`` here reuses the AGD math with quantized
-states through the reference path).
+``Q_AGD``, ``Q_Adafactor`` and ``Q_CAME`` keep their moments in the same
+codec through ``QState`` (decode -> fp32 update -> encode; row/column
+statistics of factored second moments stay fp32 since they are O(rows+cols)).
+
+Parity: ATorch ``atorch/optimizers/low_bit/optim/{q_adamw,q_agd,q_adafactor,
+q_came}.py`` (``q_bits``, ``threshold`` and the per-optimizer hyper-parameters).
 """
 
 import math
@@ -181,3 +183,282 @@ class Q_AdamW(torch.optim.Optimizer):  # noqa: N801 (reference name)
     def state_bytes(self) -> int:
         return sum(t.numel() * t.element_size() for st in self.state.values() for t in st.values()
                    if torch.is_tensor(t))
+
+
+# ------------------------------------------------------------ generic quantized state
+class QState:
+    """One optimizer state tensor held as group-quantized codes (128 elements
+    per fp32 scale).  ``signed=True`` uses the first-moment map (sign +
+    magnitude), ``signed=False`` the second-moment (sqrt-spaced, non-negative)
+    map; ``bits`` 4 packs two codes per byte.  ``bits=32`` keeps fp32."""
+
+    def __init__(self, like: torch.Tensor, bits: int, signed: bool):
+        self.shape, self.n = like.shape, like.numel()
+        self.bits, self.signed = bits, signed
+        dev = like.device
+        if bits == 32:
+            self.full = torch.zeros(self.n, dtype=torch.float32, device=dev)
+            return
+        npad = _pad(self.n)
+        self.codes = torch.zeros(npad // 2 if bits == 4 else npad, dtype=torch.uint8, device=dev)
+        self.scale = torch.zeros(npad // GROUP, dtype=torch.float32, device=dev)
+
+    def decode(self) -> torch.Tensor:
+        if self.bits == 32:
+            return self.full.clone().view(self.shape)
+        G = self.scale.numel()
+        c = _unpack4(self.codes) if self.bits == 4 else self.codes
+        x = (dequant_m if self.signed else dequant_v)(c.view(G, GROUP), self.scale, self.bits)
+        x = torch.where(self.scale[:, None] > 0, x, torch.zeros_like(x))
+        return x.view(-1)[:self.n].view(self.shape)
+
+    def encode(self, x: torch.Tensor):
+        if self.bits == 32:
+            self.full.copy_(x.reshape(-1))
+            return
+        G = self.scale.numel()
+        buf = torch.zeros(G * GROUP, dtype=torch.float32, device=x.device)
+        buf[:self.n] = x.reshape(-1).float()
+        codes, scale = (quant_m if self.signed else quant_v)(buf.view(G, GROUP), self.bits)
+        self.codes.copy_(_pack4(codes.view(-1)) if self.bits == 4 else codes.view(-1))
+        self.scale.copy_(scale)
+
+    def nbytes(self) -> int:
+        if self.bits == 32:
+            return self.full.numel() * 4
+        return self.codes.numel() + self.scale.numel() * 4
+
+
+def _rms(t: torch.Tensor) -> torch.Tensor:
+    return t.norm(2) / (t.numel() ** 0.5)
+
+
+def _approx_sq(row: torch.Tensor, col: torch.Tensor) -> torch.Tensor:
+    r = (row / row.mean(dim=-1, keepdim=True)).rsqrt_().unsqueeze(-1)
+    c = col.unsqueeze(-2).rsqrt()
+    return r * c
+
+
+class _LowBitBase(torch.optim.Optimizer):
+    def __init__(self, params, defaults, q_bits: int, threshold: int):
+        if q_bits not in (4, 8, 32):
+            raise ValueError("q_bits must be 4, 8 or 32")
+        defaults = dict(defaults, q_bits=q_bits, threshold=threshold)
+        super().__init__(params, defaults)
+
+    def _q(self, p, group, signed: bool) -> QState:
+        bits = group["q_bits"] if p.numel() >= group["threshold"] else 32
+        return QState(p, bits, signed)
+
+    def state_bytes(self) -> int:
+        total = 0
+        for st in self.state.values():
+            for v in st.values():
+                if isinstance(v, QState):
+                    total += v.nbytes()
+                elif torch.is_tensor(v):
+                    total += v.numel() * v.element_size()
+        return total
+
+
+class Q_AGD(_LowBitBase):  # noqa: N801 (reference name)
+    """AGD (``optimizers/agd.py``) with 4/8-bit first and second moments.
+    Parity: ``atorch/optimizers/low_bit/optim/q_agd.py``."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), delta=1e-5, weight_decay=0.0, amsgrad=False,
+                 clip=None, q_bits: int = 4, threshold: int = 4096):
+        super().__init__(params, dict(lr=lr, betas=betas, delta=delta, weight_decay=weight_decay,
+                                      amsgrad=amsgrad, clip=clip), q_bits, threshold)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for grp in self.param_groups:
+            b1, b2 = grp["betas"]
+            lr, wd = grp["lr"], grp["weight_decay"]
+            for p in grp["params"]:
+                if p.grad is None:
+                    continue
+                g = p.grad.float()
+                st = self.state[p]
+                if not st:
+                    st["step"] = 0
+                    st["exp_avg"] = self._q(p, grp, True)
+                    st["exp_avg_sq"] = self._q(p, grp, False)
+                    if grp["amsgrad"]:
+                        st["max_exp_avg_sq"] = self._q(p, grp, False)
+                st["step"] += 1
+                t = st["step"]
+                m, v = st["exp_avg"].decode(), st["exp_avg_sq"].decode()
+                bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
+                prev = m / (1 - b1 ** (t - 1)) if t > 1 else torch.zeros_like(m)
+                m.mul_(b1).add_(g, alpha=1 - b1)
+                diff = m / bc1 - prev
+                v.mul_(b2).addcmul_(diff, diff, value=1 - b2)
+                if grp["amsgrad"]:
+                    vmax = torch.maximum(st["max_exp_avg_sq"].decode(), v)
+                    st["max_exp_avg_sq"].encode(vmax)
+                    den = vmax.sqrt()
+                else:
+                    den = v.sqrt()
+                den.clamp_(min=grp["delta"] * math.sqrt(bc2))
+                upd = m / den
+                if grp["clip"] is not None:
+                    upd.clamp_(-grp["clip"], grp["clip"])
+                pf = p.float()
+                if wd:
+                    pf.mul_(1.0 - lr * wd)
+                pf.add_(upd, alpha=-lr * math.sqrt(bc2) / bc1)
+                p.copy_(pf)
+                st["exp_avg"].encode(m)
+                st["exp_avg_sq"].encode(v)
+        return loss
+
+
+class Q_Adafactor(_LowBitBase):  # noqa: N801 (reference name)
+    """Adafactor with factored second moments for >= 2-D parameters (row /
+    column statistics stay fp32: they are tiny) and quantized first moment /
+    unfactored second moment.  Parity:
+    ``atorch/optimizers/low_bit/optim/q_adafactor.py`` (same hyper-parameters:
+    relative_step, scale_parameter, warmup_init, decay_rate, clip_threshold)."""
+
+    def __init__(self, params, lr=None, eps2=(1e-30, 1e-3), clip_threshold=1.0, decay_rate=-0.8, beta1=None,
+                 weight_decay=0.0, scale_parameter=True, relative_step=True, warmup_init=False, q_bits: int = 4,
+                 threshold: int = 4096):
+        if lr is not None and relative_step:
+            relative_step = False  # an explicit lr wins
+        if lr is None and not relative_step:
+            raise ValueError("lr is required when relative_step=False")
+        super().__init__(params, dict(lr=lr, eps2=eps2, clip_threshold=clip_threshold, decay_rate=decay_rate,
+                                      beta1=beta1, weight_decay=weight_decay, scale_parameter=scale_parameter,
+                                      relative_step=relative_step, warmup_init=warmup_init), q_bits, threshold)
+
+    @staticmethod
+    def _lr(grp, st):
+        rel = grp["lr"]
+        if grp["relative_step"]:
+            min_step = 1e-6 * st["step"] if grp["warmup_init"] else 1e-2
+            rel = min(min_step, 1.0 / math.sqrt(st["step"]))
+        scale = max(grp["eps2"][1], float(st["RMS"])) if grp["scale_parameter"] else 1.0
+        return scale * rel
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for grp in self.param_groups:
+            for p in grp["params"]:
+                if p.grad is None:
+                    continue
+                g = p.grad.float()
+                st = self.state[p]
+                factored = g.dim() >= 2
+                if not st:
+                    st["step"] = 0
+                    if grp["beta1"] is not None:
+                        st["exp_avg"] = self._q(p, grp, True)
+                    if factored:
+                        st["exp_avg_sq_row"] = torch.zeros(g.shape[:-1], device=p.device)
+                        st["exp_avg_sq_col"] = torch.zeros(g.shape[:-2] + g.shape[-1:], device=p.device)
+                    else:
+                        st["exp_avg_sq"] = self._q(p, grp, False)
+                st["step"] += 1
+                pf = p.float()
+                st["RMS"] = _rms(pf)
+                lr = self._lr(grp, st)
+                beta2t = 1.0 - math.pow(st["step"], grp["decay_rate"])
+                upd = g * g + grp["eps2"][0]
+                if factored:
+                    row, col = st["exp_avg_sq_row"], st["exp_avg_sq_col"]
+                    row.mul_(beta2t).add_(upd.mean(dim=-1), alpha=1.0 - beta2t)
+                    col.mul_(beta2t).add_(upd.mean(dim=-2), alpha=1.0 - beta2t)
+                    upd = _approx_sq(row, col).mul_(g)
+                else:
+                    v = st["exp_avg_sq"].decode()
+                    v.mul_(beta2t).add_(upd, alpha=1.0 - beta2t)
+                    st["exp_avg_sq"].encode(v)
+                    upd = v.rsqrt().mul_(g)
+                upd.div_(max(1.0, float(_rms(upd)) / grp["clip_threshold"]))
+                upd.mul_(lr)
+                if grp["beta1"] is not None:
+                    m = st["exp_avg"].decode()
+                    m.mul_(grp["beta1"]).add_(upd, alpha=1 - grp["beta1"])
+                    st["exp_avg"].encode(m)
+                    upd = m
+                if grp["weight_decay"]:
+                    pf.mul_(1 - grp["weight_decay"] * lr)
+                pf.sub_(upd)
+                p.copy_(pf)
+        return loss
+
+
+class Q_CAME(_LowBitBase):  # noqa: N801 (reference name)
+    """CAME (confidence-guided adaptive memory-efficient optimisation):
+    Adafactor-style factored second moment plus a factored "instability"
+    statistic of (update - exp_avg)^2 that scales the first moment.  Parity:
+    ``atorch/optimizers/low_bit/optim/q_came.py``."""
+
+    def __init__(self, params, lr=None, eps=(1e-30, 1e-16), clip_threshold=1.0, betas=(0.9, 0.999, 0.9999),
+                 weight_decay=0.0, q_bits: int = 4, threshold: int = 4096):
+        if lr is None:
+            raise ValueError("Q_CAME needs an explicit lr")
+        super().__init__(params, dict(lr=lr, eps=eps, clip_threshold=clip_threshold, betas=betas,
+                                      weight_decay=weight_decay), q_bits, threshold)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for grp in self.param_groups:
+            b1, b2, b3 = grp["betas"]
+            for p in grp["params"]:
+                if p.grad is None:
+                    continue
+                g = p.grad.float()
+                st = self.state[p]
+                factored = g.dim() >= 2
+                if not st:
+                    st["step"] = 0
+                    st["exp_avg"] = self._q(p, grp, True)
+                    if factored:
+                        for k, shp in (("exp_avg_sq_row", g.shape[:-1]), ("exp_avg_sq_col", g.shape[:-2] + g.shape[-1:]),
+                                       ("exp_avg_res_row", g.shape[:-1]),
+                                       ("exp_avg_res_col", g.shape[:-2] + g.shape[-1:])):
+                            st[k] = torch.zeros(shp, device=p.device)
+                    else:
+                        st["exp_avg_sq"] = self._q(p, grp, False)
+                st["step"] += 1
+                upd = g * g + grp["eps"][0]
+                if factored:
+                    st["exp_avg_sq_row"].mul_(b2).add_(upd.mean(dim=-1), alpha=1.0 - b2)
+                    st["exp_avg_sq_col"].mul_(b2).add_(upd.mean(dim=-2), alpha=1.0 - b2)
+                    upd = _approx_sq(st["exp_avg_sq_row"], st["exp_avg_sq_col"]).mul_(g)
+                else:
+                    v = st["exp_avg_sq"].decode()
+                    v.mul_(b2).add_(upd, alpha=1.0 - b2)
+                    st["exp_avg_sq"].encode(v)
+                    upd = v.rsqrt().mul_(g)
+                upd.div_((_rms(upd) / grp["clip_threshold"]).clamp_(min=1.0))
+                m = st["exp_avg"].decode()
+                m.mul_(b1).add_(upd, alpha=1 - b1)
+                st["exp_avg"].encode(m)
+                if factored:
+                    res = (upd - m) ** 2 + grp["eps"][1]
+                    st["exp_avg_res_row"].mul_(b3).add_(res.mean(dim=-1), alpha=1.0 - b3)
+                    st["exp_avg_res_col"].mul_(b3).add_(res.mean(dim=-2), alpha=1.0 - b3)
+                    upd = _approx_sq(st["exp_avg_res_row"], st["exp_avg_res_col"]).mul_(m)
+                else:
+                    upd = m
+                pf = p.float()
+                if grp["weight_decay"]:
+                    pf.mul_(1 - grp["weight_decay"] * grp["lr"])
+                pf.add_(upd, alpha=-grp["lr"])
+                p.copy_(pf)
+        return loss

@@ -135,3 +135,59 @@ def test_bf16_optimizer_keeps_fp32_masters_and_skips_nonfinite():
     opt2 = BF16Optimizer(torch.optim.SGD(lo.parameters(), lr=1e-3))
     opt2.load_state_dict(sd)
     assert torch.equal(opt2.master_groups[0][0], masters[0])
+
+
+def _toy_problem(seed=0):
+    import torch
+
+    g = torch.Generator().manual_seed(seed)
+    w_true = torch.randn(64, 96, generator=g)
+    x = torch.randn(256, 96, generator=g)
+    return x, x @ w_true.T
+
+
+def _fit(opt_cls, steps=150, **kw):
+    import torch
+
+    torch.manual_seed(0)
+    x, y = _toy_problem()
+    lin = torch.nn.Linear(96, 64)
+    opt = opt_cls(lin.parameters(), **kw)
+    first = None
+    for _ in range(steps):
+        loss = (lin(x) - y).square().mean()
+        first = first if first is not None else float(loss.detach())
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+    return first, float((lin(x) - y).square().mean()), opt, lin
+
+
+def test_q_adafactor_fp32_matches_transformers_adafactor():
+    import torch
+    from transformers.optimization import Adafactor
+
+    from dlrover_wuqiong_amd.optimizers.low_bit import Q_Adafactor
+
+    _, l_ref, _, lin_ref = _fit(Adafactor, steps=30, lr=None, relative_step=True, scale_parameter=True,
+                                warmup_init=False)
+    _, l_q, _, lin_q = _fit(Q_Adafactor, steps=30, q_bits=32, threshold=0)
+    assert torch.allclose(lin_ref.weight, lin_q.weight, atol=1e-5), (l_ref, l_q)
+
+
+def test_low_bit_optimizers_converge_with_small_state():
+    from dlrover_wuqiong_amd.optimizers.agd import AGD
+    from dlrover_wuqiong_amd.optimizers.low_bit import Q_AGD, Q_CAME, Q_Adafactor
+
+    # fp32-state Q_AGD == AGD
+    _, l_agd, _, lin_a = _fit(AGD, steps=20, lr=1e-2)
+    _, l_qagd32, _, lin_b = _fit(Q_AGD, steps=20, lr=1e-2, q_bits=32)
+    import torch
+
+    assert torch.allclose(lin_a.weight, lin_b.weight, atol=1e-5)
+    for cls, kw in ((Q_AGD, dict(lr=1e-2)), (Q_CAME, dict(lr=1e-2)), (Q_Adafactor, dict(lr=1e-2, beta1=0.9))):
+        first, last, opt4, _ = _fit(cls, q_bits=4, threshold=1024, **kw)
+        _, last32, opt32, _ = _fit(cls, q_bits=32, threshold=1024, **kw)
+        assert last < 0.85 * first, (cls.__name__, first, last)
+        assert last < 3 * last32 + 0.01 * first, (cls.__name__, last, last32)
+        assert opt4.state_bytes() < 0.5 * opt32.state_bytes(), cls.__name__
