@@ -139,6 +139,9 @@ def _declare_runtime(lib):
         "dw_ring_abort": (i32, [vp]),
         "dw_ring_next_epoch": (i32, [vp, dbl]),
         "dw_ring_wait_epoch": (i32, [vp, u32, dbl]),
+        "dw_cpu_adamw": (i32, [vp, vp, i32, vp, vp, vp, u64, c.c_float, c.c_float, c.c_float, c.c_float,
+                               c.c_float, c.c_float, c.c_float, c.c_float, i32]),
+        "dw_cpu_sumsq": (dbl, [vp, i32, u64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
