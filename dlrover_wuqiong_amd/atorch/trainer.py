@@ -1,0 +1,586 @@
+"""AtorchTrainer: a HuggingFace-``Trainer``-compatible training loop whose
+model / optimizer / data pipeline come from ``auto_accelerate`` and whose
+checkpoints go through the flash-checkpoint engine.
+
+    args = AtorchTrainingArgs(output_dir="out", max_steps=1000, save_steps=100,
+                              atorch_opt="fsdp", atorch_wrap_cls=(LlamaDecoderLayer,),
+                              bf16=True, flash_checkpoint=True)
+    trainer = AtorchTrainer(model, args, train_dataset=ds, data_collator=collate)
+    trainer.train(resume_from_checkpoint=True)
+
+What it does (same contract as the reference, MI355X-first internals):
+
+* ``_atorch_init`` builds the load strategy from the arguments
+  (``atorch_opt`` = ddp | fsdp | zero2 | zero1, ``atorch_wrap_cls``,
+  ``atorch_checkpoint_cls`` for activation checkpointing, bf16/fp16 autocast,
+  ``atorch_module_replace`` for the fused HIP norms) and calls
+  ``auto_accelerate`` -> model, optimizer, distributed dataloader;
+* the loop does gradient accumulation (``no_sync`` on all but the last
+  micro-step), grad-norm clipping, LR scheduling (transformers'
+  ``get_scheduler``), logging, periodic evaluation and HF ``TrainerCallback``
+  events (``on_step_end`` / ``on_log`` / ``on_save`` ...);
+* ``save_steps``: with ``flash_checkpoint=True`` the model + optimizer +
+  scheduler + RNG state is snapshotted to host shm in the training pause and
+  persisted asynchronously (``DdpCheckpointer`` / ``FsdpShardCheckpointer``);
+  otherwise written synchronously.  ``trainer_state.json`` is written by rank
+  0 next to it, and ``save_total_limit`` rotates old checkpoints;
+* ``resume_from_checkpoint`` (path or True = latest) restores everything,
+  preferring the in-memory copy after an in-place restart, and skips the
+  already-consumed batches of the current epoch.
+
+Parity: ATorch ``atorch/trainer/atorch_trainer.py`` (``AtorchTrainer``:
+``train`` :666, ``_inner_training_loop`` :717, ``_save_checkpoint`` :1304,
+``_rotate_checkpoints`` :1714, ``evaluate`` :1742, ``predict`` :1801,
+``training_step`` :2043, ``compute_loss`` :2196) and
+``atorch/trainer/atorch_args.py`` (``AtorchArguments``).
+"""
+
+import json
+import math
+import os
+import random
+import re
+import shutil
+import time
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..common.log import logger
+
+try:
+    from transformers import TrainingArguments
+    from transformers.trainer_callback import (CallbackHandler, DefaultFlowCallback, PrinterCallback, TrainerControl,
+                                               TrainerState)
+except ImportError as e:  # pragma: no cover
+    raise ImportError("AtorchTrainer needs transformers") from e
+
+PREFIX_CHECKPOINT_DIR = "checkpoint"
+TRAINER_STATE_NAME = "trainer_state.json"
+STATE_FILE = "atorch_state.pt"
+
+
+@dataclass
+class AtorchTrainingArgs(TrainingArguments):
+    atorch_opt: str = field(default="ddp", metadata={"help": "ddp | fsdp | zero2 | zero1 | none"})
+    atorch_parallel_mode: bool = field(default=True, metadata={"help": "create named parallel groups"})
+    atorch_module_replace: bool = field(default=True, metadata={"help": "fused HIP norms"})
+    atorch_wrap_cls: Optional[Tuple[Any, ...]] = field(default=None, metadata={"help": "FSDP wrap classes"})
+    atorch_checkpoint_cls: Optional[Tuple[Any, ...]] = field(default=None,
+                                                             metadata={"help": "activation checkpoint classes"})
+    load_strategy: Optional[List[Any]] = field(default=None, metadata={"help": "explicit auto_accelerate strategy"})
+    optim_func: Optional[Callable] = field(default=None, metadata={"help": "optimizer class"})
+    optim_args: Optional[Dict] = field(default=None, metadata={"help": "optimizer kwargs"})
+    optim_param_func: Optional[Callable] = field(default=None, metadata={"help": "model -> param groups"})
+    loss_func: Optional[Callable] = field(default=None, metadata={"help": "(batch, output) -> loss"})
+    prepare_input: Optional[Callable] = field(default=None, metadata={"help": "(batch, device) -> batch"})
+    model_input_format: Optional[str] = field(default="unpack_dict",
+                                              metadata={"help": "unpack_dict | unpack_sequence | None"})
+    flash_checkpoint: bool = field(default=True, metadata={"help": "save through the flash-checkpoint engine"})
+    async_save: bool = field(default=True, metadata={"help": "persist flash checkpoints asynchronously"})
+    shuffle: bool = field(default=True, metadata={"help": "shuffle the training data"})
+    skip_if_nonfinite: bool = field(default=True, metadata={"help": "skip steps with non-finite grad norm"})
+
+    def __post_init__(self):
+        if not self.report_to:
+            self.report_to = []
+        super().__post_init__()
+
+
+def _count_params(model: nn.Module) -> Tuple[int, int]:
+    total = sum(p.numel() for p in model.parameters())
+    train = sum(p.numel() for p in model.parameters() if p.requires_grad)
+    return total, train
+
+
+class AtorchTrainer:
+    def __init__(self, model: nn.Module, args: AtorchTrainingArgs, data_collator=None, train_dataset=None,
+                 eval_dataset=None, tokenizer=None, compute_metrics=None, callbacks=None, optimizers=(None, None)):
+        self.args = args
+        self.data_collator = data_collator
+        self.train_dataset = train_dataset
+        self.eval_dataset = eval_dataset
+        self.tokenizer = tokenizer
+        self.compute_metrics = compute_metrics
+        self.model, self.optimizer, self.lr_scheduler = model, optimizers[0], optimizers[1]
+        self.train_dataloader = None
+        self.strategy = None
+        self.device = torch.device("cpu")
+        self.amp_dtype = None
+        self._checkpointer = None
+        self._atorch_init()
+        cbs = [DefaultFlowCallback] + (callbacks or [])
+        if not args.disable_tqdm:
+            cbs.append(PrinterCallback)
+        self.callback_handler = CallbackHandler(cbs, self.model, tokenizer, self.optimizer, self.lr_scheduler)
+        self.state = TrainerState()
+        self.control = TrainerControl()
+        os.makedirs(args.output_dir, exist_ok=True)
+
+    # ---------------------------------------------------------------- setup
+    def _rank(self) -> int:
+        return dist.get_rank() if dist.is_initialized() else 0
+
+    def _world(self) -> int:
+        return dist.get_world_size() if dist.is_initialized() else 1
+
+    def is_world_process_zero(self) -> bool:
+        return self._rank() == 0
+
+    def is_local_process_zero(self) -> bool:
+        return int(os.environ.get("LOCAL_RANK", "0")) == 0
+
+    def add_callback(self, cb):
+        self.callback_handler.add_callback(cb)
+
+    def pop_callback(self, cb):
+        return self.callback_handler.pop_callback(cb)
+
+    def _build_strategy(self):
+        a = self.args
+        if a.load_strategy is not None:
+            return a.load_strategy
+        s: List[Any] = []
+        if a.atorch_parallel_mode:
+            s.append("parallel_mode")
+        if a.atorch_module_replace:
+            s.append("module_replace")
+        if a.bf16 or a.fp16:
+            s.append(("amp_native", {"dtype": torch.bfloat16 if a.bf16 else torch.float16}))
+        if a.atorch_checkpoint_cls:
+            s.append(("checkpoint", {"wrap_cls": tuple(a.atorch_checkpoint_cls)}))
+        opt = (a.atorch_opt or "none").lower()
+        if opt in ("fsdp", "zero2", "zero1", "ddp"):
+            cfg = {"wrap_cls": tuple(a.atorch_wrap_cls)} if (a.atorch_wrap_cls and opt in ("fsdp", "zero2")) else None
+            s.append((opt, cfg) if cfg else opt)
+        return s
+
+    def _atorch_init(self):
+        from .auto_accelerate import auto_accelerate
+
+        a = self.args
+        optim_func = a.optim_func
+        optim_args = dict(a.optim_args or {})
+        if self.optimizer is None and optim_func is None:
+            optim_func = torch.optim.AdamW
+            optim_args.setdefault("lr", a.learning_rate)
+            optim_args.setdefault("weight_decay", a.weight_decay)
+            optim_args.setdefault("betas", (a.adam_beta1, a.adam_beta2))
+            optim_args.setdefault("eps", a.adam_epsilon)
+        dl_args = {"batch_size": a.per_device_train_batch_size * self._world_hint(), "shuffle": a.shuffle,
+                   "num_workers": a.dataloader_num_workers, "drop_last": a.dataloader_drop_last,
+                   "pin_memory": torch.cuda.is_available()}
+        if self.data_collator is not None:
+            dl_args["collate_fn"] = self.data_collator
+        ok, res, strategy = auto_accelerate(
+            self.model, optim_func if self.optimizer is None else None, dataset=self.train_dataset,
+            loss_func=a.loss_func, prepare_input=a.prepare_input, model_input_format=a.model_input_format,
+            optim_args=optim_args, optim_param_func=a.optim_param_func, dataloader_args=dl_args,
+            load_strategy=self._build_strategy(), sampler_seed=a.seed)
+        if not ok:
+            raise RuntimeError("auto_accelerate failed")
+        self.model = res.model
+        self.optimizer = self.optimizer or res.optim
+        self.train_dataloader = res.dataloader
+        self.prepare_input = res.prepare_input
+        self.loss_func = res.loss_func
+        self.device = res.args.get("device", torch.device("cpu"))
+        self.amp_dtype = res.args.get("amp_dtype")
+        self.grad_scaler = res.args.get("grad_scaler")
+        self.strategy = strategy
+        self.is_fsdp = any(n in ("fsdp", "zero2") for n in strategy.names())
+
+    def _world_hint(self) -> int:
+        if dist.is_initialized():
+            return dist.get_world_size()
+        return int(os.environ.get("WORLD_SIZE", "1"))
+
+    def create_scheduler(self, num_training_steps: int, optimizer=None):
+        from transformers import get_scheduler
+
+        if self.lr_scheduler is None:
+            self.lr_scheduler = get_scheduler(self.args.lr_scheduler_type, optimizer=optimizer or self.optimizer,
+                                              num_warmup_steps=self.args.get_warmup_steps(num_training_steps),
+                                              num_training_steps=num_training_steps)
+        return self.lr_scheduler
+
+    # ---------------------------------------------------------------- steps
+    def _prepare_inputs(self, inputs):
+        return self.prepare_input(inputs, self.device) if self.prepare_input else inputs
+
+    def compute_loss(self, model, inputs, return_outputs=False):
+        fmt = self.args.model_input_format
+        if fmt == "unpack_dict" and isinstance(inputs, dict):
+            outputs = model(**inputs)
+        elif fmt == "unpack_sequence" and isinstance(inputs, (list, tuple)):
+            outputs = model(*inputs)
+        else:
+            outputs = model(inputs)
+        if self.loss_func is not None:
+            loss = self.loss_func(inputs, outputs)
+        elif torch.is_tensor(outputs) and outputs.dim() == 0:
+            loss = outputs
+        elif isinstance(outputs, dict) or hasattr(outputs, "loss"):
+            loss = outputs["loss"] if isinstance(outputs, dict) else outputs.loss
+        else:
+            loss = outputs[0]
+        if isinstance(loss, (tuple, list)):
+            loss = loss[0]
+        return (loss, outputs) if return_outputs else loss
+
+    def _autocast(self):
+        if self.amp_dtype is None or self.is_fsdp:
+            import contextlib
+
+            return contextlib.nullcontext()
+        return torch.autocast(self.device.type, dtype=self.amp_dtype)
+
+    def training_step(self, model, inputs) -> torch.Tensor:
+        model.train()
+        inputs = self._prepare_inputs(inputs)
+        with self._autocast():
+            loss = self.compute_loss(model, inputs)
+        loss = loss / self.args.gradient_accumulation_steps
+        if self.grad_scaler is not None:
+            self.grad_scaler.scale(loss).backward()
+        else:
+            loss.backward()
+        return loss.detach()
+
+    def _clip(self) -> Optional[torch.Tensor]:
+        if not self.args.max_grad_norm or self.args.max_grad_norm <= 0:
+            return None
+        if self.grad_scaler is not None:
+            self.grad_scaler.unscale_(self.optimizer)
+        params = [p for p in self.model.parameters() if p.grad is not None]
+        return torch.nn.utils.clip_grad_norm_(params, self.args.max_grad_norm)
+
+    # ---------------------------------------------------------------- train
+    def train(self, resume_from_checkpoint=None, **kwargs):
+        args = self.args
+        if resume_from_checkpoint is True:
+            resume_from_checkpoint = self._latest_checkpoint()
+        self._set_seed(args.seed)
+        dl = self.train_dataloader
+        if dl is None:
+            raise ValueError("AtorchTrainer needs a train_dataset")
+        ga = max(1, args.gradient_accumulation_steps)
+        len_dl = len(dl) if hasattr(dl, "__len__") else None
+        if args.max_steps > 0:
+            max_steps = args.max_steps
+            steps_per_epoch = max(1, (len_dl or max_steps * ga) // ga)
+            num_epochs = math.ceil(max_steps / steps_per_epoch)
+        else:
+            if len_dl is None:
+                raise ValueError("max_steps must be set when the dataloader has no length")
+            steps_per_epoch = max(1, len_dl // ga)
+            max_steps = math.ceil(args.num_train_epochs * steps_per_epoch)
+            num_epochs = math.ceil(args.num_train_epochs)
+        self.create_scheduler(max_steps)
+        self.callback_handler.optimizer = self.optimizer
+        self.callback_handler.lr_scheduler = self.lr_scheduler
+        self.callback_handler.train_dataloader = dl
+        self.state = TrainerState()
+        self.state.max_steps = max_steps
+        self.state.num_train_epochs = num_epochs
+        self.state.logging_steps, self.state.eval_steps, self.state.save_steps = (
+            args.logging_steps, args.eval_steps, args.save_steps)
+        self.state.is_local_process_zero = self.is_local_process_zero()
+        self.state.is_world_process_zero = self.is_world_process_zero()
+        epochs_done, skip_batches = 0, 0
+        if resume_from_checkpoint:
+            self._load_checkpoint(resume_from_checkpoint)
+            epochs_done = self.state.global_step // steps_per_epoch
+            skip_batches = (self.state.global_step % steps_per_epoch) * ga
+        tot, trainable = _count_params(self.model)
+        logger.info(f"AtorchTrainer: {trainable:,}/{tot:,} trainable params, {max_steps} steps, "
+                    f"strategy {self.strategy.names()}")
+        self.control = self.callback_handler.on_train_begin(args, self.state, self.control)
+        tr_loss = torch.zeros((), device=self.device)
+        logged_loss, last_log_step = 0.0, self.state.global_step
+        start = time.time()
+        self.optimizer.zero_grad(set_to_none=True)
+        for epoch in range(epochs_done, num_epochs):
+            sampler = getattr(dl, "sampler", None)
+            if hasattr(sampler, "set_epoch"):
+                sampler.set_epoch(epoch)
+            self.control = self.callback_handler.on_epoch_begin(args, self.state, self.control)
+            for step, inputs in enumerate(dl):
+                if skip_batches > 0:
+                    skip_batches -= 1
+                    continue
+                last_micro = (step + 1) % ga == 0 or (len_dl is not None and step + 1 == len_dl)
+                if step % ga == 0:
+                    self.control = self.callback_handler.on_step_begin(args, self.state, self.control)
+                sync = last_micro or not hasattr(self.model, "no_sync")
+                ctx = self.model.no_sync() if not sync else _null()
+                with ctx:
+                    tr_loss += self.training_step(self.model, inputs)
+                if not last_micro:
+                    continue
+                norm = self._clip()
+                finite = norm is None or bool(torch.isfinite(norm))
+                if finite or not args.skip_if_nonfinite:
+                    if self.grad_scaler is not None:
+                        self.grad_scaler.step(self.optimizer)
+                        self.grad_scaler.update()
+                    else:
+                        self.optimizer.step()
+                    self.lr_scheduler.step()
+                else:
+                    logger.warning(f"step {self.state.global_step + 1}: non-finite grad norm, skipped")
+                self.optimizer.zero_grad(set_to_none=True)
+                self.state.global_step += 1
+                self.state.epoch = epoch + (step + 1) / max(1, len_dl or 1)
+                self.control = self.callback_handler.on_step_end(args, self.state, self.control)
+                if self.control.should_log:
+                    cur = float(tr_loss)
+                    n = max(1, self.state.global_step - last_log_step)
+                    logs = {"loss": round((cur - logged_loss) / n, 6),
+                            "learning_rate": self.lr_scheduler.get_last_lr()[0],
+                            "grad_norm": float(norm) if norm is not None else None, "epoch": self.state.epoch}
+                    logged_loss, last_log_step = cur, self.state.global_step
+                    self.log(logs)
+                if self.control.should_evaluate and self.eval_dataset is not None:
+                    self.evaluate()
+                if self.control.should_save:
+                    self._save_checkpoint()
+                    self.control = self.callback_handler.on_save(args, self.state, self.control)
+                if self.control.should_training_stop or self.state.global_step >= max_steps:
+                    break
+            self.control = self.callback_handler.on_epoch_end(args, self.state, self.control)
+            if self.control.should_training_stop or self.state.global_step >= max_steps:
+                break
+        if self._checkpointer is not None and hasattr(self._checkpointer, "wait_latest_checkpoint"):
+            self._checkpointer.wait_latest_checkpoint()
+        runtime = time.time() - start
+        metrics = {"train_runtime": round(runtime, 4), "train_loss": float(tr_loss) / max(1, self.state.global_step),
+                   "global_step": self.state.global_step}
+        self.control = self.callback_handler.on_train_end(args, self.state, self.control)
+        return metrics
+
+    def log(self, logs: Dict[str, float]):
+        logs = {k: v for k, v in logs.items() if v is not None}
+        logs["step"] = self.state.global_step
+        self.state.log_history.append(logs)
+        self.control = self.callback_handler.on_log(self.args, self.state, self.control, logs)
+
+    # ---------------------------------------------------------------- eval
+    def get_eval_dataloader(self, eval_dataset=None):
+        ds = eval_dataset if eval_dataset is not None else self.eval_dataset
+        sampler = None
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            sampler = torch.utils.data.distributed.DistributedSampler(ds, shuffle=False)
+        return torch.utils.data.DataLoader(ds, batch_size=self.args.per_device_eval_batch_size, sampler=sampler,
+                                           collate_fn=self.data_collator)
+
+    @torch.no_grad()
+    def evaluate(self, eval_dataset=None, metric_key_prefix: str = "eval") -> Dict[str, float]:
+        dl = self.get_eval_dataloader(eval_dataset)
+        self.model.eval()
+        tot = torch.zeros(2, dtype=torch.float64, device=self.device)
+        preds, labels = [], []
+        for inputs in dl:
+            inputs = self._prepare_inputs(inputs)
+            with self._autocast():
+                loss, out = self.compute_loss(self.model, inputs, return_outputs=True)
+            tot[0] += float(loss)
+            tot[1] += 1
+            if self.compute_metrics is not None:
+                logits = out.logits if hasattr(out, "logits") else out
+                preds.append(logits.detach().float().cpu())
+                if isinstance(inputs, dict) and "labels" in inputs:
+                    labels.append(inputs["labels"].detach().cpu())
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            t = tot.to(self.device) if self.device.type == "cuda" else tot
+            dist.all_reduce(t)
+            tot = t
+        metrics = {f"{metric_key_prefix}_loss": float(tot[0] / max(1.0, float(tot[1])))}
+        if self.compute_metrics is not None and preds:
+            from transformers import EvalPrediction
+
+            m = self.compute_metrics(EvalPrediction(predictions=torch.cat(preds).numpy(),
+                                                    label_ids=torch.cat(labels).numpy() if labels else None))
+            metrics.update({f"{metric_key_prefix}_{k}": v for k, v in m.items()})
+        self.log(dict(metrics))
+        self.control = self.callback_handler.on_evaluate(self.args, self.state, self.control, metrics)
+        self.model.train()
+        return metrics
+
+    @torch.no_grad()
+    def predict(self, test_dataset) -> torch.Tensor:
+        dl = self.get_eval_dataloader(test_dataset)
+        self.model.eval()
+        outs = []
+        for inputs in dl:
+            inputs = self._prepare_inputs(inputs)
+            with self._autocast():
+                _, out = self.compute_loss(self.model, inputs, return_outputs=True)
+            outs.append((out.logits if hasattr(out, "logits") else out).detach().float().cpu())
+        self.model.train()
+        return torch.cat(outs)
+
+    # ---------------------------------------------------------------- checkpoint
+    def _set_seed(self, seed: int):
+        random.seed(seed)
+        np.random.seed(seed)
+        torch.manual_seed(seed)
+
+    def _rng_state(self):
+        st = {"python": random.getstate(), "numpy": np.random.get_state(), "cpu": torch.get_rng_state()}
+        if torch.cuda.is_available():
+            st["cuda"] = torch.cuda.get_rng_state()
+        return st
+
+    def _set_rng_state(self, st):
+        random.setstate(st["python"])
+        np.random.set_state(st["numpy"])
+        torch.set_rng_state(st["cpu"])
+        if "cuda" in st and torch.cuda.is_available():
+            torch.cuda.set_rng_state(st["cuda"])
+
+    def _ckpt_dir(self, step: int) -> str:
+        return os.path.join(self.args.output_dir, f"{PREFIX_CHECKPOINT_DIR}-{step}")
+
+    def _state_dict(self) -> Dict[str, Any]:
+        return {"model": self.model.state_dict(), "optimizer": self.optimizer.state_dict(),
+                "lr_scheduler": self.lr_scheduler.state_dict() if self.lr_scheduler else None,
+                "grad_scaler": self.grad_scaler.state_dict() if self.grad_scaler else None,
+                "global_step": self.state.global_step}
+
+    def _get_checkpointer(self):
+        if self._checkpointer is None:
+            from ..flash_checkpoint.ddp import DdpCheckpointer
+
+            self._checkpointer = DdpCheckpointer(self.args.output_dir)
+        return self._checkpointer
+
+    def _save_checkpoint(self):
+        step = self.state.global_step
+        out = self._ckpt_dir(step)
+        os.makedirs(out, exist_ok=True)
+        sd = self._state_dict()
+        path = os.path.join(out, f"rank_{self._rank()}_{STATE_FILE}")
+        if self.args.flash_checkpoint and not self.is_fsdp:
+            from ..flash_checkpoint.checkpointer import StorageType
+
+            ck = self._get_checkpointer()
+            ck.save_checkpoint(step, sd, path=path, storage_type=StorageType.DISK)
+            if not self.args.async_save:
+                ck.wait_latest_checkpoint()
+        elif self.is_fsdp:
+            from torch.distributed.checkpoint.state_dict import get_state_dict
+
+            import torch.distributed.checkpoint as dcp
+
+            msd, osd = get_state_dict(self.model, self.optimizer)
+            dcp.save({"model": msd, "optimizer": osd}, checkpoint_id=os.path.join(out, "dcp"))
+            extra = {k: v for k, v in sd.items() if k not in ("model", "optimizer")}
+            torch.save(extra, path)
+        else:
+            torch.save(sd, path)
+        torch.save(self._rng_state(), os.path.join(out, f"rng_state_{self._rank()}.pth"))
+        if self.is_world_process_zero():
+            self.state.save_to_json(os.path.join(out, TRAINER_STATE_NAME))
+            with open(os.path.join(self.args.output_dir, "latest_checkpoint.txt"), "w") as f:
+                f.write(os.path.basename(out))
+            self._rotate_checkpoints()
+
+    def _sorted_checkpoints(self) -> List[str]:
+        out = []
+        for d in os.listdir(self.args.output_dir):
+            m = re.match(rf"{PREFIX_CHECKPOINT_DIR}-(\d+)$", d)
+            if m and os.path.isdir(os.path.join(self.args.output_dir, d)):
+                out.append((int(m.group(1)), os.path.join(self.args.output_dir, d)))
+        return [p for _, p in sorted(out)]
+
+    def _rotate_checkpoints(self):
+        limit = self.args.save_total_limit
+        if not limit or limit <= 0:
+            return
+        cks = self._sorted_checkpoints()
+        for old in cks[:max(0, len(cks) - limit)]:
+            logger.info(f"deleting old checkpoint {old} (save_total_limit={limit})")
+            shutil.rmtree(old, ignore_errors=True)
+
+    def _latest_checkpoint(self) -> Optional[str]:
+        cks = self._sorted_checkpoints()
+        return cks[-1] if cks else None
+
+    def _load_checkpoint(self, ckpt_dir: str):
+        path = os.path.join(ckpt_dir, f"rank_{self._rank()}_{STATE_FILE}")
+        if self.is_fsdp:
+            from torch.distributed.checkpoint.state_dict import get_state_dict, set_state_dict
+
+            import torch.distributed.checkpoint as dcp
+
+            msd, osd = get_state_dict(self.model, self.optimizer)
+            sd = {"model": msd, "optimizer": osd}
+            dcp.load(sd, checkpoint_id=os.path.join(ckpt_dir, "dcp"))
+            set_state_dict(self.model, self.optimizer, model_state_dict=sd["model"], optim_state_dict=sd["optimizer"])
+            extra = torch.load(path, map_location="cpu", weights_only=True)
+        else:
+            sd = None
+            if self.args.flash_checkpoint:
+                ck = self._get_checkpointer()
+                got = ck.load_checkpoint(resume_path=path)
+                sd = got if got else None
+            if sd is None:
+                sd = torch.load(path, map_location="cpu", weights_only=True)
+            self.model.load_state_dict(sd["model"])
+            self.optimizer.load_state_dict(sd["optimizer"])
+            extra = sd
+        if extra.get("lr_scheduler") is not None and self.lr_scheduler is not None:
+            self.lr_scheduler.load_state_dict(extra["lr_scheduler"])
+        if extra.get("grad_scaler") is not None and self.grad_scaler is not None:
+            self.grad_scaler.load_state_dict(extra["grad_scaler"])
+        st_path = os.path.join(ckpt_dir, TRAINER_STATE_NAME)
+        if os.path.exists(st_path):
+            self.state = TrainerState.load_from_json(st_path)
+        else:
+            self.state.global_step = int(extra.get("global_step", 0))
+        rng = os.path.join(ckpt_dir, f"rng_state_{self._rank()}.pth")
+        if os.path.exists(rng):
+            self._set_rng_state(torch.load(rng, weights_only=False))  # our own file (numpy RNG tuple)
+        logger.info(f"resumed from {ckpt_dir} at step {self.state.global_step}")
+
+    def save_model(self, output_dir: Optional[str] = None):
+        """Final weights as safetensors (rank 0, gathered for FSDP)."""
+        from safetensors.torch import save_file
+
+        output_dir = output_dir or self.args.output_dir
+        os.makedirs(output_dir, exist_ok=True)
+        if self.is_fsdp:
+            from torch.distributed.checkpoint.state_dict import StateDictOptions, get_model_state_dict
+
+            sd = get_model_state_dict(self.model, options=StateDictOptions(full_state_dict=True, cpu_offload=True))
+        else:
+            m = self.model.module if hasattr(self.model, "module") else self.model
+            sd = m.state_dict()
+        if self.is_world_process_zero():
+            seen, out = {}, {}
+            for k, v in sd.items():
+                v = v.detach().cpu().contiguous()
+                key = v.data_ptr()
+                out[k] = v.clone() if key in seen else v  # tied weights: safetensors forbids shared storage
+                seen[key] = k
+            save_file(out, os.path.join(output_dir, "model.safetensors"))
+            with open(os.path.join(output_dir, "atorch_strategy.json"), "w") as f:
+                json.dump([str(n) for n in self.strategy.names()], f)
+
+    def close(self):
+        if self._checkpointer is not None:
+            self._checkpointer.close()
+            self._checkpointer = None
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
