@@ -87,4 +87,4 @@ def test_cpu_offload_adamw_gpu_pipeline():
         flat.zero_grad()
     torch.cuda.synchronize()
     assert torch.allclose(opt.master, master.detach(), atol=1e-6)
-    assert torch.equal(flat.data.cpu(), master.detach().to(torch.bfloat16))
+    assert torch.equal(flat.data.cpu(), opt.master.to(torch.bfloat16))  # H2D of RNE-rounded masters
