@@ -29,6 +29,8 @@ Optimizations (applied in a fixed, dependency-respecting order):
   zero1              ZeroRedundancyOptimizer on top of DDP
   ddp                DistributedDataParallel (default when data parallel > 1)
 
+``load_strategy="search"`` (with ``model_fn=`` and ``sample_batch=``) dry-runs
+candidate strategies and keeps the fastest (``atorch/auto_search.py``).
 ``load_strategy=None`` plans semi-automatically from the model size and the
 GPU memory (288 GB per MI355X): DDP when weights + grads + Adam states fit in
 ~70 % of HBM, otherwise FSDP; bf16 autocast always.  (The reference searches
@@ -366,6 +368,14 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
     """Returns ``(status, AutoAccelerateResult, Strategy)``."""
     dev = _device()
     world = int(os.getenv("WORLD_SIZE", "1")) if not dist.is_initialized() else dist.get_world_size()
+    if isinstance(load_strategy, str) and load_strategy == "search":
+        # dry-run search (atorch/auto_search.py): needs a model factory + a sample batch
+        from .auto_search import search_strategy
+
+        load_strategy, report = search_strategy(kwargs["model_fn"], optim_func, optim_args or {},
+                                                kwargs["sample_batch"], loss_func,
+                                                max_trials=kwargs.get("max_trials"),
+                                                model_input_format=model_input_format)
     strategy = Strategy.from_spec(load_strategy) if load_strategy is not None else plan_strategy(model, world)
     if excluded:
         strategy = Strategy([o for o in strategy.opts if o[0] not in excluded])
