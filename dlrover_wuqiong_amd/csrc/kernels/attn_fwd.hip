@@ -1,49 +1,56 @@
 // Flash attention forward for gfx950 (bf16 in/out, fp32 accumulate).
 //
 // Layout: q [B, S, H, D], k/v [B, S, Hkv, D] (GQA: H % Hkv == 0), o like q,
-// lse [B, H, S] fp32 (natural log), D in {64, 128}.
+// lse [B, H, S] fp32 (natural log), D in {64, 128}; arbitrary batch / row
+// strides (q/k/v may be views into one packed QKV projection).
 //
 // CDNA4 design (cdna_hip_programming.md App. B "fused attention prefill"):
-//  * Swapped product: S^T = K * Q^T with v_mfma_f32_16x16x32_bf16, so the
-//    accumulator puts the QUERY on the lane (col = lane&15) and 4 keys in the
-//    registers.  Row statistics (max / sum over keys) are then in-lane plus
-//    two xor-shuffles across the 4 lane groups — no LDS round trip.
-//  * O^T = V^T * P^T: the P^T accumulator registers ARE the B operand of the
-//    second MFMA (k order permuted identically on both operands), V^T comes
-//    from the row-major V tile via ds_read_b64_tr_b16 (hardware transpose
-//    read, T10) — P never touches LDS.
-//  * K tile read with ds_read_b128 from an XOR-swizzled image (T2) so the 16
-//    lanes of a group (16 different key rows, same d chunk) hit 16 different
-//    16-byte slots.
-//  * Block = 4 waves x 32 queries = 128 queries of one (b, h); K/V tiles of
-//    64 keys staged through LDS by all 256 threads (16-byte loads, register
-//    staged so the global loads of tile t+1 are issued before the MFMAs of
-//    tile t — T14 issue-early / write-late).
-//  * exp2 with the softmax scale folded into log2(e); causal tiles above the
-//    diagonal are skipped entirely.
+//  * 8 waves x 32 query rows = 256 queries per workgroup; K/V tiles of 64
+//    keys double-buffered in LDS (one barrier per tile); every tile is read
+//    from HBM once per 256 queries.
+//  * v_mfma_f32_32x32x16_bf16 with the swapped product S^T = K * Q^T: the
+//    accumulator puts the QUERY on the lane (col = lane & 31) and 16 keys in
+//    the registers, so the row max / sum are in-lane over 32 values plus ONE
+//    exchange with lane ^ 32 for the max (the sum stays a per-half partial
+//    until the epilogue).
+//  * O^T += V^T * P^T: the S^T accumulator registers, packed pairwise to
+//    bf16, ARE the B operand of the second MFMA ("an accumulator tile as the
+//    next MFMA's operand", guide §3): P never touches LDS.  The V^T operand
+//    comes from the row-major V tile via ds_read_b64_tr_b16 (T10), two reads
+//    per 16-key k-step.
+//  * One LDS image per tile in the "8-row x 32-column subtile" layout of
+//    guide T10 (a): conflict-free for the K row reads (ds_read_b128, A
+//    operand of S^T) and the V transposed reads.
+//  * Register-staged global loads issued one tile ahead (T14 issue-early /
+//    write-late); exp2 with the softmax scale folded into log2(e); causal:
+//    tiles above a wave's diagonal are skipped by that wave, the longest
+//    query blocks are dispatched first.
 #include "dw_common.h"
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 
 template <int D>
-struct AttnCfg {
-  static constexpr int BQ = 128;           // queries per block
-  static constexpr int BK = 64;            // keys per tile
-  static constexpr int NCH = D / 8;        // 16-byte chunks per row
-  static constexpr int KSTEPS = D / 32;    // MFMA k-steps over head dim
-  static constexpr int DT = D / 16;        // 16-wide d tiles of O^T
-  static constexpr int TILE_BYTES = BK * D * 2;
-  static constexpr int VEC_PER_THREAD = BK * NCH / 256;  // 16B vectors per thread per tile
+struct Fwd2Cfg {
+  // D=128: 8 waves share each K/V tile (MFMA-bound, maximise reuse);
+  // D=64: softmax (VALU) bound -> 4-wave blocks, 3 blocks per CU
+  static constexpr int WAVES = D == 128 ? 8 : 4;
+  static constexpr int BQ = 32 * WAVES;  // queries per block
+  static constexpr int BK = 64;          // keys per tile
+  static constexpr int NCH = D / 8;      // 16-byte chunks per row
+  static constexpr int KK = D / 16;      // MFMA k-steps over the head dim
+  static constexpr int DT = D / 32;      // 32-wide d tiles of O^T
+  static constexpr int TILE = BK * D * 2;
+  static constexpr int VPT = BK * NCH / (64 * WAVES);  // staged 16-B vectors per thread per tensor
 };
 
-// byte offset of 16-byte chunk `c` of row `r` in a swizzled [rows][D] tile
+// byte offset of 16-byte chunk `ch` of row `row` (guide T10 layout (a))
 template <int D>
-__device__ __forceinline__ int swz(int r, int c) {
-  constexpr int NCH = D / 8;
-  return (r * NCH + (c ^ (r & (NCH - 1)))) * 16;
+__device__ __forceinline__ int img_off(int row, int ch) {
+  return (D * 16) * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
 }
 
 __device__ __forceinline__ bf16x8_t as_bf16x8(const u32x4& v) { return __builtin_bit_cast(bf16x8_t, v); }
@@ -52,196 +59,190 @@ __device__ __forceinline__ unsigned int pack2(float a, float b) {
   return (unsigned int)f2bf(a) | ((unsigned int)f2bf(b) << 16);
 }
 
+__device__ __forceinline__ unsigned int pack_s16(short a, short b) {
+  return (unsigned int)(unsigned short)a | ((unsigned int)(unsigned short)b << 16);
+}
+
 template <int D, bool CAUSAL>
-__global__ void __launch_bounds__(256, (D <= 64 ? 2 : 1))
+__global__ void __launch_bounds__(64 * Fwd2Cfg<D>::WAVES, 1)
 attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
                 bf16_t* __restrict__ O, float* __restrict__ LSE, int S, int H, int HKV, float scale_log2,
                 AttnStrides st) {
-  using C = AttnCfg<D>;
+  using C = Fwd2Cfg<D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* k_lds = smem;
-  char* v_lds = smem + C::TILE_BYTES;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int g = lane >> 4, li = lane & 15;
+  const int r = lane & 31, hh = lane >> 5;
   const int b = blockIdx.z, h = blockIdx.y;
   const int hk = h / (H / HKV);
-  // causal: the longest (last) query blocks are dispatched first so the
-  // short ones fill in the tail of the grid
   const int qblk = CAUSAL ? (int)(gridDim.x - 1 - blockIdx.x) : (int)blockIdx.x;
   const int q_blk0 = qblk * C::BQ;
   const int q0 = q_blk0 + wid * 32;
-  const int64_t q_rs = st.q_rs, k_rs = st.k_rs, v_rs = st.v_rs;
   const bf16_t* Qb = Q + (int64_t)b * st.q_bs + (int64_t)h * D;
   const bf16_t* Kb = K + (int64_t)b * st.k_bs + (int64_t)hk * D;
   const bf16_t* Vb = V + (int64_t)b * st.v_bs + (int64_t)hk * D;
 
-  // ---- Q fragments (B operand): lane holds Q[q0+16qt+li][32kk + 8g .. +7]
-  u32x4 qf[2][C::KSTEPS];
+  // ---- Q fragments (B operand of S^T): lane holds Q[q0 + r][16 kk + 8 hh .. +7]
+  u32x4 qf[C::KK];
+  {
+    const int q = q0 + r;
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int q = q0 + 16 * qt + li;
-#pragma unroll
-    for (int kk = 0; kk < C::KSTEPS; ++kk) {
-      if (q < S) qf[qt][kk] = *(const u32x4*)(Qb + (int64_t)q * q_rs + 32 * kk + 8 * g);
-      else qf[qt][kk] = (u32x4){0, 0, 0, 0};
-    }
+    for (int kk = 0; kk < C::KK; ++kk)
+      qf[kk] = (q < S) ? *(const u32x4*)(Qb + (int64_t)q * st.q_rs + 16 * kk + 8 * hh) : (u32x4){0, 0, 0, 0};
   }
 
-  f32x4 o[C::DT][2];
+  f32x16 o[C::DT];
 #pragma unroll
   for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) o[dt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float m_i[2] = {-INFINITY, -INFINITY}, l_i[2] = {0.f, 0.f};
+    for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
+  float m_i = -INFINITY, l_i = 0.f;  // l_i: this lane-half's partial row sum
 
   int n_tiles = (S + C::BK - 1) / C::BK;
-  if (CAUSAL) {
-    const int last_q = min(S - 1, q_blk0 + C::BQ - 1);
-    n_tiles = min(n_tiles, last_q / C::BK + 1);
-  }
+  if (CAUSAL) n_tiles = min(n_tiles, min(S - 1, q_blk0 + C::BQ - 1) / C::BK + 1);
 
-  // register staging of the next K/V tile (T14)
-  u32x4 kst[C::VEC_PER_THREAD], vst[C::VEC_PER_THREAD];
+  u32x4 kst[C::VPT], vst[C::VPT];
   auto issue_load = [&](int t) {
 #pragma unroll
-    for (int i = 0; i < C::VEC_PER_THREAD; ++i) {
-      const int v = tid + 256 * i;
-      const int r = v / C::NCH, c = v % C::NCH;
-      const int key = t * C::BK + r;
+    for (int i = 0; i < C::VPT; ++i) {
+      const int v = tid + 64 * C::WAVES * i;
+      const int row = v / C::NCH, c = v % C::NCH;
+      const int key = t * C::BK + row;
       if (key < S) {
-        kst[i] = *(const u32x4*)(Kb + (int64_t)key * k_rs + c * 8);
-        vst[i] = *(const u32x4*)(Vb + (int64_t)key * v_rs + c * 8);
+        kst[i] = *(const u32x4*)(Kb + (int64_t)key * st.k_rs + c * 8);
+        vst[i] = *(const u32x4*)(Vb + (int64_t)key * st.v_rs + c * 8);
       } else {
         kst[i] = (u32x4){0, 0, 0, 0};
         vst[i] = (u32x4){0, 0, 0, 0};
       }
     }
   };
-  auto write_lds = [&]() {
+  auto write_lds = [&](int buf) {
+    char* kl = smem + buf * 2 * C::TILE;
+    char* vl = kl + C::TILE;
 #pragma unroll
-    for (int i = 0; i < C::VEC_PER_THREAD; ++i) {
-      const int v = tid + 256 * i;
-      const int r = v / C::NCH, c = v % C::NCH;
-      *(u32x4*)(k_lds + swz<D>(r, c)) = kst[i];
-      *(u32x4*)(v_lds + swz<D>(r, c)) = vst[i];
+    for (int i = 0; i < C::VPT; ++i) {
+      const int v = tid + 64 * C::WAVES * i;
+      const int row = v / C::NCH, c = v % C::NCH;
+      *(u32x4*)(kl + img_off<D>(row, c)) = kst[i];
+      *(u32x4*)(vl + img_off<D>(row, c)) = vst[i];
     }
   };
 
   issue_load(0);
+  write_lds(0);
+  if (n_tiles > 1) issue_load(1);
+  __syncthreads();
+
+  const int g4 = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+
   for (int t = 0; t < n_tiles; ++t) {
-    __syncthreads();  // previous tile fully consumed
-    write_lds();
-    __syncthreads();
-    if (t + 1 < n_tiles) issue_load(t + 1);  // in flight during this tile's math
     const int k0 = t * C::BK;
-
-    // ---- S^T = K Q^T : acc[i][qt], key tile i (16 keys), query tile qt
-    f32x4 s[4][2];
+    const char* kl = smem + (t & 1) * 2 * C::TILE;
+    const char* vl = kl + C::TILE;
+    // a wave whose 32 queries all lie before this tile has nothing to do here
+    const bool active = !CAUSAL || (k0 <= q0 + 31);
+    if (active) {
+      // ---- S^T = K Q^T : two 32-key subtiles
+      f32x16 s[2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int sb = 0; sb < 2; ++sb) {
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) s[i][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < 16; ++i) s[sb][i] = 0.f;
 #pragma unroll
-    for (int kk = 0; kk < C::KSTEPS; ++kk) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const u32x4 kf = *(const u32x4*)(k_lds + swz<D>(16 * i + li, 4 * kk + g));
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
-          s[i][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(kf), as_bf16x8(qf[qt][kk]), s[i][qt], 0, 0, 0);
+        for (int kk = 0; kk < C::KK; ++kk) {
+          const u32x4 kf = *(const u32x4*)(kl + img_off<D>(32 * sb + r, 2 * kk + hh));
+          s[sb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf), as_bf16x8(qf[kk]), s[sb], 0, 0, 0);
+        }
       }
-    }
 
-    // ---- online softmax (query on the lane)
-    const bool need_mask = (k0 + C::BK > S) || (CAUSAL && (k0 + C::BK - 1 > q0));
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const int q = q0 + 16 * qt + li;
+      // ---- online softmax: lane = query q0 + r, its 32 keys in registers.
+      // The max runs on the raw scores (scale > 0) and the scale is folded
+      // into the exponent's FMA: p = exp2(s * c - m * c).
+      const int q = q0 + r;
+      const bool need_mask = (k0 + C::BK > S) || (CAUSAL && (k0 + C::BK - 1 > q0));
       float mx = -INFINITY;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float x = s[i][qt][r] * scale_log2;
+        for (int i = 0; i < 16; ++i) {
           if (need_mask) {
-            const int key = k0 + 16 * i + 4 * g + r;
-            if (key >= S || (CAUSAL && key > q)) x = -INFINITY;
+            const int key = k0 + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            if (key >= S || (CAUSAL && key > q)) s[sb][i] = -INFINITY;
           }
-          s[i][qt][r] = x;
-          mx = fmaxf(mx, x);
+          mx = fmaxf(mx, s[sb][i]);
         }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_i[qt], mx);
-      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-      const float alpha = exp2f(m_i[qt] - m_use);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;
+      if (!__all(mx <= m_i)) {
+        // some row's max grew: rescale O and l (exact; skipped otherwise)
+        const float m_new = fmaxf(m_i, mx);
+        const float alpha = (m_new == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m_i - m_new);
+        m_i = m_new;
+        l_i *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+      }
+      const float m_use = (m_i == -INFINITY) ? 0.f : m_i;
       float rs = 0.f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(s[i][qt][r] - m_use);
-          s[i][qt][r] = p;
+        for (int i = 0; i < 16; ++i) {
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[sb][i], scale_log2, -m_use));
+          s[sb][i] = p;
           rs += p;
         }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
-      l_i[qt] = l_i[qt] * alpha + rs;
-      m_i[qt] = m_new;
-#pragma unroll
-      for (int dt = 0; dt < C::DT; ++dt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[dt][qt][r] *= alpha;
-    }
+      l_i += rs;
 
-    // ---- O^T += V^T P^T   (2 k-steps of 32 keys)
+      // ---- O^T += V^T P^T : 4 k-steps of 16 keys
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      u32x4 pf[2];
+      for (int sb = 0; sb < 2; ++sb) {
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        const f32x4 a = s[2 * ks][qt], c2 = s[2 * ks + 1][qt];
-        pf[qt] = (u32x4){pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(c2[0], c2[1]), pack2(c2[2], c2[3])};
-      }
-      const int qrow = li >> 2, p = li & 3;
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const f32x16& a = s[sb];
+          const u32x4 pf = {pack2(a[8 * s2 + 0], a[8 * s2 + 1]), pack2(a[8 * s2 + 2], a[8 * s2 + 3]),
+                            pack2(a[8 * s2 + 4], a[8 * s2 + 5]), pack2(a[8 * s2 + 6], a[8 * s2 + 7])};
+          const int kb = 32 * sb + 16 * s2 + 4 * hh + tq;  // key row this lane addresses
 #pragma unroll
-      for (int dt = 0; dt < C::DT; ++dt) {
-        const int col = 16 * dt + 4 * p;  // element column
-        const int r0 = 32 * ks + 4 * g + qrow, r1 = r0 + 16;
-        const int off0 = swz<D>(r0, col >> 3) + (col & 7) * 2;
-        const int off1 = swz<D>(r1, col >> 3) + (col & 7) * 2;
-        const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)LDS_PTR(v_lds + off0));
-        const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)LDS_PTR(v_lds + off1));
-        u32x4 vf;
-        vf[0] = (unsigned short)v0[0] | ((unsigned int)(unsigned short)v0[1] << 16);
-        vf[1] = (unsigned short)v0[2] | ((unsigned int)(unsigned short)v0[3] << 16);
-        vf[2] = (unsigned short)v1[0] | ((unsigned int)(unsigned short)v1[1] << 16);
-        vf[3] = (unsigned short)v1[2] | ((unsigned int)(unsigned short)v1[3] << 16);
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
-          o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(vf), as_bf16x8(pf[qt]), o[dt][qt], 0, 0, 0);
+          for (int dt = 0; dt < C::DT; ++dt) {
+            const int ch = (32 * dt + 16 * (g4 & 1)) / 8 + (tp >> 1);
+            const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s16x4*)LDS_PTR(vl + img_off<D>(kb, ch) + 8 * (tp & 1)));
+            const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s16x4*)LDS_PTR(vl + img_off<D>(kb + 8, ch) + 8 * (tp & 1)));
+            const u32x4 vf = {pack_s16(v0[0], v0[1]), pack_s16(v0[2], v0[3]), pack_s16(v1[0], v1[1]),
+                              pack_s16(v1[2], v1[3])};
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(vf), as_bf16x8(pf), o[dt], 0, 0, 0);
+          }
+        }
       }
     }
+    if (t + 1 < n_tiles) {
+      write_lds((t + 1) & 1);
+      if (t + 2 < n_tiles) issue_load(t + 2);
+    }
+    __syncthreads();
   }
 
   // ---- epilogue: O = O^T / l ; lse
-  bf16_t* Ob = O + (int64_t)b * st.o_bs + (int64_t)h * D;
+  const float l_tot = l_i + __shfl_xor(l_i, 32, 64);
+  const int q = q0 + r;
+  if (q < S) {
+    bf16_t* Oq = O + (int64_t)b * st.o_bs + (int64_t)h * D + (int64_t)q * st.o_rs;
+    const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int q = q0 + 16 * qt + li;
-    if (q >= S) continue;
-    const float inv = l_i[qt] > 0.f ? 1.f / l_i[qt] : 0.f;
+    for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
-    for (int dt = 0; dt < C::DT; ++dt) {
-      const f32x4 a = o[dt][qt];
-      uint2 w;
-      w.x = pack2(a[0] * inv, a[1] * inv);
-      w.y = pack2(a[2] * inv, a[3] * inv);
-      *(uint2*)(Ob + (int64_t)q * st.o_rs + 16 * dt + 4 * g) = w;
-    }
-    if (g == 0 && LSE) {
-      const float lse = (l_i[qt] > 0.f) ? (m_i[qt] + log2f(l_i[qt])) * 0.6931471805599453f : -INFINITY;
+      for (int g = 0; g < 4; ++g) {
+        uint2 w;
+        w.x = pack2(o[dt][4 * g + 0] * inv, o[dt][4 * g + 1] * inv);
+        w.y = pack2(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
+        *(uint2*)(Oq + 32 * dt + 8 * g + 4 * hh) = w;
+      }
+    if (hh == 0 && LSE) {
+      const float lse = (l_tot > 0.f) ? (m_i + log2f(l_tot)) * 0.6931471805599453f : -INFINITY;
       LSE[((int64_t)b * H + h) * S + q] = lse;
     }
   }
@@ -250,8 +251,9 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
 template <int D>
 static void launch_fwd(const void* q, const void* k, const void* v, void* o, void* lse, int B, int S, int H, int HKV,
                        int causal, float scale_log2, const AttnStrides& st, hipStream_t s) {
-  dim3 grid((S + AttnCfg<D>::BQ - 1) / AttnCfg<D>::BQ, H, B), block(256);
-  const int lds = 2 * AttnCfg<D>::TILE_BYTES;
+  using C = Fwd2Cfg<D>;
+  dim3 grid((S + C::BQ - 1) / C::BQ, H, B), block(64 * C::WAVES);
+  const int lds = 4 * C::TILE;
   if (causal)
     hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
                        (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st);

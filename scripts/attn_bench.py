@@ -42,9 +42,23 @@ def main():
         tf = t(f)
         tb = t(lambda: torch.autograd.grad(o, ins, do, retain_graph=True))
         fl = 4 * B * H * S * S * D / 2
+        # torch SDPA (ROCm flash backend) on the same problem, [B, H, S, D] layout
+        qs = torch.randn(B, H, S, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+        ks = torch.randn(B, H, S, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+        vs = torch.randn(B, H, S, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
+        fs = lambda: torch.nn.functional.scaled_dot_product_attention(qs, ks, vs, is_causal=True)  # noqa: E731
+        try:
+            os_ = fs()
+            dos = torch.randn_like(os_)
+            sf = t(fs)
+            sb = t(lambda: torch.autograd.grad(os_, [qs, ks, vs], dos, retain_graph=True))
+        except Exception:
+            sf = sb = float("nan")
         print(json.dumps({"B": B, "S": S, "H": H, "HKV": HKV, "D": D, "packed": packed, "fwd_us": round(tf * 1e3, 1),
                           "bwd_us": round(tb * 1e3, 1), "fwd_tflops": round(fl / tf / 1e9, 1),
-                          "bwd_tflops": round(2.5 * fl / tb / 1e9, 1)}), flush=True)
+                          "bwd_tflops": round(2.5 * fl / tb / 1e9, 1),
+                          "sdpa_fwd_tflops": round(fl / sf / 1e9, 1), "sdpa_bwd_tflops": round(2.5 * fl / sb / 1e9, 1)}),
+              flush=True)
 
 
 if __name__ == "__main__":
