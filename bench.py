@@ -58,6 +58,8 @@ def parse():
     p.add_argument("--ckpt-interval", type=int, default=4)
     p.add_argument("--ckpt-dir", default="/tmp/dwamd_bench_ckpt")
     p.add_argument("--no-fault", action="store_true")
+    p.add_argument("--lr", type=float, default=1e-4)
+    p.add_argument("--act-ckpt", action="store_true", help="activation checkpointing (Llama configs)")
     return p.parse_args()
 
 
@@ -107,15 +109,29 @@ def main():
     from dlrover_wuqiong_amd.parallel.flat import FlatParams
 
     dtype = torch.bfloat16 if cuda else torch.float32
-    cfg = GPT2Config.named(args.model)
-    cfg.n_positions = max(cfg.n_positions, args.seq)
     torch.manual_seed(1234)
-    with torch.device(device):
-        model = GPT2(cfg)
+    if args.model.startswith("llama") or args.model.startswith("mixtral"):
+        # secondary configs (BASELINE.json "Llama-3 8B ... async ckpt"): same
+        # flat-buffer DDP + fused optimizer + flash checkpoint path
+        from dlrover_wuqiong_amd.models.llama import Llama, LlamaConfig
+
+        cfg = LlamaConfig.named(args.model)
+        cfg.activation_checkpointing = args.act_ckpt
+        with torch.device(device):
+            model = Llama(cfg)
+        desc = (f"{args.model} ({cfg.num_hidden_layers}L, {cfg.hidden_size}H, {cfg.num_attention_heads}/"
+                f"{cfg.num_key_value_heads} heads)")
+    else:
+        cfg = GPT2Config.named(args.model)
+        cfg.n_positions = max(cfg.n_positions, args.seq)
+        with torch.device(device):
+            model = GPT2(cfg)
+        desc = ("GPT2-1.5B (gpt2-xl: 48L, 1600H, 25 heads)" if args.model == "gpt2-1.5b" else
+                f"{args.model} ({cfg.n_layer}L, {cfg.n_embd}H, {cfg.n_head} heads)")
     model.to(dtype)
     nparams = model.num_params()
     flat = FlatParams(model, dtype=dtype, device=device)
-    opt = FusedAdamW(flat, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0)
+    opt = FusedAdamW(flat, lr=args.lr, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0)
     ddp = FlatDDP(model, flat, bucket_mb=128)
     opt.grad_scale = 1.0 / max(1, world)
     log(f"model {args.model}: {nparams/1e9:.3f} B params, world {world}, device {device}")
@@ -159,12 +175,13 @@ def main():
     sync_all(device)
 
     # ---------------- timed: train + flash checkpoint every ckpt_interval steps
-    save_times, step_times = [], []
+    save_times, step_times, losses = [], [], []
     sync_all(device)
     t_start = time.perf_counter()
     for i in range(args.steps):
         ts = time.perf_counter()
         loss = train_step()
+        losses.append(loss.detach())
         if cuda:
             # compute-stream sync only: a device-wide sync would also wait for
             # the checkpoint flush running on its own stream
@@ -177,6 +194,7 @@ def main():
     sync_all(device)
     t_timed = time.perf_counter() - t_start
     log("step ms:", [round(1000 * x, 1) for x in step_times], "save ms:", [round(1000 * x, 1) for x in save_times])
+    log("losses:", [round(float(x), 4) for x in losses])
     t_timed = max_over_ranks(t_timed, device)
     save_sec = max_over_ranks(statistics.mean(save_times) if save_times else 0.0, device)
     save_max = max_over_ranks(max(save_times) if save_times else 0.0, device)
@@ -255,17 +273,16 @@ def main():
         "ms_per_step": round(1000.0 * t_timed / args.steps, 2),
         "higher_is_better": False,
         "scaling": "strong",
-        "vs_baseline": round(save_sec / REF_SAVE_SEC, 4),
+        "vs_baseline": round(save_sec / REF_SAVE_SEC, 4) if args.model == "gpt2-1.5b" else None,
         "dtype": "bf16" if cuda else "fp32",
         "data": "synthetic tokens, random-init weights",
-        "config": {"model": ("GPT2-1.5B (gpt2-xl: 48L, 1600H, 25 heads)" if args.model == "gpt2-1.5b" else
-                             f"{args.model} ({cfg.n_layer}L, {cfg.n_embd}H, {cfg.n_head} heads)"),
+        "config": {"model": desc,
                    "global_batch": B * world,
                    "seq_len": S, "parallelism": f"dp{world}"},
         "save_sec_mean": round(save_sec, 4),
         "save_sec_max": round(save_max, 4),
         "load_sec": round(load_sec, 4),
-        "load_vs_baseline": round(load_sec / REF_LOAD_SEC, 4),
+        "load_vs_baseline": round(load_sec / REF_LOAD_SEC, 4) if args.model == "gpt2-1.5b" else None,
         "load_verified": load_ok,
         "recover_sec": round(recover_sec, 3),
         "goodput_pct": round(goodput, 2) if goodput is not None else None,
