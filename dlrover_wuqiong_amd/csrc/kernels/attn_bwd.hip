@@ -89,11 +89,10 @@ attn_bwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   constexpr int BKB = 128;     // keys per block
   constexpr int QI = 32;       // queries per iteration
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* k_lds = smem;                         // [128][D]
-  char* q_lds = k_lds + BKB * D * 2;          // [32][D]
-  char* do_lds = q_lds + QI * D * 2;          // [32][D]
-  char* ds_lds = do_lds + QI * D * 2;         // [32][128]
-  float* stat_lds = (float*)(ds_lds + QI * BKB * 2);  // lse_log2[32], delta[32]
+  char* k_lds = smem;                              // [128][D]
+  char* ds_lds = k_lds + BKB * D * 2;              // [32][128]
+  char* qbuf = ds_lds + QI * BKB * 2;              // 2 x {Q [32][D], dO [32][D], lse_log2[32], delta[32]}
+  constexpr int QBUF = 2 * QI * D * 2 + 2 * QI * 4;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -139,34 +138,71 @@ attn_bwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
     }
 
   const int q_start = CAUSAL ? (kb0 / QI) * QI : 0;
-  for (int hh = 0; hh < group; ++hh) {
-    const int h = hk * group + hh;
+  const int nq = (S - q_start + QI - 1) / QI;  // query slices per head
+  const int n_it = group * nq;
+  // Software pipeline over (head, query slice): the Q / dO rows, LSE and
+  // delta of slice i+1 are loaded into registers while slice i computes and
+  // written to the other LDS buffer after its dQ pass (T14 issue-early /
+  // write-late): HBM latency stays off the critical path even at one wave
+  // per SIMD.  Two barriers per slice.
+  constexpr int LV = QI * NCH / 256;  // 16-byte vectors per thread per tensor
+  u32x4 q_st[LV], do_st[LV];
+  float lse_st = INFINITY, del_st = 0.f;
+  auto issue_slice = [&](int it) {
+    const int h = hk * group + it / nq;
+    const int qb = q_start + (it % nq) * QI;
     const bf16_t* Qb = Q + (int64_t)b * st.q_bs + (int64_t)h * D;
     const bf16_t* dOb = dO + (int64_t)b * st.do_bs + (int64_t)h * D;
-    const float* lse_b = LSE + ((int64_t)b * H + h) * S;
-    const float* del_b = DELTA + ((int64_t)b * H + h) * S;
+#pragma unroll
+    for (int i = 0; i < LV; ++i) {
+      const int v = tid + 256 * i;
+      const int r = v / NCH, c = v % NCH;
+      const int q = qb + r;
+      if (q < S) {
+        q_st[i] = *(const u32x4*)(Qb + (int64_t)q * st.q_rs + c * 8);
+        do_st[i] = *(const u32x4*)(dOb + (int64_t)q * st.do_rs + c * 8);
+      } else {
+        q_st[i] = (u32x4){0, 0, 0, 0};
+        do_st[i] = (u32x4){0, 0, 0, 0};
+      }
+    }
+    if (tid < QI) {
+      const int q = qb + tid;
+      const int64_t off = ((int64_t)b * H + h) * S + q;
+      lse_st = q < S ? LSE[off] * 1.4426950408889634f : INFINITY;
+      del_st = q < S ? DELTA[off] : 0.f;
+    }
+  };
+  auto write_slice = [&](int buf) {
+    char* ql = qbuf + buf * QBUF;
+    char* dl = ql + QI * D * 2;
+    float* stl = (float*)(dl + QI * D * 2);
+#pragma unroll
+    for (int i = 0; i < LV; ++i) {
+      const int v = tid + 256 * i;
+      const int r = v / NCH, c = v % NCH;
+      *(u32x4*)(ql + swzb<D>(r, c)) = q_st[i];
+      *(u32x4*)(dl + swzb<D>(r, c)) = do_st[i];
+    }
+    if (tid < QI) {
+      stl[tid] = lse_st;
+      stl[QI + tid] = del_st;
+    }
+  };
+  if (n_it > 0) {
+    issue_slice(0);
+    write_slice(0);
+  }
+  __syncthreads();  // K block + first slice visible
+  for (int it = 0; it < n_it; ++it) {
+    const int h = hk * group + it / nq;
+    const int qb = q_start + (it % nq) * QI;
     float* dQb = dQacc + (int64_t)b * S * q_acc_rs + (int64_t)h * D;
-
-    for (int qb = q_start; qb < S; qb += QI) {
-      __syncthreads();  // previous iteration's LDS reads done
-      for (int v = tid; v < QI * NCH; v += 256) {
-        const int r = v / NCH, c = v % NCH;
-        const int q = qb + r;
-        u32x4 x = (u32x4){0, 0, 0, 0}, y = (u32x4){0, 0, 0, 0};
-        if (q < S) {
-          x = *(const u32x4*)(Qb + (int64_t)q * st.q_rs + c * 8);
-          y = *(const u32x4*)(dOb + (int64_t)q * st.do_rs + c * 8);
-        }
-        *(u32x4*)(q_lds + swzb<D>(r, c)) = x;
-        *(u32x4*)(do_lds + swzb<D>(r, c)) = y;
-      }
-      if (tid < QI) {
-        const int q = qb + tid;
-        stat_lds[tid] = q < S ? lse_b[q] * 1.4426950408889634f : INFINITY;
-        stat_lds[QI + tid] = q < S ? del_b[q] : 0.f;
-      }
-      __syncthreads();
-
+    const char* q_lds = qbuf + (it & 1) * QBUF;
+    const char* do_lds = q_lds + QI * D * 2;
+    const float* stat_lds = (const float*)(do_lds + QI * D * 2);
+    if (it + 1 < n_it) issue_slice(it + 1);
+    {
       // S = Q K^T and dP = dO V^T : [qt][kt], lane holds [q = 4g + r][key = li]
       f32x4 s[2][2], dp[2][2];
 #pragma unroll
@@ -281,6 +317,10 @@ attn_bwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
           }
       }
     }
+    // next slice -> the other buffer (last read in iteration it-1, which every
+    // wave finished before the dS barrier above); dS / this buffer free after
+    if (it + 1 < n_it) write_slice((it + 1) & 1);
+    __syncthreads();
   }
   // write dK, dV: lane holds [d = 16dt + 4g + r][key = kw0 + 16kt + li]
   bf16_t* dKb = dK + (int64_t)b * st.dk_bs + (int64_t)hk * D;
@@ -333,7 +373,7 @@ extern "C" int64_t dw_attn_bwd_workspace(int B, int S, int H, int D) {
 
 template <int D>
 static size_t bwd_lds_bytes() {
-  return 128 * D * 2 + 2 * 32 * D * 2 + 32 * 128 * 2 + 64 * 4;
+  return 128 * D * 2 + 32 * 128 * 2 + 2 * (2 * 32 * D * 2 + 2 * 32 * 4);
 }
 
 template <int D>
