@@ -14,8 +14,8 @@ distributed, mixed-precision, memory-optimised training setup.
 Optimizations (applied in a fixed, dependency-respecting order):
   parallel_mode      named groups ``[("data", n)]`` or mixed ``[("tensor", t),
                      ("sequence", s), ("data", d)]`` (``atorch/distributed.py``)
-  module_replace     nn.LayerNorm / RMSNorm -> fused HIP norms; HF-style attention
-                     stays on torch SDPA (hipBLASLt / AOTriton)
+  module_replace     nn.LayerNorm / RMSNorm -> fused HIP norms; transformers models'
+                     attention -> the MFMA flash-attention kernels (``hf_attention.py``)
   half               parameters in bf16 (fused optimizers keep fp32 masters)
   amp_native         autocast (bf16 default on MI355X; fp16 adds a GradScaler)
   tensor_parallel    DTensor TP plan inferred from Llama/GPT-style layer names
@@ -181,8 +181,12 @@ def _replace_norms(model: nn.Module):
 
 
 def _apply_module_replace(ctx, cfg):
+    from .hf_attention import enable_dwamd_attention
+
     n = _replace_norms(ctx["model"])
-    logger.info(f"module_replace: {n} norm layers -> fused HIP norms")
+    hf = enable_dwamd_attention(ctx["model"])
+    logger.info(f"module_replace: {n} norm layers -> fused HIP norms"
+                + ("; HF attention -> MFMA flash attention" if hf else ""))
 
 
 def _apply_half(ctx, cfg):
