@@ -1,50 +1,54 @@
 // Flash attention backward for gfx950 (bf16 in/out, fp32 accumulate).
 //
-// Recompute P from Q, K and the forward's LSE; five MFMA products per tile
-// (S = Q K^T, dP = dO V^T, dV^T += dO^T P, dK^T += Q^T dS, dQ += dS K).
+// Recompute P from Q, K and the forward's LSE (per query row); with
+// delta = rowsum(dO * O) and dS = P * (dP - delta):
+//   dV = P^T dO,  dK = scale * dS^T Q,  dQ = scale * dS K.
 //
-// Structure (cdna_hip_programming.md App. B "Attention backward"):
-//  * one block = 4 waves = 128 keys of one (batch, kv-head); each wave owns
-//    32 keys and keeps dK^T, dV^T for them in registers while the block
-//    sweeps every query head of the GQA group x 32-query slices, so dK/dV
-//    need no cross-block sum (written once, bf16).
-//  * KEY on the lane: S and dP accumulators (query in registers, key on the
-//    lane) are directly the B operands of dV^T and dK^T (query order permuted
-//    identically on both operands); dO^T and Q^T come from LDS with the
-//    ds_read_b64_tr_b16 transpose read.  K/V fragments of the wave's keys
-//    stay in registers for the whole sweep.
-//  * only dS crosses LDS (once), for dQ = dS K; dQ partial tiles are summed
-//    across key blocks with fp32 atomics into a workspace (atomic bytes per
-//    FLOP sized per Guideline 12), converted to bf16 by a final pass.
-//  * softmax scale folded into dS; causal slices fully below the diagonal
-//    are skipped.
-#include "dw_common.h"
+// Split into two atomic-free kernels built on v_mfma_f32_32x32x16_bf16
+// (cdna_hip_programming.md App. B "Attention backward"; why split: the fused
+// form sums dQ across key blocks with float atomics, which at S = 4096 cost
+// ~40 % of its time against the 1.3 TB/s chip-wide atomic rate):
+//  * attn_bwd_dkdv_kernel -- key-major: each wave owns 32 keys ON THE MFMA
+//    LANE; S = Q K^T and dP = dO V^T (K, V fragments of the wave's keys stay
+//    in registers) put queries in the accumulator registers, so P and dS,
+//    packed pairwise to bf16, ARE the B operands of dV^T += dO^T P and
+//    dK^T += Q^T dS ("accumulator as the next MFMA's operand", guide §3);
+//    dO^T / Q^T come from ds_read_b64_tr_b16 of the same LDS images the row
+//    reads use (T10 (a)).  Q / dO / LSE / delta tiles of 64 queries are
+//    register-staged one tile ahead into double-buffered LDS (T14), one
+//    barrier per tile.  One query head per workgroup (grid.y = H): GQA
+//    groups write fp32 partials that a tiny pass sums per kv head, so every
+//    (b, head, key block) is an independent workgroup (fills 256 CUs even at
+//    batch 1).
+//  * attn_bwd_dq_kernel -- query-major twin of the forward kernel: dQ summed
+//    in registers and written once in bf16.
+// Softmax scale folded into the exponent FMA and applied to dK / dQ in the
+// epilogues; causal tiles wholly above a wave's diagonal are skipped.
+#include "attn_common.h"
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 
-template <int D>
-__device__ __forceinline__ int swzb(int r, int c) {  // byte offset of chunk c of row r
-  constexpr int NCH = D / 8;
-  return (r * NCH + (c ^ (r & (NCH - 1)))) * 16;
-}
-// dS tile: [32 q][128 keys] bf16, rows of 256 B (16 chunks)
-__device__ __forceinline__ int swz_ds(int r, int c) { return (r * 16 + (c ^ (r & 15))) * 16; }
-
 __device__ __forceinline__ bf16x8_t as_bf(const u32x4& v) { return __builtin_bit_cast(bf16x8_t, v); }
 __device__ __forceinline__ unsigned int pk2(float a, float b) {
   return (unsigned int)f2bf(a) | ((unsigned int)f2bf(b) << 16);
 }
-__device__ __forceinline__ u32x4 tr_pair(const char* base, int off0, int off1) {
-  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)LDS_PTR(base + off0));
-  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)LDS_PTR(base + off1));
-  u32x4 v;
-  v[0] = (unsigned short)a[0] | ((unsigned int)(unsigned short)a[1] << 16);
-  v[1] = (unsigned short)a[2] | ((unsigned int)(unsigned short)a[3] << 16);
-  v[2] = (unsigned short)b[0] | ((unsigned int)(unsigned short)b[1] << 16);
-  v[3] = (unsigned short)b[2] | ((unsigned int)(unsigned short)b[3] << 16);
-  return v;
+
+// A operand of a 32x32x16 MFMA that sums over 16 rows of a row-major LDS
+// image (rows r0 .. r0+15, columns d0 .. d0+31): element j of lane half h is
+// row r0 + 8(j>>2) + 4h + (j&3), matching the k order of a packed 32x32
+// accumulator used as the B operand.  Two ds_read_b64_tr_b16 per fragment.
+template <int D>
+__device__ __forceinline__ u32x4 tr_frag(const char* img, int r0, int d0, int lane) {
+  const int g4 = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3, h = lane >> 5;
+  const int row = r0 + 4 * h + tq;
+  const int ch = (d0 + 16 * (g4 & 1)) / 8 + (tp >> 1);
+  const s16x4 v0 =
+      __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)LDS_PTR(img + img_off<D>(row, ch) + 8 * (tp & 1)));
+  const s16x4 v1 =
+      __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)LDS_PTR(img + img_off<D>(row + 8, ch) + 8 * (tp & 1)));
+  return (u32x4){pack_s16(v0[0], v0[1]), pack_s16(v0[2], v0[3]), pack_s16(v1[0], v1[1]), pack_s16(v1[2], v1[3])};
 }
 
 // delta[b,h,q] = sum_d dO*O.  D/8 lanes per (b, s, h) row (16-byte loads),
@@ -77,87 +81,84 @@ __global__ void __launch_bounds__(256) attn_bwd_pre_kernel(const bf16_t* __restr
   if (ok && c == 0) delta[((int64_t)b * H + h) * S + s] = acc;
 }
 
-template <int D, bool CAUSAL>
-__global__ void __launch_bounds__(256, (D <= 64 ? 2 : 1))  // D=64: keep 2 waves/SIMD (<= 256 VGPR+AGPR)
-attn_bwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
-                const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
-                float* __restrict__ dQacc, bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int S, int H, int HKV,
-                float scale, float scale_log2, AttnStrides st) {
-  constexpr int KS = D / 32;   // k-steps over d
-  constexpr int DT = D / 16;   // d tiles
-  constexpr int NCH = D / 8;
-  constexpr int BKB = 128;     // keys per block
-  constexpr int QI = 32;       // queries per iteration
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* k_lds = smem;                              // [128][D]
-  char* ds_lds = k_lds + BKB * D * 2;              // [32][128]
-  char* qbuf = ds_lds + QI * BKB * 2;              // 2 x {Q [32][D], dO [32][D], lse_log2[32], delta[32]}
-  constexpr int QBUF = 2 * QI * D * 2 + 2 * QI * 4;
 
+// ---------------------------------------------------------------------------
+// Key-major dK / dV kernel.
+template <int D>
+struct DkvCfg {
+  // 4 waves x 32 keys, 32-query tiles: a wave's dK^T + dV^T accumulators
+  // are 128 registers at D = 128; with K fragments, S / dP and a 16-register
+  // staging slot it still fits 256, so two workgroups (2 waves per SIMD,
+  // ~65 KiB LDS each) share a CU
+  static constexpr int WAVES = 4;
+  static constexpr int BKB = 32 * WAVES;   // keys per workgroup
+  static constexpr int BQT = 32;           // queries per tile
+  static constexpr int NCH = D / 8;
+  static constexpr int KK = D / 16;
+  static constexpr int DT = D / 32;
+  static constexpr int TILE = BQT * D * 2;            // one [64][D] bf16 image
+  static constexpr int BUF = 2 * TILE + 2 * BQT * 4;  // Q, dO, lse2[64], delta[64]
+  static constexpr int VPT = BQT * NCH / (64 * WAVES);
+  static constexpr int VIMG = BKB * D * 2;            // the block's V rows (LDS-resident)
+};
+
+template <int D, bool CAUSAL, bool PARTIAL>
+__global__ void __launch_bounds__(64 * DkvCfg<D>::WAVES, 2)
+attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
+                     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+                     bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, float* __restrict__ dKp,
+                     float* __restrict__ dVp, int S, int H, int HKV, float scale, float scale_log2,
+                     AttnStrides st) {
+  using C = DkvCfg<D>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  const int b = blockIdx.z, hk = blockIdx.y;
-  // causal: the key blocks with the most queries (the first ones) go first
-  const int kb0 = blockIdx.x * BKB;  // causal: the first key blocks (most queries) dispatch first
-  const int kw0 = kb0 + 32 * wid;  // this wave's first key
-  const int group = H / HKV;
-  const int64_t q_acc_rs = (int64_t)H * D;  // fp32 dQ workspace is contiguous BSHD
+  const int r = lane & 31, hh = lane >> 5;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int hk = h / (H / HKV);
+  const int kb0 = blockIdx.x * C::BKB;  // causal: low key blocks (most queries) dispatch first
+  const int kw0 = kb0 + 32 * wid;
+  const int key = kw0 + r;
+  const bf16_t* Qb = Q + (int64_t)b * st.q_bs + (int64_t)h * D;
+  const bf16_t* dOb = dO + (int64_t)b * st.do_bs + (int64_t)h * D;
   const bf16_t* Kb = K + (int64_t)b * st.k_bs + (int64_t)hk * D;
   const bf16_t* Vb = V + (int64_t)b * st.v_bs + (int64_t)hk * D;
+  const float* lse_b = LSE + ((int64_t)b * H + h) * S;
+  const float* del_b = DELTA + ((int64_t)b * H + h) * S;
 
-  // K block -> LDS (for the dQ transpose reads); K,V fragments -> registers
-  for (int v = tid; v < BKB * NCH; v += 256) {
-    const int r = v / NCH, c = v % NCH;
-    const int key = kb0 + r;
-    u32x4 x = (u32x4){0, 0, 0, 0};
-    if (key < S) x = *(const u32x4*)(Kb + (int64_t)key * st.k_rs + c * 8);
-    *(u32x4*)(k_lds + swzb<D>(r, c)) = x;
+  // K fragments of this wave's keys stay in registers (B operand of S):
+  // K[key][16 kk + 8 hh .. +7]; the block's V rows live in LDS (B operand of
+  // dP, row-read per k-step) -- registers for 2 waves per SIMD.
+  char* v_img = smem + 2 * C::BUF;
+  for (int v = tid; v < C::BKB * C::NCH; v += 64 * C::WAVES) {
+    const int row = v / C::NCH, c = v % C::NCH;
+    const int kv = kb0 + row;
+    *(u32x4*)(v_img + img_off<D>(row, c)) =
+        kv < S ? *(const u32x4*)(Vb + (int64_t)kv * st.v_rs + c * 8) : (u32x4){0, 0, 0, 0};
   }
-  u32x4 kf[2][KS], vf[2][KS];  // B operand frags: [key = li][d = 32kk + 8g..]
+  u32x4 kf[C::KK];
 #pragma unroll
-  for (int kt = 0; kt < 2; ++kt) {
-    const int key = kw0 + 16 * kt + li;
+  for (int kk = 0; kk < C::KK; ++kk)
+    kf[kk] = key < S ? *(const u32x4*)(Kb + (int64_t)key * st.k_rs + 16 * kk + 8 * hh) : (u32x4){0, 0, 0, 0};
+  f32x16 dk[C::DT], dv[C::DT];
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
-      if (key < S) {
-        kf[kt][kk] = *(const u32x4*)(Kb + (int64_t)key * st.k_rs + 32 * kk + 8 * g);
-        vf[kt][kk] = *(const u32x4*)(Vb + (int64_t)key * st.v_rs + 32 * kk + 8 * g);
-      } else {
-        kf[kt][kk] = (u32x4){0, 0, 0, 0};
-        vf[kt][kk] = (u32x4){0, 0, 0, 0};
-      }
-    }
-  }
-  f32x4 dk[DT][2], dv[DT][2];
+  for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
-  for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      dk[dt][kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      dv[dt][kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 16; ++i) {
+      dk[dt][i] = 0.f;
+      dv[dt][i] = 0.f;
     }
 
-  const int q_start = CAUSAL ? (kb0 / QI) * QI : 0;
-  const int nq = (S - q_start + QI - 1) / QI;  // query slices per head
-  const int n_it = group * nq;
-  // Software pipeline over (head, query slice): the Q / dO rows, LSE and
-  // delta of slice i+1 are loaded into registers while slice i computes and
-  // written to the other LDS buffer after its dQ pass (T14 issue-early /
-  // write-late): HBM latency stays off the critical path even at one wave
-  // per SIMD.  Two barriers per slice.
-  constexpr int LV = QI * NCH / 256;  // 16-byte vectors per thread per tensor
-  u32x4 q_st[LV], do_st[LV];
+  const int q_lo = CAUSAL ? (kb0 / C::BQT) * C::BQT : 0;
+  const int n_it = max(0, (S - q_lo + C::BQT - 1) / C::BQT);
+  u32x4 q_st[C::VPT], do_st[C::VPT];
   float lse_st = INFINITY, del_st = 0.f;
-  auto issue_slice = [&](int it) {
-    const int h = hk * group + it / nq;
-    const int qb = q_start + (it % nq) * QI;
-    const bf16_t* Qb = Q + (int64_t)b * st.q_bs + (int64_t)h * D;
-    const bf16_t* dOb = dO + (int64_t)b * st.do_bs + (int64_t)h * D;
+  auto issue = [&](int it) {
+    const int q0 = q_lo + it * C::BQT;
 #pragma unroll
-    for (int i = 0; i < LV; ++i) {
-      const int v = tid + 256 * i;
-      const int r = v / NCH, c = v % NCH;
-      const int q = qb + r;
+    for (int i = 0; i < C::VPT; ++i) {
+      const int v = tid + 64 * C::WAVES * i;
+      const int row = v / C::NCH, c = v % C::NCH;
+      const int q = q0 + row;
       if (q < S) {
         q_st[i] = *(const u32x4*)(Qb + (int64_t)q * st.q_rs + c * 8);
         do_st[i] = *(const u32x4*)(dOb + (int64_t)q * st.do_rs + c * 8);
@@ -166,235 +167,391 @@ attn_bwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
         do_st[i] = (u32x4){0, 0, 0, 0};
       }
     }
-    if (tid < QI) {
-      const int q = qb + tid;
-      const int64_t off = ((int64_t)b * H + h) * S + q;
-      lse_st = q < S ? LSE[off] * 1.4426950408889634f : INFINITY;
-      del_st = q < S ? DELTA[off] : 0.f;
+    if (tid < C::BQT) {
+      const int q = q0 + tid;
+      lse_st = q < S ? lse_b[q] * 1.4426950408889634f : INFINITY;
+      del_st = q < S ? del_b[q] : 0.f;
     }
   };
-  auto write_slice = [&](int buf) {
-    char* ql = qbuf + buf * QBUF;
-    char* dl = ql + QI * D * 2;
-    float* stl = (float*)(dl + QI * D * 2);
+  auto write = [&](int buf) {
+    char* ql = smem + buf * C::BUF;
+    char* dl = ql + C::TILE;
+    float* stl = (float*)(dl + C::TILE);
 #pragma unroll
-    for (int i = 0; i < LV; ++i) {
-      const int v = tid + 256 * i;
-      const int r = v / NCH, c = v % NCH;
-      *(u32x4*)(ql + swzb<D>(r, c)) = q_st[i];
-      *(u32x4*)(dl + swzb<D>(r, c)) = do_st[i];
+    for (int i = 0; i < C::VPT; ++i) {
+      const int v = tid + 64 * C::WAVES * i;
+      const int row = v / C::NCH, c = v % C::NCH;
+      *(u32x4*)(ql + img_off<D>(row, c)) = q_st[i];
+      *(u32x4*)(dl + img_off<D>(row, c)) = do_st[i];
     }
-    if (tid < QI) {
+    if (tid < C::BQT) {
       stl[tid] = lse_st;
-      stl[QI + tid] = del_st;
+      stl[C::BQT + tid] = del_st;
     }
   };
   if (n_it > 0) {
-    issue_slice(0);
-    write_slice(0);
+    issue(0);
+    write(0);
+    if (n_it > 1) issue(1);
   }
-  __syncthreads();  // K block + first slice visible
+  __syncthreads();
+
   for (int it = 0; it < n_it; ++it) {
-    const int h = hk * group + it / nq;
-    const int qb = q_start + (it % nq) * QI;
-    float* dQb = dQacc + (int64_t)b * S * q_acc_rs + (int64_t)h * D;
-    const char* q_lds = qbuf + (it & 1) * QBUF;
-    const char* do_lds = q_lds + QI * D * 2;
-    const float* stat_lds = (const float*)(do_lds + QI * D * 2);
-    if (it + 1 < n_it) issue_slice(it + 1);
-    {
-      // S = Q K^T and dP = dO V^T : [qt][kt], lane holds [q = 4g + r][key = li]
-      f32x4 s[2][2], dp[2][2];
+    const int q0 = q_lo + it * C::BQT;
+    const char* ql = smem + (it & 1) * C::BUF;
+    const char* dl = ql + C::TILE;
+    const float* stl = (const float*)(dl + C::TILE);
+    // all queries of this tile precede this wave's keys: nothing to add
+    if (!CAUSAL || q0 + C::BQT - 1 >= kw0) {
+      const bool need_mask = (q0 + C::BQT > S) || (kw0 + 32 > S) || (CAUSAL && kw0 + 31 > q0);
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
+      for (int qs = 0; qs < C::BQT / 32; ++qs) {
+        // S = Q K^T, dP = dO V^T for 32 queries: key on the lane, query in the registers
+        f32x16 s, dp;
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          s[qt][kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-          dp[qt][kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < 16; ++i) {
+          s[i] = 0.f;
+          dp[i] = 0.f;
         }
 #pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
+        for (int kk = 0; kk < C::KK; ++kk) {
+          const u32x4 qa = *(const u32x4*)(ql + img_off<D>(32 * qs + r, 2 * kk + hh));
+          const u32x4 da = *(const u32x4*)(dl + img_off<D>(32 * qs + r, 2 * kk + hh));
+          const u32x4 vb = *(const u32x4*)(v_img + img_off<D>(32 * wid + r, 2 * kk + hh));
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(qa), as_bf(kf[kk]), s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(da), as_bf(vb), dp, 0, 0, 0);
+        }
+        // rows of register group g: queries 32 qs + 8 g + 4 hh + 0..3
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
-          const u32x4 qa = *(const u32x4*)(q_lds + swzb<D>(16 * qt + li, 4 * kk + g));
-          const u32x4 da = *(const u32x4*)(do_lds + swzb<D>(16 * qt + li, 4 * kk + g));
+        for (int g = 0; g < 4; ++g) {
+          const int qi = 32 * qs + 8 * g + 4 * hh;
+          const f32x4 l4 = *(const f32x4*)(stl + qi);
+          const f32x4 d4 = *(const f32x4*)(stl + C::BQT + qi);
 #pragma unroll
-          for (int kt = 0; kt < 2; ++kt) {
-            s[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(qa), as_bf(kf[kt][kk]), s[qt][kt], 0, 0, 0);
-            dp[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(da), as_bf(vf[kt][kk]), dp[qt][kt], 0, 0, 0);
+          for (int j = 0; j < 4; ++j) {
+            const int i = 4 * g + j;
+            float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], scale_log2, -l4[j]));
+            if (need_mask) {
+              const int q = q0 + qi + j;
+              if (q >= S || key >= S || (CAUSAL && key > q)) p = 0.f;
+            }
+            s[i] = p;
+            dp[i] = p * (dp[i] - d4[j]);  // dS (scale applied in the epilogue)
           }
         }
-      }
-      // P and dS (scaled) in place
+        // dV^T += dO^T P ; dK^T += Q^T dS : 2 k-steps of 16 queries
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const u32x4 pf = {pk2(s[8 * s2 + 0], s[8 * s2 + 1]), pk2(s[8 * s2 + 2], s[8 * s2 + 3]),
+                            pk2(s[8 * s2 + 4], s[8 * s2 + 5]), pk2(s[8 * s2 + 6], s[8 * s2 + 7])};
+          const u32x4 sf = {pk2(dp[8 * s2 + 0], dp[8 * s2 + 1]), pk2(dp[8 * s2 + 2], dp[8 * s2 + 3]),
+                            pk2(dp[8 * s2 + 4], dp[8 * s2 + 5]), pk2(dp[8 * s2 + 6], dp[8 * s2 + 7])};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ql = 16 * qt + 4 * g + r;
-          const int q = qb + ql;
-          const float lse2 = stat_lds[ql], dl = stat_lds[QI + ql];
+          for (int dt = 0; dt < C::DT; ++dt) {
+            const u32x4 doT = tr_frag<D>(dl, 32 * qs + 16 * s2, 32 * dt, lane);
+            dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(doT), as_bf(pf), dv[dt], 0, 0, 0);
+          }
 #pragma unroll
-          for (int kt = 0; kt < 2; ++kt) {
-            const int key = kw0 + 16 * kt + li;
-            float p = exp2f(s[qt][kt][r] * scale_log2 - lse2);
-            if (key >= S || q >= S || (CAUSAL && key > q)) p = 0.f;
-            s[qt][kt][r] = p;
-            dp[qt][kt][r] = p * (dp[qt][kt][r] - dl) * scale;
+          for (int dt = 0; dt < C::DT; ++dt) {
+            const u32x4 qT = tr_frag<D>(ql, 32 * qs + 16 * s2, 32 * dt, lane);
+            dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(qT), as_bf(sf), dk[dt], 0, 0, 0);
           }
         }
-      // dV^T += dO^T P ; dK^T += Q^T dS  (k = 32 queries, permuted order)
-      {
-        u32x4 pb[2], sb[2];
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          const f32x4 a = s[0][kt], c = s[1][kt];
-          pb[kt] = (u32x4){pk2(a[0], a[1]), pk2(a[2], a[3]), pk2(c[0], c[1]), pk2(c[2], c[3])};
-          const f32x4 e = dp[0][kt], f = dp[1][kt];
-          sb[kt] = (u32x4){pk2(e[0], e[1]), pk2(e[2], e[3]), pk2(f[0], f[1]), pk2(f[2], f[3])};
-        }
-        const int qrow = li >> 2, p4 = li & 3;
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          const int col = 16 * dt + 4 * p4;
-          const int r0 = 4 * g + qrow, r1 = r0 + 16;
-          const int o0 = swzb<D>(r0, col >> 3) + (col & 7) * 2;
-          const int o1 = swzb<D>(r1, col >> 3) + (col & 7) * 2;
-          const u32x4 doT = tr_pair(do_lds, o0, o1);
-          const u32x4 qT = tr_pair(q_lds, o0, o1);
-#pragma unroll
-          for (int kt = 0; kt < 2; ++kt) {
-            dv[dt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(doT), as_bf(pb[kt]), dv[dt][kt], 0, 0, 0);
-            dk[dt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(qT), as_bf(sb[kt]), dk[dt][kt], 0, 0, 0);
-          }
-        }
-      }
-      // dS -> LDS as [q][key_in_block] bf16
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int ql = 16 * qt + 4 * g + r;
-            const int kl = 32 * wid + 16 * kt + li;
-            *(bf16_t*)(ds_lds + swz_ds(ql, kl >> 3) + (kl & 7) * 2) = f2bf(dp[qt][kt][r]);
-          }
-      __syncthreads();
-      // dQ[q][d] = sum_key dS[q][key] K[key][d]; wave -> q tile (wid&1), d tiles (wid>>1)*DT/2..
-      {
-        const int qt = wid & 1;
-        constexpr int DTW = DT / 2;
-        const int dt0 = (wid >> 1) * DTW;
-        f32x4 acc[DTW];
-#pragma unroll
-        for (int i = 0; i < DTW; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < BKB / 32; ++ks) {
-          // A = dS[q = li][key = 32ks + perm]: keys 32ks + 4g + j (j<4), 32ks+16+4g+j-4
-          // build from two 8-byte pieces of the row
-          const int qr = 16 * qt + li;
-          const int ka = 32 * ks + 4 * g, kb = ka + 16;
-          const uint2 pa = *(const uint2*)(ds_lds + swz_ds(qr, ka >> 3) + (ka & 7) * 2);
-          const uint2 pbv = *(const uint2*)(ds_lds + swz_ds(qr, kb >> 3) + (kb & 7) * 2);
-          const u32x4 af = (u32x4){pa.x, pa.y, pbv.x, pbv.y};
-          const int qrow = li >> 2, p4 = li & 3;
-#pragma unroll
-          for (int i = 0; i < DTW; ++i) {
-            const int col = 16 * (dt0 + i) + 4 * p4;
-            const int r0 = 32 * ks + 4 * g + qrow, r1 = r0 + 16;
-            const u32x4 kT = tr_pair(k_lds, swzb<D>(r0, col >> 3) + (col & 7) * 2,
-                                     swzb<D>(r1, col >> 3) + (col & 7) * 2);
-            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(af), as_bf(kT), acc[i], 0, 0, 0);
-          }
-        }
-        // C: [q = 4g + r][d = li]
-#pragma unroll
-        for (int i = 0; i < DTW; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int q = qb + 16 * qt + 4 * g + r;
-            if (q < S) atomicAdd(dQb + (int64_t)q * q_acc_rs + 16 * (dt0 + i) + li, acc[i][r]);
-          }
       }
     }
-    // next slice -> the other buffer (last read in iteration it-1, which every
-    // wave finished before the dS barrier above); dS / this buffer free after
-    if (it + 1 < n_it) write_slice((it + 1) & 1);
+    if (it + 1 < n_it) {
+      write((it + 1) & 1);  // buffer last read in iteration it-1
+      if (it + 2 < n_it) issue(it + 2);
+    }
     __syncthreads();
   }
-  // write dK, dV: lane holds [d = 16dt + 4g + r][key = kw0 + 16kt + li]
-  bf16_t* dKb = dK + (int64_t)b * st.dk_bs + (int64_t)hk * D;
-  bf16_t* dVb = dV + (int64_t)b * st.dv_bs + (int64_t)hk * D;
+  if (key >= S) return;
+  // accumulator rows = d: register i of tile dt is d = 32 dt + 8 (i>>2) + 4 hh + (i&3)
+  if (PARTIAL) {
+    float* kp = dKp + (((int64_t)b * S + key) * H + h) * D;
+    float* vp = dVp + (((int64_t)b * S + key) * H + h) * D;
 #pragma unroll
-  for (int kt = 0; kt < 2; ++kt) {
-    const int key = kw0 + 16 * kt + li;
-    if (key >= S) continue;
+    for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      uint2 wk, wv;
-      wk.x = pk2(dk[dt][kt][0], dk[dt][kt][1]);
-      wk.y = pk2(dk[dt][kt][2], dk[dt][kt][3]);
-      wv.x = pk2(dv[dt][kt][0], dv[dt][kt][1]);
-      wv.y = pk2(dv[dt][kt][2], dv[dt][kt][3]);
-      *(uint2*)(dKb + (int64_t)key * st.dk_rs + 16 * dt + 4 * g) = wk;
-      *(uint2*)(dVb + (int64_t)key * st.dv_rs + 16 * dt + 4 * g) = wv;
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * hh;
+        *(f32x4*)(kp + d) = (f32x4){dk[dt][4 * g] * scale, dk[dt][4 * g + 1] * scale, dk[dt][4 * g + 2] * scale,
+                                    dk[dt][4 * g + 3] * scale};
+        *(f32x4*)(vp + d) = (f32x4){dv[dt][4 * g], dv[dt][4 * g + 1], dv[dt][4 * g + 2], dv[dt][4 * g + 3]};
+      }
+  } else {
+    bf16_t* dKk = dK + (int64_t)b * st.dk_bs + (int64_t)hk * D + (int64_t)key * st.dk_rs;
+    bf16_t* dVk = dV + (int64_t)b * st.dv_bs + (int64_t)hk * D + (int64_t)key * st.dv_rs;
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * dt + 8 * g + 4 * hh;
+        uint2 wk, wv;
+        wk.x = pk2(dk[dt][4 * g] * scale, dk[dt][4 * g + 1] * scale);
+        wk.y = pk2(dk[dt][4 * g + 2] * scale, dk[dt][4 * g + 3] * scale);
+        wv.x = pk2(dv[dt][4 * g], dv[dt][4 * g + 1]);
+        wv.y = pk2(dv[dt][4 * g + 2], dv[dt][4 * g + 3]);
+        *(uint2*)(dKk + d) = wk;
+        *(uint2*)(dVk + d) = wv;
+      }
+  }
+}
+
+// GQA: dK[b, s, hk, :] = sum over the group's query heads of the fp32 partials
+// (8 elements per thread; partial layout [B, S, H, D]).
+template <int D>
+__global__ void gqa_reduce_kernel(const float* __restrict__ pk, const float* __restrict__ pv, bf16_t* __restrict__ dK,
+                                  bf16_t* __restrict__ dV, int64_t BS, int S, int H, int HKV, AttnStrides st) {
+  const int group = H / HKV;
+  const int64_t nv = BS * HKV * (D / 8);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % (D / 8));
+    const int64_t t = i / (D / 8);
+    const int hk = (int)(t % HKV);
+    const int64_t bs = t / HKV;
+    const int64_t b = bs / S, sq = bs % S;
+    float fk[8] = {0, 0, 0, 0, 0, 0, 0, 0}, fv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int g = 0; g < group; ++g) {
+      const int64_t off = (bs * H + hk * group + g) * D + c * 8;
+      const f32x4 a0 = *(const f32x4*)(pk + off), a1 = *(const f32x4*)(pk + off + 4);
+      const f32x4 b0 = *(const f32x4*)(pv + off), b1 = *(const f32x4*)(pv + off + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        fk[j] += a0[j];
+        fk[4 + j] += a1[j];
+        fv[j] += b0[j];
+        fv[4 + j] += b1[j];
+      }
+    }
+    *(u32x4*)(dK + b * st.dk_bs + sq * st.dk_rs + hk * D + c * 8) = pack8(fk);
+    *(u32x4*)(dV + b * st.dv_bs + sq * st.dv_rs + hk * D + c * 8) = pack8(fv);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Query-major dQ kernel (split backward: no atomics).
+//
+// dQ = scale * sum_keys dS K with dS = P * (dP - delta), P = exp2(S*c - lse2).
+// Same structure as the forward kernel: per wave 32 queries on the MFMA lane
+// (swapped products S^T = K Q^T and dP^T = V dO^T with v_mfma_f32_32x32x16),
+// K/V tiles of 64 keys double-buffered in the T10(a) LDS image, and
+// dQ^T += K^T dS^T with the packed dS^T accumulator as the B operand and K^T
+// from ds_read_b64_tr_b16.  Every dQ element is summed in registers by one
+// wave and written once, in bf16, straight into the (possibly packed) dQ
+// view: no fp32 workspace, no memset, no conversion pass -- the fused
+// kernel's atomics (1.3 TB/s chip-wide, ~40 % of its time at S = 4096) are
+// gone at the price of recomputing S and dP here.
+template <int D>
+struct DqCfg {
+  static constexpr int WAVES = D == 128 ? 8 : 4;
+  static constexpr int BQ = 32 * WAVES;
+  static constexpr int BK = 64;
+  static constexpr int NCH = D / 8;
+  static constexpr int KK = D / 16;
+  static constexpr int DT = D / 32;
+  static constexpr int TILE = BK * D * 2;
+  static constexpr int VPT = BK * NCH / (64 * WAVES);
+};
+
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(64 * DqCfg<D>::WAVES, 1)
+attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
+                   const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+                   bf16_t* __restrict__ dQ, int S, int H, int HKV, float scale, float scale_log2, AttnStrides st) {
+  using C = DqCfg<D>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int hk = h / (H / HKV);
+  const int qblk = CAUSAL ? (int)(gridDim.x - 1 - blockIdx.x) : (int)blockIdx.x;
+  const int q_blk0 = qblk * C::BQ;
+  const int q0 = q_blk0 + wid * 32;
+  const int q = q0 + r;
+  const bf16_t* Qb = Q + (int64_t)b * st.q_bs + (int64_t)h * D;
+  const bf16_t* dOb = dO + (int64_t)b * st.do_bs + (int64_t)h * D;
+  const bf16_t* Kb = K + (int64_t)b * st.k_bs + (int64_t)hk * D;
+  const bf16_t* Vb = V + (int64_t)b * st.v_bs + (int64_t)hk * D;
+
+  // Q and dO fragments (B operands): lane holds row q, d = 16 kk + 8 hh .. +7
+  u32x4 qf[C::KK], dof[C::KK];
+#pragma unroll
+  for (int kk = 0; kk < C::KK; ++kk) {
+    if (q < S) {
+      qf[kk] = *(const u32x4*)(Qb + (int64_t)q * st.q_rs + 16 * kk + 8 * hh);
+      dof[kk] = *(const u32x4*)(dOb + (int64_t)q * st.do_rs + 16 * kk + 8 * hh);
+    } else {
+      qf[kk] = (u32x4){0, 0, 0, 0};
+      dof[kk] = (u32x4){0, 0, 0, 0};
     }
   }
-}
+  const int64_t so = ((int64_t)b * H + h) * S + q;
+  const float lse2 = q < S ? LSE[so] * 1.4426950408889634f : INFINITY;
+  const float dl = q < S ? DELTA[so] : 0.f;
 
-// dQ workspace (contiguous fp32 BSHD) -> bf16 dq with its own batch/row strides
-__global__ void dq_to_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t rows, int S, int HD,
-                                  long long bs, long long rs) {
-  const int per_row = HD / 8;
-  const int64_t nv = rows * per_row;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t row = i / per_row;  // (b, s)
-    const int c = (int)(i % per_row);
-    const int64_t b = row / S, sq = row % S;
-    const f32x4 a = *(const f32x4*)(x + i * 8), bb = *(const f32x4*)(x + i * 8 + 4);
-    const float f[8] = {a[0], a[1], a[2], a[3], bb[0], bb[1], bb[2], bb[3]};
-    *(u32x4*)(y + b * bs + sq * rs + c * 8) = pack8(f);
+  f32x16 acc[C::DT];
+#pragma unroll
+  for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[dt][i] = 0.f;
+
+  int n_tiles = (S + C::BK - 1) / C::BK;
+  if (CAUSAL) n_tiles = min(n_tiles, min(S - 1, q_blk0 + C::BQ - 1) / C::BK + 1);
+
+  u32x4 kst[C::VPT], vst[C::VPT];
+  auto issue_load = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < C::VPT; ++i) {
+      const int v = tid + 64 * C::WAVES * i;
+      const int row = v / C::NCH, c = v % C::NCH;
+      const int key = t * C::BK + row;
+      if (key < S) {
+        kst[i] = *(const u32x4*)(Kb + (int64_t)key * st.k_rs + c * 8);
+        vst[i] = *(const u32x4*)(Vb + (int64_t)key * st.v_rs + c * 8);
+      } else {
+        kst[i] = (u32x4){0, 0, 0, 0};
+        vst[i] = (u32x4){0, 0, 0, 0};
+      }
+    }
+  };
+  auto write_lds = [&](int buf) {
+    char* kl = smem + buf * 2 * C::TILE;
+    char* vl = kl + C::TILE;
+#pragma unroll
+    for (int i = 0; i < C::VPT; ++i) {
+      const int v = tid + 64 * C::WAVES * i;
+      const int row = v / C::NCH, c = v % C::NCH;
+      *(u32x4*)(kl + img_off<D>(row, c)) = kst[i];
+      *(u32x4*)(vl + img_off<D>(row, c)) = vst[i];
+    }
+  };
+  issue_load(0);
+  write_lds(0);
+  if (n_tiles > 1) issue_load(1);
+  __syncthreads();
+  const int g4 = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+
+  for (int t = 0; t < n_tiles; ++t) {
+    const int k0 = t * C::BK;
+    const char* kl = smem + (t & 1) * 2 * C::TILE;
+    const char* vl = kl + C::TILE;
+    if (!CAUSAL || k0 <= q0 + 31) {
+      const bool need_mask = (k0 + C::BK > S) || (CAUSAL && (k0 + C::BK - 1 > q0));
+      // one 32-key subtile at a time keeps S^T / dP^T at 32 registers
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        f32x16 s, dp;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          s[i] = 0.f;
+          dp[i] = 0.f;
+        }
+#pragma unroll
+        for (int kk = 0; kk < C::KK; ++kk) {
+          const u32x4 kf = *(const u32x4*)(kl + img_off<D>(32 * sb + r, 2 * kk + hh));
+          const u32x4 vf = *(const u32x4*)(vl + img_off<D>(32 * sb + r, 2 * kk + hh));
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(kf), as_bf(qf[kk]), s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(vf), as_bf(dof[kk]), dp, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], scale_log2, -lse2));
+          if (need_mask) {
+            const int key = k0 + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            if (key >= S || (CAUSAL && key > q)) p = 0.f;
+          }
+          s[i] = p * (dp[i] - dl);  // dS^T (scale applied in the epilogue)
+        }
+        // dQ^T += K^T dS^T : 2 k-steps of 16 keys, K^T from transposed reads
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const u32x4 pf = {pk2(s[8 * s2 + 0], s[8 * s2 + 1]), pk2(s[8 * s2 + 2], s[8 * s2 + 3]),
+                            pk2(s[8 * s2 + 4], s[8 * s2 + 5]), pk2(s[8 * s2 + 6], s[8 * s2 + 7])};
+          const int kb = 32 * sb + 16 * s2 + 4 * hh + tq;
+#pragma unroll
+          for (int dt = 0; dt < C::DT; ++dt) {
+            const int ch = (32 * dt + 16 * (g4 & 1)) / 8 + (tp >> 1);
+            const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s16x4*)LDS_PTR(kl + img_off<D>(kb, ch) + 8 * (tp & 1)));
+            const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s16x4*)LDS_PTR(kl + img_off<D>(kb + 8, ch) + 8 * (tp & 1)));
+            const u32x4 kt = {pack_s16(v0[0], v0[1]), pack_s16(v0[2], v0[3]), pack_s16(v1[0], v1[1]),
+                              pack_s16(v1[2], v1[3])};
+            acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(kt), as_bf(pf), acc[dt], 0, 0, 0);
+          }
+        }
+      }
+    }
+    if (t + 1 < n_tiles) {
+      write_lds((t + 1) & 1);
+      if (t + 2 < n_tiles) issue_load(t + 2);
+    }
+    __syncthreads();
+  }
+  if (q < S) {
+    bf16_t* dQq = dQ + (int64_t)b * st.dq_bs + (int64_t)h * D + (int64_t)q * st.dq_rs;
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint2 w;
+        w.x = pk2(acc[dt][4 * g + 0] * scale, acc[dt][4 * g + 1] * scale);
+        w.y = pk2(acc[dt][4 * g + 2] * scale, acc[dt][4 * g + 3] * scale);
+        *(uint2*)(dQq + 32 * dt + 8 * g + 4 * hh) = w;
+      }
   }
 }
 
-__global__ void f32_to_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t n) {
-  const int64_t nv = n >> 3;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
-    const f32x4 a = *(const f32x4*)(x + i * 8), b = *(const f32x4*)(x + i * 8 + 4);
-    const float f[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-    *(u32x4*)(y + i * 8) = pack8(f);
-  }
-}
-
-// workspace: dq_acc fp32 [B,S,H,D] + delta fp32 [B,H,S]
+// workspace: delta fp32 [B, H, S] (+ GQA fp32 partials 2 x [B, S, H, D])
 extern "C" int64_t dw_attn_bwd_workspace(int B, int S, int H, int D) {
-  return (int64_t)B * S * H * D * 4 + (int64_t)B * H * S * 4 + 256;
-}
-
-template <int D>
-static size_t bwd_lds_bytes() {
-  return 128 * D * 2 + 32 * 128 * 2 + 2 * (2 * 32 * D * 2 + 2 * 32 * 4);
+  return (int64_t)B * H * S * 4 + 2 * (int64_t)B * S * H * D * 4 + 512;
 }
 
 template <int D>
 static void launch_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const void* lse,
-                       float* dq_acc, float* delta, void* dk, void* dv, int B, int S, int H, int HKV, int causal,
+                       char* ws, void* dq, void* dk, void* dv, int B, int S, int H, int HKV, int causal,
                        float softmax_scale, const AttnStrides& st, hipStream_t s) {
+  float* delta = (float*)ws;
   const int64_t rows = (int64_t)B * S * H;
   constexpr int RPB = 4 * (64 / (D / 8));  // rows per 256-thread block
   hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3((unsigned)((rows + RPB - 1) / RPB)), dim3(256), 0, s,
                      (const bf16_t*)o, (const bf16_t*)dout, delta, B, S, H, st);
   const float scale_log2 = softmax_scale * 1.4426950408889634f;
-  dim3 grid((S + 127) / 128, HKV, B);
-  const size_t lds = bwd_lds_bytes<D>();
+  // key-major dK / dV
+  using KC = DkvCfg<D>;
+  const bool partial = H != HKV;
+  float* pk = (float*)(ws + (((int64_t)B * H * S * 4 + 255) / 256) * 256);
+  float* pv = pk + (int64_t)B * S * H * D;
+  dim3 gk((S + KC::BKB - 1) / KC::BKB, H, B);
+  const int lk = 2 * KC::BUF + KC::VIMG;
+#define DKDV(CA, PA)                                                                                          \
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CA, PA>), gk, dim3(64 * KC::WAVES), lk, s, (const bf16_t*)q,   \
+                     (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta,      \
+                     (bf16_t*)dk, (bf16_t*)dv, pk, pv, S, H, HKV, softmax_scale, scale_log2, st)
+  if (causal) {
+    if (partial) DKDV(true, true); else DKDV(true, false);
+  } else {
+    if (partial) DKDV(false, true); else DKDV(false, false);
+  }
+#undef DKDV
+  if (partial) {
+    const int64_t nv = (int64_t)B * S * HKV * (D / 8);
+    hipLaunchKernelGGL(gqa_reduce_kernel<D>, dim3(dw_grid_for(nv, 256, 4096)), dim3(256), 0, s, pk, pv,
+                       (bf16_t*)dk, (bf16_t*)dv, (int64_t)B * S, S, H, HKV, st);
+  }
+  // query-major dQ
+  using DC = DqCfg<D>;
+  dim3 gq((S + DC::BQ - 1) / DC::BQ, H, B);
+  const int lq = 4 * DC::TILE;
   if (causal)
-    hipLaunchKernelGGL((attn_bwd_kernel<D, true>), grid, dim3(256), lds, s, (const bf16_t*)q, (const bf16_t*)k,
-                       (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta, dq_acc, (bf16_t*)dk,
-                       (bf16_t*)dv, S, H, HKV, softmax_scale, scale_log2, st);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, true>), gq, dim3(64 * DC::WAVES), lq, s, (const bf16_t*)q,
+                       (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta,
+                       (bf16_t*)dq, S, H, HKV, softmax_scale, scale_log2, st);
   else
-    hipLaunchKernelGGL((attn_bwd_kernel<D, false>), grid, dim3(256), lds, s, (const bf16_t*)q, (const bf16_t*)k,
-                       (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta, dq_acc, (bf16_t*)dk,
-                       (bf16_t*)dv, S, H, HKV, softmax_scale, scale_log2, st);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, false>), gq, dim3(64 * DC::WAVES), lq, s, (const bf16_t*)q,
+                       (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta,
+                       (bf16_t*)dq, S, H, HKV, softmax_scale, scale_log2, st);
 }
 
 // strides: int64[16] = q, k, v, o, do, dq, dk, dv  x (batch, row) in elements
@@ -407,17 +564,9 @@ extern "C" int dw_attn_bwd_strided(const void* q, const void* k, const void* v, 
   long long* f = &st.q_bs;
   for (int i = 0; i < 16; ++i) f[i] = strides[i];
   hipStream_t s = (hipStream_t)stream;
-  float* dq_acc = (float*)workspace;
-  float* delta = dq_acc + (int64_t)B * S * H * D;
-  hipError_t e = hipMemsetAsync(dq_acc, 0, (size_t)B * S * H * D * 4, s);
-  if (e != hipSuccess) return (int)e;
-  if (D == 128) launch_bwd<128>(q, k, v, o, dout, lse, dq_acc, delta, dk, dv, B, S, H, HKV, causal, softmax_scale,
-                                st, s);
-  else launch_bwd<64>(q, k, v, o, dout, lse, dq_acc, delta, dk, dv, B, S, H, HKV, causal, softmax_scale, st, s);
-  const int64_t rows = (int64_t)B * S;
-  const int64_t nv = rows * H * D / 8;
-  hipLaunchKernelGGL(dq_to_bf16_kernel, dim3(dw_grid_for(nv, 256, 4096)), dim3(256), 0, s, dq_acc, (bf16_t*)dq,
-                     rows, S, H * D, st.dq_bs, st.dq_rs);
+  char* ws = (char*)workspace;
+  if (D == 128) launch_bwd<128>(q, k, v, o, dout, lse, ws, dq, dk, dv, B, S, H, HKV, causal, softmax_scale, st, s);
+  else launch_bwd<64>(q, k, v, o, dout, lse, ws, dq, dk, dv, B, S, H, HKV, causal, softmax_scale, st, s);
   DW_LAUNCH_RET;
 }
 

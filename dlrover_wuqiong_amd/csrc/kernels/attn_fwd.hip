@@ -25,11 +25,10 @@
 //    write-late); exp2 with the softmax scale folded into log2(e); causal:
 //    tiles above a wave's diagonal are skipped by that wave, the longest
 //    query blocks are dispatched first.
-#include "dw_common.h"
+#include "attn_common.h"
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 
@@ -47,20 +46,10 @@ struct Fwd2Cfg {
   static constexpr int VPT = BK * NCH / (64 * WAVES);  // staged 16-B vectors per thread per tensor
 };
 
-// byte offset of 16-byte chunk `ch` of row `row` (guide T10 layout (a))
-template <int D>
-__device__ __forceinline__ int img_off(int row, int ch) {
-  return (D * 16) * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
-}
-
 __device__ __forceinline__ bf16x8_t as_bf16x8(const u32x4& v) { return __builtin_bit_cast(bf16x8_t, v); }
 
 __device__ __forceinline__ unsigned int pack2(float a, float b) {
   return (unsigned int)f2bf(a) | ((unsigned int)f2bf(b) << 16);
-}
-
-__device__ __forceinline__ unsigned int pack_s16(short a, short b) {
-  return (unsigned int)(unsigned short)a | ((unsigned int)(unsigned short)b << 16);
 }
 
 template <int D, bool CAUSAL>
