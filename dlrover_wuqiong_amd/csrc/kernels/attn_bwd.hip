@@ -92,7 +92,7 @@ struct DkvCfg {
   // ~65 KiB LDS each) share a CU
   static constexpr int WAVES = 4;
   static constexpr int BKB = 32 * WAVES;   // keys per workgroup
-  static constexpr int BQT = 32;           // queries per tile
+  static constexpr int BQT = D == 64 ? 64 : 32;  // queries per tile
   static constexpr int NCH = D / 8;
   static constexpr int KK = D / 16;
   static constexpr int DT = D / 32;
@@ -344,7 +344,7 @@ __global__ void gqa_reduce_kernel(const float* __restrict__ pk, const float* __r
 // gone at the price of recomputing S and dP here.
 template <int D>
 struct DqCfg {
-  static constexpr int WAVES = D == 128 ? 8 : 4;
+  static constexpr int WAVES = 8;
   static constexpr int BQ = 32 * WAVES;
   static constexpr int BK = 64;
   static constexpr int NCH = D / 8;

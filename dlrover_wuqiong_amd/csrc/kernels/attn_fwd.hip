@@ -36,7 +36,7 @@ template <int D>
 struct Fwd2Cfg {
   // D=128: 8 waves share each K/V tile (MFMA-bound, maximise reuse);
   // D=64: softmax (VALU) bound -> 4-wave blocks, 3 blocks per CU
-  static constexpr int WAVES = D == 128 ? 8 : 4;
+  static constexpr int WAVES = 8;
   static constexpr int BQ = 32 * WAVES;  // queries per block
   static constexpr int BK = 64;          // keys per tile
   static constexpr int NCH = D / 8;      // 16-byte chunks per row
