@@ -180,6 +180,25 @@ def main(argv=None) -> int:
             jr, lambda addr: ProcessScaler(a.job_name, addr, a.entry, a.nproc_per_node, str(a.node_num),
                                            a.log_dir, agent_args=shlex.split(a.agent_args)),
             port=a.port, loop_interval=min(a.loop_interval, 5.0), max_relaunch_count=a.max_relaunch_count)
+    elif a.platform in ("k8s", "pyk8s"):
+        # in-cluster: worker pods through the Kubernetes API (platform/k8s.py)
+        import os
+        import shlex
+
+        from ..common.node import JobResource
+        from ..platform.k8s import K8sClient, PodScaler, PodWatcher
+
+        jr = JobResource()
+        jr.update_node_group_resource("worker", a.node_num)
+        cli = K8sClient(a.namespace)
+        svc = f"elasticjob-{a.job_name}-dlrover-master"
+        image = os.environ.get("DWAMD_WORKER_IMAGE", "")
+        cmd = shlex.split(os.environ.get("DWAMD_WORKER_COMMAND", "dwamd-run --nnodes auto train.py"))
+        m = DistributedJobMaster(
+            jr, lambda addr: PodScaler(a.job_name, cli, image, f"{svc}:{addr.rsplit(':', 1)[1]}", cmd,
+                                       gpus_per_node=a.nproc_per_node),
+            watcher_factory=lambda scaler: PodWatcher(a.job_name, cli), port=a.port,
+            loop_interval=a.loop_interval, max_relaunch_count=a.max_relaunch_count)
     else:
         m = JobMaster(port=a.port, node_num=a.node_num, loop_interval=a.loop_interval)
     m.prepare()

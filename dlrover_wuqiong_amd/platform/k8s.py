@@ -1,0 +1,320 @@
+"""Kubernetes platform layer: REST client, pod scaler / watcher for the job
+master, and the ElasticJob operator (reconciler) -- in Python, on the plain
+Kubernetes REST API (``requests``), no client library or Go toolchain.
+
+* ``K8sClient``: in-cluster config (service-account token + CA) or an
+  explicit ``base_url``; pods, services, nodes (cordon), custom objects
+  (``ElasticJob`` / ``ScalePlan`` of ``elastic.iml.github.io/v1alpha1``) and
+  watch streams (``?watch=true`` JSON lines).
+* ``PodScaler``: the master's ``Scaler`` -- creates worker pods named
+  ``{job}-worker-{id}`` from the job's replica template (``amd.com/gpu``
+  resources, ``dwamd-run`` command, ``DWAMD_*`` env incl. the master address
+  and node rank) and deletes removed ones.
+* ``PodWatcher``: ``NodeWatcher`` mapping pod phases / container exit codes
+  (OOMKilled, 137 ...) to ``Node`` status and exit reasons.
+* ``ElasticJobOperator``: reconcile loop -- for every ElasticJob without a
+  master, create the master pod + service (``python -m
+  dlrover_wuqiong_amd.master.master --platform k8s``); mirror the master
+  pod phase into ``status.phase``; apply ``ScalePlan`` objects (manual or
+  Brain-generated) to the job's replica counts and mark them consumed.
+
+Parity: reference ``dlrover/python/scheduler/kubernetes.py`` (``k8sClient``
+:121-572), ``master/scaler/pod_scaler.py`` / ``elasticjob_scaler.py``,
+``master/watcher/k8s_watcher.py`` (``PodWatcher`` :194,
+``K8sScalePlanWatcher`` :267) and the Go operator
+``go/operator/pkg/controllers/{elasticjob,scaleplan}_controller.go``.
+"""
+
+import json
+import os
+import threading
+import time
+from typing import Dict, Iterator, List, Optional
+
+from ..common.constants import NodeEventType, NodeExitReason, NodeStatus, NodeType
+from ..common.log import logger
+from ..common.node import Node, NodeResource
+from ..master.scaler import ScalePlan, Scaler
+from ..master.watcher import NodeEvent, NodeWatcher
+
+GROUP, VERSION = "elastic.iml.github.io", "v1alpha1"
+SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+JOB_LABEL, TYPE_LABEL, ID_LABEL, RANK_LABEL = ("elasticjob.dlrover/name", "elasticjob.dlrover/replica-type",
+                                              "elasticjob.dlrover/replica-id", "elasticjob.dlrover/rank-index")
+
+
+class K8sClient:
+    def __init__(self, namespace: str = "default", base_url: Optional[str] = None, token: Optional[str] = None,
+                 verify=None, timeout: float = 10.0):
+        import requests
+
+        self.ns = namespace
+        if base_url is None:
+            host, port = os.environ.get("KUBERNETES_SERVICE_HOST"), os.environ.get("KUBERNETES_SERVICE_PORT", "443")
+            if not host:
+                raise RuntimeError("not in a cluster and no base_url given")
+            base_url = f"https://{host}:{port}"
+            if token is None and os.path.exists(f"{SA_DIR}/token"):
+                token = open(f"{SA_DIR}/token").read().strip()
+            if verify is None and os.path.exists(f"{SA_DIR}/ca.crt"):
+                verify = f"{SA_DIR}/ca.crt"
+        self.base = base_url.rstrip("/")
+        self.s = requests.Session()
+        if token:
+            self.s.headers["Authorization"] = f"Bearer {token}"
+        self.s.verify = True if verify is None else verify
+        self.timeout = timeout
+
+    # -- generic
+    def _req(self, method: str, path: str, body=None, params=None, content_type="application/json"):
+        r = self.s.request(method, self.base + path, data=json.dumps(body) if body is not None else None,
+                           params=params, headers={"Content-Type": content_type}, timeout=self.timeout)
+        if r.status_code == 404:
+            return None
+        if r.status_code >= 400:
+            raise RuntimeError(f"k8s {method} {path}: {r.status_code} {r.text[:300]}")
+        return r.json() if r.content else {}
+
+    def _core(self, kind: str, name: str = "") -> str:
+        return f"/api/v1/namespaces/{self.ns}/{kind}" + (f"/{name}" if name else "")
+
+    def _custom(self, plural: str, name: str = "") -> str:
+        return f"/apis/{GROUP}/{VERSION}/namespaces/{self.ns}/{plural}" + (f"/{name}" if name else "")
+
+    # -- pods / services / nodes
+    def create_pod(self, pod: Dict):
+        return self._req("POST", self._core("pods"), pod)
+
+    def get_pod(self, name: str):
+        return self._req("GET", self._core("pods", name))
+
+    def delete_pod(self, name: str):
+        return self._req("DELETE", self._core("pods", name))
+
+    def list_pods(self, label_selector: str = "") -> List[Dict]:
+        res = self._req("GET", self._core("pods"), params={"labelSelector": label_selector} if label_selector else None)
+        return (res or {}).get("items", [])
+
+    def watch_pods(self, label_selector: str = "", resource_version: str = "", timeout_s: int = 60) -> Iterator[Dict]:
+        params = {"watch": "true", "timeoutSeconds": str(timeout_s)}
+        if label_selector:
+            params["labelSelector"] = label_selector
+        if resource_version:
+            params["resourceVersion"] = resource_version
+        with self.s.get(self.base + self._core("pods"), params=params, stream=True, timeout=timeout_s + 5) as r:
+            for line in r.iter_lines():
+                if line:
+                    yield json.loads(line)
+
+    def create_service(self, svc: Dict):
+        return self._req("POST", self._core("services"), svc)
+
+    def get_service(self, name: str):
+        return self._req("GET", self._core("services", name))
+
+    def cordon_node(self, node_name: str):
+        return self._req("PATCH", f"/api/v1/nodes/{node_name}", {"spec": {"unschedulable": True}},
+                         content_type="application/merge-patch+json")
+
+    # -- custom objects
+    def list_custom(self, plural: str) -> List[Dict]:
+        return (self._req("GET", self._custom(plural)) or {}).get("items", [])
+
+    def get_custom(self, plural: str, name: str):
+        return self._req("GET", self._custom(plural, name))
+
+    def create_custom(self, plural: str, body: Dict):
+        return self._req("POST", self._custom(plural), body)
+
+    def patch_custom(self, plural: str, name: str, patch: Dict):
+        return self._req("PATCH", self._custom(plural, name), patch, content_type="application/merge-patch+json")
+
+    def patch_custom_status(self, plural: str, name: str, status: Dict):
+        return self._req("PATCH", self._custom(plural, name) + "/status", {"status": status},
+                         content_type="application/merge-patch+json")
+
+
+# ----------------------------------------------------------------------------- pods <-> nodes
+
+_PHASE = {"Pending": NodeStatus.PENDING, "Running": NodeStatus.RUNNING, "Succeeded": NodeStatus.SUCCEEDED,
+          "Failed": NodeStatus.FAILED, "Unknown": NodeStatus.UNKNOWN}
+
+
+def pod_name(job: str, node_type: str, node_id: int) -> str:
+    return f"{job}-{node_type}-{node_id}"
+
+
+def pod_to_node(pod: Dict) -> Node:
+    meta, status = pod.get("metadata", {}), pod.get("status", {})
+    labels = meta.get("labels", {})
+    node = Node(type=labels.get(TYPE_LABEL, NodeType.WORKER), id=int(labels.get(ID_LABEL, 0)),
+                rank_index=int(labels.get(RANK_LABEL, labels.get(ID_LABEL, 0))), name=meta.get("name", ""))
+    node.status = _PHASE.get(status.get("phase", "Unknown"), NodeStatus.UNKNOWN)
+    if meta.get("deletionTimestamp"):
+        node.status = NodeStatus.DELETED
+    node.host_addr = status.get("podIP", "")
+    for cs in status.get("containerStatuses", []) or []:
+        term = (cs.get("state", {}) or {}).get("terminated") or (cs.get("lastState", {}) or {}).get("terminated")
+        if term:
+            reason, code = term.get("reason", ""), int(term.get("exitCode", 0))
+            if reason == "OOMKilled":
+                node.exit_reason = NodeExitReason.OOM
+            elif code == 0:
+                node.exit_reason = NodeExitReason.SUCCEEDED
+            elif code in (137, 143):
+                node.exit_reason = NodeExitReason.KILLED
+            elif code in (201, 202):  # reserved: hardware fault detected by the agent
+                node.exit_reason = NodeExitReason.HARDWARE_ERROR
+            else:
+                node.exit_reason = NodeExitReason.FATAL_ERROR
+    return node
+
+
+class PodScaler(Scaler):
+    def __init__(self, job_name: str, client: K8sClient, image: str, master_addr: str, command: List[str],
+                 gpus_per_node: int = 8, env: Optional[Dict[str, str]] = None, namespace_labels=None):
+        super().__init__(job_name)
+        self.client, self.image, self.master_addr = client, image, master_addr
+        self.command, self.gpus = command, gpus_per_node
+        self.env = dict(env or {})
+
+    def pod_spec(self, node: Node) -> Dict:
+        res: NodeResource = node.config_resource
+        limits = {"amd.com/gpu": str(res.gpu_num or self.gpus)}
+        if res.cpu:
+            limits["cpu"] = str(res.cpu)
+        if res.memory:
+            limits["memory"] = f"{res.memory}Mi"
+        env = {"DWAMD_MASTER_ADDR": self.master_addr, "NODE_RANK": str(node.rank_index), "NODE_ID": str(node.id),
+               "DWAMD_JOB_NAME": self.job_name, "HSA_ENABLE_IPC_MODE_LEGACY": "0", **self.env}
+        return {
+            "apiVersion": "v1", "kind": "Pod",
+            "metadata": {"name": pod_name(self.job_name, node.type, node.id),
+                         "labels": {JOB_LABEL: self.job_name, TYPE_LABEL: node.type, ID_LABEL: str(node.id),
+                                    RANK_LABEL: str(node.rank_index)}},
+            "spec": {"restartPolicy": "Never",
+                     "containers": [{"name": "main", "image": self.image, "command": self.command,
+                                     "env": [{"name": k, "value": v} for k, v in env.items()],
+                                     "resources": {"limits": limits, "requests": dict(limits)},
+                                     "volumeMounts": [{"name": "dshm", "mountPath": "/dev/shm"}]}],
+                     # flash checkpoints live in /dev/shm: size it for the node's host memory
+                     "volumes": [{"name": "dshm", "emptyDir": {"medium": "Memory"}}]},
+        }
+
+    def scale(self, plan: ScalePlan):
+        for node in plan.launch_nodes:
+            logger.info(f"k8s: creating pod for {node.type}-{node.id} (rank {node.rank_index})")
+            self.client.create_pod(self.pod_spec(node))
+        for node in plan.remove_nodes:
+            logger.info(f"k8s: deleting pod {pod_name(self.job_name, node.type, node.id)}")
+            self.client.delete_pod(pod_name(self.job_name, node.type, node.id))
+
+
+class PodWatcher(NodeWatcher):
+    def __init__(self, job_name: str, client: K8sClient):
+        self.job_name, self.client = job_name, client
+        self.selector = f"{JOB_LABEL}={job_name}"
+
+    def list(self) -> List[Node]:
+        return [pod_to_node(p) for p in self.client.list_pods(self.selector)]
+
+    def watch(self) -> Iterator[NodeEvent]:
+        for ev in self.client.watch_pods(self.selector):
+            t = ev.get("type", NodeEventType.MODIFIED)
+            yield NodeEvent(t, pod_to_node(ev.get("object", {})))
+
+
+# ----------------------------------------------------------------------------- operator
+
+
+class ElasticJobOperator:
+    """Reconciles ``ElasticJob`` and ``ScalePlan`` custom objects."""
+
+    def __init__(self, client: K8sClient, master_image: str, master_port: int = 50001):
+        self.client, self.image, self.port = client, master_image, master_port
+        self._stop = threading.Event()
+
+    def master_pod(self, job: Dict) -> Dict:
+        name = job["metadata"]["name"]
+        spec = job.get("spec", {})
+        workers = spec.get("replicaSpecs", {}).get("worker", {}).get("replicas", 1)
+        cmd = ["python", "-m", "dlrover_wuqiong_amd.master.master", "--platform", "k8s", "--job_name", name,
+               "--namespace", self.client.ns, "--port", str(self.port), "--node_num", str(workers)]
+        return {"apiVersion": "v1", "kind": "Pod",
+                "metadata": {"name": f"elasticjob-{name}-dlrover-master",
+                             "labels": {JOB_LABEL: name, TYPE_LABEL: NodeType.MASTER},
+                             "ownerReferences": [{"apiVersion": f"{GROUP}/{VERSION}", "kind": "ElasticJob",
+                                                  "name": name, "uid": job["metadata"].get("uid", "")}]},
+                "spec": {"restartPolicy": "Never",
+                         "containers": [{"name": "master", "image": self.image, "command": cmd,
+                                         "ports": [{"containerPort": self.port}]}]}}
+
+    def master_service(self, job: Dict) -> Dict:
+        name = job["metadata"]["name"]
+        return {"apiVersion": "v1", "kind": "Service",
+                "metadata": {"name": f"elasticjob-{name}-dlrover-master", "labels": {JOB_LABEL: name}},
+                "spec": {"selector": {JOB_LABEL: name, TYPE_LABEL: NodeType.MASTER},
+                         "ports": [{"port": self.port, "targetPort": self.port}]}}
+
+    def reconcile_job(self, job: Dict):
+        name = job["metadata"]["name"]
+        mname = f"elasticjob-{name}-dlrover-master"
+        pod = self.client.get_pod(mname)
+        phase = (job.get("status") or {}).get("phase", "")
+        if pod is None:
+            if phase in ("Succeeded", "Failed"):
+                return
+            logger.info(f"operator: creating master of ElasticJob {name}")
+            self.client.create_pod(self.master_pod(job))
+            if self.client.get_service(mname) is None:
+                self.client.create_service(self.master_service(job))
+            self.client.patch_custom_status("elasticjobs", name, {"phase": "Pending"})
+            return
+        pphase = (pod.get("status") or {}).get("phase", "Pending")
+        new = {"Pending": "Pending", "Running": "Running", "Succeeded": "Succeeded", "Failed": "Failed"}.get(pphase)
+        if new and new != phase:
+            self.client.patch_custom_status("elasticjobs", name, {"phase": new})
+
+    def reconcile_scaleplan(self, plan: Dict):
+        st = plan.get("status") or {}
+        if st.get("phase") == "Succeeded":
+            return
+        spec = plan.get("spec", {})
+        job = spec.get("ownerJob")
+        rs = spec.get("replicaResourceSpecs", {})
+        patch = {"spec": {"replicaSpecs": {t: {"replicas": int(v.get("replicas", 0))} for t, v in rs.items()}}}
+        if job and rs:
+            self.client.patch_custom("elasticjobs", job, patch)
+        self.client.patch_custom_status("scaleplans", plan["metadata"]["name"], {"phase": "Succeeded"})
+
+    def reconcile_once(self):
+        for job in self.client.list_custom("elasticjobs"):
+            self.reconcile_job(job)
+        for plan in self.client.list_custom("scaleplans"):
+            self.reconcile_scaleplan(plan)
+
+    def run(self, interval: float = 5.0):
+        while not self._stop.is_set():
+            try:
+                self.reconcile_once()
+            except Exception as e:  # keep reconciling through API hiccups
+                logger.warning(f"operator reconcile failed: {e}")
+            self._stop.wait(interval)
+
+    def stop(self):
+        self._stop.set()
+
+
+def main(argv=None):
+    import argparse
+
+    p = argparse.ArgumentParser("dwamd-operator")
+    p.add_argument("--namespace", default="default")
+    p.add_argument("--master-image", required=True)
+    p.add_argument("--interval", type=float, default=5.0)
+    a = p.parse_args(argv)
+    ElasticJobOperator(K8sClient(a.namespace), a.master_image).run(a.interval)
+
+
+if __name__ == "__main__":
+    main()
