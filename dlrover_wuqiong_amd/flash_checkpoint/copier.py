@@ -21,6 +21,7 @@ Reference behaviour being replaced: per-tensor synchronous
 """
 
 import ctypes
+import os
 import threading
 import time
 from concurrent.futures import Future, ThreadPoolExecutor
@@ -178,35 +179,81 @@ class GpuCopier:
         self.flush_blocks = int(os.environ.get("DWAMD_FLUSH_BLOCKS", "64"))
         self.flush_stats: List[Tuple[int, float]] = []
         self.pinned = PinnedRegistry()
-        self._staging: Optional[torch.Tensor] = None
+        # Snapshot staging in HBM.  Two buffers when the card has room (288 GB
+        # MI355X: a 22 GB GPT2-1.5B state twice is nothing): snapshot k+1 then
+        # never waits for the PCIe flush of snapshot k -- the flushes queue on
+        # the single D2H thread and the training pause is just the HBM copy.
+        # One buffer (the old wait-for-flush behaviour) when memory is tight.
+        self._stagings: List[Optional[torch.Tensor]] = [None, None]
+        self._futures: List[Optional[Future]] = [None, None]
+        self._nbuf = 0  # decided at the first snapshot
+        self._next_stage = 0
+        self.staging_reserve = int(os.environ.get("DWAMD_STAGING_RESERVE_GB", "24")) << 30
         self._executor = ThreadPoolExecutor(max_workers=1, thread_name_prefix="dwamd-d2h")
-        self._inflight: Optional[Future] = None
         self._desc_cache = {}
 
+    @property
+    def _staging(self) -> Optional[torch.Tensor]:
+        return self._stagings[0]
+
+    def _alloc(self, idx: int, nbytes: int) -> torch.Tensor:
+        t = self._stagings[idx]
+        if t is None or t.numel() < nbytes:
+            self._stagings[idx] = None
+            t = self._stagings[idx] = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.device)
+        return t
+
     def staging(self, nbytes: int) -> torch.Tensor:
-        if self._staging is None or self._staging.numel() < nbytes:
-            self._staging = None
-            self._staging = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.device)
-        return self._staging
+        """Buffer 0 (restore / gather path)."""
+        self.wait()
+        return self._alloc(0, nbytes)
+
+    def _decide_buffers(self, nbytes: int):
+        if self._nbuf:
+            return
+        nb = 1
+        if os.environ.get("DWAMD_STAGING_BUFFERS", "auto") != "1":
+            try:
+                free, _total = torch.cuda.mem_get_info(self.device)
+                have = sum(t.numel() for t in self._stagings if t is not None)
+                if free + have >= 2 * nbytes + self.staging_reserve:
+                    nb = 2
+            except Exception:
+                nb = 1
+        self._nbuf = nb
 
     def wait(self):
-        f = self._inflight
+        for i, f in enumerate(self._futures):
+            if f is not None:
+                f.result()
+                self._futures[i] = None
+
+    def wait_stage(self):
+        """Wait only for the flush that last used the staging buffer the next
+        snapshot will overwrite (all flushes with one buffer)."""
+        if self._nbuf <= 1:
+            return self.wait()
+        f = self._futures[self._next_stage]
         if f is not None:
             f.result()
-            self._inflight = None
+            self._futures[self._next_stage] = None
 
     def busy(self) -> bool:
-        return self._inflight is not None and not self._inflight.done()
+        return any(f is not None and not f.done() for f in self._futures)
 
     # ----------------------------------------------------------------- save
     def save_slice(self, layout: Layout, shm_payload_addr: int, lo: int, hi: int,
                    on_done: Callable[[], None], sync: bool = False):
         """Snapshot payload bytes [lo, hi) of ``layout`` and flush to shm."""
-        self.wait()  # the staging buffer is reused
         n = hi - lo
+        self._decide_buffers(n)
+        self.wait_stage()  # this staging buffer's previous flush must have landed
+        idx = self._next_stage
+        self._next_stage = (idx + 1) % max(1, self._nbuf)
         cur = torch.cuda.current_stream(self.device)
+        stg = None
         if n > 0:
-            stg = self.staging(n)
+            stg = self._alloc(idx, n)
             base = stg.data_ptr()
             key = (layout.signature, lo, hi, base, tuple(e.src_ptr for e in layout.extents))
             descs = self._desc_cache.get(key)
@@ -214,7 +261,9 @@ class GpuCopier:
                 pieces = [(e.src_ptr + (a - e.offset), base + (a - lo), b - a)
                           for e, a, b in intersect_extents(layout.gpu_extents(), lo, hi)]
                 descs = build_descs(pieces, self.device)
-                self._desc_cache = {key: descs}
+                if len(self._desc_cache) >= 4:  # one entry per staging buffer (+ slack)
+                    self._desc_cache.pop(next(iter(self._desc_cache)))
+                self._desc_cache[key] = descs
             launch_multi_copy(descs, cur)
             # CPU tensors go straight to shm (small: counters, rng state...)
             for e, a, b in intersect_extents(layout.cpu_extents(), lo, hi):
@@ -233,7 +282,7 @@ class GpuCopier:
                     self.side_stream.wait_event(ev)  # device-side dependency only
                     t0 = time.perf_counter()
                     dst = shm_payload_addr + lo
-                    src = self._staging.data_ptr()
+                    src = stg.data_ptr()
                     sp = ctypes.c_void_p(self.side_stream.cuda_stream)
                     segs = self.pinned.split(dst, n) if pinned else [(dst, n, False)]
                     dptr = _kern().dw_host_device_ptr(ctypes.c_void_p(dst)) if (
@@ -255,9 +304,10 @@ class GpuCopier:
             on_done()
 
         if sync:
+            self.wait()
             flush()
         else:
-            self._inflight = self._executor.submit(flush)
+            self._futures[idx] = self._executor.submit(flush)
 
     # ----------------------------------------------------------------- load
     def restore(self, pieces_gpu: List[Tuple[int, int, int]], shm_payload_addr: int, payload_bytes: int,
@@ -319,7 +369,7 @@ class GpuCopier:
         finally:
             self._executor.shutdown(wait=True)
             self.pinned.release_all()
-            self._staging = None
+            self._stagings = [None, None]
             if self._cumask_ptr:
                 self.side_stream.synchronize()
                 _kern().dw_stream_destroy(ctypes.c_void_p(self._cumask_ptr))

@@ -20,6 +20,7 @@ Replicated vs sharded state:
    rank, each rank moves its own shard.
 """
 
+import gc
 import os
 import threading
 import time
@@ -39,6 +40,9 @@ from ..common.storage import CheckpointStorage, get_checkpoint_storage
 from .layout import Layout, TensorMeta, iter_leaves, plan_layout, split_ranges, traverse
 from .shm_handler import (DLROVER_CKPT_CONFIG_KEY, EVENT_QUEUE_SIZE, CheckpointConfig,
                           CheckpointSharedObjPrefix, SharedMemoryHandler, slot_lock_name)
+
+
+_TIMING = os.environ.get("DWAMD_CKPT_TIMING", "0") == "1"  # log per-phase save times
 
 
 class CheckpointEventType:
@@ -157,7 +161,8 @@ class CheckpointEngine(ABC):
         self._copier = None
         self._layout: Optional[Layout] = None
         self._layout_key = None
-        self._lock_held = False
+        self._held_slots = set()  # slots whose lock this process holds until their flush lands
+        self._gc_frozen = False
         self._generation = 0
         self._last_save_blocking = 0.0
         self._notify_agent_to_create_saver()
@@ -264,6 +269,23 @@ class CheckpointEngine(ABC):
 
     # ----------------------------------------------------------- core save
     def save_state_dict_to_memory(self, state_dict: Dict, conf: CheckpointConfig) -> bool:
+        # The training pause must not absorb a full (generation-2) Python GC
+        # pass, which with a model's worth of tensors, layouts and meta trees
+        # costs ~90 ms: collection is deferred past the snapshot, and after the
+        # first save every long-lived object (model, optimizer, cached layout)
+        # is frozen out of future full collections.
+        enabled = gc.isenabled()
+        gc.disable()
+        try:
+            return self._save_state_dict_to_memory(state_dict, conf)
+        finally:
+            if not self._gc_frozen:
+                gc.freeze()
+                self._gc_frozen = True
+            if enabled:
+                gc.enable()
+
+    def _save_state_dict_to_memory(self, state_dict: Dict, conf: CheckpointConfig) -> bool:
         if not self._replicated and self._local_rank != self.local_shard_id:
             # not a saving rank (e.g. a data-parallel replica of a TP/PP shard):
             # still takes part in the slot vote of the saving ranks
@@ -272,23 +294,34 @@ class CheckpointEngine(ABC):
                 dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self._ctl_group)
             return False
         t0 = time.perf_counter()
+        marks = [("start", t0)] if _TIMING else None
         copier = self._device_copier()
         if copier is not None:
-            copier.wait()  # previous flush must land before the staging buffer is reused
-        self._wait_own_lock_release()
+            # only the flush that used the staging buffer (and shm slot) this
+            # snapshot reuses; with double staging the previous one may still run
+            copier.wait_stage()
+        if self._next_slot is not None:
+            self._wait_own_lock_release(slot=self._next_slot)
+        if marks is not None:
+            marks.append(("wait_prev", time.perf_counter()))
 
         layout = self._plan(state_dict)
         self._ensure_shm(layout.total_bytes)
+        if marks is not None:
+            marks.append(("plan+shm", time.perf_counter()))
         h = self._shm_handler
         if self._next_slot is None:
             # first save of this process (nothing in flight): never the latest complete slot
             self._next_slot = h.write_slot()
         slot = self._choose_slot(h, bool(state_dict))
+        if marks is not None:
+            marks.append(("slot", time.perf_counter()))
         if slot < 0:
             logger.info(f"rank {self._rank} skips the memory checkpoint of step {conf.step}: "
                         "the agent is persisting the in-memory checkpoints")
             return False
-        self._lock_held = self._is_shard_owner
+        if self._is_shard_owner:
+            self._held_slots.add(slot)
         self._next_slot = (slot + 1) % h.num_slots
 
         conf.rank = self._rank
@@ -315,6 +348,10 @@ class CheckpointEngine(ABC):
             on_done()
         self._cached_step = step
         self._last_save_blocking = time.perf_counter() - t0
+        if marks is not None:
+            marks.append(("snapshot", time.perf_counter()))
+            logger.info("ckpt save phases (ms): " + ", ".join(
+                f"{n}={1000 * (t - marks[i][1]):.1f}" for i, (n, t) in enumerate(marks[1:])))
         self._replica_manager.backup(self._shm_handler)
         return True
 
@@ -366,7 +403,7 @@ class CheckpointEngine(ABC):
 
     def _release_when_complete(self, step: int, slot: int):
         """Shard owner: keep the slot lock until every slice holds ``step``."""
-        if not self._lock_held:
+        if slot not in self._held_slots:
             return
         h = self._shm_handler
         deadline = time.time() + self._save_timeout
@@ -376,7 +413,7 @@ class CheckpointEngine(ABC):
                 if all(s == step for s in h.slice_steps(slot, self._num_slices)):
                     break
                 time.sleep(0.0005)
-            self._lock_held = False
+            self._held_slots.discard(slot)
             self._shm_locks[slot].release()
 
         if self._num_slices <= 1:
@@ -384,9 +421,11 @@ class CheckpointEngine(ABC):
         else:
             threading.Thread(target=_wait, daemon=True, name="dwamd-ckpt-unlock").start()
 
-    def _wait_own_lock_release(self, timeout: float = 600.0):
+    def _wait_own_lock_release(self, timeout: float = 600.0, slot: Optional[int] = None):
+        """Wait until this process no longer holds ``slot``'s lock (any slot
+        when None), i.e. the snapshot written there has fully landed."""
         deadline = time.time() + timeout
-        while self._lock_held and time.time() < deadline:
+        while time.time() < deadline and (self._held_slots if slot is None else slot in self._held_slots):
             time.sleep(0.0005)
 
     def wait_for_memory_save(self):
