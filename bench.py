@@ -206,6 +206,9 @@ def main():
     loss_v = float(loss.float().item())
 
     # ---------------- load (restore from shm into live tensors)
+    # untimed snapshot of the final state, so the restore can be verified bit-exact
+    if not save_times or (args.steps - 1) % args.ckpt_interval != 0:
+        save()
     ckpt.wait_latest_checkpoint()
     sync_all(device)
     third = opt.master if opt.master is not None else opt.exp_avg_sq
