@@ -91,7 +91,10 @@ def main():
     os.environ.setdefault("LOCAL_WORLD_SIZE", str(world))
     os.environ.setdefault("DWAMD_SHM_PREFIX", f"bench{os.getpid() if world == 1 else os.environ.get('MASTER_PORT', '0')}")
     cuda = torch.cuda.is_available()
-    device = torch.device("cuda", local_rank) if cuda else torch.device("cpu")
+    # rehearsal knobs (never set by the driver): several ranks on one GPU over gloo
+    dev_idx = int(os.environ.get("DWAMD_BENCH_DEVICE", local_rank))
+    backend = os.environ.get("DWAMD_BENCH_BACKEND", "nccl" if cuda else "gloo")
+    device = torch.device("cuda", dev_idx) if cuda else torch.device("cpu")
     if cuda:
         torch.cuda.set_device(device)
         if os.environ.get("DWAMD_COMPUTE_STREAM", "1") == "1":
@@ -99,7 +102,7 @@ def main():
             # stream, which implicitly serialises with every blocking stream)
             torch.cuda.set_stream(torch.cuda.Stream(device))
     if world > 1:
-        dist.init_process_group("nccl" if cuda else "gloo", device_id=device if cuda else None)
+        dist.init_process_group(backend, device_id=device if (cuda and backend == "nccl") else None)
 
     from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
     from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
@@ -213,6 +216,15 @@ def main():
     sync_all(device)
     third = opt.master if opt.master is not None else opt.exp_avg_sq
     ref_sum = flat.data.float().sum().item(), opt.exp_avg.sum().item(), third.sum().item()
+    # replicated (DDP) state must be bit-identical across ranks: the node's one
+    # checkpoint copy is assembled from every local rank's slice
+    replicas_identical = True
+    if world > 1:
+        chk = torch.tensor([ref_sum[0], ref_sum[2]], dtype=torch.float64, device=device)
+        lo_, hi_ = chk.clone(), chk.clone()
+        dist.all_reduce(lo_, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi_, op=dist.ReduceOp.MAX)
+        replicas_identical = bool(torch.equal(lo_, hi_))
     flat.data.zero_()
     opt.exp_avg.zero_()
     third.zero_()
@@ -241,17 +253,21 @@ def main():
             store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world,
                                   is_master=False, timeout=__import__("datetime").timedelta(seconds=300))
             pstore = dist.PrefixStore("dwamd_recover_1", store)
-            dist.init_process_group("nccl" if cuda else "gloo", store=pstore, rank=rank, world_size=world,
-                                    device_id=device if cuda else None)
+            dist.init_process_group(backend, store=pstore, rank=rank, world_size=world,
+                                    device_id=device if (cuda and backend == "nccl") else None)
             ddp.pg = None
             ckpt.close()
             ckpt = DdpCheckpointer(os.path.join(args.ckpt_dir, f"w{world}"))
         flat.data.zero_()  # the restarted rank has lost its GPU state
         ckpt.load_checkpoint(target=state())
-        train_step()  # first useful step after recovery
         if cuda:
             torch.cuda.synchronize()
-        recover_sec = time.perf_counter() - t0 - step_sec  # exclude the useful step itself
+        t1 = time.perf_counter()
+        train_step()  # first useful step after recovery (lazy communicator init lands here)
+        if cuda:
+            torch.cuda.synchronize()
+        # re-form + restore, plus whatever the first step costs beyond a normal step
+        recover_sec = (t1 - t0) + max(0.0, time.perf_counter() - t1 - step_sec)
         recover_sec = max_over_ranks(recover_sec, device)
         useful = args.steps * step_sec
         goodput = 100.0 * useful / (t_timed + recover_sec)
@@ -291,6 +307,7 @@ def main():
         "load_sec": round(load_sec, 4),
         "load_vs_baseline": round(load_sec / REF_LOAD_SEC, 4) if args.model == "gpt2-1.5b" else None,
         "load_verified": load_ok,
+        "replicas_identical": replicas_identical,
         "recover_sec": round(recover_sec, 3),
         "goodput_pct": round(goodput, 2) if goodput is not None else None,
         "goodput_pct_1fail_per_hour": round(goodput_1h, 3),

@@ -7,9 +7,12 @@ into it themselves -- weight GEMMs with ``addmm_`` (beta = 1: the hipBLASLt
 epilogue does the add), bias / norm-weight reductions with an accumulating
 finish kernel -- and return ``None`` to autograd.  That removes one
 elementwise ``grad += g`` pass per parameter per micro-batch (hundreds of
-kernels per step) and the temporary ``g``.  ``_dwamd_grad_ready`` (set by
-``FlatDDP``) is then invoked so bucketed all-reduce still starts as soon as
-a bucket's gradients are final.
+kernels per step) and the temporary ``g``.  Autograd still fires the
+parameter's post-accumulate hook after the op's backward returns (the grad
+it hands over is undefined), which is what ``FlatDDP`` counts.  The optional
+``_dwamd_grad_ready`` callback is an extra, earlier readiness signal for
+code that wants it; ``FlatDDP`` deliberately does not use it (it would count
+each parameter twice).
 """
 
 from typing import Optional

@@ -11,6 +11,16 @@ Bucket sizing for MI355X: an 8-GPU node is a fully connected xGMI mesh
 large buckets (default 128 MiB) amortise the per-collective latency while
 still leaving several buckets to overlap with backward.
 
+Readiness is counted, not assumed: the first synchronised backward only
+records how many times each parameter's hook fires (PyTorch fires the
+post-accumulate hook once per backward even for the fused ops that write the
+flat gradient themselves and return ``None``; a parameter shared by two ops
+fires twice) and reduces every bucket at ``finish_gradient_sync``.  Later
+backwards launch a bucket when all of its recorded hook calls have arrived.
+Buckets holding a parameter that was unused in the calibration pass are never
+launched early (an MoE expert may get tokens later), and a gradient arriving
+for an already-launched bucket raises instead of being silently dropped.
+
 Gradients are SUMMED; the optimizer divides by the world size inside its
 fused update (``grad_scale``), in fp32, instead of a separate scaling pass.
 
@@ -45,14 +55,14 @@ class FlatDDP(nn.Module):
         self._pending: List[int] = []
         self._works: List[Optional[object]] = []
         self._sync = True
+        self._expected: Optional[List[int]] = None  # hook calls per parameter per backward
+        self._calls = [0] * len(flat.params)
         self._reset()
         if self.world > 1:
             if broadcast_params:
                 dist.broadcast(flat.data, src=self._global_src(), group=process_group)
             for i, p in enumerate(flat.params):
-                hook = self._make_hook(i)
-                p.register_post_accumulate_grad_hook(hook)
-                p._dwamd_grad_ready = hook  # fused ops that accumulate directly (ops/_grad.py)
+                p.register_post_accumulate_grad_hook(self._make_hook(i))
 
     def _global_src(self):
         if self.pg is None:
@@ -60,18 +70,31 @@ class FlatDDP(nn.Module):
         return dist.get_global_rank(self.pg, 0)
 
     def _reset(self):
-        self._pending = [len(idxs) for (_s, _e, idxs) in self.buckets]
+        self._calls = [0] * len(self.flat.params)
         self._works = [None] * len(self.buckets)
+        if self._expected is None:
+            self._pending = [-1] * len(self.buckets)  # calibration pass: never launch early
+            return
+        self._pending = []
+        for (_s, _e, idxs) in self.buckets:
+            exp = [self._expected[i] for i in idxs]
+            self._pending.append(sum(exp) if all(exp) else -1)
 
     def _make_hook(self, idx):
         def hook(_p):
             if not self._sync:
                 return
+            self._calls[idx] += 1
             b = self._bucket_of[idx]
-            self._pending[b] -= 1
-            if self._pending[b] == 0:
-                s, e, _ = self.buckets[b]
-                self._works[b] = dist.all_reduce(self.flat.grad[s:e], group=self.pg, async_op=True)
+            if self._works[b] is not None:
+                raise RuntimeError(
+                    f"FlatDDP: gradient of parameter {idx} arrived after its bucket {b} was reduced "
+                    "(the parameter is used more often than in the first backward)")
+            if self._pending[b] > 0:
+                self._pending[b] -= 1
+                if self._pending[b] == 0:
+                    s, e, _ = self.buckets[b]
+                    self._works[b] = dist.all_reduce(self.flat.grad[s:e], group=self.pg, async_op=True)
         return hook
 
     def forward(self, *args, **kwargs):
@@ -92,6 +115,8 @@ class FlatDDP(nn.Module):
         buckets holding unused parameters)."""
         if self.world <= 1:
             return
+        if self._expected is None:
+            self._expected = list(self._calls)
         for b, (s, e, _) in enumerate(self.buckets):
             if self._works[b] is None:
                 self._works[b] = dist.all_reduce(self.flat.grad[s:e], group=self.pg, async_op=True)

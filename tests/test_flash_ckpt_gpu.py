@@ -129,3 +129,130 @@ def test_gpu_fsdp2_shard_checkpoint(tmp_path, monkeypatch):
         ck.close()
     finally:
         dist.destroy_process_group()
+
+
+def _two_rank_worker(rank, port, q, nbuf):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE="2", DWAMD_STAGING_BUFFERS=nbuf)
+    try:
+        from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+        from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=2)
+        model, opt, flat = _model_and_opt()
+        ck = DdpCheckpointer(os.environ["CKDIR"])
+        state = lambda: {"model": model.state_dict(), "opt": opt.state_dict()}  # noqa
+        for step in (1, 2, 3):  # several saves: both slots / staging buffers in play
+            opt.exp_avg.add_(step)
+            assert ck.save_checkpoint(step, state(), storage_type=StorageType.MEMORY)
+        ck.wait_latest_checkpoint()
+        dist.barrier()
+        ref = [t.clone() for t in (flat.data, opt.exp_avg, opt.master)]
+        ck.engine._copier.pinned.release_all()  # cold restore, as after a restart
+        flat.data.zero_()
+        opt.exp_avg.fill_(7.0)
+        opt.master.zero_()
+        ck.load_checkpoint(target=state())
+        torch.cuda.synchronize()
+        bad = [i for i, (a, b) in enumerate(zip(ref, (flat.data, opt.exp_avg, opt.master))) if not torch.equal(a, b)]
+        q.put((rank, bad))
+        ck.close()
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        traceback.print_exc()
+        q.put((rank, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("nbuf", ["1", "auto"])
+def test_gpu_two_rank_sliced_save_gathered_restore(tmp_path, nbuf):
+    """Replicated (DDP) state: each local rank snapshots / flushes half of the
+    node copy, restore = half H2D per rank + all-gather.  Two ranks share the
+    one GPU over gloo (RCCL refuses two ranks per device)."""
+    import torch.multiprocessing as mp
+
+    from conftest import free_port
+
+    os.environ["CKDIR"] = str(tmp_path / "ck")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_two_rank_worker, args=(r, port, q, nbuf)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res == [(0, []), (1, [])], res
+
+
+def _ddp_worker(rank, port, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2")
+    try:
+        from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
+        from dlrover_wuqiong_amd.parallel.ddp import FlatDDP
+        from dlrover_wuqiong_amd.parallel.flat import FlatParams
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=2)
+        torch.cuda.set_stream(torch.cuda.Stream())  # as bench.py: a dedicated compute stream
+        cfg = GPT2Config.named("gpt2-tiny")
+        res = {}
+        for mode in ("manual", "ddp"):
+            torch.manual_seed(0)
+            with torch.device("cuda"):
+                model = GPT2(cfg)
+            model.to(torch.bfloat16)
+            flat = FlatParams(model)
+            ddp = FlatDDP(model, flat, bucket_mb=1) if mode == "ddp" else None
+            for step in range(2):  # step 0 calibrates the hook counts, step 1 overlaps
+                flat.zero_grad()
+                g = torch.Generator().manual_seed(100 + 10 * step + rank)
+                x = torch.randint(0, cfg.vocab_size, (2, 129), generator=g).cuda()
+                loss = (ddp or model)(x[:, :-1], x[:, 1:])
+                loss.backward()
+                if ddp is not None:
+                    ddp.finish_gradient_sync()
+                else:
+                    torch.cuda.synchronize()
+                    dist.all_reduce(flat.grad)
+                torch.cuda.synchronize()
+                res[(mode, step)] = flat.grad.float().clone()
+        diff = max(float((res[("ddp", s)] - res[("manual", s)]).abs().max()) for s in range(2))
+        q.put((rank, diff))
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        traceback.print_exc()
+        q.put((rank, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_gpu_flat_ddp_bucketed_allreduce_matches_manual_sum():
+    """FlatDDP's hook-launched bucket all-reduce must equal an all-reduce of
+    the finished local gradients (catches buckets launched before every
+    gradient of the bucket has landed)."""
+    import torch.multiprocessing as mp
+
+    from conftest import free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_ddp_worker, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert all(isinstance(d, float) and d == 0.0 for _, d in res), res
