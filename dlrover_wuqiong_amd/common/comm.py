@@ -365,5 +365,32 @@ class ElasticRunConfig(Message):
     configs: Dict[str, str] = field(default_factory=dict)
 
 
+@message
+class ClusterVersionRequest(Message):
+    task_type: str = ""
+    task_id: int = 0
+    version_type: str = ""
+
+
+@message
+class ClusterVersion(Message):
+    task_type: str = ""
+    task_id: int = 0
+    version_type: str = ""
+    version: int = 0
+
+
+@message
+class PsNodesRequest(Message):
+    pass
+
+
+@message
+class PsNodes(Message):
+    nodes: List[Any] = field(default_factory=list)
+    new_ps_ready: bool = False
+    ps_failure: bool = False
+
+
 def is_message(x) -> bool:
     return isinstance(x, Message) and is_dataclass(x)

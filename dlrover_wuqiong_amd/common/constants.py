@@ -17,6 +17,12 @@ class NodeType:
     EVALUATOR = "evaluator"
 
 
+class PSClusterVersionType:
+    GLOBAL = "GLOBAL"
+    LOCAL = "LOCAL"
+    RESTORED = "RESTORED"
+
+
 class NodeStatus:
     INITIAL = "Initial"
     PENDING = "Pending"

@@ -209,6 +209,20 @@ class MasterClient:
     def need_to_restart_training(self) -> bool:
         return self._get(comm.CheckHardwareResetRequest()).success
 
+    # ------------------------------------------------ elastic PS versions
+    def get_cluster_version(self, version_type: str, task_type: str, task_id: int) -> int:
+        return int(self._get(comm.ClusterVersionRequest(task_type=task_type, task_id=task_id,
+                                                        version_type=version_type)).version)
+
+    def update_cluster_version(self, version_type: str, version: int, task_type: str, task_id: int):
+        return self._report(comm.ClusterVersion(task_type=task_type, task_id=task_id, version_type=version_type,
+                                                version=version))
+
+    def query_ps_nodes(self):
+        """(ps NodeMeta list, all new PS running, some PS failed)."""
+        r = self._get(comm.PsNodesRequest())
+        return r.nodes, r.new_ps_ready, r.ps_failure
+
     def get_elastic_run_config(self) -> Dict[str, str]:
         return dict(self._get(comm.ElasticRunConfigRequest()).configs)
 

@@ -55,6 +55,25 @@ class TaskRescheduleCallback(NodeEventCallback):
             self._task_manager.recover_tasks(node.id)
 
 
+class PsClusterVersionCallback(NodeEventCallback):
+    """A PS that fails or is removed changes the PS cluster: bump the global
+    cluster version so workers rebuild their sessions (reference
+    ``event_callback.py:186,199``)."""
+
+    def __init__(self, elastic_ps):
+        self._ps = elastic_ps
+
+    @NodeEventCallback.log_callback_exception
+    def on_node_failed(self, node, cluster_context=None):
+        if node.type == NodeType.PS:
+            self._ps.inc_global_cluster_version()
+
+    @NodeEventCallback.log_callback_exception
+    def on_node_deleted(self, node, cluster_context=None):
+        if node.type == NodeType.PS:
+            self._ps.inc_global_cluster_version()
+
+
 class AllReduceNodeHandlingCallback(NodeEventCallback):
     """Keeps rendezvous membership in sync with node life-cycle and stops the
     job when a critical node fails for good or too many workers failed."""

@@ -100,7 +100,7 @@ class DistributedJobMaster(JobMaster):
                  heartbeat_timeout: float = 300.0, node_unit: int = 1, auto_worker: bool = False,
                  stats_path: str = ""):
         from .dist_job_manager import DistributedJobManager
-        from .event_callback import AllReduceNodeHandlingCallback, TaskRescheduleCallback
+        from .event_callback import AllReduceNodeHandlingCallback, PsClusterVersionCallback, TaskRescheduleCallback
         from .stats import JobMetricCollector, LocalStatsReporter
         from .watcher import ProcessWatcher
 
@@ -118,6 +118,7 @@ class DistributedJobMaster(JobMaster):
             job_resource.worker_num, job_resource.worker_num, 60, node_unit)
         jm.add_node_event_callback(TaskRescheduleCallback(self.task_manager))
         jm.add_node_event_callback(AllReduceNodeHandlingCallback(self))
+        jm.add_node_event_callback(PsClusterVersionCallback(self.servicer.elastic_ps))
         self.metric_collector = JobMetricCollector(jm, speed, LocalStatsReporter(stats_path))
         self._stop_request = None
 

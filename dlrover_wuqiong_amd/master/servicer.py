@@ -14,8 +14,8 @@ from ..common.constants import NodeStatus, NodeType, RendezvousName
 from ..common.log import logger
 from .job_manager import JobManager
 from .rendezvous import RendezvousManager
-from .services import (DiagnosisManager, ErrorMonitor, KVStoreService, SimpleStrategyGenerator, SpeedMonitor,
-                       SyncService)
+from .services import (DiagnosisManager, ElasticPsService, ErrorMonitor, KVStoreService, SimpleStrategyGenerator,
+                       SpeedMonitor, SyncService)
 from .shard import TaskManager
 
 
@@ -23,7 +23,8 @@ class MasterServicer:
     def __init__(self, job_manager: JobManager, task_manager: TaskManager, speed_monitor: SpeedMonitor,
                  rdzv_managers: Dict[str, RendezvousManager], kv_store: KVStoreService,
                  sync_service: SyncService, error_monitor: Optional[ErrorMonitor] = None,
-                 diagnosis: Optional[DiagnosisManager] = None, run_configs: Optional[Dict[str, str]] = None):
+                 diagnosis: Optional[DiagnosisManager] = None, run_configs: Optional[Dict[str, str]] = None,
+                 elastic_ps: Optional[ElasticPsService] = None):
         self.job_manager = job_manager
         self.task_manager = task_manager
         self.speed_monitor = speed_monitor
@@ -34,6 +35,7 @@ class MasterServicer:
         self.diagnosis = diagnosis or DiagnosisManager(speed_monitor)
         self.strategy = SimpleStrategyGenerator()
         self.run_configs = run_configs or {}
+        self.elastic_ps = elastic_ps or ElasticPsService()
         self._paral_configs: Dict[int, comm.ParallelConfig] = {}
         self._start_training_time = 0.0
 
@@ -109,7 +111,24 @@ class MasterServicer:
         if isinstance(m, comm.GlobalStep):
             return comm.GlobalStep(step=self.speed_monitor.completed_global_step,
                                    timestamp=int(self.speed_monitor.last_step_time()))
+        if isinstance(m, comm.ClusterVersionRequest):
+            return comm.ClusterVersion(task_type=m.task_type, task_id=m.task_id, version_type=m.version_type,
+                                       version=self.elastic_ps.get_version(m.task_type, m.version_type, m.task_id))
+        if isinstance(m, comm.PsNodesRequest):
+            return self._ps_nodes()
         return comm.Response(success=False, reason=f"unknown get request {type(m).__name__}")
+
+    def _ps_nodes(self) -> comm.PsNodes:
+        """The PS cluster workers should connect to (reference
+        ``servicer.py:_query_ps_nodes``): alive PS by rank, whether all of
+        them are running, and whether one has failed."""
+        ps_nodes = sorted(getattr(self.job_manager, "job_nodes", {}).get(NodeType.PS, {}).values(), key=lambda n: n.rank_index)
+        alive = [n for n in ps_nodes if not n.is_released and n.status not in (NodeStatus.FAILED, NodeStatus.DELETED)]
+        metas = [comm.NodeMeta(type=NodeType.PS, id=n.id, rank=n.rank_index, addr=n.host_addr, status=n.status)
+                 for n in alive]
+        ready = bool(alive) and all(n.status == NodeStatus.RUNNING for n in alive)
+        failed = any(n.status == NodeStatus.FAILED for n in ps_nodes)
+        return comm.PsNodes(nodes=metas, new_ps_ready=ready, ps_failure=failed)
 
     def _join_rendezvous(self, m: comm.JoinRendezvousRequest, nid: int):
         name = m.rdzv_name or RendezvousName.ELASTIC_TRAINING
@@ -180,6 +199,8 @@ class MasterServicer:
             ok = self.rdzv[RendezvousName.ELASTIC_TRAINING].sync_ckpt_nodes(nid, m.step)
         elif isinstance(m, comm.DiagnosisReport):
             self.diagnosis.collect(m.node_id or nid, m.data_cls, m.data_content, m.timestamp or None)
+        elif isinstance(m, comm.ClusterVersion):
+            ok = self.elastic_ps.update_version(m.task_type, m.version_type, m.task_id, m.version)
         elif isinstance(m, comm.RendezvousParams):
             for r in self.rdzv.values():
                 r.update_rdzv_params(m.min_nodes, m.max_nodes, m.waiting_timeout, m.node_unit)

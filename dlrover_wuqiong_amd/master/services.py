@@ -16,7 +16,7 @@ import time
 from collections import deque
 from typing import Dict, List, Optional, Set, Tuple
 
-from ..common.constants import TrainingExceptionLevel
+from ..common.constants import NodeType, PSClusterVersionType, TrainingExceptionLevel
 from ..common.log import logger
 
 
@@ -224,3 +224,60 @@ class SimpleStrategyGenerator:
         return ParallelConfig(dataloader=DataLoaderConfig(version=version + 1, batch_size=new_bs,
                                                           last_batch_size=batch_size),
                               optimizer=OptimizerConfig(version=version + 1))
+
+
+class ElasticPsService:
+    """Cluster versions for elastic parameter-server training.
+
+    The *global* version counts PS-set changes (bumped by the master when a
+    PS fails or is removed); each PS and worker reports the *local* version it
+    is running with, and a worker the *restored* version its model state came
+    from, so workers know when to rebuild their PS sessions.
+
+    Parity: reference ``master/elastic_training/elastic_ps.py``
+    (``ElasticPsService``) and ``servicer.py:173-187,478-490``.
+    """
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self.global_version = 0
+        self._ps_local: Dict[int, int] = {}
+        self._worker_local: Dict[int, int] = {}
+        self._worker_restored: Dict[int, int] = {}
+
+    def inc_global_cluster_version(self) -> int:
+        with self._lock:
+            self.global_version += 1
+            logger.info(f"PS cluster global version -> {self.global_version}")
+            return self.global_version
+
+    def get_version(self, task_type: str, version_type: str, task_id: int) -> int:
+        V = PSClusterVersionType
+        with self._lock:
+            if version_type == V.GLOBAL:
+                return self.global_version
+            if task_type == NodeType.PS and version_type == V.LOCAL:
+                return self._ps_local.get(task_id, 0)
+            if task_type == NodeType.WORKER and version_type == V.LOCAL:
+                return self._worker_local.get(task_id, 0)
+            if task_type == NodeType.WORKER and version_type == V.RESTORED:
+                return self._worker_restored.get(task_id, -1)
+        logger.warning(f"unsupported cluster version query {task_type}/{version_type}")
+        return 0
+
+    def update_version(self, task_type: str, version_type: str, task_id: int, version: int) -> bool:
+        V = PSClusterVersionType
+        with self._lock:
+            if version_type == V.GLOBAL:
+                self.global_version = version
+            elif task_type == NodeType.PS and version_type == V.LOCAL:
+                self._ps_local[task_id] = version
+            elif task_type == NodeType.WORKER and version_type == V.LOCAL:
+                self._worker_local[task_id] = version
+            elif task_type == NodeType.WORKER and version_type == V.RESTORED:
+                self._worker_restored[task_id] = version
+            else:
+                logger.warning(f"unsupported cluster version update {task_type}/{version_type}")
+                return False
+        return True
+

@@ -190,3 +190,28 @@ def test_shard_checkpoint_restore():
     while tm2.get_dataset_task(0, "d") is not None:
         n += 1
     assert n == 10  # the in-flight shard is included
+
+
+def test_elastic_ps_cluster_versions(master):
+    """Parity: reference tests/test_elastic_ps.py + servicer cluster-version RPCs."""
+    from dlrover_wuqiong_amd.common.constants import NodeType, PSClusterVersionType as V
+    from dlrover_wuqiong_amd.common.node import Node
+    from dlrover_wuqiong_amd.elastic_agent.master_client import MasterClient
+    from dlrover_wuqiong_amd.master.event_callback import PsClusterVersionCallback
+
+    c = MasterClient(master.addr, node_id=0, node_type=NodeType.WORKER, retries=2, retry_interval=0.1)
+    assert c.get_cluster_version(V.GLOBAL, NodeType.WORKER, 0) == 0
+    assert c.get_cluster_version(V.RESTORED, NodeType.WORKER, 0) == -1
+    c.update_cluster_version(V.LOCAL, 3, NodeType.PS, 1)
+    c.update_cluster_version(V.LOCAL, 2, NodeType.WORKER, 0)
+    c.update_cluster_version(V.RESTORED, 1, NodeType.WORKER, 0)
+    assert c.get_cluster_version(V.LOCAL, NodeType.PS, 1) == 3
+    assert c.get_cluster_version(V.LOCAL, NodeType.WORKER, 0) == 2
+    assert c.get_cluster_version(V.RESTORED, NodeType.WORKER, 0) == 1
+    # a failed PS bumps the global version
+    cb = PsClusterVersionCallback(master.servicer.elastic_ps)
+    cb.on_node_failed(Node(NodeType.PS, 5))
+    cb.on_node_failed(Node(NodeType.WORKER, 6))
+    assert c.get_cluster_version(V.GLOBAL, NodeType.PS, 1) == 1
+    nodes, ready, failed = c.query_ps_nodes()
+    assert nodes == [] and not ready and not failed
