@@ -34,8 +34,9 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 template <int D>
 struct Fwd2Cfg {
-  // D=128: 8 waves share each K/V tile (MFMA-bound, maximise reuse);
-  // D=64: softmax (VALU) bound -> 4-wave blocks, 3 blocks per CU
+  // 8 waves share each K/V tile.  D=128 (236 VGPRs) runs one block per CU;
+  // causal D=64 is instantiated with MINW=4 (<=128 VGPRs) so two blocks share
+  // a CU and one block's softmax overlaps the other's MFMAs.
   static constexpr int WAVES = 8;
   static constexpr int BQ = 32 * WAVES;  // queries per block
   static constexpr int BK = 64;          // keys per tile
@@ -52,8 +53,8 @@ __device__ __forceinline__ unsigned int pack2(float a, float b) {
   return (unsigned int)f2bf(a) | ((unsigned int)f2bf(b) << 16);
 }
 
-template <int D, bool CAUSAL>
-__global__ void __launch_bounds__(64 * Fwd2Cfg<D>::WAVES, 1)
+template <int D, bool CAUSAL, int MINW = 1>
+__global__ void __launch_bounds__(64 * Fwd2Cfg<D>::WAVES, MINW)
 attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
                 bf16_t* __restrict__ O, float* __restrict__ LSE, int S, int H, int HKV, float scale_log2,
                 AttnStrides st) {
@@ -243,7 +244,13 @@ static void launch_fwd(const void* q, const void* k, const void* v, void* o, voi
   using C = Fwd2Cfg<D>;
   dim3 grid((S + C::BQ - 1) / C::BQ, H, B), block(64 * C::WAVES);
   const int lds = 4 * C::TILE;
-  if (causal)
+  // D=64 causal capped at 128 VGPRs (8 B/lane spill): two blocks per CU,
+  // +9% measured (profiles/attn_bench_latest.jsonl); the non-causal variant
+  // would spill 116 B/lane, so it keeps one block per CU
+  if (causal && D == 64)
+    hipLaunchKernelGGL((attn_fwd_kernel<D, true, 4>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
+                       (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st);
+  else if (causal)
     hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
                        (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st);
   else
