@@ -113,9 +113,10 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int b = blockIdx.z, h = blockIdx.y;
+  const BlockXYZ bc = xcd_block((S + C::BKB - 1) / C::BKB, H);
+  const int b = bc.z, h = bc.y;
   const int hk = h / (H / HKV);
-  const int kb0 = blockIdx.x * C::BKB;  // causal: low key blocks (most queries) dispatch first
+  const int kb0 = bc.x * C::BKB;  // causal: low key blocks (most queries) dispatch first
   const int kw0 = kb0 + 32 * wid;
   const int key = kw0 + r;
   const bf16_t* Qb = Q + (int64_t)b * st.q_bs + (int64_t)h * D;
@@ -363,9 +364,11 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int b = blockIdx.z, h = blockIdx.y;
+  const int nqb = (S + C::BQ - 1) / C::BQ;
+  const BlockXYZ bc = xcd_block(nqb, H);
+  const int b = bc.z, h = bc.y;
   const int hk = h / (H / HKV);
-  const int qblk = CAUSAL ? (int)(gridDim.x - 1 - blockIdx.x) : (int)blockIdx.x;
+  const int qblk = CAUSAL ? nqb - 1 - bc.x : bc.x;
   const int q_blk0 = qblk * C::BQ;
   const int q0 = q_blk0 + wid * 32;
   const int q = q0 + r;
@@ -523,7 +526,7 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
   const bool partial = H != HKV;
   float* pk = (float*)(ws + (((int64_t)B * H * S * 4 + 255) / 256) * 256);
   float* pv = pk + (int64_t)B * S * H * D;
-  dim3 gk((S + KC::BKB - 1) / KC::BKB, H, B);
+  dim3 gk((unsigned)((S + KC::BKB - 1) / KC::BKB * H * B));  // 1-D: xcd_block()
   const int lk = 2 * KC::BUF + KC::VIMG;
 #define DKDV(CA, PA)                                                                                          \
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CA, PA>), gk, dim3(64 * KC::WAVES), lk, s, (const bf16_t*)q,   \
@@ -542,7 +545,7 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
   }
   // query-major dQ
   using DC = DqCfg<D>;
-  dim3 gq((S + DC::BQ - 1) / DC::BQ, H, B);
+  dim3 gq((unsigned)((S + DC::BQ - 1) / DC::BQ * H * B));  // 1-D: xcd_block()
   const int lq = 4 * DC::TILE;
   if (causal)
     hipLaunchKernelGGL((attn_bwd_dq_kernel<D, true>), gq, dim3(64 * DC::WAVES), lq, s, (const bf16_t*)q,

@@ -14,6 +14,29 @@ __device__ __forceinline__ int img_off(int row, int ch) {
   return (D * 16) * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
 }
 
+// Block coordinates of a 1-D launch over nx * ny * nz workgroups (x fastest).
+// Hardware hands consecutive workgroup ids to the 8 XCDs round-robin, and each
+// XCD has a private L2; the remap gives every XCD a contiguous chunk of the
+// logical grid, so the x-blocks of one (head, batch) -- which all stream the
+// same K/V (forward, dQ) or Q/dO (dK/dV) -- meet in one L2 instead of eight
+// (cdna_hip_programming.md T1).  Bijective; a grid not divisible by 8 keeps
+// its tail unmapped.
+struct BlockXYZ {
+  int x, y, z;
+};
+
+__device__ __forceinline__ BlockXYZ xcd_block(int nx, int ny) {
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int cpx = nwg >> 3;
+  const int l = bid < (cpx << 3) ? (bid & 7) * cpx + (bid >> 3) : bid;
+  BlockXYZ r;
+  r.x = l % nx;
+  const int yz = l / nx;
+  r.y = yz % ny;
+  r.z = yz / ny;
+  return r;
+}
+
 __device__ __forceinline__ unsigned int pack_s16(short a, short b) {
   return (unsigned int)(unsigned short)a | ((unsigned int)(unsigned short)b << 16);
 }

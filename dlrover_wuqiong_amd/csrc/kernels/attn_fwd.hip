@@ -63,9 +63,11 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int b = blockIdx.z, h = blockIdx.y;
+  const int nqb = (S + C::BQ - 1) / C::BQ;
+  const BlockXYZ bc = xcd_block(nqb, H);
+  const int b = bc.z, h = bc.y;
   const int hk = h / (H / HKV);
-  const int qblk = CAUSAL ? (int)(gridDim.x - 1 - blockIdx.x) : (int)blockIdx.x;
+  const int qblk = CAUSAL ? nqb - 1 - bc.x : bc.x;  // causal: heaviest query blocks first
   const int q_blk0 = qblk * C::BQ;
   const int q0 = q_blk0 + wid * 32;
   const bf16_t* Qb = Q + (int64_t)b * st.q_bs + (int64_t)h * D;
@@ -242,7 +244,7 @@ template <int D>
 static void launch_fwd(const void* q, const void* k, const void* v, void* o, void* lse, int B, int S, int H, int HKV,
                        int causal, float scale_log2, const AttnStrides& st, hipStream_t s) {
   using C = Fwd2Cfg<D>;
-  dim3 grid((S + C::BQ - 1) / C::BQ, H, B), block(64 * C::WAVES);
+  dim3 grid((unsigned)((S + C::BQ - 1) / C::BQ * H * B)), block(64 * C::WAVES);  // 1-D: xcd_block()
   const int lds = 4 * C::TILE;
   // D=64 causal capped at 128 VGPRs (8 B/lane spill): two blocks per CU,
   // +9% measured (profiles/attn_bench_latest.jsonl); the non-causal variant
