@@ -1,0 +1,196 @@
+"""Flash-checkpoint pause / restore for ONE tensor-parallel rank of a
+Megatron-LM model, in Megatron's checkpoint layout (BASELINE.json config
+"Llama-3 70B Megatron-LM TP=8 checkpoint-format-compatible async save
+(288 GB HBM sizing)").
+
+The state is exactly what TP rank 0 of Llama-3 70B at TP=8 holds with the
+non-distributed mixed-precision optimizer: Megatron-core parameter names and
+per-rank shard shapes (QKV / FC1 column-split, proj / FC2 row-split,
+vocab-split embedding and output layer), bf16 weights, and fp32 main
+params + Adam exp_avg / exp_avg_sq per parameter -- ~8.8 B parameters,
+~123 GB on the one GPU.  Between checkpoints the compute stream runs ~3 s of
+bf16 GEMMs (stand-in for the training steps of one checkpoint interval: one
+70B TP=8 step at 64K tokens is ~3.4 PFLOP per GPU) and nudges the state so
+successive checkpoints differ.  The background flush of the previous
+checkpoint (HBM staging -> pinned shared memory, ~2.2 s for 123 GB) runs
+under that compute; a snapshot only waits for it when the interval is
+shorter than the flush.
+
+Measured: paused time of ``MegatronCheckpointer.save_checkpoint`` (memory
+save; the agent-side persist to ``iter_XXXXXXX/mp_rank_00/model_optim_rng.pt``
+is asynchronous) and the cold in-memory restore into the live GPU tensors,
+verified by checksums.  Synthetic values; one rank of the TP group.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+SHAPES = {
+    "llama3-70b": dict(vocab=128256, hidden=8192, ffn=28672, layers=80, heads=64, kv_heads=8, head_dim=128),
+    "llama3-8b": dict(vocab=128256, hidden=4096, ffn=14336, layers=32, heads=32, kv_heads=8, head_dim=128),
+    "llama-tiny": dict(vocab=1024, hidden=256, ffn=688, layers=2, heads=8, kv_heads=8, head_dim=32),
+}
+
+
+def shard_param_shapes(m, tp):
+    """Megatron-core GPTModel parameter names -> TP-rank shard shapes."""
+    h, hd = m["hidden"], m["head_dim"]
+    qkv = (m["heads"] + 2 * m["kv_heads"]) * hd // tp
+    out = {"embedding.word_embeddings.weight": (m["vocab"] // tp, h)}
+    for i in range(m["layers"]):
+        p = f"decoder.layers.{i}."
+        out[p + "self_attention.linear_qkv.layer_norm_weight"] = (h,)
+        out[p + "self_attention.linear_qkv.weight"] = (qkv, h)
+        out[p + "self_attention.linear_proj.weight"] = (h, m["heads"] * hd // tp)
+        out[p + "mlp.linear_fc1.layer_norm_weight"] = (h,)
+        out[p + "mlp.linear_fc1.weight"] = (2 * m["ffn"] // tp, h)
+        out[p + "mlp.linear_fc2.weight"] = (h, m["ffn"] // tp)
+    out["decoder.final_layernorm.weight"] = (h,)
+    out["output_layer.weight"] = (m["vocab"] // tp, h)
+    return out
+
+
+def build_state(shapes, device):
+    model, main, exp_avg, exp_avg_sq = {}, [], {}, {}
+    for i, (name, shp) in enumerate(shapes.items()):
+        w = torch.empty(shp, dtype=torch.bfloat16, device=device).normal_(0, 0.02)
+        model[name] = w
+        main.append(w.float())
+        exp_avg[i] = torch.empty(shp, dtype=torch.float32, device=device).normal_(0, 1e-3)
+        exp_avg_sq[i] = torch.empty(shp, dtype=torch.float32, device=device).uniform_(0, 1e-6)
+    optim = {
+        "optimizer": {"state": {i: {"exp_avg": exp_avg[i], "exp_avg_sq": exp_avg_sq[i], "step": 0}
+                                for i in exp_avg},
+                      "param_groups": [{"lr": 1.5e-4, "betas": (0.9, 0.95), "eps": 1e-8, "weight_decay": 0.1,
+                                        "params": list(exp_avg)}]},
+        "fp32_from_fp16_params": [main],
+    }
+    return {"model": model, "optimizer": optim, "rng_state": [{"random_rng_state": 0}]}
+
+
+def tensors(sd):
+    if isinstance(sd, torch.Tensor):
+        yield sd
+    elif isinstance(sd, dict):
+        for v in sd.values():
+            yield from tensors(v)
+    elif isinstance(sd, (list, tuple)):
+        for v in sd:
+            yield from tensors(v)
+
+
+def checksum(sd):
+    return float(sum(t.float().sum(dtype=torch.float64).item() for t in tensors(sd)))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--model", default="llama3-70b", choices=sorted(SHAPES))
+    p.add_argument("--tp", type=int, default=8)
+    p.add_argument("--saves", type=int, default=3)
+    p.add_argument("--work-gemms", type=int, default=4000, help="bf16 8192^3 GEMMs between saves (~3.3 s)")
+    p.add_argument("--ckpt-dir", default="/tmp/dwamd_megatron_ckpt")
+    args = p.parse_args()
+    os.environ.setdefault("LOCAL_WORLD_SIZE", "1")
+    os.environ.setdefault("DWAMD_SHM_PREFIX", f"mtp{os.getpid()}")
+    from dlrover_wuqiong_amd.common.constants import CheckpointConstant
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.megatron import MegatronCheckpointer, get_checkpoint_name
+
+    cuda = torch.cuda.is_available()
+    device = torch.device("cuda", 0) if cuda else torch.device("cpu")
+    if cuda:
+        torch.cuda.set_device(device)
+        torch.cuda.set_stream(torch.cuda.Stream(device))
+    m = SHAPES[args.model]
+    shapes = shard_param_shapes(m, args.tp)
+    nparams = sum(int(torch.Size(s).numel()) for s in shapes.values())
+    t0 = time.perf_counter()
+    sd = build_state(shapes, device)
+    nbytes = sum(t.numel() * t.element_size() for t in tensors(sd))
+    print(f"{args.model} TP={args.tp} rank-0 shard: {nparams / 1e9:.2f} B params, {len(shapes)} tensors, "
+          f"{nbytes / 1e9:.1f} GB state, built in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+
+    n = 8192 if cuda else 256
+    a = torch.randn(n, n, dtype=torch.bfloat16 if cuda else torch.float32, device=device)
+    bmat = torch.randn_like(a)
+
+    def work():
+        for _ in range(args.work_gemms):
+            torch.mm(a, bmat)
+        for t in list(tensors(sd["model"]))[:8]:  # the step changes the state
+            t.add_(1e-3)
+
+    ckpt = MegatronCheckpointer(args.ckpt_dir)
+    it = 0
+
+    def save():
+        nonlocal it
+        it += 1
+        ts = time.perf_counter()
+        ok = ckpt.save_checkpoint(it, sd, storage_type=StorageType.MEMORY)
+        if cuda:
+            torch.cuda.current_stream().synchronize()
+        return time.perf_counter() - ts, ok
+
+    # once per job: the first save creates and registers the shared-memory
+    # segment, the second is the first write of the second in-memory slot
+    setup, flush_s = [], 0.0
+    for _ in range(2):
+        setup.append(save()[0])
+        tf = time.perf_counter()
+        ckpt.wait_latest_checkpoint()
+        flush_s = time.perf_counter() - tf
+    print(f"setup saves {[round(x, 2) for x in setup]} s, flush {flush_s:.2f} s", file=sys.stderr, flush=True)
+    pauses, work_s = [], []
+    for _ in range(args.saves):
+        tw = time.perf_counter()
+        work()
+        if cuda:
+            torch.cuda.current_stream().synchronize()
+        work_s.append(time.perf_counter() - tw)
+        pause, ok = save()
+        assert ok, "memory save refused"
+        pauses.append(pause)
+        print(f"save {it}: pause {pause * 1e3:.1f} ms after {work_s[-1]:.2f} s of compute", file=sys.stderr,
+              flush=True)
+    ckpt.wait_latest_checkpoint()
+    if cuda:
+        torch.cuda.synchronize()
+    ref = checksum(sd)
+    for t in tensors(sd):
+        t.zero_()
+    copier = getattr(ckpt.engine, "_copier", None)
+    if copier is not None:
+        copier.pinned.release_all()  # a restarted process has nothing pinned: cold restore
+    if cuda:
+        torch.cuda.synchronize()
+    tl = time.perf_counter()
+    target = {CheckpointConstant.MODEL_STATES_NAME: dict(sd, iteration=it, checkpoint_version=3.0)}
+    step, _restored = ckpt.load_checkpoint(target=target)
+    if cuda:
+        torch.cuda.synchronize()
+    load_s = time.perf_counter() - tl
+    got = checksum(sd)
+    verified = step == it and abs(got - ref) <= 1e-9 * max(1.0, abs(ref))
+    ckpt.close()
+    print(json.dumps({
+        "metric": "megatron tp-shard flash ckpt pause s", "value": round(sum(pauses) / len(pauses), 4), "unit": "s",
+        "higher_is_better": False, "dtype": "bf16 params + fp32 main/Adam", "data": "synthetic values",
+        "config": {"model": f"{args.model} (Megatron-core names)", "parallelism": f"tp{args.tp}: rank 0's shard "
+                   "on one GPU", "layout": os.path.relpath(get_checkpoint_name(args.ckpt_dir, it), args.ckpt_dir)},
+        "params": nparams, "ckpt_bytes": nbytes, "save_sec": [round(x, 4) for x in pauses],
+        "save_sec_max": round(max(pauses), 4), "load_sec": round(load_s, 3), "load_step": step,
+        "load_verified": bool(verified), "compute_between_saves_s": round(sum(work_s) / len(work_s), 2),
+        "setup_saves_s": [round(x, 2) for x in setup], "flush_s": round(flush_s, 2),
+        "shm_slots": 2}))
+
+
+if __name__ == "__main__":
+    main()
