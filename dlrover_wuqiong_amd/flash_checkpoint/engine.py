@@ -428,6 +428,15 @@ class CheckpointEngine(ABC):
         while time.time() < deadline and (self._held_slots if slot is None else slot in self._held_slots):
             time.sleep(0.0005)
 
+    def snapshot_fence(self):
+        """Order the current stream after a pending overlapped snapshot
+        (``DWAMD_OVERLAP_SNAPSHOT=1``).  Optimizer steps do this themselves
+        (global step pre-hook); call it before writing checkpointed tensors
+        any other way between a save and the next optimizer step."""
+        c = getattr(self, "_copier", None)
+        if c is not None:
+            c.fence()
+
     def wait_for_memory_save(self):
         """Block until this process's last snapshot is in shm."""
         if self._copier is not None:

@@ -180,3 +180,28 @@ def test_replicated_split_save_two_ranks(tmp_path):
     for p in ps:
         p.join(timeout=60)
     assert sorted(res) == [(0, True), (1, True)]
+
+
+def test_overlapped_snapshot_fence_runs_before_any_optimizer_step():
+    """copier.py's global optimizer step pre-hook fences pending snapshots
+    (the GPU data path is covered by test_flash_ckpt_gpu.py)."""
+    from dlrover_wuqiong_amd.flash_checkpoint import copier
+
+    copier._install_fence_hook()
+    copier._install_fence_hook()  # idempotent
+
+    class _Pending:
+        fenced = 0
+
+        def fence(self):
+            _Pending.fenced += 1
+
+    p = _Pending()
+    copier._FENCED.add(p)
+    w = torch.nn.Parameter(torch.ones(3))
+    opt = torch.optim.SGD([w], lr=0.1)
+    w.sum().backward()
+    opt.step()
+    assert _Pending.fenced == 1 and len(copier._FENCED) == 0
+    opt.step()
+    assert _Pending.fenced == 1

@@ -61,6 +61,44 @@ def test_gpu_save_and_restore_in_place(tmp_path):
     ck.close()
 
 
+def test_gpu_overlapped_snapshot_is_fenced_by_the_optimizer(tmp_path, monkeypatch):
+    """DWAMD_OVERLAP_SNAPSHOT=1: the snapshot copy runs on its own stream while
+    training continues; the next optimizer step (the first writer of the
+    state) must wait for it, so the checkpoint holds the pre-step state."""
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+    from dlrover_wuqiong_amd.models.gpt2 import GPT2Config
+
+    monkeypatch.setenv("DWAMD_OVERLAP_SNAPSHOT", "1")
+    model, opt, flat = _model_and_opt()
+    cfg = GPT2Config.named("gpt2-tiny")
+    ck = DdpCheckpointer(str(tmp_path / "ck"))
+    state = lambda: {"model": model.state_dict(), "opt": opt.state_dict()}  # noqa
+    for step in (1, 2):
+        torch.cuda.synchronize()
+        ref = flat.data.clone(), opt.exp_avg.clone(), opt.master.clone()
+        assert ck.save_checkpoint(step, state(), storage_type=StorageType.MEMORY)
+        assert ck.engine._copier.overlap and ck.engine._copier._fence_ev is not None
+        # keep training right away: forward/backward read the state, the step writes it
+        x = torch.randint(0, cfg.vocab_size, (2, 65), device="cuda")
+        model(x[:, :-1], x[:, 1:]).backward()
+        opt.step()
+        flat.zero_grad()
+        assert ck.engine._copier._fence_ev is None  # the optimizer's pre-hook fenced it
+        ck.wait_latest_checkpoint()
+        torch.cuda.synchronize()
+        assert not torch.equal(flat.data, ref[0])  # the step did change the state
+    flat.data.zero_()
+    opt.exp_avg.zero_()
+    opt.master.zero_()
+    ck.load_checkpoint(target=state())
+    torch.cuda.synchronize()
+    assert torch.equal(flat.data, ref[0])
+    assert torch.equal(opt.exp_avg, ref[1])
+    assert torch.equal(opt.master, ref[2])
+    ck.close()
+
+
 def test_gpu_save_to_disk_is_torch_loadable(tmp_path):
     import time
 
