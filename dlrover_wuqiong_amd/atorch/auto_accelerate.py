@@ -326,9 +326,20 @@ def _apply_fsdp(ctx, cfg, reshard=True):
         mesh = DeviceMesh("cuda" if torch.cuda.is_available() else "cpu", ranks, mesh_dim_names=("data",))
     model = ctx["model"]
     n = 0
+    done = set()
     for m in list(model.modules()):
-        if classes and isinstance(m, classes):
+        if not classes or id(m) in done:
+            continue
+        # activation checkpointing runs first: shard the CheckpointWrapper, not
+        # the layer inside it.  FSDP(CheckpointWrapper(layer)) casts the layer
+        # inputs to param_dtype once, before the checkpointed region; the
+        # inverted nesting recomputes on uncast fp32 inputs (FSDP2 skips its
+        # input cast in the pre-backward recompute) and the recomputed saved
+        # tensors no longer match the forward ones.
+        inner = getattr(m, "_checkpoint_wrapped_module", None)
+        if isinstance(m, classes) or (inner is not None and isinstance(inner, classes)):
             fully_shard(m, mesh=mesh, mp_policy=mp, reshard_after_forward=reshard)
+            done.update(id(x) for x in m.modules())
             n += 1
     fully_shard(model, mesh=mesh, mp_policy=mp, reshard_after_forward=reshard)
     ctx["fsdp"] = True

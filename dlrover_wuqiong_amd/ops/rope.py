@@ -63,8 +63,24 @@ class _RopeFn(torch.autograd.Function):
         return dx, None, None, None
 
 
+def _table(t, x, pos_ids):
+    # The kernel reads an fp32 [rows, D/2] table.  Callers under FSDP2 mixed
+    # precision get the table re-cast to bf16 as a layer input: upcast it here
+    # (reading a bf16 table as fp32 walks past its end).
+    B, S, NH, D = x.shape
+    if t.dim() != 2 or t.shape[1] != D // 2:
+        raise _hip.HipKernelError(f"rope table shape {tuple(t.shape)} does not match head_dim {D}")
+    if pos_ids is None and t.shape[0] < S:
+        raise _hip.HipKernelError(f"rope table has {t.shape[0]} rows < seq_len {S}")
+    if pos_ids is not None and pos_ids.numel() != B * S:
+        raise _hip.HipKernelError(f"rope pos_ids has {pos_ids.numel()} entries, expected {B * S}")
+    if t.dtype != torch.float32 or not t.is_contiguous() or t.device != x.device:
+        t = t.to(device=x.device, dtype=torch.float32).contiguous()
+    return t
+
+
 def apply_rope(x, cos, sin, pos_ids=None):
-    """x: [B, S, NH, D]; cos/sin: [>=S, D/2] fp32."""
+    """x: [B, S, NH, D]; cos/sin: [>=S, D/2] (fp32; other dtypes upcast)."""
     if _hip.use_hip(x):
-        return _RopeFn.apply(x, cos, sin, pos_ids)
+        return _RopeFn.apply(x, _table(cos, x, pos_ids), _table(sin, x, pos_ids), pos_ids)
     return _rope_ref(x, cos, sin, 1.0, pos_ids)

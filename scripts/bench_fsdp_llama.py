@@ -1,0 +1,135 @@
+"""Llama-3 8B through ``auto_accelerate`` (fused-op module replacement, bf16
+autocast, FSDP2 per decoder layer, activation checkpointing) with
+``FsdpShardCheckpointer`` flash checkpoints (BASELINE.json config "Llama-3 8B
+FSDP + ATorch auto_accelerate fused ops, async ckpt").
+
+One process per GPU; launch with torch.distributed.run for N GPUs (on one GPU
+FSDP holds the whole model: fp32 parameters + AdamW states, ~96 GB).  Random
+weights, synthetic tokens.  Reports the step time, the memory-save pause
+(DTensor shards + optimizer state -> HBM snapshot, async flush to shared
+memory), and the in-place restore time, verified against the saved shards.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--model", default="llama3-8b")
+    p.add_argument("--seq", type=int, default=4096)
+    p.add_argument("--micro-batch", type=int, default=1)
+    p.add_argument("--steps", type=int, default=8)
+    p.add_argument("--ckpt-interval", type=int, default=4)
+    p.add_argument("--ckpt-dir", default="/tmp/dwamd_fsdp_ckpt")
+    a = p.parse_args()
+    for k, v in dict(MASTER_ADDR="127.0.0.1", MASTER_PORT="29571", RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+                     LOCAL_WORLD_SIZE="1").items():
+        os.environ.setdefault(k, v)
+    os.environ.setdefault("DWAMD_SHM_PREFIX", f"fsdp{os.environ['MASTER_PORT']}")
+    lr = int(os.environ["LOCAL_RANK"])
+    cuda = torch.cuda.is_available()
+    dev = torch.device("cuda", lr) if cuda else torch.device("cpu")
+    if cuda:
+        torch.cuda.set_device(lr)
+        dist.init_process_group("nccl", device_id=dev)
+    else:  # CPU rehearsal of the same flow (gloo)
+        dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+
+    from dlrover_wuqiong_amd.atorch.auto_accelerate import auto_accelerate
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.fsdp import FsdpShardCheckpointer
+    from dlrover_wuqiong_amd.models.llama import Llama, LlamaConfig, LlamaDecoderLayer
+
+    cfg = LlamaConfig.named(a.model)
+    torch.manual_seed(0)
+    with torch.device(dev):
+        model = Llama(cfg)
+    ok, res, strategy = auto_accelerate(
+        model, torch.optim.AdamW, optim_args={"lr": 2e-5, "betas": (0.9, 0.95), "weight_decay": 0.1},
+        load_strategy=["module_replace", ("amp_native", {"dtype": torch.bfloat16}),
+                       ("fsdp", {"wrap_cls": (LlamaDecoderLayer,)}), ("checkpoint", {"wrap_cls": (LlamaDecoderLayer,)})])
+    assert ok, "auto_accelerate failed"
+    model, opt = res.model, res.optim
+    g = torch.Generator().manual_seed(rank)
+    data = torch.randint(0, cfg.vocab_size, (2, a.micro_batch, a.seq + 1), generator=g).to(dev)
+    ck = FsdpShardCheckpointer(a.ckpt_dir)
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+
+    def step(i):
+        b = data[i % 2]
+        loss = model(b[:, :-1], b[:, 1:])  # bf16 compute via FSDP2's MixedPrecisionPolicy
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    for i in range(2):  # warm-up (+ the optimizer states get created)
+        step(i)
+        print(f"warm-up step {i} done", file=sys.stderr, flush=True)
+    sync()
+    ts = time.perf_counter()
+    ck.save_checkpoint(0, model, opt, storage_type=StorageType.MEMORY)  # segment setup, untimed
+    sync()
+    setup_s = time.perf_counter() - ts
+    ck.wait_latest_checkpoint()
+    print(f"setup save {setup_s:.2f} s", file=sys.stderr, flush=True)
+    pauses, steps, losses = [], [], []
+    for i in range(a.steps):
+        t0 = time.perf_counter()
+        losses.append(float(step(i).item()))
+        sync()
+        steps.append(time.perf_counter() - t0)
+        if i % a.ckpt_interval == 0:
+            t0 = time.perf_counter()
+            ck.save_checkpoint(i + 1, model, opt, storage_type=StorageType.MEMORY)
+            sync()
+            pauses.append(time.perf_counter() - t0)
+    last = a.steps
+    ck.save_checkpoint(last + 1, model, opt, storage_type=StorageType.MEMORY)  # final state, untimed
+    ck.wait_latest_checkpoint()
+    sync()
+    want = {k: v.to_local().clone() for k, v in model.state_dict().items()}
+    with torch.no_grad():
+        for v in model.state_dict().values():
+            v.to_local().zero_()
+    copier = getattr(ck.engine, "_copier", None)
+    if copier is not None:
+        copier.pinned.release_all()
+    sync()
+    t0 = time.perf_counter()
+    extra = ck.load_checkpoint(model, opt)
+    sync()
+    load_s = time.perf_counter() - t0
+    verified = extra.get("step") == last + 1 and all(
+        torch.equal(v.to_local(), want[k]) for k, v in model.state_dict().items())
+    nbytes = ck.engine._shm_handler.payload_size if ck.engine._shm_handler.shared_memory else 0
+    if rank == 0:
+        print(json.dumps({
+            "metric": "fsdp flash ckpt pause s", "value": round(sum(pauses) / len(pauses), 4), "unit": "s",
+            "higher_is_better": False, "n_gpus": world, "dtype": "bf16 autocast, fp32 params + AdamW",
+            "data": "synthetic tokens, random-init weights",
+            "config": {"model": a.model, "seq_len": a.seq, "micro_batch": a.micro_batch,
+                       "strategy": str(strategy)[:300]},
+            "save_sec": [round(x, 4) for x in pauses], "setup_save_s": round(setup_s, 2),
+            "load_sec": round(load_s, 3), "load_verified": bool(verified), "ckpt_bytes_per_rank": nbytes,
+            "train_step_ms": round(1000 * sorted(steps)[len(steps) // 2], 1),
+            "tokens_per_s": round(world * a.micro_batch * a.seq / sorted(steps)[len(steps) // 2], 1),
+            "losses": [round(x, 3) for x in losses]}))
+    ck.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -138,3 +138,60 @@ def test_two_rank_ddp_fsdp_zero1():
 def test_two_rank_tensor_parallel():
     res = _run([("parallel_mode", ([("tensor", 2)], None)), "tensor_parallel"])
     assert [r[1] for r in res] == [True, True], res
+
+
+def _llama_fsdp_ckpt_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from dlrover_wuqiong_amd.atorch import distributed as adist
+
+    try:
+        from torch.distributed.algorithms._checkpoint.checkpoint_wrapper import CheckpointWrapper
+        from torch.distributed.fsdp import FSDPModule
+
+        from dlrover_wuqiong_amd.atorch.auto_accelerate import auto_accelerate
+        from dlrover_wuqiong_amd.models.llama import Llama, LlamaConfig, LlamaDecoderLayer
+
+        adist.init_distributed("gloo")
+        torch.manual_seed(0)
+        model = Llama(LlamaConfig.named("llama-tiny"))
+        ok, res, _ = auto_accelerate(
+            model, torch.optim.AdamW, optim_args={"lr": 1e-3},
+            load_strategy=["module_replace", ("amp_native", {"dtype": torch.bfloat16}),
+                           ("fsdp", {"wrap_cls": (LlamaDecoderLayer,)}),
+                           ("checkpoint", {"wrap_cls": (LlamaDecoderLayer,)})])
+        # FSDP must wrap the CheckpointWrapper (inputs cast once, outside the
+        # recomputed region), never the layer inside it
+        wrapped = [m for m in res.model.modules() if isinstance(m, CheckpointWrapper)]
+        nested_ok = bool(wrapped) and all(isinstance(m, FSDPModule) for m in wrapped) and not any(
+            isinstance(m, FSDPModule) for m in res.model.modules() if isinstance(m, LlamaDecoderLayer))
+        g = torch.Generator().manual_seed(rank)
+        ids = torch.randint(0, 1024, (2, 65), generator=g)
+        losses = []
+        for _ in range(3):
+            loss = res.model(ids[:, :-1], ids[:, 1:])
+            loss.backward()  # recompute must match the checkpointed forward
+            res.optim.step()
+            res.optim.zero_grad(set_to_none=True)
+            losses.append(float(loss))
+        q.put((rank, bool(ok and nested_ok and all(x == x for x in losses))))
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        traceback.print_exc()
+        q.put((rank, repr(e)))
+    finally:
+        adist.reset_distributed()
+
+
+def test_two_rank_llama_fsdp_with_activation_checkpointing():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_llama_fsdp_ckpt_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in ps), key=lambda x: x[0])
+    for p in ps:
+        p.join(timeout=30)
+    assert [r[1] for r in res] == [True, True], res

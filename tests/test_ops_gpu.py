@@ -133,6 +133,21 @@ def test_rope():
     assert _rel(x.grad, xf.grad) < 2e-2
 
 
+def test_rope_bf16_table_and_bad_shape():
+    """FSDP2 mixed precision casts the cos/sin layer inputs to bf16: the op
+    upcasts them (never reads a bf16 table as fp32) and rejects short tables."""
+    from dlrover_wuqiong_amd.ops._hip import HipKernelError
+    from dlrover_wuqiong_amd.ops.rope import _rope_ref, apply_rope, rope_table
+
+    B, S, NH, D = 1, 256, 4, 64
+    cos, sin = rope_table(S, D, device=DEV)
+    x = torch.randn(B, S, NH, D, device=DEV, dtype=torch.bfloat16)
+    y = apply_rope(x, cos.bfloat16(), sin.bfloat16())
+    assert _rel(y, _rope_ref(x.float(), cos.bfloat16().float(), sin.bfloat16().float())) < 1e-2
+    with pytest.raises(HipKernelError):
+        apply_rope(x, cos[: S // 2], sin[: S // 2])
+
+
 @pytest.mark.parametrize("V", [50304, 1000])
 def test_cross_entropy(V):
     from dlrover_wuqiong_amd.ops.cross_entropy import cross_entropy
