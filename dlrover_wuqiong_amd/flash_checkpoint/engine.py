@@ -246,6 +246,11 @@ class CheckpointEngine(ABC):
         h = self._shm_handler
         cur = h.payload_size if h.shared_memory is not None else -1
         need_resize = cur != total
+        if need_resize and self._copier is not None:
+            # registrations of the old mapping must not outlive it (a new
+            # mmap may land on the same addresses and look pinned)
+            self._copier.wait()
+            self._copier.pinned.release_all()
         if self._replicated:
             # every local rank plans the same layout -> same decision
             if need_resize:
@@ -266,6 +271,20 @@ class CheckpointEngine(ABC):
             h.shared_memory.prefault(8)
             self._generation += 1
             self._next_slot = None
+        if need_resize:
+            self._pin_slots(total)
+
+    def _pin_slots(self, total: int):
+        """hipHostRegister this rank's slice of EVERY slot now: registering a
+        96 GB slot costs ~0.6 s, which otherwise lands in the training pause
+        of the first save that rotates onto that slot."""
+        copier = self._device_copier()
+        if copier is None or total <= 0:
+            return
+        h = self._shm_handler
+        lo, hi = split_ranges(total, self._num_slices)[self._slice_idx]
+        for slot in range(h.num_slots):
+            copier.pinned.ensure(h.payload_addr(slot) + lo, hi - lo)
 
     # ----------------------------------------------------------- core save
     def save_state_dict_to_memory(self, state_dict: Dict, conf: CheckpointConfig) -> bool:

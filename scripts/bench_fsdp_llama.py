@@ -64,8 +64,11 @@ def main():
     ck = FsdpShardCheckpointer(a.ckpt_dir)
 
     def sync():
+        # the training stream only: a device-wide synchronize would also wait
+        # for the async D2H flush on the copier's side stream, which the
+        # training loop never waits for
         if cuda:
-            torch.cuda.synchronize()
+            torch.cuda.current_stream().synchronize()
 
     def step(i):
         b = data[i % 2]
@@ -92,14 +95,26 @@ def main():
         sync()
         steps.append(time.perf_counter() - t0)
         if i % a.ckpt_interval == 0:
+            prof = None
+            if os.environ.get("DWAMD_PROFILE_SAVE") == "1" and rank == 0:
+                import cProfile
+
+                prof = cProfile.Profile()
+                prof.enable()
             t0 = time.perf_counter()
             ck.save_checkpoint(i + 1, model, opt, storage_type=StorageType.MEMORY)
             sync()
             pauses.append(time.perf_counter() - t0)
+            if prof is not None:
+                import pstats
+
+                prof.disable()
+                pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(30)
     last = a.steps
     ck.save_checkpoint(last + 1, model, opt, storage_type=StorageType.MEMORY)  # final state, untimed
     ck.wait_latest_checkpoint()
-    sync()
+    if cuda:
+        torch.cuda.synchronize()
     want = {k: v.to_local().clone() for k, v in model.state_dict().items()}
     with torch.no_grad():
         for v in model.state_dict().values():
@@ -110,7 +125,8 @@ def main():
     sync()
     t0 = time.perf_counter()
     extra = ck.load_checkpoint(model, opt)
-    sync()
+    if cuda:
+        torch.cuda.synchronize()  # restore is complete only when every stream is
     load_s = time.perf_counter() - t0
     verified = extra.get("step") == last + 1 and all(
         torch.equal(v.to_local(), want[k]) for k, v in model.state_dict().items())
