@@ -1,51 +1,71 @@
 #!/usr/bin/env python
-"""Headline benchmark: flash-checkpoint save/load seconds for GPT2-1.5B DDP,
-plus goodput under an injected rank failure, on 1..8 MI355X GPUs.
+"""Headline benchmark: flash-checkpoint save/load seconds for GPT2-1.5B DDP
+and goodput under a real rank failure, on N MI355X GPUs of one node.
 
 Metric (BASELINE.json): "ckpt save/load sec GPT2-1.5B; goodput% under
 injected faults at 1/2/4/8 GPU".  Reference numbers (DLRover flash
-checkpoint, GPT-2 xl 1.5B, A100 x2, docs/figures/ft_llm_training/
+checkpoint, GPT-2 xl 1.5B, 2x A100, docs/figures/ft_llm_training/
 checkpoint_{save,load}_time): DDP save (paused training) 2.2 s, DDP load
-3.7 s.
+(recovery in memory) 3.7 s.
 
-What one rank does:
+Process structure (nothing here touches HIP before the workers exist):
+
+  bench.py (launcher, never initialises the GPU)
+    `-- dwamd-run --nproc-per-node N --standby-mode deep   (elastic agent + job master)
+          |-- N worker processes  = bench.py in worker mode, one per GPU, RCCL world of N
+          `-- N deep standbys     = bench.py in worker mode, parked in standby_point()
+
+  Under ``torch.distributed.run --nproc-per-node N`` (how the driver runs
+  N > 1) only RANK 0 launches; the other N-1 launcher processes exit at once,
+  so the job still has exactly one process per GPU.
+
+What a worker does (incarnation 0):
   1. builds GPT-2 xl (48 layers, 1600 hidden, 1.56 B params, random init)
-     in bf16 with fp32 master weights + AdamW state in flat buffers, wrapped
-     in FlatDDP (RCCL bucketed all-reduce);
-  2. runs W untimed warm-up steps, then K timed steps; EVERY step trains on a
-     synthetic token batch (full forward/backward/all-reduce/optimizer step)
-     and then takes a flash checkpoint of model + optimizer state to host
-     shared memory (DdpCheckpointer, StorageType.MEMORY).  The save time is
-     the training pause: wall time of save_checkpoint() + the GPU snapshot it
-     enqueues (torch.cuda.synchronize() before and after);
-  3. load: after the last save lands in shm, the live parameters/optimizer
-     state are poisoned and restored from shm in place; timed until the
-     restored state is on the GPU (synchronised), and verified bit-exact;
-  4. goodput: a rank failure is injected (every rank tears down its RCCL
-     communicator), the world is re-formed under a new store prefix, the
-     state is restored from shm and training resumes; goodput = useful
-     training time / (timed wall + recovery wall).
+     in bf16 with fp32 master weights + AdamW state in flat buffers, FlatDDP
+     (RCCL bucketed all-reduce over xGMI);
+  2. W warm-up steps (each followed by a flash save), then waits until every
+     local standby is parked (one-time set-up cost, kept out of the timed
+     window);
+  3. TIMED: K steps, every ``--ckpt-interval``-th followed by a flash save of
+     model + optimizer state (21.8 GB) to the node's shm
+     (DdpCheckpointer, StorageType.MEMORY).  The save time is the training
+     pause: save_checkpoint() + the GPU snapshot it enqueued.  Bracketed by
+     barrier + cuda.synchronize on both sides; MAX over ranks;
+  4. time-to-durable (pause + PCIe flush until every slice is in shm) and a
+     DISK save persisted by the agent (native parallel pwrite) while
+     training continues: persist GB/s and the step-time interference;
+  5. fault window: training continues with saves; mid-step (after backward,
+     before the optimizer step) the last rank SIGKILLs itself.
 
-Prints ONE JSON line (rank 0).  Timed region is bracketed by barrier +
-cuda.synchronize on both sides and reduced with MAX over ranks.
+The agent detects the death, SIGKILLs the survivors stuck in RCCL, re-runs
+the rendezvous (new master port -> a new RCCL world), and activates the
+standbys.  Incarnation 1 restores model + optimizer from shm (sliced H2D +
+RCCL all-gather over xGMI for N > 1) -- that restore time is ``load_sec``
+-- and trains to the end of the window.  goodput = productive step time /
+window wall time, where the window contains the saves, the lost (redone)
+steps, detection, restart, RCCL re-formation, restore and the first step.
+
+Prints ONE JSON line (launcher = rank 0 of the driver's launch).
 """
 
 import argparse
 import json
 import os
+import shutil
+import signal
 import statistics
+import subprocess
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
+REPO = os.path.dirname(os.path.abspath(__file__))
 REF_SAVE_SEC = 2.2  # DLRover DDP GPT-1.5B "DLRover Async Persist" (paused training time)
 REF_LOAD_SEC = 3.7  # DLRover DDP GPT-1.5B "DLRover Recovery In-Memory"
 METRIC = "ckpt save/load sec GPT2-1.5B; goodput% under injected faults at 1/2/4/8 GPU"
+WORKER_ENV = "DWAMD_BENCH_WORKER"
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=12)
@@ -53,294 +73,535 @@ def parse():
     p.add_argument("--model", default="gpt2-1.5b")
     p.add_argument("--micro-batch", type=int, default=8)
     p.add_argument("--seq", type=int, default=1024)
-    # checkpoint every 4 steps (~0.6 s at N=1): frequent enough that the pause
-    # is measured with the previous flush of the 21.8 GB payload completed
+    # checkpoint every 4 steps (~0.5 s at N=1): the previous flush of the
+    # 21.8 GB payload (~0.4 s) has landed by the next save
     p.add_argument("--ckpt-interval", type=int, default=4)
+    p.add_argument("--fault-window", type=int, default=16, help="steps in the measured fault window")
     p.add_argument("--ckpt-dir", default="/tmp/dwamd_bench_ckpt")
     p.add_argument("--no-fault", action="store_true")
+    p.add_argument("--no-persist", action="store_true", help="skip the DISK persist measurement")
     p.add_argument("--lr", type=float, default=1e-4)
     p.add_argument("--act-ckpt", action="store_true", help="activation checkpointing (Llama configs)")
-    return p.parse_args()
+    p.add_argument("--timeout", type=float, default=900.0)
+    p.add_argument("--out-dir", default="", help="keep the run's logs here (default: a temp dir, removed)")
+    # worker-only
+    p.add_argument("--run-dir", default="", help=argparse.SUPPRESS)
+    return p.parse_args(argv)
 
 
 def log(*a):
-    if int(os.environ.get("RANK", "0")) == 0:
-        print(*a, file=sys.stderr, flush=True)
+    print(*a, file=sys.stderr, flush=True)
 
 
-def max_over_ranks(x: float, device) -> float:
-    if dist.is_initialized() and dist.get_world_size() > 1:
-        t = torch.tensor([x], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
-    return x
+# =========================================================================
+# launcher (no HIP in this process)
+# =========================================================================
+_SCRUB = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE", "ROLE_RANK",
+          "ROLE_NAME", "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID",
+          "TORCHELASTIC_RESTART_COUNT", "TORCHELASTIC_MAX_RESTARTS", "TORCHELASTIC_USE_AGENT_STORE",
+          "TORCHELASTIC_ERROR_FILE", "TORCH_NCCL_ASYNC_ERROR_HANDLING", "DLROVER_MASTER_ADDR", "NODE_RANK")
 
 
-def sync_all(device):
-    if dist.is_initialized():
-        dist.barrier()
-    if device.type == "cuda":
-        torch.cuda.synchronize()
+def _read_jsonl(path):
+    out = []
+    if not os.path.exists(path):
+        return out
+    with open(path) as f:
+        for line in f:
+            line = line.strip()
+            if line:
+                try:
+                    out.append(json.loads(line))
+                except ValueError:
+                    pass
+    return out
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+def _kill_after(a, s0):
+    """Completed steps at the kill for a fault window starting at step s0:
+    the kill lands in the step right before the window's 2nd save, so
+    ckpt_interval - 1 completed steps (plus the partial one) are lost."""
+    return s0 + 2 * a.ckpt_interval - 1
+
+
+def launcher(a) -> int:
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    os.environ.setdefault("LOCAL_WORLD_SIZE", str(world))
-    os.environ.setdefault("DWAMD_SHM_PREFIX", f"bench{os.getpid() if world == 1 else os.environ.get('MASTER_PORT', '0')}")
+    if os.environ.get("TORCHELASTIC_RUN_ID") and rank != 0:
+        return 0  # torchrun's other ranks: rank 0 launches one worker per GPU
+    n = a.gpus
+    lws = os.environ.get("LOCAL_WORLD_SIZE")
+    if lws and int(lws) != n:
+        log(f"bench: --gpus {n} but the launcher started {lws} processes; using --gpus")
+    run_dir = a.out_dir or os.path.join("/tmp", f"dwamd_bench_{os.getpid()}")
+    shutil.rmtree(run_dir, ignore_errors=True)
+    os.makedirs(run_dir, exist_ok=True)
+    env = {k: v for k, v in os.environ.items() if k not in _SCRUB}
+    env.update({
+        WORKER_ENV: "1",
+        "PYTHONPATH": REPO + os.pathsep + env.get("PYTHONPATH", ""),
+        "DWAMD_SHM_PREFIX": f"bench{os.getpid()}",
+        "HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
+        "DWAMD_FAILURE_STOP_TIMEOUT": "0",  # survivors are stuck in RCCL with the dead rank
+    })
+    wargs = [os.path.abspath(__file__), "--run-dir", run_dir, "--gpus", str(n), "--steps", str(a.steps),
+             "--warmup", str(a.warmup), "--model", a.model, "--micro-batch", str(a.micro_batch), "--seq",
+             str(a.seq), "--ckpt-interval", str(a.ckpt_interval), "--fault-window", str(a.fault_window),
+             "--ckpt-dir", os.path.join(a.ckpt_dir, f"w{n}_{os.getpid()}"), "--lr", str(a.lr)]
+    if a.no_fault:
+        wargs.append("--no-fault")
+    if a.no_persist:
+        wargs.append("--no-persist")
+    if a.act_ckpt:
+        wargs.append("--act-ckpt")
+    cmd = [sys.executable, "-u", "-m", "dlrover_wuqiong_amd.trainer.run", "--nnodes", "1", "--nproc-per-node",
+           str(n), "--max-restarts", "1", "--monitor-interval", "0.05", "--standby-mode", "deep",
+           "--standby-delay", "0", "--event-log", os.path.join(run_dir, "agent.jsonl")] + wargs
+    log("bench launcher:", " ".join(cmd))
+    t0 = time.time()
+    # the agent's and workers' output goes to stderr: stdout carries the one JSON line
+    p = subprocess.Popen(cmd, env=env, stdout=sys.stderr, stderr=sys.stderr, start_new_session=True)
+    try:
+        rc = p.wait(timeout=a.timeout)
+    except subprocess.TimeoutExpired:
+        log("bench: timeout; killing the job")
+        os.killpg(p.pid, signal.SIGKILL)
+        p.wait()
+        rc = 124
+    wall = time.time() - t0
+    try:
+        res = summarize(a, run_dir, n, wall)
+    finally:
+        for f in os.listdir("/dev/shm"):
+            if f.startswith(f"dwamd_{env['DWAMD_SHM_PREFIX']}"):
+                try:
+                    os.remove(os.path.join("/dev/shm", f))
+                except OSError:
+                    pass
+        shutil.rmtree(os.path.join(a.ckpt_dir, f"w{n}_{os.getpid()}"), ignore_errors=True)
+        if not a.out_dir:
+            shutil.rmtree(run_dir, ignore_errors=True)
+    if res is None:
+        log(f"bench: job failed (rc={rc}); no result")
+        return rc or 1
+    print(json.dumps(res), flush=True)
+    return 0 if rc == 0 else rc
+
+
+def summarize(a, run_dir, n, wall):
+    ev = _read_jsonl(os.path.join(run_dir, "steps.jsonl"))
+    agent = _read_jsonl(os.path.join(run_dir, "agent.jsonl"))
+    phase0 = next((e for e in ev if e["event"] == "phase0"), None)
+    if phase0 is None:
+        return None
+    step_sec = phase0["step_sec"]
+    save_sec = phase0["save_sec_mean"]
+    res = {
+        "metric": METRIC,
+        "value": round(save_sec, 4),
+        "unit": "s",
+        "n_gpus": phase0["world"],
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(1000.0 * phase0["t_timed"] / a.steps, 2),
+        "higher_is_better": False,
+        "scaling": "weak",
+        "vs_baseline": round(save_sec / REF_SAVE_SEC, 4) if a.model == "gpt2-1.5b" else None,
+        "dtype": phase0["dtype"],
+        "data": "synthetic tokens, random-init weights",
+        "config": {"model": phase0["desc"], "global_batch": a.micro_batch * phase0["world"], "seq_len": a.seq,
+                   "parallelism": f"dp{phase0['world']}"},
+        "save_sec_mean": round(save_sec, 4),
+        "save_sec_max": round(phase0["save_sec_max"], 4),
+        "time_to_durable_sec": round(phase0["durable_sec"], 4),
+        "flush_gbps": phase0.get("flush_gbps"),
+        "load_sec_warm_process": round(phase0["load_sec_warm"], 4),
+        "load_verified": phase0["load_ok"],
+        "replicas_identical": phase0["replicas_identical"],
+        "ckpt_interval_steps": a.ckpt_interval,
+        "ckpt_bytes": phase0["ckpt_bytes"],
+        "params": phase0["params"],
+        "train_step_ms": round(1000 * step_sec, 2),
+        "tokens_per_s": round(a.micro_batch * a.seq * phase0["world"] / step_sec, 1),
+        "loss": phase0["loss"],
+        "rccl_world": phase0["world"],
+        "launcher_wall_s": round(wall, 1),
+    }
+    persist = next((e for e in ev if e["event"] == "persisted"), None)
+    if persist is not None:
+        res["persist_sec"] = round(persist["persist_sec"], 3)
+        res["persist_gbps"] = round(phase0["ckpt_bytes"] / persist["persist_sec"] / 1e9, 2)
+        res["persist_step_ms_during"] = persist.get("step_ms_during")
+        res["persist_step_interference_pct"] = persist.get("interference_pct")
+    done = next((e for e in ev if e["event"] == "done"), None)
+    kill = next((e for e in ev if e["event"] == "kill"), None)
+    if a.no_fault or done is None or kill is None:
+        res["goodput_pct"] = None
+        res["load_sec"] = None
+        return res
+    fail = next((e for e in agent if e["event"] == "failure_detected"), None)
+    started = [e for e in agent if e["event"] == "workers_started"]
+    rdzv = [e for e in agent if e["event"] == "rendezvous"]
+    restart = started[1] if len(started) > 1 else None
+    inc1 = next((e for e in ev if e["event"] == "start" and e["incarnation"] > 0), None)
+    steps1 = [e for e in ev if e["event"] == "step" and e.get("incarnation", 0) > 0]
+    fstart = next(e for e in ev if e["event"] == "fault_start")
+    t_win0 = fstart["t"]
+    t_end = done["t"]
+    window = t_end - t_win0
+    productive_steps = done["step"] - fstart["s0"]
+    productive = productive_steps * step_sec
+    goodput = 100.0 * productive / window
+    lost_steps = kill["completed_step"] - inc1["restored_step"]
+    first_step_end = steps1[0]["t"] if steps1 else t_end
+    # wall from the kill until the first post-restore step completes, minus
+    # that step's own compute: the time with no forward progress
+    recovery = first_step_end - kill["t"] - step_sec
+    res.update({
+        "load_sec": round(inc1["restore_sec"], 4),
+        "load_vs_baseline": round(inc1["restore_sec"] / REF_LOAD_SEC, 4) if a.model == "gpt2-1.5b" else None,
+        "load_verified_after_restart": inc1["restore_ok"],
+        "goodput_pct": round(goodput, 2),
+        "goodput_window_s": round(window, 3),
+        "goodput_window_steps": productive_steps,
+        "recover_sec": round(recovery, 3),
+        "lost_steps": lost_steps,
+        "recovery_breakdown_s": {
+            "detect": round(fail["t"] - kill["t"], 3) if fail else None,
+            "agent_restart": round(restart["t"] - fail["t"], 3) if (restart and fail) else None,
+            "rendezvous": rdzv[-1].get("seconds") if len(rdzv) > 1 else None,
+            "activate_to_pg_ready": round(inc1["t_pg"] - inc1["t_activated"], 3),
+            "ckpt_engine_init": round(inc1["t_ckpt"] - inc1["t_pg"], 3),
+            "restore": round(inc1["restore_sec"], 3),
+            "first_step": round(first_step_end - inc1["t_restored"], 3),
+        },
+        "standby_prepin_s": inc1.get("prepin_s"),
+        "restarts": len(started) - 1,
+    })
+    # extrapolation to production: one failure per hour, a checkpoint every
+    # ckpt_interval steps (mean loss: half an interval of steps)
+    per_step = step_sec + save_sec / a.ckpt_interval
+    fail_cost = recovery + 0.5 * a.ckpt_interval * step_sec
+    res["goodput_pct_1fail_per_hour"] = round(100.0 * ((3600.0 - fail_cost) / per_step) * step_sec / 3600.0, 3)
+    return res
+
+
+# =========================================================================
+# worker (one per GPU, started by the agent; also the deep standby)
+# =========================================================================
+def worker(a) -> int:
+    t_proc = time.time()
+    import torch
+    import torch.distributed as dist
+
+    from dlrover_wuqiong_amd.trainer.elastic import standby_point
+
+    lr = int(os.environ.get("LOCAL_RANK", "0"))
     cuda = torch.cuda.is_available()
-    # rehearsal knobs (never set by the driver): several ranks on one GPU over gloo
-    dev_idx = int(os.environ.get("DWAMD_BENCH_DEVICE", local_rank))
-    backend = os.environ.get("DWAMD_BENCH_BACKEND", "nccl" if cuda else "gloo")
-    device = torch.device("cuda", dev_idx) if cuda else torch.device("cpu")
+    device = torch.device("cuda", lr) if cuda else torch.device("cpu")
     if cuda:
         torch.cuda.set_device(device)
-        if os.environ.get("DWAMD_COMPUTE_STREAM", "1") == "1":
-            # train on a dedicated non-blocking stream (not the legacy null
-            # stream, which implicitly serialises with every blocking stream)
-            torch.cuda.set_stream(torch.cuda.Stream(device))
-    if world > 1:
-        dist.init_process_group(backend, device_id=device if (cuda and backend == "nccl") else None)
+        # train on a dedicated non-blocking stream (not the legacy null stream)
+        torch.cuda.set_stream(torch.cuda.Stream(device))
 
-    # DWAMD_OVERLAP_SNAPSHOT=1 (copier.py) would run the snapshot copy beside
-    # the next forward/backward: measured on GPT2-1.5B the pause drops 16 ->
-    # 9 ms but the next step grows by the same ~7 ms (the copy is HBM-bound
-    # and takes the CUs), so the bench reports the blocking snapshot
+    from dlrover_wuqiong_amd.common.constants import CheckpointConstant
     from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
     from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
-    from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
     from dlrover_wuqiong_amd.optimizers.fused import FusedAdamW
     from dlrover_wuqiong_amd.parallel.ddp import FlatDDP
     from dlrover_wuqiong_amd.parallel.flat import FlatParams
 
     dtype = torch.bfloat16 if cuda else torch.float32
     torch.manual_seed(1234)
-    if args.model.startswith("llama") or args.model.startswith("mixtral"):
-        # secondary configs (BASELINE.json "Llama-3 8B ... async ckpt"): same
-        # flat-buffer DDP + fused optimizer + flash checkpoint path
+    if a.model.startswith("llama") or a.model.startswith("mixtral"):
         from dlrover_wuqiong_amd.models.llama import Llama, LlamaConfig
 
-        cfg = LlamaConfig.named(args.model)
-        cfg.activation_checkpointing = args.act_ckpt
+        cfg = LlamaConfig.named(a.model)
+        cfg.activation_checkpointing = a.act_ckpt
         with torch.device(device):
             model = Llama(cfg)
-        desc = (f"{args.model} ({cfg.num_hidden_layers}L, {cfg.hidden_size}H, {cfg.num_attention_heads}/"
+        desc = (f"{a.model} ({cfg.num_hidden_layers}L, {cfg.hidden_size}H, {cfg.num_attention_heads}/"
                 f"{cfg.num_key_value_heads} heads)")
     else:
-        cfg = GPT2Config.named(args.model)
-        cfg.n_positions = max(cfg.n_positions, args.seq)
+        from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
+
+        cfg = GPT2Config.named(a.model)
+        cfg.n_positions = max(cfg.n_positions, a.seq)
         with torch.device(device):
             model = GPT2(cfg)
-        desc = ("GPT2-1.5B (gpt2-xl: 48L, 1600H, 25 heads)" if args.model == "gpt2-1.5b" else
-                f"{args.model} ({cfg.n_layer}L, {cfg.n_embd}H, {cfg.n_head} heads)")
+        desc = ("GPT2-1.5B (gpt2-xl: 48L, 1600H, 25 heads)" if a.model == "gpt2-1.5b" else
+                f"{a.model} ({cfg.n_layer}L, {cfg.n_embd}H, {cfg.n_head} heads)")
     model.to(dtype)
     nparams = model.num_params()
     flat = FlatParams(model, dtype=dtype, device=device)
-    opt = FusedAdamW(flat, lr=args.lr, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0)
+    opt = FusedAdamW(flat, lr=a.lr, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0)
+    B, S = a.micro_batch, a.seq
+
+    from dlrover_wuqiong_amd.elastic_agent.standby import is_standby
+
+    if is_standby():
+        # warm every kernel / allocator pool / library heuristic the first
+        # real step will use (forward + backward, no optimizer update)
+        x = torch.randint(0, cfg.vocab_size, (B, S + 1), device=device)
+        model(x[:, :-1], x[:, 1:]).backward()
+        flat.zero_grad()
+        if cuda:
+            torch.cuda.synchronize()
+    info = standby_point()  # deep standby: parks here until the agent activates it
+    t_act = time.time()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    incarnation = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
+    backend = "nccl" if cuda else "gloo"
+    if world > 1:
+        dist.init_process_group(backend, device_id=device if cuda else None)
+    assert world == a.gpus, f"RCCL world {world} != --gpus {a.gpus}"
     ddp = FlatDDP(model, flat, bucket_mb=128)
     opt.grad_scale = 1.0 / max(1, world)
-    log(f"model {args.model}: {nparams/1e9:.3f} B params, world {world}, device {device}")
-
-    B, S = args.micro_batch, args.seq
+    if world > 1:
+        # the communicator is created lazily by the first collective: do it now
+        # so it is part of the measured re-formation, not of the first step
+        t = torch.ones(1, device=device)
+        dist.all_reduce(t)
+        if cuda:
+            torch.cuda.synchronize()
+    t_pg = time.time()
     g = torch.Generator(device="cpu").manual_seed(rank)
     data = torch.randint(0, cfg.vocab_size, (4, B, S + 1), generator=g).to(device)
+    ckpt = DdpCheckpointer(a.ckpt_dir)
+    t_ckpt = time.time()
+    step_log = os.path.join(a.run_dir, "steps.jsonl")
 
-    ckpt = DdpCheckpointer(os.path.join(args.ckpt_dir, f"w{world}"))
+    def emit(obj, all_ranks=False):
+        if rank == 0 or all_ranks:
+            with open(step_log, "a") as f:
+                f.write(json.dumps(obj) + "\n")
+                f.flush()
+                os.fsync(f.fileno())
 
-    def state():
-        return {"model": model.state_dict(), "optimizer": opt.state_dict()}
+    def mx(x: float) -> float:
+        if world > 1:
+            t = torch.tensor([x], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t.item())
+        return x
+
+    def sync_all():
+        if world > 1:
+            dist.barrier()
+        if cuda:
+            torch.cuda.synchronize()
 
     step = 0
 
-    def train_step():
+    def state():
+        return {"model": model.state_dict(), "optimizer": opt.state_dict(), "step": step}
+
+    def train_step(kill_check=True):
         nonlocal step
         batch = data[step % data.shape[0]]
         loss = ddp(batch[:, :-1], batch[:, 1:])
         loss.backward()
+        if kill_check:
+            _maybe_kill(step)
         ddp.finish_gradient_sync()
         opt.step()
         flat.zero_grad()
         step += 1
         return loss
 
-    def save():
+    kill_after = -1
+
+    def _maybe_kill(completed):
+        # mid-step: forward + backward enqueued (gradients all-reducing), the
+        # optimizer step not yet -- SIGKILL, like a crashed / OOM-killed rank
+        if incarnation == 0 and completed == kill_after and rank == world - 1:
+            emit({"event": "kill", "t": time.time(), "completed_step": completed, "rank": rank}, all_ranks=True)
+            os.kill(os.getpid(), signal.SIGKILL)
+
+    def save(st=None):
         t0 = time.perf_counter()
-        ok = ckpt.save_checkpoint(step, state(), storage_type=StorageType.MEMORY)
+        ok = ckpt.save_checkpoint(step, state(), storage_type=st or StorageType.MEMORY)
         if cuda:
             torch.cuda.current_stream().synchronize()
         return time.perf_counter() - t0, ok
 
-    # ---------------- warm-up
-    for i in range(args.warmup):
-        train_step()
-        if cuda:
-            torch.cuda.synchronize()
-        save()
-    ckpt.wait_latest_checkpoint()
-    sync_all(device)
-
-    # ---------------- timed: train + flash checkpoint every ckpt_interval steps
-    save_times, step_times, losses = [], [], []
-    sync_all(device)
-    t_start = time.perf_counter()
-    for i in range(args.steps):
-        ts = time.perf_counter()
-        loss = train_step()
-        losses.append(loss.detach())
+    def sync_step():
         if cuda:
             # compute-stream sync only: a device-wide sync would also wait for
             # the checkpoint flush running on its own stream
             torch.cuda.current_stream().synchronize()
-        te = time.perf_counter()
-        step_times.append(te - ts)
-        # checkpoint after the first step of every interval: the background
-        # PCIe flush (~0.4 s for 21.8 GB) then overlaps the rest of the
-        # interval, as in steady-state training, instead of being charged to
-        # the closing device synchronize of the timed window
-        if i % args.ckpt_interval == 0:
-            st, ok = save()
-            save_times.append(st)
-    sync_all(device)
-    t_timed = time.perf_counter() - t_start
-    log("step ms:", [round(1000 * x, 1) for x in step_times], "save ms:", [round(1000 * x, 1) for x in save_times])
-    log("losses:", [round(float(x), 4) for x in losses])
-    t_timed = max_over_ranks(t_timed, device)
-    save_sec = max_over_ranks(statistics.mean(save_times) if save_times else 0.0, device)
-    save_max = max_over_ranks(max(save_times) if save_times else 0.0, device)
-    step_sec = max_over_ranks(statistics.median(step_times), device)
-    loss_v = float(loss.float().item())
 
-    # ---------------- load (restore from shm into live tensors)
-    # untimed snapshot of the final state, so the restore can be verified bit-exact
-    if not save_times or (args.steps - 1) % args.ckpt_interval != 0:
-        save()
-    ckpt.wait_latest_checkpoint()
-    sync_all(device)
-    third = opt.master if opt.master is not None else opt.exp_avg_sq
-    ref_sum = flat.data.float().sum().item(), opt.exp_avg.sum().item(), third.sum().item()
-    # replicated (DDP) state must be bit-identical across ranks: the node's one
-    # checkpoint copy is assembled from every local rank's slice
-    replicas_identical = True
-    if world > 1:
-        chk = torch.tensor([ref_sum[0], ref_sum[2]], dtype=torch.float64, device=device)
-        lo_, hi_ = chk.clone(), chk.clone()
-        dist.all_reduce(lo_, op=dist.ReduceOp.MIN)
-        dist.all_reduce(hi_, op=dist.ReduceOp.MAX)
-        replicas_identical = bool(torch.equal(lo_, hi_))
-    flat.data.zero_()
-    opt.exp_avg.zero_()
-    third.zero_()
-    if ckpt.engine._copier is not None:
-        # a restarted process has nothing pinned: measure the load cold
-        ckpt.engine._copier.pinned.release_all()
-    sync_all(device)
-    t0 = time.perf_counter()
-    restored = ckpt.load_checkpoint(target=state())
-    if cuda:
-        torch.cuda.synchronize()
-    load_sec = time.perf_counter() - t0
-    got = flat.data.float().sum().item(), opt.exp_avg.sum().item(), third.sum().item()
-    load_ok = all(abs(a - b) <= 1e-6 * max(1.0, abs(a)) for a, b in zip(ref_sum, got))
-    load_sec = max_over_ranks(load_sec, device)
+    if incarnation == 0:
+        # ---------------- warm-up (includes the first, set-up-paying save)
+        first_save = None
+        for _ in range(a.warmup):
+            train_step(False)
+            sync_step()
+            dt, _ok = save()
+            first_save = dt if first_save is None else first_save
+        ckpt.wait_latest_checkpoint()
+        # wait for this node's deep standbys (built concurrently with the
+        # warm-up): their one-time model build must not land in the timed window
+        ctl = os.environ.get("DWAMD_AGENT_CTL_DIR", "")
+        if ctl and not a.no_fault:
+            deadline = time.time() + 600
+            lw = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+            # parked + (on a GPU) this rank's shm slices registered
+            marks = ["standby_ready."] + (["standby_pinned."] if cuda else [])
+            while time.time() < deadline and not all(
+                    os.path.exists(os.path.join(ctl, f"{m}{i}")) for i in range(lw) for m in marks):
+                time.sleep(0.05)
+        sync_all()
 
-    # ---------------- goodput under an injected fault (RCCL re-form + restore)
-    recover_sec = 0.0
-    goodput = None
-    if not args.no_fault:
-        sync_all(device)
+        # ---------------- timed: train + flash checkpoint every ckpt_interval steps
+        save_times, step_times, losses = [], [], []
+        sync_all()
+        t_start = time.perf_counter()
+        for i in range(a.steps):
+            ts = time.perf_counter()
+            loss = train_step(False)
+            losses.append(loss.detach())
+            sync_step()
+            step_times.append(time.perf_counter() - ts)
+            # checkpoint after the first step of every interval: the
+            # background PCIe flush then overlaps the rest of the interval
+            if i % a.ckpt_interval == 0:
+                save_times.append(save()[0])
+        sync_all()
+        t_timed = mx(time.perf_counter() - t_start)
+        log(f"[rank {rank}] step ms:", [round(1000 * x, 1) for x in step_times], "save ms:",
+            [round(1000 * x, 1) for x in save_times])
+        save_sec = mx(statistics.mean(save_times))
+        save_max = mx(max(save_times))
+        step_sec = mx(statistics.median(step_times))
+        loss_v = float(loss.float().item())
+
+        # ---------------- time to durable: pause + flush until in shm
+        ckpt.wait_latest_checkpoint()
+        sync_all()
         t0 = time.perf_counter()
-        fail_step = step
+        save()
+        ckpt.wait_latest_checkpoint()
+        durable = mx(time.perf_counter() - t0)
+        cp = ckpt.engine._copier
+        flush_gbps = None
+        if cp is not None and cp.flush_stats:
+            nb, dt = cp.flush_stats[-1]
+            flush_gbps = round(nb / dt / 1e9, 1)
+
+        # ---------------- in-process load (warm process; verified bit-exact)
+        sync_all()
+        third = opt.master if opt.master is not None else opt.exp_avg_sq
+        ref_sum = flat.data.float().sum().item(), opt.exp_avg.sum().item(), third.sum().item()
+        replicas_identical = True
         if world > 1:
-            dist.destroy_process_group()
-            store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world,
-                                  is_master=False, timeout=__import__("datetime").timedelta(seconds=300))
-            pstore = dist.PrefixStore("dwamd_recover_1", store)
-            dist.init_process_group(backend, store=pstore, rank=rank, world_size=world,
-                                    device_id=device if (cuda and backend == "nccl") else None)
-            ddp.pg = None
-            ckpt.close()
-            ckpt = DdpCheckpointer(os.path.join(args.ckpt_dir, f"w{world}"))
-        flat.data.zero_()  # the restarted rank has lost its GPU state
+            chk = torch.tensor([ref_sum[0], ref_sum[2]], dtype=torch.float64, device=device)
+            lo_, hi_ = chk.clone(), chk.clone()
+            dist.all_reduce(lo_, op=dist.ReduceOp.MIN)
+            dist.all_reduce(hi_, op=dist.ReduceOp.MAX)
+            replicas_identical = bool(torch.equal(lo_, hi_))
+        flat.data.zero_()
+        opt.exp_avg.zero_()
+        third.zero_()
+        sync_all()
+        t0 = time.perf_counter()
         ckpt.load_checkpoint(target=state())
         if cuda:
             torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        train_step()  # first useful step after recovery (lazy communicator init lands here)
+        load_warm = mx(time.perf_counter() - t0)
+        got = flat.data.float().sum().item(), opt.exp_avg.sum().item(), third.sum().item()
+        load_ok = all(abs(x - y) <= 1e-6 * max(1.0, abs(x)) for x, y in zip(ref_sum, got))
+        ckpt_bytes = ckpt.engine._shm_handler.payload_size
+
+        emit({"event": "phase0", "world": world, "dtype": "bf16" if cuda else "fp32", "desc": desc,
+              "params": nparams, "t_timed": t_timed, "save_sec_mean": save_sec, "save_sec_max": save_max,
+              "step_sec": step_sec, "loss": round(loss_v, 4), "durable_sec": durable, "flush_gbps": flush_gbps,
+              "load_sec_warm": load_warm, "load_ok": load_ok, "replicas_identical": replicas_identical,
+              "ckpt_bytes": ckpt_bytes, "first_save_sec": first_save})
+
+        # ---------------- DISK persist (agent: torch.save archive written from
+        # shm with parallel pwrite) while training continues: persist time and
+        # step-time interference (steps measured while it is in flight)
+        if not a.no_persist:
+            tracker = os.path.join(a.ckpt_dir, CheckpointConstant.TRACER_FILE_NAME)
+            sync_all()
+            persist_step = step
+            persist_t0 = time.time()
+            ckpt.save_checkpoint(step, state(), storage_type=StorageType.DISK)
+            during, persist_done = [], None
+            while persist_done is None:
+                if len(during) < 400:
+                    ts = time.perf_counter()
+                    train_step(False)
+                    sync_step()
+                    during.append(time.perf_counter() - ts)
+                else:
+                    time.sleep(0.01)
+                done_here = 0
+                if rank == 0:
+                    try:
+                        with open(tracker) as f:
+                            done_here = 1 if f.read().strip() == str(persist_step) else 0
+                    except OSError:
+                        pass
+                if world > 1:
+                    t = torch.tensor([done_here], device=device)
+                    dist.broadcast(t, 0)
+                    done_here = int(t.item())
+                if done_here:
+                    persist_done = time.time() - persist_t0
+            med = mx(statistics.median(during)) if during else None
+            emit({"event": "persisted", "persist_sec": persist_done, "steps_during": len(during),
+                  "step_ms_during": round(1000 * med, 2) if med else None,
+                  "interference_pct": round(100 * (med / step_sec - 1), 2) if med else None})
+        sync_all()
+        s0 = step
+        emit({"event": "fault_start", "t": time.time(), "s0": s0})
+        start_step = step
+    else:
+        # ---------------- restarted incarnation: restore from the node's shm
+        sync_all()
+        t0 = time.perf_counter()
+        restored = ckpt.load_checkpoint(target=state())
         if cuda:
             torch.cuda.synchronize()
-        # re-form + restore, plus whatever the first step costs beyond a normal step
-        recover_sec = (t1 - t0) + max(0.0, time.perf_counter() - t1 - step_sec)
-        recover_sec = max_over_ranks(recover_sec, device)
-        useful = args.steps * step_sec
-        goodput = 100.0 * useful / (t_timed + recover_sec)
-        assert step == fail_step + 1
-    # extrapolated: one failure per hour, checkpoint every ckpt_interval steps;
-    # a failure costs the recovery + on average half an interval of lost steps
-    per_step = step_sec + save_sec / args.ckpt_interval
-    fail_cost = recover_sec + 0.5 * args.ckpt_interval * step_sec
-    goodput_1h = 100.0 * ((3600.0 - fail_cost) / per_step) * step_sec / 3600.0
+        restore_sec = mx(time.perf_counter() - t0)
+        step = int(restored.get("step", 0)) if restored else 0
+        restore_ok = bool(restored) and step > 0
+        t_restored = time.time()
+        emit({"event": "start", "incarnation": incarnation, "t": time.time(), "restored_step": step,
+              "restore_sec": restore_sec, "restore_ok": restore_ok, "t_proc": t_proc, "t_activated": t_act,
+              "t_pg": t_pg, "t_ckpt": t_ckpt, "t_restored": t_restored,
+              "prepin_s": info.get("prepin_s") if info else None})
+        if not restore_ok:
+            log(f"[rank {rank}] restore from memory failed: starting over")
+        start_step = step
+        s0 = next(e for e in _read_jsonl(step_log) if e["event"] == "fault_start")["s0"]
 
-    tokens = B * S * world
-    cp = ckpt.engine._copier
-    flush_info = (0, None, None)
-    if cp is not None and cp.flush_stats:
-        fb = sum(n for n, _ in cp.flush_stats)
-        ft = sum(t for _, t in cp.flush_stats)
-        flush_info = (cp.flush_cus, round(fb / ft / 1e9, 1), cp.flush_mode)
-    ckpt_bytes = ckpt.engine._shm_handler.payload_size if ckpt.engine._shm_handler.shared_memory else 0
-    res = {
-        "metric": METRIC,
-        "value": round(save_sec, 4),
-        "unit": "s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(1000.0 * t_timed / args.steps, 2),
-        "higher_is_better": False,
-        "scaling": "strong",
-        "vs_baseline": round(save_sec / REF_SAVE_SEC, 4) if args.model == "gpt2-1.5b" else None,
-        "dtype": "bf16" if cuda else "fp32",
-        "data": "synthetic tokens, random-init weights",
-        "config": {"model": desc,
-                   "global_batch": B * world,
-                   "seq_len": S, "parallelism": f"dp{world}"},
-        "save_sec_mean": round(save_sec, 4),
-        "save_sec_max": round(save_max, 4),
-        "load_sec": round(load_sec, 4),
-        "load_vs_baseline": round(load_sec / REF_LOAD_SEC, 4) if args.model == "gpt2-1.5b" else None,
-        "load_verified": load_ok,
-        "replicas_identical": replicas_identical,
-        "recover_sec": round(recover_sec, 3),
-        "goodput_pct": round(goodput, 2) if goodput is not None else None,
-        "goodput_pct_1fail_per_hour": round(goodput_1h, 3),
-        "ckpt_interval_steps": args.ckpt_interval,
-        "ckpt_bytes": ckpt_bytes,
-        "flush_cus": flush_info[0],
-        "flush_gbps": flush_info[1],
-        "flush_mode": flush_info[2],
-        "snapshot": "overlapped" if (cp is not None and cp.overlap) else "blocking",
-        "params": nparams,
-        "train_step_ms": round(1000 * step_sec, 2),
-        "tokens_per_s": round(tokens / step_sec, 1),
-        "loss": round(loss_v, 4),
-    }
-    if rank == 0:
-        print(json.dumps(res), flush=True)
+    # ---------------- fault window: train + save every interval; rank n-1 dies mid-step
+    kill_after = _kill_after(a, s0) if not a.no_fault else -1
+    s_end = s0 + a.fault_window
+    while step < s_end:
+        train_step(True)
+        sync_step()
+        if (step - s0) % a.ckpt_interval == 0:
+            save()
+        emit({"event": "step", "step": step, "t": time.time(), "incarnation": incarnation})
+    sync_all()
+    emit({"event": "done", "t": time.time(), "step": step, "start_step": start_step, "incarnation": incarnation})
     ckpt.close()
-    if dist.is_initialized():
+    if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    if rank == 0:
-        # leave no 20 GB segments behind on the box
-        import glob
+    return 0
 
-        for f in glob.glob(f"/dev/shm/dwamd_{os.environ['DWAMD_SHM_PREFIX']}*"):
-            try:
-                os.remove(f)
-            except OSError:
-                pass
+
+def main():
+    a = parse()
+    if os.environ.get(WORKER_ENV) == "1":
+        sys.exit(worker(a))
+    sys.exit(launcher(a))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,8 @@
+"""Compatibility import path (reference: dlrover/trainer/torch/flash_checkpoint/ddp.py:25-117).
+
+Thin re-export onto the MI355X-native implementation in ``dlrover_wuqiong_amd.flash_checkpoint.ddp``;
+existing DLRover / ATorch user code imports unchanged.
+"""
+
+from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType  # noqa: F401
+from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer  # noqa: F401

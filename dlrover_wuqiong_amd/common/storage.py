@@ -22,6 +22,86 @@ from .log import logger
 from .serialize import ClassMeta
 
 
+_BIG_WRITE = 4 << 20  # records at least this large go through the native parallel pwrite
+
+
+class _ParallelFileWriter:
+    """Sequential-write file object for ``torch.save``.
+
+    ``torch.save`` streams its zip archive through ``write()`` and hands each
+    tensor storage over as ONE zero-copy memoryview of the storage bytes (for
+    a flash checkpoint: straight out of the shm segment).  Small records
+    (pickle, zip headers) are ``os.pwrite``'n; storages go through the native
+    runtime's multi-threaded ``pwrite`` at the current offset.  The archive is
+    byte-for-byte a regular torch zip file (``torch.load`` reads it)."""
+
+    def __init__(self, path: str, threads: int):
+        self.path = path
+        self.threads = threads
+        self.fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+        self.off = 0
+        self.big_bytes = 0
+
+    def write(self, b) -> int:
+        mv = memoryview(b).cast("B")
+        n = mv.nbytes
+        if n >= _BIG_WRITE:
+            import numpy as np
+
+            addr = np.frombuffer(mv, dtype=np.uint8).ctypes.data
+            r = runtime().dw_write_file(self.path.encode(), ctypes.c_void_p(addr), n, self.off, self.threads, 0)
+            if r != 0:
+                raise OSError(f"write {self.path}: {last_error()}")
+            self.big_bytes += n
+        else:
+            done = 0
+            while done < n:
+                done += os.pwrite(self.fd, mv[done:], self.off + done)
+        self.off += n
+        return n
+
+    def flush(self):
+        pass
+
+    def close(self, fsync: bool = True):
+        if self.fd >= 0:
+            if fsync:
+                os.fsync(self.fd)
+            os.close(self.fd)
+            self.fd = -1
+
+
+def fast_torch_save(obj, path: str, threads: int = 16, fsync: bool = True) -> int:
+    """``torch.save(obj, path)`` with tensor storages written by parallel
+    ``pwrite`` streams, page-aligned records and no CRC pass (the zip CRC is a
+    single-threaded ~1 GB/s scan that would dominate a 20+ GB checkpoint;
+    ``torch.load`` accepts CRC-less archives).  Returns bytes written."""
+    import torch
+    from torch.utils.serialization import config
+
+    path = str(path)
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+    tmp = path + ".tmp"
+    old = (config.save.compute_crc32, config.save.storage_alignment)
+    f = _ParallelFileWriter(tmp, threads)
+    try:
+        config.save.compute_crc32 = False
+        config.save.storage_alignment = 4096
+        torch.save(obj, f)
+        f.close(fsync=fsync)
+    except BaseException:
+        f.close(fsync=False)
+        try:
+            os.remove(tmp)
+        except OSError:
+            pass
+        raise
+    finally:
+        config.save.compute_crc32, config.save.storage_alignment = old
+    os.replace(tmp, path)
+    return f.off
+
+
 class CheckpointStorage(ABC):
     @abstractmethod
     def write(self, content, path):

@@ -81,6 +81,18 @@ class ElasticLaunchConfig:
     # pre-started interpreters (torch imported) that become the next workers
     warm_standby: bool = field(default_factory=lambda: os.getenv("DWAMD_WARM_STANDBY", "1") == "1")
     standby_delay: float = field(default_factory=lambda: float(os.getenv("DWAMD_STANDBY_DELAY", "3")))
+    # "import": standbys pre-import torch only (any script); "deep": standbys
+    # run the script up to standby_point() (model on the GPU, kernels warm,
+    # checkpoint shm pinned) -- see standby.py
+    standby_mode: str = field(default_factory=lambda: os.getenv("DWAMD_STANDBY_MODE", "import"))
+    # on a worker failure the surviving local workers are usually blocked in
+    # a collective with the dead rank: give them this long after SIGTERM
+    # before SIGKILL (the breakpoint checkpoint is persisted from shm by the
+    # agent, not by the dying workers)
+    failure_stop_timeout: float = field(default_factory=lambda: float(os.getenv("DWAMD_FAILURE_STOP_TIMEOUT", "2")))
+    # JSONL timeline of agent events (failure detected, restart, ...) for
+    # goodput accounting; "" = off
+    event_log: str = field(default_factory=lambda: os.getenv("DWAMD_AGENT_EVENT_LOG", ""))
     # persist the breakpoint checkpoint while the new workers already start
     async_breakpoint_save: bool = True
     # exit (and let the platform relaunch the node) on GPU/driver fault signatures
@@ -152,6 +164,10 @@ class MasterRendezvousHandler:
     def next_rendezvous(self) -> Tuple[int, int, Dict[int, int]]:
         self.client.join_rendezvous(self.node_rank, self.config.nproc_per_node, self.name)
         start = time.time()
+        # poll fast first (a single-node restart completes on the first polls),
+        # then back off to the reference's 1 s interval
+        delay = 0.02
+        cap = JobConstant.RDZV_POLL_INTERVAL if self.config.lastcall_timeout > 1 else 0.1
         while True:
             rnd, group, world = self.client.get_comm_world(self.name, self.node_rank)
             if world and self.node_rank in world:
@@ -160,7 +176,8 @@ class MasterRendezvousHandler:
                 raise RendezvousTimeoutError("node not admitted into the world")
             if time.time() - start > self.config.join_timeout:
                 raise RendezvousTimeoutError(f"rendezvous {self.name} timed out after {self.config.join_timeout}s")
-            time.sleep(JobConstant.RDZV_POLL_INTERVAL if self.config.lastcall_timeout > 1 else 0.1)
+            time.sleep(delay)
+            delay = min(cap, delay * 2)
 
     def num_nodes_waiting(self) -> int:
         return self.client.num_nodes_waiting(self.name)
@@ -189,10 +206,21 @@ class ElasticTrainingAgent:
         self._standby: Dict[int, subprocess.Popen] = {}
         self._workers_started_at = 0.0
         self._bp_thread: Optional[threading.Thread] = None
+        self._reapers: List[threading.Thread] = []
         # worker <-> agent control files (heartbeats, relaunch requests)
         self.ctl_dir = os.path.join(tempfile.gettempdir(), "dwamd_ctl",
                                     f"{config.run_id}_n{config.node_rank}_{os.getpid()}")
         os.makedirs(self.ctl_dir, exist_ok=True)
+
+    def _event(self, what: str, **kw):
+        t = time.time()
+        self.events.append((t, what))
+        if self.config.event_log:
+            try:
+                with open(self.config.event_log, "a") as f:
+                    f.write(json.dumps(dict({"t": t, "event": what, "restart": self.restart_count}, **kw)) + "\n")
+            except OSError:
+                pass
 
     # ------------------------------------------------------------ ranks
     @staticmethod
@@ -237,7 +265,7 @@ class ElasticTrainingAgent:
                 if time.time() > deadline:
                     raise RendezvousTimeoutError("no MASTER_ADDR published")
                 time.sleep(0.05)
-        self.events.append((time.time(), "rendezvous"))
+        self._event("rendezvous", seconds=round(time.time() - t0, 4), round=self.round)
         logger.info(f"rendezvous round {self.round} ({time.time() - t0:.2f}s): world={self.world} "
                     f"group_rank={self.group_rank} ranks={ranks} master={self.master_addr}:{self.master_port}")
         return ranks, world_size
@@ -328,7 +356,7 @@ class ElasticTrainingAgent:
                 warm += 1
             self.workers.append(WorkerProcess(lr, gr, p, log_path))
         self._workers_started_at = time.time()
-        self.events.append((self._workers_started_at, "workers_started"))
+        self._event("workers_started", warm=warm, n=len(self.workers))
         logger.info(f"started {len(self.workers)} workers (restart {self.restart_count}, "
                     f"{warm} from warm standby)")
 
@@ -344,20 +372,68 @@ class ElasticTrainingAgent:
         return p
 
     # ------------------------------------------------------ warm standby
-    def _spawn_standbys(self):
-        """Start one idle interpreter per local rank for the next (re)start."""
-        if not self.config.warm_standby:
-            return
+    def _standby_env(self, local_rank: int) -> Dict[str, str]:
         env = dict(os.environ)
         env.update(self.config.extra_env)
         env.setdefault("OMP_NUM_THREADS", "1")
+        if self.config.standby_mode == "deep":
+            from .standby import STANDBY_ENV
+
+            # provisional worker environment: the device is known, the world
+            # is not (RANK / WORLD_SIZE / MASTER_* arrive at activation)
+            for k in ("RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "GROUP_RANK", "ROLE_RANK"):
+                env.pop(k, None)
+            env.update({
+                "LOCAL_RANK": str(local_rank),
+                "LOCAL_WORLD_SIZE": str(self.config.nproc_per_node),
+                "ROLE_NAME": "dlrover-trainer",
+                "TORCHELASTIC_RESTART_COUNT": str(self.restart_count + 1),
+                "TORCHELASTIC_RUN_ID": self.config.run_id,
+                NodeEnv.NODE_RANK: str(self.config.node_rank),
+                "HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
+                "DWAMD_AGENT_CTL_DIR": self.ctl_dir,
+                STANDBY_ENV: "1",
+            })
+        return env
+
+    def _spawn_standbys(self):
+        """Start one standby process per local rank for the next (re)start."""
+        if not self.config.warm_standby:
+            return
+        deep = self.config.standby_mode == "deep"
         for lr in range(self.config.nproc_per_node):
             p = self._standby.get(lr)
             if p is not None and p.poll() is None:
                 continue
+            env = self._standby_env(lr)
+            if deep:
+                from .standby import SPEC_ENV
+
+                log = ""
+                if self.config.log_dir:
+                    os.makedirs(self.config.log_dir, exist_ok=True)
+                    log = os.path.join(self.config.log_dir, f"{self.config.run_id}_standby{self.restart_count + 1}"
+                                                            f"_local{lr}.log")
+                env[SPEC_ENV] = json.dumps({"entry": self.entrypoint, "args": self.args, "module": self.is_module,
+                                            "cwd": os.getcwd(), "log": log})
             self._standby[lr] = subprocess.Popen(
                 [sys.executable, "-u", "-m", "dlrover_wuqiong_amd.elastic_agent.standby"], env=env,
                 stdin=subprocess.PIPE, start_new_session=True, text=True)
+        self._event("standby_spawned", mode=self.config.standby_mode)
+
+    def standbys_ready(self) -> bool:
+        """All local standbys alive (and, in deep mode, parked in standby_point)."""
+        if not self.config.warm_standby or len(self._standby) < self.config.nproc_per_node:
+            return False
+        for lr, p in self._standby.items():
+            if p.poll() is not None:
+                return False
+            if self.config.standby_mode == "deep":
+                from .standby import READY_PREFIX
+
+                if not os.path.exists(os.path.join(self.ctl_dir, READY_PREFIX + str(lr))):
+                    return False
+        return True
 
     def _activate_standby(self, local_rank: int, env: Dict[str, str], log_path: str):
         p = self._standby.pop(local_rank, None)
@@ -387,25 +463,38 @@ class ElasticTrainingAgent:
                     pass
         self._standby = {}
 
-    def _stop_workers(self, timeout: Optional[float] = None):
+    def _stop_workers(self, timeout: Optional[float] = None, wait: bool = True):
+        """SIGTERM every live worker group, SIGKILL after ``timeout``.
+        ``wait=False``: return at once and reap in the background (the next
+        workers may start while the old processes are still being torn down
+        -- their GPU memory is released by the driver at exit)."""
         timeout = self.config.stop_timeout if timeout is None else timeout
-        for w in self.workers:
+        workers, self.workers = self.workers, []
+        for w in workers:
             if w.proc.poll() is None:
                 try:
-                    os.killpg(w.proc.pid, signal.SIGTERM)
+                    os.killpg(w.proc.pid, signal.SIGTERM if timeout > 0 else signal.SIGKILL)
                 except ProcessLookupError:
                     pass
-        deadline = time.time() + timeout
-        for w in self.workers:
-            while w.proc.poll() is None and time.time() < deadline:
-                time.sleep(0.05)
-            if w.proc.poll() is None:
-                try:
-                    os.killpg(w.proc.pid, signal.SIGKILL)
-                except ProcessLookupError:
-                    pass
-                w.proc.wait()
-        self.workers = []
+
+        def reap():
+            deadline = time.time() + timeout
+            for w in workers:
+                while w.proc.poll() is None and time.time() < deadline:
+                    time.sleep(0.02)
+                if w.proc.poll() is None:
+                    try:
+                        os.killpg(w.proc.pid, signal.SIGKILL)
+                    except ProcessLookupError:
+                        pass
+                    w.proc.wait()
+
+        if wait:
+            reap()
+        else:
+            t = threading.Thread(target=reap, daemon=True, name="dwamd-reap")
+            t.start()
+            self._reapers.append(t)
 
     def _monitor_workers(self) -> RunResult:
         codes = [(w, w.proc.poll()) for w in self.workers]
@@ -502,6 +591,8 @@ class ElasticTrainingAgent:
         finally:
             self._stop_hb.set()
             self._discard_standbys()
+            for t in self._reapers:
+                t.join(timeout=30)
             if self._bp_thread is not None:
                 self._bp_thread.join(timeout=600)
 
@@ -514,7 +605,7 @@ class ElasticTrainingAgent:
                 self._spawn_standbys()
             res = self._monitor_workers()
             if res.state == RunResult.SUCCEEDED:
-                self.events.append((time.time(), "succeeded"))
+                self._event("succeeded")
                 self._discard_standbys()
                 if self._bp_thread is not None:
                     self._bp_thread.join(timeout=600)
@@ -528,17 +619,19 @@ class ElasticTrainingAgent:
                     logger.warning(f"final success report not delivered: {e}")
                 return 0
             if res.state == RunResult.FAILED:
-                self.events.append((time.time(), "failed"))
+                self._event("failure_detected", ranks={str(r): f["exitcode"] for r, f in res.failures.items()})
                 logger.error(f"worker failure: { {r: (f['exitcode']) for r, f in res.failures.items()} }")
                 from .diagnosis import classify_failure
 
                 level = max((classify_failure(f.get("message", "")) for f in res.failures.values()),
                             key=lambda lv: lv == TrainingExceptionLevel.NODE_ERROR)
+                self._stop_workers(timeout=self.config.failure_stop_timeout,
+                                   wait=self.config.standby_mode != "deep")
+                self._event("workers_stopped")
                 try:
                     self.client.report_failures(json.dumps(res.failures), self.restart_count, level)
                 except Exception:
                     pass
-                self._stop_workers()
                 self._save_ckpt_to_storage()
                 if level == TrainingExceptionLevel.NODE_ERROR and self.config.exit_on_node_error:
                     # hardware signature: let the platform replace this node

@@ -38,7 +38,9 @@ from ..flash_checkpoint.shm_handler import (DLROVER_CKPT_CONFIG_KEY, EVENT_QUEUE
 
 def _writer_for(path: str):
     """File format by extension: safetensors for ``*.safetensors`` (HF
-    weights), ``torch.save`` otherwise."""
+    weights), a ``torch.save`` archive otherwise -- written by
+    :func:`fast_torch_save` (storages streamed from shm with parallel pwrite;
+    ``DWAMD_PERSIST_WRITER=torch`` selects plain ``torch.save``)."""
     if str(path).endswith(".safetensors"):
         def write(sd, p):
             from safetensors.torch import save_file
@@ -46,7 +48,12 @@ def _writer_for(path: str):
             save_file({k: v.contiguous() for k, v in sd.items()}, p, metadata={"format": "pt"})
 
         return write
-    return torch.save
+    if os.environ.get("DWAMD_PERSIST_WRITER", "fast") == "torch":
+        return torch.save
+    from ..common.storage import fast_torch_save
+
+    threads = int(os.environ.get("DWAMD_PERSIST_THREADS", "16"))
+    return lambda sd, p: fast_torch_save(sd, p, threads=threads)
 
 
 class AsyncCheckpointSaver:

@@ -1,17 +1,36 @@
-"""Warm standby worker: a pre-started interpreter that becomes a worker.
+"""Warm standby workers: pre-started processes that become the next workers.
 
-Restarting a worker after a fault costs a fresh ``python`` + ``import torch``
-(1-2 s, more on a cold page cache) before the training script even starts.
-The agent therefore keeps one *standby* interpreter per local rank that has
-already imported torch and this package (nothing that touches the GPU: HIP is
-initialised only after the worker environment is applied) and blocks on its
-stdin.  On (re)start the agent sends one JSON line -- worker environment,
-argv, entrypoint, log file -- and the standby turns into the worker in
-place (``runpy``, ``__main__`` semantics).  No ``exec``: the process simply
-continues as the worker, so nothing GPU-initialised is ever replaced.
+Restarting a worker after a fault normally costs a fresh ``python`` +
+``import torch`` + HIP init + model build + kernel warm-up + pinning the
+checkpoint shm before the first useful step.  The agent therefore keeps one
+*standby* process per local rank ready.  Two modes:
 
-The reference (torchelastic-based agent) always cold-starts workers; this is
-an MI355X-deployment goodput optimisation (see ``scripts/goodput_experiment.py``).
+``import`` (default, safe for any script)
+    The standby imports torch and this package (nothing that touches the
+    GPU) and blocks on stdin.  On (re)start the agent sends one JSON line
+    -- worker environment, argv, entrypoint, log file -- and the standby
+    turns into the worker in place (``runpy``, ``__main__`` semantics).
+
+``deep`` (opt-in: ``dwamd-run --standby-mode deep``; the script must call
+:func:`standby_point`)
+    The standby runs the training script *immediately* with a provisional
+    environment (``LOCAL_RANK`` / ``LOCAL_WORLD_SIZE`` known, no ``RANK`` /
+    ``WORLD_SIZE`` / ``MASTER_*``).  The script does everything that does not
+    need the world -- HIP init, model + optimizer allocation on its GPU,
+    kernel warm-up -- and then calls :func:`standby_point`, which pins this
+    rank's part of the node's checkpoint shm (so the restore is a plain DMA),
+    reports readiness to the agent and blocks.  At activation it applies the
+    real worker environment and returns; the script continues with
+    ``init_process_group``, restores from shm and trains.  A restart is then
+    rendezvous + RCCL init + H2D restore.  On MI355X the standby's copy of the
+    model fits next to the live worker (288 GB HBM per GPU).
+
+No ``exec`` anywhere: a process that has initialised the GPU is never
+replaced; it simply continues as the worker.
+
+The reference (torchelastic-based agent, ``training.py:580-645,704``) always
+cold-starts workers; this is an MI355X-deployment goodput optimisation
+measured by ``bench.py``.
 """
 
 import importlib
@@ -19,6 +38,19 @@ import json
 import os
 import runpy
 import sys
+import time
+from typing import Optional
+
+STANDBY_ENV = "DWAMD_STANDBY"
+SPEC_ENV = "DWAMD_STANDBY_SPEC"
+READY_PREFIX = "standby_ready."
+
+_activated: Optional[dict] = None
+
+
+def is_standby() -> bool:
+    """True in a deep standby that has not been activated yet."""
+    return os.environ.get(STANDBY_ENV, "0") == "1" and _activated is None
 
 
 def _preload():
@@ -42,24 +74,131 @@ def _redirect(log_path: str):
     os.close(fd)
 
 
-def main():
-    _preload()
-    line = sys.stdin.readline()
-    if not line.strip():
-        return 0  # agent discarded the standby
-    cmd = json.loads(line)
+def _apply(cmd: dict):
     _redirect(cmd.get("log", ""))
     os.environ.clear()
     os.environ.update(cmd["env"])
     if cmd.get("cwd"):
         os.chdir(cmd["cwd"])
-    entry = cmd["entry"]
-    sys.argv = [entry] + list(cmd.get("args", []))
-    if cmd.get("module"):
+
+
+PINNED_PREFIX = "standby_pinned."
+
+
+def _prepin_checkpoint_shm() -> float:
+    """Map + hipHostRegister this local rank's part of the node's flash
+    checkpoint segments (kept for the checkpoint engine to adopt).  Returns
+    seconds spent; idempotent (re-pins only a re-created segment)."""
+    try:
+        from ..flash_checkpoint.prewarm import prepin_local_checkpoint_shm
+
+        return prepin_local_checkpoint_shm()
+    except Exception as e:  # never fatal: the restore pins on demand
+        print(f"[standby] shm pre-pin skipped: {e}", file=sys.stderr)
+        return 0.0
+
+
+def _pinned_bytes() -> int:
+    try:
+        from ..flash_checkpoint.prewarm import prepinned_bytes
+
+        return prepinned_bytes()
+    except Exception:
+        return 0
+
+
+def _mark(ctl: str, prefix: str, lr: str, text: str):
+    if not ctl:
+        return
+    path = os.path.join(ctl, prefix + lr)
+    with open(path + ".tmp", "w") as f:
+        f.write(text)
+    os.replace(path + ".tmp", path)
+
+
+def standby_point(prepin_shm: bool = True, repin_interval: float = 0.25) -> Optional[dict]:
+    """Call once in the training script after world-independent set-up.
+
+    Not a standby: returns ``None`` immediately.  Deep standby: signals
+    readiness and blocks until the agent activates this process (returns
+    ``{"activated_at": t, "waited_s": s, "prepin_s": p}``) or discards it
+    (the process exits 0 without returning).  While parked it keeps this
+    rank's part of the node's checkpoint shm pinned (the segment may appear,
+    or be re-created at a new size, only after the standby parked).
+    """
+    global _activated
+    if not is_standby():
+        return None
+    import select
+
+    ctl = os.environ.get("DWAMD_AGENT_CTL_DIR", "")
+    lr = os.environ.get("LOCAL_RANK", "0")
+    pin_s = _prepin_checkpoint_shm() if prepin_shm else 0.0
+    _mark(ctl, READY_PREFIX, lr, f"{os.getpid()} {time.time()}\n")
+    pinned_marked = False
+    t0 = time.time()
+    buf = b""
+    fd = sys.stdin.fileno()
+    while True:
+        if not pinned_marked and prepin_shm and _pinned_bytes() > 0:
+            _mark(ctl, PINNED_PREFIX, lr, f"{_pinned_bytes()}\n")
+            pinned_marked = True
+        r, _, _ = select.select([fd], [], [], repin_interval)
+        if r:
+            chunk = os.read(fd, 1 << 20)
+            if not chunk:
+                sys.stdout.flush()
+                sys.stderr.flush()
+                os._exit(0)  # discarded by the agent (stdin closed)
+            buf += chunk
+            if b"\n" in buf:
+                break
+        elif prepin_shm:
+            pin_s += _prepin_checkpoint_shm()
+    cmd = json.loads(buf.split(b"\n", 1)[0].decode())
+    _apply(cmd)
+    _activated = {"activated_at": time.time(), "waited_s": time.time() - t0, "prepin_s": pin_s,
+                  "pinned_bytes": _pinned_bytes()}
+    return dict(_activated)
+
+
+def activation_info() -> Optional[dict]:
+    return dict(_activated) if _activated else None
+
+
+def _run_entry(entry: str, args, module: bool):
+    sys.argv = [entry] + list(args)
+    if module:
         runpy.run_module(entry, run_name="__main__", alter_sys=True)
     else:
         sys.path.insert(0, os.path.dirname(os.path.abspath(entry)))
         runpy.run_path(entry, run_name="__main__")
+
+
+def main():
+    spec = os.environ.get(SPEC_ENV, "")
+    if spec:
+        # deep standby: run the script now; it blocks in standby_point()
+        s = json.loads(spec)
+        _redirect(s.get("log", ""))
+        if s.get("cwd"):
+            os.chdir(s["cwd"])
+        os.environ.pop(SPEC_ENV, None)
+        _run_entry(s["entry"], s.get("args", []), s.get("module", False))
+        if _activated is None:
+            # the script finished without ever reaching standby_point(): it is
+            # not standby-aware; report and exit non-zero so the agent cold-starts
+            print("[standby] script returned before standby_point(); not a deep-standby script",
+                  file=sys.stderr)
+            return 3
+        return 0
+    _preload()
+    line = sys.stdin.readline()
+    if not line.strip():
+        return 0  # agent discarded the standby
+    cmd = json.loads(line)
+    _apply(cmd)
+    _run_entry(cmd["entry"], cmd.get("args", []), cmd.get("module", False))
     return 0
 
 

@@ -138,6 +138,27 @@ class PinnedRegistry:
                 _kern().dw_host_unregister(ctypes.c_void_p(a))
             self._ranges.clear()
 
+    def release_range(self, addr: int, nbytes: int):
+        """Unregister every registration that lies inside [addr, addr+nbytes)
+        (a mapping that is about to be unmapped)."""
+        end = addr + nbytes
+        with self._lock:
+            keep = []
+            for (a, e) in self._ranges:
+                if a >= addr and e <= end:
+                    _kern().dw_host_unregister(ctypes.c_void_p(a))
+                else:
+                    keep.append((a, e))
+            self._ranges = keep
+
+    def covers(self, addr: int, nbytes: int) -> bool:
+        return all(p for _a, _n, p in self.split(addr, nbytes))
+
+
+# One registry per process: a deep standby pre-registers the checkpoint shm
+# (prewarm.py) before the engine and its copier exist.
+PINNED = PinnedRegistry()
+
 
 _FENCED = None  # copiers with a pending overlapped snapshot (weak set)
 
@@ -198,7 +219,13 @@ class GpuCopier:
         self.flush_mode = os.environ.get("DWAMD_FLUSH_MODE", "memcpy")
         self.flush_blocks = int(os.environ.get("DWAMD_FLUSH_BLOCKS", "64"))
         self.flush_stats: List[Tuple[int, float]] = []
-        self.pinned = PinnedRegistry()
+        # (t_snapshot_enqueued, t_flush_start, t_flush_end, nbytes) per flush
+        self.flush_log: List[Tuple[float, float, float, int]] = []
+        self.pinned = PINNED
+        # Future of the engine's background shm preparation (prefault +
+        # hipHostRegister of this rank's slices): the flush -- never the
+        # training pause -- waits for it.
+        self.pending_prep: Optional[Future] = None
         # Snapshot staging in HBM.  Two buffers when the card has room (288 GB
         # MI355X: a 22 GB GPT2-1.5B state twice is nothing): snapshot k+1 then
         # never waits for the PCIe flush of snapshot k -- the flushes queue on
@@ -307,7 +334,8 @@ class GpuCopier:
             for e, a, b in intersect_extents(layout.cpu_extents(), lo, hi):
                 runtime().dw_memcpy_parallel(ctypes.c_void_p(shm_payload_addr + a),
                                              ctypes.c_void_p(e.src_ptr + (a - e.offset)), b - a, 4)
-            pinned = self.pinned.ensure(shm_payload_addr + lo, n)
+        prep = self.pending_prep
+        t_enq = time.perf_counter()
         ev = torch.cuda.Event()
         ev.record(copy_stream)
         if copy_stream is not cur:
@@ -319,6 +347,11 @@ class GpuCopier:
         # for the whole PCIe transfer and stall the training thread's launches.
         def flush():
             if n > 0:
+                if prep is not None:
+                    prep.result()  # segment prefault + registration (first save of a segment)
+                # registering here (flush thread), not in the training pause:
+                # a no-op once the range is covered
+                pinned = self.pinned.ensure(shm_payload_addr + lo, n)
                 with torch.cuda.stream(self.side_stream):
                     self.side_stream.wait_event(ev)  # device-side dependency only
                     t0 = time.perf_counter()
@@ -336,8 +369,9 @@ class GpuCopier:
                             _check(_kern().dw_memcpy_async(ctypes.c_void_p(a), ctypes.c_void_p(src + (a - dst)), c,
                                                            1 if p else 3, sp), "D2H flush")
                 _check(_kern().dw_stream_sync(ctypes.c_void_p(self.side_stream.cuda_stream)), "flush sync")
-                dt = time.perf_counter() - t0
-                self.flush_stats.append((n, dt))
+                t1 = time.perf_counter()
+                self.flush_stats.append((n, t1 - t0))
+                self.flush_log.append((t_enq, t0, t1, n))
             else:
                 with torch.cuda.stream(self.side_stream):
                     self.side_stream.wait_event(ev)

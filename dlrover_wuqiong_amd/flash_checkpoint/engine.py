@@ -125,6 +125,13 @@ class CheckpointEngine(ABC):
     def __init__(self, checkpoint_dir: str, storage: Optional[CheckpointStorage] = None,
                  comm_backend: str = "", save_timeout: int = CheckpointConstant.SAVE_TIMEOUT,
                  replica_count: int = 0, replicated: bool = False):
+        from ..elastic_agent.standby import is_standby
+
+        if is_standby():
+            # a deep standby has no rank yet: it must block in standby_point()
+            # before touching the node's checkpoint (it would otherwise write
+            # the live job's shm as a world-1 trainer)
+            raise RuntimeError("checkpoint engine created in a deep standby before standby_point()")
         _LocalSaverThread.ensure()
         self.checkpoint_dir = checkpoint_dir
         self.storage = storage or get_checkpoint_storage()
@@ -164,6 +171,9 @@ class CheckpointEngine(ABC):
         self._held_slots = set()  # slots whose lock this process holds until their flush lands
         self._gc_frozen = False
         self._generation = 0
+        self._shm_prep = None  # Future: background prefault + pin of this rank's slot slices
+        self._prep_pool = None
+        self._prepped_for = None
         self._last_save_blocking = 0.0
         self._notify_agent_to_create_saver()
         self._update_saver_config()
@@ -242,7 +252,11 @@ class CheckpointEngine(ABC):
         return layout
 
     def _ensure_shm(self, total: int):
-        """(Re)create the segment when the payload size changes."""
+        """(Re)create the segment when the payload size changes.  Only the
+        create/attach (ftruncate + mmap, ~ms) happens here, inside the
+        training pause; prefaulting and hipHostRegister of this rank's slices
+        (~1 s per 20 GB) run on a background thread that the first flush --
+        not the training thread -- waits for."""
         h = self._shm_handler
         cur = h.payload_size if h.shared_memory is not None else -1
         need_resize = cur != total
@@ -250,6 +264,8 @@ class CheckpointEngine(ABC):
             # registrations of the old mapping must not outlive it (a new
             # mmap may land on the same addresses and look pinned)
             self._copier.wait()
+            if self._shm_prep is not None:
+                self._shm_prep.result()
             self._copier.pinned.release_all()
         if self._replicated:
             # every local rank plans the same layout -> same decision
@@ -258,7 +274,6 @@ class CheckpointEngine(ABC):
                 if self._local_rank == 0:
                     h.close()
                     h.init_shared_memory(create=True, size=total)
-                    h.shared_memory.prefault(8)
                 self._ctl_barrier()
                 if self._local_rank != 0:
                     h.close()
@@ -268,23 +283,47 @@ class CheckpointEngine(ABC):
         elif need_resize:
             h.close()
             h.init_shared_memory(create=True, size=total)
-            h.shared_memory.prefault(8)
             self._generation += 1
             self._next_slot = None
-        if need_resize:
-            self._pin_slots(total)
+        key = (h.shared_memory.ino if h.shared_memory is not None else -1, total)
+        if self._prepped_for != key:
+            # new segment, or an existing one this process attached (restart):
+            # make sure every slot this rank writes is pinned before its flush
+            self._prepped_for = key
+            self._start_shm_prep(total, prefault=need_resize)
 
-    def _pin_slots(self, total: int):
-        """hipHostRegister this rank's slice of EVERY slot now: registering a
-        96 GB slot costs ~0.6 s, which otherwise lands in the training pause
-        of the first save that rotates onto that slot."""
+    def _start_shm_prep(self, total: int, prefault: bool):
         copier = self._device_copier()
-        if copier is None or total <= 0:
-            return
         h = self._shm_handler
+        if total <= 0 or h.shared_memory is None:
+            return
         lo, hi = split_ranges(total, self._num_slices)[self._slice_idx]
-        for slot in range(h.num_slots):
-            copier.pinned.ensure(h.payload_addr(slot) + lo, hi - lo)
+        ranges = [(h.payload_addr(slot) + lo, hi - lo) for slot in range(h.num_slots)]
+
+        def prep():
+            import ctypes
+
+            from .._native import runtime
+
+            t0 = time.perf_counter()
+            for addr, n in ranges:
+                if prefault and n > 0:
+                    # a fresh segment: populate with parallel threads (faster
+                    # than the single-threaded faulting inside hipHostRegister)
+                    runtime().dw_prefault(ctypes.c_void_p(addr), n, 8)
+                if copier is not None:
+                    copier.pinned.ensure(addr, n)
+            if _TIMING:
+                logger.info(f"shm prep ({len(ranges)} slot slices, {hi - lo} B each): "
+                            f"{1000 * (time.perf_counter() - t0):.1f} ms (background)")
+
+        from concurrent.futures import ThreadPoolExecutor
+
+        if self._prep_pool is None:
+            self._prep_pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="dwamd-shm-prep")
+        self._shm_prep = self._prep_pool.submit(prep)
+        if copier is not None:
+            copier.pending_prep = self._shm_prep
 
     # ----------------------------------------------------------- core save
     def save_state_dict_to_memory(self, state_dict: Dict, conf: CheckpointConfig) -> bool:
@@ -539,6 +578,11 @@ class CheckpointEngine(ABC):
 
     def close(self):
         try:
+            if self._shm_prep is not None:
+                self._shm_prep.result()
+            if self._prep_pool is not None:
+                self._prep_pool.shutdown(wait=True)
+                self._prep_pool = None
             if self._copier is not None:
                 self._copier.wait()
                 self._wait_own_lock_release(timeout=30)

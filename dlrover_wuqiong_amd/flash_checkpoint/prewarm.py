@@ -1,0 +1,113 @@
+"""Pre-pinning of the node's flash-checkpoint shm before a worker needs it.
+
+A restarted worker restores from the agent-owned shm segment.  The DMA
+itself runs at ~55 GB/s per GPU, but the host range must first be
+``hipHostRegister``'ed (page-table walk + pinning, ~0.5 s per 20 GB), and its
+first save after the restart would pay the same for the other slot.  A deep
+standby (``elastic_agent/standby.py``) calls
+:func:`prepin_local_checkpoint_shm` while it waits: it maps the segment(s)
+this local rank will touch, registers exactly its byte ranges (its slice of
+every slot for a replicated checkpoint, the whole payload of its own shard
+otherwise) with the process-wide :data:`~.copier.PINNED` registry, and parks
+the mapping so the checkpoint engine adopts the *same* virtual addresses
+(registrations are per address range).  Calling it again is cheap: a
+segment that was re-created (new inode, e.g. resized) is unregistered,
+unmapped and pinned afresh; ranges that became known later (slice metadata
+written by the first save) are added.
+"""
+
+import time
+from typing import Dict, List, Tuple
+
+from ..common import env_utils
+from ..common.log import logger
+from ..common.multi_process import SharedDict, SharedMemory
+from .shm_handler import (_ADOPTABLE, DLROVER_CKPT_CONFIG_KEY, HEADER_BYTES, MAGIC, CheckpointSharedObjPrefix,
+                          adopt_mapping)
+
+_PINNED_BYTES: Dict[str, int] = {}
+
+
+def _slot_ranges(shm: SharedMemory, shard: int, local_rank: int) -> List[Tuple[int, int]]:
+    import numpy as np
+
+    hdr = np.frombuffer(shm.buf, dtype=np.int64, count=HEADER_BYTES // 8)
+    if int(hdr[0]) != MAGIC:
+        return []
+    size, stride, nslots = int(hdr[1]), int(hdr[3]), int(hdr[4])
+    out = []
+    for s in range(nslots):
+        try:
+            meta = SharedDict(f"{CheckpointSharedObjPrefix.META_NAME}{shard}_{s}", create=False, timeout=0.2).get()
+        except FileNotFoundError:
+            meta = {}
+        cfg = meta.get(DLROVER_CKPT_CONFIG_KEY)
+        nsl = max(1, getattr(cfg, "num_slices", 1)) if cfg is not None else 1
+        base = HEADER_BYTES + s * stride
+        if nsl > 1:
+            from .layout import split_ranges
+
+            if local_rank >= nsl:
+                continue
+            lo, hi = split_ranges(size, nsl)[local_rank]
+        elif shard == local_rank:
+            lo, hi = 0, size
+        else:
+            continue
+        if hi > lo:
+            out.append((shm.addr + base + lo, hi - lo))
+    return out
+
+
+def prepinned_bytes() -> int:
+    return sum(_PINNED_BYTES.values())
+
+
+def prepin_local_checkpoint_shm() -> float:
+    """Returns seconds spent.  No-op (0.0) when no segment exists yet."""
+    import torch
+
+    if not torch.cuda.is_available():
+        return 0.0
+    from .copier import PINNED
+
+    t0 = time.time()
+    lr = env_utils.get_local_rank()
+    changed = False
+    for shard in sorted({0, lr}):
+        name = CheckpointSharedObjPrefix.SHM_NAME + str(shard)
+        shm = _ADOPTABLE.get(name)
+        if shm is not None and shm.stale():
+            # re-created by the live workers (resize): drop the old pins + mapping
+            PINNED.release_range(shm.addr, shm.size)
+            _ADOPTABLE.pop(name, None)
+            _PINNED_BYTES.pop(name, None)
+            shm.close()
+            shm = None
+        if shm is None:
+            if not SharedMemory.exists(name):
+                continue
+            try:
+                shm = SharedMemory(name, create=False)
+            except FileNotFoundError:
+                continue
+        ranges = _slot_ranges(shm, shard, lr)
+        if not ranges:
+            if name not in _ADOPTABLE:
+                shm.close()
+            continue
+        nbytes = 0
+        for addr, n in ranges:
+            # no explicit prefault: the live worker may be flushing into these
+            # pages; hipHostRegister populates whatever is still missing
+            if PINNED.covers(addr, n):
+                nbytes += n
+            elif PINNED.ensure(addr, n):
+                nbytes += n
+                changed = True
+        adopt_mapping(name, shm)
+        _PINNED_BYTES[name] = nbytes
+    dt = time.time() - t0
+    if changed:
+        logger.info(f"standby pre-pinned checkpoint shm {dict(_PINNED_BYTES)} in {dt:.2f}s")
+    return dt

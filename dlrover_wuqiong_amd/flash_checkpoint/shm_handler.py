@@ -50,6 +50,23 @@ DLROVER_CKPT_CONFIG_KEY = "_DLORVER_CKPT_CONFIG"
 EVENT_QUEUE_SIZE = 16  # checkpoint events buffered between workers and the saver
 
 
+_ADOPTABLE: Dict[str, SharedMemory] = {}
+
+
+def adopt_mapping(name: str, shm: SharedMemory):
+    """Park an already-mapped (and typically hipHostRegister'ed) segment so
+    the next attach of ``name`` in this process reuses the same addresses
+    (see ``prewarm.py``)."""
+    _ADOPTABLE[name] = shm
+
+
+def _open_segment(name: str) -> SharedMemory:
+    shm = _ADOPTABLE.pop(name, None)
+    if shm is not None and not shm.stale() and not shm._closed:
+        return shm
+    return SharedMemory(name, create=False)
+
+
 def default_num_slots() -> int:
     return max(1, min(2, int(os.environ.get("DWAMD_CKPT_SLOTS", "2"))))
 
@@ -119,7 +136,7 @@ class SharedMemoryHandler:
                 self.shared_memory = SharedMemory(self._shm_name, create=True,
                                                   size=HEADER_BYTES + stride * self.num_slots)
             else:
-                self.shared_memory = SharedMemory(self._shm_name, create=False)
+                self.shared_memory = _open_segment(self._shm_name)
         except FileNotFoundError:
             self.shared_memory = None
             return False

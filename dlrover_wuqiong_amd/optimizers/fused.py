@@ -33,11 +33,21 @@ class _FlatOptimizer(torch.optim.Optimizer):
         self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
         self.master = flat.data.float().clone() if self.master_weights else None
-        self.step_count = 0
+        # the step counter lives in a CPU tensor that the state dict exposes
+        # directly: an in-place (flash checkpoint) restore restores it too
+        self._step_t = torch.zeros((), dtype=torch.float32)
         self.max_grad_norm = max_grad_norm
         self.grad_scale = 1.0  # e.g. 1/world for summed DDP gradients
         self._scalars = torch.zeros(4, dtype=torch.float32, device=dev)  # sumsq, coef, norm, pad
         self.last_grad_norm = None
+
+    @property
+    def step_count(self) -> int:
+        return int(self._step_t.item())
+
+    @step_count.setter
+    def step_count(self, v: int):
+        self._step_t.fill_(float(v))
 
     # ------------------------------------------------------------ helpers
     def _gscale_ptr(self):
@@ -81,7 +91,6 @@ class _FlatOptimizer(torch.optim.Optimizer):
         # The per-parameter views never change: build them once.  All params
         # share one "step" tensor (same value), updated in place.
         if getattr(self, "_sd_views", None) is None:
-            self._step_t = torch.zeros((), dtype=torch.float32)
             views = {}
             for i, (o, c) in enumerate(self.flat.offsets):
                 p = self.flat.params[i]
@@ -91,7 +100,6 @@ class _FlatOptimizer(torch.optim.Optimizer):
                     v["master_param"] = self.master[o:o + c].view(p.shape)
                 views[i] = v
             self._sd_views = views
-        self._step_t.fill_(float(self.step_count))
         state = {i: {"step": self._step_t, **v} for i, v in self._sd_views.items()}
         groups = []
         for g in self.param_groups:

@@ -36,16 +36,33 @@ def _rank_world():
 
 
 def maybe_inject_fault(step: int):
-    """Exit the process with code 17 at ``DWAMD_FAULT_INJECT_STEP`` on
+    """Kill this rank at ``DWAMD_FAULT_INJECT_STEP`` on
     ``DWAMD_FAULT_INJECT_RANK`` during the first run only (restart count 0).
-    Used by the goodput experiments and the agent tests."""
+    ``DWAMD_FAULT_INJECT_MODE``: ``exit`` (default, exit code 17) or
+    ``sigkill`` (the process is SIGKILLed: no handler, no flush, no cleanup
+    -- what a crashed/OOM-killed rank looks like to the agent).
+    Used by the goodput benchmark and the agent tests."""
     s = os.getenv(NodeEnv.FAULT_INJECT_STEP, "")
     if not s or int(os.getenv("TORCHELASTIC_RESTART_COUNT", "0")) != 0:
         return
     r = int(os.getenv(NodeEnv.FAULT_INJECT_RANK, "0"))
     if step == int(s) and _rank_world()[0] == r:
         logger.error(f"injected fault at step {step} on rank {r}")
+        if os.getenv("DWAMD_FAULT_INJECT_MODE", "exit") == "sigkill":
+            import signal
+
+            os.kill(os.getpid(), signal.SIGKILL)
         os._exit(17)
+
+
+def standby_point(prepin_shm: bool = True):
+    """Deep warm-standby hand-off (see ``elastic_agent/standby.py``): call
+    after world-independent set-up (device, model, optimizer, warm-up) and
+    before ``init_process_group``.  Returns ``None`` when this process is a
+    regular worker, activation info when it was a standby."""
+    from ..elastic_agent.standby import standby_point as _sp
+
+    return _sp(prepin_shm=prepin_shm)
 
 
 @dataclass

@@ -63,6 +63,15 @@ def parse_args(argv=None):
     p.add_argument("--save_at_breakpoint", "--save-at-breakpoint", type=_bool, default=True)
     p.add_argument("--relaunch-on-hang", "--relaunch_on_hanging", type=float, default=0.0, metavar="SECONDS",
                    help="relaunch the worker group when a worker heartbeat is older than SECONDS")
+    p.add_argument("--standby-mode", "--standby_mode", choices=["import", "deep", "off"],
+                   default=os.getenv("DWAMD_STANDBY_MODE", "import"),
+                   help="warm standby per local rank: 'import' pre-imports torch (any script); 'deep' runs the "
+                        "script up to trainer.elastic.standby_point() (model on GPU, kernels warm, ckpt shm pinned)")
+    p.add_argument("--standby-delay", "--standby_delay", type=float,
+                   default=float(os.getenv("DWAMD_STANDBY_DELAY", "3")),
+                   help="seconds after (re)starting the workers before the next standbys are spawned")
+    p.add_argument("--event-log", "--event_log", default=os.getenv("DWAMD_AGENT_EVENT_LOG", ""),
+                   help="append the agent's timeline (failures, restarts, rendezvous) as JSON lines")
     p.add_argument("--xpu-timer", "--xpu_timer", action="store_true",
                    help="install the xpu_timer (GEMM/collective timing + hang detection) in every worker")
     p.add_argument("--accelerator", default=Accelerators.AMD_GPU,
@@ -116,6 +125,11 @@ def build_config(a) -> "ElasticLaunchConfig":
                               save_at_breakpoint=a.save_at_breakpoint, auto_config=a.auto_config,
                               auto_tunning=a.auto_tunning, accelerator=a.accelerator, log_dir=a.log_dir,
                               node_rank=a.node_rank, local_addr=a.local_addr)
+    cfg.warm_standby = a.standby_mode != "off"
+    if a.standby_mode != "off":
+        cfg.standby_mode = a.standby_mode
+    cfg.standby_delay = a.standby_delay
+    cfg.event_log = a.event_log
     if a.relaunch_on_hang > 0:
         cfg.hang_timeout = a.relaunch_on_hang
     if a.xpu_timer:
