@@ -275,6 +275,7 @@ def summarize(a, run_dir, n, wall):
             "first_step": round(first_step_end - inc1["t_restored"], 3),
         },
         "standby_prepin_s": inc1.get("prepin_s"),
+        "restore_source": inc1.get("restore_source"),
         "restarts": len(started) - 1,
     })
     # extrapolation to production: one failure per hour, a checkpoint every
@@ -344,8 +345,10 @@ def worker(a) -> int:
         x = torch.randint(0, cfg.vocab_size, (B, S + 1), device=device)
         model(x[:, :-1], x[:, 1:]).backward()
         flat.zero_grad()
+        del x
         if cuda:
             torch.cuda.synchronize()
+            torch.cuda.empty_cache()  # the parked standby keeps only model + optimizer (+ HBM staging)
     info = standby_point()  # deep standby: parks here until the agent activates it
     t_act = time.time()
 
@@ -447,11 +450,16 @@ def worker(a) -> int:
         if ctl and not a.no_fault:
             deadline = time.time() + 600
             lw = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
-            # parked + (on a GPU) this rank's shm slices registered
-            marks = ["standby_ready."] + (["standby_pinned."] if cuda else [])
+            # parked + (on a GPU) this rank's shm slices registered and the
+            # HBM-tier staging buffers published
+            marks = ["standby_ready.{}"] + (["standby_pinned.{}", "hbm_staging.{}.json"] if cuda else [])
             while time.time() < deadline and not all(
-                    os.path.exists(os.path.join(ctl, f"{m}{i}")) for i in range(lw) for m in marks):
+                    os.path.exists(os.path.join(ctl, m.format(i))) for i in range(lw) for m in marks):
                 time.sleep(0.05)
+            # one untimed save: the copier switches to the standby-owned
+            # staging buffers (waits for in-flight flushes once)
+            save()
+            ckpt.wait_latest_checkpoint()
         sync_all()
 
         # ---------------- timed: train + flash checkpoint every ckpt_interval steps
@@ -573,7 +581,8 @@ def worker(a) -> int:
         emit({"event": "start", "incarnation": incarnation, "t": time.time(), "restored_step": step,
               "restore_sec": restore_sec, "restore_ok": restore_ok, "t_proc": t_proc, "t_activated": t_act,
               "t_pg": t_pg, "t_ckpt": t_ckpt, "t_restored": t_restored,
-              "prepin_s": info.get("prepin_s") if info else None})
+              "prepin_s": info.get("prepin_s") if info else None,
+              "restore_source": getattr(ckpt.engine, "last_restore_source", None)})
         if not restore_ok:
             log(f"[rank {rank}] restore from memory failed: starting over")
         start_step = step

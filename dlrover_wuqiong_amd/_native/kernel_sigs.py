@@ -19,6 +19,13 @@ SIGS = {
     "dw_stream_create_prio": (vp, [i32, c.POINTER(i32)]),
     "dw_host_device_ptr": (vp, [vp]),
     "dw_stream_copy": (i32, [vp, vp, u64, i32, vp]),
+    "dw_device_malloc": (i32, [u64, c.POINTER(vp)]),
+    "dw_device_free": (i32, [vp]),
+    "dw_ipc_handle_size": (i32, []),
+    "dw_ipc_get_handle": (i32, [vp, vp]),
+    "dw_ipc_open_handle": (i32, [vp, c.POINTER(vp)]),
+    "dw_ipc_close_handle": (i32, [vp]),
+    "dw_mem_get_info": (i32, [c.POINTER(u64), c.POINTER(u64)]),
     "dw_hip_error_string": (cp, [i32]),
     "dw_kernels_abi_version": (i32, []),
     # xpu_timer.hip

@@ -14,6 +14,8 @@
 //    an explicit stream (so the D2H/H2D overlap with training).
 #include "dw_common.h"
 
+#include <cstring>
+
 struct CopyDesc {
   const char* src;
   char* dst;
@@ -166,6 +168,32 @@ extern "C" int dw_stream_copy(void* dst, const void* src, uint64_t bytes, int bl
   hipLaunchKernelGGL(stream_copy_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const u32x4*)src,
                      (u32x4*)dst, (int64_t)(bytes >> 4));
   DW_LAUNCH_RET;
+}
+
+// ------------------------- cross-process HBM buffers ------------------------
+// The checkpoint staging buffers of a local rank are allocated by its warm
+// standby process and imported by the live worker (dmabuf IPC), so a snapshot
+// survives the worker's death in HBM and the replacement restores with a
+// device-to-device copy instead of a PCIe H2D.  Plain hipMalloc (not the
+// torch caching allocator): an IPC handle names a whole allocation.
+extern "C" int dw_device_malloc(uint64_t bytes, void** out) { return (int)hipMalloc(out, bytes); }
+extern "C" int dw_device_free(void* p) { return (int)hipFree(p); }
+extern "C" int dw_ipc_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+extern "C" int dw_ipc_get_handle(void* p, void* handle_out) {
+  return (int)hipIpcGetMemHandle((hipIpcMemHandle_t*)handle_out, p);
+}
+extern "C" int dw_ipc_open_handle(const void* handle, void** out) {
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof(h));
+  return (int)hipIpcOpenMemHandle(out, h, hipIpcMemLazyEnablePeerAccess);
+}
+extern "C" int dw_ipc_close_handle(void* p) { return (int)hipIpcCloseMemHandle(p); }
+extern "C" int dw_mem_get_info(uint64_t* free_b, uint64_t* total_b) {
+  size_t f = 0, t = 0;
+  hipError_t e = hipMemGetInfo(&f, &t);
+  *free_b = f;
+  *total_b = t;
+  return (int)e;
 }
 
 extern "C" const char* dw_hip_error_string(int e) { return hipGetErrorString((hipError_t)e); }

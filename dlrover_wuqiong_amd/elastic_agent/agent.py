@@ -498,6 +498,10 @@ class ElasticTrainingAgent:
 
     def _monitor_workers(self) -> RunResult:
         codes = [(w, w.proc.poll()) for w in self.workers]
+        # a SIGKILLed / crashing worker is reaped only after its address space
+        # (tens of GB of pinned host + GPU mappings) is torn down, ~0.7 s on
+        # MI355X; the kernel publishes the exit code before that teardown
+        codes = [(w, c if c is not None else _exiting_code(w.proc.pid)) for w, c in codes]
         failed = {w.global_rank: self._failure(w, c) for w, c in codes if c not in (None, 0)}
         if failed:
             return RunResult(RunResult.FAILED, failed)
@@ -628,22 +632,31 @@ class ElasticTrainingAgent:
                 self._stop_workers(timeout=self.config.failure_stop_timeout,
                                    wait=self.config.standby_mode != "deep")
                 self._event("workers_stopped")
-                try:
-                    self.client.report_failures(json.dumps(res.failures), self.restart_count, level)
-                except Exception:
-                    pass
-                self._save_ckpt_to_storage()
                 if level == TrainingExceptionLevel.NODE_ERROR and self.config.exit_on_node_error:
                     # hardware signature: let the platform replace this node
                     logger.error("GPU/driver fault signature in the worker log: exiting for node relaunch")
+                    try:
+                        self.client.report_failures(json.dumps(res.failures), self.restart_count, level)
+                    except Exception:
+                        pass
+                    self._save_ckpt_to_storage()
                     self._discard_standbys()
                     if self._bp_thread is not None:
                         self._bp_thread.join(timeout=600)
                     self.client.report_node_event(NodeStatus.FAILED, "node error")
                     return 2
-                if self.remaining_restarts > 0:
+                restart = self.remaining_restarts > 0
+                if restart:
+                    # restart first: reporting and the breakpoint persist are
+                    # off the recovery critical path
                     self.remaining_restarts -= 1
                     self._restart_workers()
+                try:
+                    self.client.report_failures(json.dumps(res.failures), self.restart_count - int(restart), level)
+                except Exception:
+                    pass
+                self._save_ckpt_to_storage()
+                if restart:
                     continue
                 self._discard_standbys()
                 self.client.report_node_event(NodeStatus.FAILED, "max restarts reached")
@@ -714,6 +727,35 @@ class ElasticTrainingAgent:
                 os.remove(f)
             except OSError:
                 pass
+
+
+_PF_EXITING = 0x4
+
+
+def _exiting_code(pid: int) -> Optional[int]:
+    """Exit status of a process that is already inside ``do_exit`` but not
+    yet reaped (``Popen.returncode`` convention: -signal or exit code), or
+    None while it runs.  Reads ``/proc/<pid>/stat``: ``flags`` (field 9)
+    carries PF_EXITING, ``exit_code`` (field 52, Linux >= 3.5) the wait
+    status.  A clean exit (0) is left to ``poll()``: success needs the real
+    reap, only failures are worth acting on early."""
+    try:
+        with open(f"/proc/{pid}/stat", "rb") as f:
+            raw = f.read()
+    except OSError:
+        return None
+    fields = raw[raw.rfind(b")") + 2:].split()
+    if len(fields) < 50:
+        return None
+    try:
+        flags = int(fields[6])
+        status = int(fields[49])
+    except ValueError:
+        return None
+    if not flags & _PF_EXITING or status == 0:
+        return None
+    sig = status & 0x7F
+    return -sig if sig else (status >> 8) & 0xFF
 
 
 def _local_ip() -> str:

@@ -107,6 +107,22 @@ def _pinned_bytes() -> int:
         return 0
 
 
+def _publish_hbm_staging(ctl: str, lr: str):
+    """Own the live worker's checkpoint staging buffers (HBM tier): they
+    then survive the worker, and this standby restores from them D2D."""
+    if os.environ.get("DWAMD_HBM_TIER", "1") != "1":
+        return
+    try:
+        from ..flash_checkpoint.hbm_tier import publish_standby_buffers
+        from ..flash_checkpoint.prewarm import local_slice_bytes
+
+        n = local_slice_bytes()
+        if n > 0:
+            publish_standby_buffers(ctl, int(lr), n)
+    except Exception as e:  # never fatal: the restore falls back to shm
+        print(f"[standby] HBM staging not published: {e}", file=sys.stderr)
+
+
 def _mark(ctl: str, prefix: str, lr: str, text: str):
     if not ctl:
         return
@@ -134,6 +150,8 @@ def standby_point(prepin_shm: bool = True, repin_interval: float = 0.25) -> Opti
     ctl = os.environ.get("DWAMD_AGENT_CTL_DIR", "")
     lr = os.environ.get("LOCAL_RANK", "0")
     pin_s = _prepin_checkpoint_shm() if prepin_shm else 0.0
+    if prepin_shm:
+        _publish_hbm_staging(ctl, lr)
     _mark(ctl, READY_PREFIX, lr, f"{os.getpid()} {time.time()}\n")
     pinned_marked = False
     t0 = time.time()
@@ -155,6 +173,7 @@ def standby_point(prepin_shm: bool = True, repin_interval: float = 0.25) -> Opti
                 break
         elif prepin_shm:
             pin_s += _prepin_checkpoint_shm()
+            _publish_hbm_staging(ctl, lr)
     cmd = json.loads(buf.split(b"\n", 1)[0].decode())
     _apply(cmd)
     _activated = {"activated_at": time.time(), "waited_s": time.time() - t0, "prepin_s": pin_s,

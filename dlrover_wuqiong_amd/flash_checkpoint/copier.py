@@ -232,6 +232,8 @@ class GpuCopier:
         # the single D2H thread and the training pause is just the HBM copy.
         # One buffer (the old wait-for-flush behaviour) when memory is tight.
         self._stagings: List[Optional[torch.Tensor]] = [None, None]
+        self._ext = None  # HbmBuffer staging owned by a standby (hbm_tier.py)
+        self._ext_key = None
         self._futures: List[Optional[Future]] = [None, None]
         self._nbuf = 0  # decided at the first snapshot
         self._next_stage = 0
@@ -254,6 +256,50 @@ class GpuCopier:
     @property
     def _staging(self) -> Optional[torch.Tensor]:
         return self._stagings[0]
+
+    # ------------------------------------------------- HBM tier (hbm_tier.py)
+    def _refresh_external(self, nbytes: int):
+        """Snapshot into standby-owned buffers when available: this process's
+        own (it was the standby) or the current standby's published ones.
+        Switching waits for in-flight flushes of the old buffers."""
+        from . import hbm_tier
+
+        if os.environ.get("DWAMD_HBM_TIER", "1") != "1" or nbytes <= 0:
+            return
+        cand, key = None, None
+        own = [b for b in hbm_tier.OWNED if b.ptr and b.nbytes >= nbytes]
+        info = hbm_tier.find_published(os.environ.get("DWAMD_AGENT_CTL_DIR", ""),
+                                       int(os.environ.get("LOCAL_RANK", "0")))
+        if info is not None and int(info["nbytes"]) >= nbytes and len(info["handles"]) >= 2:
+            if info["_key"] == self._ext_key:
+                return
+            key = info["_key"]
+        elif own and len(own) >= 2:
+            if self._ext_key == ("own", os.getpid()):
+                return
+            cand, key = own[:2], ("own", os.getpid())
+        else:
+            return
+        self.wait()
+        if cand is None:
+            cand = hbm_tier.import_published(info)
+            if cand is None:
+                self._ext_key = key  # do not retry a failing import every save
+                return
+        old = self._ext
+        self._ext, self._ext_key = cand, key
+        self._stagings = [cand[0], cand[1]]
+        self._nbuf = 2
+        self._next_stage = 0
+        self._desc_cache.clear()
+        for b in old or []:
+            b.release()
+        logger.info(f"checkpoint staging: using HBM buffers owned by pid {cand[0].owner_pid} "
+                    f"({'own' if cand[0].owned else 'imported from the standby'})")
+
+    def stage_owner(self, idx: int) -> int:
+        b = self._stagings[idx] if idx < len(self._stagings) else None
+        return getattr(b, "owner_pid", os.getpid())
 
     def _alloc(self, idx: int, nbytes: int) -> torch.Tensor:
         t = self._stagings[idx]
@@ -302,13 +348,20 @@ class GpuCopier:
 
     # ----------------------------------------------------------------- save
     def save_slice(self, layout: Layout, shm_payload_addr: int, lo: int, hi: int,
-                   on_done: Callable[[], None], sync: bool = False):
-        """Snapshot payload bytes [lo, hi) of ``layout`` and flush to shm."""
+                   on_done: Callable[[], None], sync: bool = False,
+                   before_copy: Optional[Callable[[int], None]] = None):
+        """Snapshot payload bytes [lo, hi) of ``layout`` and flush to shm.
+        ``before_copy(staging_idx)`` runs before the snapshot is enqueued
+        (HBM-tier stamp invalidation)."""
         n = hi - lo
+        self._refresh_external(n)
         self._decide_buffers(n)
         self.wait_stage()  # this staging buffer's previous flush must have landed
         idx = self._next_stage
         self._next_stage = (idx + 1) % max(1, self._nbuf)
+        self.last_stage = idx
+        if before_copy is not None:
+            before_copy(idx)
         cur = torch.cuda.current_stream(self.device)
         copy_stream = cur
         if self.overlap and n > 0:
@@ -394,36 +447,48 @@ class GpuCopier:
 
     # ----------------------------------------------------------------- load
     def restore(self, pieces_gpu: List[Tuple[int, int, int]], shm_payload_addr: int, payload_bytes: int,
-                lo: int, hi: int, gather_group=None, world: int = 1):
+                lo: int, hi: int, gather_group=None, world: int = 1, hbm_src: Optional[int] = None):
         """Restore GPU targets.
 
         pieces_gpu: (payload_off, dst_addr, nbytes) for every GPU target.
         If ``gather_group`` is None this process copies every piece itself
         (H2D straight into the targets).  Otherwise this process H2D's only
-        its slice [lo, hi) into a full-size staging buffer, the group
+        its slice [lo, hi) into a full-size temporary buffer, the group
         all-gathers, and one kernel scatters into the targets.
+        ``hbm_src``: device address of an HBM-tier buffer holding payload
+        bytes [lo, hi) of the step being restored -- the slice is then copied
+        device-to-device (multi-copy kernel) instead of H2D from shm.
         """
         self.fence()  # the restore overwrites the state a pending snapshot still reads
         cur = torch.cuda.current_stream(self.device)
         if gather_group is None or world <= 1:
-            self._pipelined_h2d([(shm_payload_addr + off, dst, n) for off, dst, n in _merge_pieces(pieces_gpu)],
-                                cur)
+            merged = _merge_pieces(pieces_gpu)
+            if hbm_src is not None:
+                launch_multi_copy(build_descs([(hbm_src + (off - lo), dst, n) for off, dst, n in merged],
+                                              self.device), cur)
+            else:
+                self._pipelined_h2d([(shm_payload_addr + off, dst, n) for off, dst, n in merged], cur)
             return
         import torch.distributed as dist
 
         per = hi - lo
-        stg = self.staging(per * world)
+        # a temporary buffer, never the staging buffers: with the HBM tier they
+        # hold the checkpoint being restored
+        full = torch.empty(per * world, dtype=torch.uint8, device=self.device)
         # every rank's slice has the same size `per` (last one may be short in
         # payload terms but is padded): copy what exists.
         real = max(0, min(hi, payload_bytes) - lo)
         if real > 0:
-            self._pipelined_h2d([(shm_payload_addr + lo, stg.data_ptr() + lo, real)], cur)
-        full = stg[: per * world]
+            if hbm_src is not None:
+                launch_multi_copy(build_descs([(hbm_src, full.data_ptr() + lo, real)], self.device), cur)
+            else:
+                self._pipelined_h2d([(shm_payload_addr + lo, full.data_ptr() + lo, real)], cur)
         mine = full[lo: lo + per]
         dist.all_gather_into_tensor(full, mine, group=gather_group)
-        base = stg.data_ptr()
+        base = full.data_ptr()
         descs = build_descs([(base + off, dst, n) for off, dst, n in _merge_pieces(pieces_gpu)], self.device)
         launch_multi_copy(descs, cur)
+        del full
 
     def _pipelined_h2d(self, copies: List[Tuple[int, int, int]], stream, chunk: int = 512 << 20):
         """H2D of (host_src, dev_dst, nbytes) ranges.  Pinning (hipHostRegister,
@@ -454,6 +519,9 @@ class GpuCopier:
             self._executor.shutdown(wait=True)
             self.pinned.release_all()
             self._stagings = [None, None]
+            for b in self._ext or []:
+                b.release()
+            self._ext = None
             if self._cumask_ptr:
                 self.side_stream.synchronize()
                 _kern().dw_stream_destroy(ctypes.c_void_p(self._cumask_ptr))

@@ -175,6 +175,7 @@ class CheckpointEngine(ABC):
         self._prep_pool = None
         self._prepped_for = None
         self._last_save_blocking = 0.0
+        self.last_restore_source = None  # "hbm" | "shm" after an in-place restore
         self._notify_agent_to_create_saver()
         self._update_saver_config()
         from .replica import CkptReplicaManager
@@ -393,14 +394,25 @@ class CheckpointEngine(ABC):
         lo, hi = split_ranges(layout.total_bytes, self._num_slices)[self._slice_idx]
         step = conf.step
 
+        stage = {}
+
+        def before_copy(idx: int):
+            # HBM tier: this staging buffer is about to be overwritten
+            stage["idx"] = idx
+            h.set_hbm_stamp(self._slice_idx, idx, 0)
+
         def on_done():
             h.set_slice_step(slot, self._slice_idx, step)
+            if "idx" in stage:
+                # the staging buffer now holds exactly the bytes of the slice
+                # that just became complete in shm
+                h.set_hbm_stamp(self._slice_idx, stage["idx"], step, copier.stage_owner(stage["idx"]), hi - lo)
             if self._is_shard_owner:
                 self._release_when_complete(step, slot)
 
         has_gpu = any(e.device == "cuda" for e in layout.extents)
         if has_gpu and copier is not None:
-            copier.save_slice(layout, h.payload_addr(slot), lo, hi, on_done)
+            copier.save_slice(layout, h.payload_addr(slot), lo, hi, on_done, before_copy=before_copy)
         else:
             self._cpu_save_slice(layout, h.payload_addr(slot), lo, hi)
             on_done()
@@ -517,7 +529,7 @@ class CheckpointEngine(ABC):
                     f"(complete in memory: {sorted(h.complete_steps())})")
         tree = h.get_meta(slot)["tree"]
         if target is not None:
-            sd = self._restore_into(tree, target, slot)
+            sd = self._restore_into(tree, target, slot, step)
             if sd is not None:
                 return step, sd
         sd = h.load_state_dict(slot)
@@ -525,7 +537,21 @@ class CheckpointEngine(ABC):
             sd.pop(DLROVER_CKPT_CONFIG_KEY, None)
         return step, sd
 
-    def _restore_into(self, tree, target, slot: int):
+    def _hbm_source(self, step: int, lo: int, hi: int) -> Optional[int]:
+        """Device address of an HBM-tier buffer owned by this process that
+        holds payload bytes [lo, hi) of ``step`` (see hbm_tier.py)."""
+        from . import hbm_tier
+
+        if not hbm_tier.OWNED or os.environ.get("DWAMD_HBM_TIER", "1") != "1":
+            return None
+        h = self._shm_handler
+        for b, buf in enumerate(hbm_tier.OWNED[:2]):
+            st, pid, nb = h.hbm_stamp(self._slice_idx, b)
+            if st == step and pid == os.getpid() and nb == hi - lo and buf.ptr and buf.nbytes >= nb:
+                return buf.ptr
+        return None
+
+    def _restore_into(self, tree, target, slot: int, step: int = 0):
         """Fast path: H2D (sliced + all-gather for replicated) straight into
         the live tensors of ``target`` (same structure as the saved dict)."""
         from .copier import match_targets
@@ -552,11 +578,18 @@ class CheckpointEngine(ABC):
         if copier is None:
             it = iter([t for _, t in pairs])
             return traverse(tree, lambda v: next(it) if isinstance(v, TensorMeta) else v)
+        s_lo, s_hi = split_ranges(total, self._num_slices)[self._slice_idx]
+        hbm_src = self._hbm_source(step, s_lo, s_hi) if step > 0 else None
+        self.last_restore_source = "hbm" if hbm_src is not None else "shm"
         if self._replicated and self._num_slices > 1 and self._gather_group is not None:
             per = split_ranges(total, self._num_slices)[0][1]
             lo = self._slice_idx * per
-            copier.restore(gpu_pieces, base, total, lo, lo + per, self._gather_group, self._num_slices)
+            copier.restore(gpu_pieces, base, total, lo, lo + per, self._gather_group, self._num_slices,
+                           hbm_src=hbm_src)
+        elif self._num_slices <= 1:
+            copier.restore(gpu_pieces, base, total, 0, total, hbm_src=hbm_src)
         else:
+            # replicated but no gather group (gloo world): every byte from shm
             copier.restore(gpu_pieces, base, total, 0, total)
         it = iter([t for _, t in pairs])
 

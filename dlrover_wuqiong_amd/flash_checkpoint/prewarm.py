@@ -26,22 +26,27 @@ from .shm_handler import (_ADOPTABLE, DLROVER_CKPT_CONFIG_KEY, HEADER_BYTES, MAG
                           adopt_mapping)
 
 _PINNED_BYTES: Dict[str, int] = {}
+_SLICE_BYTES: Dict[str, int] = {}  # segment -> this rank's slice bytes (layout known)
 
 
-def _slot_ranges(shm: SharedMemory, shard: int, local_rank: int) -> List[Tuple[int, int]]:
+def _slot_ranges(shm: SharedMemory, shard: int, local_rank: int) -> Tuple[List[Tuple[int, int]], bool]:
+    """(addr, nbytes) of this rank's slice in every slot, and whether the
+    slice layout is known (slot metadata written by a save)."""
     import numpy as np
 
     hdr = np.frombuffer(shm.buf, dtype=np.int64, count=HEADER_BYTES // 8)
     if int(hdr[0]) != MAGIC:
-        return []
+        return [], False
     size, stride, nslots = int(hdr[1]), int(hdr[3]), int(hdr[4])
     out = []
+    known = False
     for s in range(nslots):
         try:
             meta = SharedDict(f"{CheckpointSharedObjPrefix.META_NAME}{shard}_{s}", create=False, timeout=0.2).get()
         except FileNotFoundError:
             meta = {}
         cfg = meta.get(DLROVER_CKPT_CONFIG_KEY)
+        known = known or cfg is not None
         nsl = max(1, getattr(cfg, "num_slices", 1)) if cfg is not None else 1
         base = HEADER_BYTES + s * stride
         if nsl > 1:
@@ -56,11 +61,16 @@ def _slot_ranges(shm: SharedMemory, shard: int, local_rank: int) -> List[Tuple[i
             continue
         if hi > lo:
             out.append((shm.addr + base + lo, hi - lo))
-    return out
+    return out, known
 
 
 def prepinned_bytes() -> int:
     return sum(_PINNED_BYTES.values())
+
+
+def local_slice_bytes() -> int:
+    """Bytes of the payload slice this local rank snapshots (0: unknown yet)."""
+    return max(_SLICE_BYTES.values(), default=0)
 
 
 def prepin_local_checkpoint_shm() -> float:
@@ -82,6 +92,7 @@ def prepin_local_checkpoint_shm() -> float:
             PINNED.release_range(shm.addr, shm.size)
             _ADOPTABLE.pop(name, None)
             _PINNED_BYTES.pop(name, None)
+            _SLICE_BYTES.pop(name, None)
             shm.close()
             shm = None
         if shm is None:
@@ -91,7 +102,9 @@ def prepin_local_checkpoint_shm() -> float:
                 shm = SharedMemory(name, create=False)
             except FileNotFoundError:
                 continue
-        ranges = _slot_ranges(shm, shard, lr)
+        ranges, known = _slot_ranges(shm, shard, lr)
+        if known and ranges:
+            _SLICE_BYTES[name] = ranges[0][1]
         if not ranges:
             if name not in _ADOPTABLE:
                 shm.close()

@@ -183,6 +183,31 @@ class SharedMemoryHandler:
         base = 8 + slot * MAX_SLICES
         return [int(self._header[base + i]) for i in range(n)]
 
+    # HBM-tier stamps (see hbm_tier.py): (step, owner pid, nbytes) per
+    # (slice, staging buffer)
+    def set_hbm_stamp(self, slice_idx: int, buf: int, step: int, pid: int = 0, nbytes: int = 0):
+        from .hbm_tier import MAX_STAMP_SLICES, stamp_index
+
+        if self._header is None or slice_idx >= MAX_STAMP_SLICES:
+            return
+        i = stamp_index(slice_idx, buf)
+        if step == 0:
+            self._header[i] = 0  # invalidate first: a reader never sees a stale step with new bytes
+            self._header[i + 1] = 0
+            self._header[i + 2] = 0
+        else:
+            self._header[i + 1] = pid
+            self._header[i + 2] = nbytes
+            self._header[i] = step
+
+    def hbm_stamp(self, slice_idx: int, buf: int):
+        from .hbm_tier import MAX_STAMP_SLICES, stamp_index
+
+        if self._header is None or slice_idx >= MAX_STAMP_SLICES:
+            return 0, 0, 0
+        i = stamp_index(slice_idx, buf)
+        return int(self._header[i]), int(self._header[i + 1]), int(self._header[i + 2])
+
     def reset_slices(self, slot: int, n: int):
         if self._header is not None:
             base = 8 + slot * MAX_SLICES
