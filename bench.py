@@ -155,7 +155,7 @@ def launcher(a) -> int:
         wargs.append("--act-ckpt")
     cmd = [sys.executable, "-u", "-m", "dlrover_wuqiong_amd.trainer.run", "--nnodes", "1", "--nproc-per-node",
            str(n), "--max-restarts", "1", "--monitor-interval", "0.05", "--standby-mode", "deep",
-           "--standby-delay", "0", "--event-log", os.path.join(run_dir, "agent.jsonl")] + wargs
+           "--standby-delay", "0", "--local-addr", "127.0.0.1", "--event-log", os.path.join(run_dir, "agent.jsonl")] + wargs
     log("bench launcher:", " ".join(cmd))
     t0 = time.time()
     # the agent's and workers' output goes to stderr: stdout carries the one JSON line

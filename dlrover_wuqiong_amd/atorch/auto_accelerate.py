@@ -422,6 +422,18 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
     if optim_func is not None:
         params = optim_param_func(model) if optim_param_func else model.parameters()
         args = dict(optim_args or {})
+        if kwargs.get("fused_optimizer", True):
+            # torch AdamW/Adam and ATorch AGD -> one multi-tensor HIP launch
+            # over the (DTensor-sharded) parameters, fp32 masters for bf16 ones
+            from ..optimizers.multi_tensor import fused_equivalent
+
+            fcls, fargs = fused_equivalent(optim_func, args)
+            if fcls is not None:
+                params = list(params)
+                n_groups = len(params) if params and isinstance(params[0], dict) else 1
+                if n_groups <= 16:
+                    optim_func, args = fcls, fargs
+                    logger.info(f"optimizer: {fcls.__name__} (multi-tensor HIP kernel)")
         if ctx.get("zero1"):
             from torch.distributed.optim import ZeroRedundancyOptimizer
 

@@ -161,22 +161,80 @@ PINNED = PinnedRegistry()
 
 
 _FENCED = None  # copiers with a pending overlapped snapshot (weak set)
+_OPTIMIZERS = None  # optimizers seen stepping (weak set): their tensors are written only in step()
 
 
-def _optimizer_step_fence(_opt, _args, _kwargs):
+def _optimizer_step_fence(opt, _args, _kwargs):
+    _OPTIMIZERS.add(opt)
     for c in list(_FENCED):
         c.fence()
     _FENCED.clear()
 
 
+def register_optimizer(opt):
+    """Declare an optimizer whose parameters/state are written only inside
+    its ``step()`` (done automatically at its first step)."""
+    _install_fence_hook()
+    _OPTIMIZERS.add(opt)
+
+
+def fence_all():
+    """Order the current stream after every pending overlapped snapshot: call
+    before writing checkpointed tensors outside ``Optimizer.step`` (e.g. a
+    SAM first step)."""
+    if _FENCED:
+        for c in list(_FENCED):
+            c.fence()
+        _FENCED.clear()
+
+
+def _step_only_ranges() -> List[Tuple[int, int]]:
+    """Sorted, merged device address ranges of every storage that only an
+    optimizer step writes (parameters + optimizer state of the optimizers
+    seen so far).  An overlapped snapshot may read these after the save call
+    returns; anything else (BatchNorm running stats, EMA buffers, ...) can be
+    written by the next forward and is copied before the call returns."""
+    rng = []
+    for opt in list(_OPTIMIZERS or ()):
+        ts = [p for g in opt.param_groups for p in g["params"]]
+        for st in opt.state.values():
+            ts.extend(v for v in st.values() if torch.is_tensor(v))
+        extra = getattr(opt, "checkpoint_safe_tensors", None)
+        if extra is not None:
+            ts.extend(extra())
+        for t in ts:
+            t = getattr(t, "_local_tensor", t)
+            if t is None or not t.is_cuda:
+                continue
+            s = t.untyped_storage()
+            if s.nbytes():
+                rng.append((s.data_ptr(), s.data_ptr() + s.nbytes()))
+    rng.sort()
+    merged: List[Tuple[int, int]] = []
+    for a, b in rng:
+        if merged and a <= merged[-1][1]:
+            merged[-1] = (merged[-1][0], max(merged[-1][1], b))
+        else:
+            merged.append((a, b))
+    return merged
+
+
+def _covered(ranges: List[Tuple[int, int]], starts: List[int], a: int, n: int) -> bool:
+    import bisect
+
+    i = bisect.bisect_right(starts, a) - 1
+    return i >= 0 and a + n <= ranges[i][1]
+
+
 def _install_fence_hook():
-    global _FENCED
+    global _FENCED, _OPTIMIZERS
     if _FENCED is None:
         import weakref
 
         from torch.optim.optimizer import register_optimizer_step_pre_hook
 
         _FENCED = weakref.WeakSet()
+        _OPTIMIZERS = weakref.WeakSet()
         register_optimizer_step_pre_hook(_optimizer_step_fence)
 
 
@@ -373,16 +431,30 @@ class GpuCopier:
         if n > 0:
             stg = self._alloc(idx, n)
             base = stg.data_ptr()
-            key = (layout.signature, lo, hi, base, tuple(e.src_ptr for e in layout.extents))
+            overlapped = copy_stream is not cur
+            key = (layout.signature, lo, hi, base, tuple(e.src_ptr for e in layout.extents), overlapped,
+                   len(_OPTIMIZERS) if overlapped else 0)
             descs = self._desc_cache.get(key)
             if descs is None:
                 pieces = [(e.src_ptr + (a - e.offset), base + (a - lo), b - a)
                           for e, a, b in intersect_extents(layout.gpu_extents(), lo, hi)]
-                descs = build_descs(pieces, self.device)
+                if overlapped:
+                    # only storages that just an optimizer step writes may be
+                    # read after this call returns; the rest is copied now
+                    rng = _step_only_ranges()
+                    starts = [a for a, _b in rng]
+                    late = [p for p in pieces if _covered(rng, starts, p[0], p[2])]
+                    now = [p for p in pieces if not _covered(rng, starts, p[0], p[2])]
+                    descs = (build_descs(now, self.device), build_descs(late, self.device))
+                else:
+                    descs = (build_descs(pieces, self.device), None)
                 if len(self._desc_cache) >= 4:  # one entry per staging buffer (+ slack)
                     self._desc_cache.pop(next(iter(self._desc_cache)))
                 self._desc_cache[key] = descs
-            launch_multi_copy(descs, copy_stream)
+            launch_multi_copy(descs[0], cur)
+            if descs[1] is not None:
+                copy_stream.wait_stream(cur)  # the "now" part is ordered before the flush too
+                launch_multi_copy(descs[1], copy_stream)
             # CPU tensors go straight to shm (small: counters, rng state...)
             for e, a, b in intersect_extents(layout.cpu_extents(), lo, hi):
                 runtime().dw_memcpy_parallel(ctypes.c_void_p(shm_payload_addr + a),

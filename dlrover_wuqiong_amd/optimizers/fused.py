@@ -86,6 +86,11 @@ class _FlatOptimizer(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = False):
         self.flat.zero_grad()
 
+    def checkpoint_safe_tensors(self):
+        """Tensors only ``step()`` writes (an overlapped flash-checkpoint
+        snapshot may still be reading them after the save call returns)."""
+        return [t for t in (self.flat.data, self.exp_avg, self.exp_avg_sq, self.master) if t is not None]
+
     # -------------------------------------------------------- state dict
     def state_dict(self):
         # The per-parameter views never change: build them once.  All params

@@ -70,6 +70,11 @@ class WeightedSAM(torch.optim.Optimizer):
 
     @torch.no_grad()
     def first_step(self, zero_grad=False):
+        # writes the parameters outside step(): order after any overlapped
+        # flash-checkpoint snapshot still reading them
+        from ..flash_checkpoint.copier import fence_all
+
+        fence_all()
         gnorm = self._grad_norm()
         for group in self.param_groups:
             ps = self._params(group)

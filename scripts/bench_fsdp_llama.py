@@ -29,6 +29,11 @@ def main():
     p.add_argument("--steps", type=int, default=8)
     p.add_argument("--ckpt-interval", type=int, default=4)
     p.add_argument("--ckpt-dir", default="/tmp/dwamd_fsdp_ckpt")
+    p.add_argument("--precision", choices=["amp", "half"], default="amp",
+                   help="amp: fp32 sharded params, FSDP2 casts to bf16 per gather; half: bf16 params + fp32 "
+                        "masters inside the fused optimizer")
+    p.add_argument("--torch-optim", action="store_true", help="keep torch.optim.AdamW (no multi-tensor HIP kernel)")
+    p.add_argument("--no-ckpt", action="store_true", help="step time only (no flash checkpoints)")
     a = p.parse_args()
     for k, v in dict(MASTER_ADDR="127.0.0.1", MASTER_PORT="29571", RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
                      LOCAL_WORLD_SIZE="1").items():
@@ -53,10 +58,12 @@ def main():
     torch.manual_seed(0)
     with torch.device(dev):
         model = Llama(cfg)
+    prec = ("amp_native", {"dtype": torch.bfloat16}) if a.precision == "amp" else "half"
     ok, res, strategy = auto_accelerate(
         model, torch.optim.AdamW, optim_args={"lr": 2e-5, "betas": (0.9, 0.95), "weight_decay": 0.1},
-        load_strategy=["module_replace", ("amp_native", {"dtype": torch.bfloat16}),
-                       ("fsdp", {"wrap_cls": (LlamaDecoderLayer,)}), ("checkpoint", {"wrap_cls": (LlamaDecoderLayer,)})])
+        load_strategy=["module_replace", prec,
+                       ("fsdp", {"wrap_cls": (LlamaDecoderLayer,)}), ("checkpoint", {"wrap_cls": (LlamaDecoderLayer,)})],
+        fused_optimizer=not a.torch_optim)
     assert ok, "auto_accelerate failed"
     model, opt = res.model, res.optim
     g = torch.Generator().manual_seed(rank)
@@ -82,6 +89,23 @@ def main():
         step(i)
         print(f"warm-up step {i} done", file=sys.stderr, flush=True)
     sync()
+    if a.no_ckpt:
+        steps, losses = [], []
+        for i in range(a.steps):
+            t0 = time.perf_counter()
+            losses.append(float(step(i).item()))
+            sync()
+            steps.append(time.perf_counter() - t0)
+        med = sorted(steps)[len(steps) // 2]
+        if rank == 0:
+            print(json.dumps({"metric": "fsdp train step", "n_gpus": world, "model": a.model, "seq_len": a.seq,
+                              "precision": a.precision, "optimizer": type(opt).__name__,
+                              "train_step_ms": round(1000 * med, 1),
+                              "tokens_per_s": round(world * a.micro_batch * a.seq / med, 1),
+                              "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if cuda else None,
+                              "step_ms": [round(1000 * x, 1) for x in steps], "losses": [round(x, 3) for x in losses]}))
+        dist.destroy_process_group()
+        return
     ts = time.perf_counter()
     ck.save_checkpoint(0, model, opt, storage_type=StorageType.MEMORY)  # segment setup, untimed
     sync()
@@ -134,7 +158,8 @@ def main():
     if rank == 0:
         print(json.dumps({
             "metric": "fsdp flash ckpt pause s", "value": round(sum(pauses) / len(pauses), 4), "unit": "s",
-            "higher_is_better": False, "n_gpus": world, "dtype": "bf16 autocast, fp32 params + AdamW",
+            "higher_is_better": False, "n_gpus": world, "dtype": ("bf16 autocast, fp32 params" if a.precision == "amp" else "bf16 params, fp32 masters"),
+            "optimizer": type(opt).__name__,
             "data": "synthetic tokens, random-init weights",
             "config": {"model": a.model, "seq_len": a.seq, "micro_batch": a.micro_batch,
                        "strategy": str(strategy)[:300]},
