@@ -70,7 +70,7 @@ SIGS = {
     "dw_add_norm_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, f32, i32, vp]),
     "dw_swiglu_fwd": (i32, [vp, vp, i64, i32, vp]),
     "dw_swiglu_bwd": (i32, [vp, vp, vp, i64, i32, vp]),
-    "dw_rope": (i32, [vp, vp, vp, vp, i64, i32, i32, i32, i32, vp, vp]),
+    "dw_rope": (i32, [vp, vp, vp, vp, i64, i32, i32, i32, i32, vp, i32, vp]),
     # xent.hip
     "dw_xent_fwd": (i32, [vp, vp, vp, vp, vp, vp, i64, i32, i64, i64, f32, vp]),
     "dw_xent_bwd": (i32, [vp, vp, vp, vp, i32, vp, i64, i32, i64, i64, f32, vp]),

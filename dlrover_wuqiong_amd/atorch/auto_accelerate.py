@@ -326,20 +326,22 @@ def _apply_fsdp(ctx, cfg, reshard=True):
         mesh = DeviceMesh("cuda" if torch.cuda.is_available() else "cpu", ranks, mesh_dim_names=("data",))
     model = ctx["model"]
     n = 0
-    done = set()
-    for m in list(model.modules()):
-        if not classes or id(m) in done:
+    # activation checkpointing runs first: shard the CheckpointWrapper, not
+    # the layer inside it.  FSDP(CheckpointWrapper(layer)) casts the layer
+    # inputs to param_dtype once, before the checkpointed region; the
+    # inverted nesting recomputes on uncast fp32 inputs (FSDP2 skips its
+    # input cast in the pre-backward recompute) and the recomputed saved
+    # tensors no longer match the forward ones.
+    ckpt_inner = {id(m._checkpoint_wrapped_module) for m in model.modules()
+                  if getattr(m, "_checkpoint_wrapped_module", None) is not None}
+    # bottom-up (children before parents, as fully_shard requires): nested
+    # wrap classes, e.g. (DecoderLayer, MLP), each become their own FSDP unit
+    for m in reversed(list(model.modules())):
+        if not classes or m is model or id(m) in ckpt_inner:
             continue
-        # activation checkpointing runs first: shard the CheckpointWrapper, not
-        # the layer inside it.  FSDP(CheckpointWrapper(layer)) casts the layer
-        # inputs to param_dtype once, before the checkpointed region; the
-        # inverted nesting recomputes on uncast fp32 inputs (FSDP2 skips its
-        # input cast in the pre-backward recompute) and the recomputed saved
-        # tensors no longer match the forward ones.
         inner = getattr(m, "_checkpoint_wrapped_module", None)
         if isinstance(m, classes) or (inner is not None and isinstance(inner, classes)):
             fully_shard(m, mesh=mesh, mp_policy=mp, reshard_after_forward=reshard)
-            done.update(id(x) for x in m.modules())
             n += 1
     fully_shard(model, mesh=mesh, mp_policy=mp, reshard_after_forward=reshard)
     ctx["fsdp"] = True

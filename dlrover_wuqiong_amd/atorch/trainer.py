@@ -51,6 +51,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..common.log import logger
+from ..common.serialize import safe_torch_load
 
 try:
     from transformers import TrainingArguments
@@ -545,7 +546,7 @@ class AtorchTrainer:
             self.state.global_step = int(extra.get("global_step", 0))
         rng = os.path.join(ckpt_dir, f"rng_state_{self._rank()}.pth")
         if os.path.exists(rng):
-            self._set_rng_state(torch.load(rng, weights_only=False))  # our own file (numpy RNG tuple)
+            self._set_rng_state(safe_torch_load(rng))  # numpy RNG tuple: allow-listed unpickler
         logger.info(f"resumed from {ckpt_dir} at step {self.state.global_step}")
 
     def save_model(self, output_dir: Optional[str] = None):

@@ -56,7 +56,14 @@ def find_free_port(port: int = 0) -> int:
 
 
 def find_free_port_in_range(start: int, end: int) -> int:
-    for p in range(start, end):
+    # scan from a random offset: concurrent jobs probing in the same order
+    # would all pick the first free port (probe-then-bind race)
+    import random
+
+    n = end - start
+    off = random.SystemRandom().randrange(n) if n > 0 else 0
+    for i in range(n):
+        p = start + (off + i) % n
         try:
             return find_free_port(p)
         except OSError:

@@ -176,7 +176,7 @@ extern "C" int dw_swiglu_bwd(const void* dy, const void* x, void* dx, int64_t R,
 __global__ void __launch_bounds__(256) rope_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                    const float* __restrict__ cosb, const float* __restrict__ sinb,
                                                    int64_t BS, int S, int NH, int D, float sign,
-                                                   const int* __restrict__ pos_ids) {
+                                                   const int* __restrict__ pos_ids, int rows) {
   const int half = D >> 1;
   const int hv = half >> 3;  // 8-wide vectors per half
   const int64_t total = BS * NH * hv;
@@ -185,7 +185,8 @@ __global__ void __launch_bounds__(256) rope_kernel(const bf16_t* __restrict__ x,
     const int v = (int)(t % hv);
     const int64_t rh = t / hv;  // (b*S + s)*NH + h
     const int64_t bs = rh / NH;
-    const int s = pos_ids ? pos_ids[bs] : (int)(bs % S);
+    // positions outside the table clamp to its range (never read past it)
+    const int s = pos_ids ? min(max(pos_ids[bs], 0), rows - 1) : (int)(bs % S);
     const bf16_t* xr = x + rh * D;
     bf16_t* yr = y + rh * D;
     float a[8], b[8], o1[8], o2[8];
@@ -204,11 +205,11 @@ __global__ void __launch_bounds__(256) rope_kernel(const bf16_t* __restrict__ x,
   }
 }
 extern "C" int dw_rope(const void* x, void* y, const void* cosb, const void* sinb, int64_t B, int S,
-                       int NH, int D, int backward, const void* pos_ids, void* stream) {
-  if (D % 16) return (int)hipErrorInvalidValue;
+                       int NH, int D, int backward, const void* pos_ids, int rows, void* stream) {
+  if (D % 16 || rows < 1 || (!pos_ids && rows < S)) return (int)hipErrorInvalidValue;
   const int64_t total = B * S * NH * (D / 16);
   hipLaunchKernelGGL(rope_kernel, dim3(dw_grid_for(total, 256, 4096)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)x, (bf16_t*)y, (const float*)cosb, (const float*)sinb, B * S, S, NH, D,
-                     backward ? -1.f : 1.f, (const int*)pos_ids);
+                     backward ? -1.f : 1.f, (const int*)pos_ids, rows);
   DW_LAUNCH_RET;
 }

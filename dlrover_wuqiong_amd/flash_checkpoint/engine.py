@@ -172,6 +172,7 @@ class CheckpointEngine(ABC):
         self._gc_frozen = False
         self._generation = 0
         self._shm_prep = None  # Future: background prefault + pin of this rank's slot slices
+        self._shm_handler.before_unmap = self._quiesce_shm_users
         self._prep_pool = None
         self._prepped_for = None
         self._last_save_blocking = 0.0
@@ -292,6 +293,18 @@ class CheckpointEngine(ABC):
             # make sure every slot this rank writes is pinned before its flush
             self._prepped_for = key
             self._start_shm_prep(total, prefault=need_resize)
+
+    def _quiesce_shm_users(self):
+        """Before this process unmaps its segment (resize, a stale mapping
+        replaced by a writer, close): the prep thread and in-flight flushes
+        write into it, and pinned registrations must not outlive it."""
+        if self._shm_prep is not None:
+            self._shm_prep.result()
+            self._shm_prep = None
+            self._prepped_for = None
+        if self._copier is not None:
+            self._copier.wait()
+            self._copier.pinned.release_all()
 
     def _start_shm_prep(self, total: int, prefault: bool):
         copier = self._device_copier()

@@ -39,6 +39,7 @@ import torch.distributed as dist
 
 from ..common.constants import CheckpointConstant
 from ..common.log import logger
+from ..common.serialize import restricted_loads, safe_torch_load
 from ..common.storage import CheckpointStorage, PosixDiskStorage, get_checkpoint_storage
 from .checkpointer import Checkpointer, StorageType
 from .engine import FullCheckpointEngine, ShardCheckpointEngine, check_all_rank_ready
@@ -119,6 +120,7 @@ def build_dcp_payload(planner, plan: _DcpPlan, rank: int) -> Dict[str, Any]:
     _, _, WriteItemType = _dcp()
     tensors: Dict[str, Any] = {}
     index = []
+    views: Dict[str, torch.Tensor] = {}
     for n, it in enumerate(plan.items):
         data = planner.resolve_data(it)
         key = str(n)
@@ -126,10 +128,24 @@ def build_dcp_payload(planner, plan: _DcpPlan, rank: int) -> Dict[str, Any]:
             tensors[key] = bytes(data.getbuffer())
         else:
             t = data.detach()
-            tensors[key] = t if t.is_contiguous() else t.contiguous()
+            if t.is_contiguous():
+                tensors[key] = t
+            else:
+                # snapshot from a contiguous copy; a restore lands in the copy
+                # and is written back through the live view (restore_views)
+                tensors[key] = t.contiguous()
+                views[key] = t
         off = list(it.index.offset) if it.index.offset is not None else None
         index.append([it.index.fqn, off, it.index.index, int(it.type.value), bool(plan.persist[n])])
-    return {"items": tensors, "index": index, "rank": rank, "metadata": plan.metadata_bytes}
+    return {"items": tensors, "index": index, "rank": rank, "metadata": plan.metadata_bytes, "_views": views}
+
+
+def restore_views(payload: Dict[str, Any], views: Dict[str, torch.Tensor]):
+    """Copy restored contiguous stand-ins back into their non-contiguous live
+    tensors (``views`` = the ``_views`` entry popped off the payload)."""
+    with torch.no_grad():
+        for key, live in views.items():
+            live.copy_(payload["items"][key])
 
 
 # ---------------------------------------------------------------- persisting
@@ -189,7 +205,7 @@ def finalize_dcp_checkpoint(storage: CheckpointStorage, path: str, world_size: i
     if len(names) < world_size:
         logger.error(f"DCP storage index incomplete: {len(names)}/{world_size} ranks")
         return False
-    md = pickle.loads(storage.read(os.path.join(parts, META_PART), mode="rb"))  # written by rank 0 of this job
+    md = restricted_loads(storage.read(os.path.join(parts, META_PART), mode="rb"))  # rank 0 of this job
     storage_data = {}
     for name in names:
         for fqn, off, idx, rel, start, length in json.loads(storage.read(os.path.join(parts, name))):
@@ -222,6 +238,7 @@ class FsdpCheckpointEngine(ShardCheckpointEngine):
 
     def save_to_memory(self, step, state_dict, paths):
         _, _, payload = self._payload(state_dict)
+        payload.pop("_views", None)
         return super().save_to_memory(step, {DCP_KEY: payload}, paths)
 
     def save_to_storage(self, step, state_dict, paths):
@@ -247,6 +264,7 @@ class FsdpCheckpointEngine(ShardCheckpointEngine):
         from torch.distributed.checkpoint._traverse import set_element
 
         planner, plan, payload = self._payload(state_dict)
+        views = payload.pop("_views", {})
         # same tree as the saved one -> tensors restored in place into the live shards
         step, sd = self.get_state_dict_from_memory(target={DCP_KEY: payload})
         if step <= 0 or not sd:
@@ -259,16 +277,14 @@ class FsdpCheckpointEngine(ShardCheckpointEngine):
         for n, (fqn, _off, _idx, _typ, _p) in enumerate(saved["index"]):
             v = items[str(n)]
             if isinstance(v, (bytes, bytearray)):
-                try:
-                    obj = torch.load(io.BytesIO(v), weights_only=True)
-                except Exception:
-                    obj = torch.load(io.BytesIO(v), weights_only=False)  # our own job's bytes
+                obj = safe_torch_load(io.BytesIO(v))
                 set_element(state_dict, planner.mappings[fqn], obj)
             elif torch.is_tensor(v):
                 dst = payload["items"][str(n)]
                 if v.data_ptr() != dst.data_ptr():
                     with torch.no_grad():
                         dst.copy_(v.view(dst.shape))
+        restore_views(payload, views)
         return step
 
     def _resume_dir(self, resume_path: str) -> str:

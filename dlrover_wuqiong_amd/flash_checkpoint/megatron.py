@@ -35,6 +35,7 @@ import torch.distributed as dist
 from ..common import env_utils
 from ..common.constants import CheckpointConstant
 from ..common.log import logger
+from ..common.serialize import safe_torch_load
 from ..common.storage import get_checkpoint_storage
 from .checkpointer import StorageType
 from .engine import FullCheckpointEngine
@@ -245,10 +246,10 @@ class MegatronCheckpointer:
         out = {}
         path = get_checkpoint_name(self.checkpoint_dir, iteration, ranks=self.engine.ranks)
         if os.path.exists(path):
-            out[CheckpointConstant.MODEL_STATES_NAME] = torch.load(path, map_location="cpu", weights_only=False)
+            out[CheckpointConstant.MODEL_STATES_NAME] = safe_torch_load(path)
         opath = get_dist_optimizer_checkpoint_name(self.checkpoint_dir, iteration)
         if os.path.exists(opath):
-            out[CheckpointConstant.OPTIM_STATES_NAME] = torch.load(opath, map_location="cpu", weights_only=False)
+            out[CheckpointConstant.OPTIM_STATES_NAME] = safe_torch_load(opath)
         return iteration, out
 
     def wait_latest_checkpoint(self):

@@ -26,6 +26,7 @@ import torch.distributed as dist
 
 from ..common import env_utils
 from ..common.log import logger
+from ..common.serialize import restricted_loads
 from ..common.multi_process import SharedMemory
 from .shm_handler import SharedMemoryHandler
 
@@ -128,7 +129,7 @@ class CkptReplicaManager:
                     n, mlen = int(hdr[0]), int(hdr[1])
                     del hdr
                     data = bytes(seg.buf[4096: 4096 + n])
-                    meta = pickle.loads(bytes(seg.buf[4096 + n: 4096 + n + mlen])) if mlen else None
+                    meta = restricted_loads(bytes(seg.buf[4096 + n: 4096 + n + mlen])) if mlen else None
                     seg.close()
                     obj = [(data, meta)]
                 except FileNotFoundError:

@@ -34,7 +34,7 @@ Parity: reference ``SharedMemoryHandler`` (``ckpt_saver.py:209-341``).
 
 import os
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional
+from typing import Any, Callable, Dict, List, Optional
 
 import numpy as np
 
@@ -106,6 +106,7 @@ class SharedMemoryHandler:
         self.shared_memory: Optional[SharedMemory] = None
         self._header: Optional[np.ndarray] = None
         self._need_creation = True
+        self.before_unmap: Optional[Callable[[], None]] = None
 
     # ------------------------------------------------------------------ shm
     @property
@@ -313,6 +314,10 @@ class SharedMemoryHandler:
         self._need_creation = True
 
     def close(self):
+        if self.shared_memory is not None and self.before_unmap is not None:
+            # the owner's background users of this mapping (prefault/pin
+            # thread, in-flight D2H flushes) must finish before it goes away
+            self.before_unmap()
         self._header = None
         if self.shared_memory is not None:
             try:

@@ -48,7 +48,7 @@ class _RopeFn(torch.autograd.Function):
         y = torch.empty_like(x)
         pid = pos_ids.to(torch.int32).contiguous() if pos_ids is not None else None
         _hip.check(_hip.lib().dw_rope(_hip.ptr(x), _hip.ptr(y), _hip.ptr(cos), _hip.ptr(sin), B, S, NH, D, 0,
-                                      _hip.ptr(pid), _hip.stream()), "rope")
+                                      _hip.ptr(pid), cos.shape[0], _hip.stream()), "rope")
         ctx.save_for_backward(cos, sin, pid)
         return y
 
@@ -59,7 +59,7 @@ class _RopeFn(torch.autograd.Function):
         B, S, NH, D = dy.shape
         dx = torch.empty_like(dy)
         _hip.check(_hip.lib().dw_rope(_hip.ptr(dy), _hip.ptr(dx), _hip.ptr(cos), _hip.ptr(sin), B, S, NH, D, 1,
-                                      _hip.ptr(pid), _hip.stream()), "rope_bwd")
+                                      _hip.ptr(pid), cos.shape[0], _hip.stream()), "rope_bwd")
         return dx, None, None, None
 
 
@@ -72,8 +72,13 @@ def _table(t, x, pos_ids):
         raise _hip.HipKernelError(f"rope table shape {tuple(t.shape)} does not match head_dim {D}")
     if pos_ids is None and t.shape[0] < S:
         raise _hip.HipKernelError(f"rope table has {t.shape[0]} rows < seq_len {S}")
-    if pos_ids is not None and pos_ids.numel() != B * S:
-        raise _hip.HipKernelError(f"rope pos_ids has {pos_ids.numel()} entries, expected {B * S}")
+    if pos_ids is not None:
+        if pos_ids.numel() != B * S:
+            raise _hip.HipKernelError(f"rope pos_ids has {pos_ids.numel()} entries, expected {B * S}")
+        if pos_ids.device != x.device or pos_ids.dtype.is_floating_point or pos_ids.dtype == torch.bool:
+            raise _hip.HipKernelError(f"rope pos_ids must be an integer tensor on {x.device} "
+                                      f"(got {pos_ids.dtype} on {pos_ids.device})")
+        # out-of-table positions are clamped by the kernel (never read past the table)
     if t.dtype != torch.float32 or not t.is_contiguous() or t.device != x.device:
         t = t.to(device=x.device, dtype=torch.float32).contiguous()
     return t

@@ -174,6 +174,20 @@ def _llama_fsdp_ckpt_worker(rank, world, port, q):
             res.optim.step()
             res.optim.zero_grad(set_to_none=True)
             losses.append(float(loss))
+        # nested wrap classes: every DecoderLayer AND every MLP inside it is its own FSDP unit
+        from dlrover_wuqiong_amd.models.llama import LlamaMLP
+
+        torch.manual_seed(0)
+        m2 = Llama(LlamaConfig.named("llama-tiny"))
+        ok2, res2, _ = auto_accelerate(m2, torch.optim.AdamW, optim_args={"lr": 1e-3},
+                                       load_strategy=[("fsdp", {"wrap_cls": (LlamaDecoderLayer, LlamaMLP)})])
+        units = [m for m in res2.model.modules() if isinstance(m, FSDPModule)]
+        nlayers = LlamaConfig.named("llama-tiny").num_hidden_layers
+        nested_ok = nested_ok and ok2 and sum(isinstance(m, LlamaMLP) for m in units) == nlayers and \
+            sum(isinstance(m, LlamaDecoderLayer) for m in units) == nlayers
+        loss = res2.model(ids[:, :-1], ids[:, 1:])
+        loss.backward()
+        res2.optim.step()
         q.put((rank, bool(ok and nested_ok and all(x == x for x in losses))))
     except Exception as e:  # pragma: no cover
         import traceback

@@ -18,7 +18,7 @@ def test_bench_two_ranks_real_kill(tmp_path):
            "240"]
     r = subprocess.run(cmd, env=env, cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                        timeout=300)
-    assert r.returncode == 0, r.stderr[-4000:]
+    assert r.returncode == 0, r.stderr[-20000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     res = json.loads(lines[0])

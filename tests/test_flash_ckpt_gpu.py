@@ -99,6 +99,44 @@ def test_gpu_overlapped_snapshot_is_fenced_by_the_optimizer(tmp_path, monkeypatc
     ck.close()
 
 
+def test_gpu_overlapped_snapshot_copies_forward_written_buffers_first(tmp_path, monkeypatch):
+    """BatchNorm running stats are written by the next forward, not by the
+    optimizer: the overlapped snapshot must copy them before save returns
+    (only optimizer-step-only storages are left to the side stream)."""
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+
+    monkeypatch.setenv("DWAMD_OVERLAP_SNAPSHOT", "1")
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.BatchNorm1d(256), torch.nn.Linear(256, 8)).cuda()
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+
+    def train():
+        model(torch.randn(512, 64, device="cuda")).pow(2).mean().backward()
+        opt.step()
+        opt.zero_grad()
+
+    train()
+    ck = DdpCheckpointer(str(tmp_path / "ck"))
+    state = lambda: {"model": model.state_dict(), "opt": opt.state_dict()}  # noqa
+    torch.cuda.synchronize()
+    want = {k: v.clone() for k, v in model.state_dict().items()}
+    assert ck.save_checkpoint(1, state(), storage_type=StorageType.MEMORY)
+    cp = ck.engine._copier
+    now, late = next(iter(cp._desc_cache.values()))
+    assert late is not None and now.shape[0] > 0 and late.shape[0] > 0  # buffers now, params/moments late
+    for _ in range(3):  # forwards right away: running stats change
+        model(torch.randn(512, 64, device="cuda") * 5)
+    ck.wait_latest_checkpoint()
+    torch.cuda.synchronize()
+    assert not torch.equal(model[1].running_mean, want["1.running_mean"])
+    ck.load_checkpoint(target=state())
+    torch.cuda.synchronize()
+    for k, v in model.state_dict().items():
+        assert torch.equal(v, want[k]), k
+    ck.close()
+
+
 def test_gpu_save_to_disk_is_torch_loadable(tmp_path):
     import time
 

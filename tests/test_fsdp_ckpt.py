@@ -46,16 +46,19 @@ def _fsdp_worker(rank, world, port, root, q):
         opt = torch.optim.AdamW(model.parameters(), lr=1e-2)
         _train(model, opt, 1)
         ck = FsdpShardCheckpointer(root)
-        assert ck.save_checkpoint(2, model, opt, {"epoch": 7}, storage_type=StorageType.MEMORY)
+        proj = torch.arange(12.0).view(3, 4)  # saved through a non-contiguous view
+        assert ck.save_checkpoint(2, model, opt, {"epoch": 7, "proj": proj.t()}, storage_type=StorageType.MEMORY)
         ck.wait_latest_checkpoint()
         want = _local(model)
         want_m = {k: v.to_local().clone() for k, v in opt.state_dict()["state"][0].items()
                   if torch.is_tensor(v) and hasattr(v, "to_local")}
         _train(model, opt, 2)
         _train(model, opt, 3)
-        extra = ck.load_checkpoint(model, opt, extra_sd={"epoch": 0})
+        proj.zero_()
+        extra = ck.load_checkpoint(model, opt, extra_sd={"epoch": 0, "proj": proj.t()})
         got = _local(model)
         ok = extra.get("epoch") == 7 and extra.get("step") == 2
+        ok = ok and torch.equal(proj, torch.arange(12.0).view(3, 4))  # restored through the live view
         ok = ok and all(torch.equal(got[k], want[k]) for k in want)
         st = opt.state_dict()["state"][0]
         ok = ok and all(torch.equal(st[k].to_local(), v) for k, v in want_m.items())

@@ -148,6 +148,29 @@ def test_rope_bf16_table_and_bad_shape():
         apply_rope(x, cos[: S // 2], sin[: S // 2])
 
 
+def test_rope_pos_ids_validated_and_clamped():
+    """pos_ids must be an integer tensor on the GPU; positions past the table
+    clamp to its last row inside the kernel (never read past the table)."""
+    from dlrover_wuqiong_amd.ops._hip import HipKernelError
+    from dlrover_wuqiong_amd.ops.rope import _rope_ref, apply_rope, rope_table
+
+    B, S, NH, D = 2, 64, 4, 64
+    cos, sin = rope_table(S, D, device=DEV)
+    x = torch.randn(B, S, NH, D, device=DEV, dtype=torch.bfloat16)
+    pos = torch.randint(0, S, (B, S), device=DEV)
+    assert _rel(apply_rope(x, cos, sin, pos), _rope_ref(x.float(), cos, sin, pos_ids=pos)) < 1e-2
+    with pytest.raises(HipKernelError):
+        apply_rope(x, cos, sin, pos.cpu())
+    with pytest.raises(HipKernelError):
+        apply_rope(x, cos, sin, pos.float())
+    far = pos.clone()
+    far[0, 0] = 10 * S
+    y = apply_rope(x, cos, sin, far)
+    torch.cuda.synchronize()
+    far[0, 0] = S - 1
+    assert _rel(y, _rope_ref(x.float(), cos, sin, pos_ids=far)) < 1e-2
+
+
 @pytest.mark.parametrize("V", [50304, 1000])
 def test_cross_entropy(V):
     from dlrover_wuqiong_amd.ops.cross_entropy import cross_entropy
