@@ -251,14 +251,15 @@ class CheckpointDeletionStrategy(ABC):
 class KeepStepIntervalStrategy(CheckpointDeletionStrategy):
     """Keep only steps that are multiples of ``keep_interval``."""
 
-    def __init__(self, keep_interval: int, checkpoint_dir: str):
+    def __init__(self, keep_interval: int, checkpoint_dir: str, dir_format: str = "{}"):
         self._keep_interval = keep_interval
         self._checkpoint_dir = checkpoint_dir
+        self._dir_format = dir_format  # step -> directory name (Megatron: "iter_{:07d}")
 
     def clean_up(self, step, delete_func):
         if self._keep_interval > 0 and step % self._keep_interval == 0:
             return
-        target = os.path.join(self._checkpoint_dir, str(step))
+        target = os.path.join(self._checkpoint_dir, self._dir_format.format(step))
         try:
             delete_func(target)
         except Exception:
@@ -268,16 +269,17 @@ class KeepStepIntervalStrategy(CheckpointDeletionStrategy):
 class KeepLatestStepStrategy(CheckpointDeletionStrategy):
     """Keep the newest ``max_to_keep`` steps."""
 
-    def __init__(self, max_to_keep: int, checkpoint_dir: str):
+    def __init__(self, max_to_keep: int, checkpoint_dir: str, dir_format: str = "{}"):
         self._max_to_keep = max(1, max_to_keep)
         self._checkpoint_dir = checkpoint_dir
+        self._dir_format = dir_format
         self._steps: List[int] = []
 
     def clean_up(self, step, delete_func):
         self._steps.append(step)
         while len(self._steps) >= self._max_to_keep:
             old = self._steps.pop(0)
-            target = os.path.join(self._checkpoint_dir, str(old))
+            target = os.path.join(self._checkpoint_dir, self._dir_format.format(old))
             try:
                 delete_func(target)
             except Exception:

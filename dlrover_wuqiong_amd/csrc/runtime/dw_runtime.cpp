@@ -121,7 +121,9 @@ int dw_shm_unlink(const char* name) {
 // zeroes them now rather than inside a later (timed) copy.
 int dw_prefault(void* p, uint64_t size, int nthreads) {
   if (size == 0) return 0;
-  if (madvise(p, size, MADV_POPULATE_WRITE) == 0 && nthreads <= 1) return 0;
+  // one kernel-side populate is the fastest on tmpfs (parallel populates of
+  // one shmem object contend); touch pages from threads only without it
+  if (madvise(p, size, MADV_POPULATE_WRITE) == 0) return 0;
   nthreads = std::max(1, nthreads);
   const uint64_t page = 4096;
   uint64_t per = ((size / nthreads) + page - 1) / page * page;

@@ -309,6 +309,20 @@ class GpuCopier:
         self.overlap = os.environ.get("DWAMD_OVERLAP_SNAPSHOT", "0") == "1"
         self._snap_stream: Optional[torch.cuda.Stream] = None
         self._fence_ev: Optional[torch.cuda.Event] = None
+        # Bounded staging ring (``DWAMD_STAGING=ring``, or automatically when
+        # not even one full-size staging buffer fits next to the model): K
+        # chunks of C bytes of HBM instead of 1-2x the shard (_save_slice_ring)
+        self.staging_mode = os.environ.get("DWAMD_STAGING", "auto")  # auto | full | ring
+        self.ring_slots = max(2, int(os.environ.get("DWAMD_RING_SLOTS", "4")))
+        self.ring_chunk = max(1 << 20, int(os.environ.get("DWAMD_RING_CHUNK_MB", "1024")) << 20)
+        self._ring: Optional[torch.Tensor] = None
+        self._ring_free: List[torch.cuda.Event] = []
+        self._ring_decision: Optional[Tuple[int, bool]] = None
+        self._ring_gate: Optional[threading.Event] = None
+        self._ring_last: dict = {}
+        self._now_buf: Optional[torch.Tensor] = None
+        self._ring_cache: dict = {}
+        self.last_snapshot_mode = ""
         _install_fence_hook()
 
     @property
@@ -412,6 +426,9 @@ class GpuCopier:
         ``before_copy(staging_idx)`` runs before the snapshot is enqueued
         (HBM-tier stamp invalidation)."""
         n = hi - lo
+        if self._use_ring(n):
+            return self._save_slice_ring(layout, shm_payload_addr, lo, hi, on_done, sync)
+        self.last_snapshot_mode = "full"
         self._refresh_external(n)
         self._decide_buffers(n)
         self.wait_stage()  # this staging buffer's previous flush must have landed
@@ -512,10 +529,190 @@ class GpuCopier:
     def fence(self):
         """Make the current stream wait for a pending overlapped snapshot
         (called before anything may write the checkpointed state)."""
+        gate = self._ring_gate
+        if gate is not None:
+            # the ring's last chunk copy is enqueued by the flush thread
+            gate.wait()
+            self._ring_gate = None
+            ev = self._ring_last.pop("ev", None)
+            if ev is not None:
+                torch.cuda.current_stream(self.device).wait_event(ev)
         ev = self._fence_ev
         if ev is not None:
             torch.cuda.current_stream(self.device).wait_event(ev)
             self._fence_ev = None
+
+    # ------------------------------------------------------- staging ring
+    def _use_ring(self, n: int) -> bool:
+        if n <= 0 or self.staging_mode == "full":
+            return False
+        if self.staging_mode == "ring":
+            return True
+        if self._ring_decision is not None and self._ring_decision[0] == n:
+            return self._ring_decision[1]
+        ring = False
+        if self._ext is None:
+            try:
+                free, _total = torch.cuda.mem_get_info(self.device)
+                have = sum(t.numel() for t in self._stagings if t is not None)
+                ring = free + have < n + self.staging_reserve
+            except Exception:
+                ring = False
+        self._ring_decision = (n, ring)
+        if ring:
+            self.wait()
+            self._stagings = [None, None]  # give full-size buffers back
+            logger.info(f"checkpoint staging: {n / 2**30:.1f} GiB slice does not fit in HBM next to the model; "
+                        f"bounded ring of {self.ring_slots} x {self.ring_chunk >> 20} MiB")
+        return ring
+
+    @property
+    def staging_hbm_bytes(self) -> int:
+        """HBM this copier holds for snapshot staging right now."""
+        b = sum(t.numel() for t in self._stagings if t is not None)
+        if self._ring is not None:
+            b += self._ring.numel()
+        if self._now_buf is not None:
+            b += self._now_buf.numel()
+        return b
+
+    def _save_slice_ring(self, layout: Layout, shm_payload_addr: int, lo: int, hi: int,
+                         on_done: Callable[[], None], sync: bool):
+        """Snapshot through K x C bytes of HBM.
+
+        The slice streams chunk by chunk: a copy stream gathers chunk j from
+        the live tensors into ring slot j % K (after slot j % K's previous
+        D2H has drained, a device-side event wait) and the flush stream DMAs
+        it to pinned shm.  Nothing is copied before this call returns except
+        storages that something other than ``Optimizer.step`` may write
+        (buffers): those go into a small HBM side buffer on the compute
+        stream first.  Parameters and optimizer state are read by the ring
+        while forward/backward run; the next optimizer step is fenced on the
+        last chunk copy (global step pre-hook).  If the non-optimizer part
+        exceeds one chunk (e.g. no optimizer has stepped yet), the call
+        blocks until the ring has drained.  Host-side enqueueing happens on
+        the flush thread (it also waits for the shm registration), so the
+        training thread never waits on PCIe unless it reaches the fence."""
+        self.last_snapshot_mode = "ring"
+        n = hi - lo
+        self.wait()  # one ring: the previous pipeline must have drained
+        self.fence()
+        K, C = self.ring_slots, self.ring_chunk
+        C = min(C, max(16, (n + K - 1) // K + 15 & ~15))  # tiny slices: no oversized ring
+        if self._ring is None or self._ring.numel() < K * C:
+            self._ring = None
+            self._ring = torch.empty(K * C, dtype=torch.uint8, device=self.device)
+            self._ring_free = [torch.cuda.Event() for _ in range(K)]
+            self._ring_cache.clear()
+        if self._snap_stream is None:
+            self._snap_stream = torch.cuda.Stream(device=self.device)
+        cur = torch.cuda.current_stream(self.device)
+        cstream = self._snap_stream
+        ring_base = self._ring.data_ptr()
+
+        gpu = [(e.src_ptr + (a - e.offset), a - lo, b - a) for e, a, b in intersect_extents(layout.gpu_extents(), lo, hi)]
+        rng = _step_only_ranges()
+        starts = [a for a, _b in rng]
+        now = [p for p in gpu if not _covered(rng, starts, p[0], p[2])]
+        now_bytes = sum(p[2] for p in now)
+        blocking = sync or now_bytes > C
+        if not blocking and now:
+            if self._now_buf is None or self._now_buf.numel() < now_bytes:
+                self._now_buf = torch.empty(max(now_bytes, 1 << 20), dtype=torch.uint8, device=self.device)
+        nb = self._now_buf.data_ptr() if (self._now_buf is not None and not blocking and now) else 0
+        key = (layout.signature, lo, hi, tuple(e.src_ptr for e in layout.extents), ring_base, C, nb, blocking,
+               len(_OPTIMIZERS or ()))
+        plan = self._ring_cache.get(key)
+        if plan is None:
+            now_set = set(now)
+            srcs, now_descs, k = [], [], 0
+            for p in gpu:
+                if nb and p in now_set:
+                    now_descs.append((p[0], nb + k, p[2]))
+                    srcs.append((nb + k, p[1], p[2]))
+                    k += p[2]
+                else:
+                    srcs.append(p)
+            srcs.sort(key=lambda x: x[1])
+            rows, bounds = [], []
+            nchunks = (n + C - 1) // C
+            i = 0
+            for j in range(nchunks):
+                c0, c1 = j * C, min(n, (j + 1) * C)
+                r0 = len(rows)
+                while i < len(srcs) and srcs[i][1] + srcs[i][2] <= c0:
+                    i += 1
+                t = i
+                while t < len(srcs) and srcs[t][1] < c1:
+                    s_, off, ln = srcs[t]
+                    a_, b_ = max(off, c0), min(off + ln, c1)
+                    o = a_
+                    while o < b_:  # CHUNK-sized descriptor rows
+                        c = min(CHUNK, b_ - o)
+                        rows.append((s_ + (o - off), ring_base + (j % K) * C + (o - c0), c))
+                        o += c
+                    t += 1
+                bounds.append((r0, len(rows), c0, c1))
+            descs = (torch.from_numpy(np.asarray(rows, dtype=np.uint64).view(np.int64)).to(self.device)
+                     if rows else torch.empty(0, 3, dtype=torch.int64, device=self.device))
+            plan = (descs, bounds, build_descs(now_descs, self.device) if now_descs else None)
+            if len(self._ring_cache) >= 4:
+                self._ring_cache.pop(next(iter(self._ring_cache)))
+            self._ring_cache[key] = plan
+        descs, bounds, now_d = plan
+        if now_d is not None:
+            launch_multi_copy(now_d, cur)  # forward-written storages: copied before returning
+        for e, a, b in intersect_extents(layout.cpu_extents(), lo, hi):
+            runtime().dw_memcpy_parallel(ctypes.c_void_p(shm_payload_addr + a),
+                                         ctypes.c_void_p(e.src_ptr + (a - e.offset)), b - a, 4)
+        ev_start = torch.cuda.Event()
+        ev_start.record(cur)
+        prep = self.pending_prep
+        gate = threading.Event()
+        holder = self._ring_last
+        holder.pop("ev", None)
+        free = self._ring_free
+        t_enq = time.perf_counter()
+
+        def flush():
+            try:
+                if prep is not None:
+                    prep.result()
+                pinned = self.pinned.ensure(shm_payload_addr + lo, n)
+                sp = ctypes.c_void_p(self.side_stream.cuda_stream)
+                t0 = time.perf_counter()
+                cstream.wait_event(ev_start)
+                for j, (r0, r1, c0, c1) in enumerate(bounds):
+                    if j >= K:
+                        cstream.wait_event(free[j % K])  # slot's previous D2H has landed
+                    launch_multi_copy(descs[r0:r1], cstream)
+                    ready = torch.cuda.Event()
+                    ready.record(cstream)
+                    self.side_stream.wait_event(ready)
+                    dst = shm_payload_addr + lo + c0
+                    src = ring_base + (j % K) * C
+                    for a_, c_, p_ in (self.pinned.split(dst, c1 - c0) if pinned else [(dst, c1 - c0, False)]):
+                        _check(_kern().dw_memcpy_async(ctypes.c_void_p(a_), ctypes.c_void_p(src + (a_ - dst)), c_,
+                                                       1 if p_ else 3, sp), "ring D2H")
+                    free[j % K].record(self.side_stream)
+                last = torch.cuda.Event()
+                last.record(cstream)
+                holder["ev"] = last
+            finally:
+                gate.set()
+            _check(_kern().dw_stream_sync(ctypes.c_void_p(self.side_stream.cuda_stream)), "ring flush sync")
+            t1 = time.perf_counter()
+            self.flush_stats.append((n, t1 - t0))
+            self.flush_log.append((t_enq, t0, t1, n))
+            on_done()
+
+        self._ring_gate = gate
+        _FENCED.add(self)
+        self._futures[0] = self._executor.submit(flush)
+        if blocking:
+            self._futures[0].result()
+            self._futures[0] = None
+            self.fence()
 
     # ----------------------------------------------------------------- load
     def restore(self, pieces_gpu: List[Tuple[int, int, int]], shm_payload_addr: int, payload_bytes: int,
@@ -591,6 +788,8 @@ class GpuCopier:
             self._executor.shutdown(wait=True)
             self.pinned.release_all()
             self._stagings = [None, None]
+            self._ring = None
+            self._now_buf = None
             for b in self._ext or []:
                 b.release()
             self._ext = None

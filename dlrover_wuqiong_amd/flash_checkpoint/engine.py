@@ -25,6 +25,7 @@ import os
 import threading
 import time
 from abc import ABC, abstractmethod
+from concurrent.futures import Future
 from datetime import timedelta
 from typing import Any, Dict, List, Optional
 
@@ -43,6 +44,7 @@ from .shm_handler import (DLROVER_CKPT_CONFIG_KEY, EVENT_QUEUE_SIZE, CheckpointC
 
 
 _TIMING = os.environ.get("DWAMD_CKPT_TIMING", "0") == "1"  # log per-phase save times
+_PREP_PIECE = max(64, int(os.environ.get("DWAMD_PREP_PIECE_MB", "1024"))) << 20  # shm prefault/pin granularity
 
 
 class CheckpointEventType:
@@ -173,6 +175,11 @@ class CheckpointEngine(ABC):
         self._generation = 0
         self._shm_prep = None  # Future: background prefault + pin of this rank's slot slices
         self._shm_handler.before_unmap = self._quiesce_shm_users
+        # learn which optimizers exist from their first step on (an
+        # overlapped / ring snapshot only defers copying step-only storages)
+        from .copier import _install_fence_hook
+
+        _install_fence_hook()
         self._prep_pool = None
         self._prepped_for = None
         self._last_save_blocking = 0.0
@@ -312,7 +319,13 @@ class CheckpointEngine(ABC):
         if total <= 0 or h.shared_memory is None:
             return
         lo, hi = split_ranges(total, self._num_slices)[self._slice_idx]
-        ranges = [(h.payload_addr(slot) + lo, hi - lo) for slot in range(h.num_slots)]
+        # the slot the next save writes first: its flush waits only for that
+        # slot's prefault + registration, not for the whole segment's
+        first = self._next_slot if self._next_slot is not None else h.write_slot()
+        order = [first] + [s for s in range(h.num_slots) if s != first]
+        ranges = [(h.payload_addr(slot) + lo, hi - lo) for slot in order]
+        first_done: Future = Future()
+        piece = _PREP_PIECE
 
         def prep():
             import ctypes
@@ -320,16 +333,27 @@ class CheckpointEngine(ABC):
             from .._native import runtime
 
             t0 = time.perf_counter()
-            for addr, n in ranges:
-                if prefault and n > 0:
-                    # a fresh segment: populate with parallel threads (faster
-                    # than the single-threaded faulting inside hipHostRegister)
-                    runtime().dw_prefault(ctypes.c_void_p(addr), n, 8)
-                if copier is not None:
-                    copier.pinned.ensure(addr, n)
+            try:
+                for i, (addr, n) in enumerate(ranges):
+                    # piecewise: populating / registering tens of GB in one
+                    # call holds this process's mm lock for seconds, and every
+                    # HIP allocation of the training thread queues behind it
+                    for o in range(0, n, piece):
+                        c = min(piece, n - o)
+                        if prefault:
+                            runtime().dw_prefault(ctypes.c_void_p(addr + o), c, 1)
+                        if copier is not None:
+                            copier.pinned.ensure(addr + o, c)
+                        time.sleep(0.001)  # let a waiting mm writer in
+                    if i == 0:
+                        first_done.set_result(time.perf_counter() - t0)
+            finally:
+                if not first_done.done():
+                    first_done.set_result(None)
             if _TIMING:
-                logger.info(f"shm prep ({len(ranges)} slot slices, {hi - lo} B each): "
-                            f"{1000 * (time.perf_counter() - t0):.1f} ms (background)")
+                logger.info(f"shm prep ({len(ranges)} slot slices, {hi - lo} B each): first slot "
+                            f"{1000 * (first_done.result() or 0):.1f} ms, all {1000 * (time.perf_counter() - t0):.1f} ms "
+                            "(background)")
 
         from concurrent.futures import ThreadPoolExecutor
 
@@ -337,7 +361,7 @@ class CheckpointEngine(ABC):
             self._prep_pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="dwamd-shm-prep")
         self._shm_prep = self._prep_pool.submit(prep)
         if copier is not None:
-            copier.pending_prep = self._shm_prep
+            copier.pending_prep = first_done
 
     # ----------------------------------------------------------- core save
     def save_state_dict_to_memory(self, state_dict: Dict, conf: CheckpointConfig) -> bool:

@@ -50,10 +50,11 @@ class LlamaConfig:
     num_experts_per_tok: int = 2
     moe_intermediate_size: int = 0
     activation_checkpointing: bool = False
+    head_dim_override: int = 0     # >0: head_dim != hidden/heads (e.g. one TP rank's shard)
 
     @property
     def head_dim(self) -> int:
-        return self.hidden_size // self.num_attention_heads
+        return self.head_dim_override or self.hidden_size // self.num_attention_heads
 
     @staticmethod
     def named(name: str) -> "LlamaConfig":
@@ -74,6 +75,13 @@ class LlamaConfig:
             "llama3-70b": dict(vocab_size=128256, hidden_size=8192, intermediate_size=28672, num_hidden_layers=80,
                                num_attention_heads=64, num_key_value_heads=8, max_position_embeddings=8192,
                                rope_theta=500000.0),
+            # what ONE rank of Llama-3 70B at TP=8 computes and stores (heads,
+            # FFN and vocab split 8 ways; no TP collectives): checkpoint/HBM
+            # sizing runs on a single GPU
+            "llama3-70b-tp8-shard": dict(vocab_size=128256 // 8, hidden_size=8192, intermediate_size=28672 // 8,
+                                         num_hidden_layers=80, num_attention_heads=64 // 8,
+                                         num_key_value_heads=8 // 8, max_position_embeddings=8192,
+                                         rope_theta=500000.0, head_dim_override=128),
             "mixtral-8x7b": dict(hidden_size=4096, intermediate_size=14336, num_hidden_layers=32,
                                  num_attention_heads=32, num_key_value_heads=8, max_position_embeddings=32768,
                                  rope_theta=1e6, num_experts=8, moe_intermediate_size=14336),
@@ -102,10 +110,11 @@ class LlamaAttention(nn.Module):
             from ..parallel.tensor_parallel import ColumnParallelLinear, RowParallelLinear
 
             self.qkv_proj = ColumnParallelLinear(cfg.hidden_size, qkv_out, bias=False, group=tp_group)
-            self.o_proj = RowParallelLinear(cfg.hidden_size, cfg.hidden_size, bias=False, group=tp_group)
+            self.o_proj = RowParallelLinear(cfg.num_attention_heads * self.hd, cfg.hidden_size, bias=False,
+                                            group=tp_group)
         else:
             self.qkv_proj = nn.Linear(cfg.hidden_size, qkv_out, bias=False)
-            self.o_proj = nn.Linear(cfg.hidden_size, cfg.hidden_size, bias=False)
+            self.o_proj = nn.Linear(cfg.num_attention_heads * self.hd, cfg.hidden_size, bias=False)
 
     def forward(self, x, cos, sin):
         B, S, _ = x.shape

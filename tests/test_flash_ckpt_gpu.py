@@ -137,6 +137,51 @@ def test_gpu_overlapped_snapshot_copies_forward_written_buffers_first(tmp_path, 
     ck.close()
 
 
+@pytest.mark.parametrize("stepped", [True, False])
+def test_gpu_staging_ring_snapshot(tmp_path, monkeypatch, stepped):
+    """DWAMD_STAGING=ring: the slice streams through 4 x 1 MiB of HBM.  The
+    next optimizer step is fenced on the ring; forward-written buffers are
+    copied before save returns; before any optimizer step (nothing known to
+    be step-only) the save blocks until the ring has drained."""
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+
+    monkeypatch.setenv("DWAMD_STAGING", "ring")
+    monkeypatch.setenv("DWAMD_RING_CHUNK_MB", "1")
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(256, 1024), torch.nn.BatchNorm1d(1024),
+                                torch.nn.Linear(1024, 512)).cuda()
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+
+    def train():
+        model(torch.randn(256, 256, device="cuda")).pow(2).mean().backward()
+        opt.step()
+        opt.zero_grad()
+
+    if stepped:
+        train()
+    ck = DdpCheckpointer(str(tmp_path / "ck"))
+    state = lambda: {"model": model.state_dict(), "opt": opt.state_dict()}  # noqa
+    for step in (1, 2, 3):
+        torch.cuda.synchronize()
+        want = {k: v.clone() for k, v in model.state_dict().items()}
+        want_opt = [s["exp_avg"].clone() for s in opt.state.values()]
+        assert ck.save_checkpoint(step, state(), storage_type=StorageType.MEMORY)
+        cp = ck.engine._copier
+        assert cp.last_snapshot_mode == "ring" and cp.staging_hbm_bytes <= 4 * (1 << 20) + (1 << 20) * 2
+        train()  # forward writes BN stats; the step waits for the ring (fence)
+        ck.wait_latest_checkpoint()
+    torch.cuda.synchronize()
+    ck.load_checkpoint(target=state())
+    torch.cuda.synchronize()
+    for k, v in model.state_dict().items():
+        assert torch.equal(v, want[k]), k
+    for s, w in zip(opt.state.values(), want_opt):
+        assert torch.equal(s["exp_avg"], w)
+    assert ck.engine._shm_handler.payload_size > 4 * (1 << 20)  # really more than the ring
+    ck.close()
+
+
 def test_gpu_save_to_disk_is_torch_loadable(tmp_path):
     import time
 
