@@ -5,9 +5,11 @@ MFMA flash-attention kernels.
 ``"dwamd_mfma"`` with transformers' ``AttentionInterface`` and switches the
 model (and every sub-config) to it, so LlamaAttention / MistralAttention /
 Qwen2Attention ... call ``ops.attention.flash_attn_func`` (BSHD, GQA, causal,
-head_dim 64/128) instead of SDPA.  Cases the kernel does not cover -- a
-padding mask, dropout, head_dim not in {64, 128}, non-bf16 or CPU tensors --
-fall back to transformers' own SDPA path for that call.
+head_dim 64/128) instead of SDPA; padded batches (left or right padding)
+run the varlen kernels on the unpadded tokens.  Cases the kernels do not
+cover -- dropout, head_dim not in {64, 128}, sliding windows, KV-cache
+decoding (q_len != k_len), non-bf16 or CPU tensors -- fall back to
+transformers' own SDPA path for that call.
 
 ``auto_accelerate``'s ``module_replace`` applies it to any
 ``PreTrainedModel`` together with the fused norm replacement.
@@ -40,16 +42,27 @@ def dwamd_attention_forward(module, query: torch.Tensor, key: torch.Tensor, valu
     q_len, k_len = query.shape[2], key.shape[2]
     usable = (_hip.use_hip(query) and query.dtype == torch.bfloat16 and D in (64, 128) and dropout == 0.0
               and q_len == k_len and causal and kwargs.get("sliding_window") is None)
+    key_valid = None
     if usable and attention_mask is not None:
-        # a pure causal mask (no padding) is what the kernel implements
-        usable = attention_mask.dim() == 4 and bool((attention_mask[:, :, -1, :] == 0).all()) \
-            if attention_mask.dtype != torch.bool else bool(attention_mask[:, :, -1, :].all())
+        if attention_mask.dim() != 4 or attention_mask.shape[-1] != k_len:
+            usable = False
+        else:
+            # causal + padding: the last query row of the 4-D mask lists the
+            # valid keys (left or right padding); padded batches go through
+            # the varlen kernels (unpad -> packed sequences -> pad)
+            last = attention_mask[:, 0, -1, :]
+            key_valid = last if attention_mask.dtype == torch.bool else (last == 0)
+            if bool(key_valid.all()):
+                key_valid = None  # a pure causal mask: the dense kernel
     if not usable:
         return sdpa_attention_forward(module, query, key, value, attention_mask, dropout=dropout, scaling=scaling,
                                       is_causal=is_causal, **kwargs)
-    o = flash_attn_func(query.transpose(1, 2), key.transpose(1, 2), value.transpose(1, 2), causal=True,
-                        softmax_scale=scaling)
-    return o, None
+    q, k, v = query.transpose(1, 2), key.transpose(1, 2), value.transpose(1, 2)
+    if key_valid is not None:
+        from ..ops.attention import flash_attn_padded_func
+
+        return flash_attn_padded_func(q, k, v, key_valid, causal=True, softmax_scale=scaling), None
+    return flash_attn_func(q, k, v, causal=True, softmax_scale=scaling), None
 
 
 def register() -> str:
@@ -58,6 +71,16 @@ def register() -> str:
         from transformers import AttentionInterface
 
         AttentionInterface.register(NAME, dwamd_attention_forward)
+        try:
+            # without a registered mask builder transformers hands an unknown
+            # implementation no mask at all (padding would be silently lost):
+            # SDPA's boolean 4-D mask (None for a pure causal batch)
+            from transformers import AttentionMaskInterface
+            from transformers.masking_utils import sdpa_mask
+
+            AttentionMaskInterface.register(NAME, sdpa_mask)
+        except ImportError:  # pragma: no cover - older transformers build 4-D masks for any implementation
+            pass
         _registered = True
     return NAME
 

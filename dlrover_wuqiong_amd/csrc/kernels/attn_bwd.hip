@@ -108,7 +108,7 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                      const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
                      bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, float* __restrict__ dKp,
                      float* __restrict__ dVp, int S, int H, int HKV, float scale, float scale_log2,
-                     AttnStrides st) {
+                     AttnStrides st, AttnVarlen vl) {
   using C = DkvCfg<D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -117,14 +117,17 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
   const int b = bc.z, h = bc.y;
   const int hk = h / (H / HKV);
   const int kb0 = bc.x * C::BKB;  // causal: low key blocks (most queries) dispatch first
+  const SeqRange sr = seq_range(vl, b, h, H, S);  // S: the grid's (maximum) key length
+  if (kb0 >= sr.sk) return;
+  const int SQ = sr.sq, SK = sr.sk, co = SK - SQ;  // co: bottom-right causal offset
   const int kw0 = kb0 + 32 * wid;
   const int key = kw0 + r;
-  const bf16_t* Qb = Q + (int64_t)b * st.q_bs + (int64_t)h * D;
-  const bf16_t* dOb = dO + (int64_t)b * st.do_bs + (int64_t)h * D;
-  const bf16_t* Kb = K + (int64_t)b * st.k_bs + (int64_t)hk * D;
-  const bf16_t* Vb = V + (int64_t)b * st.v_bs + (int64_t)hk * D;
-  const float* lse_b = LSE + ((int64_t)b * H + h) * S;
-  const float* del_b = DELTA + ((int64_t)b * H + h) * S;
+  const bf16_t* Qb = Q + (int64_t)b * st.q_bs + (int64_t)sr.q_off * st.q_rs + (int64_t)h * D;
+  const bf16_t* dOb = dO + (int64_t)b * st.do_bs + (int64_t)sr.q_off * st.do_rs + (int64_t)h * D;
+  const bf16_t* Kb = K + (int64_t)b * st.k_bs + (int64_t)sr.k_off * st.k_rs + (int64_t)hk * D;
+  const bf16_t* Vb = V + (int64_t)b * st.v_bs + (int64_t)sr.k_off * st.v_rs + (int64_t)hk * D;
+  const float* lse_b = LSE + sr.lse_base;
+  const float* del_b = DELTA + sr.lse_base;
 
   // K fragments of this wave's keys stay in registers (B operand of S):
   // K[key][16 kk + 8 hh .. +7]; the block's V rows live in LDS (B operand of
@@ -134,12 +137,12 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
     const int row = v / C::NCH, c = v % C::NCH;
     const int kv = kb0 + row;
     *(u32x4*)(v_img + img_off<D>(row, c)) =
-        kv < S ? *(const u32x4*)(Vb + (int64_t)kv * st.v_rs + c * 8) : (u32x4){0, 0, 0, 0};
+        kv < SK ? *(const u32x4*)(Vb + (int64_t)kv * st.v_rs + c * 8) : (u32x4){0, 0, 0, 0};
   }
   u32x4 kf[C::KK];
 #pragma unroll
   for (int kk = 0; kk < C::KK; ++kk)
-    kf[kk] = key < S ? *(const u32x4*)(Kb + (int64_t)key * st.k_rs + 16 * kk + 8 * hh) : (u32x4){0, 0, 0, 0};
+    kf[kk] = key < SK ? *(const u32x4*)(Kb + (int64_t)key * st.k_rs + 16 * kk + 8 * hh) : (u32x4){0, 0, 0, 0};
   f32x16 dk[C::DT], dv[C::DT];
 #pragma unroll
   for (int dt = 0; dt < C::DT; ++dt)
@@ -149,8 +152,9 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
       dv[dt][i] = 0.f;
     }
 
-  const int q_lo = CAUSAL ? (kb0 / C::BQT) * C::BQT : 0;
-  const int n_it = max(0, (S - q_lo + C::BQT - 1) / C::BQT);
+  // first query that sees key kb0: key <= q + co
+  const int q_lo = CAUSAL ? (max(0, kb0 - co) / C::BQT) * C::BQT : 0;
+  const int n_it = max(0, (SQ - q_lo + C::BQT - 1) / C::BQT);
   u32x4 q_st[C::VPT], do_st[C::VPT];
   float lse_st = INFINITY, del_st = 0.f;
   auto issue = [&](int it) {
@@ -160,7 +164,7 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
       const int v = tid + 64 * C::WAVES * i;
       const int row = v / C::NCH, c = v % C::NCH;
       const int q = q0 + row;
-      if (q < S) {
+      if (q < SQ) {
         q_st[i] = *(const u32x4*)(Qb + (int64_t)q * st.q_rs + c * 8);
         do_st[i] = *(const u32x4*)(dOb + (int64_t)q * st.do_rs + c * 8);
       } else {
@@ -170,8 +174,8 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
     }
     if (tid < C::BQT) {
       const int q = q0 + tid;
-      lse_st = q < S ? lse_b[q] * 1.4426950408889634f : INFINITY;
-      del_st = q < S ? del_b[q] : 0.f;
+      lse_st = q < SQ ? lse_b[q] * 1.4426950408889634f : INFINITY;
+      del_st = q < SQ ? del_b[q] : 0.f;
     }
   };
   auto write = [&](int buf) {
@@ -203,8 +207,8 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
     const char* dl = ql + C::TILE;
     const float* stl = (const float*)(dl + C::TILE);
     // all queries of this tile precede this wave's keys: nothing to add
-    if (!CAUSAL || q0 + C::BQT - 1 >= kw0) {
-      const bool need_mask = (q0 + C::BQT > S) || (kw0 + 32 > S) || (CAUSAL && kw0 + 31 > q0);
+    if (!CAUSAL || q0 + C::BQT - 1 + co >= kw0) {
+      const bool need_mask = (q0 + C::BQT > SQ) || (kw0 + 32 > SK) || (CAUSAL && kw0 + 31 > q0 + co);
 #pragma unroll
       for (int qs = 0; qs < C::BQT / 32; ++qs) {
         // S = Q K^T, dP = dO V^T for 32 queries: key on the lane, query in the registers
@@ -234,7 +238,7 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
             float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], scale_log2, -l4[j]));
             if (need_mask) {
               const int q = q0 + qi + j;
-              if (q >= S || key >= S || (CAUSAL && key > q)) p = 0.f;
+              if (q >= SQ || key >= SK || (CAUSAL && key > q + co)) p = 0.f;
             }
             s[i] = p;
             dp[i] = p * (dp[i] - d4[j]);  // dS (scale applied in the epilogue)
@@ -266,11 +270,13 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
     }
     __syncthreads();
   }
-  if (key >= S) return;
+  if (key >= SK) return;
   // accumulator rows = d: register i of tile dt is d = 32 dt + 8 (i>>2) + 4 hh + (i&3)
   if (PARTIAL) {
-    float* kp = dKp + (((int64_t)b * S + key) * H + h) * D;
-    float* vp = dVp + (((int64_t)b * S + key) * H + h) * D;
+    // partials [rows, H, D]: rows = B*S (dense) or total_k (packed)
+    const int64_t prow = vl.cu_q ? (int64_t)sr.k_off + key : (int64_t)b * S + key;
+    float* kp = dKp + (prow * H + h) * D;
+    float* vp = dVp + (prow * H + h) * D;
 #pragma unroll
     for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
@@ -281,8 +287,8 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
         *(f32x4*)(vp + d) = (f32x4){dv[dt][4 * g], dv[dt][4 * g + 1], dv[dt][4 * g + 2], dv[dt][4 * g + 3]};
       }
   } else {
-    bf16_t* dKk = dK + (int64_t)b * st.dk_bs + (int64_t)hk * D + (int64_t)key * st.dk_rs;
-    bf16_t* dVk = dV + (int64_t)b * st.dv_bs + (int64_t)hk * D + (int64_t)key * st.dv_rs;
+    bf16_t* dKk = dK + (int64_t)b * st.dk_bs + (int64_t)hk * D + (int64_t)(sr.k_off + key) * st.dk_rs;
+    bf16_t* dVk = dV + (int64_t)b * st.dv_bs + (int64_t)hk * D + (int64_t)(sr.k_off + key) * st.dv_rs;
 #pragma unroll
     for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
@@ -359,7 +365,8 @@ template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(64 * DqCfg<D>::WAVES, 1)
 attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
                    const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
-                   bf16_t* __restrict__ dQ, int S, int H, int HKV, float scale, float scale_log2, AttnStrides st) {
+                   bf16_t* __restrict__ dQ, int S, int H, int HKV, float scale, float scale_log2, AttnStrides st,
+                   AttnVarlen vl) {
   using C = DqCfg<D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -370,18 +377,21 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
   const int hk = h / (H / HKV);
   const int qblk = CAUSAL ? nqb - 1 - bc.x : bc.x;
   const int q_blk0 = qblk * C::BQ;
+  const SeqRange sr = seq_range(vl, b, h, H, S);  // S: the grid's (maximum) query length
+  if (q_blk0 >= sr.sq) return;
+  const int SQ = sr.sq, SK = sr.sk, co = SK - SQ;
   const int q0 = q_blk0 + wid * 32;
   const int q = q0 + r;
-  const bf16_t* Qb = Q + (int64_t)b * st.q_bs + (int64_t)h * D;
-  const bf16_t* dOb = dO + (int64_t)b * st.do_bs + (int64_t)h * D;
-  const bf16_t* Kb = K + (int64_t)b * st.k_bs + (int64_t)hk * D;
-  const bf16_t* Vb = V + (int64_t)b * st.v_bs + (int64_t)hk * D;
+  const bf16_t* Qb = Q + (int64_t)b * st.q_bs + (int64_t)sr.q_off * st.q_rs + (int64_t)h * D;
+  const bf16_t* dOb = dO + (int64_t)b * st.do_bs + (int64_t)sr.q_off * st.do_rs + (int64_t)h * D;
+  const bf16_t* Kb = K + (int64_t)b * st.k_bs + (int64_t)sr.k_off * st.k_rs + (int64_t)hk * D;
+  const bf16_t* Vb = V + (int64_t)b * st.v_bs + (int64_t)sr.k_off * st.v_rs + (int64_t)hk * D;
 
   // Q and dO fragments (B operands): lane holds row q, d = 16 kk + 8 hh .. +7
   u32x4 qf[C::KK], dof[C::KK];
 #pragma unroll
   for (int kk = 0; kk < C::KK; ++kk) {
-    if (q < S) {
+    if (q < SQ) {
       qf[kk] = *(const u32x4*)(Qb + (int64_t)q * st.q_rs + 16 * kk + 8 * hh);
       dof[kk] = *(const u32x4*)(dOb + (int64_t)q * st.do_rs + 16 * kk + 8 * hh);
     } else {
@@ -389,9 +399,9 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
       dof[kk] = (u32x4){0, 0, 0, 0};
     }
   }
-  const int64_t so = ((int64_t)b * H + h) * S + q;
-  const float lse2 = q < S ? LSE[so] * 1.4426950408889634f : INFINITY;
-  const float dl = q < S ? DELTA[so] : 0.f;
+  const int64_t so = sr.lse_base + q;
+  const float lse2 = q < SQ ? LSE[so] * 1.4426950408889634f : INFINITY;
+  const float dl = q < SQ ? DELTA[so] : 0.f;
 
   f32x16 acc[C::DT];
 #pragma unroll
@@ -399,8 +409,11 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[dt][i] = 0.f;
 
-  int n_tiles = (S + C::BK - 1) / C::BK;
-  if (CAUSAL) n_tiles = min(n_tiles, min(S - 1, q_blk0 + C::BQ - 1) / C::BK + 1);
+  int n_tiles = (SK + C::BK - 1) / C::BK;
+  if (CAUSAL) {
+    const int last = min(SK - 1, min(SQ - 1, q_blk0 + C::BQ - 1) + co);
+    n_tiles = last < 0 ? 0 : min(n_tiles, last / C::BK + 1);
+  }
 
   u32x4 kst[C::VPT], vst[C::VPT];
   auto issue_load = [&](int t) {
@@ -409,7 +422,7 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
       const int v = tid + 64 * C::WAVES * i;
       const int row = v / C::NCH, c = v % C::NCH;
       const int key = t * C::BK + row;
-      if (key < S) {
+      if (key < SK) {
         kst[i] = *(const u32x4*)(Kb + (int64_t)key * st.k_rs + c * 8);
         vst[i] = *(const u32x4*)(Vb + (int64_t)key * st.v_rs + c * 8);
       } else {
@@ -439,8 +452,8 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
     const int k0 = t * C::BK;
     const char* kl = smem + (t & 1) * 2 * C::TILE;
     const char* vl = kl + C::TILE;
-    if (!CAUSAL || k0 <= q0 + 31) {
-      const bool need_mask = (k0 + C::BK > S) || (CAUSAL && (k0 + C::BK - 1 > q0));
+    if (!CAUSAL || k0 <= q0 + 31 + co) {
+      const bool need_mask = (k0 + C::BK > SK) || (CAUSAL && (k0 + C::BK - 1 > q0 + co));
       // one 32-key subtile at a time keeps S^T / dP^T at 32 registers
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb) {
@@ -462,7 +475,7 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
           float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], scale_log2, -lse2));
           if (need_mask) {
             const int key = k0 + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hh;
-            if (key >= S || (CAUSAL && key > q)) p = 0.f;
+            if (key >= SK || (CAUSAL && key > q + co)) p = 0.f;
           }
           s[i] = p * (dp[i] - dl);  // dS^T (scale applied in the epilogue)
         }
@@ -492,8 +505,8 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
     }
     __syncthreads();
   }
-  if (q < S) {
-    bf16_t* dQq = dQ + (int64_t)b * st.dq_bs + (int64_t)h * D + (int64_t)q * st.dq_rs;
+  if (q < SQ) {
+    bf16_t* dQq = dQ + (int64_t)b * st.dq_bs + (int64_t)h * D + (int64_t)(sr.q_off + q) * st.dq_rs;
 #pragma unroll
     for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
@@ -513,25 +526,30 @@ extern "C" int64_t dw_attn_bwd_workspace(int B, int S, int H, int D) {
 
 template <int D>
 static void launch_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const void* lse,
-                       char* ws, void* dq, void* dk, void* dv, int B, int S, int H, int HKV, int causal,
-                       float softmax_scale, const AttnStrides& st, hipStream_t s) {
+                       char* ws, void* dq, void* dk, void* dv, int B, int Sq, int Sk, int H, int HKV, int causal,
+                       float softmax_scale, const AttnStrides& st, const AttnVarlen& vl, hipStream_t s) {
+  // workspace layout (dw_attn_bwd_workspace with S = max(Sq, Sk)): delta, then
+  // the GQA partials; packed batches use [H, total_q] / [total_k, H, D] inside
+  const int Smax = Sq > Sk ? Sq : Sk;
   float* delta = (float*)ws;
-  const int64_t rows = (int64_t)B * S * H;
+  // delta rows: (b, s, h) of the dense tensor, or (row, h) of the packed one
+  const int pre_b = vl.cu_q ? 1 : B, pre_s = vl.cu_q ? vl.total_q : Sq;
+  const int64_t rows = (int64_t)pre_b * pre_s * H;
   constexpr int RPB = 4 * (64 / (D / 8));  // rows per 256-thread block
   hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3((unsigned)((rows + RPB - 1) / RPB)), dim3(256), 0, s,
-                     (const bf16_t*)o, (const bf16_t*)dout, delta, B, S, H, st);
+                     (const bf16_t*)o, (const bf16_t*)dout, delta, pre_b, pre_s, H, st);
   const float scale_log2 = softmax_scale * 1.4426950408889634f;
   // key-major dK / dV
   using KC = DkvCfg<D>;
   const bool partial = H != HKV;
-  float* pk = (float*)(ws + (((int64_t)B * H * S * 4 + 255) / 256) * 256);
-  float* pv = pk + (int64_t)B * S * H * D;
-  dim3 gk((unsigned)((S + KC::BKB - 1) / KC::BKB * H * B));  // 1-D: xcd_block()
+  float* pk = (float*)(ws + (((int64_t)B * H * Smax * 4 + 255) / 256) * 256);
+  float* pv = pk + (int64_t)B * Smax * H * D;
+  dim3 gk((unsigned)((Sk + KC::BKB - 1) / KC::BKB * H * B));  // 1-D: xcd_block()
   const int lk = 2 * KC::BUF + KC::VIMG;
 #define DKDV(CA, PA)                                                                                          \
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CA, PA>), gk, dim3(64 * KC::WAVES), lk, s, (const bf16_t*)q,   \
                      (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta,      \
-                     (bf16_t*)dk, (bf16_t*)dv, pk, pv, S, H, HKV, softmax_scale, scale_log2, st)
+                     (bf16_t*)dk, (bf16_t*)dv, pk, pv, Sk, H, HKV, softmax_scale, scale_log2, st, vl)
   if (causal) {
     if (partial) DKDV(true, true); else DKDV(true, false);
   } else {
@@ -539,22 +557,25 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
   }
 #undef DKDV
   if (partial) {
-    const int64_t nv = (int64_t)B * S * HKV * (D / 8);
+    // partial rows: B*Sk (dense) or total_k (packed, one "batch")
+    const int64_t prow = vl.cu_q ? (int64_t)vl.total_k : (int64_t)B * Sk;
+    const int pS = vl.cu_q ? vl.total_k : Sk;
+    const int64_t nv = prow * HKV * (D / 8);
     hipLaunchKernelGGL(gqa_reduce_kernel<D>, dim3(dw_grid_for(nv, 256, 4096)), dim3(256), 0, s, pk, pv,
-                       (bf16_t*)dk, (bf16_t*)dv, (int64_t)B * S, S, H, HKV, st);
+                       (bf16_t*)dk, (bf16_t*)dv, prow, pS, H, HKV, st);
   }
   // query-major dQ
   using DC = DqCfg<D>;
-  dim3 gq((unsigned)((S + DC::BQ - 1) / DC::BQ * H * B));  // 1-D: xcd_block()
+  dim3 gq((unsigned)((Sq + DC::BQ - 1) / DC::BQ * H * B));  // 1-D: xcd_block()
   const int lq = 4 * DC::TILE;
   if (causal)
     hipLaunchKernelGGL((attn_bwd_dq_kernel<D, true>), gq, dim3(64 * DC::WAVES), lq, s, (const bf16_t*)q,
                        (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta,
-                       (bf16_t*)dq, S, H, HKV, softmax_scale, scale_log2, st);
+                       (bf16_t*)dq, Sq, H, HKV, softmax_scale, scale_log2, st, vl);
   else
     hipLaunchKernelGGL((attn_bwd_dq_kernel<D, false>), gq, dim3(64 * DC::WAVES), lq, s, (const bf16_t*)q,
                        (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta,
-                       (bf16_t*)dq, S, H, HKV, softmax_scale, scale_log2, st);
+                       (bf16_t*)dq, Sq, H, HKV, softmax_scale, scale_log2, st, vl);
 }
 
 // strides: int64[16] = q, k, v, o, do, dq, dk, dv  x (batch, row) in elements
@@ -568,8 +589,35 @@ extern "C" int dw_attn_bwd_strided(const void* q, const void* k, const void* v, 
   for (int i = 0; i < 16; ++i) f[i] = strides[i];
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
-  if (D == 128) launch_bwd<128>(q, k, v, o, dout, lse, ws, dq, dk, dv, B, S, H, HKV, causal, softmax_scale, st, s);
-  else launch_bwd<64>(q, k, v, o, dout, lse, ws, dq, dk, dv, B, S, H, HKV, causal, softmax_scale, st, s);
+  const AttnVarlen vl = {nullptr, nullptr, 0, 0};
+  if (D == 128)
+    launch_bwd<128>(q, k, v, o, dout, lse, ws, dq, dk, dv, B, S, S, H, HKV, causal, softmax_scale, st, vl, s);
+  else
+    launch_bwd<64>(q, k, v, o, dout, lse, ws, dq, dk, dv, B, S, S, H, HKV, causal, softmax_scale, st, vl, s);
+  DW_LAUNCH_RET;
+}
+
+// Packed variable-length batch (see dw_attn_fwd_varlen).  row_strides
+// int64[8] = q, k, v, o, do, dq, dk, dv row strides (elements).  Workspace:
+// dw_attn_bwd_workspace(B, max(max_seqlen_q, max_seqlen_k), H, D).
+extern "C" int dw_attn_bwd_varlen(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                                  const void* lse, void* dq, void* dk, void* dv, void* workspace, const void* cu_q,
+                                  const void* cu_k, int B, int max_seqlen_q, int max_seqlen_k, int total_q,
+                                  int total_k, int H, int HKV, int D, const long long* row_strides, int causal,
+                                  float softmax_scale, void* stream) {
+  if (H % HKV != 0 || (D != 64 && D != 128) || !cu_q || !cu_k) return (int)hipErrorInvalidValue;
+  AttnStrides st = {};
+  st.q_rs = row_strides[0]; st.k_rs = row_strides[1]; st.v_rs = row_strides[2]; st.o_rs = row_strides[3];
+  st.do_rs = row_strides[4]; st.dq_rs = row_strides[5]; st.dk_rs = row_strides[6]; st.dv_rs = row_strides[7];
+  const AttnVarlen vl = {(const int*)cu_q, (const int*)cu_k, total_q, total_k};
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  if (D == 128)
+    launch_bwd<128>(q, k, v, o, dout, lse, ws, dq, dk, dv, B, max_seqlen_q, max_seqlen_k, H, HKV, causal,
+                    softmax_scale, st, vl, s);
+  else
+    launch_bwd<64>(q, k, v, o, dout, lse, ws, dq, dk, dv, B, max_seqlen_q, max_seqlen_k, H, HKV, causal,
+                   softmax_scale, st, vl, s);
   DW_LAUNCH_RET;
 }
 

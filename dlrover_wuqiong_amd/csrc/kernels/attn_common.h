@@ -37,6 +37,38 @@ __device__ __forceinline__ BlockXYZ xcd_block(int nx, int ny) {
   return r;
 }
 
+// Variable-length (packed) batches, flash-attn "varlen" convention: q rows of
+// sequence b are [cu_q[b], cu_q[b+1]) of a [total_q, H, D] tensor, k/v rows
+// [cu_k[b], cu_k[b+1]); LSE / delta are [H, total_q].  cu_q == nullptr: dense
+// [B, S, H, D] with LSE [B, H, S].  Causal masks align bottom-right
+// (key <= q + len_k - len_q), as flash-attn does for len_q != len_k.
+struct AttnVarlen {
+  const int* cu_q;
+  const int* cu_k;
+  int total_q, total_k;
+};
+
+struct SeqRange {
+  int q_off, k_off, sq, sk;
+  long long lse_base;  // LSE / delta index of (b, h, query 0)
+};
+
+__device__ __forceinline__ SeqRange seq_range(const AttnVarlen& vl, int b, int h, int H, int S) {
+  SeqRange r;
+  if (vl.cu_q) {
+    r.q_off = vl.cu_q[b];
+    r.k_off = vl.cu_k[b];
+    r.sq = vl.cu_q[b + 1] - r.q_off;
+    r.sk = vl.cu_k[b + 1] - r.k_off;
+    r.lse_base = (long long)h * vl.total_q + r.q_off;
+  } else {
+    r.q_off = r.k_off = 0;
+    r.sq = r.sk = S;
+    r.lse_base = ((long long)b * H + h) * S;
+  }
+  return r;
+}
+
 __device__ __forceinline__ unsigned int pack_s16(short a, short b) {
   return (unsigned int)(unsigned short)a | ((unsigned int)(unsigned short)b << 16);
 }

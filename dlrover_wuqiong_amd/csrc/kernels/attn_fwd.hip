@@ -57,7 +57,7 @@ template <int D, bool CAUSAL, int MINW = 1>
 __global__ void __launch_bounds__(64 * Fwd2Cfg<D>::WAVES, MINW)
 attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
                 bf16_t* __restrict__ O, float* __restrict__ LSE, int S, int H, int HKV, float scale_log2,
-                AttnStrides st) {
+                AttnStrides st, AttnVarlen vl) {
   using C = Fwd2Cfg<D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -69,10 +69,15 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   const int hk = h / (H / HKV);
   const int qblk = CAUSAL ? nqb - 1 - bc.x : bc.x;  // causal: heaviest query blocks first
   const int q_blk0 = qblk * C::BQ;
+  // this (batch | packed sequence)'s query / key extents; S is the grid's
+  // (maximum) length
+  const SeqRange sr = seq_range(vl, b, h, H, S);
+  if (q_blk0 >= sr.sq) return;  // whole block past a short sequence
+  const int SQ = sr.sq, SK = sr.sk, co = SK - SQ;  // co: bottom-right causal offset
   const int q0 = q_blk0 + wid * 32;
-  const bf16_t* Qb = Q + (int64_t)b * st.q_bs + (int64_t)h * D;
-  const bf16_t* Kb = K + (int64_t)b * st.k_bs + (int64_t)hk * D;
-  const bf16_t* Vb = V + (int64_t)b * st.v_bs + (int64_t)hk * D;
+  const bf16_t* Qb = Q + (int64_t)b * st.q_bs + (int64_t)sr.q_off * st.q_rs + (int64_t)h * D;
+  const bf16_t* Kb = K + (int64_t)b * st.k_bs + (int64_t)sr.k_off * st.k_rs + (int64_t)hk * D;
+  const bf16_t* Vb = V + (int64_t)b * st.v_bs + (int64_t)sr.k_off * st.v_rs + (int64_t)hk * D;
 
   // ---- Q fragments (B operand of S^T): lane holds Q[q0 + r][16 kk + 8 hh .. +7]
   u32x4 qf[C::KK];
@@ -80,7 +85,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
     const int q = q0 + r;
 #pragma unroll
     for (int kk = 0; kk < C::KK; ++kk)
-      qf[kk] = (q < S) ? *(const u32x4*)(Qb + (int64_t)q * st.q_rs + 16 * kk + 8 * hh) : (u32x4){0, 0, 0, 0};
+      qf[kk] = (q < SQ) ? *(const u32x4*)(Qb + (int64_t)q * st.q_rs + 16 * kk + 8 * hh) : (u32x4){0, 0, 0, 0};
   }
 
   f32x16 o[C::DT];
@@ -90,8 +95,11 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
     for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
   float m_i = -INFINITY, l_i = 0.f;  // l_i: this lane-half's partial row sum
 
-  int n_tiles = (S + C::BK - 1) / C::BK;
-  if (CAUSAL) n_tiles = min(n_tiles, min(S - 1, q_blk0 + C::BQ - 1) / C::BK + 1);
+  int n_tiles = (SK + C::BK - 1) / C::BK;
+  if (CAUSAL) {
+    const int last = min(SK - 1, min(SQ - 1, q_blk0 + C::BQ - 1) + co);  // last key the block's queries see
+    n_tiles = last < 0 ? 0 : min(n_tiles, last / C::BK + 1);
+  }
 
   u32x4 kst[C::VPT], vst[C::VPT];
   auto issue_load = [&](int t) {
@@ -100,7 +108,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
       const int v = tid + 64 * C::WAVES * i;
       const int row = v / C::NCH, c = v % C::NCH;
       const int key = t * C::BK + row;
-      if (key < S) {
+      if (key < SK) {
         kst[i] = *(const u32x4*)(Kb + (int64_t)key * st.k_rs + c * 8);
         vst[i] = *(const u32x4*)(Vb + (int64_t)key * st.v_rs + c * 8);
       } else {
@@ -133,7 +141,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
     const char* kl = smem + (t & 1) * 2 * C::TILE;
     const char* vl = kl + C::TILE;
     // a wave whose 32 queries all lie before this tile has nothing to do here
-    const bool active = !CAUSAL || (k0 <= q0 + 31);
+    const bool active = !CAUSAL || (k0 <= q0 + 31 + co);
     if (active) {
       // ---- S^T = K Q^T : two 32-key subtiles
       f32x16 s[2];
@@ -152,7 +160,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
       // The max runs on the raw scores (scale > 0) and the scale is folded
       // into the exponent's FMA: p = exp2(s * c - m * c).
       const int q = q0 + r;
-      const bool need_mask = (k0 + C::BK > S) || (CAUSAL && (k0 + C::BK - 1 > q0));
+      const bool need_mask = (k0 + C::BK > SK) || (CAUSAL && (k0 + C::BK - 1 > q0 + co));
       float mx = -INFINITY;
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb)
@@ -160,7 +168,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
         for (int i = 0; i < 16; ++i) {
           if (need_mask) {
             const int key = k0 + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hh;
-            if (key >= S || (CAUSAL && key > q)) s[sb][i] = -INFINITY;
+            if (key >= SK || (CAUSAL && key > q + co)) s[sb][i] = -INFINITY;
           }
           mx = fmaxf(mx, s[sb][i]);
         }
@@ -221,8 +229,8 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   // ---- epilogue: O = O^T / l ; lse
   const float l_tot = l_i + __shfl_xor(l_i, 32, 64);
   const int q = q0 + r;
-  if (q < S) {
-    bf16_t* Oq = O + (int64_t)b * st.o_bs + (int64_t)h * D + (int64_t)q * st.o_rs;
+  if (q < SQ) {
+    bf16_t* Oq = O + (int64_t)b * st.o_bs + (int64_t)h * D + (int64_t)(sr.q_off + q) * st.o_rs;
     const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
 #pragma unroll
     for (int dt = 0; dt < C::DT; ++dt)
@@ -235,14 +243,14 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
       }
     if (hh == 0 && LSE) {
       const float lse = (l_tot > 0.f) ? (m_i + log2f(l_tot)) * 0.6931471805599453f : -INFINITY;
-      LSE[((int64_t)b * H + h) * S + q] = lse;
+      LSE[sr.lse_base + q] = lse;
     }
   }
 }
 
 template <int D>
 static void launch_fwd(const void* q, const void* k, const void* v, void* o, void* lse, int B, int S, int H, int HKV,
-                       int causal, float scale_log2, const AttnStrides& st, hipStream_t s) {
+                       int causal, float scale_log2, const AttnStrides& st, const AttnVarlen& vl, hipStream_t s) {
   using C = Fwd2Cfg<D>;
   dim3 grid((unsigned)((S + C::BQ - 1) / C::BQ * H * B)), block(64 * C::WAVES);  // 1-D: xcd_block()
   const int lds = 4 * C::TILE;
@@ -251,13 +259,13 @@ static void launch_fwd(const void* q, const void* k, const void* v, void* o, voi
   // would spill 116 B/lane, so it keeps one block per CU
   if (causal && D == 64)
     hipLaunchKernelGGL((attn_fwd_kernel<D, true, 4>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
-                       (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st);
+                       (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st, vl);
   else if (causal)
     hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
-                       (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st);
+                       (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st, vl);
   else
     hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
-                       (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st);
+                       (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st, vl);
 }
 
 // strides: int64[8] = q_bs, q_rs, k_bs, k_rs, v_bs, v_rs, o_bs, o_rs (elements)
@@ -270,8 +278,29 @@ extern "C" int dw_attn_fwd_strided(const void* q, const void* k, const void* v, 
   st.v_bs = strides[4]; st.v_rs = strides[5]; st.o_bs = strides[6]; st.o_rs = strides[7];
   const float scale_log2 = softmax_scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
-  if (D == 128) launch_fwd<128>(q, k, v, o, lse, B, S, H, HKV, causal, scale_log2, st, s);
-  else if (D == 64) launch_fwd<64>(q, k, v, o, lse, B, S, H, HKV, causal, scale_log2, st, s);
+  const AttnVarlen vl = {nullptr, nullptr, 0, 0};
+  if (D == 128) launch_fwd<128>(q, k, v, o, lse, B, S, H, HKV, causal, scale_log2, st, vl, s);
+  else if (D == 64) launch_fwd<64>(q, k, v, o, lse, B, S, H, HKV, causal, scale_log2, st, vl, s);
+  else return (int)hipErrorInvalidValue;
+  DW_LAUNCH_RET;
+}
+
+// Packed variable-length batch: q [total_q, H, D], k/v [total_k, HKV, D] (row
+// strides given: rows_strides int64[4] = q, k, v, o), cu_seqlens int32 [B+1]
+// on the device, lse [H, total_q].  max_seqlen_q sizes the grid; blocks past
+// a sequence's end exit at once.
+extern "C" int dw_attn_fwd_varlen(const void* q, const void* k, const void* v, void* o, void* lse,
+                                  const void* cu_q, const void* cu_k, int B, int max_seqlen_q, int total_q, int H,
+                                  int HKV, int D, const long long* row_strides, int causal, float softmax_scale,
+                                  void* stream) {
+  if (H % HKV != 0 || !cu_q || !cu_k) return (int)hipErrorInvalidValue;
+  AttnStrides st = {};
+  st.q_rs = row_strides[0]; st.k_rs = row_strides[1]; st.v_rs = row_strides[2]; st.o_rs = row_strides[3];
+  const AttnVarlen vl = {(const int*)cu_q, (const int*)cu_k, total_q, 0};
+  const float scale_log2 = softmax_scale * 1.4426950408889634f;
+  hipStream_t s = (hipStream_t)stream;
+  if (D == 128) launch_fwd<128>(q, k, v, o, lse, B, max_seqlen_q, H, HKV, causal, scale_log2, st, vl, s);
+  else if (D == 64) launch_fwd<64>(q, k, v, o, lse, B, max_seqlen_q, H, HKV, causal, scale_log2, st, vl, s);
   else return (int)hipErrorInvalidValue;
   DW_LAUNCH_RET;
 }

@@ -72,12 +72,40 @@ def launch_multi_copy(descs: torch.Tensor, stream=None):
                                  ctypes.c_void_p(s.cuda_stream)), "multi_copy")
 
 
+class PrepTracker:
+    """Futures of the background prefault + registration of shm ranges
+    (engine ``_start_shm_prep``): a flush waits only for the ranges it
+    writes, so the first save of a fresh segment never waits for the other
+    slot's preparation."""
+
+    def __init__(self):
+        self._ranges: List[Tuple[int, int, Future]] = []
+
+    def add(self, addr: int, nbytes: int) -> Future:
+        f: Future = Future()
+        self._ranges.append((addr, addr + nbytes, f))
+        return f
+
+    def wait(self, addr: Optional[int] = None, nbytes: int = 0):
+        for a, e, f in self._ranges:
+            if addr is None or (a < addr + nbytes and addr < e):
+                f.result()
+
+    result = wait  # Future-like: wait for everything
+
+    def fail_pending(self):
+        for _a, _e, f in self._ranges:
+            if not f.done():
+                f.set_result(None)
+
+
 class PinnedRegistry:
     """Tracks hipHostRegister'ed ranges of shm mappings."""
 
     def __init__(self):
         self._ranges: List[Tuple[int, int]] = []
         self._lock = threading.Lock()
+        self.piece = max(64, int(os.environ.get("DWAMD_PREP_PIECE_MB", "1024"))) << 20
 
     def ensure(self, addr: int, nbytes: int) -> bool:
         if nbytes <= 0:
@@ -98,13 +126,26 @@ class PinnedRegistry:
                     break
             if cur < e:
                 gaps.append((cur, e))
-            for ga, ge in gaps:
-                err = _kern().dw_host_register(ctypes.c_void_p(ga), ge - ga)
-                if err != 0:
-                    logger.warning(f"hipHostRegister({ge - ga} B) failed with {err}; using pageable copies")
-                    return False
-                self._ranges.append((ga, ge))
-            return True
+        # register in pieces, the lock released in between: one huge
+        # hipHostRegister holds the process's mm lock (and the runtime's) for
+        # seconds, stalling the training thread's allocations and launches
+        for ga, ge in gaps:
+            o = ga
+            while o < ge:
+                with self._lock:  # another thread may have registered parts meanwhile
+                    inside = next((re for ra, re in self._ranges if ra <= o < re), None)
+                    if inside is not None:
+                        o = inside
+                        continue
+                    nxt = min([ra for ra, _re in self._ranges if ra > o] + [ge])
+                    c = min(self.piece, nxt - o)
+                    err = _kern().dw_host_register(ctypes.c_void_p(o), c)
+                    if err != 0:
+                        logger.warning(f"hipHostRegister({c} B) failed with {err}; using pageable copies")
+                        return False
+                    self._ranges.append((o, o + c))
+                o += c
+        return True
 
     def split(self, addr: int, nbytes: int) -> List[Tuple[int, int, bool]]:
         """Cut [addr, addr+nbytes) at registration boundaries: HIP rejects a
@@ -283,7 +324,7 @@ class GpuCopier:
         # Future of the engine's background shm preparation (prefault +
         # hipHostRegister of this rank's slices): the flush -- never the
         # training pause -- waits for it.
-        self.pending_prep: Optional[Future] = None
+        self.pending_prep: Optional[PrepTracker] = None
         # Snapshot staging in HBM.  Two buffers when the card has room (288 GB
         # MI355X: a 22 GB GPT2-1.5B state twice is nothing): snapshot k+1 then
         # never waits for the PCIe flush of snapshot k -- the flushes queue on
@@ -490,7 +531,7 @@ class GpuCopier:
         def flush():
             if n > 0:
                 if prep is not None:
-                    prep.result()  # segment prefault + registration (first save of a segment)
+                    prep.wait(shm_payload_addr + lo, n)  # this range's prefault + registration
                 # registering here (flush thread), not in the training pause:
                 # a no-op once the range is covered
                 pinned = self.pinned.ensure(shm_payload_addr + lo, n)
@@ -677,7 +718,7 @@ class GpuCopier:
         def flush():
             try:
                 if prep is not None:
-                    prep.result()
+                    prep.wait(shm_payload_addr + lo, n)
                 pinned = self.pinned.ensure(shm_payload_addr + lo, n)
                 sp = ctypes.c_void_p(self.side_stream.cuda_stream)
                 t0 = time.perf_counter()

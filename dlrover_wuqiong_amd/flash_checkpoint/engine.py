@@ -25,7 +25,6 @@ import os
 import threading
 import time
 from abc import ABC, abstractmethod
-from concurrent.futures import Future
 from datetime import timedelta
 from typing import Any, Dict, List, Optional
 
@@ -324,7 +323,11 @@ class CheckpointEngine(ABC):
         first = self._next_slot if self._next_slot is not None else h.write_slot()
         order = [first] + [s for s in range(h.num_slots) if s != first]
         ranges = [(h.payload_addr(slot) + lo, hi - lo) for slot in order]
-        first_done: Future = Future()
+        from .copier import PrepTracker
+
+        tracker = PrepTracker()
+        futs = [tracker.add(a, n) for a, n in ranges]
+        first_done = futs[0]
         piece = _PREP_PIECE
 
         def prep():
@@ -345,11 +348,9 @@ class CheckpointEngine(ABC):
                         if copier is not None:
                             copier.pinned.ensure(addr + o, c)
                         time.sleep(0.001)  # let a waiting mm writer in
-                    if i == 0:
-                        first_done.set_result(time.perf_counter() - t0)
+                    futs[i].set_result(time.perf_counter() - t0)
             finally:
-                if not first_done.done():
-                    first_done.set_result(None)
+                tracker.fail_pending()
             if _TIMING:
                 logger.info(f"shm prep ({len(ranges)} slot slices, {hi - lo} B each): first slot "
                             f"{1000 * (first_done.result() or 0):.1f} ms, all {1000 * (time.perf_counter() - t0):.1f} ms "
@@ -361,7 +362,7 @@ class CheckpointEngine(ABC):
             self._prep_pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="dwamd-shm-prep")
         self._shm_prep = self._prep_pool.submit(prep)
         if copier is not None:
-            copier.pending_prep = first_done
+            copier.pending_prep = tracker
 
     # ----------------------------------------------------------- core save
     def save_state_dict_to_memory(self, state_dict: Dict, conf: CheckpointConfig) -> bool:

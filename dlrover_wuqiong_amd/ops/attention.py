@@ -149,3 +149,128 @@ def flash_attn_func(q, k, v, causal: bool = True, softmax_scale=None):
     o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
                                        is_causal=causal, scale=scale)
     return o.transpose(1, 2)
+
+
+# ---------------------------------------------------------------------------
+# Variable-length (packed) batches: flash-attn's varlen API on the same
+# kernels (``dw_attn_fwd_varlen`` / ``dw_attn_bwd_varlen``; per-block
+# sequence extents from cu_seqlens on the device, no padding compute).
+def _rows_dense(t: torch.Tensor) -> torch.Tensor:
+    """[total, H, D] with dense (H, D): any row stride is fine."""
+    return t if (t.stride(2) == 1 and t.stride(1) == t.shape[2]) else t.contiguous()
+
+
+def _row_strides(*ts) -> ctypes.Array:
+    return (ctypes.c_longlong * len(ts))(*[t.stride(0) for t in ts])
+
+
+class _FlashAttnVarlenFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, cu_q, cu_k, max_sq, max_sk, causal, scale):
+        _hip.require_bf16(q, k, v)
+        q, k, v = _rows_dense(q), _rows_dense(k), _rows_dense(v)
+        cu_q = cu_q.to(device=q.device, dtype=torch.int32).contiguous()
+        cu_k = cu_k.to(device=q.device, dtype=torch.int32).contiguous()
+        total_q, H, D = q.shape
+        HKV = k.shape[1]
+        B = cu_q.numel() - 1
+        o = torch.empty(total_q, H, D, device=q.device, dtype=q.dtype)
+        lse = torch.empty(H, total_q, device=q.device, dtype=torch.float32)
+        _hip.check(_hip.lib().dw_attn_fwd_varlen(_hip.ptr(q), _hip.ptr(k), _hip.ptr(v), _hip.ptr(o), _hip.ptr(lse),
+                                                 _hip.ptr(cu_q), _hip.ptr(cu_k), B, int(max_sq), total_q, H, HKV, D,
+                                                 _row_strides(q, k, v, o), int(causal), float(scale), _hip.stream()),
+                   "attn_fwd_varlen")
+        ctx.save_for_backward(q, k, v, o, lse, cu_q, cu_k)
+        ctx.meta = (int(max_sq), int(max_sk), bool(causal), float(scale))
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, cu_q, cu_k = ctx.saved_tensors
+        max_sq, max_sk, causal, scale = ctx.meta
+        do = _rows_dense(do.to(torch.bfloat16))
+        total_q, H, D = q.shape
+        total_k, HKV = k.shape[0], k.shape[1]
+        B = cu_q.numel() - 1
+        L = _hip.lib()
+        ws = torch.empty(L.dw_attn_bwd_workspace(B, max(max_sq, max_sk), H, D), device=q.device, dtype=torch.uint8)
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        _hip.check(L.dw_attn_bwd_varlen(_hip.ptr(q), _hip.ptr(k), _hip.ptr(v), _hip.ptr(o), _hip.ptr(do),
+                                        _hip.ptr(lse), _hip.ptr(dq), _hip.ptr(dk), _hip.ptr(dv), _hip.ptr(ws),
+                                        _hip.ptr(cu_q), _hip.ptr(cu_k), B, max_sq, max_sk, total_q, total_k, H, HKV,
+                                        D, _row_strides(q, k, v, o, do, dq, dk, dv), int(causal), float(scale),
+                                        _hip.stream()), "attn_bwd_varlen")
+        return dq, dk, dv, None, None, None, None, None, None
+
+
+def varlen_attention_reference(q, k, v, cu_seqlens_q, cu_seqlens_k, causal=False, softmax_scale=None):
+    """fp32 reference of the packed layout (bottom-right causal alignment)."""
+    H, D = q.shape[1], q.shape[2]
+    HKV = k.shape[1]
+    scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(D)
+    cq, ck = cu_seqlens_q.tolist(), cu_seqlens_k.tolist()
+    out = torch.zeros(q.shape, dtype=torch.float32, device=q.device)
+    for b in range(len(cq) - 1):
+        qs, ks = q[cq[b]:cq[b + 1]].float(), k[ck[b]:ck[b + 1]].float()
+        vs = v[ck[b]:ck[b + 1]].float()
+        sq, sk = qs.shape[0], ks.shape[0]
+        if sq == 0:
+            continue
+        if HKV != H:
+            ks = ks.repeat_interleave(H // HKV, dim=1)
+            vs = vs.repeat_interleave(H // HKV, dim=1)
+        s = torch.einsum("qhd,khd->hqk", qs, ks) * scale
+        if causal:
+            qi = torch.arange(sq, device=q.device)[:, None]
+            kj = torch.arange(sk, device=q.device)[None, :]
+            s = s.masked_fill(kj > qi + (sk - sq), float("-inf"))
+        p = torch.softmax(s, dim=-1).nan_to_num(0.0)  # rows with no visible key -> 0
+        out[cq[b]:cq[b + 1]] = torch.einsum("hqk,khd->qhd", p, vs)
+    return out.to(q.dtype)
+
+
+def flash_attn_varlen_func(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, dropout_p=0.0,
+                           softmax_scale=None, causal=False, window_size=(-1, -1), alibi_slopes=None,
+                           deterministic=False, return_attn_probs=False):
+    """flash-attn's ``flash_attn_varlen_func``: q [total_q, H, D], k/v
+    [total_k, Hkv, D], cu_seqlens int32 [B+1] -> [total_q, H, D].
+    (Reference use: atorch/atorch/modules/transformer/layers.py:1226-1244.)"""
+    if dropout_p or tuple(window_size) != (-1, -1) or alibi_slopes is not None or return_attn_probs:
+        raise NotImplementedError("dropout / sliding window / alibi / attention probs are not supported")
+    D = q.shape[-1]
+    scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(D)
+    if _hip.use_hip(q):
+        return _FlashAttnVarlenFn.apply(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, causal,
+                                        scale)
+    return varlen_attention_reference(q, k, v, cu_seqlens_q, cu_seqlens_k, causal, scale)
+
+
+def unpad_input(hidden: torch.Tensor, attention_mask: torch.Tensor):
+    """flash-attn ``bert_padding.unpad_input``: hidden [B, S, ...], mask
+    [B, S] (1 = token) -> (hidden[valid] [total, ...], indices, cu_seqlens
+    int32 [B+1], max_seqlen)."""
+    seqlens = attention_mask.sum(dim=-1, dtype=torch.int32)
+    indices = torch.nonzero(attention_mask.flatten(), as_tuple=False).flatten()
+    cu = torch.zeros(seqlens.numel() + 1, dtype=torch.int32, device=hidden.device)
+    cu[1:] = torch.cumsum(seqlens, dim=0)
+    flat = hidden.reshape(hidden.shape[0] * hidden.shape[1], *hidden.shape[2:])
+    return flat.index_select(0, indices), indices, cu, int(seqlens.max()) if seqlens.numel() else 0
+
+
+def pad_input(hidden: torch.Tensor, indices: torch.Tensor, batch: int, seqlen: int) -> torch.Tensor:
+    """Inverse of :func:`unpad_input` (padding positions are zero)."""
+    out = torch.zeros(batch * seqlen, *hidden.shape[1:], device=hidden.device, dtype=hidden.dtype)
+    out.index_copy_(0, indices, hidden)
+    return out.view(batch, seqlen, *hidden.shape[1:])
+
+
+def flash_attn_padded_func(q, k, v, key_padding_mask: torch.Tensor, causal: bool = True, softmax_scale=None):
+    """BSHD attention of a padded batch (``key_padding_mask`` [B, S], True =
+    token, left or right padding): unpad -> varlen kernels -> pad.  Padded
+    query rows return zeros."""
+    B, S = q.shape[0], q.shape[1]
+    qu, idx, cu, mx = unpad_input(q, key_padding_mask)
+    ku = k.reshape(B * S, *k.shape[2:]).index_select(0, idx)
+    vu = v.reshape(B * S, *v.shape[2:]).index_select(0, idx)
+    o = flash_attn_varlen_func(qu, ku, vu, cu, cu, mx, mx, softmax_scale=softmax_scale, causal=causal)
+    return pad_input(o, idx, B, S)

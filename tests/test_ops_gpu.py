@@ -211,6 +211,56 @@ def test_flash_attention(D, causal, S, H, HKV):
     assert _rel(v.grad, vf.grad) < 3e-2
 
 
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("H,HKV", [(4, 4), (8, 2)])
+def test_flash_attention_varlen(D, causal, H, HKV):
+    """Packed batch with empty, sub-tile, multi-block sequences and
+    len_q != len_k (bottom-right causal) vs the fp32 per-sequence reference."""
+    from dlrover_wuqiong_amd.ops.attention import flash_attn_varlen_func, varlen_attention_reference
+
+    torch.manual_seed(3)
+    lq = [37, 0, 300, 1, 513, 64]
+    lk = [37, 5, 300, 40, 513, 64] if not causal else [50, 0, 300, 1, 520, 64]
+    cu_q = torch.tensor([0] + list(__import__("itertools").accumulate(lq)), dtype=torch.int32, device=DEV)
+    cu_k = torch.tensor([0] + list(__import__("itertools").accumulate(lk)), dtype=torch.int32, device=DEV)
+    q = torch.randn(sum(lq), H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(sum(lk), HKV, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(sum(lk), HKV, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = flash_attn_varlen_func(q, k, v, cu_q, cu_k, max(lq), max(lk), causal=causal)
+    qf, kf, vf = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = varlen_attention_reference(qf, kf, vf, cu_q, cu_k, causal=causal)
+    assert _rel(o, orf) < 2e-2
+    do = torch.randn_like(o)
+    o.backward(do)
+    orf.backward(do.float())
+    assert _rel(q.grad, qf.grad) < 3e-2
+    assert _rel(k.grad, kf.grad) < 3e-2
+    assert _rel(v.grad, vf.grad) < 3e-2
+
+
+def test_flash_attention_padded_batch():
+    """Left + right padded batch through unpad -> varlen -> pad equals dense
+    attention of each sequence's valid tokens."""
+    from dlrover_wuqiong_amd.ops.attention import attention_reference, flash_attn_padded_func
+
+    torch.manual_seed(4)
+    B, S, H, D = 3, 200, 4, 128
+    q = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    mask = torch.zeros(B, S, dtype=torch.bool, device=DEV)
+    mask[0, :150] = True   # right padding
+    mask[1, 77:] = True    # left padding
+    mask[2, :] = True
+    o = flash_attn_padded_func(q, k, v, mask, causal=True)
+    for b, (lo, hi) in enumerate([(0, 150), (77, 200), (0, 200)]):
+        ref = attention_reference(q[b:b + 1, lo:hi].float(), k[b:b + 1, lo:hi].float(), v[b:b + 1, lo:hi].float(),
+                                  causal=True)
+        assert _rel(o[b:b + 1, lo:hi], ref) < 2e-2
+        assert (lo == 0 or o[b, :lo].abs().max() == 0) and (hi == S or o[b, hi:].abs().max() == 0)
+
+
 @pytest.mark.parametrize("D,causal,S", [(64, True, 1024), (64, False, 200), (128, True, 384)])
 def test_flash_attention_qkvpacked(D, causal, S):
     """Packed [B, S, 3, H, D] path: strided q/k/v reads, packed dQKV writes."""
