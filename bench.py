@@ -34,8 +34,10 @@ What a worker does (incarnation 0):
   4. time-to-durable (pause + PCIe flush until every slice is in shm) and a
      DISK save persisted by the agent (native parallel pwrite) while
      training continues: persist GB/s and the step-time interference;
-  5. fault window: training continues with saves; mid-step (after backward,
-     before the optimizer step) the last rank SIGKILLs itself.
+  5. fault window (64 steps): training continues with saves; half-way
+     through a checkpoint interval (the expected loss of a failure at a
+     random time), mid-step (after backward, before the optimizer step),
+     the last rank SIGKILLs itself.
 
 The agent detects the death, SIGKILLs the survivors stuck in RCCL, re-runs
 the rendezvous (new master port -> a new RCCL world), and activates the
@@ -76,7 +78,7 @@ def parse(argv=None):
     # checkpoint every 4 steps (~0.5 s at N=1): the previous flush of the
     # 21.8 GB payload (~0.4 s) has landed by the next save
     p.add_argument("--ckpt-interval", type=int, default=4)
-    p.add_argument("--fault-window", type=int, default=16, help="steps in the measured fault window")
+    p.add_argument("--fault-window", type=int, default=64, help="steps in the measured fault window (~8 s)")
     p.add_argument("--ckpt-dir", default="/tmp/dwamd_bench_ckpt")
     p.add_argument("--no-fault", action="store_true")
     p.add_argument("--no-persist", action="store_true", help="skip the DISK persist measurement")
@@ -119,9 +121,10 @@ def _read_jsonl(path):
 
 def _kill_after(a, s0):
     """Completed steps at the kill for a fault window starting at step s0:
-    the kill lands in the step right before the window's 2nd save, so
-    ckpt_interval - 1 completed steps (plus the partial one) are lost."""
-    return s0 + 2 * a.ckpt_interval - 1
+    half-way through the window's 2nd checkpoint interval -- the expected
+    loss of a failure at a uniformly random time (ckpt_interval / 2 completed
+    steps plus the partial one are redone)."""
+    return s0 + a.ckpt_interval + a.ckpt_interval // 2
 
 
 def launcher(a) -> int:
@@ -422,6 +425,10 @@ def worker(a) -> int:
             emit({"event": "kill", "t": time.time(), "completed_step": completed, "rank": rank}, all_ranks=True)
             os.kill(os.getpid(), signal.SIGKILL)
 
+    def state_sums():
+        third = opt.master if opt.master is not None else opt.exp_avg_sq
+        return [float(flat.data.float().sum()), float(opt.exp_avg.sum()), float(third.sum())]
+
     def save(st=None):
         t0 = time.perf_counter()
         ok = ckpt.save_checkpoint(step, state(), storage_type=st or StorageType.MEMORY)
@@ -577,6 +584,12 @@ def worker(a) -> int:
         restore_sec = mx(time.perf_counter() - t0)
         step = int(restored.get("step", 0)) if restored else 0
         restore_ok = bool(restored) and step > 0
+        # bit-exact check against the sums incarnation 0 logged right after
+        # that save (the last one before the kill)
+        want = [e for e in _read_jsonl(step_log) if e["event"] == "saved_sums" and e["rank"] == rank
+                and e["step"] == step]
+        if restore_ok and want:
+            restore_ok = state_sums() == want[-1]["sums"]
         t_restored = time.time()
         emit({"event": "start", "incarnation": incarnation, "t": time.time(), "restored_step": step,
               "restore_sec": restore_sec, "restore_ok": restore_ok, "t_proc": t_proc, "t_activated": t_act,
@@ -591,14 +604,22 @@ def worker(a) -> int:
     # ---------------- fault window: train + save every interval; rank n-1 dies mid-step
     kill_after = _kill_after(a, s0) if not a.no_fault else -1
     s_end = s0 + a.fault_window
+    last_before_kill = kill_after - (kill_after - s0) % a.ckpt_interval if kill_after > 0 else -1
     while step < s_end:
         train_step(True)
         sync_step()
         if (step - s0) % a.ckpt_interval == 0:
             save()
+            if incarnation == 0 and step == last_before_kill:
+                emit({"event": "saved_sums", "step": step, "rank": rank, "sums": state_sums()}, all_ranks=True)
         emit({"event": "step", "step": step, "t": time.time(), "incarnation": incarnation})
-    sync_all()
+    # end of the window: every rank's compute done (the background flush of
+    # the last checkpoint is not training time and is not waited for)
+    if world > 1:
+        dist.barrier()
+    sync_step()
     emit({"event": "done", "t": time.time(), "step": step, "start_step": start_step, "incarnation": incarnation})
+    sync_all()
     ckpt.close()
     if world > 1:
         dist.barrier()

@@ -14,6 +14,7 @@ SIGS = {
     "dw_host_registered": (i32, [vp]),
     "dw_memcpy_async": (i32, [vp, vp, u64, i32, vp]),
     "dw_stream_sync": (i32, [vp]),
+    "dw_event_sync": (i32, [vp]),
     "dw_stream_create_cumask": (vp, [i32, c.POINTER(i32)]),
     "dw_stream_destroy": (i32, [vp]),
     "dw_stream_create_prio": (vp, [i32, c.POINTER(i32)]),

@@ -106,6 +106,7 @@ extern "C" int dw_memcpy_async(void* dst, const void* src, uint64_t bytes, int k
 }
 
 extern "C" int dw_stream_sync(void* stream) { return (int)hipStreamSynchronize((hipStream_t)stream); }
+extern "C" int dw_event_sync(void* event) { return (int)hipEventSynchronize((hipEvent_t)event); }
 
 // A stream whose kernels (including the runtime's blit kernels that
 // implement hipMemcpyAsync to/from host memory) may only run on a subset of

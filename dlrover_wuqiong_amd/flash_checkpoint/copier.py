@@ -462,10 +462,14 @@ class GpuCopier:
     # ----------------------------------------------------------------- save
     def save_slice(self, layout: Layout, shm_payload_addr: int, lo: int, hi: int,
                    on_done: Callable[[], None], sync: bool = False,
-                   before_copy: Optional[Callable[[int], None]] = None):
+                   before_copy: Optional[Callable[[int], None]] = None,
+                   on_snapshot: Optional[Callable[[], None]] = None):
         """Snapshot payload bytes [lo, hi) of ``layout`` and flush to shm.
         ``before_copy(staging_idx)`` runs before the snapshot is enqueued
-        (HBM-tier stamp invalidation)."""
+        (HBM-tier stamp invalidation); ``on_snapshot()`` on the flush thread
+        once the snapshot sits complete in the staging buffer, before its
+        PCIe flush (HBM-tier stamp: a standby-owned staging buffer survives
+        this process, so the step is recoverable from then on)."""
         n = hi - lo
         if self._use_ring(n):
             return self._save_slice_ring(layout, shm_payload_addr, lo, hi, on_done, sync)
@@ -530,6 +534,9 @@ class GpuCopier:
         # for the whole PCIe transfer and stall the training thread's launches.
         def flush():
             if n > 0:
+                if on_snapshot is not None:
+                    _check(_kern().dw_event_sync(ctypes.c_void_p(ev.cuda_event)), "snapshot sync")
+                    on_snapshot()
                 if prep is not None:
                     prep.wait(shm_payload_addr + lo, n)  # this range's prefault + registration
                 # registering here (flush thread), not in the training pause:

@@ -439,6 +439,12 @@ class CheckpointEngine(ABC):
             stage["idx"] = idx
             h.set_hbm_stamp(self._slice_idx, idx, 0)
 
+        def on_snapshot():
+            if "idx" in stage:
+                # the (standby-owned) staging buffer holds the whole slice of
+                # ``step``: recoverable even if this process dies mid-flush
+                h.set_hbm_stamp(self._slice_idx, stage["idx"], step, copier.stage_owner(stage["idx"]), hi - lo)
+
         def on_done():
             h.set_slice_step(slot, self._slice_idx, step)
             if "idx" in stage:
@@ -450,7 +456,8 @@ class CheckpointEngine(ABC):
 
         has_gpu = any(e.device == "cuda" for e in layout.extents)
         if has_gpu and copier is not None:
-            copier.save_slice(layout, h.payload_addr(slot), lo, hi, on_done, before_copy=before_copy)
+            copier.save_slice(layout, h.payload_addr(slot), lo, hi, on_done, before_copy=before_copy,
+                              on_snapshot=on_snapshot)
         else:
             self._cpu_save_slice(layout, h.payload_addr(slot), lo, hi)
             on_done()
@@ -552,24 +559,61 @@ class CheckpointEngine(ABC):
         self._wait_own_lock_release()
 
     # ----------------------------------------------------------- core load
+    def _hbm_only_steps(self) -> Dict[int, int]:
+        """{step: shm slot holding its metadata} of snapshots whose slice of
+        this rank sits complete in an HBM-tier buffer this process owns while
+        their shm flush never finished (the previous worker died mid-flush).
+        GPU bytes come from HBM; metadata and CPU tensors were written to the
+        slot synchronously at save time."""
+        from . import hbm_tier
+
+        if not hbm_tier.OWNED or os.environ.get("DWAMD_HBM_TIER", "1") != "1":
+            return {}
+        if self._replicated and self._num_slices > 1 and self._gather_group is None:
+            return {}  # that restore path reads every slice from shm
+        h = self._shm_handler
+        if h.shared_memory is None and not h.init_shared_memory(create=False):
+            return {}
+        complete = h.complete_steps()
+        out = {}
+        for b in range(min(2, len(hbm_tier.OWNED))):
+            st, pid, _nb = h.hbm_stamp(self._slice_idx, b)
+            if st <= 0 or pid != os.getpid() or st in complete:
+                continue
+            for s in range(h.num_slots):
+                cfg = h.get_meta(s).get(DLROVER_CKPT_CONFIG_KEY)
+                if cfg is not None and cfg.step == st and cfg.num_slices == self._num_slices:
+                    out[st] = s
+        return out
+
     def get_state_dict_from_memory(self, target: Any = None):
         """Returns (step, state_dict) from shm, or (0, {})."""
         self._restore_memory_from_replica()
         h = self._shm_handler
         holds = self._replicated or self._local_rank == self.local_shard_id
-        step = agree_on_step(self._ctl_group, list(h.complete_steps()) if holds else None)
-        slot = h.slot_of(step) if (step > 0 and holds) else -1
+        complete = h.complete_steps() if holds else {}
+        # a snapshot still in (standby-owned) HBM when the last worker died
+        # counts too -- only for an in-place GPU restore
+        hbm_only = self._hbm_only_steps() if (holds and target is not None) else {}
+        cands = dict(hbm_only)
+        cands.update(complete)
+        step = agree_on_step(self._ctl_group, list(cands) if holds else None)
+        slot = cands.get(step, -1) if (step > 0 and holds) else -1
         if step <= 0 or not check_all_rank_ready(self._ctl_group, slot >= 0 or not holds):
             return 0, {}
         if not holds:
             return 0, {}
+        from_hbm_only = step not in complete
         logger.info(f"rank {self._rank}: restoring step {step} from memory slot {slot} "
-                    f"(complete in memory: {sorted(h.complete_steps())})")
+                    f"(complete in memory: {sorted(complete)}"
+                    f"{', in HBM only: ' + str(sorted(hbm_only)) if hbm_only else ''})")
         tree = h.get_meta(slot)["tree"]
         if target is not None:
-            sd = self._restore_into(tree, target, slot, step)
+            sd = self._restore_into(tree, target, slot, step, require_hbm=from_hbm_only)
             if sd is not None:
                 return step, sd
+        if from_hbm_only:
+            return 0, {}  # never serve an incomplete shm slot
         sd = h.load_state_dict(slot)
         if isinstance(sd, dict):
             sd.pop(DLROVER_CKPT_CONFIG_KEY, None)
@@ -589,12 +633,19 @@ class CheckpointEngine(ABC):
                 return buf.ptr
         return None
 
-    def _restore_into(self, tree, target, slot: int, step: int = 0):
+    def _restore_into(self, tree, target, slot: int, step: int = 0, require_hbm: bool = False):
         """Fast path: H2D (sliced + all-gather for replicated) straight into
-        the live tensors of ``target`` (same structure as the saved dict)."""
+        the live tensors of ``target`` (same structure as the saved dict).
+        ``require_hbm``: the shm slot is incomplete -- every rank must copy
+        its slice from its HBM-tier buffer."""
         from .copier import match_targets
 
         pairs, ok = match_targets(tree, target)
+        if require_hbm:
+            total = self._shm_handler.payload_size
+            s_lo, s_hi = split_ranges(total, self._num_slices)[self._slice_idx]
+            ok = ok and self._hbm_source(step, s_lo, s_hi) is not None and any(
+                t.is_cuda for _m, t in pairs)
         ok_all = check_all_rank_ready(self._ctl_group, ok)
         if not ok_all:
             return None

@@ -14,7 +14,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_bench_two_ranks_real_kill(tmp_path):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--model", "gpt2-tiny", "--micro-batch",
-           "2", "--seq", "64", "--steps", "8", "--warmup", "2", "--ckpt-dir", str(tmp_path / "ckpt"), "--timeout",
+           "2", "--seq", "64", "--steps", "8", "--warmup", "2", "--fault-window", "16", "--ckpt-dir", str(tmp_path / "ckpt"), "--timeout",
            "240"]
     r = subprocess.run(cmd, env=env, cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                        timeout=300)
