@@ -8,9 +8,10 @@ Token path (per MoE layer):
   3. expert parallel: the buffer is exchanged with ONE variable-split
      ``all_to_all_single`` over the EP group (RCCL; the per-expert counts go
      first in a tiny all_to_all) and regrouped by local expert;
-  4. the local experts run as a grouped GEMM over the contiguous groups
-     (``grouped_mlp``: per-expert hipBLASLt GEMMs on views of one buffer --
-     no padding, no capacity drop);
+  4. the local experts run as grouped GEMMs over the contiguous groups
+     (``grouped_mlp`` -> ``ops.grouped_gemm``: one MFMA launch per projection
+     for all experts, group offsets on the device -- no host sync, no
+     padding, no capacity drop);
   5. the inverse exchange + un-permute + weighted sum over k.
 
 MI355X sizing: with 288 GB per GPU experts can stay resident at high EP
@@ -79,10 +80,35 @@ class TopKGate(nn.Module):
         return w, idx, aux + z
 
 
-def grouped_mlp(x: torch.Tensor, counts: List[int], w1: torch.Tensor, w2: torch.Tensor,
+def grouped_mlp(x: torch.Tensor, counts, w1: torch.Tensor, w2: torch.Tensor,
                 w3: Optional[torch.Tensor] = None, activation: str = "silu") -> torch.Tensor:
     """Expert FFN over contiguous groups: rows [off_e, off_e + counts[e]) go
-    through expert e.  w1/w3 [E, F, H] (w3: SwiGLU gate), w2 [E, H, F]."""
+    through expert e.  w1/w3 [E, F, H] (w3: SwiGLU gate), w2 [E, H, F].
+    ``counts``: per-expert row counts (device tensor or host list).  On a GPU
+    every projection is ONE grouped-GEMM launch over all experts with the
+    offsets on the device (no host sync); on the CPU a per-expert loop."""
+    from ..ops import _hip
+
+    E = w1.shape[0]
+    # Few large experts (Mixtral-style, >= 2048 rows each): hipBLASLt's tuned
+    # per-expert GEMMs beat the grouped kernel 1.8x and the one host read of
+    # the counts is noise next to ms-long GEMMs.  Many small experts
+    # (fine-grained MoE): the grouped kernel wins 2.5-10x
+    # (profiles/r2/grouped_gemm_bench.jsonl).
+    few_large = E <= 16 and x.shape[0] >= 2048 * E
+    if _hip.use_hip(x) and x.dtype == torch.bfloat16 and not few_large:
+        from ..ops.grouped_gemm import grouped_linear, offsets_from_counts
+
+        offs = offsets_from_counts(counts, x.device)
+        h = grouped_linear(x, w1, offs)
+        if w3 is not None:
+            h = F.silu(h) * grouped_linear(x, w3, offs) if activation == "silu" else F.gelu(h) * grouped_linear(
+                x, w3, offs)
+        else:
+            h = F.silu(h) if activation == "silu" else F.gelu(h)
+        return grouped_linear(h, w2, offs)
+    if torch.is_tensor(counts):
+        counts = counts.tolist()
     outs = []
     off = 0
     act = F.silu if activation == "silu" else F.gelu
@@ -163,7 +189,7 @@ class MoELayer(nn.Module):
             inv[perm] = torch.arange(perm.numel(), device=x.device)
             y = all_to_all_v(y.index_select(0, inv), in_splits, out_splits, self.ep_group)
         else:
-            y = self.experts(xs, counts.tolist())
+            y = self.experts(xs, counts)  # device counts: no host sync on the GPU path
         # un-permute and combine the k expert outputs per token
         out = torch.zeros(T * k, y.shape[-1], dtype=y.dtype, device=y.device)
         out = out.index_copy(0, order, y)
