@@ -153,6 +153,7 @@ def _apply_parallel_mode(ctx, cfg):
     if adist.parallel_config() is None:
         adist.create_parallel_group(config)
     ctx["dp_group"] = adist.parallel_group("data")
+    ctx["zero_group"] = adist.parallel_group("zero")
     ctx["tp_group"] = adist.parallel_group("tensor")
     ctx["sp_group"] = adist.parallel_group("sequence")
 
@@ -309,6 +310,31 @@ def _apply_pipeline_parallel(ctx, cfg):
                 f"layers {[(c.start, c.end) for c in pipe.chunks]} schedule {pipe.schedule_name}")
 
 
+def _hsdp_mesh(ctx):
+    """Hybrid sharding (HSDP): with ``parallel_mode`` groups ("zero", z) and
+    ("data", d), both > 1, parameters are sharded inside each zero group and
+    replicated across the data groups -- a 2-D FSDP2 mesh
+    (replicate = data, shard = zero): reduce-scatter within a node's xGMI
+    group, all-reduce of the shards across nodes.  Parity: ATorch
+    zero_optimization.py:377-394 (FSDP HYBRID_SHARD)."""
+    zg, dpg = ctx.get("zero_group"), ctx.get("dp_group")
+    if zg is None or dpg is None or dist.get_world_size(zg) <= 1 or dist.get_world_size(dpg) <= 1:
+        return None
+    if dist.get_world_size(zg) * dist.get_world_size(dpg) != dist.get_world_size():
+        raise ValueError("HSDP needs zero x data == world size (no other parallel dimensions)")
+    from torch.distributed.device_mesh import DeviceMesh
+
+    rows = sorted(sorted(r) for _g, r in adist._DistributedContext.PARALLEL_GROUPS_AND_RANKS["zero"])
+    data_groups = {tuple(sorted(r)) for _g, r in adist._DistributedContext.PARALLEL_GROUPS_AND_RANKS["data"]}
+    cols = {tuple(sorted(row[j] for row in rows)) for j in range(len(rows[0]))}
+    if cols != data_groups:
+        raise ValueError(f"zero groups {rows} and data groups {sorted(data_groups)} do not form a 2-D grid")
+    mesh = DeviceMesh("cuda" if torch.cuda.is_available() else "cpu", torch.tensor(rows),
+                      mesh_dim_names=("replicate", "shard"))
+    logger.info(f"fsdp: hybrid sharding over a {len(rows)} x {len(rows[0])} (replicate x shard) mesh")
+    return mesh
+
+
 def _apply_fsdp(ctx, cfg, reshard=True):
     from torch.distributed.fsdp import MixedPrecisionPolicy, fully_shard
 
@@ -317,9 +343,9 @@ def _apply_fsdp(ctx, cfg, reshard=True):
     classes = _wrap_cls(ctx, cfg)
     dtype = ctx.get("amp_dtype")
     mp = MixedPrecisionPolicy(param_dtype=dtype, reduce_dtype=torch.float32) if dtype else MixedPrecisionPolicy()
-    mesh = None
+    mesh = _hsdp_mesh(ctx)
     dpg = ctx.get("dp_group")
-    if dpg is not None and dist.get_world_size(dpg) != dist.get_world_size():
+    if mesh is None and dpg is not None and dist.get_world_size(dpg) != dist.get_world_size():
         from torch.distributed.device_mesh import DeviceMesh
 
         _g, ranks = adist.parallel_group_and_ranks("data")
@@ -453,6 +479,11 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
             (dist.get_world_size() if dist.is_initialized() else 1)
         dp_rank = dist.get_rank(dpg) if (dist.is_initialized() and dpg is not None) else \
             (dist.get_rank() if dist.is_initialized() else 0)
+        zg = ctx.get("zero_group")
+        if zg is not None and dist.get_world_size(zg) > 1:
+            # zero (sharding) ranks are data parallel too: each reads its own batch
+            dp_rank = dp_rank * dist.get_world_size(zg) + dist.get_rank(zg)
+            dp_size = dp_size * dist.get_world_size(zg)
         if dp_size > 1:
             bs = dl_args.get("batch_size", 1)
             dl_args["batch_size"] = max(1, bs // dp_size)  # batch_size is the global batch

@@ -209,3 +209,52 @@ def test_two_rank_llama_fsdp_with_activation_checkpointing():
     for p in ps:
         p.join(timeout=30)
     assert [r[1] for r in res] == [True, True], res
+
+
+def _hsdp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    from dlrover_wuqiong_amd.atorch import distributed as adist
+
+    try:
+        from torch.distributed.tensor import Replicate, Shard
+
+        from dlrover_wuqiong_amd.atorch.auto_accelerate import auto_accelerate
+
+        adist.init_distributed("gloo")
+        torch.manual_seed(0)
+        ok, res, strat = auto_accelerate(
+            Toy(), torch.optim.AdamW, dataset=DS(), loss_func=loss_func, optim_args={"lr": 1e-2},
+            dataloader_args={"batch_size": 8},
+            load_strategy=[("parallel_mode", ([("zero", 2), ("data", 2)], None)), ("fsdp", {"wrap_cls": (Block,)})])
+        p = next(res.model.parameters())
+        placements_ok = tuple(p.placements) == (Replicate(), Shard(0)) and p.device_mesh.ndim == 2
+        losses = _train(res, 5)
+        sums = torch.tensor([float(sum(v.full_tensor().double().sum() for v in res.model.state_dict().values()))],
+                            dtype=torch.float64)
+        allsums = [torch.zeros_like(sums) for _ in range(world)]
+        dist.all_gather(allsums, sums)
+        same = all(torch.equal(s, allsums[0]) for s in allsums)
+        q.put((rank, bool(ok and placements_ok and same and losses[-1] < losses[0] and len(res.dataloader) == 4)))
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        traceback.print_exc()
+        q.put((rank, repr(e)))
+    finally:
+        adist.reset_distributed()
+
+
+def test_four_rank_hsdp():
+    """("zero", 2) x ("data", 2): shard within zero groups, replicate across
+    data groups (FSDP2 2-D mesh); every rank reads its own quarter of the batch."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_hsdp_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in ps), key=lambda x: x[0])
+    for p in ps:
+        p.join(timeout=30)
+    assert [r[1] for r in res] == [True] * 4, res
