@@ -59,6 +59,7 @@ class JobExitReason:
     WORKER_ERROR = "WorkerError"
     HANG_ERROR = "HangError"
     RDZV_TIMEOUT_ERROR = "RdzvTimeout"
+    PENDING_TIMEOUT = "PendingTimeout"
     UNKNOWN_ERROR = "UnknownError"
 
 
@@ -173,3 +174,16 @@ class CommBackend:
 
     RCCL = "nccl"
     GLOO = "gloo"
+
+
+class NodeResourceLimit:
+    """Bounds for automatic resource adjustment (reference constants.py:131).
+    Memory in MiB.  MI355X hosts carry far more RAM than the reference's CPU
+    pods: the OOM bump ceiling is sized for a GPU node's host memory."""
+
+    MAX_CPU_CORES = 256
+    MIN_CPU_CORES = 4
+    MIN_MEMORY = 6144
+    MAX_MEMORY = 2 * 1024 * 1024  # 2 TiB
+    INCREMENTAL_MEMORY_FACTOR = 2
+    MAX_INCREMENTAL_MEMORY = 256 * 1024  # one OOM relaunch adds at most 256 GiB

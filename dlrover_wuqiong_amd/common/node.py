@@ -82,6 +82,8 @@ class Node:
     paral_config: object = None
     restart_training: bool = False
     reported_failures: List[Tuple[str, str]] = field(default_factory=list)
+    is_recovered_oom: bool = False  # relaunched with more memory after an OOM kill
+    create_time: float = field(default_factory=time.time)
 
     def update_status(self, status: str) -> bool:
         from ..master.job_manager import get_node_state_flow
@@ -122,6 +124,7 @@ class Node:
         n.exit_reason = ""
         n.is_released = False
         n.reported_failures = []
+        n.create_time = time.time()
         return n
 
 

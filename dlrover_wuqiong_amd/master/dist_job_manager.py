@@ -16,8 +16,8 @@ import threading
 import time
 from typing import Dict, List, Optional
 
-from ..common.constants import (DistributionStrategy, JobConstant, NodeExitReason, NodeStatus, NodeType,
-                                TrainingExceptionLevel)
+from ..common.constants import (DistributionStrategy, JobConstant, NodeExitReason, NodeResourceLimit, NodeStatus,
+                                NodeType, TrainingExceptionLevel)
 from ..common.log import logger
 from ..common.node import JobResource, Node
 from .autoscale import new_job_auto_scaler
@@ -156,7 +156,48 @@ class DistributedJobManager(JobManager):
         if n.relaunch_count >= n.max_relaunch_count:
             logger.warning(f"{n.name} reached max relaunch count {n.max_relaunch_count}")
             return False
+        if reason == NodeExitReason.OOM:
+            mem = n.config_resource.memory
+            if mem >= NodeResourceLimit.MAX_MEMORY:
+                logger.warning(f"{n.name} was OOM-killed at {mem} MiB >= the {NodeResourceLimit.MAX_MEMORY} MiB "
+                               "limit: not relaunching")
+                return False
+            n.is_recovered_oom = True
+            self.adjust_oom_resource(n)
         return n.relaunchable
+
+    @staticmethod
+    def adjust_oom_resource(n: Node):
+        """More host memory for the relaunch of an OOM-killed node: x factor,
+        at most +MAX_INCREMENTAL_MEMORY, capped at MAX_MEMORY (reference
+        dist_job_manager.py:561-580 + the job optimizer's adjust_oom_resource)."""
+        mem = max(n.config_resource.memory, NodeResourceLimit.MIN_MEMORY)
+        new = min(mem * NodeResourceLimit.INCREMENTAL_MEMORY_FACTOR, mem + NodeResourceLimit.MAX_INCREMENTAL_MEMORY,
+                  NodeResourceLimit.MAX_MEMORY)
+        logger.info(f"{n.name} OOM: memory {n.config_resource.memory} -> {new} MiB for the relaunch")
+        n.config_resource.memory = int(new)
+
+    def pending_timeout_nodes(self, timeout: Optional[float] = None) -> List[Node]:
+        """Nodes stuck in PENDING longer than ``seconds_to_wait_pending_pod``
+        (no schedulable GPU node): the master fails the job instead of
+        waiting forever (reference ``_process_insufficient_node`` /
+        pending-pod checks)."""
+        from ..common.global_context import Context
+
+        timeout = Context.singleton_instance().seconds_to_wait_pending_pod if timeout is None else timeout
+        now = time.time()
+        out = []
+        for ns in self.job_nodes.values():
+            for n in ns.values():
+                if n.status == NodeStatus.PENDING and not n.is_released and now - n.create_time > timeout:
+                    out.append(n)
+        return out
+
+    def is_job_pending_too_long(self, timeout: Optional[float] = None) -> bool:
+        stuck = self.pending_timeout_nodes(timeout)
+        if stuck:
+            logger.error(f"nodes pending beyond the timeout: {[n.name for n in stuck]}")
+        return bool(stuck)
 
     def _relaunch_node(self, node: Node):
         mgr = self._managers.get(node.type, self.worker_manager)

@@ -63,6 +63,11 @@ class JobMaster:
             if self.diagnosis.check_training_hang():
                 logger.error("training hang detected (no global step progress)")
                 self.exit_reason = JobExitReason.HANG_ERROR
+            pending_check = getattr(self.job_manager, "is_job_pending_too_long", None)
+            if pending_check is not None and pending_check():
+                self.exit_reason = JobExitReason.PENDING_TIMEOUT
+                self.metric_collector.collect_job_exit_reason(self.exit_reason)
+                return 1
             if self.job_manager.all_workers_exited():
                 if self.job_manager.all_workers_failed():
                     self.exit_reason = JobExitReason.WORKER_ERROR
@@ -138,6 +143,11 @@ class DistributedJobMaster(JobMaster):
             if self.diagnosis.check_training_hang():
                 logger.error("training hang detected (no global step progress)")
                 self.exit_reason = JobExitReason.HANG_ERROR
+            pending_check = getattr(self.job_manager, "is_job_pending_too_long", None)
+            if pending_check is not None and pending_check():
+                self.exit_reason = JobExitReason.PENDING_TIMEOUT
+                self.metric_collector.collect_job_exit_reason(self.exit_reason)
+                return 1
             if self.job_manager.all_workers_exited():
                 ok = self.job_manager.all_workers_succeeded()
                 self.exit_reason = JobExitReason.SUCCEEDED if ok else JobExitReason.WORKER_ERROR
