@@ -700,6 +700,7 @@ class CheckpointEngine(ABC):
 
     def close(self):
         try:
+            self._replica_manager.close()
             if self._shm_prep is not None:
                 self._shm_prep.result()
             if self._prep_pool is not None:
