@@ -414,6 +414,42 @@ class DeepSpeedCheckpointSaver(CommonDirCheckpointSaver):
         self.storage.write(tag, os.path.join(self.checkpoint_dir, self.TRACER_FILE))
 
 
+class FsdpFlatCheckpointSaver(TempDirCheckpointSaver):
+    """ATorch flat FSDP layout (atorch/fsdp_flat_ckpt.py): tensor categories
+    as safetensors streamed from shm, metadata as JSON, staged then moved
+    into place; tracker ``latest_checkpointed_iteration.txt``.  Parity:
+    reference atorch/atorch/utils/fsdp_async_ckpt_util.py:29-67."""
+
+    TRACER_FILE = "latest_checkpointed_iteration.txt"
+
+    def persist_to_storage(self, shard_id, cfg, slot):
+        import json
+
+        from ..atorch.fsdp_flat_ckpt import BUFFERS, CKPT_META, OPTIM_STATES, PARAM_GROUPS, PARAM_META, PARAMS
+        from ..atorch.fsdp_flat_ckpt import safetensors_dump
+
+        h = self._shm_handlers[shard_id]
+        sd = h.load_state_dict(slot)
+        sd.pop(DLROVER_CKPT_CONFIG_KEY, None)
+        stage = os.path.join(self.checkpoint_dir, self._STAGE_DIR, str(cfg.step))
+        for name, path in (cfg.paths or {}).items():
+            if name not in sd:
+                continue
+            dst = os.path.join(stage, os.path.relpath(path, self.checkpoint_dir))
+            if name in (PARAMS, OPTIM_STATES, BUFFERS):
+                safetensors_dump(sd[name], dst)
+            elif name in (PARAM_META, PARAM_GROUPS, CKPT_META):
+                os.makedirs(os.path.dirname(dst), exist_ok=True)
+                with open(dst, "w") as f:
+                    json.dump(sd[name], f)
+            else:
+                self.storage.write_state_dict(sd[name], dst, _writer_for(path))
+
+    def update_tracker_file(self, step):
+        super().update_tracker_file(step)
+        self.storage.write(str(step), os.path.join(self.checkpoint_dir, self.TRACER_FILE))
+
+
 class FsdpDcpSaver(CommonDirCheckpointSaver):
     """Writes torch.distributed.checkpoint-compatible ``.distcp`` shards +
     ``.metadata`` (see flash_checkpoint/fsdp.py for the layout)."""
