@@ -31,6 +31,9 @@ Optimizations (applied in a fixed, dependency-respecting order):
 
 ``load_strategy="search"`` (with ``model_fn=`` and ``sample_batch=``) dry-runs
 candidate strategies and keeps the fastest (``atorch/auto_search.py``).
+``load_strategy="engine"`` runs the acceleration-engine service
+(``atorch/engine/``): rank 0 serves a planner/executor, every rank runs the
+analyse / tune / dry-run tasks it hands out, and the fastest strategy wins.
 ``load_strategy=None`` plans semi-automatically from the model size and the
 GPU memory (288 GB per MI355X): DDP when weights + grads + Adam states fit in
 ~70 % of HBM, otherwise FSDP; bf16 autocast always.  (The reference searches
@@ -419,7 +422,24 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
                                                 kwargs["sample_batch"], loss_func,
                                                 max_trials=kwargs.get("max_trials"),
                                                 model_input_format=model_input_format)
-    strategy = Strategy.from_spec(load_strategy) if load_strategy is not None else plan_strategy(model, world)
+    elif isinstance(load_strategy, str) and load_strategy == "engine":
+        # acceleration-engine service (atorch/engine/): analyse, tune and dry
+        # run candidate strategies across all ranks, keep the fastest
+        from .engine.worker import search as engine_search
+
+        sample = kwargs.get("sample_batch")
+        if sample is None and dataset is not None:
+            bs = max(1, (dataloader_args or {}).get("batch_size", 1) // max(1, world))
+            sample = next(iter(torch.utils.data.DataLoader(dataset, batch_size=bs)))
+        load_strategy = engine_search(model, optim_func, optim_args, loss_func, sample,
+                                      model_fn=kwargs.get("model_fn"), model_input_format=model_input_format,
+                                      included=included, excluded=excluded, time_limit=kwargs.get("time_limit"),
+                                      load_strategy=kwargs.get("engine_load_strategy"),
+                                      verbose=kwargs.get("verbose", False),
+                                      warmup=int(os.getenv("DWAMD_DRYRUN_WARMUP", "2")),
+                                      steps=int(os.getenv("DWAMD_DRYRUN_STEPS", "3")))
+        included = excluded = None  # already applied by the engine's planner
+    strategy =Strategy.from_spec(load_strategy) if load_strategy is not None else plan_strategy(model, world)
     if excluded:
         strategy = Strategy([o for o in strategy.opts if o[0] not in excluded])
     if included:

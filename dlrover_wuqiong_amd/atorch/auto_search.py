@@ -80,7 +80,7 @@ class DryRunner:
     @staticmethod
     def profile(model_fn: Callable[[], nn.Module], strategy: List[Any], optim_func, optim_args: Dict,
                 sample_batch, loss_func: Callable, warmup: int = 2, steps: int = 3,
-                model_input_format: Optional[str] = None) -> DryRunResult:
+                model_input_format: Optional[str] = None, keep_groups: bool = False) -> DryRunResult:
         from .auto_accelerate import auto_accelerate
 
         dev_cuda = torch.cuda.is_available()
@@ -119,7 +119,7 @@ class DryRunner:
             if dev_cuda:
                 torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / steps
-            dp = dist.get_world_size() if dist.is_initialized() else 1
+            dp = _data_parallel_size()
             mem = torch.cuda.max_memory_allocated() if dev_cuda else 0
             del model, opt, res
             return DryRunResult(strategy, True, throughput=bs * dp / dt, step_time=dt, max_memory_bytes=mem)
@@ -129,9 +129,27 @@ class DryRunner:
         finally:
             from . import distributed as adist
 
-            # each candidate re-creates its parallel groups
-            if adist.parallel_config() is not None:
+            # each candidate re-creates its parallel groups (the engine
+            # keeps them across dry runs sharing a parallel mode)
+            if not keep_groups and adist.parallel_config() is not None:
                 adist.destroy_parallel_group()
+
+
+def _data_parallel_size() -> int:
+    """Ranks reading distinct batches: data x zero groups (tensor /
+    pipeline ranks of one replica share a batch)."""
+    from . import distributed as adist
+
+    if not dist.is_initialized():
+        return 1
+    if adist.parallel_config() is None:
+        return dist.get_world_size()
+    n = 1
+    for name in ("data", "zero"):
+        g = adist.parallel_group(name)
+        if g is not None:
+            n *= dist.get_world_size(g)
+    return n
 
 
 def candidate_strategies(world: int, include_fsdp: bool = True) -> List[List[Any]]:
