@@ -217,3 +217,10 @@ def test_two_rank_auto_accelerate_engine():
         p.join(timeout=30)
     assert all(r[1] is True for r in res), res
     assert res[0][2] == res[1][2] and "parallel_mode" in res[0][2]
+
+
+def test_reference_import_paths():
+    from atorch.auto.engine.acceleration_engine import AccelerationEngine as A
+    from atorch.auto.engine_client import EngineClient as C
+
+    assert A is AccelerationEngine and C is EngineClient
