@@ -470,9 +470,18 @@ class GpuCopier:
         once the snapshot sits complete in the staging buffer, before its
         PCIe flush (HBM-tier stamp: a standby-owned staging buffer survives
         this process, so the step is recoverable from then on)."""
-        n = hi - lo
-        if self._use_ring(n):
+        if self._use_ring(hi - lo):
             return self._save_slice_ring(layout, shm_payload_addr, lo, hi, on_done, sync)
+        snap = self.snapshot(layout, lo, hi, before_copy)
+        self.flush_snapshot(snap, shm_payload_addr, on_done, sync=sync, on_snapshot=on_snapshot)
+
+    def snapshot(self, layout: Layout, lo: int, hi: int,
+                 before_copy: Optional[Callable[[int], None]] = None) -> dict:
+        """Enqueue the HBM->staging copy of payload bytes [lo, hi) (full
+        staging mode) and return a handle for :meth:`flush_snapshot`.  The
+        shm slot is not needed yet: the engine enqueues this first and picks /
+        stamps the slot (gloo vote, metadata pickling) while the copy runs."""
+        n = hi - lo
         self.last_snapshot_mode = "full"
         self._refresh_external(n)
         self._decide_buffers(n)
@@ -517,17 +526,27 @@ class GpuCopier:
             if descs[1] is not None:
                 copy_stream.wait_stream(cur)  # the "now" part is ordered before the flush too
                 launch_multi_copy(descs[1], copy_stream)
-            # CPU tensors go straight to shm (small: counters, rng state...)
-            for e, a, b in intersect_extents(layout.cpu_extents(), lo, hi):
-                runtime().dw_memcpy_parallel(ctypes.c_void_p(shm_payload_addr + a),
-                                             ctypes.c_void_p(e.src_ptr + (a - e.offset)), b - a, 4)
-        prep = self.pending_prep
-        t_enq = time.perf_counter()
         ev = torch.cuda.Event()
         ev.record(copy_stream)
         if copy_stream is not cur:
             self._fence_ev = ev
             _FENCED.add(self)
+        return {"layout": layout, "lo": lo, "hi": hi, "idx": idx, "stg": stg, "ev": ev,
+                "t_enq": time.perf_counter()}
+
+    def flush_snapshot(self, snap: dict, shm_payload_addr: int, on_done: Callable[[], None], sync: bool = False,
+                       on_snapshot: Optional[Callable[[], None]] = None):
+        """Copy the CPU extents into the shm slot now and queue the PCIe flush
+        of the staged bytes behind the snapshot's event."""
+        layout, lo, hi, idx, stg, ev = (snap[k] for k in ("layout", "lo", "hi", "idx", "stg", "ev"))
+        n = hi - lo
+        t_enq = snap["t_enq"]
+        if n > 0:
+            # CPU tensors go straight to shm (small: counters, rng state...)
+            for e, a, b in intersect_extents(layout.cpu_extents(), lo, hi):
+                runtime().dw_memcpy_parallel(ctypes.c_void_p(shm_payload_addr + a),
+                                             ctypes.c_void_p(e.src_ptr + (a - e.offset)), b - a, 4)
+        prep = self.pending_prep
 
         # NOTE: every host-side wait in this thread goes through ctypes (which
         # drops the GIL); torch's Stream/Event.synchronize would hold the GIL

@@ -407,6 +407,24 @@ class CheckpointEngine(ABC):
         if marks is not None:
             marks.append(("plan+shm", time.perf_counter()))
         h = self._shm_handler
+        lo, hi = split_ranges(layout.total_bytes, self._num_slices)[self._slice_idx]
+        step = conf.step
+        stage = {}
+
+        def before_copy(idx: int):
+            # HBM tier: this staging buffer is about to be overwritten
+            stage["idx"] = idx
+            h.set_hbm_stamp(self._slice_idx, idx, 0)
+
+        has_gpu = any(e.device == "cuda" for e in layout.extents)
+        snap = None
+        if has_gpu and copier is not None and bool(state_dict) and not copier._use_ring(hi - lo):
+            # the HBM->staging copy needs no shm slot: enqueue it first, so the
+            # slot vote (a gloo collective) and the metadata pickling below run
+            # on the host while the GPU copies
+            snap = copier.snapshot(layout, lo, hi, before_copy)
+            if marks is not None:
+                marks.append(("enqueue", time.perf_counter()))
         if self._next_slot is None:
             # first save of this process (nothing in flight): never the latest complete slot
             self._next_slot = h.write_slot()
@@ -429,15 +447,6 @@ class CheckpointEngine(ABC):
         h.set_slice_step(slot, self._slice_idx, 0)  # slot reads incomplete before any byte changes
         if self._is_shard_owner:
             h.set_metadata(slot, layout.meta_tree, conf)
-        lo, hi = split_ranges(layout.total_bytes, self._num_slices)[self._slice_idx]
-        step = conf.step
-
-        stage = {}
-
-        def before_copy(idx: int):
-            # HBM tier: this staging buffer is about to be overwritten
-            stage["idx"] = idx
-            h.set_hbm_stamp(self._slice_idx, idx, 0)
 
         def on_snapshot():
             if "idx" in stage:
@@ -454,8 +463,9 @@ class CheckpointEngine(ABC):
             if self._is_shard_owner:
                 self._release_when_complete(step, slot)
 
-        has_gpu = any(e.device == "cuda" for e in layout.extents)
-        if has_gpu and copier is not None:
+        if snap is not None:
+            copier.flush_snapshot(snap, h.payload_addr(slot), on_done, on_snapshot=on_snapshot)
+        elif has_gpu and copier is not None:
             copier.save_slice(layout, h.payload_addr(slot), lo, hi, on_done, before_copy=before_copy,
                               on_snapshot=on_snapshot)
         else:

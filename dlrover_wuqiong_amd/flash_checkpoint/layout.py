@@ -121,29 +121,80 @@ class LayoutCache:
         self._metas: List[TensorMeta] = []
 
     def plan(self, state_dict: Any) -> Tuple[Layout, List[torch.Tensor]]:
-        tensors: List[torch.Tensor] = []
+        if self._layout is not None:
+            try:
+                tree, tensors = self._hit(state_dict)
+                lay = self._layout
+                return Layout(meta_tree=tree, extents=lay.extents, total_bytes=lay.total_bytes,
+                              signature=lay.signature), tensors
+            except _Miss:
+                pass
         key: List[Tuple] = []
 
         def collect(v):
             if torch.is_tensor(v):
                 key.append((v.data_ptr(), v.numel(), v.dtype, v.is_contiguous()))
-                tensors.append(v)
             return v
 
         traverse(state_dict, collect)
-        key_t = tuple(key)
-        all_contig = all(k[3] for k in key)  # temporaries of non-contiguous leaves are never cached
-        if all_contig and key_t == self._key and self._layout is not None:
-            it = iter(self._metas)
-            tree = traverse(state_dict, lambda v: next(it) if torch.is_tensor(v) else v)
-            lay = self._layout
-            return Layout(meta_tree=tree, extents=lay.extents, total_bytes=lay.total_bytes,
-                          signature=lay.signature), tensors
         layout, tens = plan_layout(state_dict)
-        self._key = key_t
-        self._layout = layout
+        # temporaries of non-contiguous leaves are never reused
+        all_contig = all(k[3] for k in key)
+        self._key = key if all_contig else None
+        self._layout = layout if all_contig else None
         self._metas = [m for m in iter_leaves(layout.meta_tree) if isinstance(m, TensorMeta)]
         return layout, tens
+
+    def _hit(self, state_dict: Any):
+        """One pass over ``state_dict``: verify every tensor leaf against the
+        cached key and rebuild the meta tree (same shape rules as
+        :func:`traverse`).  Raises ``_Miss`` on the first mismatch.  Lists of
+        plain scalars (optimizer ``param_groups[...]["params"]``) are copied
+        without per-element recursion -- a state dict of a few thousand
+        tensors is re-planned in about a millisecond."""
+        key, metas = self._key, self._metas
+        n = len(key)
+        tensors: List[torch.Tensor] = []
+        T = torch.Tensor
+
+        def rec(v):
+            tv = type(v)
+            if tv is dict or isinstance(v, dict):
+                items = [(k, rec(x)) for k, x in v.items()]
+                if tv is dict:
+                    return dict(items)
+                try:
+                    return tv(items)
+                except Exception:
+                    return dict(items)
+            if tv is list or isinstance(v, list):
+                if all(type(x) in _SCALARS for x in v):
+                    return list(v)
+                return [rec(x) for x in v]
+            if isinstance(v, tuple) and not hasattr(v, "_fields"):
+                return tuple(rec(x) for x in v)
+            if isinstance(v, T):
+                i = len(tensors)
+                if i >= n:
+                    raise _Miss
+                k = key[i]
+                if v.data_ptr() != k[0] or v.numel() != k[1] or v.dtype != k[2] or not v.is_contiguous():
+                    raise _Miss
+                tensors.append(v)
+                return metas[i]
+            return v
+
+        tree = rec(state_dict)
+        if len(tensors) != n:
+            raise _Miss
+        return tree, tensors
+
+
+_SCALARS = frozenset((int, float, str, bool, type(None)))
+
+
+class _Miss(Exception):
+    pass
 
 
 def plan_layout(state_dict: Any) -> Tuple[Layout, List[torch.Tensor]]:

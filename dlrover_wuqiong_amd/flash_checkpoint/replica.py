@@ -262,7 +262,7 @@ class CkptReplicaManager:
                     dist.recv(_u8(handler.shared_memory.buf, off + lo, off + min(n, lo + self.chunk)), donor,
                               group=self._group)
                 cfg = meta[DLROVER_CKPT_CONFIG_KEY]
-                handler.metas[0].set(meta)
+                handler.set_meta_dict(0, meta)
                 for r in range(cfg.num_slices):
                     handler.set_slice_step(0, r, cfg.step)
                 logger.info(f"rank {target} restored its checkpoint shard of step {step} ({n} B) from peer {donor}")

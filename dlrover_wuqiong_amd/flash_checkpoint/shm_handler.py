@@ -7,6 +7,8 @@ Segment layout (one segment per local checkpoint shard)::
                                     2 layout generation, 3 slot stride,
                                     4 number of slots,
                                     8 + s*MAX_SLICES + r: step of slice r of slot s
+                                    META_WORDS + 2s, +1: step / slice count of
+                                      slot s's metadata (read without unpickling it)
     [HEADER + s*stride, ...)      payload slot s: the coalesced tensor extents
 
 Two payload *slots*: a save always writes the slot that does NOT hold the
@@ -46,6 +48,7 @@ HEADER_BYTES = 64 * 1024
 MAGIC = 0x44574B5053484D32  # "DWKPSHM2"
 MAX_SLICES = 1024
 SLOT_ALIGN = 2 << 20
+META_WORDS = 7168  # header word index of slot 0's (metadata step, num_slices)
 DLROVER_CKPT_CONFIG_KEY = "_DLORVER_CKPT_CONFIG"
 EVENT_QUEUE_SIZE = 16  # checkpoint events buffered between workers and the saver
 
@@ -227,7 +230,18 @@ class SharedMemoryHandler:
         return self.get_meta(slot).get(DLROVER_CKPT_CONFIG_KEY, default_config or CheckpointConfig())
 
     def set_metadata(self, slot: int, meta_tree: Any, config: CheckpointConfig):
-        self.metas[slot].set({"tree": meta_tree, DLROVER_CKPT_CONFIG_KEY: config})
+        self.set_meta_dict(slot, {"tree": meta_tree, DLROVER_CKPT_CONFIG_KEY: config})
+
+    def set_meta_dict(self, slot: int, meta: dict):
+        """Write a slot's metadata: the pickled dict, then its (step, slice
+        count) header words -- what completeness checks read."""
+        cfg = meta.get(DLROVER_CKPT_CONFIG_KEY)
+        if self._header is not None:
+            self._header[META_WORDS + 2 * slot] = 0
+        self.metas[slot].set(meta)
+        if self._header is not None and cfg is not None:
+            self._header[META_WORDS + 2 * slot + 1] = max(1, int(cfg.num_slices))
+            self._header[META_WORDS + 2 * slot] = int(cfg.step)
 
     def _attached(self) -> bool:
         if self.shared_memory is not None and not self.shared_memory.stale():
@@ -237,13 +251,17 @@ class SharedMemoryHandler:
         return self.init_shared_memory(create=False)
 
     def slot_step(self, slot: int) -> int:
-        """Step of the complete checkpoint in ``slot``; 0 if none/partial."""
-        cfg = self.get_meta(slot).get(DLROVER_CKPT_CONFIG_KEY)
-        if cfg is None or cfg.step <= 0 or not self._attached():
+        """Step of the complete checkpoint in ``slot``; 0 if none/partial.
+        Reads header words only (a save checks both slots: unpickling the
+        metadata trees would cost milliseconds of training pause)."""
+        if not self._attached() or self._header is None:
             return 0
-        steps = self.slice_steps(slot, cfg.num_slices)
-        if steps and all(s == cfg.step for s in steps):
-            return cfg.step
+        step = int(self._header[META_WORDS + 2 * slot])
+        if step <= 0:
+            return 0
+        steps = self.slice_steps(slot, int(self._header[META_WORDS + 2 * slot + 1]))
+        if steps and all(s == step for s in steps):
+            return step
         return 0
 
     def complete_steps(self) -> Dict[int, int]:
@@ -306,7 +324,7 @@ class SharedMemoryHandler:
         off = self.payload_offset(0)
         self.shared_memory.buf[off: off + len(data)] = data
         cfg: CheckpointConfig = meta[DLROVER_CKPT_CONFIG_KEY]
-        self.metas[0].set(meta)
+        self.set_meta_dict(0, meta)
         for r in range(cfg.num_slices):
             self.set_slice_step(0, r, cfg.step)
 
