@@ -8,6 +8,7 @@ vp, i64, i32, u32, u64, f32, cp = (c.c_void_p, c.c_int64, c.c_int, c.c_uint32, c
 SIGS = {
     # ckpt_copy.hip
     "dw_multi_copy": (i32, [vp, i64, vp]),
+    "dw_multi_copy_grid": (i32, [vp, i64, i32, vp]),
     "dw_fill_u32": (i32, [vp, i64, u32, vp]),
     "dw_host_register": (i32, [vp, u64]),
     "dw_host_unregister": (i32, [vp]),

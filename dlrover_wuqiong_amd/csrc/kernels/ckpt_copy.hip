@@ -63,12 +63,19 @@ __global__ void __launch_bounds__(256) multi_copy_kernel(const CopyDesc* __restr
   }
 }
 
-extern "C" int dw_multi_copy(const void* descs_dev, int64_t n, void* stream) {
+// max_blocks > 0 bounds the grid: a background snapshot copy that trickles
+// through a few CUs beside the training kernels instead of taking the chip.
+extern "C" int dw_multi_copy_grid(const void* descs_dev, int64_t n, int max_blocks, void* stream) {
   if (n <= 0) return 0;
-  int grid = (int)(n < 4096 ? n : 4096);
+  const int64_t cap = max_blocks > 0 ? max_blocks : 4096;
+  int grid = (int)(n < cap ? n : cap);
   hipLaunchKernelGGL(multi_copy_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
                      (const CopyDesc*)descs_dev, n);
   DW_LAUNCH_RET;
+}
+
+extern "C" int dw_multi_copy(const void* descs_dev, int64_t n, void* stream) {
+  return dw_multi_copy_grid(descs_dev, n, 0, stream);
 }
 
 // Fill `n` bytes with a byte value (used to poison buffers in tests).

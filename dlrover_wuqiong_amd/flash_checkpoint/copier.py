@@ -64,12 +64,12 @@ def build_descs(pieces: List[Tuple[int, int, int]], device) -> torch.Tensor:
     return torch.from_numpy(arr).to(device, non_blocking=False)
 
 
-def launch_multi_copy(descs: torch.Tensor, stream=None):
+def launch_multi_copy(descs: torch.Tensor, stream=None, max_blocks: int = 0):
     if descs.numel() == 0:
         return
     s = stream if stream is not None else torch.cuda.current_stream()
-    _check(_kern().dw_multi_copy(ctypes.c_void_p(descs.data_ptr()), descs.shape[0],
-                                 ctypes.c_void_p(s.cuda_stream)), "multi_copy")
+    _check(_kern().dw_multi_copy_grid(ctypes.c_void_p(descs.data_ptr()), descs.shape[0], int(max_blocks),
+                                      ctypes.c_void_p(s.cuda_stream)), "multi_copy")
 
 
 class PrepTracker:
@@ -348,6 +348,10 @@ class GpuCopier:
         # (GPT2-1.5B: pause 16 -> 9 ms, next step +7 ms): worth it only when
         # the step has HBM headroom to hide it.
         self.overlap = os.environ.get("DWAMD_OVERLAP_SNAPSHOT", "0") == "1"
+        # grid of the overlapped ("late") copy: 0 = the whole chip (done
+        # fastest, but it competes with the next forward); a few dozen blocks
+        # trickle it through a few CUs during the ~100 ms before the fence
+        self.overlap_blocks = int(os.environ.get("DWAMD_OVERLAP_BLOCKS", "0"))
         self._snap_stream: Optional[torch.cuda.Stream] = None
         self._fence_ev: Optional[torch.cuda.Event] = None
         # Bounded staging ring (``DWAMD_STAGING=ring``, or automatically when
@@ -525,7 +529,7 @@ class GpuCopier:
             launch_multi_copy(descs[0], cur)
             if descs[1] is not None:
                 copy_stream.wait_stream(cur)  # the "now" part is ordered before the flush too
-                launch_multi_copy(descs[1], copy_stream)
+                launch_multi_copy(descs[1], copy_stream, self.overlap_blocks)
         ev = torch.cuda.Event()
         ev.record(copy_stream)
         if copy_stream is not cur:
