@@ -32,7 +32,10 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 __device__ __forceinline__ bf16x8_t as_bf(const u32x4& v) { return __builtin_bit_cast(bf16x8_t, v); }
 __device__ __forceinline__ unsigned int pk2(float a, float b) {
-  return (unsigned int)f2bf(a) | ((unsigned int)f2bf(b) << 16);
+  // one v_cvt_pk_bf16_f32 (RNE) for the pair
+  typedef __bf16 bf16x2_v __attribute__((ext_vector_type(2)));
+  typedef float f32x2_v __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned int, __builtin_convertvector((f32x2_v){a, b}, bf16x2_v));
 }
 
 // A operand of a 32x32x16 MFMA that sums over 16 rows of a row-major LDS
@@ -48,7 +51,7 @@ __device__ __forceinline__ u32x4 tr_frag(const char* img, int r0, int d0, int la
       __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)LDS_PTR(img + img_off<D>(row, ch) + 8 * (tp & 1)));
   const s16x4 v1 =
       __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)LDS_PTR(img + img_off<D>(row + 8, ch) + 8 * (tp & 1)));
-  return (u32x4){pack_s16(v0[0], v0[1]), pack_s16(v0[2], v0[3]), pack_s16(v1[0], v1[1]), pack_s16(v1[2], v1[3])};
+  return join_tr(v0, v1);
 }
 
 // delta[b,h,q] = sum_d dO*O.  D/8 lanes per (b, s, h) row (16-byte loads),
@@ -111,7 +114,8 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                      AttnStrides st, AttnVarlen vl) {
   using C = DkvCfg<D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar wave index
   const int r = lane & 31, hh = lane >> 5;
   const BlockXYZ bc = xcd_block((S + C::BKB - 1) / C::BKB, H);
   const int b = bc.z, h = bc.y;
@@ -238,7 +242,8 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
             float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], scale_log2, -l4[j]));
             if (need_mask) {
               const int q = q0 + qi + j;
-              if (q >= SQ || key >= SK || (CAUSAL && key > q + co)) p = 0.f;
+              const bool keep = (q < SQ) & (key < SK) & (!CAUSAL | (key <= q + co));
+              p = keep ? p : 0.f;
             }
             s[i] = p;
             dp[i] = p * (dp[i] - d4[j]);  // dS (scale applied in the epilogue)
@@ -369,7 +374,8 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
                    AttnVarlen vl) {
   using C = DqCfg<D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar wave index
   const int r = lane & 31, hh = lane >> 5;
   const int nqb = (S + C::BQ - 1) / C::BQ;
   const BlockXYZ bc = xcd_block(nqb, H);
@@ -454,6 +460,7 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
     const char* vl = kl + C::TILE;
     if (!CAUSAL || k0 <= q0 + 31 + co) {
       const bool need_mask = (k0 + C::BK > SK) || (CAUSAL && (k0 + C::BK - 1 > q0 + co));
+      const int lim = CAUSAL ? min(SK, q + co + 1) : SK;  // keys < lim are visible to this lane's query
       // one 32-key subtile at a time keeps S^T / dP^T at 32 registers
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb) {
@@ -475,7 +482,7 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
           float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], scale_log2, -lse2));
           if (need_mask) {
             const int key = k0 + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hh;
-            if (key >= SK || (CAUSAL && key > q + co)) p = 0.f;
+            p = key < lim ? p : 0.f;
           }
           s[i] = p * (dp[i] - dl);  // dS^T (scale applied in the epilogue)
         }
@@ -492,8 +499,7 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
                 (lds_s16x4*)LDS_PTR(kl + img_off<D>(kb, ch) + 8 * (tp & 1)));
             const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                 (lds_s16x4*)LDS_PTR(kl + img_off<D>(kb + 8, ch) + 8 * (tp & 1)));
-            const u32x4 kt = {pack_s16(v0[0], v0[1]), pack_s16(v0[2], v0[3]), pack_s16(v1[0], v1[1]),
-                              pack_s16(v1[2], v1[3])};
+            const u32x4 kt = join_tr(v0, v1);
             acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(kt), as_bf(pf), acc[dt], 0, 0, 0);
           }
         }

@@ -69,6 +69,16 @@ __device__ __forceinline__ SeqRange seq_range(const AttnVarlen& vl, int b, int h
   return r;
 }
 
+// two ds_read_b64_tr_b16 results -> one MFMA operand (pure register
+// renaming: the 4 shorts of each read are already the packed bf16 pairs)
+template <typename V>
+__device__ __forceinline__ u32x4 join_tr(const V& a, const V& b) {
+  static_assert(sizeof(V) == 8, "8-byte transposed read");
+  typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+  const u32x2_t x = __builtin_bit_cast(u32x2_t, a), y = __builtin_bit_cast(u32x2_t, b);
+  return (u32x4){x[0], x[1], y[0], y[1]};
+}
+
 __device__ __forceinline__ unsigned int pack_s16(short a, short b) {
   return (unsigned int)(unsigned short)a | ((unsigned int)(unsigned short)b << 16);
 }

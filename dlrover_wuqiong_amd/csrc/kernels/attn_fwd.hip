@@ -50,7 +50,10 @@ struct Fwd2Cfg {
 __device__ __forceinline__ bf16x8_t as_bf16x8(const u32x4& v) { return __builtin_bit_cast(bf16x8_t, v); }
 
 __device__ __forceinline__ unsigned int pack2(float a, float b) {
-  return (unsigned int)f2bf(a) | ((unsigned int)f2bf(b) << 16);
+  // one v_cvt_pk_bf16_f32 (RNE) for the pair
+  typedef __bf16 bf16x2_v __attribute__((ext_vector_type(2)));
+  typedef float f32x2_v __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned int, __builtin_convertvector((f32x2_v){a, b}, bf16x2_v));
 }
 
 template <int D, bool CAUSAL, int MINW = 1>
@@ -61,7 +64,10 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   using C = Fwd2Cfg<D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  // wave index as a scalar: keeps q0 / causal skips / mask decisions in SGPRs
+  // (a VGPR wid turns every per-element mask into an exec-mask branch)
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5;
   const int nqb = (S + C::BQ - 1) / C::BQ;
   const BlockXYZ bc = xcd_block(nqb, H);
@@ -162,16 +168,21 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
       const int q = q0 + r;
       const bool need_mask = (k0 + C::BK > SK) || (CAUSAL && (k0 + C::BK - 1 > q0 + co));
       float mx = -INFINITY;
+      if (need_mask) {
+        // keys < lim are visible to this lane's query (branch-free selects)
+        const int lim = CAUSAL ? min(SK, q + co + 1) : SK;
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = k0 + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            s[sb][i] = key < lim ? s[sb][i] : -INFINITY;
+          }
+      }
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          if (need_mask) {
-            const int key = k0 + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hh;
-            if (key >= SK || (CAUSAL && key > q + co)) s[sb][i] = -INFINITY;
-          }
-          mx = fmaxf(mx, s[sb][i]);
-        }
+        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[sb][i]);
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;
       if (!__all(mx <= m_i)) {
         // some row's max grew: rescale O and l (exact; skipped otherwise)
@@ -212,8 +223,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
                 (lds_s16x4*)LDS_PTR(vl + img_off<D>(kb, ch) + 8 * (tp & 1)));
             const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                 (lds_s16x4*)LDS_PTR(vl + img_off<D>(kb + 8, ch) + 8 * (tp & 1)));
-            const u32x4 vf = {pack_s16(v0[0], v0[1]), pack_s16(v0[2], v0[3]), pack_s16(v1[0], v1[1]),
-                              pack_s16(v1[2], v1[3])};
+            const u32x4 vf = join_tr(v0, v1);
             o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(vf), as_bf16x8(pf), o[dt], 0, 0, 0);
           }
         }
@@ -257,8 +267,15 @@ static void launch_fwd(const void* q, const void* k, const void* v, void* o, voi
   // D=64 causal capped at 128 VGPRs (8 B/lane spill): two blocks per CU,
   // +9% measured (profiles/attn_bench_latest.jsonl); the non-causal variant
   // would spill 116 B/lane, so it keeps one block per CU
-  if (causal && D == 64)
-    hipLaunchKernelGGL((attn_fwd_kernel<D, true, 4>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
+  if constexpr (D == 64) {
+    if (causal) {
+      hipLaunchKernelGGL((attn_fwd_kernel<D, true, 4>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
+                         (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st, vl);
+      return;
+    }
+  }
+  if (false)
+    hipLaunchKernelGGL((attn_fwd_kernel<D, true, 1>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
                        (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st, vl);
   else if (causal)
     hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
