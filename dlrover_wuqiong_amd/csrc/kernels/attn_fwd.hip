@@ -5,7 +5,8 @@
 // strides (q/k/v may be views into one packed QKV projection).
 //
 // CDNA4 design (cdna_hip_programming.md App. B "fused attention prefill"):
-//  * 8 waves x 32 query rows = 256 queries per workgroup; K/V tiles of 64
+//  * W waves x 32 query rows per workgroup (D=128: 8 -> 256 queries; D=64: 4
+//    -> 128); K/V tiles of 64
 //    keys double-buffered in LDS (one barrier per tile); every tile is read
 //    from HBM once per 256 queries.
 //  * v_mfma_f32_32x32x16_bf16 with the swapped product S^T = K * Q^T: the
@@ -32,12 +33,11 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 
-template <int D>
+template <int D, int W = 8>
 struct Fwd2Cfg {
-  // 8 waves share each K/V tile.  D=128 (236 VGPRs) runs one block per CU;
-  // causal D=64 is instantiated with MINW=4 (<=128 VGPRs) so two blocks share
-  // a CU and one block's softmax overlaps the other's MFMAs.
-  static constexpr int WAVES = 8;
+  // W waves share each K/V tile.  D=128: 8 waves (236 VGPRs, one block per
+  // CU); D=64: 4 waves (see launch_fwd).
+  static constexpr int WAVES = W;
   static constexpr int BQ = 32 * WAVES;  // queries per block
   static constexpr int BK = 64;          // keys per tile
   static constexpr int NCH = D / 8;      // 16-byte chunks per row
@@ -56,12 +56,12 @@ __device__ __forceinline__ unsigned int pack2(float a, float b) {
   return __builtin_bit_cast(unsigned int, __builtin_convertvector((f32x2_v){a, b}, bf16x2_v));
 }
 
-template <int D, bool CAUSAL, int MINW = 1>
-__global__ void __launch_bounds__(64 * Fwd2Cfg<D>::WAVES, MINW)
+template <int D, bool CAUSAL, int W = 8, int MINW = 1>
+__global__ void __launch_bounds__(64 * W, MINW)
 attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
                 bf16_t* __restrict__ O, float* __restrict__ LSE, int S, int H, int HKV, float scale_log2,
                 AttnStrides st, AttnVarlen vl) {
-  using C = Fwd2Cfg<D>;
+  using C = Fwd2Cfg<D, W>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -258,31 +258,25 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   }
 }
 
+template <int D, bool CAUSAL, int W, int MINW>
+static void launch_fwd_v(const void* q, const void* k, const void* v, void* o, void* lse, int B, int S, int H,
+                         int HKV, float scale_log2, const AttnStrides& st, const AttnVarlen& vl, hipStream_t s) {
+  using C = Fwd2Cfg<D, W>;
+  dim3 grid((unsigned)((S + C::BQ - 1) / C::BQ * H * B)), block(64 * W);  // 1-D: xcd_block()
+  hipLaunchKernelGGL((attn_fwd_kernel<D, CAUSAL, W, MINW>), grid, block, 4 * C::TILE, s, (const bf16_t*)q,
+                     (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st, vl);
+}
+
 template <int D>
 static void launch_fwd(const void* q, const void* k, const void* v, void* o, void* lse, int B, int S, int H, int HKV,
                        int causal, float scale_log2, const AttnStrides& st, const AttnVarlen& vl, hipStream_t s) {
-  using C = Fwd2Cfg<D>;
-  dim3 grid((unsigned)((S + C::BQ - 1) / C::BQ * H * B)), block(64 * C::WAVES);  // 1-D: xcd_block()
-  const int lds = 4 * C::TILE;
-  // D=64 causal capped at 128 VGPRs (8 B/lane spill): two blocks per CU,
-  // +9% measured (profiles/attn_bench_latest.jsonl); the non-causal variant
-  // would spill 116 B/lane, so it keeps one block per CU
-  if constexpr (D == 64) {
-    if (causal) {
-      hipLaunchKernelGGL((attn_fwd_kernel<D, true, 4>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
-                         (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st, vl);
-      return;
-    }
-  }
-  if (false)
-    hipLaunchKernelGGL((attn_fwd_kernel<D, true, 1>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
-                       (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st, vl);
-  else if (causal)
-    hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
-                       (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st, vl);
-  else
-    hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, block, lds, s, (const bf16_t*)q, (const bf16_t*)k,
-                       (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st, vl);
+  // D=64: 4 waves (128 queries per block, 184 VGPRs, two blocks per CU):
+  // twice the blocks of the 8-wave form for a finer causal balance; measured
+  // against 8 waves capped at 128 VGPRs (spills) / uncapped and 4 waves
+  // capped: 289-311 vs 239-288 TF/s (profiles/r2/attn_fwd64_variants.jsonl)
+  constexpr int W = D == 64 ? 4 : 8;
+  return causal ? launch_fwd_v<D, true, W, 1>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, s)
+                : launch_fwd_v<D, false, W, 1>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, s);
 }
 
 // strides: int64[8] = q_bs, q_rs, k_bs, k_rs, v_bs, v_rs, o_bs, o_rs (elements)
