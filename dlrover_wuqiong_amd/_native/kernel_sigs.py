@@ -90,6 +90,7 @@ OPTIONAL = {
     "dw_attn_fwd_strided": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, f32, i32, vp]),
     "dw_attn_bwd_strided": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, f32,
                                   i32, vp]),
+    "dw_attn_decode": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, f32, vp]),
     "dw_attn_fwd_varlen": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, i32, f32, vp]),
     "dw_attn_bwd_varlen": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32,
                                  i32, vp, i32, f32, vp]),

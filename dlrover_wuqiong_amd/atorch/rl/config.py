@@ -12,6 +12,10 @@ class PPOConfig:
     max_new_tokens: int = 32
     temperature: float = 1.0
     top_k: int = 0
+    # KV-cached generation from the training weights (Llama actors;
+    # ``hybrid_engine.py``), HIP-graph decode on the GPU
+    use_hybrid_engine: bool = True
+    max_seq_len: Optional[int] = None   # cache length; default prompt + max_new_tokens
     # rollout / optimisation
     rollout_batch_size: int = 16
     mini_batch_size: int = 8

@@ -139,6 +139,25 @@ class PPOTrainer(RLTrainer):
         self.gen = torch.Generator(device="cpu").manual_seed(config.seed)
         self._last = {}
 
+    def _hybrid(self, prompts):
+        """The actor's hybrid (KV-cache) engine, or None to sample with full
+        forwards (non-Llama or tensor/sequence-parallel actors)."""
+        c = self.config
+        if not c.use_hybrid_engine:
+            return None
+        need = (prompts.shape[0], c.max_seq_len or prompts.shape[1] + c.max_new_tokens)
+        hy = getattr(self, "_hy", None)
+        if hy is None or hy.max_batch < need[0] or hy.max_len < need[1]:
+            from .hybrid_engine import HybridEngine, find_llama
+
+            llama = find_llama(self.engine.actor)
+            if llama is None or getattr(llama, "tp_group", None) is not None or \
+                    getattr(llama, "sp_group", None) is not None:
+                self.config.use_hybrid_engine = False
+                return None
+            hy = self._hy = HybridEngine(self.engine.actor, need[0], need[1])
+        return hy
+
     def _response_stats(self, model, seq, P):
         logits = model(seq)
         resp_logits = logits[:, P - 1:-1, :]
@@ -149,7 +168,11 @@ class PPOTrainer(RLTrainer):
         c, e = self.config, self.engine
         P = prompts.shape[1]
         g = self.gen if prompts.device.type == "cpu" else None
-        seq = sample(e.actor, prompts, c.max_new_tokens, c.temperature, c.top_k, generator=g)
+        hy = self._hybrid(prompts)
+        if hy is not None:
+            seq = hy.generate(prompts, c.max_new_tokens, c.temperature, c.top_k, generator=g)
+        else:
+            seq = sample(e.actor, prompts, c.max_new_tokens, c.temperature, c.top_k, generator=g)
         R = seq.shape[1] - P
         mask = torch.ones(seq.shape[0], R, device=seq.device)
         _, logprobs, _ = self._response_stats(e.actor, seq, P)

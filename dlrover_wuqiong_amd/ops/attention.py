@@ -274,3 +274,58 @@ def flash_attn_padded_func(q, k, v, key_padding_mask: torch.Tensor, causal: bool
     vu = v.reshape(B * S, *v.shape[2:]).index_select(0, idx)
     o = flash_attn_varlen_func(qu, ku, vu, cu, cu, mx, mx, softmax_scale=softmax_scale, causal=causal)
     return pad_input(o, idx, B, S)
+
+
+# ------------------------------------------------------------------ decode
+_DEC_WS = {}
+
+
+def decode_attention_reference(q, k_cache, v_cache, lens, softmax_scale=None):
+    """q [B, H, D], caches [B, Smax, Hkv, D], lens [B] -> [B, H, D] (fp32 math)."""
+    B, H, D = q.shape
+    hkv = k_cache.shape[2]
+    scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(D)
+    out = torch.empty_like(q)
+    for b in range(B):
+        n = int(lens[b])
+        k = k_cache[b, :n].float().repeat_interleave(H // hkv, dim=1)  # [n, H, D]
+        v = v_cache[b, :n].float().repeat_interleave(H // hkv, dim=1)
+        s = torch.einsum("hd,nhd->hn", q[b].float(), k) * scale
+        out[b] = torch.einsum("hn,nhd->hd", s.softmax(-1), v).to(q.dtype)
+    return out
+
+
+def decode_attention(q, k_cache, v_cache, lens, softmax_scale=None, chunk: int = 256):
+    """One-token-per-sequence attention over a static KV cache.
+
+    q [B, H, D]; k_cache / v_cache [B, Smax, Hkv, D] (row-contiguous heads,
+    any batch / row stride); lens [B] int32 on the device (valid keys per
+    sequence).  The launch depends only on Smax, so a decode step can be
+    captured once in a HIP graph and replayed while ``lens`` grows
+    (``csrc/kernels/attn_decode.hip``: split-KV, HBM-bound)."""
+    if not _hip.use_hip(q):
+        return decode_attention_reference(q, k_cache, v_cache, lens, softmax_scale)
+    _hip.require_bf16(q, k_cache, v_cache)
+    B, H, D = q.shape
+    Smax, hkv = k_cache.shape[1], k_cache.shape[2]
+    if D not in (64, 128) or H % hkv or k_cache.stride(3) != 1 or k_cache.stride(2) != D or \
+            v_cache.stride(3) != 1 or v_cache.stride(2) != D or lens.dtype != torch.int32 or lens.numel() != B \
+            or lens.device != q.device:
+        raise _hip.HipKernelError("decode_attention: bf16 q [B,H,D], caches [B,S,Hkv,D] with D in {64,128}, "
+                                  "int32 device lens [B]")
+    q = q.contiguous()
+    nsplit = (Smax + chunk - 1) // chunk
+    key = (q.device, B, H, D, nsplit)
+    ws = _DEC_WS.get(key)
+    if ws is None:
+        ws = (torch.empty(B * H * nsplit * D, device=q.device, dtype=torch.float32),
+              torch.empty(B * H * nsplit * 2, device=q.device, dtype=torch.float32))
+        _DEC_WS[key] = ws
+    out = torch.empty_like(q)
+    st = (ctypes.c_longlong * 6)(q.stride(0), k_cache.stride(0), k_cache.stride(1), v_cache.stride(0),
+                                 v_cache.stride(1), out.stride(0))
+    scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(D)
+    _hip.check(_hip.lib().dw_attn_decode(_hip.ptr(q), _hip.ptr(k_cache), _hip.ptr(v_cache), _hip.ptr(lens),
+                                         _hip.ptr(out), _hip.ptr(ws[0]), _hip.ptr(ws[1]), B, H, hkv, D, nsplit,
+                                         chunk, st, ctypes.c_float(scale), _hip.stream()), "attn_decode")
+    return out
