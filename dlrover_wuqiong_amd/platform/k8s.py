@@ -228,26 +228,55 @@ class PodWatcher(NodeWatcher):
 
 
 class ElasticJobOperator:
-    """Reconciles ``ElasticJob`` and ``ScalePlan`` custom objects."""
+    """Reconciles ``ElasticJob`` and ``ScalePlan`` custom objects (CRDs in
+    ``deploy/crds/``).
+
+    * ElasticJob: create the job master pod + service (image/resources from
+      ``replicaSpecs["dlrover-master"].template`` when given, ``spec.envs``
+      forwarded), mirror the master pod's phase into ``status.phase``, and
+      on a terminal phase clean up the job's remaining worker pods;
+    * ScalePlan: ``replicaResourceSpecs`` patch the job's replica counts
+      (the master scales to them); ``createPods`` / ``removePods`` /
+      ``migratePods`` create pods from the job's per-type pod template and
+      delete the named ones (migration: the new pod first, then the old).
+
+    Parity: reference Go operator ``go/operator/pkg/controllers``
+    (ElasticJob + ScalePlan reconcilers, master pod/service creation).
+    """
 
     def __init__(self, client: K8sClient, master_image: str, master_port: int = 50001):
         self.client, self.image, self.port = client, master_image, master_port
         self._stop = threading.Event()
 
+    @staticmethod
+    def _envs(job: Dict) -> List[Dict]:
+        envs = (job.get("spec") or {}).get("envs") or {}
+        return [{"name": k, "value": str(v)} for k, v in envs.items()]
+
     def master_pod(self, job: Dict) -> Dict:
         name = job["metadata"]["name"]
         spec = job.get("spec", {})
-        workers = spec.get("replicaSpecs", {}).get("worker", {}).get("replicas", 1)
+        rs = spec.get("replicaSpecs", {})
+        workers = rs.get("worker", {}).get("replicas", 1)
         cmd = ["python", "-m", "dlrover_wuqiong_amd.master.master", "--platform", "k8s", "--job_name", name,
                "--namespace", self.client.ns, "--port", str(self.port), "--node_num", str(workers)]
+        container = {"name": "master", "image": self.image, "command": cmd,
+                     "ports": [{"containerPort": self.port}], "env": self._envs(job)}
+        tmpl = ((rs.get("dlrover-master") or {}).get("template") or {}).get("spec") or {}
+        tc = (tmpl.get("containers") or [{}])[0]
+        for k in ("image", "resources", "volumeMounts", "imagePullPolicy"):
+            if k in tc:
+                container[k] = tc[k]
+        pod_spec = {"restartPolicy": "Never", "containers": [container]}
+        for k in ("volumes", "nodeSelector", "tolerations", "priorityClassName", "serviceAccountName"):
+            if k in tmpl:
+                pod_spec[k] = tmpl[k]
         return {"apiVersion": "v1", "kind": "Pod",
                 "metadata": {"name": f"elasticjob-{name}-dlrover-master",
                              "labels": {JOB_LABEL: name, TYPE_LABEL: NodeType.MASTER},
                              "ownerReferences": [{"apiVersion": f"{GROUP}/{VERSION}", "kind": "ElasticJob",
                                                   "name": name, "uid": job["metadata"].get("uid", "")}]},
-                "spec": {"restartPolicy": "Never",
-                         "containers": [{"name": "master", "image": self.image, "command": cmd,
-                                         "ports": [{"containerPort": self.port}]}]}}
+                "spec": pod_spec}
 
     def master_service(self, job: Dict) -> Dict:
         name = job["metadata"]["name"]
@@ -255,6 +284,36 @@ class ElasticJobOperator:
                 "metadata": {"name": f"elasticjob-{name}-dlrover-master", "labels": {JOB_LABEL: name}},
                 "spec": {"selector": {JOB_LABEL: name, TYPE_LABEL: NodeType.MASTER},
                          "ports": [{"port": self.port, "targetPort": self.port}]}}
+
+    def replica_pod(self, job: Dict, node_type: str, node_id: int, rank: int, resource: Optional[Dict] = None,
+                    name: Optional[str] = None) -> Dict:
+        """A worker (or other replica type) pod from the job's pod template."""
+        import copy
+
+        jname = job["metadata"]["name"]
+        tmpl = copy.deepcopy(((job.get("spec", {}).get("replicaSpecs", {}).get(node_type) or {})
+                              .get("template") or {}))
+        spec = tmpl.get("spec") or {"containers": [{"name": "main", "image": self.image}]}
+        spec.setdefault("restartPolicy", "Never")
+        c = spec["containers"][0]
+        env = [e for e in c.get("env", []) if e.get("name") not in ("DWAMD_MASTER_ADDR", "NODE_RANK", "NODE_ID")]
+        env += [{"name": "DWAMD_MASTER_ADDR", "value": f"elasticjob-{jname}-dlrover-master:{self.port}"},
+                {"name": "NODE_RANK", "value": str(rank)}, {"name": "NODE_ID", "value": str(node_id)},
+                {"name": "DWAMD_JOB_NAME", "value": jname}] + self._envs(job)
+        c["env"] = env
+        if resource:
+            lim = dict((c.get("resources") or {}).get("limits") or {})
+            for k, v in resource.items():
+                lim[{"gpu": "amd.com/gpu"}.get(k, k)] = str(v)
+            c["resources"] = {"limits": lim, "requests": dict(lim)}
+        meta = tmpl.get("metadata") or {}
+        labels = dict(meta.get("labels") or {})
+        labels.update({JOB_LABEL: jname, TYPE_LABEL: node_type, ID_LABEL: str(node_id), RANK_LABEL: str(rank)})
+        return {"apiVersion": "v1", "kind": "Pod",
+                "metadata": {"name": name or pod_name(jname, node_type, node_id), "labels": labels,
+                             "ownerReferences": [{"apiVersion": f"{GROUP}/{VERSION}", "kind": "ElasticJob",
+                                                  "name": jname, "uid": job["metadata"].get("uid", "")}]},
+                "spec": spec}
 
     def reconcile_job(self, job: Dict):
         name = job["metadata"]["name"]
@@ -273,18 +332,50 @@ class ElasticJobOperator:
         pphase = (pod.get("status") or {}).get("phase", "Pending")
         new = {"Pending": "Pending", "Running": "Running", "Succeeded": "Succeeded", "Failed": "Failed"}.get(pphase)
         if new and new != phase:
-            self.client.patch_custom_status("elasticjobs", name, {"phase": new})
+            st = {"phase": new}
+            if new in ("Succeeded", "Failed"):
+                import datetime
+
+                st["completionTime"] = datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
+                # the job is over: its workers must not keep the GPUs
+                for p in self.client.list_pods(f"{JOB_LABEL}={name}"):
+                    if p["metadata"]["name"] != mname:
+                        self.client.delete_pod(p["metadata"]["name"])
+            elif new == "Running" and not (job.get("status") or {}).get("startTime"):
+                import datetime
+
+                st["startTime"] = datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
+            self.client.patch_custom_status("elasticjobs", name, st)
 
     def reconcile_scaleplan(self, plan: Dict):
         st = plan.get("status") or {}
-        if st.get("phase") == "Succeeded":
+        if st.get("phase") in ("Succeeded", "Failed"):
             return
         spec = plan.get("spec", {})
-        job = spec.get("ownerJob")
+        jname = spec.get("ownerJob")
+        job = self.client.get_custom("elasticjobs", jname) if jname else None
+        if job is None:
+            logger.warning(f"operator: ScalePlan {plan['metadata']['name']} names unknown job {jname}")
+            self.client.patch_custom_status("scaleplans", plan["metadata"]["name"], {"phase": "Failed"})
+            return
         rs = spec.get("replicaResourceSpecs", {})
-        patch = {"spec": {"replicaSpecs": {t: {"replicas": int(v.get("replicas", 0))} for t, v in rs.items()}}}
-        if job and rs:
-            self.client.patch_custom("elasticjobs", job, patch)
+        if rs:
+            patch = {"spec": {"replicaSpecs": {t: {"replicas": int(v.get("replicas", 0))} for t, v in rs.items()}}}
+            self.client.patch_custom("elasticjobs", jname, patch)
+        pname = plan["metadata"]["name"]
+        creates = [(item, item.get("name")) for item in spec.get("createPods") or []]
+        # migration: the replacement (fresh name) is created before the old pod goes
+        creates += [(item, f"{pod_name(jname, item.get('type', NodeType.WORKER), int(item.get('id', 0)))}"
+                           f"-mig-{pname}"[:63]) for item in spec.get("migratePods") or []]
+        for item, new_name in creates:
+            t, i = item.get("type", NodeType.WORKER), int(item.get("id", 0))
+            pod = self.replica_pod(job, t, i, int(item.get("rankIndex", i)), item.get("resource"), new_name)
+            if self.client.get_pod(pod["metadata"]["name"]) is None:
+                self.client.create_pod(pod)
+        for item in (spec.get("removePods") or []) + (spec.get("migratePods") or []):
+            n = item.get("name") or pod_name(jname, item.get("type", NodeType.WORKER), int(item.get("id", 0)))
+            if self.client.get_pod(n) is not None:
+                self.client.delete_pod(n)
         self.client.patch_custom_status("scaleplans", plan["metadata"]["name"], {"phase": "Succeeded"})
 
     def reconcile_once(self):

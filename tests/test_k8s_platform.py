@@ -167,3 +167,83 @@ def test_elasticjob_operator_reconcile(k8s):
     n_pods = len([k for k in fake.objs if k[0] == "pods"])
     op.reconcile_once()  # idempotent
     assert len([k for k in fake.objs if k[0] == "pods"]) == n_pods
+
+
+def test_operator_scaleplan_pods_master_template_and_cleanup(k8s):
+    from dlrover_wuqiong_amd.platform.k8s import ElasticJobOperator
+
+    fake, cli = k8s
+    tmpl = {"spec": {"containers": [{"name": "main", "image": "train:1", "command": ["dwamd-run", "t.py"],
+                                     "resources": {"limits": {"amd.com/gpu": 8}}}]}}
+    cli.create_custom("elasticjobs", {"metadata": {"name": "j2", "uid": "u2"},
+                                      "spec": {"envs": {"FOO": "1"},
+                                               "replicaSpecs": {"worker": {"replicas": 2, "template": tmpl},
+                                                                "dlrover-master": {"template": {"spec": {
+                                                                    "containers": [{"image": "master:2"}],
+                                                                    "nodeSelector": {"pool": "cpu"}}}}}}})
+    op = ElasticJobOperator(cli, "img:1")
+    op.reconcile_once()
+    mp = cli.get_pod("elasticjob-j2-dlrover-master")
+    assert mp["spec"]["containers"][0]["image"] == "master:2" and mp["spec"]["nodeSelector"] == {"pool": "cpu"}
+    assert {"name": "FOO", "value": "1"} in mp["spec"]["containers"][0]["env"]
+    cli.create_custom("scaleplans", {"metadata": {"name": "sp2"},
+                                     "spec": {"ownerJob": "j2", "manualScaling": True,
+                                              "createPods": [{"type": "worker", "id": 5, "rankIndex": 1,
+                                                              "resource": {"gpu": 4}}]}})
+    op.reconcile_once()
+    w = cli.get_pod("j2-worker-5")
+    c = w["spec"]["containers"][0]
+    assert c["image"] == "train:1" and c["resources"]["limits"]["amd.com/gpu"] == "4"
+    assert {"name": "NODE_RANK", "value": "1"} in c["env"] and w["metadata"]["labels"]["elasticjob.dlrover/name"] == "j2"
+    cli.create_custom("scaleplans", {"metadata": {"name": "sp3"},
+                                     "spec": {"ownerJob": "j2", "migratePods": [{"type": "worker", "id": 5}]}})
+    op.reconcile_once()
+    assert cli.get_pod("j2-worker-5") is None and cli.get_pod("j2-worker-5-mig-sp3") is not None
+    cli.create_custom("scaleplans", {"metadata": {"name": "sp4"},
+                                     "spec": {"ownerJob": "j2", "removePods": [{"name": "j2-worker-5-mig-sp3"}]}})
+    op.reconcile_once()
+    assert cli.get_pod("j2-worker-5-mig-sp3") is None
+    cli.create_custom("scaleplans", {"metadata": {"name": "bad"}, "spec": {"ownerJob": "nope"}})
+    op.reconcile_once()
+    assert cli.get_custom("scaleplans", "bad")["status"]["phase"] == "Failed"
+    # master finished -> status + remaining workers cleaned up
+    cli.create_pod(op.replica_pod(cli.get_custom("elasticjobs", "j2"), "worker", 0, 0))
+    fake.objs[("pods", "elasticjob-j2-dlrover-master")]["status"]["phase"] = "Succeeded"
+    op.reconcile_once()
+    st = cli.get_custom("elasticjobs", "j2")["status"]
+    assert st["phase"] == "Succeeded" and st["completionTime"]
+    assert cli.get_pod("j2-worker-0") is None
+
+
+def test_deploy_manifests():
+    import os
+
+    import yaml
+
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "deploy")
+    docs = {}
+    for dirpath, _d, files in os.walk(root):
+        for f in files:
+            with open(os.path.join(dirpath, f)) as fh:
+                docs[f] = [d for d in yaml.safe_load_all(fh) if d]
+    ej = docs["elastic.iml.github.io_elasticjobs.yaml"][0]
+    sp = docs["elastic.iml.github.io_scaleplans.yaml"][0]
+    from dlrover_wuqiong_amd.platform.k8s import GROUP, VERSION
+
+    for crd, plural in ((ej, "elasticjobs"), (sp, "scaleplans")):
+        assert crd["kind"] == "CustomResourceDefinition" and crd["spec"]["group"] == GROUP
+        assert crd["metadata"]["name"] == f"{plural}.{GROUP}" and crd["spec"]["names"]["plural"] == plural
+        v = crd["spec"]["versions"][0]
+        assert v["name"] == VERSION and "status" in v["subresources"]
+    # every spec field the operator reads is in the schema
+    ejs = ej["spec"]["versions"][0]["schema"]["openAPIV3Schema"]["properties"]["spec"]["properties"]
+    assert {"replicaSpecs", "envs"} <= set(ejs)
+    assert "template" in ejs["replicaSpecs"]["additionalProperties"]["properties"]
+    sps = sp["spec"]["versions"][0]["schema"]["openAPIV3Schema"]["properties"]["spec"]["properties"]
+    assert {"ownerJob", "replicaResourceSpecs", "createPods", "removePods", "migratePods"} <= set(sps)
+    kinds = [d["kind"] for d in docs["operator.yaml"]]
+    assert kinds == ["ServiceAccount", "ClusterRole", "ClusterRoleBinding", "Deployment"]
+    ex = docs["llama3_8b_fsdp_mi355x.yaml"][0]
+    assert ex["apiVersion"] == f"{GROUP}/{VERSION}" and ex["kind"] == "ElasticJob"
+    limits = ex["spec"]["replicaSpecs"]["worker"]["template"]["spec"]["containers"][0]["resources"]["limits"]
+    assert limits["amd.com/gpu"] == 8
