@@ -20,6 +20,22 @@ Optimisation algorithms (``opt_type``):
   ``max_workers`` and round down to ``node_unit``.
 * ``job_hot_ps``           PS nodes whose CPU utilisation exceeds the
   threshold get ``factor`` x CPU (the PS path of the reference).
+* ``job_ps_create_resource``  PS count / CPU / memory of a new PS job from its
+  name's history (count = max seen, CPU p90, memory max, x (1 + margin)).
+* ``job_ps_cold_create_resource``  no history for the name: the nearest job
+  of the same user by parameter count (JOB_META), scaled by the size ratio;
+  defaults when nothing is comparable.
+* ``job_ps_init_adjust_resource``  early in a run PS memory grows with the
+  embedding tables: a least-squares line over (step, memory) extrapolated to
+  ``max_steps`` sizes each PS; CPU from its utilisation.
+* ``job_ps_resource_util``  over-provisioned PS (utilisation below ``low``)
+  shrink to used x (1 + margin), never below ``min_cpu``.
+* ``job_ps_oom_resource`` / ``job_worker_create_oom_resource``  OOM at run /
+  at creation: memory x factor of the largest OOMed size (creation OOMs use
+  the job-name history so a re-submitted job starts big enough).
+* ``job_gpu_host_memory``  host memory per GPU node for flash checkpointing:
+  model/optimizer state per node x shm slots (2) + pinned staging + the
+  agent's headroom, from the JOB_META ``ckpt_bytes_per_node``.
 
 Parity: reference ``dlrover/proto/brain.proto`` (``persist_metrics``,
 ``get_job_metrics``, ``optimize``) and ``dlrover/python/brain/client.py``.
@@ -162,6 +178,123 @@ class BrainOptimizer:
             if m.get("cpu", 0) > 0 and m.get("cpu_used", 0) / m["cpu"] > thr:
                 plan[name] = {"cpu": round(m["cpu"] * factor, 2)}
         return {"ps_nodes": plan} if plan else {}
+
+
+    # ------------------------------------------------------------- PS jobs
+    def _usage(self, req, node_type: str, name: Optional[str] = None):
+        q = self.store.query(job_uuid=req.get("job_uuid") if name is None else None, job_name=name,
+                             metrics_type=MetricsType.RESOURCE_USAGE)
+        return [r for r in q if r["metrics"].get("node_type") == node_type]
+
+    def _opt_job_ps_create_resource(self, req):
+        name = req.get("job_name") or self._job_name(req.get("job_uuid", ""))
+        rows = [r for r in self._usage(req, "ps", name) if r["job_uuid"] != req.get("job_uuid")]
+        if not rows:
+            return self._opt_job_ps_cold_create_resource(req)
+        per_job: Dict[str, set] = {}
+        for r in rows:
+            per_job.setdefault(r["job_uuid"], set()).add(r["metrics"].get("node_name", "ps"))
+        count = max(len(v) for v in per_job.values())
+        mem = max(r["metrics"].get("memory_used_mb", 0) for r in rows)
+        cpus = sorted(r["metrics"].get("cpu_used", 0.0) for r in rows)
+        p90 = cpus[min(len(cpus) - 1, int(0.9 * len(cpus)))]
+        return {"ps": {"count": count, "cpu": round(max(1.0, p90 * (1 + self.margin)), 2),
+                       "memory_mb": int(min(self.max_memory_mb, mem * (1 + self.margin)))},
+                "source": f"history({len(per_job)} jobs)"}
+
+    def _opt_job_ps_cold_create_resource(self, req):
+        params = float(req.get("model_params", 0))
+        user = req.get("user")
+        metas = [r for r in self.store.query(metrics_type=MetricsType.JOB_META)
+                 if r["job_uuid"] != req.get("job_uuid") and (user is None or r["user"] == user)]
+        best = None
+        for m in metas:
+            p = float(m["metrics"].get("model_params", 0))
+            if p > 0 and params > 0:
+                d = abs(p - params) / max(p, params)
+                if best is None or d < best[0]:
+                    best = (d, m, p)
+        if best is not None and best[0] <= 0.5:
+            _d, m, p = best
+            ref = self._opt_job_ps_create_resource({"job_uuid": "", "job_name": m["job_name"]})
+            if ref.get("source", "").startswith("history"):
+                ratio = params / p
+                ps = dict(ref["ps"])
+                ps["memory_mb"] = int(min(self.max_memory_mb, ps["memory_mb"] * ratio))
+                ps["count"] = max(1, int(round(ps["count"] * max(1.0, ratio))))
+                return {"ps": ps, "source": f"similar({m['job_name']}, ratio {ratio:.2f})"}
+        return {"ps": {"count": int(req.get("default_ps", 1)), "cpu": self.default_cpu,
+                       "memory_mb": self.default_memory_mb}, "source": "default"}
+
+    def _opt_job_ps_init_adjust_resource(self, req):
+        max_steps = float(req.get("max_steps", 0))
+        out = {}
+        by_ps: Dict[str, List[Dict]] = {}
+        for r in self._usage(req, "ps"):
+            by_ps.setdefault(r["metrics"].get("node_name", "ps"), []).append(r["metrics"])
+        for name, ms in by_ps.items():
+            pts = [(float(m["step"]), float(m.get("memory_used_mb", 0))) for m in ms if "step" in m]
+            plan = {}
+            if len(pts) >= 2 and max_steps > 0:
+                n = len(pts)
+                mx = sum(p[0] for p in pts) / n
+                my = sum(p[1] for p in pts) / n
+                sxx = sum((p[0] - mx) ** 2 for p in pts)
+                slope = sum((p[0] - mx) * (p[1] - my) for p in pts) / sxx if sxx > 0 else 0.0
+                final = my + max(0.0, slope) * (max_steps - mx)
+                plan["memory_mb"] = int(min(self.max_memory_mb, max(pts[-1][1], final) * (1 + self.margin)))
+            last = ms[-1]
+            if last.get("cpu", 0) > 0:
+                plan["cpu"] = round(max(1.0, last.get("cpu_used", 0.0) * (1 + self.margin)), 2)
+            if plan:
+                out[name] = plan
+        return {"ps_nodes": out} if out else {}
+
+    def _opt_job_ps_resource_util(self, req):
+        low = float(req.get("low_threshold", 0.3))
+        min_cpu = float(req.get("min_cpu", 1.0))
+        latest: Dict[str, Dict] = {}
+        for r in self._usage(req, "ps"):
+            latest[r["metrics"].get("node_name", "ps")] = r["metrics"]
+        plan = {}
+        for name, m in latest.items():
+            cpu, used = float(m.get("cpu", 0)), float(m.get("cpu_used", 0))
+            if cpu > 0 and used / cpu < low:
+                plan[name] = {"cpu": round(max(min_cpu, used * (1 + self.margin)), 2)}
+        return {"ps_nodes": plan} if plan else {}
+
+    def _opt_job_ps_oom_resource(self, req):
+        ooms = [r["metrics"] for r in self.store.query(job_uuid=req["job_uuid"], metrics_type=MetricsType.OOM)
+                if r["metrics"].get("node_type") == "ps"]
+        if not ooms:
+            return {}
+        mem = max(o.get("memory_mb", self.default_memory_mb) for o in ooms)
+        return {"ps": {"memory_mb": int(min(self.max_memory_mb, mem * self.oom_factor))}}
+
+    def _opt_job_worker_create_oom_resource(self, req):
+        name = req.get("job_name") or self._job_name(req.get("job_uuid", ""))
+        ooms = [r["metrics"] for r in self.store.query(job_name=name, metrics_type=MetricsType.OOM)
+                if r["metrics"].get("node_type", "worker") == "worker"]
+        base = self._opt_job_create_resource(req)["worker"]
+        if not ooms:
+            return {"worker": base}
+        mem = max(o.get("memory_mb", 0) for o in ooms) * self.oom_factor
+        return {"worker": {"cpu": base["cpu"], "memory_mb": int(min(self.max_memory_mb, max(mem,
+                                                                                           base["memory_mb"])))}}
+
+    # ------------------------------------------------------- GPU host memory
+    def _opt_job_gpu_host_memory(self, req):
+        metas = [r["metrics"] for r in self.store.query(job_uuid=req["job_uuid"], metrics_type=MetricsType.JOB_META)]
+        ckpt = int(req.get("ckpt_bytes_per_node", 0)) or max((int(m.get("ckpt_bytes_per_node", 0)) for m in metas),
+                                                              default=0)
+        if ckpt <= 0:
+            return {}
+        slots = int(req.get("shm_slots", 2))
+        staging = int(req.get("pinned_staging_bytes", 0))
+        headroom = int(req.get("headroom_mb", 64 << 10))
+        mb = (ckpt * slots + staging) // (1 << 20) + headroom
+        return {"worker": {"memory_mb": int(min(self.max_memory_mb, mb))},
+                "detail": {"ckpt_mb": ckpt >> 20, "slots": slots, "headroom_mb": headroom}}
 
 
 class BrainService:

@@ -40,18 +40,35 @@ class JobResourceOptimizer(ABC):
 
 
 class AllreduceJobResourceOptimizer(JobResourceOptimizer):
-    def __init__(self, job_resource: JobResource, max_workers: int = 0, node_unit: int = 1):
+    """Worker count = alive nodes (replaced nodes come back), raised to what
+    the resource optimizer's speed curve recommends (``resource_optimizer``:
+    ``master/resource_optimizer.py``; scale-up only while the marginal
+    per-node throughput holds), capped at ``max_workers`` and whole
+    ``node_unit`` groups."""
+
+    def __init__(self, job_resource: JobResource, max_workers: int = 0, node_unit: int = 1,
+                 resource_optimizer=None):
         self._job_resource = job_resource
         self._max_workers = max_workers or job_resource.worker_num
         self._node_unit = max(1, node_unit)
         self._alive_node_num = 0
+        self.resource_optimizer = resource_optimizer
 
     def set_alive_node_num(self, n: int):
         self._alive_node_num = n
 
     def get_job_resource_plan(self) -> ResourcePlan:
         g = self._job_resource.get_node_group_resource(NodeType.WORKER) or NodeGroupResource()
-        target = min(self._max_workers, max(self._alive_node_num, g.count))
+        target = max(self._alive_node_num, g.count)
+        if self.resource_optimizer is not None:
+            from .resource_optimizer import OptimizeStage
+
+            rp = self.resource_optimizer.generate_opt_plan(OptimizeStage.RUNNING,
+                                                           {"current_workers": self._alive_node_num})
+            rg = rp.node_group_resources.get(NodeType.WORKER)
+            if rg is not None and rg.count > 0:
+                target = max(self._alive_node_num, rg.count)
+        target = min(self._max_workers, target)
         target = target // self._node_unit * self._node_unit
         plan = ResourcePlan()
         plan.node_group_resources[NodeType.WORKER] = NodeGroupResource(target, g.node_resource)
@@ -131,6 +148,10 @@ class AllreduceTrainingAutoScaler(JobAutoScaler):
 
     def adjust_once(self) -> Optional[ScalePlan]:
         alive = self._get_alive_worker_num()
+        ro = getattr(self._job_optimizer, "resource_optimizer", None)
+        speed = self._speed_monitor.running_speed() if self._speed_monitor is not None else 0.0
+        if ro is not None and speed > 0 and alive > 0:
+            ro.report_speed(alive, speed)  # one point of the speed-vs-workers curve
         self._job_optimizer.set_alive_node_num(alive)
         plan = self._job_optimizer.get_job_resource_plan()
         g = plan.node_group_resources.get(NodeType.WORKER)
@@ -189,12 +210,14 @@ class PSTrainingAutoScaler(JobAutoScaler):
 
 
 def new_job_auto_scaler(strategy: str, job_resource: JobResource, job_nodes, speed_monitor, worker_manager,
-                        node_scaler, enabled: bool = False, node_unit: int = 1) -> JobAutoScaler:
+                        node_scaler, enabled: bool = False, node_unit: int = 1, resource_optimizer=None,
+                        max_workers: int = 0) -> JobAutoScaler:
     from ..common.constants import DistributionStrategy
 
     if strategy == DistributionStrategy.PS:
         return PSTrainingAutoScaler(job_resource, job_nodes, PSJobResourceOptimizer(job_resource), node_scaler)
-    opt = AllreduceJobResourceOptimizer(job_resource, node_unit=node_unit)
+    opt = AllreduceJobResourceOptimizer(job_resource, max_workers=max_workers, node_unit=node_unit,
+                                        resource_optimizer=resource_optimizer)
     return AllreduceTrainingAutoScaler(job_resource, job_nodes, opt, speed_monitor, worker_manager, node_scaler,
                                        enabled=enabled)
 

@@ -33,7 +33,7 @@ class DistributedJobManager(JobManager):
                  max_relaunch_count: int = JobConstant.MAX_RESTART_DEFAULT,
                  heartbeat_timeout: float = JobConstant.NODE_HEARTBEAT_TIMEOUT, speed_monitor=None,
                  strategy: str = DistributionStrategy.ALLREDUCE, node_unit: int = 1, auto_worker: bool = False,
-                 poll_interval: float = 0.5):
+                 poll_interval: float = 0.5, resource_optimizer=None, max_workers: int = 0):
         super().__init__(job_resource.worker_num, None, heartbeat_timeout, max_relaunch_count)
         self.job_resource = job_resource
         self.job_nodes: Dict[str, Dict[int, Node]] = job_resource.init_job_node_meta(max_relaunch_count)
@@ -57,7 +57,9 @@ class DistributedJobManager(JobManager):
         self.speed_monitor = speed_monitor or SpeedMonitor()
         self.auto_scaler = new_job_auto_scaler(strategy, job_resource, self.job_nodes, self.speed_monitor,
                                                self.worker_manager, scaler, enabled=auto_worker,
-                                               node_unit=node_unit)
+                                               node_unit=node_unit, resource_optimizer=resource_optimizer,
+                                               max_workers=max_workers)
+        self.resource_optimizer = resource_optimizer
 
     # ----------------------------------------------------------- helpers
     def _new_node_id(self) -> int:

@@ -103,7 +103,8 @@ class DistributedJobMaster(JobMaster):
     def __init__(self, job_resource, scaler_factory, watcher_factory=None, port: int = 0,
                  loop_interval: float = 5.0, hang_secs: float = 1800.0, max_relaunch_count: int = 3,
                  heartbeat_timeout: float = 300.0, node_unit: int = 1, auto_worker: bool = False,
-                 stats_path: str = ""):
+                 stats_path: str = "", optimize_mode: str = "single-job", brain_addr: str = "",
+                 job_name: str = "local", max_workers: int = 0):
         from .dist_job_manager import DistributedJobManager
         from .event_callback import AllReduceNodeHandlingCallback, PsClusterVersionCallback, TaskRescheduleCallback
         from .stats import JobMetricCollector, LocalStatsReporter
@@ -113,9 +114,16 @@ class DistributedJobMaster(JobMaster):
         self.scaler = scaler_factory(f"127.0.0.1:{port}")
         watcher = watcher_factory(self.scaler) if watcher_factory else ProcessWatcher(self.scaler)
         speed = SpeedMonitor()
+        from .resource_optimizer import ResourceLimits, new_resource_optimizer
+
+        # single-job: the Brain algorithms over this master's metrics; cluster: the Brain service
+        self.resource_optimizer = new_resource_optimizer(
+            optimize_mode, f"{job_name}-{port}", job_name,
+            ResourceLimits(max_workers=max_workers, node_unit=node_unit), brain_addr=brain_addr or None)
         jm = DistributedJobManager(job_resource, self.scaler, watcher, max_relaunch_count=max_relaunch_count,
                                    heartbeat_timeout=heartbeat_timeout, speed_monitor=speed, node_unit=node_unit,
-                                   auto_worker=auto_worker)
+                                   auto_worker=auto_worker, resource_optimizer=self.resource_optimizer,
+                                   max_workers=max_workers)
         super().__init__(port=port, node_num=job_resource.worker_num, loop_interval=loop_interval,
                          hang_secs=hang_secs, max_relaunch_count=max_relaunch_count, job_manager=jm,
                          speed_monitor=speed)
@@ -177,6 +185,9 @@ def main(argv=None) -> int:
     p.add_argument("--max_relaunch_count", "--max-relaunch-count", type=int, default=3)
     p.add_argument("--log_dir", "--log-dir", default="")
     p.add_argument("--agent_args", "--agent-args", default="", help="extra dwamd-run flags (one string)")
+    p.add_argument("--optimize_mode", "--optimize-mode", default="single-job", choices=["single-job", "cluster"])
+    p.add_argument("--brain_addr", "--brain-addr", default="")
+    p.add_argument("--max_workers", "--max-workers", type=int, default=0)
     p.add_argument("entry", nargs=argparse.REMAINDER, help="training script + args (platform=process)")
     a = p.parse_args(argv)
     if a.platform == "process":
@@ -190,7 +201,8 @@ def main(argv=None) -> int:
         m = DistributedJobMaster(
             jr, lambda addr: ProcessScaler(a.job_name, addr, a.entry, a.nproc_per_node, str(a.node_num),
                                            a.log_dir, agent_args=shlex.split(a.agent_args)),
-            port=a.port, loop_interval=min(a.loop_interval, 5.0), max_relaunch_count=a.max_relaunch_count)
+            port=a.port, loop_interval=min(a.loop_interval, 5.0), max_relaunch_count=a.max_relaunch_count,
+            optimize_mode=a.optimize_mode, brain_addr=a.brain_addr, job_name=a.job_name, max_workers=a.max_workers)
     elif a.platform in ("k8s", "pyk8s"):
         # in-cluster: worker pods through the Kubernetes API (platform/k8s.py)
         import os
@@ -209,7 +221,8 @@ def main(argv=None) -> int:
             jr, lambda addr: PodScaler(a.job_name, cli, image, f"{svc}:{addr.rsplit(':', 1)[1]}", cmd,
                                        gpus_per_node=a.nproc_per_node),
             watcher_factory=lambda scaler: PodWatcher(a.job_name, cli), port=a.port,
-            loop_interval=a.loop_interval, max_relaunch_count=a.max_relaunch_count)
+            loop_interval=a.loop_interval, max_relaunch_count=a.max_relaunch_count,
+            optimize_mode=a.optimize_mode, brain_addr=a.brain_addr, job_name=a.job_name, max_workers=a.max_workers)
     else:
         m = JobMaster(port=a.port, node_num=a.node_num, loop_interval=a.loop_interval)
     m.prepare()
