@@ -92,7 +92,8 @@ def build_kernels(verbose=False, jobs=None):
         objs = list(ex.map(_compile_hip, srcs))
     out = kernels_lib_path()
     tmp = out + f".tmp{os.getpid()}"
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+    # hipBLASLt for the epilogue-fused GEMMs (gemm_epilogue.hip)
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ["-lhipblaslt"]
     o = _run(cmd)
     if verbose and o:
         print(o)

@@ -8,6 +8,8 @@ vp, i64, i32, u32, u64, f32, cp = (c.c_void_p, c.c_int64, c.c_int, c.c_uint32, c
 SIGS = {
     # ckpt_copy.hip
     "dw_multi_copy": (i32, [vp, i64, vp]),
+    "dw_gemm_dgelu": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),
+    "dw_gemm_dgelu_bgrad": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, vp]),
     "dw_multi_copy_grid": (i32, [vp, i64, i32, vp]),
     "dw_fill_u32": (i32, [vp, i64, u32, vp]),
     "dw_host_register": (i32, [vp, u64]),

@@ -11,6 +11,7 @@ vocab cross-entropy (all HIP).  Plain GEMMs go through hipBLASLt
 """
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -21,7 +22,12 @@ from ..ops.activation import bias_gelu
 from ..ops.attention import flash_attn_qkvpacked_func
 from ..ops.cross_entropy import cross_entropy
 from ..ops.linear import FusedLinear, linear
+from ..ops.mlp import fused_gelu_mlp
 from ..ops.norm import LayerNorm
+
+# epilogue-fused MLP (ops/mlp.py): measured equal to the bias-GELU kernel path on
+# GPT2-1.5B end to end (121.6 vs 122.2 ms/step, profiles/r2/gpt2_fused_mlp_ab.jsonl), so opt-in
+_FUSED_MLP = os.environ.get("DWAMD_FUSED_MLP", "0") == "1"
 
 
 @dataclass
@@ -71,6 +77,10 @@ class MLP(nn.Module):
         self.c_proj = FusedLinear(4 * cfg.n_embd, cfg.n_embd)
 
     def forward(self, x):
+        if _FUSED_MLP and x.is_cuda:
+            # bias + GELU in the c_fc GEMM's epilogue, dGELU + bias grad in the
+            # c_proj dgrad GEMM's epilogue (ops/mlp.py)
+            return fused_gelu_mlp(x, self.c_fc, self.c_proj)
         h = linear(x, self.c_fc.weight)  # bias fused into the activation kernel
         h = bias_gelu(h, self.c_fc.bias)
         return self.c_proj(h)
