@@ -263,9 +263,34 @@ def _apply_tensor_parallel(ctx, cfg):
 
 
 def _apply_sequence_parallel(ctx, cfg):
-    size = (cfg or {}).get("size", 0) if isinstance(cfg, dict) else (cfg or 0)
-    if size and size > 1 and adist.get_sequence_parallel_group() is None:
+    """Ulysses sequence parallel (ATorch ``SequenceParallelOptimization``):
+    ``{"sp_size": n, "module": cls | (cls, ...) | None, "set_sp_func_name":
+    "set_sp", "batch_sp_processing_fn": fn(batch, sp_size, sp_rank)}``.
+    Creates the SP groups (consecutive ranks: one xGMI-connected node), calls
+    ``set_sp(sp_size, sp_rank, sp_group)`` on the model (or on every module of
+    the given classes) and splits each batch along the sequence in
+    ``prepare_input``; the ranks of one SP group read the same batch."""
+    cfg = cfg if isinstance(cfg, dict) else {"sp_size": cfg or 0}
+    size = int(cfg.get("sp_size", cfg.get("size", 0)) or 0)
+    if size <= 1:
+        return
+    if adist.get_sequence_parallel_group() is None:
         adist.create_sequence_parallel_group(size)
+    group, rank = adist.get_sequence_parallel_group(), adist.get_sequence_parallel_rank()
+    fname = cfg.get("set_sp_func_name", "set_sp")
+    mods = cfg.get("module")
+    model = ctx["model"]
+    if mods is None:
+        targets = [model] if hasattr(model, fname) else []
+    else:
+        mods = tuple(mods) if isinstance(mods, (list, tuple)) else (mods,)
+        targets = [m for m in model.modules() if isinstance(m, mods)]
+    for m in targets:
+        getattr(m, fname)(size, rank, group)
+    if not targets:
+        logger.warning(f"sequence_parallel: no module with {fname}(); only the SP groups were created")
+    ctx["sp"] = (size, rank, cfg.get("batch_sp_processing_fn"))
+    logger.info(f"sequence_parallel: {size}-way, {len(targets)} {fname}() call(s)")
 
 
 def _wrap_cls(ctx, cfg):
@@ -499,6 +524,12 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
             (dist.get_world_size() if dist.is_initialized() else 1)
         dp_rank = dist.get_rank(dpg) if (dist.is_initialized() and dpg is not None) else \
             (dist.get_rank() if dist.is_initialized() else 0)
+        if ctx.get("sp") and dist.is_initialized() and dp_size == dist.get_world_size():
+            # the data group spans the SP groups (ATorch: SP is independent of
+            # DP): the ranks of one SP group share a batch -> one sampler
+            # replica per group (gradients still average over every rank)
+            sp = ctx["sp"][0]
+            dp_size, dp_rank = dp_size // sp, dp_rank // sp
         zg = ctx.get("zero_group")
         if zg is not None and dist.get_world_size(zg) > 1:
             # zero (sharding) ranks are data parallel too: each reads its own batch
@@ -515,6 +546,12 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
         dataloader = torch.utils.data.DataLoader(dataset, **dl_args)
 
     prep = prepare_input or _default_prepare_input
+    if ctx.get("sp") and ctx["sp"][2] is not None:
+        sp_size, sp_rank, sp_fn = ctx["sp"]
+        base_prep = prep
+
+        def prep(data, device, _b=base_prep):  # noqa: F811
+            return sp_fn(_b(data, device), sp_size, sp_rank)
     result = AutoAccelerateResult(model=model, optim=optim, dataloader=dataloader, loss_func=loss_func,
                                   prepare_input=prep, lr_scheduler=sched,
                                   args={"model_input_format": model_input_format,

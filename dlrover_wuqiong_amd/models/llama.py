@@ -218,6 +218,14 @@ class Llama(nn.Module):
     def num_params(self):
         return sum(p.numel() for p in self.parameters())
 
+    def set_sp(self, sp_size: int, sp_rank: int, sp_group):
+        """Switch to Ulysses sequence parallel after construction (ATorch
+        ``set_sp`` interface): forward then takes this rank's sequence shard."""
+        g = sp_group if sp_size > 1 else None
+        self.sp_group = g
+        for layer in self.layers:
+            layer.self_attn.sp_group = g
+
     def forward(self, ids, targets=None):
         B, S = ids.shape
         sp = _ws(self.sp_group)

@@ -258,3 +258,69 @@ def test_four_rank_hsdp():
     for p in ps:
         p.join(timeout=30)
     assert [r[1] for r in res] == [True] * 4, res
+
+
+def _sp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    try:
+        from dlrover_wuqiong_amd.atorch import distributed as adist
+        from dlrover_wuqiong_amd.atorch.auto_accelerate import auto_accelerate
+        from dlrover_wuqiong_amd.models.llama import Llama, LlamaConfig
+
+        adist.init_distributed("gloo")
+
+        class LM(Llama):
+            def forward(self, ids, labels=None):
+                return super().forward(ids, labels)
+
+        class Tok(torch.utils.data.Dataset):
+            def __len__(self):
+                return 8
+
+            def __getitem__(self, i):
+                g = torch.Generator().manual_seed(i)
+                ids = torch.randint(0, 1024, (17,), generator=g)
+                return {"ids": ids[:-1], "labels": ids[1:]}
+
+        def split(batch, sp_size, sp_rank):
+            n = batch["ids"].shape[1] // sp_size
+            return {k: v[:, sp_rank * n:(sp_rank + 1) * n] for k, v in batch.items()}
+
+        torch.manual_seed(0)
+        cfg = LlamaConfig.named("llama-tiny")
+        full = LM(cfg)
+        torch.manual_seed(0)
+        ok, res, strat = auto_accelerate(
+            LM(cfg), torch.optim.SGD, dataset=Tok(), loss_func=lambda b, out: out, optim_args={"lr": 0.1},
+            dataloader_args={"batch_size": 2, "shuffle": False}, model_input_format="unpack_dict",
+            load_strategy=["parallel_mode", ("sequence_parallel", {"sp_size": 2, "batch_sp_processing_fn": split})])
+        batch = next(iter(res.dataloader))
+        shard = res.prepare_input(batch, torch.device("cpu"))
+        loss = res.model(**shard)
+        # both SP ranks got the same batch; the mean of their shard losses is the full-sequence loss
+        lt = loss.detach().clone()
+        dist.all_reduce(lt)
+        ref = full(batch["ids"], batch["labels"])
+        q.put((rank, bool(abs(float(lt) / 2 - float(ref)) < 1e-4 and shard["ids"].shape[1] == 8
+                          and len(res.dataloader) == 4), strat.names()))
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        traceback.print_exc()
+        q.put((rank, repr(e), None))
+    finally:
+        adist.reset_distributed()
+
+
+def test_two_rank_sequence_parallel_strategy():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_sp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in ps), key=lambda x: x[0])
+    for p in ps:
+        p.join(timeout=30)
+    assert all(r[1] is True for r in res), res
