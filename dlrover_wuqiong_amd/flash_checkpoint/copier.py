@@ -334,6 +334,8 @@ class GpuCopier:
         self._ext = None  # HbmBuffer staging owned by a standby (hbm_tier.py)
         self._ext_key = None
         self._futures: List[Optional[Future]] = [None, None]
+        self._flush_t0: List[float] = [0.0, 0.0]  # when each staging buffer's flush began moving bytes (0: not yet)
+        self._flush_n: List[int] = [0, 0]
         self._nbuf = 0  # decided at the first snapshot
         self._next_stage = 0
         self.staging_reserve = int(os.environ.get("DWAMD_STAGING_RESERVE_GB", "24")) << 30
@@ -460,6 +462,32 @@ class GpuCopier:
             f.result()
             self._futures[self._next_stage] = None
 
+    def stage_busy_eta(self) -> float:
+        """Seconds until the staging buffer the next snapshot uses is free:
+        0 when idle; its flush's remaining bytes at the measured D2H rate when
+        moving; +inf while that flush still waits (queue / shm preparation)."""
+        if self._use_ring_cached():
+            return 0.0
+        idx = self._next_stage if self._nbuf > 1 else 0
+        f = self._futures[idx] if idx < len(self._futures) else None
+        if self._nbuf <= 1:
+            pend = [i for i, x in enumerate(self._futures) if x is not None and not x.done()]
+            if not pend:
+                return 0.0
+            idx = pend[-1]
+            f = self._futures[idx]
+        if f is None or f.done():
+            return 0.0
+        t0 = self._flush_t0[idx]
+        if t0 <= 0.0:
+            return float("inf")
+        recent = self.flush_stats[-4:]
+        rate = (sum(n for n, _ in recent) / max(1e-6, sum(t for _, t in recent))) if recent else 50e9
+        return max(0.0, self._flush_n[idx] / rate - (time.perf_counter() - t0))
+
+    def _use_ring_cached(self) -> bool:
+        return self._ring_decision is not None and self._ring_decision[1]
+
     def busy(self) -> bool:
         return any(f is not None and not f.done() for f in self._futures)
 
@@ -568,6 +596,7 @@ class GpuCopier:
                 with torch.cuda.stream(self.side_stream):
                     self.side_stream.wait_event(ev)  # device-side dependency only
                     t0 = time.perf_counter()
+                    self._flush_t0[idx], self._flush_n[idx] = t0, n
                     dst = shm_payload_addr + lo
                     src = stg.data_ptr()
                     sp = ctypes.c_void_p(self.side_stream.cuda_stream)
@@ -591,6 +620,7 @@ class GpuCopier:
                 _check(_kern().dw_stream_sync(ctypes.c_void_p(self.side_stream.cuda_stream)), "flush sync")
             on_done()
 
+        self._flush_t0[idx] = 0.0
         if sync:
             self.wait()
             flush()

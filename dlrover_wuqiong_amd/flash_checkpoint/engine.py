@@ -170,6 +170,7 @@ class CheckpointEngine(ABC):
         self._layout: Optional[Layout] = None
         self._layout_key = None
         self._held_slots = set()  # slots whose lock this process holds until their flush lands
+        self.skipped_saves = 0  # saves skipped while the previous snapshot was still flushing
         self._gc_frozen = False
         self._generation = 0
         self._shm_prep = None  # Future: background prefault + pin of this rank's slot slices
@@ -382,7 +383,41 @@ class CheckpointEngine(ABC):
             if enabled:
                 gc.enable()
 
+    def _skip_busy(self) -> bool:
+        """Reference semantics (a save is skipped while the previous one is
+        still being written): skip when the staging buffer this snapshot needs
+        is still flushing and would not be free within DWAMD_CKPT_MAX_WAIT_MS
+        (``DWAMD_CKPT_BUSY=wait`` blocks instead).  Decided collectively so
+        every rank skips the same saves."""
+        if os.environ.get("DWAMD_CKPT_BUSY", "skip") != "skip" or getattr(self, "_storage_save", False):
+            return False
+        c = self._copier
+        eta = c.stage_busy_eta() if c is not None else 0.0
+        busy = 1 if eta * 1000.0 > float(os.environ.get("DWAMD_CKPT_MAX_WAIT_MS", "250")) else 0
+        if dist.is_available() and dist.is_initialized() and self._ctl_group is not None:
+            t = torch.tensor([busy], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self._ctl_group)
+            busy = int(t)
+        if busy:
+            self.skipped_saves += 1
+            if self.skipped_saves <= 3 or self.skipped_saves % 50 == 0:
+                logger.info(f"rank {self._rank}: memory checkpoint skipped, the previous one is still being "
+                            f"written to shm ({self.skipped_saves} skipped so far)")
+        return bool(busy)
+
+    def precheck_skip(self) -> bool:
+        """Collective busy check a checkpointer runs BEFORE building an
+        expensive state dict (FSDP DCP payload); the save that follows does
+        not vote again."""
+        skip = self._skip_busy()
+        self._prechecked = not skip
+        return skip
+
     def _save_state_dict_to_memory(self, state_dict: Dict, conf: CheckpointConfig) -> bool:
+        if getattr(self, "_prechecked", False):
+            self._prechecked = False
+        elif self._skip_busy():
+            return False
         if not self._replicated and self._local_rank != self.local_shard_id:
             # not a saving rank (e.g. a data-parallel replica of a TP/PP shard):
             # still takes part in the slot vote of the saving ranks
@@ -795,7 +830,11 @@ class FullCheckpointEngine(CheckpointEngine):
     def save_to_storage(self, step, state_dict, paths):
         ok = True
         if step > self._cached_step:
-            ok = self.save_to_memory(step, state_dict, paths)
+            self._storage_save = True  # a requested persist waits for a busy staging buffer
+            try:
+                ok = self.save_to_memory(step, state_dict, paths)
+            finally:
+                self._storage_save = False
         if dist.is_available() and dist.is_initialized():
             dist.barrier(group=self._ctl_group)
         if ok:

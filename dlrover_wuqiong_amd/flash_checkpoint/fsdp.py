@@ -244,7 +244,11 @@ class FsdpCheckpointEngine(ShardCheckpointEngine):
     def save_to_storage(self, step, state_dict, paths):
         ok = True
         if step > self._cached_step:
-            ok = self.save_to_memory(step, state_dict, paths)
+            self._storage_save = True  # a requested persist waits for a busy staging buffer
+            try:
+                ok = self.save_to_memory(step, state_dict, paths)
+            finally:
+                self._storage_save = False
         if dist.is_available() and dist.is_initialized():
             dist.barrier(group=self._ctl_group)
         if ok:
@@ -364,6 +368,8 @@ class FsdpShardCheckpointer(Checkpointer):
 
     def save_checkpoint(self, step, model, optimizer, extra_sd=None, path="", storage_type=StorageType.DISK):
         path = path or os.path.join(self.checkpoint_dir, str(step))
+        if storage_type == StorageType.MEMORY and self._engine.precheck_skip():
+            return False  # previous snapshot still flushing: do not even build the DCP payload
         sd = self._state(model, optimizer, extra_sd)
         paths = {DCP_KEY: path}
         if storage_type == StorageType.MEMORY:

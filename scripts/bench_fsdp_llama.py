@@ -112,7 +112,7 @@ def main():
     setup_s = time.perf_counter() - ts
     ck.wait_latest_checkpoint()
     print(f"setup save {setup_s:.2f} s", file=sys.stderr, flush=True)
-    pauses, steps, losses = [], [], []
+    pauses, steps, losses, landed = [], [], [], []
     for i in range(a.steps):
         t0 = time.perf_counter()
         losses.append(float(step(i).item()))
@@ -126,15 +126,17 @@ def main():
                 prof = cProfile.Profile()
                 prof.enable()
             t0 = time.perf_counter()
-            ck.save_checkpoint(i + 1, model, opt, storage_type=StorageType.MEMORY)
+            ok = ck.save_checkpoint(i + 1, model, opt, storage_type=StorageType.MEMORY)
             sync()
             pauses.append(time.perf_counter() - t0)
+            landed.append(bool(ok))
             if prof is not None:
                 import pstats
 
                 prof.disable()
                 pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(30)
     last = a.steps
+    ck.wait_latest_checkpoint()  # the final save must not be skipped as busy
     ck.save_checkpoint(last + 1, model, opt, storage_type=StorageType.MEMORY)  # final state, untimed
     ck.wait_latest_checkpoint()
     if cuda:
@@ -164,6 +166,10 @@ def main():
             "config": {"model": a.model, "seq_len": a.seq, "micro_batch": a.micro_batch,
                        "strategy": str(strategy)[:300]},
             "save_sec": [round(x, 4) for x in pauses], "setup_save_s": round(setup_s, 2),
+            "saves_landed": landed, "pause_landed_mean_s": round(
+                sum(p for p, ok in zip(pauses, landed) if ok) / max(1, sum(landed)), 4),
+            "flush_gbps": round(sum(n for n, _ in ck.engine._copier.flush_stats) / max(1e-9, sum(
+                t for _, t in ck.engine._copier.flush_stats)) / 1e9, 1) if getattr(ck.engine, "_copier", None) else None,
             "load_sec": round(load_s, 3), "load_verified": bool(verified), "ckpt_bytes_per_rank": nbytes,
             "train_step_ms": round(1000 * sorted(steps)[len(steps) // 2], 1),
             "tokens_per_s": round(world * a.micro_batch * a.seq / sorted(steps)[len(steps) // 2], 1),

@@ -5,6 +5,12 @@ import uuid
 import pytest
 
 
+# Tests save back to back and assert every save lands: block on a busy
+# staging buffer instead of the production default (skip the save, reference
+# semantics); test_flash_ckpt_gpu::test_gpu_busy_save_is_skipped covers "skip".
+os.environ.setdefault("DWAMD_CKPT_BUSY", "wait")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: long-running test")

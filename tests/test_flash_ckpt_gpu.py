@@ -2,6 +2,7 @@
 in-place H2D restore, single process (real HIP)."""
 
 import os
+import time
 
 import pytest
 import torch
@@ -377,3 +378,29 @@ def test_gpu_flat_ddp_bucketed_allreduce_matches_manual_sum():
     for p in ps:
         p.join(timeout=60)
     assert all(isinstance(d, float) and d == 0.0 for _, d in res), res
+
+
+def test_gpu_busy_save_is_skipped(tmp_path, monkeypatch):
+    """Production policy: a memory save whose staging buffer is still being
+    flushed is skipped (returns False, nothing blocks); a storage save waits."""
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+
+    monkeypatch.setenv("DWAMD_CKPT_BUSY", "skip")
+    monkeypatch.setenv("DWAMD_CKPT_MAX_WAIT_MS", "0")
+    monkeypatch.setenv("DWAMD_STAGING_BUFFERS", "1")  # one staging buffer: the 2nd save finds it flushing
+    w = torch.randn(512 << 20, device="cuda", dtype=torch.bfloat16)  # 1 GiB
+    ck = DdpCheckpointer(str(tmp_path / "ck"))
+    assert ck.save_checkpoint(1, {"w": w}, storage_type=StorageType.MEMORY)
+    t0 = time.perf_counter()
+    ok2 = ck.save_checkpoint(2, {"w": w}, storage_type=StorageType.MEMORY)
+    dt = time.perf_counter() - t0
+    assert ok2 is False and dt < 0.5 and ck.engine.skipped_saves == 1
+    assert ck.save_checkpoint(3, {"w": w}, storage_type=StorageType.DISK)  # waits instead
+    ck.wait_latest_checkpoint()
+    w.zero_()
+    target = {"w": w}
+    ck.load_checkpoint(target=target)
+    torch.cuda.synchronize()
+    assert target["w"].abs().sum().item() > 0
+    ck.close()
