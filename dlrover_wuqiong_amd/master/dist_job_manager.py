@@ -77,6 +77,31 @@ class DistributedJobManager(JobManager):
     def start_auto_scaling(self):
         self.auto_scaler.start_auto_scaling()
 
+    def apply_scale_plan(self, plan: ScalePlan) -> ScalePlan:
+        """Manual scaling (a ScalePlan from the user / the K8s ScalePlan
+        watcher): per-type target counts go through the node managers (new
+        nodes get ids and ranks, surplus nodes are removed); explicit removals
+        are passed through."""
+        out = ScalePlan()
+        for t, g in plan.node_group_resources.items():
+            mgr = self._managers.get(t)
+            if mgr is None or g.count <= 0:
+                continue
+            cur = self.job_resource.get_node_group_resource(t)
+            res = cur.node_resource if cur is not None else g.node_resource
+            if g.node_resource.memory or g.node_resource.cpu or g.node_resource.gpu_num:
+                res = g.node_resource
+            self.job_resource.update_node_group_resource(t, g.count, res.cpu, res.memory)
+            if t == NodeType.WORKER:
+                out.merge(self.worker_manager.adjust_worker(self.job_resource.get_node_group_resource(t)))
+        for n in plan.remove_nodes:
+            for mgr in self._managers.values():
+                if n.id in getattr(mgr, "_nodes", {}):
+                    out.merge(mgr.remove_node(n.id))
+        if not out.empty():
+            self._scaler.scale(out)
+        return out
+
     def all_critical_node_completed(self) -> bool:
         crit = [n for ns in self.job_nodes.values() for n in ns.values() if n.critical and not n.is_released]
         return all(n.status in (NodeStatus.SUCCEEDED, NodeStatus.FINISHED) for n in crit)

@@ -209,7 +209,7 @@ def main(argv=None) -> int:
         import shlex
 
         from ..common.node import JobResource
-        from ..platform.k8s import K8sClient, PodScaler, PodWatcher
+        from ..platform.k8s import ElasticJobScaler, K8sClient, K8sScalePlanWatcher, PodScaler, PodWatcher
 
         jr = JobResource()
         jr.update_node_group_resource("worker", a.node_num)
@@ -217,12 +217,27 @@ def main(argv=None) -> int:
         svc = f"elasticjob-{a.job_name}-dlrover-master"
         image = os.environ.get("DWAMD_WORKER_IMAGE", "")
         cmd = shlex.split(os.environ.get("DWAMD_WORKER_COMMAND", "dwamd-run --nnodes auto train.py"))
+        if a.platform == "k8s":
+            # the ElasticJob operator creates / deletes pods from our ScalePlans
+            scaler_factory = lambda addr: ElasticJobScaler(a.job_name, cli)  # noqa: E731
+        else:
+            # pyk8s: the master creates the pods itself
+            scaler_factory = lambda addr: PodScaler(a.job_name, cli, image,  # noqa: E731
+                                                    f"{svc}:{addr.rsplit(':', 1)[1]}", cmd,
+                                                    gpus_per_node=a.nproc_per_node)
         m = DistributedJobMaster(
-            jr, lambda addr: PodScaler(a.job_name, cli, image, f"{svc}:{addr.rsplit(':', 1)[1]}", cmd,
-                                       gpus_per_node=a.nproc_per_node),
+            jr, scaler_factory,
             watcher_factory=lambda scaler: PodWatcher(a.job_name, cli), port=a.port,
             loop_interval=a.loop_interval, max_relaunch_count=a.max_relaunch_count,
             optimize_mode=a.optimize_mode, brain_addr=a.brain_addr, job_name=a.job_name, max_workers=a.max_workers)
+        # manual ScalePlans (spec.manualScaling) of this job -> the job manager
+        sp_watcher = K8sScalePlanWatcher(a.job_name, cli)
+
+        def _manual_scaling():
+            for plan in sp_watcher.watch(interval=a.loop_interval):
+                m.job_manager.apply_scale_plan(plan)
+
+        threading.Thread(target=_manual_scaling, daemon=True, name="dwamd-scaleplan-watcher").start()
     else:
         m = JobMaster(port=a.port, node_num=a.node_num, loop_interval=a.loop_interval)
     m.prepare()

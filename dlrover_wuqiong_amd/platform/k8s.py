@@ -224,6 +224,112 @@ class PodWatcher(NodeWatcher):
             yield NodeEvent(t, pod_to_node(ev.get("object", {})))
 
 
+class ElasticJobScaler(Scaler):
+    """Master -> operator: every ScalePlan of the job master becomes a
+    ``ScalePlan`` custom object (``createPods`` / ``removePods`` /
+    ``replicaResourceSpecs``) that the operator applies (vs ``PodScaler``,
+    which creates the pods itself).  Parity: reference
+    ``master/scaler/elasticjob_scaler.py``."""
+
+    def __init__(self, job_name: str, client: K8sClient):
+        super().__init__(job_name)
+        self.client = client
+        self._n = 0
+
+    @staticmethod
+    def _res(node: Node) -> Dict:
+        r: NodeResource = node.config_resource
+        out = {}
+        if r.gpu_num:
+            out["amd.com/gpu"] = str(r.gpu_num)
+        if r.cpu:
+            out["cpu"] = str(r.cpu)
+        if r.memory:
+            out["memory"] = f"{r.memory}Mi"
+        return out
+
+    def plan_object(self, plan: ScalePlan) -> Dict:
+        self._n += 1
+        spec: Dict = {"ownerJob": self.job_name, "manualScaling": False}
+        if plan.node_group_resources:
+            spec["replicaResourceSpecs"] = {
+                t: {"replicas": int(g.count),
+                    "resource": {k: v for k, v in (("cpu", g.node_resource.cpu),
+                                                   ("memory", f"{g.node_resource.memory}Mi"
+                                                    if g.node_resource.memory else 0),
+                                                   ("amd.com/gpu", g.node_resource.gpu_num)) if v}}
+                for t, g in plan.node_group_resources.items()}
+        if plan.launch_nodes:
+            spec["createPods"] = [{"name": pod_name(self.job_name, n.type, n.id), "type": n.type, "id": n.id,
+                                   "rankIndex": n.rank_index, "resource": self._res(n)} for n in plan.launch_nodes]
+        if plan.remove_nodes:
+            spec["removePods"] = [{"name": pod_name(self.job_name, n.type, n.id), "type": n.type, "id": n.id}
+                                  for n in plan.remove_nodes]
+        return {"apiVersion": f"{GROUP}/{VERSION}", "kind": "ScalePlan",
+                "metadata": {"name": f"{self.job_name}-{int(time.time())}-{self._n}",
+                             "labels": {JOB_LABEL: self.job_name, "scale-type": "auto"}},
+                "spec": spec}
+
+    def scale(self, plan: ScalePlan):
+        if plan is None or plan.empty():
+            return
+        obj = self.plan_object(plan)
+        logger.info(f"k8s: ScalePlan {obj['metadata']['name']} for ElasticJob {self.job_name}")
+        self.client.create_custom("scaleplans", obj)
+
+
+class K8sScalePlanWatcher:
+    """Manual scaling: ``ScalePlan`` objects of this job with
+    ``spec.manualScaling: true`` become master-side ScalePlans (replica
+    counts / resources per node type, explicit pod removals); each is
+    consumed once (status ``Succeeded``).  Parity: reference
+    ``master/watcher/k8s_watcher.py:267`` (``K8sScalePlanWatcher``)."""
+
+    def __init__(self, job_name: str, client: K8sClient):
+        self.job_name, self.client = job_name, client
+
+    @staticmethod
+    def _mem_mb(v) -> int:
+        s = str(v)
+        for suf, mul in (("Gi", 1024), ("Mi", 1), ("G", 1000), ("M", 1)):
+            if s.endswith(suf):
+                return int(float(s[:-len(suf)]) * mul)
+        return int(float(s)) // (1 << 20) if s else 0
+
+    def to_plan(self, obj: Dict) -> ScalePlan:
+        from ..common.node import NodeGroupResource
+
+        sp = ScalePlan()
+        for t, v in (obj.get("spec", {}).get("replicaResourceSpecs") or {}).items():
+            r = v.get("resource") or {}
+            sp.node_group_resources[t] = NodeGroupResource(
+                int(v.get("replicas", 0)),
+                NodeResource(cpu=float(r.get("cpu", 0) or 0), memory=self._mem_mb(r.get("memory", 0) or 0),
+                             gpu_num=int(r.get("amd.com/gpu", r.get("gpu", 0)) or 0)))
+        for p in obj.get("spec", {}).get("removePods") or []:
+            sp.remove_nodes.append(Node(type=p.get("type", NodeType.WORKER), id=int(p.get("id", 0)),
+                                        name=p.get("name", "")))
+        return sp
+
+    def poll(self) -> List[ScalePlan]:
+        out = []
+        for obj in self.client.list_custom("scaleplans"):
+            spec, st = obj.get("spec", {}), obj.get("status") or {}
+            if spec.get("ownerJob") != self.job_name or not spec.get("manualScaling") or st.get("phase") in (
+                    "Succeeded", "Failed"):
+                continue
+            out.append(self.to_plan(obj))
+            self.client.patch_custom_status("scaleplans", obj["metadata"]["name"], {"phase": "Succeeded"})
+        return out
+
+    def watch(self, interval: float = 5.0, stop: Optional[threading.Event] = None) -> Iterator[ScalePlan]:
+        stop = stop or threading.Event()
+        while not stop.is_set():
+            for p in self.poll():
+                yield p
+            stop.wait(interval)
+
+
 # ----------------------------------------------------------------------------- operator
 
 

@@ -247,3 +247,69 @@ def test_deploy_manifests():
     assert ex["apiVersion"] == f"{GROUP}/{VERSION}" and ex["kind"] == "ElasticJob"
     limits = ex["spec"]["replicaSpecs"]["worker"]["template"]["spec"]["containers"][0]["resources"]["limits"]
     assert limits["amd.com/gpu"] == 8
+
+
+def test_elasticjob_scaler_to_operator_and_manual_scaleplan_watcher(k8s):
+    from dlrover_wuqiong_amd.common.node import Node, NodeGroupResource, NodeResource
+    from dlrover_wuqiong_amd.master.scaler import ScalePlan
+    from dlrover_wuqiong_amd.platform.k8s import ElasticJobOperator, ElasticJobScaler, K8sScalePlanWatcher
+
+    fake, cli = k8s
+    tmpl = {"spec": {"containers": [{"name": "main", "image": "train:1"}]}}
+    cli.create_custom("elasticjobs", {"metadata": {"name": "j3"},
+                                      "spec": {"replicaSpecs": {"worker": {"replicas": 1, "template": tmpl}}}})
+    sc = ElasticJobScaler("j3", cli)
+    n = Node(id=4, rank_index=2)
+    n.config_resource = NodeResource(gpu_num=8, memory=1024)
+    sc.scale(ScalePlan(launch_nodes=[n], node_group_resources={"worker": NodeGroupResource(3, NodeResource(gpu_num=8))}))
+    plans = cli.list_custom("scaleplans")
+    assert len(plans) == 1 and plans[0]["spec"]["createPods"][0]["rankIndex"] == 2
+    assert plans[0]["spec"]["replicaResourceSpecs"]["worker"]["replicas"] == 3
+    ElasticJobOperator(cli, "img").reconcile_once()
+    pod = cli.get_pod("j3-worker-4")
+    assert pod is not None and pod["spec"]["containers"][0]["resources"]["limits"]["amd.com/gpu"] == "8"
+    # a manual plan by the user -> a master-side ScalePlan, consumed once
+    cli.create_custom("scaleplans", {"metadata": {"name": "manual-1"},
+                                     "spec": {"ownerJob": "j3", "manualScaling": True,
+                                              "replicaResourceSpecs": {"worker": {"replicas": 5, "resource": {
+                                                  "memory": "64Gi", "amd.com/gpu": 8}}},
+                                              "removePods": [{"type": "worker", "id": 1}]}})
+    w = K8sScalePlanWatcher("j3", cli)
+    got = w.poll()
+    assert len(got) == 1 and got[0].node_group_resources["worker"].count == 5
+    assert got[0].node_group_resources["worker"].node_resource.memory == 65536 and got[0].remove_nodes[0].id == 1
+    assert w.poll() == []
+
+
+def test_dist_job_manager_applies_manual_plan():
+    from dlrover_wuqiong_amd.common.constants import NodeStatus
+    from dlrover_wuqiong_amd.common.node import JobResource, Node, NodeGroupResource, NodeResource
+    from dlrover_wuqiong_amd.master.dist_job_manager import DistributedJobManager
+    from dlrover_wuqiong_amd.master.scaler import ScalePlan, Scaler
+    from dlrover_wuqiong_amd.master.watcher import NodeWatcher
+
+    class Rec(Scaler):
+        def __init__(self):
+            super().__init__("j")
+            self.plans = []
+
+        def scale(self, plan):
+            self.plans.append(plan)
+
+    class W(NodeWatcher):
+        def list(self):
+            return []
+
+        def watch(self):
+            return iter(())
+
+    jr = JobResource()
+    jr.node_group_resources["worker"] = NodeGroupResource(2, NodeResource(gpu_num=8))
+    rec = Rec()
+    jm = DistributedJobManager(jr, rec, W())
+    for n in jm.nodes.values():
+        n.status = NodeStatus.RUNNING
+    out = jm.apply_scale_plan(ScalePlan(node_group_resources={"worker": NodeGroupResource(4, NodeResource())}))
+    assert len(out.launch_nodes) == 2 and rec.plans
+    out = jm.apply_scale_plan(ScalePlan(remove_nodes=[Node(id=0)]))
+    assert [n.id for n in out.remove_nodes] == [0]
