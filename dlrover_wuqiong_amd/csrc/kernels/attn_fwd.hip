@@ -86,12 +86,21 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   const bf16_t* Vb = V + (int64_t)b * st.v_bs + (int64_t)sr.k_off * st.v_rs + (int64_t)hk * D;
 
   // ---- Q fragments (B operand of S^T): lane holds Q[q0 + r][16 kk + 8 hh .. +7]
+  // Q is prescaled by softmax_scale * log2(e) once (guide: operand prescale),
+  // so the scores come out of the MFMA already in the exp2 domain
   u32x4 qf[C::KK];
   {
     const int q = q0 + r;
 #pragma unroll
-    for (int kk = 0; kk < C::KK; ++kk)
-      qf[kk] = (q < SQ) ? *(const u32x4*)(Qb + (int64_t)q * st.q_rs + 16 * kk + 8 * hh) : (u32x4){0, 0, 0, 0};
+    for (int kk = 0; kk < C::KK; ++kk) {
+      const u32x4 raw =
+          (q < SQ) ? *(const u32x4*)(Qb + (int64_t)q * st.q_rs + 16 * kk + 8 * hh) : (u32x4){0, 0, 0, 0};
+      float f[8];
+      unpack8(raw, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] *= scale_log2;
+      qf[kk] = (u32x4){pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7])};
+    }
   }
 
   f32x16 o[C::DT];
@@ -99,7 +108,14 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
     for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
-  float m_i = -INFINITY, l_i = 0.f;  // l_i: this lane-half's partial row sum
+  // m_i: the row's reference offset (exp2 domain), only raised when a tile's
+  // max exceeds it by more than RESCALE_T (deferred rescale, guide T13): p
+  // may reach 2^RESCALE_T, harmless in fp32 / bf16, and O / l are rescaled
+  // on a handful of tiles instead of nearly every one.  l_i: this
+  // lane-half's partial row sum.
+  constexpr float RESCALE_T = 8.f;
+  float m_i = 0.f, l_i = 0.f;
+  bool seeded = false;  // the row's offset was set from its first visible scores
 
   int n_tiles = (SK + C::BK - 1) / C::BK;
   if (CAUSAL) {
@@ -149,12 +165,14 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
     // a wave whose 32 queries all lie before this tile has nothing to do here
     const bool active = !CAUSAL || (k0 <= q0 + 31 + co);
     if (active) {
-      // ---- S^T = K Q^T : two 32-key subtiles
+      // ---- S'^T = K Q'^T - m : two 32-key subtiles; the accumulator starts at
+      // -m_i (row constant as the initial accumulator), so p = exp2(S') needs
+      // no subtraction
       f32x16 s[2];
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) s[sb][i] = 0.f;
+        for (int i = 0; i < 16; ++i) s[sb][i] = -m_i;
 #pragma unroll
         for (int kk = 0; kk < C::KK; ++kk) {
           const u32x4 kf = *(const u32x4*)(kl + img_off<D>(32 * sb + r, 2 * kk + hh));
@@ -162,12 +180,9 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
         }
       }
 
-      // ---- online softmax: lane = query q0 + r, its 32 keys in registers.
-      // The max runs on the raw scores (scale > 0) and the scale is folded
-      // into the exponent's FMA: p = exp2(s * c - m * c).
+      // ---- online softmax: lane = query q0 + r, its 32 keys in registers
       const int q = q0 + r;
       const bool need_mask = (k0 + C::BK > SK) || (CAUSAL && (k0 + C::BK - 1 > q0 + co));
-      float mx = -INFINITY;
       if (need_mask) {
         // keys < lim are visible to this lane's query (branch-free selects)
         const int lim = CAUSAL ? min(SK, q + co + 1) : SK;
@@ -179,29 +194,36 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
             s[sb][i] = key < lim ? s[sb][i] : -INFINITY;
           }
       }
+      float mx = -INFINITY;
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[sb][i]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;
-      if (!__all(mx <= m_i)) {
-        // some row's max grew: rescale O and l (exact; skipped otherwise)
-        const float m_new = fmaxf(m_i, mx);
-        const float alpha = (m_new == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m_i - m_new);
-        m_i = m_new;
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));  // the row's max above its offset
+      // move the offset of the rows that outgrew it, and seed it from the
+      // first visible scores of a row (they may sit far below 0); O and l follow
+      const bool shift = (mx > RESCALE_T) || (!seeded && mx > -INFINITY);
+      seeded = seeded || (mx > -INFINITY);
+      if (__any(shift)) {
+        const float d = shift ? mx : 0.f;
+        const float alpha = __builtin_amdgcn_exp2f(-d);
+        m_i += d;
         l_i *= alpha;
 #pragma unroll
         for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
           for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) s[sb][i] -= d;
       }
-      const float m_use = (m_i == -INFINITY) ? 0.f : m_i;
       float rs = 0.f;
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[sb][i], scale_log2, -m_use));
+          const float p = __builtin_amdgcn_exp2f(s[sb][i]);
           s[sb][i] = p;
           rs += p;
         }

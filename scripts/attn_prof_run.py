@@ -7,12 +7,17 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dlrover_wuqiong_amd.ops.attention import flash_attn_func  # noqa: E402
 
-for spec in sys.argv[1:]:
+fwd_only = "--fwd" in sys.argv
+for spec in [a for a in sys.argv[1:] if not a.startswith("--")]:
     B, S, H, HKV, D = map(int, spec.split(","))
     q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     k = torch.randn(B, S, HKV, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     v = torch.randn(B, S, HKV, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     for _ in range(5):
+        if fwd_only:
+            with torch.no_grad():
+                o = flash_attn_func(q, k, v, causal=True)
+            continue
         o = flash_attn_func(q, k, v, causal=True)
         o.backward(torch.ones_like(o))
     torch.cuda.synchronize()

@@ -213,6 +213,31 @@ def test_flash_attention(D, causal, S, H, HKV):
 
 @pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("qscale,shift", [(12.0, 0.0), (0.05, 0.0), (1.0, -60.0)])
+def test_flash_attention_score_ranges(D, causal, qscale, shift):
+    """Peaked (large scores: the deferred-rescale offset moves many times),
+    flat, and far-negative-shifted scores (the row offset is seeded from the
+    first visible tile) against the fp32 reference, with the LSE."""
+    from dlrover_wuqiong_amd.ops.attention import attention_reference, flash_attn_func
+
+    torch.manual_seed(3)
+    B, S, H = 1, 700, 4
+    q = (torch.randn(B, S, H, D, device=DEV) * qscale).to(torch.bfloat16)
+    k = torch.randn(B, S, H, D, device=DEV).to(torch.bfloat16)
+    if shift:
+        # a constant key component aligned with a constant query component
+        # shifts every score of a row by the same large negative amount
+        q[..., 0] = 1.0
+        k[..., 0] = shift * math.sqrt(D)
+    v = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    o = flash_attn_func(q, k, v, causal=causal)
+    orf = attention_reference(q.float(), k.float(), v.float(), causal=causal)
+    assert torch.isfinite(o.float()).all()
+    assert _rel(o, orf) < 3e-2
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("H,HKV", [(4, 4), (8, 2)])
 def test_flash_attention_varlen(D, causal, H, HKV):
     """Packed batch with empty, sub-tile, multi-block sequences and
