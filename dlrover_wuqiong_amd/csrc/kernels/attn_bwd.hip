@@ -31,6 +31,9 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 
 __device__ __forceinline__ bf16x8_t as_bf(const u32x4& v) { return __builtin_bit_cast(bf16x8_t, v); }
+// 8 bf16 scaled by c (operand prescale: scores then leave the MFMA in the exp2 domain)
+__device__ __forceinline__ u32x4 scaled8(const u32x4& v, float c);
+
 __device__ __forceinline__ unsigned int pk2(float a, float b) {
   // one v_cvt_pk_bf16_f32 (RNE) for the pair
   typedef __bf16 bf16x2_v __attribute__((ext_vector_type(2)));
@@ -40,6 +43,12 @@ __device__ __forceinline__ unsigned int pk2(float a, float b) {
 
 // A operand of a 32x32x16 MFMA that sums over 16 rows of a row-major LDS
 // image (rows r0 .. r0+15, columns d0 .. d0+31): element j of lane half h is
+__device__ __forceinline__ u32x4 scaled8(const u32x4& v, float c) {
+  float f[8];
+  unpack8(v, f);
+  return (u32x4){pk2(f[0] * c, f[1] * c), pk2(f[2] * c, f[3] * c), pk2(f[4] * c, f[5] * c), pk2(f[6] * c, f[7] * c)};
+}
+
 // row r0 + 8(j>>2) + 4h + (j&3), matching the k order of a packed 32x32
 // accumulator used as the B operand.  Two ds_read_b64_tr_b16 per fragment.
 template <int D>
@@ -143,10 +152,12 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
     *(u32x4*)(v_img + img_off<D>(row, c)) =
         kv < SK ? *(const u32x4*)(Vb + (int64_t)kv * st.v_rs + c * 8) : (u32x4){0, 0, 0, 0};
   }
+  // K (only used for S here) prescaled by softmax_scale * log2(e)
   u32x4 kf[C::KK];
 #pragma unroll
   for (int kk = 0; kk < C::KK; ++kk)
-    kf[kk] = key < SK ? *(const u32x4*)(Kb + (int64_t)key * st.k_rs + 16 * kk + 8 * hh) : (u32x4){0, 0, 0, 0};
+    kf[kk] = key < SK ? scaled8(*(const u32x4*)(Kb + (int64_t)key * st.k_rs + 16 * kk + 8 * hh), scale_log2)
+                      : (u32x4){0, 0, 0, 0};
   f32x16 dk[C::DT], dv[C::DT];
 #pragma unroll
   for (int dt = 0; dt < C::DT; ++dt)
@@ -216,11 +227,18 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
 #pragma unroll
       for (int qs = 0; qs < C::BQT / 32; ++qs) {
         // S = Q K^T, dP = dO V^T for 32 queries: key on the lane, query in the registers
+        // row constants as the initial accumulators: S' = S*c - lse2, dP' = dP - delta
         f32x16 s, dp;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          s[i] = 0.f;
-          dp[i] = 0.f;
+        for (int g = 0; g < 4; ++g) {
+          const int qi = 32 * qs + 8 * g + 4 * hh;
+          const f32x4 l4 = *(const f32x4*)(stl + qi);
+          const f32x4 d4 = *(const f32x4*)(stl + C::BQT + qi);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            s[4 * g + j] = -l4[j];
+            dp[4 * g + j] = -d4[j];
+          }
         }
 #pragma unroll
         for (int kk = 0; kk < C::KK; ++kk) {
@@ -234,19 +252,17 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int qi = 32 * qs + 8 * g + 4 * hh;
-          const f32x4 l4 = *(const f32x4*)(stl + qi);
-          const f32x4 d4 = *(const f32x4*)(stl + C::BQT + qi);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int i = 4 * g + j;
-            float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], scale_log2, -l4[j]));
+            float p = __builtin_amdgcn_exp2f(s[i]);
             if (need_mask) {
               const int q = q0 + qi + j;
               const bool keep = (q < SQ) & (key < SK) & (!CAUSAL | (key <= q + co));
               p = keep ? p : 0.f;
             }
             s[i] = p;
-            dp[i] = p * (dp[i] - d4[j]);  // dS (scale applied in the epilogue)
+            dp[i] = p * dp[i];  // dS (scale applied in the epilogue)
           }
         }
         // dV^T += dO^T P ; dK^T += Q^T dS : 2 k-steps of 16 queries
@@ -464,6 +480,8 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
       // one 32-key subtile at a time keeps S^T / dP^T at 32 registers
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb) {
+        // (row-constant accumulator init as in the dK/dV kernel costs this
+        // kernel 40+ spilled VGPRs at D=128: kept on the plain form)
         f32x16 s, dp;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
