@@ -10,4 +10,7 @@ rc=$?
 echo "rocprof rc=$rc"
 tail -3 gpurun_out/prof/bench.log
 find gpurun_out/prof -name "*stats*" | head
+# keep the summaries only (a kernel trace of a bench run is >64 MiB)
+find gpurun_out/prof -name "*kernel_trace*" -delete
+find gpurun_out/prof -name "*.csv" -size +8M -delete
 exit $rc
