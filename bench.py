@@ -279,6 +279,7 @@ def summarize(a, run_dir, n, wall):
         },
         "standby_prepin_s": inc1.get("prepin_s"),
         "restore_source": inc1.get("restore_source"),
+        "restore_phases_s": inc1.get("restore_phases"),
         "restarts": len(started) - 1,
     })
     # extrapolation to production: one failure per hour, a checkpoint every
@@ -579,8 +580,10 @@ def worker(a) -> int:
         sync_all()
         t0 = time.perf_counter()
         restored = ckpt.load_checkpoint(target=state())
+        t_host = time.perf_counter()
         if cuda:
             torch.cuda.synchronize()
+        restore_dev = time.perf_counter() - t_host
         restore_sec = mx(time.perf_counter() - t0)
         step = int(restored.get("step", 0)) if restored else 0
         restore_ok = bool(restored) and step > 0
@@ -595,7 +598,9 @@ def worker(a) -> int:
               "restore_sec": restore_sec, "restore_ok": restore_ok, "t_proc": t_proc, "t_activated": t_act,
               "t_pg": t_pg, "t_ckpt": t_ckpt, "t_restored": t_restored,
               "prepin_s": info.get("prepin_s") if info else None,
-              "restore_source": getattr(ckpt.engine, "last_restore_source", None)})
+              "restore_source": getattr(ckpt.engine, "last_restore_source", None),
+              "restore_phases": dict(getattr(ckpt.engine, "last_restore_breakdown", {}) or {},
+                                     device_wait=round(restore_dev, 4))})
         if not restore_ok:
             log(f"[rank {rank}] restore from memory failed: starting over")
         start_step = step

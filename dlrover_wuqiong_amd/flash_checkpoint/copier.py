@@ -51,16 +51,19 @@ def _check(err, what):
 
 def build_descs(pieces: List[Tuple[int, int, int]], device) -> torch.Tensor:
     """pieces: (src_addr, dst_addr, nbytes) -> device int64 [n, 3] chunked."""
-    rows = []
+    parts = []
     for s, d, n in pieces:
-        o = 0
-        while o < n:
-            c = min(CHUNK, n - o)
-            rows.append((s + o, d + o, c))
-            o += c
-    if not rows:
+        if n <= 0:
+            continue
+        o = np.arange(0, n, CHUNK, dtype=np.uint64)  # vectorised: a 22 GB restore is ~21k rows
+        blk = np.empty((o.size, 3), dtype=np.uint64)
+        blk[:, 0] = o + np.uint64(s)
+        blk[:, 1] = o + np.uint64(d)
+        blk[:, 2] = np.minimum(np.uint64(CHUNK), np.uint64(n) - o)
+        parts.append(blk)
+    if not parts:
         return torch.empty(0, 3, dtype=torch.int64, device=device)
-    arr = np.asarray(rows, dtype=np.uint64).view(np.int64)
+    arr = (parts[0] if len(parts) == 1 else np.concatenate(parts)).view(np.int64)
     return torch.from_numpy(arr).to(device, non_blocking=False)
 
 

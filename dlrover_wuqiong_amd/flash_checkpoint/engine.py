@@ -184,6 +184,7 @@ class CheckpointEngine(ABC):
         self._prepped_for = None
         self._last_save_blocking = 0.0
         self.last_restore_source = None  # "hbm" | "shm" after an in-place restore
+        self.last_restore_breakdown: Dict[str, float] = {}  # host seconds per restore phase
         self._notify_agent_to_create_saver()
         self._update_saver_config()
         from .replica import CkptReplicaManager
@@ -621,40 +622,60 @@ class CheckpointEngine(ABC):
             return {}
         complete = h.complete_steps()
         out = {}
+        metas = {}
         for b in range(min(2, len(hbm_tier.OWNED))):
             st, pid, _nb = h.hbm_stamp(self._slice_idx, b)
             if st <= 0 or pid != os.getpid() or st in complete:
                 continue
             for s in range(h.num_slots):
-                cfg = h.get_meta(s).get(DLROVER_CKPT_CONFIG_KEY)
+                if s not in metas:
+                    metas[s] = h.get_meta(s)
+                cfg = metas[s].get(DLROVER_CKPT_CONFIG_KEY)
                 if cfg is not None and cfg.step == st and cfg.num_slices == self._num_slices:
                     out[st] = s
+        self._scanned_metas = metas  # reused by the restore that follows
         return out
 
     def get_state_dict_from_memory(self, target: Any = None):
         """Returns (step, state_dict) from shm, or (0, {})."""
+        t0 = time.perf_counter()
+        tb = self.last_restore_breakdown = {}
+
+        def lap(name):
+            nonlocal t0
+            t1 = time.perf_counter()
+            tb[name] = round(t1 - t0, 4)
+            t0 = t1
+
         self._restore_memory_from_replica()
         h = self._shm_handler
         holds = self._replicated or self._local_rank == self.local_shard_id
         complete = h.complete_steps() if holds else {}
+        lap("scan_slots")
         # a snapshot still in (standby-owned) HBM when the last worker died
         # counts too -- only for an in-place GPU restore
         hbm_only = self._hbm_only_steps() if (holds and target is not None) else {}
         cands = dict(hbm_only)
         cands.update(complete)
+        lap("hbm_scan")
         step = agree_on_step(self._ctl_group, list(cands) if holds else None)
         slot = cands.get(step, -1) if (step > 0 and holds) else -1
         if step <= 0 or not check_all_rank_ready(self._ctl_group, slot >= 0 or not holds):
             return 0, {}
+        lap("agree")
         if not holds:
             return 0, {}
         from_hbm_only = step not in complete
         logger.info(f"rank {self._rank}: restoring step {step} from memory slot {slot} "
                     f"(complete in memory: {sorted(complete)}"
                     f"{', in HBM only: ' + str(sorted(hbm_only)) if hbm_only else ''})")
-        tree = h.get_meta(slot)["tree"]
+        scanned = getattr(self, "_scanned_metas", None) or {}
+        self._scanned_metas = None
+        tree = (scanned.get(slot) or h.get_meta(slot))["tree"]
+        lap("meta")
         if target is not None:
             sd = self._restore_into(tree, target, slot, step, require_hbm=from_hbm_only)
+            lap("copy_enqueue")
             if sd is not None:
                 return step, sd
         if from_hbm_only:

@@ -85,6 +85,29 @@ def _free_hbm() -> int:
     return int(f.value)
 
 
+_warmed = False
+
+
+def _warm_restore_path():
+    """One tiny multi-copy in the standby: loads the copy kernel's code
+    object and the descriptor upload path now, not inside the restore that
+    follows the standby's activation."""
+    global _warmed
+    if _warmed:
+        return
+    try:
+        import torch
+
+        from .copier import build_descs, launch_multi_copy
+
+        t = torch.zeros(2, 4096, dtype=torch.uint8, device="cuda")
+        launch_multi_copy(build_descs([(t[0].data_ptr(), t[1].data_ptr(), 4096)], t.device))
+        torch.cuda.synchronize()
+        _warmed = True
+    except Exception as e:  # never fatal
+        logger.warning(f"standby: restore-path warm-up failed: {e}")
+
+
 def publish_standby_buffers(ctl_dir: str, local_rank: int, nbytes: int, nbuf: int = 2,
                             reserve: int = 24 << 30) -> bool:
     """Standby side: (re)allocate ``nbuf`` buffers of ``nbytes`` and publish
@@ -131,6 +154,7 @@ def publish_standby_buffers(ctl_dir: str, local_rank: int, nbytes: int, nbuf: in
         json.dump(info, f)
     os.replace(path + ".tmp", path)
     _published_key = key
+    _warm_restore_path()
     logger.info(f"standby: published {nbuf} x {nbytes / 2**30:.1f} GiB HBM checkpoint staging buffers")
     return True
 
