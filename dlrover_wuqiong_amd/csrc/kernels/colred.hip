@@ -9,20 +9,47 @@
 //     combine of the 4 waves, then ONE fp32 atomicAdd per column per block
 //     into a workspace -> grid = (C/512) x RS blocks fills the chip without
 //     any partial-row buffer or second pass over the data;
-//   * a tiny finish kernel converts the fp32 workspace into the gradient
-//     (bf16 or fp32), optionally ACCUMULATING into it (grad += sum), so the
-//     result lands directly in the flat gradient buffer.
+//   * the last block to finish in each 512-column strip (per-strip
+//     completion counters after the sums) converts the strip's fp32 sums
+//     into the gradient (bf16 or fp32), optionally
+//     ACCUMULATING into it (grad += sum), so the result lands directly in the
+//     flat gradient buffer with no second launch.  The workspace (sums +
+//     counter) is SELF-CLEANING: the finishing block zeroes what it consumed,
+//     so it is all-zero between calls and needs no per-call memset.
 // The norm dx is a separate row kernel (one wave per row, everything in
 // registers), so the backward is 2 streaming passes + 1 tiny kernel instead
 // of a row pass with per-block partial rows and a serial reduce.
 #include "dw_common.h"
 
+#include <algorithm>
+#include <cstdlib>
+
+static bool getenv_flag(const char* name) {
+  const char* v = std::getenv(name);
+  return v && v[0] == '1';
+}
+
+__device__ __forceinline__ void colred_store(void* out, int c, float v, int is_fp32, int accumulate) {
+  if (!out) return;
+  if (is_fp32) {
+    float* o = (float*)out;
+    o[c] = accumulate ? o[c] + v : v;
+  } else {
+    bf16_t* o = (bf16_t*)out;
+    o[c] = f2bf(accumulate ? bf2f(o[c]) + v : v);
+  }
+}
+
 // MODE 0: acc0 += dy ;  MODE 1: acc0 += dy * xhat, acc1 += dy (LayerNorm) ;
-// MODE 2: acc0 += dy * xhat (RMSNorm)
+// MODE 2: acc0 += dy * xhat (RMSNorm) ;
+// MODE 3: dxo = dy * gelu'(x), acc0 += dxo (GELU backward fused with the
+//         gradient of the bias added before it: one pass instead of two)
 template <int MODE>
 __global__ void __launch_bounds__(256) colred_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                     float* __restrict__ ws, int64_t rows, int C, int rows_per_blk) {
+                                                     float* __restrict__ ws, int64_t rows, int C, int rows_per_blk,
+                                                     void* __restrict__ out0, void* __restrict__ out1, int is_fp32,
+                                                     int accumulate, bf16_t* __restrict__ dxo = nullptr) {
   __shared__ float red[2][4][512 + 4];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c0 = blockIdx.x * 512 + lane * 8;
@@ -32,20 +59,45 @@ __global__ void __launch_bounds__(256) colred_kernel(const bf16_t* __restrict__ 
 #pragma unroll
   for (int k = 0; k < 8; ++k) a0[k] = a1[k] = 0.f;
   if (c0 < C) {
-    for (int64_t r = r_beg + wid; r < r_end; r += 4) {
-      float d[8];
-      unpack8(*(const u32x4*)(dy + r * C + c0), d);
-      if constexpr (MODE == 0) {
+    // U rows per wave per iteration, every load issued before any math
+    constexpr int U = 4;
+    for (int64_t r0 = r_beg + wid; r0 < r_end; r0 += 4 * U) {
+      u32x4 dv[U], xw[U];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) a0[k] += d[k];
-      } else {
-        float xv[8];
-        unpack8(*(const u32x4*)(x + r * C + c0), xv);
-        const float mu = (MODE == 1) ? mean[r] : 0.f, rs = rstd[r];
+      for (int u = 0; u < U; ++u) {
+        const int64_t r = r0 + 4 * u;
+        if (r < r_end) {
+          dv[u] = *(const u32x4*)(dy + r * C + c0);
+          if constexpr (MODE != 0) xw[u] = *(const u32x4*)(x + r * C + c0);
+        }
+      }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          a0[k] += d[k] * (xv[k] - mu) * rs;
-          if constexpr (MODE == 1) a1[k] += d[k];
+      for (int u = 0; u < U; ++u) {
+        const int64_t r = r0 + 4 * u;
+        if (r >= r_end) break;
+        float d[8];
+        unpack8(dv[u], d);
+        if constexpr (MODE == 0) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) a0[k] += d[k];
+        } else if constexpr (MODE == 3) {
+          float xv[8];
+          unpack8(xw[u], xv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            d[k] *= gelu_tanh_grad(xv[k]);
+            a0[k] += d[k];
+          }
+          *(u32x4*)(dxo + r * C + c0) = pack8(d);
+        } else {
+          float xv[8];
+          unpack8(xw[u], xv);
+          const float mu = (MODE == 1) ? mean[r] : 0.f, rs = rstd[r];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            a0[k] += d[k] * (xv[k] - mu) * rs;
+            if constexpr (MODE == 1) a1[k] += d[k];
+          }
         }
       }
     }
@@ -69,26 +121,46 @@ __global__ void __launch_bounds__(256) colred_kernel(const bf16_t* __restrict__ 
       atomicAdd(ws + C + c, s1);
     }
   }
-}
-
-// out[c] (+)= ws[c]; out dtype bf16 (is_fp32=0) or fp32.  The workspace is
-// SELF-CLEANING: every reader zeroes the words it consumed, so ws is all-zero
-// between calls and no per-call hipMemsetAsync (a 5 us fill launch, ~340 per
-// GPT2-1.5B step) is needed.  out == nullptr only clears.
-__global__ void colred_finish_kernel(float* __restrict__ ws, void* __restrict__ out, int C, int is_fp32,
-                                     int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float v = ws[c];
-  ws[c] = 0.f;
-  if (!out) return;
-  if (is_fp32) {
-    float* o = (float*)out;
-    o[c] = accumulate ? o[c] + v : v;
-  } else {
-    bf16_t* o = (bf16_t*)out;
-    o[c] = f2bf(accumulate ? bf2f(o[c]) + v : v);
+  // The last block of each 512-column strip converts the strip's fp32 sums
+  // into the output(s) -- no second launch (a ~5 us kernel per reduction,
+  // ~450 per GPT2-1.5B step), and the finish is spread over the strips.
+  //
+  // Ordering without a device-scope fence: a __threadfence() here is an L2
+  // write-back + invalidate on gfx950 (per-XCD L2s), in every block -- it
+  // made this kernel 5x slower.  All the data the finishing block reads was
+  // produced by agent-scope atomics, so it is enough that this block's
+  // atomics have COMPLETED (vmcnt drained: performed at the coherent level)
+  // before its counter increment is issued, and that the finishing block
+  // reads the sums with atomics too.
+  __shared__ int is_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  unsigned* cnt = (unsigned*)(ws + (MODE == 1 ? 2 * C : C)) + blockIdx.x;
+  if (threadIdx.x == 0)
+    is_last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.y - 1;
+  __syncthreads();
+  if (!is_last) return;
+  float v0[2], v1[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    // read + clear (self-cleaning) with the same atomics that built the sums:
+    // single-location atomicity, no cache maintenance; all in flight at once
+    const int c = blockIdx.x * 512 + threadIdx.x + 256 * j;
+    if (c < C) {
+      v0[j] = __hip_atomic_exchange(ws + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if constexpr (MODE == 1)
+        v1[j] = __hip_atomic_exchange(ws + C + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int c = blockIdx.x * 512 + threadIdx.x + 256 * j;
+    if (c < C) {
+      colred_store(out0, c, v0[j], is_fp32, accumulate);
+      if constexpr (MODE == 1) colred_store(out1, c, v1[j], is_fp32, accumulate);
+    }
+  }
+  if (threadIdx.x == 0) __hip_atomic_exchange(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // dx = rstd * (dy*g - mean(dy*g) - xhat * mean(dy*g*xhat)) [+ dres]; one wave per row
@@ -156,6 +228,123 @@ __global__ void __launch_bounds__(256) norm_dx_kernel(const bf16_t* __restrict__
   }
 }
 
+// Norm backward in ONE pass for H <= 4096: dx as norm_dx_kernel, and the
+// weight gradients dgamma = sum dy*xhat, dbeta = sum dy accumulated per lane
+// over the rows each wave visits (grid-stride over rows), reduced over the
+// block's 4 waves through LDS, one atomic per column per block into ws; the
+// last block converts ws into dgamma / dbeta (same completion protocol as
+// colred_kernel).  Saves the second read of dy and x (colred_kernel<1>).
+template <int VPL, bool RMS>
+__global__ void __launch_bounds__(256) norm_bwd_fused_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ gamma,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const bf16_t* __restrict__ dres,
+    bf16_t* __restrict__ dx, float* __restrict__ ws, void* __restrict__ dgamma, void* __restrict__ dbeta,
+    int is_fp32, int accumulate, int64_t rows, int H) {
+  static_assert(VPL <= 8, "fused norm backward keeps xhat / dy*g in registers");
+  __shared__ float red[2][4][512 + 4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nv = H >> 3;
+  float ag[VPL][8], ab[VPL][8];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ag[j][k] = ab[j][k] = 0.f;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wid; row < rows; row += (int64_t)gridDim.x * 4) {
+    const float mu = RMS ? 0.f : mean_in[row];
+    const float rstd = rstd_in[row];
+    const bf16_t* xr = x + row * H;
+    const bf16_t* dr = dy + row * H;
+    float xh[VPL][8], g[VPL][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nv) {
+        float xv[8], dv[8], gm[8];
+        unpack8(*(const u32x4*)(xr + c * 8), xv);
+        unpack8(*(const u32x4*)(dr + c * 8), dv);
+        unpack8(*(const u32x4*)(gamma + c * 8), gm);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float a = (xv[k] - mu) * rstd, b = dv[k] * gm[k];
+          xh[j][k] = a;
+          g[j][k] = b;
+          ag[j][k] += dv[k] * a;
+          if constexpr (!RMS) ab[j][k] += dv[k];
+          s1 += b;
+          s2 += b * a;
+        }
+      }
+    }
+    const float m1 = RMS ? 0.f : wave_sum(s1) / (float)H;
+    const float m2 = wave_sum(s2) / (float)H;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nv) {
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = rstd * (g[j][k] - m1 - xh[j][k] * m2);
+        if (dres) {
+          float r[8];
+          unpack8(*(const u32x4*)(dres + row * H + c * 8), r);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] += r[k];
+        }
+        *(u32x4*)(dx + row * H + c * 8) = pack8(o);
+      }
+    }
+  }
+  // block reduce, 512 columns (one j) at a time, one atomic per column
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[0][wid][lane * 8 + k] = ag[j][k];
+      if constexpr (!RMS) red[1][wid][lane * 8 + k] = ab[j][k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int cl = threadIdx.x + 256 * h;
+      const int c = 512 * j + cl;
+      if (c < H) {
+        atomicAdd(ws + c, red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl]);
+        if constexpr (!RMS) atomicAdd(ws + H + c, red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl]);
+      }
+    }
+    __syncthreads();
+  }
+  __shared__ int is_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's atomics performed (see colred_kernel)
+  __syncthreads();
+  unsigned* cnt = (unsigned*)(ws + 2 * H);
+  if (threadIdx.x == 0)
+    is_last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!is_last) return;
+  for (int c0 = threadIdx.x; c0 < H; c0 += 256 * 4) {
+    float v0[4], v1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = c0 + 256 * u;
+      if (c < H) {
+        v0[u] = __hip_atomic_exchange(ws + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (!RMS) v1[u] = __hip_atomic_exchange(ws + H + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = c0 + 256 * u;
+      if (c < H) {
+        colred_store(dgamma, c, v0[u], is_fp32, accumulate);
+        if constexpr (!RMS) colred_store(dbeta, c, v1[u], is_fp32, accumulate);
+      }
+    }
+  }
+  if (threadIdx.x == 0) __hip_atomic_exchange(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 static int colred_rows_per_blk(int64_t rows, int C) {
   // aim for ~4 blocks per CU over 256 CUs
   const int64_t col_blks = (C + 511) / 512;
@@ -166,7 +355,7 @@ static int colred_rows_per_blk(int64_t rows, int C) {
   return (int)(per < 4 ? 4 : per);
 }
 
-// ws: fp32 [C], all-zero on entry, left all-zero.  out (+)= column sums of dy [rows, C].
+// ws: fp32 [C + ceil(C/512)] (sums + per-strip completion counters), all-zero on entry, left all-zero.  out (+)= column sums of dy [rows, C].
 extern "C" int dw_colsum_acc(const void* dy, int64_t rows, int C, void* ws, void* out, int out_fp32, int accumulate,
                              void* stream) {
   if (C % 8 != 0) return (int)hipErrorInvalidValue;
@@ -174,9 +363,19 @@ extern "C" int dw_colsum_acc(const void* dy, int64_t rows, int C, void* ws, void
   const int per = colred_rows_per_blk(rows, C);
   dim3 grid((C + 511) / 512, (unsigned)((rows + per - 1) / per));
   hipLaunchKernelGGL(colred_kernel<0>, grid, dim3(256), 0, s, (const bf16_t*)dy, nullptr, nullptr, nullptr,
-                     (float*)ws, rows, C, per);
-  hipLaunchKernelGGL(colred_finish_kernel, dim3((C + 255) / 256), dim3(256), 0, s, (float*)ws, out, C, out_fp32,
-                     accumulate);
+                     (float*)ws, rows, C, per, out, nullptr, out_fp32, accumulate);
+  DW_LAUNCH_RET;
+}
+
+// dx = dy * gelu'(pre) [rows, C]; dbias (+)= column sums of dx.  ws as above.
+extern "C" int dw_gelu_bwd_dbias(const void* dy, const void* pre, void* dx, int64_t rows, int C, void* ws,
+                                 void* dbias, int out_fp32, int accumulate, void* stream) {
+  if (C % 8 != 0) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  const int per = colred_rows_per_blk(rows, C);
+  dim3 grid((C + 511) / 512, (unsigned)((rows + per - 1) / per));
+  hipLaunchKernelGGL(colred_kernel<3>, grid, dim3(256), 0, s, (const bf16_t*)dy, (const bf16_t*)pre, nullptr,
+                     nullptr, (float*)ws, rows, C, per, dbias, nullptr, out_fp32, accumulate, (bf16_t*)dx);
   DW_LAUNCH_RET;
 }
 
@@ -190,7 +389,7 @@ extern "C" int dw_colsum_acc(const void* dy, int64_t rows, int C, void* ws, void
     else { constexpr int VPL = 16; __VA_ARGS__; }     \
   } while (0)
 
-// Norm backward v2.  ws: fp32 [2H], all-zero on entry, left all-zero.
+// Norm backward v2.  ws: fp32 [2H + ceil(H/512)], all-zero on entry, left all-zero.
 // dgamma/dbeta (+)= (accumulate flag).  dres (nullable): gradient of the
 // residual sum that this norm's input also feeds (fused add+norm) -> dx += dres.
 extern "C" int dw_norm_bwd2(const void* dy, const void* x, const void* gamma, const void* mean, const void* rstd,
@@ -199,6 +398,29 @@ extern "C" int dw_norm_bwd2(const void* dy, const void* x, const void* gamma, co
   if (H % 8 != 0 || H > 8 * 64 * 16) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  static const bool two_pass = getenv_flag("DWAMD_NORM_BWD_2PASS");  // A/B switch
+  if ((dgamma || dbeta) && H >= 2048 && H <= 8 * 64 * 8 && !two_pass) {
+    // one pass: dx + weight gradients (2 blocks per CU of 4 row-striding
+    // waves).  Measured (scripts/bench_norm.py): RMSNorm 16k x 4096 141 ->
+    // 118 us; at H = 1600 the two passes are as fast (the row pass alone
+    // fills the chip better), so small H keeps them.
+    const unsigned nb = (unsigned)std::min<int64_t>((rows + 3) / 4, 512);
+    DISPATCH_VPL2(H, {
+      if constexpr (VPL <= 8) {
+        if (rms)
+          hipLaunchKernelGGL((norm_bwd_fused_kernel<VPL, true>), dim3(nb), block, 0, s, (const bf16_t*)dy,
+                             (const bf16_t*)x, (const bf16_t*)gamma, nullptr, (const float*)rstd,
+                             (const bf16_t*)dres, (bf16_t*)dx, (float*)ws, dgamma, nullptr, out_fp32, accumulate,
+                             rows, H);
+        else
+          hipLaunchKernelGGL((norm_bwd_fused_kernel<VPL, false>), dim3(nb), block, 0, s, (const bf16_t*)dy,
+                             (const bf16_t*)x, (const bf16_t*)gamma, (const float*)mean, (const float*)rstd,
+                             (const bf16_t*)dres, (bf16_t*)dx, (float*)ws, dgamma, dbeta, out_fp32, accumulate,
+                             rows, H);
+      }
+    });
+    DW_LAUNCH_RET;
+  }
   DISPATCH_VPL2(H, {
     if (rms)
       hipLaunchKernelGGL((norm_dx_kernel<VPL, true>), grid, block, 0, s, (const bf16_t*)dy, (const bf16_t*)x,
@@ -212,17 +434,13 @@ extern "C" int dw_norm_bwd2(const void* dy, const void* x, const void* gamma, co
   if (!dgamma && !dbeta) { DW_LAUNCH_RET; }
   const int per = colred_rows_per_blk(rows, H);
   dim3 cg((H + 511) / 512, (unsigned)((rows + per - 1) / per));
+  // both halves are consumed (and cleared) even if one output is absent
   if (rms)
     hipLaunchKernelGGL(colred_kernel<2>, cg, dim3(256), 0, s, (const bf16_t*)dy, (const bf16_t*)x, nullptr,
-                       (const float*)rstd, (float*)ws, rows, H, per);
+                       (const float*)rstd, (float*)ws, rows, H, per, dgamma, nullptr, out_fp32, accumulate);
   else
     hipLaunchKernelGGL(colred_kernel<1>, cg, dim3(256), 0, s, (const bf16_t*)dy, (const bf16_t*)x,
-                       (const float*)mean, (const float*)rstd, (float*)ws, rows, H, per);
-  // both halves are consumed (and cleared) even if one output is absent
-  hipLaunchKernelGGL(colred_finish_kernel, dim3((H + 255) / 256), dim3(256), 0, s, (float*)ws, dgamma, H, out_fp32,
-                     accumulate);
-  if (!rms)
-    hipLaunchKernelGGL(colred_finish_kernel, dim3((H + 255) / 256), dim3(256), 0, s, (float*)ws + H, dbeta, H,
-                       out_fp32, accumulate);
+                       (const float*)mean, (const float*)rstd, (float*)ws, rows, H, per, dgamma, dbeta, out_fp32,
+                       accumulate);
   DW_LAUNCH_RET;
 }

@@ -103,3 +103,24 @@ static inline int dw_grid_for(int64_t work_items, int per_block, int cap = 2048)
   if (g > cap) g = cap;
   return (int)g;
 }
+
+// tanh-approximate GELU and its derivative (GPT-2 MLP).  tanh(u) =
+// 1 - 2 / (1 + 2^(2u log2 e)) with the hardware exp2 / rcp (a few VALU ops
+// instead of libm tanhf's ~20: the GELU passes are VALU-bound otherwise);
+// saturates correctly (exp2 -> inf gives 1, -> 0 gives -1); ~1e-6 relative.
+__device__ __forceinline__ float fast_tanh(float u) {
+  const float e = __builtin_amdgcn_exp2f(u * 2.8853900817779268f);  // 2 * log2(e)
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + e);
+}
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * (x + k1 * x * x * x);
+  return 0.5f * x * (1.f + fast_tanh(u));
+}
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float x2 = x * x;
+  const float u = k0 * (x + k1 * x2 * x);
+  const float t = fast_tanh(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+}

@@ -6,19 +6,6 @@
 // rotary embedding; llama SwiGLU MLP).
 #include "dw_common.h"
 
-__device__ __forceinline__ float gelu_tanh(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
-}
-__device__ __forceinline__ float gelu_tanh_grad(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float x2 = x * x;
-  const float u = k0 * (x + k1 * x2 * x);
-  const float t = tanhf(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
-}
-
 // y = gelu(x + bias); x:[R, C] bf16, bias [C] bf16 (nullable). Optionally
 // writes the biased pre-activation (pre) for the backward.
 __global__ void __launch_bounds__(256) bias_gelu_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ bias,

@@ -15,7 +15,7 @@ def colsum(x2: torch.Tensor, out_dtype=None, out: torch.Tensor = None, accumulat
     R, C = x2.shape
     if out is None:
         out = torch.empty(C, device=x2.device, dtype=out_dtype or x2.dtype)
-    ws = _hip.zeroed_workspace(C, x2.device)
+    ws = _hip.zeroed_workspace(C + (C + 511) // 512, x2.device)  # sums + strip counters
     _hip.check(_hip.lib().dw_colsum_acc(_hip.ptr(x2), R, C, _hip.ptr(ws), _hip.ptr(out),
                                         int(out.dtype == torch.float32), int(accumulate), _hip.stream()), "colsum")
     return out
@@ -45,17 +45,21 @@ class _BiasGeluFn(torch.autograd.Function):
         (pre,) = ctx.saved_tensors
         dy = dy.contiguous().to(torch.bfloat16)
         dx = torch.empty_like(pre)
-        _hip.check(_hip.lib().dw_gelu_bwd(_hip.ptr(dy), _hip.ptr(pre), _hip.ptr(dx), pre.numel(),
-                                          _hip.stream()), "gelu_bwd")
-        db = None
-        if ctx.has_bias:
-            C = pre.shape[-1]
-            g = direct_grad(ctx.bias_param)
-            if g is not None:
-                colsum(dx.view(-1, C), out=g, accumulate=True)
-                notify(ctx.bias_param)
-            else:
-                db = colsum(dx.view(-1, C), ctx.bias_dtype)
+        if not ctx.has_bias:
+            _hip.check(_hip.lib().dw_gelu_bwd(_hip.ptr(dy), _hip.ptr(pre), _hip.ptr(dx), pre.numel(),
+                                              _hip.stream()), "gelu_bwd")
+            return dx, None
+        # one pass: dx = dy * gelu'(pre) and dbias (+)= colsum(dx)
+        C = pre.shape[-1]
+        g = direct_grad(ctx.bias_param)
+        db = g if g is not None else torch.empty(C, device=pre.device, dtype=ctx.bias_dtype)
+        ws = _hip.zeroed_workspace(C + (C + 511) // 512, pre.device)
+        _hip.check(_hip.lib().dw_gelu_bwd_dbias(_hip.ptr(dy), _hip.ptr(pre), _hip.ptr(dx), pre.numel() // C, C,
+                                                _hip.ptr(ws), _hip.ptr(db), int(db.dtype == torch.float32),
+                                                int(g is not None), _hip.stream()), "gelu_bwd_dbias")
+        if g is not None:
+            notify(ctx.bias_param)
+            return dx, None
         return dx, db
 
 

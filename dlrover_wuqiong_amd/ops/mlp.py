@@ -6,8 +6,8 @@ GELU gradient fused into hipBLASLt GEMM epilogues
             g = gelu_tanh(pre)                (one read, one write)
             y = g W2^T + b2                   (bias epilogue)
   backward  dW2 += dy^T g, db2 += colsum(dy)
-            dh (, db1) = DGELU[_BGRAD](dy W2, pre)   (no separate gelu_bwd pass;
-                                                      colsum(dh) when BGRAD has no kernel)
+            dh (, db1) = DGELU[_BGRAD](dy W2, pre)   (epilogue forms), or
+                         dy W2, then one gelu_bwd + colsum pass (default)
             dW1 += dh^T x, dx = dh W1
 
 Gradients of flat-buffer parameters accumulate in place (``_grad.py``).
@@ -98,9 +98,12 @@ class _FusedMLPFn(torch.autograd.Function):
             else:
                 _hip.check(rc, "gemm_dgelu")
         if mode == "unfused":
+            # dgrad GEMM, then ONE pass: dh = dg * gelu'(pre) and db1 = colsum(dh)
             dg = (dy2 @ w2).contiguous()
-            _hip.check(_hip.lib().dw_gelu_bwd(_hip.ptr(dg), _hip.ptr(pre), _hip.ptr(dh), dg.numel(),
-                                              _hip.stream()), "gelu_bwd")
+            db1_f = torch.empty(N1, device=dy.device, dtype=torch.float32)
+            ws = _hip.zeroed_workspace(N1 + (N1 + 511) // 512, dy.device)
+            _hip.check(_hip.lib().dw_gelu_bwd_dbias(_hip.ptr(dg), _hip.ptr(pre), _hip.ptr(dh), M, N1, _hip.ptr(ws),
+                                                    _hip.ptr(db1_f), 1, 0, _hip.stream()), "gelu_bwd_dbias")
         _BWD_MODE.setdefault(key, mode)
         if db1_f is None:
             db1_f = colsum(dh, torch.float32)

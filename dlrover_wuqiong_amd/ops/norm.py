@@ -26,7 +26,7 @@ def _norm_backward(ctx, dy, dres):
         dres = dres.contiguous().view(-1, H)
         if dres.dtype != torch.bfloat16:
             dres = dres.to(torch.bfloat16)
-    ws = _hip.zeroed_workspace(2 * H, x2.device)
+    ws = _hip.zeroed_workspace(2 * H + (H + 511) // 512, x2.device)  # sums + strip counters
     dx = torch.empty_like(x2)
     wp, bp = ctx.weight_param, ctx.bias_param
     gd, bd = direct_grad(wp), direct_grad(bp) if ctx.has_bias else None

@@ -25,16 +25,18 @@ def _need_gpu():
     kernels(required=True)
 
 
-@pytest.mark.parametrize("H", [256, 1600, 4096])
+@pytest.mark.parametrize("H,R", [(256, 777), (1600, 777), (4096, 777), (8192, 777), (1600, 9000)])
 @pytest.mark.parametrize("rms", [False, True])
-def test_norm_fwd_bwd(H, rms):
+def test_norm_fwd_bwd(H, R, rms):
+    """H <= 4096: one-pass backward (dx + weight grads, row-striding waves,
+    last-block finish); 8192: row pass + column-reduction pass."""
     from dlrover_wuqiong_amd.ops.norm import layer_norm, rms_norm
 
     torch.manual_seed(0)
-    x = torch.randn(777, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    x = torch.randn(R, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     w = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16).requires_grad_()
     b = (0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16).requires_grad_()
-    dy = torch.randn(777, H, device=DEV, dtype=torch.bfloat16)
+    dy = torch.randn(R, H, device=DEV, dtype=torch.bfloat16)
     xf, wf, bf = x.detach().float().requires_grad_(), w.detach().float().requires_grad_(), b.detach().float().requires_grad_()
     if rms:
         y = rms_norm(x, w, 1e-6)
@@ -100,6 +102,33 @@ def test_bias_gelu():
     yr.backward(dy.float())
     assert _rel(x.grad, xf.grad) < 2e-2
     assert _rel(b.grad, bf.grad) < 2e-2
+
+
+@pytest.mark.parametrize("R,C", [(8192, 6400), (1000, 1600), (37, 4800)])
+def test_gelu_bwd_dbias_fused(R, C):
+    """One-pass GELU backward + bias gradient (last-block finish, self-cleaning
+    workspace): repeated calls, fp32 accumulate and bf16 write."""
+    from dlrover_wuqiong_amd.ops import _hip
+
+    torch.manual_seed(R)
+    dy = torch.randn(R, C, device=DEV, dtype=torch.bfloat16)
+    pre = torch.randn(R, C, device=DEV, dtype=torch.bfloat16)
+    pf = pre.float().requires_grad_()
+    F.gelu(pf, approximate="tanh").backward(dy.float())
+    ref_dx, ref_db = pf.grad, pf.grad.sum(0)
+    acc = torch.zeros(C, device=DEV, dtype=torch.float32)
+    for it in range(3):
+        dx = torch.empty_like(pre)
+        ws = _hip.zeroed_workspace(C + (C + 511) // 512, DEV)
+        _hip.check(_hip.lib().dw_gelu_bwd_dbias(_hip.ptr(dy), _hip.ptr(pre), _hip.ptr(dx), R, C, _hip.ptr(ws),
+                                                _hip.ptr(acc), 1, 1, _hip.stream()), "gelu_bwd_dbias")
+        assert _rel(dx, ref_dx) < 1e-2
+        assert _rel(acc, (it + 1) * ref_db) < 1e-3
+        assert int((ws[:C + (C + 511) // 512] != 0).sum()) == 0  # left all-zero (sums + counters)
+    db16 = torch.empty(C, device=DEV, dtype=torch.bfloat16)
+    _hip.check(_hip.lib().dw_gelu_bwd_dbias(_hip.ptr(dy), _hip.ptr(pre), _hip.ptr(dx), R, C, _hip.ptr(ws),
+                                            _hip.ptr(db16), 0, 0, _hip.stream()), "gelu_bwd_dbias")
+    assert _rel(db16, ref_db) < 1e-2
 
 
 def test_swiglu():
