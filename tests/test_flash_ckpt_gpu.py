@@ -265,6 +265,14 @@ def _two_rank_worker(rank, port, q, nbuf):
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=2)
         model, opt, flat = _model_and_opt()
+        # replicated state must be identical on the ranks (DDP's all-reduce
+        # guarantees it in training; here each rank ran its own backward, whose
+        # atomic column reductions may differ in the last bits): take rank 0's
+        for t in (flat.data, opt.exp_avg, opt.exp_avg_sq, opt.master):
+            if t is not None:
+                c = t.cpu()
+                dist.broadcast(c, 0)
+                t.copy_(c)
         ck = DdpCheckpointer(os.environ["CKDIR"])
         state = lambda: {"model": model.state_dict(), "opt": opt.state_dict()}  # noqa
         for step in (1, 2, 3):  # several saves: both slots / staging buffers in play
