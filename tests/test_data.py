@@ -103,6 +103,42 @@ def test_gpu_preloader_and_unordered_cpu():
     assert vals == list(range(20))
 
 
+class _SlowFirst(torch.utils.data.Dataset):
+    def __len__(self):
+        return 24
+
+    def __getitem__(self, i):
+        if i == 0:
+            import time
+
+            time.sleep(1.5)
+        if i == 13 and getattr(self, "fail", False):
+            raise ValueError("bad sample 13")
+        return torch.tensor([i])
+
+
+def test_unordered_loader_completion_order_and_errors():
+    """A slow sample delays only its own batch; every batch arrives exactly
+    once; the other workers keep draining the shared queue; a worker
+    exception re-raises in the main process."""
+    from dlrover_wuqiong_amd.atorch.data import UnorderedDataLoader
+
+    ul = UnorderedDataLoader(_SlowFirst(), batch_size=2, num_workers=3)
+    order = [b[:, 0].tolist() for b in ul]
+    assert sorted(v for b in order for v in b) == list(range(24))
+    assert order[0] != [0, 1] and order.index([0, 1]) >= 6  # not head-of-line blocked
+    per = ul.stats()
+    assert sum(per) == 12 and max(per) >= 5  # the slow worker produced 1; the others took the rest
+    # in-order torch DataLoader for contrast: batch 0 comes first, after the sleep
+    ref = [b[:, 0].tolist() for b in DataLoader(_SlowFirst(), batch_size=2, num_workers=3)]
+    assert ref[0] == [0, 1]
+    bad = _SlowFirst()
+    bad.fail = True
+    with pytest.raises(RuntimeError, match="bad sample 13"):
+        for _ in UnorderedDataLoader(bad, batch_size=2, num_workers=2):
+            pass
+
+
 def test_elastic_dataset_from_master():
     from dlrover_wuqiong_amd.atorch.data import SimpleElasticDataset
     from dlrover_wuqiong_amd.elastic_agent.master_client import MasterClient
