@@ -26,6 +26,8 @@
 // epilogues; causal tiles wholly above a wave's diagonal are skipped.
 #include "attn_common.h"
 
+#include <cstdlib>
+
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
@@ -548,6 +550,37 @@ extern "C" int64_t dw_attn_bwd_workspace(int B, int S, int H, int D) {
   return (int64_t)B * H * S * 4 + 2 * (int64_t)B * S * H * D * 4 + 512;
 }
 
+// dQ runs on a second stream concurrently with dK/dV (both only read q, k,
+// v, dO, lse and delta): each kernel alone leaves the CUs half occupied
+// (8 waves / CU) and has a causal tail; together they fill each other's
+// gaps.  Fork / join through events, so it is also capturable in a graph.
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
+static SideStream* side_stream() {
+  static thread_local SideStream per_dev[16];
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 16) return nullptr;
+  SideStream& ss = per_dev[d];
+  if (!ss.s) {
+    if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess)
+      return nullptr;
+  }
+  return &ss;
+}
+
+static bool bwd_concurrent() {
+  static const bool on = [] {
+    const char* v = getenv("DWAMD_ATTN_BWD_CONCURRENT");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 template <int D>
 static void launch_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const void* lse,
                        char* ws, void* dq, void* dk, void* dv, int B, int Sq, int Sk, int H, int HKV, int causal,
@@ -563,6 +596,10 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
   hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3((unsigned)((rows + RPB - 1) / RPB)), dim3(256), 0, s,
                      (const bf16_t*)o, (const bf16_t*)dout, delta, pre_b, pre_s, H, st);
   const float scale_log2 = softmax_scale * 1.4426950408889634f;
+  SideStream* side = bwd_concurrent() ? side_stream() : nullptr;
+  hipStream_t sq = s;
+  if (side && hipEventRecord(side->fork, s) == hipSuccess && hipStreamWaitEvent(side->s, side->fork, 0) == hipSuccess)
+    sq = side->s;
   // key-major dK / dV
   using KC = DkvCfg<D>;
   const bool partial = H != HKV;
@@ -588,18 +625,22 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
     hipLaunchKernelGGL(gqa_reduce_kernel<D>, dim3(dw_grid_for(nv, 256, 4096)), dim3(256), 0, s, pk, pv,
                        (bf16_t*)dk, (bf16_t*)dv, prow, pS, H, HKV, st);
   }
-  // query-major dQ
+  // query-major dQ (on the side stream when concurrent)
   using DC = DqCfg<D>;
   dim3 gq((unsigned)((Sq + DC::BQ - 1) / DC::BQ * H * B));  // 1-D: xcd_block()
   const int lq = 4 * DC::TILE;
   if (causal)
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, true>), gq, dim3(64 * DC::WAVES), lq, s, (const bf16_t*)q,
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, true>), gq, dim3(64 * DC::WAVES), lq, sq, (const bf16_t*)q,
                        (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta,
                        (bf16_t*)dq, Sq, H, HKV, softmax_scale, scale_log2, st, vl);
   else
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, false>), gq, dim3(64 * DC::WAVES), lq, s, (const bf16_t*)q,
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, false>), gq, dim3(64 * DC::WAVES), lq, sq, (const bf16_t*)q,
                        (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta,
                        (bf16_t*)dq, Sq, H, HKV, softmax_scale, scale_log2, st, vl);
+  if (sq != s) {  // join: the caller's stream continues after both
+    hipEventRecord(side->join, sq);
+    hipStreamWaitEvent(s, side->join, 0);
+  }
 }
 
 // strides: int64[16] = q, k, v, o, do, dq, dk, dv  x (batch, row) in elements
