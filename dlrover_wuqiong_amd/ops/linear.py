@@ -8,12 +8,30 @@ temporary ``g``) and ``db += colsum(dY)`` with the column-reduction kernel
 direct gradients (see ``_grad.py``).  Otherwise plain autograd semantics.
 """
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _hip
 from ._grad import direct_grad, notify
+
+# dX = dY W (dgrad) and dW += dY^T X (wgrad) are independent GEMMs;
+# DWAMD_WGRAD_STREAM=1 runs the wgrad (+ bias colsum) on a per-device side
+# stream concurrently with the dgrad, joined before this node's backward
+# returns.  Off by default: measured on the GPT2-1.5B step it is SLOWER
+# (117.4 vs 115.4 ms -- two full-chip hipBLASLt GEMMs contend for CUs and L2
+# rather than filling each other's tail waves).
+_WGRAD_STREAM = os.environ.get("DWAMD_WGRAD_STREAM", "0") == "1"
+_SIDE = {}
+
+
+def _side_stream(device) -> torch.cuda.Stream:
+    s = _SIDE.get(device.index)
+    if s is None:
+        s = _SIDE[device.index] = torch.cuda.Stream(device)
+    return s
 
 
 class _LinearFn(torch.autograd.Function):
@@ -29,11 +47,14 @@ class _LinearFn(torch.autograd.Function):
         N, K = w.shape
         dy2 = dy.reshape(-1, N)
         x2 = x.reshape(-1, K)
-        dx = (dy2 @ w).view(x.shape) if ctx.needs_input_grad[0] else None
-        dw = db = None
         b = ctx.bias_param
         gw = direct_grad(ctx.weight_param)
         gb = direct_grad(b) if b is not None else None
+        if (_WGRAD_STREAM and dy2.is_cuda and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]
+                and gw is not None and (b is None or gb is not None) and not torch.cuda.is_current_stream_capturing()):
+            return _backward_two_streams(ctx, dy2, x2, w, x.shape, gw, gb, N)
+        dx = (dy2 @ w).view(x.shape) if ctx.needs_input_grad[0] else None
+        dw = db = None
         if ctx.needs_input_grad[1]:
             if gw is not None:
                 gw.addmm_(dy2.t(), x2)
@@ -49,6 +70,31 @@ class _LinearFn(torch.autograd.Function):
             else:
                 db = dy2.sum(0).to(b.dtype)
         return dx, dw, db
+
+
+def _backward_two_streams(ctx, dy2, x2, w, x_shape, gw, gb, N):
+    """dgrad on the current stream, wgrad (+ bias colsum) on the side stream,
+    both into direct flat-gradient storage; joined before returning."""
+    cur = torch.cuda.current_stream(dy2.device)
+    side = _side_stream(dy2.device)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        gw.addmm_(dy2.t(), x2)
+        if gb is not None:
+            if _hip.use_hip(dy2) and dy2.is_contiguous() and N % 8 == 0:
+                from .activation import colsum
+
+                colsum(dy2, out=gb, accumulate=True)
+            else:
+                gb.add_(dy2.sum(0).to(gb.dtype))
+    dx = (dy2 @ w).view(x_shape)
+    # join: everything the caller's stream does next -- including freeing dy2
+    # / x2 for reuse -- is ordered after the wgrad (no record_stream needed)
+    cur.wait_stream(side)
+    notify(ctx.weight_param)
+    if gb is not None:
+        notify(ctx.bias_param)
+    return dx, None, None
 
 
 def linear(x, weight, bias=None):
