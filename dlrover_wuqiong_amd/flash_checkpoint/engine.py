@@ -46,6 +46,10 @@ _TIMING = os.environ.get("DWAMD_CKPT_TIMING", "0") == "1"  # log per-phase save 
 _PREP_PIECE = max(64, int(os.environ.get("DWAMD_PREP_PIECE_MB", "1024"))) << 20  # shm prefault/pin granularity
 
 
+
+# DWAMD_CKPT_SPECULATE=0: walk + verify the state dict before enqueueing the copy
+_SPECULATE = os.environ.get("DWAMD_CKPT_SPECULATE", "1") == "1"
+
 class CheckpointEventType:
     SAVE = 1
     UPDATE_SHARD = 2
@@ -184,6 +188,7 @@ class CheckpointEngine(ABC):
         self._prepped_for = None
         self._last_save_blocking = 0.0
         self.last_restore_source = None  # "hbm" | "shm" after an in-place restore
+        self.speculation_misses = 0  # speculative snapshots redone after the state dict changed
         self.last_restore_breakdown: Dict[str, float] = {}  # host seconds per restore phase
         self._notify_agent_to_create_saver()
         self._update_saver_config()
@@ -438,12 +443,7 @@ class CheckpointEngine(ABC):
         if marks is not None:
             marks.append(("wait_prev", time.perf_counter()))
 
-        layout = self._plan(state_dict)
-        self._ensure_shm(layout.total_bytes)
-        if marks is not None:
-            marks.append(("plan+shm", time.perf_counter()))
         h = self._shm_handler
-        lo, hi = split_ranges(layout.total_bytes, self._num_slices)[self._slice_idx]
         step = conf.step
         stage = {}
 
@@ -452,15 +452,44 @@ class CheckpointEngine(ABC):
             stage["idx"] = idx
             h.set_hbm_stamp(self._slice_idx, idx, 0)
 
-        has_gpu = any(e.device == "cuda" for e in layout.extents)
+        def can_snapshot(lay) -> bool:
+            lo_, hi_ = split_ranges(lay.total_bytes, self._num_slices)[self._slice_idx]
+            return (copier is not None and bool(state_dict) and any(e.device == "cuda" for e in lay.extents)
+                    and not copier._use_ring(hi_ - lo_))
+
         snap = None
-        if has_gpu and copier is not None and bool(state_dict) and not copier._use_ring(hi - lo):
+        # Speculative snapshot: a training loop saves the same tensors every
+        # time, so the HBM->staging copy is enqueued from the previous plan
+        # (whose tensors this engine still holds: every address stays valid)
+        # BEFORE the state dict is walked and verified against it (~3-5 ms of
+        # host time for a few thousand tensors, now overlapped with the copy).
+        # A mismatch re-plans and copies again (stream-ordered after it).
+        spec = self._layout_cache.cached() if (hasattr(self, "_layout_cache") and _SPECULATE) else None
+        if spec is not None and h.shared_memory is not None and h.payload_size == spec.total_bytes \
+                and can_snapshot(spec):
+            lo, hi = split_ranges(spec.total_bytes, self._num_slices)[self._slice_idx]
+            snap = copier.snapshot(spec, lo, hi, before_copy)
+            if marks is not None:
+                marks.append(("enqueue", time.perf_counter()))
+        layout = self._plan(state_dict)
+        if snap is not None and layout.extents is not spec.extents:
+            self.speculation_misses += 1
+            stage.clear()
+            snap = None  # the speculative copy is stream-ordered before the real one below
+        self._ensure_shm(layout.total_bytes)
+        if marks is not None:
+            marks.append(("plan+shm", time.perf_counter()))
+        lo, hi = split_ranges(layout.total_bytes, self._num_slices)[self._slice_idx]
+        has_gpu = any(e.device == "cuda" for e in layout.extents)
+        if snap is None and can_snapshot(layout):
             # the HBM->staging copy needs no shm slot: enqueue it first, so the
             # slot vote (a gloo collective) and the metadata pickling below run
             # on the host while the GPU copies
             snap = copier.snapshot(layout, lo, hi, before_copy)
             if marks is not None:
                 marks.append(("enqueue", time.perf_counter()))
+        elif snap is not None:
+            snap["layout"] = layout  # same extents; the verified meta tree
         if self._next_slot is None:
             # first save of this process (nothing in flight): never the latest complete slot
             self._next_slot = h.write_slot()

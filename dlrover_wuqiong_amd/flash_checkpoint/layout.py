@@ -120,6 +120,12 @@ class LayoutCache:
         self._layout: Optional[Layout] = None
         self._metas: List[TensorMeta] = []
 
+    def cached(self) -> Optional[Layout]:
+        """The layout of the previous plan (its tensors are kept alive by the
+        caller), for a speculative snapshot enqueued before :meth:`plan`
+        verifies that ``state_dict`` still matches it."""
+        return self._layout
+
     def plan(self, state_dict: Any) -> Tuple[Layout, List[torch.Tensor]]:
         if self._layout is not None:
             try:
@@ -156,17 +162,41 @@ class LayoutCache:
         n = len(key)
         tensors: List[torch.Tensor] = []
         T = torch.Tensor
+        append = tensors.append
+
+        def leaf(v):
+            # a tensor leaf: verified against the cached key, replaced by its meta
+            i = len(tensors)
+            if i >= n:
+                raise _Miss
+            k = key[i]
+            if v.data_ptr() != k[0] or v.numel() != k[1] or v.dtype != k[2] or not v.is_contiguous():
+                raise _Miss
+            append(v)
+            return metas[i]
+
+        def rec_dict(v, tv):
+            # tensors handled inline (no call per leaf): the bulk of a state dict
+            out = {}
+            for k, x in v.items():
+                tx = type(x)
+                out[k] = leaf(x) if (tx is T or tx is torch.nn.Parameter) else (
+                    x if tx in _SCALARS else rec(x))
+            if tv is dict:
+                return out
+            try:
+                return tv(out.items())
+            except Exception:
+                return out
 
         def rec(v):
             tv = type(v)
+            if tv is T or tv is torch.nn.Parameter:
+                return leaf(v)
+            if tv in _SCALARS:
+                return v
             if tv is dict or isinstance(v, dict):
-                items = [(k, rec(x)) for k, x in v.items()]
-                if tv is dict:
-                    return dict(items)
-                try:
-                    return tv(items)
-                except Exception:
-                    return dict(items)
+                return rec_dict(v, tv)
             if tv is list or isinstance(v, list):
                 if all(type(x) in _SCALARS for x in v):
                     return list(v)
@@ -174,14 +204,7 @@ class LayoutCache:
             if isinstance(v, tuple) and not hasattr(v, "_fields"):
                 return tuple(rec(x) for x in v)
             if isinstance(v, T):
-                i = len(tensors)
-                if i >= n:
-                    raise _Miss
-                k = key[i]
-                if v.data_ptr() != k[0] or v.numel() != k[1] or v.dtype != k[2] or not v.is_contiguous():
-                    raise _Miss
-                tensors.append(v)
-                return metas[i]
+                return leaf(v)
             return v
 
         tree = rec(state_dict)

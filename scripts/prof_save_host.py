@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--model", default="gpt2-1.5b")
     ap.add_argument("--saves", type=int, default=10)
     ap.add_argument("--out", default="gpurun_out/prof_save_host.txt")
+    ap.add_argument("--no-cprofile", action="store_true", help="plain timings (no profiler overhead)")
     a = ap.parse_args()
     from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
     from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
@@ -70,9 +71,11 @@ def main():
         t0 = time.perf_counter()
         sd = state()
         t1 = time.perf_counter()
-        pr.enable()
+        if not a.no_cprofile:
+            pr.enable()
         ckpt.save_checkpoint(step, sd, storage_type=StorageType.MEMORY)
-        pr.disable()
+        if not a.no_cprofile:
+            pr.disable()
         t2 = time.perf_counter()
         torch.cuda.current_stream().synchronize()
         t3 = time.perf_counter()
@@ -80,10 +83,12 @@ def main():
         parts.append((t1 - t0, t2 - t1, t3 - t2))
         ckpt.wait_latest_checkpoint()
     s = io.StringIO()
-    pstats.Stats(pr, stream=s).sort_stats("cumulative").print_stats(45)
+    if not a.no_cprofile:
+        pstats.Stats(pr, stream=s).sort_stats("cumulative").print_stats(45)
     res = {"save_ms_mean": 1000 * statistics.mean(times), "state_dict_ms": 1000 * statistics.mean(p[0] for p in parts),
            "save_call_ms": 1000 * statistics.mean(p[1] for p in parts),
-           "gpu_wait_ms": 1000 * statistics.mean(p[2] for p in parts)}
+           "gpu_wait_ms": 1000 * statistics.mean(p[2] for p in parts),
+           "speculate": os.environ.get("DWAMD_CKPT_SPECULATE", "1"), "cprofile": not a.no_cprofile}
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:
         f.write(json.dumps(res) + "\n" + s.getvalue())

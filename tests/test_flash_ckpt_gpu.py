@@ -62,6 +62,40 @@ def test_gpu_save_and_restore_in_place(tmp_path):
     ck.close()
 
 
+def test_gpu_speculative_snapshot_hit_and_miss(tmp_path):
+    """The snapshot copy is enqueued from the previous plan before the state
+    dict is verified: unchanged tensors -> hit (no extra copy); a replaced
+    tensor (new storage) and a changed extra tensor -> miss, re-planned and
+    re-copied, and the restore returns the NEW values."""
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+
+    model, opt, flat = _model_and_opt()
+    ck = DdpCheckpointer(str(tmp_path / "ck"))
+    extra = {"t": torch.full((1000,), 1.0, device="cuda")}
+    state = lambda: {"model": model.state_dict(), "opt": opt.state_dict(), "extra": dict(extra)}  # noqa
+    for step in (1, 2, 3):
+        opt.exp_avg.add_(1.0)
+        assert ck.save_checkpoint(step, state(), storage_type=StorageType.MEMORY)
+    assert ck.engine.speculation_misses == 0
+    extra["t"] = torch.full((1000,), 7.0, device="cuda")  # new storage, same shape
+    opt.exp_avg.add_(1.0)
+    assert ck.save_checkpoint(4, state(), storage_type=StorageType.MEMORY)
+    assert ck.engine.speculation_misses == 1
+    extra["t"] = torch.full((2000,), 9.0, device="cuda")  # new size: different payload
+    assert ck.save_checkpoint(5, state(), storage_type=StorageType.MEMORY)
+    assert ck.engine.speculation_misses == 2
+    ck.wait_latest_checkpoint()
+    ref = opt.exp_avg.clone()
+    opt.exp_avg.zero_()
+    extra["t"] = torch.zeros(2000, device="cuda")
+    out = ck.load_checkpoint(target=state())
+    torch.cuda.synchronize()
+    assert torch.equal(opt.exp_avg, ref)
+    assert torch.equal(extra["t"], torch.full((2000,), 9.0, device="cuda"))
+    ck.close()
+
+
 def test_gpu_overlapped_snapshot_is_fenced_by_the_optimizer(tmp_path, monkeypatch):
     """DWAMD_OVERLAP_SNAPSHOT=1: the snapshot copy runs on its own stream while
     training continues; the next optimizer step (the first writer of the
