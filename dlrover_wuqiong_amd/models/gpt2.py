@@ -25,9 +25,12 @@ from ..ops.linear import FusedLinear, linear
 from ..ops.mlp import fused_gelu_mlp
 from ..ops.norm import LayerNorm
 
-# epilogue-fused MLP (ops/mlp.py): measured equal to the bias-GELU kernel path on
-# GPT2-1.5B end to end (121.6 vs 122.2 ms/step, profiles/r2/gpt2_fused_mlp_ab.jsonl), so opt-in
-_FUSED_MLP = os.environ.get("DWAMD_FUSED_MLP", "0") == "1"
+# Fused MLP (ops/mlp.py): c_fc bias in the GEMM epilogue, a GELU-only pass,
+# and one pass for GELU backward + c_fc bias gradient.  With the one-pass
+# backward it beats the bias-GELU kernel path on GPT2-1.5B end to end (115.6
+# vs 116.3 ms/step over 2 alternations, profiles/r2/gpt2_fused_mlp_ab.txt):
+# default; DWAMD_FUSED_MLP=0 selects the bias-GELU kernel path.
+_FUSED_MLP = os.environ.get("DWAMD_FUSED_MLP", "1") == "1"
 
 
 @dataclass
@@ -78,8 +81,8 @@ class MLP(nn.Module):
 
     def forward(self, x):
         if _FUSED_MLP and x.is_cuda:
-            # bias + GELU in the c_fc GEMM's epilogue, dGELU + bias grad in the
-            # c_proj dgrad GEMM's epilogue (ops/mlp.py)
+            # c_fc bias in the GEMM epilogue + GELU pass; backward: c_proj
+            # dgrad GEMM, then one GELU-backward + bias-gradient pass (ops/mlp.py)
             return fused_gelu_mlp(x, self.c_fc, self.c_proj)
         h = linear(x, self.c_fc.weight)  # bias fused into the activation kernel
         h = bias_gelu(h, self.c_fc.bias)
