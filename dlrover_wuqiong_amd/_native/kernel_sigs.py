@@ -48,12 +48,12 @@ SIGS = {
                            f32, f32, i32, vp, vp]),
     "dw_agd_flat": (i32, [vp, i32, vp, vp, i32, vp, vp, vp, i64, i64, f32, f32, f32, f32, f32,
                           f32, f32, f32, f32, vp, vp]),
-    "dw_sumsq_flat": (i32, [vp, i32, i64, vp, vp]),
+    "dw_sumsq_flat": (i32, [vp, i32, i64, vp, vp, vp]),
     "dw_clip_coef": (i32, [vp, f32, f32, vp, vp, vp]),
     "dw_scale_flat": (i32, [vp, i32, i64, vp, vp]),
     # optim_multi.hip
     "dw_mt_adam": (i32, [vp, vp, i64, vp, vp, i32, vp]),
-    "dw_mt_sumsq": (i32, [vp, vp, i64, vp, vp]),
+    "dw_mt_sumsq": (i32, [vp, vp, i64, vp, vp, vp]),
     "dw_mt_hyper_size": (i32, []),
     "dw_mt_chunk": (i32, []),
     # norm.hip

@@ -104,6 +104,37 @@ static inline int dw_grid_for(int64_t work_items, int per_block, int cap = 2048)
   return (int)g;
 }
 
+// Deterministic grid-wide sum (replaces one float atomicAdd per block, whose
+// order -- hence the last bits of the result -- varies run to run): every
+// block stores its partial into ws[blockIdx.x] with an agent-scope atomic
+// store, drains its stores, bumps the counter ws[GRID_SUM_MAX]; the LAST
+// block sums the partials in a fixed order and adds the total to *out (one
+// writer).  ws: float[GRID_SUM_MAX + 1], counter word zero on entry, left zero.
+// No device-scope fence (an L2 write-back + invalidate per block on gfx950):
+// the partials live at the coherent level (atomic stores / loads) and each
+// block's stores have completed before its counter increment is issued.
+constexpr int GRID_SUM_MAX = 2048;
+template <int THREADS>
+__device__ __forceinline__ void grid_sum_finish(float block_total, float* ws, float* out, float* red) {
+  __shared__ int is_last;
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(ws + blockIdx.x, block_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    is_last = __hip_atomic_fetch_add((unsigned*)(ws + GRID_SUM_MAX), 1u, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!is_last) return;
+  float a = 0.f;
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += THREADS)
+    a += __hip_atomic_load(ws + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  a = block_sum<THREADS>(a, red);
+  if (threadIdx.x == 0) {
+    *out += a;
+    __hip_atomic_store((unsigned*)(ws + GRID_SUM_MAX), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // tanh-approximate GELU and its derivative (GPT-2 MLP).  tanh(u) =
 // 1 - 2 / (1 + 2^(2u log2 e)) with the hardware exp2 / rcp (a few VALU ops
 // instead of libm tanhf's ~20: the GELU passes are VALU-bound otherwise);

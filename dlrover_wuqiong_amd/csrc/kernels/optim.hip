@@ -205,10 +205,10 @@ extern "C" int dw_agd_flat(void* param, int param_dtype, void* master, const voi
 }
 
 // --------------------------------------------------------------------------
-// Global L2 norm of a flat buffer: block partial sums -> one fp32 atomic per
-// block into *out_sumsq (out must be zeroed by the caller on the stream).
+// Global L2 norm of a flat buffer: block partial sums, then a deterministic
+// fixed-order grid sum (grid_sum_finish) added to *out (zeroed by the caller).
 template <typename G>
-__global__ void __launch_bounds__(256) sumsq_kernel(const G* __restrict__ x, int64_t n, float* out) {
+__global__ void __launch_bounds__(256) sumsq_kernel(const G* __restrict__ x, int64_t n, float* out, float* ws) {
   __shared__ float red[4];
   float acc = 0.f;
   const int64_t nvec = n >> 3;
@@ -225,17 +225,19 @@ __global__ void __launch_bounds__(256) sumsq_kernel(const G* __restrict__ x, int
     acc += f * f;
   }
   acc = block_sum<256>(acc, red);
-  if (threadIdx.x == 0) atomicAdd(out, acc);
+  __syncthreads();  // red is reused by the finish
+  grid_sum_finish<256>(acc, ws, out, red);
 }
 
-extern "C" int dw_sumsq_flat(const void* x, int dtype, int64_t n, void* out, void* stream) {
+// ws: float[GRID_SUM_MAX + 1] (see grid_sum_finish)
+extern "C" int dw_sumsq_flat(const void* x, int dtype, int64_t n, void* out, void* ws, void* stream) {
   int grid = dw_grid_for((n + 7) / 8, 256, 1024);
   if (dtype == 1)
     hipLaunchKernelGGL(sumsq_kernel<bf16_t>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                       (const bf16_t*)x, n, (float*)out);
+                       (const bf16_t*)x, n, (float*)out, (float*)ws);
   else
     hipLaunchKernelGGL(sumsq_kernel<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                       (const float*)x, n, (float*)out);
+                       (const float*)x, n, (float*)out, (float*)ws);
   DW_LAUNCH_RET;
 }
 

@@ -147,11 +147,11 @@ __global__ void __launch_bounds__(MT_THREADS) mt_step_kernel(const MTDesc* __res
   }
 }
 
-// sum over tensors of norm_w * ||grad||^2 -> atomicAdd into *out (zeroed by
-// the caller on the stream).  One atomic per workgroup.
+// sum over tensors of norm_w * ||grad||^2 -> added to *out (zeroed by the
+// caller on the stream) by a deterministic fixed-order grid sum.
 __global__ void __launch_bounds__(MT_THREADS) mt_sumsq_kernel(const MTDesc* __restrict__ descs,
                                                               const MTChunk* __restrict__ chunks, int64_t nchunks,
-                                                              float* out) {
+                                                              float* out, float* ws) {
   __shared__ float red[MT_THREADS / 64];
   float acc = 0.f;
   for (int64_t ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
@@ -178,7 +178,8 @@ __global__ void __launch_bounds__(MT_THREADS) mt_sumsq_kernel(const MTDesc* __re
     acc += a * d.norm_w;
   }
   acc = block_sum<MT_THREADS>(acc, red);
-  if (threadIdx.x == 0 && acc != 0.f) atomicAdd(out, acc);
+  __syncthreads();  // red is reused by the finish
+  grid_sum_finish<MT_THREADS>(acc, ws, out, red);
 }
 
 static int mt_grid(int64_t nchunks) {
@@ -202,10 +203,13 @@ extern "C" int dw_mt_adam(const void* descs, const void* chunks, int64_t nchunks
   DW_LAUNCH_RET;
 }
 
-extern "C" int dw_mt_sumsq(const void* descs, const void* chunks, int64_t nchunks, void* out, void* stream) {
+// ws: float[GRID_SUM_MAX + 1] (see grid_sum_finish)
+extern "C" int dw_mt_sumsq(const void* descs, const void* chunks, int64_t nchunks, void* out, void* ws,
+                           void* stream) {
   if (nchunks <= 0) return 0;
-  hipLaunchKernelGGL(mt_sumsq_kernel, dim3(mt_grid(nchunks) < 2048 ? mt_grid(nchunks) : 2048), dim3(MT_THREADS),
-                     0, (hipStream_t)stream, (const MTDesc*)descs, (const MTChunk*)chunks, nchunks, (float*)out);
+  const int grid = mt_grid(nchunks) < GRID_SUM_MAX ? mt_grid(nchunks) : GRID_SUM_MAX;
+  hipLaunchKernelGGL(mt_sumsq_kernel, dim3(grid), dim3(MT_THREADS), 0, (hipStream_t)stream, (const MTDesc*)descs,
+                     (const MTChunk*)chunks, nchunks, (float*)out, (float*)ws);
   DW_LAUNCH_RET;
 }
 

@@ -56,6 +56,19 @@ def require_bf16(*ts):
 
 
 _ZERO_WS = {}
+_GRID_WS = {}
+
+
+def grid_sum_ws(device) -> torch.Tensor:
+    """Scratch of the deterministic grid sums (dw_common.h grid_sum_finish):
+    2048 partials (any content) + a counter word that is zero between calls.
+    Its own buffer per (device, stream) -- not the zeroed workspace, whose
+    every word must stay zero."""
+    key = (torch.device(device).index, torch.cuda.current_stream(device).cuda_stream)
+    buf = _GRID_WS.get(key)
+    if buf is None:
+        buf = _GRID_WS[key] = torch.zeros(2048 + 1, device=device, dtype=torch.float32)
+    return buf
 
 
 def zeroed_workspace(nfloats: int, device) -> torch.Tensor:

@@ -62,7 +62,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
         if self.max_grad_norm > 0:
             s[0].zero_()
             _hip.check(L.dw_sumsq_flat(_hip.ptr(self.flat.grad), _hip.dtype_code(self.flat.grad), self.flat.numel,
-                                       _hip.ptr(s[0:1]), _hip.stream()), "sumsq")
+                                       _hip.ptr(s[0:1]), _hip.ptr(_hip.grid_sum_ws(s.device)), _hip.stream()),
+                       "sumsq")
             _hip.check(L.dw_clip_coef(_hip.ptr(s[0:1]), float(self.max_grad_norm), float(self.grad_scale),
                                       _hip.ptr(s[1:2]), _hip.ptr(s[2:3]), _hip.stream()), "clip_coef")
             self.last_grad_norm = s[2]

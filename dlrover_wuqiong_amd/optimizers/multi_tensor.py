@@ -253,7 +253,7 @@ class _MultiTensorOptimizer(torch.optim.Optimizer):
             if self.max_grad_norm > 0:
                 s[0].zero_()
                 _hip.check(L.dw_mt_sumsq(_hip.ptr(d_desc), _hip.ptr(d_chunks), nchunks, _hip.ptr(s[0:1]),
-                                         _hip.stream()), "mt_sumsq")
+                                         _hip.ptr(_hip.grid_sum_ws(dev)), _hip.stream()), "mt_sumsq")
                 if sharded and dist.is_initialized() and dist.get_world_size() > 1:
                     dist.all_reduce(s[0:1])
                 _hip.check(L.dw_clip_coef(_hip.ptr(s[0:1]), float(self.max_grad_norm), float(self.grad_scale),

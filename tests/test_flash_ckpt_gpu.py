@@ -390,7 +390,11 @@ def _ddp_worker(rank, port, q):
                     dist.all_reduce(flat.grad)
                 torch.cuda.synchronize()
                 res[(mode, step)] = flat.grad.float().clone()
-        diff = max(float((res[("ddp", s)] - res[("manual", s)]).abs().max()) for s in range(2))
+        # relative to the gradient scale: the bias / norm-weight column sums
+        # use fp32 atomics, so two runs of the same backward may differ in the
+        # last bits (a bucket launched too early differs at O(1))
+        diff = max(float((res[("ddp", s)] - res[("manual", s)]).abs().max()) /
+                   max(float(res[("manual", s)].abs().max()), 1e-30) for s in range(2))
         q.put((rank, diff))
     except Exception as e:  # pragma: no cover
         import traceback
@@ -419,7 +423,7 @@ def test_gpu_flat_ddp_bucketed_allreduce_matches_manual_sum():
     res = sorted(q.get(timeout=180) for _ in ps)
     for p in ps:
         p.join(timeout=60)
-    assert all(isinstance(d, float) and d == 0.0 for _, d in res), res
+    assert all(isinstance(d, float) and d < 1e-5 for _, d in res), res
 
 
 def test_gpu_busy_save_is_skipped(tmp_path, monkeypatch):
