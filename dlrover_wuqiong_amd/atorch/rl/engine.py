@@ -15,7 +15,7 @@ save/load, actor/critic/ref_model/reward_model properties).
 """
 
 import os
-from typing import Callable, Dict, Optional
+from typing import Callable, Dict, Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -41,20 +41,26 @@ class ModelEngine:
     def __init__(self, actor: nn.Module, critic: nn.Module, ref_model: nn.Module,
                  reward_model: Callable[[torch.Tensor], torch.Tensor], actor_lr: float = 1e-5,
                  critic_lr: float = 1e-5, strategies: Optional[Dict[str, list]] = None,
-                 optim_cls=torch.optim.AdamW):
+                 optim_cls=torch.optim.AdamW, role_optimizers: Optional[Dict[str, Tuple[type, dict]]] = None):
+        """``role_optimizers`` ({role: (optimizer class, kwargs)}, e.g. from
+        an ``AtorchRLConfig``) overrides ``optim_cls`` / the role's lr."""
         self.models: Dict[str, object] = {"actor": actor, "critic": critic, "ref_model": ref_model,
                                           "reward_model": reward_model}
         self.optimizers: Dict[str, torch.optim.Optimizer] = {}
         strategies = strategies or {}
+        role_optimizers = role_optimizers or {}
         for role, lr in (("actor", actor_lr), ("critic", critic_lr)):
             m = self.models[role]
+            cls, kw = role_optimizers.get(role, (optim_cls, {}))
+            kw = dict(kw)
+            kw.setdefault("lr", lr)
             if role in strategies:
                 from ..auto_accelerate import auto_accelerate
 
-                _ok, res, _s = auto_accelerate(m, optim_cls, optim_args={"lr": lr}, load_strategy=strategies[role])
+                _ok, res, _s = auto_accelerate(m, cls, optim_args=kw, load_strategy=strategies[role])
                 self.models[role], self.optimizers[role] = res.model, res.optim
             else:
-                self.optimizers[role] = optim_cls([p for p in m.parameters() if p.requires_grad], lr=lr)
+                self.optimizers[role] = cls([p for p in m.parameters() if p.requires_grad], **kw)
         for role in ("ref_model", "reward_model"):
             m = self.models[role]
             if isinstance(m, nn.Module):

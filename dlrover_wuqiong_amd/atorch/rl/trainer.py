@@ -12,6 +12,7 @@ pre_rl_training / post_rl_training, ``make_experience``, ``rl_training``,
 ``evaluate``, ``train``) and the replay buffer of ``rl/replay_buffer``.
 """
 
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -114,7 +115,11 @@ class RLTrainer:
             for i in range(0, n - self.config.rollout_batch_size + 1, self.config.rollout_batch_size):
                 yield torch.stack([self.dataset[int(j)] for j in idx[i:i + self.config.rollout_batch_size]])
 
-    def train(self, num_rollouts: int) -> List[Dict[str, float]]:
+    def train(self, num_rollouts: int, checkpoint_interval: int = 0,
+              checkpoint_dir: Optional[str] = None) -> List[Dict[str, float]]:
+        """``checkpoint_interval`` > 0 saves actor + critic (and their
+        optimizers) to ``checkpoint_dir/rollout_{it}`` every that many
+        rollouts (reference ``TrainConfig.checkpoint_interval``)."""
         batches = self._prompt_batches()
         for it in range(num_rollouts):
             self.pre_make_experience_hook()
@@ -127,6 +132,8 @@ class RLTrainer:
             self.post_rl_training_hook()
             stats["rollout"] = it
             self.stats_history.append(stats)
+            if checkpoint_interval and checkpoint_dir and (it + 1) % checkpoint_interval == 0:
+                self.engine.save(os.path.join(checkpoint_dir, f"rollout_{it + 1}"))
             logger.info(f"rollout {it}: {stats}")
         return self.stats_history
 
