@@ -16,4 +16,8 @@ cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_gpt2 -o run -- \
   python3 bench.py --steps 4 --warmup 2 --ckpt-interval 100 --no-fault > gpurun_out/prof_gpt2/bench.log 2>&1
 rc=$?; echo prof_rc=$rc
+# keep the summaries only (a kernel trace of a bench run is >64 MiB, and
+# gpurun copies nothing back past that)
+find gpurun_out/prof_gpt2 -name "*kernel_trace*" -delete
+find gpurun_out/prof_gpt2 -name "*.csv" -size +8M -delete
 exit $rc
