@@ -100,6 +100,7 @@ class LlamaAttention(nn.Module):
         super().__init__()
         self.cfg = cfg
         self.tp_group, self.sp_group = tp_group, sp_group
+        self.cp_group = None  # context parallel (zig-zag sequence shard, K/V all-gather): Llama.set_cp
         tp = _ws(tp_group)
         assert cfg.num_attention_heads % tp == 0 and cfg.num_key_value_heads % tp == 0
         self.nh = cfg.num_attention_heads // tp
@@ -130,7 +131,12 @@ class LlamaAttention(nn.Module):
             v = seq_all_to_all(v.contiguous(), 2, 1, self.sp_group, sp)
         q = apply_rope(q.contiguous(), cos, sin)
         k = apply_rope(k.contiguous(), cos, sin)
-        y = flash_attn_func(q, k, v.contiguous(), causal=True)
+        if self.cp_group is not None:
+            from ..parallel.context_parallel import context_parallel_attention
+
+            y = context_parallel_attention(q, k, v.contiguous(), self.cp_group, causal=True)
+        else:
+            y = flash_attn_func(q, k, v.contiguous(), causal=True)
         if sp > 1:
             from ..atorch.distributed import seq_all_to_all
 
@@ -189,6 +195,7 @@ class Llama(nn.Module):
         super().__init__()
         self.cfg = cfg
         self.tp_group, self.sp_group = tp_group, sp_group
+        self.cp_group = None
         tp = _ws(tp_group)
         if tp > 1:
             from ..parallel.tensor_parallel import ColumnParallelLinear, VocabParallelEmbedding
@@ -226,11 +233,29 @@ class Llama(nn.Module):
         for layer in self.layers:
             layer.self_attn.sp_group = g
 
+    def set_cp(self, cp_group):
+        """Context parallel: forward then takes this rank's zig-zag sequence
+        shard (``parallel.context_parallel.zigzag_split`` of ids/targets) and
+        attends over the whole sequence; gradients are averaged over the CP
+        group like data parallel."""
+        g = cp_group if _ws(cp_group) > 1 else None
+        self.cp_group = g
+        for layer in self.layers:
+            layer.self_attn.cp_group = g
+
     def forward(self, ids, targets=None):
         B, S = ids.shape
         sp = _ws(self.sp_group)
         x = self.embed_tokens(ids)
-        cos, sin = rope_table(S * sp, self.cfg.head_dim, self.cfg.rope_theta, x.device)
+        if self.cp_group is not None:
+            from ..parallel.context_parallel import zigzag_positions
+
+            cp = _ws(self.cp_group)
+            cos, sin = rope_table(S * cp, self.cfg.head_dim, self.cfg.rope_theta, x.device)
+            pos = zigzag_positions(S, self.cp_group, device=x.device)
+            cos, sin = cos[pos].contiguous(), sin[pos].contiguous()
+        else:
+            cos, sin = rope_table(S * sp, self.cfg.head_dim, self.cfg.rope_theta, x.device)
         r = None
         for layer in self.layers:
             if self.cfg.activation_checkpointing and self.training:
