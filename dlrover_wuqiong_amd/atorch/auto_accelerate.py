@@ -59,6 +59,7 @@ from ..common.log import logger
 from . import distributed as adist
 
 ORDER = ["parallel_mode", "module_replace", "half", "amp_native", "tensor_parallel", "sequence_parallel",
+         "context_parallel",
          "checkpoint", "pipeline_parallel", "fsdp", "zero2", "zero1", "ddp"]
 ALIASES = {"amp": "amp_native", "amp_native_bf16": "amp_native", "fsdp2": "fsdp", "zero3": "fsdp",
            "pipe": "pipeline_parallel", "pipeline": "pipeline_parallel", "ds_3d_parallel": "pipeline_parallel"}
@@ -293,6 +294,44 @@ def _apply_sequence_parallel(ctx, cfg):
     logger.info(f"sequence_parallel: {size}-way, {len(targets)} {fname}() call(s)")
 
 
+def _apply_context_parallel(ctx, cfg):
+    """Context parallel (``parallel/context_parallel.py``): ``{"cp_size": n,
+    "set_cp_func_name": "set_cp"}`` or just ``n``.  Uses the sequence
+    parallel groups (consecutive ranks of one node), calls ``set_cp(group)``
+    on the model and, in ``prepare_input``, takes this rank's zig-zag shard
+    of every [batch, seq, ...] tensor of the batch; the CP ranks of a group
+    read the same batch and their gradients average like data parallel."""
+    cfg = cfg if isinstance(cfg, dict) else {"cp_size": cfg or 0}
+    size = int(cfg.get("cp_size", cfg.get("size", 0)) or 0)
+    if size <= 1:
+        return
+    if ctx.get("sp"):
+        raise ValueError("context_parallel and sequence_parallel share the sequence groups; use one of them")
+    if adist.get_sequence_parallel_group() is None:
+        adist.create_sequence_parallel_group(size)
+    group, rank = adist.get_sequence_parallel_group(), adist.get_sequence_parallel_rank()
+    fname = cfg.get("set_cp_func_name", "set_cp")
+    targets = [m for m in ctx["model"].modules() if hasattr(m, fname)][:1]
+    if not targets:
+        raise ValueError(f"context_parallel: the model has no {fname}() method")
+    getattr(targets[0], fname)(group)
+
+    def split(batch, _size, _rank):
+        from ..parallel.context_parallel import zigzag_split
+
+        def one(t):
+            return zigzag_split(t, group, dim=1) if torch.is_tensor(t) and t.dim() >= 2 else t
+
+        if isinstance(batch, dict):
+            return {k: one(v) for k, v in batch.items()}
+        if isinstance(batch, (list, tuple)):
+            return type(batch)(one(v) for v in batch)
+        return one(batch)
+
+    ctx["sp"] = (size, rank, cfg.get("batch_cp_processing_fn") or split)
+    logger.info(f"context_parallel: {size}-way (zig-zag shards, K/V all-gather)")
+
+
 def _wrap_cls(ctx, cfg):
     cls = None
     if isinstance(cfg, dict):
@@ -425,7 +464,8 @@ def _apply_ddp(ctx, cfg):
 
 APPLY = {"parallel_mode": _apply_parallel_mode, "module_replace": _apply_module_replace, "half": _apply_half,
          "amp_native": _apply_amp_native, "tensor_parallel": _apply_tensor_parallel,
-         "sequence_parallel": _apply_sequence_parallel, "checkpoint": _apply_checkpoint,
+         "sequence_parallel": _apply_sequence_parallel, "context_parallel": _apply_context_parallel,
+         "checkpoint": _apply_checkpoint,
          "pipeline_parallel": _apply_pipeline_parallel,
          "fsdp": _apply_fsdp, "zero2": functools.partial(_apply_fsdp, reshard=False),
          "zero1": lambda ctx, cfg: ctx.__setitem__("zero1", True), "ddp": _apply_ddp}

@@ -4,6 +4,7 @@ checkpoint, planner) and 2 ranks (ddp, fsdp, zero1, tensor_parallel)
 
 import os
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -260,7 +261,7 @@ def test_four_rank_hsdp():
     assert [r[1] for r in res] == [True] * 4, res
 
 
-def _sp_worker(rank, world, port, q):
+def _sp_worker(rank, world, port, q, mode="sp"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
     try:
@@ -294,7 +295,8 @@ def _sp_worker(rank, world, port, q):
         ok, res, strat = auto_accelerate(
             LM(cfg), torch.optim.SGD, dataset=Tok(), loss_func=lambda b, out: out, optim_args={"lr": 0.1},
             dataloader_args={"batch_size": 2, "shuffle": False}, model_input_format="unpack_dict",
-            load_strategy=["parallel_mode", ("sequence_parallel", {"sp_size": 2, "batch_sp_processing_fn": split})])
+            load_strategy=["parallel_mode", ("sequence_parallel", {"sp_size": 2, "batch_sp_processing_fn": split})
+                           if mode == "sp" else ("context_parallel", {"cp_size": 2})])
         batch = next(iter(res.dataloader))
         shard = res.prepare_input(batch, torch.device("cpu"))
         loss = res.model(**shard)
@@ -313,11 +315,12 @@ def _sp_worker(rank, world, port, q):
         adist.reset_distributed()
 
 
-def test_two_rank_sequence_parallel_strategy():
+@pytest.mark.parametrize("mode", ["sp", "cp"])
+def test_two_rank_sequence_parallel_strategy(mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    ps = [ctx.Process(target=_sp_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_sp_worker, args=(r, 2, port, q, mode)) for r in range(2)]
     for p in ps:
         p.start()
     res = sorted((q.get(timeout=240) for _ in ps), key=lambda x: x[0])
