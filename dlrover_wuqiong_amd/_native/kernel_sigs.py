@@ -43,6 +43,9 @@ SIGS = {
     "dw_xt_hang": (i32, [c.c_char_p, i32, c.POINTER(c.c_double)]),
     "dw_xt_reset": (None, []),
     "dw_xt_pending": (i64, []),
+    # quant.hip
+    "dw_quantize": (i32, [vp, i32, vp, vp, i64, i64, i32, i32, vp]),
+    "dw_dequant_reduce": (i32, [vp, vp, vp, i32, i32, i64, i64, i32, i32, vp]),
     # optim.hip
     "dw_adam_flat": (i32, [vp, i32, vp, vp, i32, vp, vp, vp, i64, i64, f32, f32, f32, f32, f32,
                            f32, f32, i32, vp, vp]),
