@@ -6,10 +6,13 @@ writes the reduced bf16 shard).
 """
 
 import json
+import os
+import sys
 
 import torch
 
-from dlrover_wuqiong_amd.ops.quantization import dequant_reduce, quantize
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dlrover_wuqiong_amd.ops.quantization import dequant_reduce, quantize  # noqa: E402
 
 
 def timed(fn, iters=20):

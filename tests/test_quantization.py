@@ -118,14 +118,15 @@ def test_quant_kernels_gpu(bits, sym, dtype):
     c, p = quantize(x, groups, bits, sym)
     c_ref, p_ref = quantize_reference(x.cpu(), groups, bits, sym)
     torch.cuda.synchronize()
-    assert torch.allclose(p.cpu(), p_ref, rtol=1e-6, atol=1e-6)
+    assert torch.allclose(p.cpu(), p_ref, rtol=1e-5, atol=1e-4)  # zero points: fp32 rounding of qmin - min*scale
     if bits == 8:
         diff = (c.cpu().to(torch.int32) - c_ref.to(torch.int32)).abs()
     else:
         from dlrover_wuqiong_amd.ops.quantization import _unpack4
 
         diff = (_unpack4(c.cpu()) - _unpack4(c_ref)).abs()
-    assert int(diff.max()) <= 1 and float((diff > 0).float().mean()) < 1e-4
+    # ties at x*scale + zp = k + 0.5 round either way under fp32 evaluation-order differences
+    assert int(diff.max()) <= 1 and float((diff > 0).float().mean()) < 1e-3
     y = dequantize(c, p, groups, bits, sym, dtype=torch.float32)
     y_ref = dequantize_reference(c.cpu(), p.cpu(), groups, bits)
     assert torch.allclose(y.cpu(), y_ref, rtol=1e-6, atol=1e-6)
