@@ -24,6 +24,14 @@ for an already-launched bucket raises instead of being silently dropped.
 Gradients are SUMMED; the optimizer divides by the world size inside its
 fused update (``grad_scale``), in fp32, instead of a separate scaling pass.
 
+``grad_comm_bits=8`` (or 4) reduces each bucket through the quantized
+collectives instead (``quantized_comm.quantized_all_reduce``: int8 / int4
+all-to-all reduce-scatter + all-gather, ~1/2 (1/4) of bf16's wire bytes)
+for bandwidth-starved links (multi-node RDMA); it runs on a side stream so
+it still overlaps the rest of backward.  Lossy: ~2^-(bits-1) of each
+group's absmax per element.  Within one xGMI node the exact bf16 all-reduce
+is the default.
+
 Parity: reference trainers wrap models in torch DDP
 (dlrover/trainer/torch/elastic/trainer.py, atorch data_parallel/*); this is
 the framework's own replacement tuned for flat buffers.
@@ -41,11 +49,15 @@ from .flat import FlatParams
 
 class FlatDDP(nn.Module):
     def __init__(self, module: nn.Module, flat: FlatParams, process_group=None, bucket_mb: int = 128,
-                 broadcast_params: bool = True):
+                 broadcast_params: bool = True, grad_comm_bits: Optional[int] = None):
         super().__init__()
         self.module = module
         self.flat = flat
         self.pg = process_group
+        if grad_comm_bits not in (None, 4, 8):
+            raise ValueError("grad_comm_bits must be None, 8 or 4")
+        self.grad_comm_bits = grad_comm_bits
+        self._side = None
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
         self.buckets = flat.grad_slices(bucket_mb << 20)
         self._bucket_of = {}
@@ -93,9 +105,30 @@ class FlatDDP(nn.Module):
             if self._pending[b] > 0:
                 self._pending[b] -= 1
                 if self._pending[b] == 0:
-                    s, e, _ = self.buckets[b]
-                    self._works[b] = dist.all_reduce(self.flat.grad[s:e], group=self.pg, async_op=True)
+                    self._works[b] = self._reduce(b)
         return hook
+
+    def _reduce(self, b):
+        s, e, _ = self.buckets[b]
+        g = self.flat.grad[s:e]
+        if self.grad_comm_bits is None:
+            return dist.all_reduce(g, group=self.pg, async_op=True)
+        from .quantized_comm import quantized_all_reduce
+
+        if not g.is_cuda:
+            quantized_all_reduce(g, self.pg, bits=self.grad_comm_bits)
+            return _Done()
+        # quantize -> all-to-all -> dequant-reduce -> quantize -> all-gather ->
+        # dequantize on a side stream, ordered after the gradient's producer
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=g.device)
+        ready = torch.cuda.current_stream(g.device).record_event()
+        with torch.cuda.stream(self._side):
+            self._side.wait_event(ready)
+            quantized_all_reduce(g, self.pg, bits=self.grad_comm_bits)
+            done = self._side.record_event()
+        g.record_stream(self._side)
+        return _StreamDone(done)
 
     def forward(self, *args, **kwargs):
         self._reset()
@@ -117,9 +150,25 @@ class FlatDDP(nn.Module):
             return
         if self._expected is None:
             self._expected = list(self._calls)
-        for b, (s, e, _) in enumerate(self.buckets):
+        for b in range(len(self.buckets)):
             if self._works[b] is None:
-                self._works[b] = dist.all_reduce(self.flat.grad[s:e], group=self.pg, async_op=True)
+                self._works[b] = self._reduce(b)
         for w in self._works:
             w.wait()
         self._reset()
+
+
+class _Done:
+    def wait(self):
+        return True
+
+
+class _StreamDone:
+    """The compute stream waits for the side-stream reduction (no host sync)."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+        return True

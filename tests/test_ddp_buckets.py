@@ -108,3 +108,58 @@ def test_flat_ddp_buckets_launch_only_when_complete():
     for p in ps:
         p.join(timeout=30)
     assert all(not errs for _, errs in res), res
+
+
+def _qworker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        from dlrover_wuqiong_amd.parallel.ddp import FlatDDP
+        from dlrover_wuqiong_amd.parallel.flat import FlatParams
+
+        dist.init_process_group("gloo", rank=rank, world_size=2)
+        torch.manual_seed(0)
+        net = nn.Sequential(nn.Linear(64, 256), nn.Tanh(), nn.Linear(256, 64))
+        import copy
+
+        ref_net = copy.deepcopy(net)
+        flat = FlatParams(net)
+        ddp = FlatDDP(net, flat, bucket_mb=1, grad_comm_bits=8)
+        errs = []
+        for step in range(3):
+            flat.zero_grad()
+            ref_net.zero_grad()
+            x = torch.randn(16, 64, generator=torch.Generator().manual_seed(10 * step + rank))
+            (ddp(x) ** 2).mean().backward()
+            (ref_net(x) ** 2).mean().backward()
+            ddp.finish_gradient_sync()
+            got = torch.cat([p.grad.reshape(-1) for p in net.parameters()])
+            ref = torch.cat([p.grad.reshape(-1) for p in ref_net.parameters()])
+            dist.all_reduce(ref)
+            rel = float((got - ref).abs().max() / ref.abs().max())
+            if rel > 2 / 128:
+                errs.append(f"step {step}: quantized reduce error {rel:.4f}")
+        # both replicas hold the same (quantized) sum
+        g = flat.grad.clone()
+        other = [torch.empty_like(g) for _ in range(2)]
+        dist.all_gather(other, g)
+        if not torch.equal(other[0], other[1]):
+            errs.append("replicas differ")
+        q.put((rank, errs))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, [repr(e)]))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_flat_ddp_quantized_grad_reduce():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_qworker, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=30)
+    assert all(not errs for _, errs in res), res

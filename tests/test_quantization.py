@@ -140,3 +140,42 @@ def test_quant_kernels_gpu(bits, sym, dtype):
     dequant_reduce(codes, params, n_src, elems, gs, bits, out=out, accumulate=True)
     ref = 1.0 + sum(dequantize_reference(a.cpu(), b.cpu(), elems // gs, bits) for a, b in qs)
     assert torch.allclose(out.float().cpu(), ref, rtol=1e-2, atol=1e-2)
+
+
+def _rccl_worker(rank, world, port, out_q):
+    import torch.distributed as dist
+
+    from dlrover_wuqiong_amd.parallel.quantized_comm import (quantized_all_gather, quantized_all_reduce,
+                                                             quantized_reduce_scatter)
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world)
+    try:
+        x = torch.randn(1 << 20, device="cuda", dtype=torch.bfloat16)
+        g = quantized_all_gather(x, bits=8)
+        rs = quantized_reduce_scatter(x, bits=8)
+        y = x.float().clone()
+        quantized_all_reduce(y, bits=4)
+        torch.cuda.synchronize()
+        amax = float(x.float().abs().max())
+        out_q.put((float((g.float() - x.float()).abs().max()) / amax, float((rs.float() - x.float()).abs().max()) / amax,
+                   float((y - x.float()).abs().max()) / amax))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_quantized_collectives_rccl_single_rank():
+    """The RCCL code paths (all_gather_into_tensor / all_to_all_single) and
+    the HIP kernels together, in a one-rank RCCL world (one GPU per box)."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(0, 1, find_free_port(), q))
+    p.start()
+    e_ag, e_rs, e_ar = q.get(timeout=120)
+    p.join(60)
+    assert p.exitcode == 0
+    assert e_ag <= 1 / 128 * 1.01 and e_rs <= 1 / 128 * 1.01 and e_ar <= 2 / 8 * 1.01, (e_ag, e_rs, e_ar)
