@@ -344,9 +344,13 @@ def worker(a) -> int:
     from dlrover_wuqiong_amd.elastic_agent.standby import is_standby
 
     if is_standby():
-        # warm every kernel / allocator pool / library heuristic the first
-        # real step will use (forward + backward, no optimizer update)
-        x = torch.randint(0, cfg.vocab_size, (B, S + 1), device=device)
+        # load every kernel / library handle the first real step will use
+        # (forward + backward, no optimizer update).  A replacement standby is
+        # spawned while training runs on the same GPU, so its warm-up steals
+        # GPU time from the live job: one sample (1/B of a step's FLOPs) loads
+        # the same kernels; the allocator pool is released below anyway.
+        wb = int(os.environ.get("DWAMD_STANDBY_WARMUP_BATCH", "1")) or B
+        x = torch.randint(0, cfg.vocab_size, (min(wb, B), S + 1), device=device)
         model(x[:, :-1], x[:, 1:]).backward()
         flat.zero_grad()
         del x
