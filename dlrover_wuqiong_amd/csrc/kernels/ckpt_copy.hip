@@ -24,7 +24,9 @@ struct CopyDesc {
 
 // Each block walks descriptors in a grid-stride manner over "chunks".
 // Descriptors are pre-split on the host into <= chunk_bytes pieces so the work
-// per descriptor is bounded and the grid fills all 256 CUs.
+// per descriptor is bounded and the grid fills all 256 CUs.  U independent
+// 16-byte loads in flight per lane; NT: nontemporal (streaming) loads/stores.
+template <int U, bool NT>
 __global__ void __launch_bounds__(256) multi_copy_kernel(const CopyDesc* __restrict__ descs,
                                                          int64_t n) {
   for (int64_t d = blockIdx.x; d < n; d += gridDim.x) {
@@ -40,16 +42,17 @@ __global__ void __launch_bounds__(256) multi_copy_kernel(const CopyDesc* __restr
       const u32x4* s = (const u32x4*)(c.src + head);
       u32x4* t = (u32x4*)(c.dst + head);
       int64_t i = threadIdx.x;
-      // 4 independent 16B loads in flight per lane
-      for (; i + 3 * 256 < nv; i += 4 * 256) {
-        u32x4 a = __builtin_nontemporal_load(s + i);
-        u32x4 b = __builtin_nontemporal_load(s + i + 256);
-        u32x4 e = __builtin_nontemporal_load(s + i + 512);
-        u32x4 f = __builtin_nontemporal_load(s + i + 768);
-        __builtin_nontemporal_store(a, t + i);
-        __builtin_nontemporal_store(b, t + i + 256);
-        __builtin_nontemporal_store(e, t + i + 512);
-        __builtin_nontemporal_store(f, t + i + 768);
+      for (; i + (U - 1) * 256 < nv; i += U * 256) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(s + i + u * 256) : s[i + u * 256];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (NT)
+            __builtin_nontemporal_store(v[u], t + i + u * 256);
+          else
+            t[i + u * 256] = v[u];
+        }
       }
       for (; i < nv; i += 256) __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), t + i);
     } else if (((sa | da | (uintptr_t)c.nbytes) & 3) == 0) {
@@ -63,15 +66,27 @@ __global__ void __launch_bounds__(256) multi_copy_kernel(const CopyDesc* __restr
   }
 }
 
+// A/B variants of the snapshot copy (scripts/bench_snapshot_copy.py):
+// 0 = U4 nontemporal (default), 1 = U8 nontemporal, 2 = U4 temporal, 3 = U8 temporal.
+extern "C" int dw_multi_copy_variant(const void* descs_dev, int64_t n, int variant, int max_blocks, void* stream) {
+  if (n <= 0) return 0;
+  const int64_t cap = max_blocks > 0 ? max_blocks : 4096;
+  const int grid = (int)(n < cap ? n : cap);
+  hipStream_t s = (hipStream_t)stream;
+  const CopyDesc* d = (const CopyDesc*)descs_dev;
+  switch (variant) {
+    case 1: hipLaunchKernelGGL((multi_copy_kernel<8, true>), dim3(grid), dim3(256), 0, s, d, n); break;
+    case 2: hipLaunchKernelGGL((multi_copy_kernel<4, false>), dim3(grid), dim3(256), 0, s, d, n); break;
+    case 3: hipLaunchKernelGGL((multi_copy_kernel<8, false>), dim3(grid), dim3(256), 0, s, d, n); break;
+    default: hipLaunchKernelGGL((multi_copy_kernel<4, true>), dim3(grid), dim3(256), 0, s, d, n); break;
+  }
+  DW_LAUNCH_RET;
+}
+
 // max_blocks > 0 bounds the grid: a background snapshot copy that trickles
 // through a few CUs beside the training kernels instead of taking the chip.
 extern "C" int dw_multi_copy_grid(const void* descs_dev, int64_t n, int max_blocks, void* stream) {
-  if (n <= 0) return 0;
-  const int64_t cap = max_blocks > 0 ? max_blocks : 4096;
-  int grid = (int)(n < cap ? n : cap);
-  hipLaunchKernelGGL(multi_copy_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                     (const CopyDesc*)descs_dev, n);
-  DW_LAUNCH_RET;
+  return dw_multi_copy_variant(descs_dev, n, 0, max_blocks, stream);
 }
 
 extern "C" int dw_multi_copy(const void* descs_dev, int64_t n, void* stream) {
