@@ -345,10 +345,21 @@ __global__ void __launch_bounds__(256) norm_bwd_fused_kernel(
   if (threadIdx.x == 0) __hip_atomic_exchange(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-static int colred_rows_per_blk(int64_t rows, int C) {
-  // aim for ~4 blocks per CU over 256 CUs
+static int colred_rows_per_blk(int64_t rows, int C, int dflt_blocks) {
+  // Grid-size target per kernel flavour (DWAMD_COLRED_BLOCKS overrides all,
+  // for A/B).  Fewer row blocks = fewer same-address atomics per column; the
+  // plain column sum is atomic-bound and wants ~1 block per CU, the fused
+  // GELU backward (3 streams of HBM traffic) wants more memory parallelism.
+  // Measured on GPT2-1.5B shapes (scripts/bench_colred.py, profiles/r2/
+  // bench_colred.jsonl): colsum 8192x1600 16.5 -> 10.9 us at 256 blocks,
+  // gelu_bwd_dbias 8192x6400 60.9 -> 56.9 us at 2048.
+  static const int env_target = [] {
+    const char* e = getenv("DWAMD_COLRED_BLOCKS");
+    return e ? atoi(e) : 0;
+  }();
+  const int target = env_target > 0 ? env_target : dflt_blocks;
   const int64_t col_blks = (C + 511) / 512;
-  int64_t rs = (1024 + col_blks - 1) / col_blks;
+  int64_t rs = (target + col_blks - 1) / col_blks;
   if (rs < 1) rs = 1;
   int64_t per = (rows + rs - 1) / rs;
   per = (per + 3) / 4 * 4;
@@ -360,7 +371,7 @@ extern "C" int dw_colsum_acc(const void* dy, int64_t rows, int C, void* ws, void
                              void* stream) {
   if (C % 8 != 0) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  const int per = colred_rows_per_blk(rows, C);
+  const int per = colred_rows_per_blk(rows, C, 256);
   dim3 grid((C + 511) / 512, (unsigned)((rows + per - 1) / per));
   hipLaunchKernelGGL(colred_kernel<0>, grid, dim3(256), 0, s, (const bf16_t*)dy, nullptr, nullptr, nullptr,
                      (float*)ws, rows, C, per, out, nullptr, out_fp32, accumulate);
@@ -372,7 +383,7 @@ extern "C" int dw_gelu_bwd_dbias(const void* dy, const void* pre, void* dx, int6
                                  void* dbias, int out_fp32, int accumulate, void* stream) {
   if (C % 8 != 0) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  const int per = colred_rows_per_blk(rows, C);
+  const int per = colred_rows_per_blk(rows, C, 2048);
   dim3 grid((C + 511) / 512, (unsigned)((rows + per - 1) / per));
   hipLaunchKernelGGL(colred_kernel<3>, grid, dim3(256), 0, s, (const bf16_t*)dy, (const bf16_t*)pre, nullptr,
                      nullptr, (float*)ws, rows, C, per, dbias, nullptr, out_fp32, accumulate, (bf16_t*)dx);
@@ -432,7 +443,11 @@ extern "C" int dw_norm_bwd2(const void* dy, const void* x, const void* gamma, co
                          (bf16_t*)dx, rows, H);
   });
   if (!dgamma && !dbeta) { DW_LAUNCH_RET; }
-  const int per = colred_rows_per_blk(rows, H);
+  static const int norm_blocks = [] {
+    const char* e = getenv("DWAMD_COLRED_NORM_BLOCKS");
+    return e && atoi(e) > 0 ? atoi(e) : 1024;
+  }();
+  const int per = colred_rows_per_blk(rows, H, norm_blocks);
   dim3 cg((H + 511) / 512, (unsigned)((rows + per - 1) / per));
   // both halves are consumed (and cleared) even if one output is absent
   if (rms)
