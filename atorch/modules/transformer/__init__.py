@@ -1,0 +1,7 @@
+"""Compatibility import path (reference: atorch/atorch/modules/transformer).
+
+Thin re-export onto the MI355X-native implementation in ``dlrover_wuqiong_amd.ops``;
+existing ATorch user code imports unchanged.
+"""
+
+from dlrover_wuqiong_amd.ops.cross_entropy import CrossEntropyLoss  # noqa: F401

@@ -175,3 +175,21 @@ def test_replay_buffer_dataset():
     assert len(ds) == 2 and ds[1] == {"a": 3, "b": 4}
     b.reset()
     assert len(b) == 0
+
+
+def test_atorch_compat_import_paths():
+    """Reference ATorch import paths resolve onto this framework."""
+    from atorch.fault_tolerance import HangingDetector  # noqa: F401
+    from atorch.modules.distributed_transformer import context_parallel_attention  # noqa: F401
+    from atorch.modules.moe import MoELayer, TopkGate  # noqa: F401
+    from atorch.modules.transformer import CrossEntropyLoss  # noqa: F401
+    from atorch.modules.transformer.layers import flash_attn_varlen_func  # noqa: F401
+    from atorch.mup import MuAdam, OutputLayer, set_base_shapes  # noqa: F401
+    from atorch.normalization import AtorchLayerNorm
+    from atorch.ops.quantizer import CUDAQuantizer
+
+    x = torch.randn(4, 16)
+    ln = AtorchLayerNorm(16)
+    assert ln(x).shape == x.shape
+    c, p = CUDAQuantizer().quantize(torch.randn(8000))
+    assert c.dtype == torch.int8 and p.shape[1] == 2
