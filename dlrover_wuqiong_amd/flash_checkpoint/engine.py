@@ -647,8 +647,11 @@ class CheckpointEngine(ABC):
         if self._replicated and self._num_slices > 1 and self._gather_group is None:
             return {}  # that restore path reads every slice from shm
         h = self._shm_handler
+        t0 = time.perf_counter()
+        sub = self.hbm_scan_breakdown = {}
         if h.shared_memory is None and not h.init_shared_memory(create=False):
             return {}
+        sub["attach"] = round(time.perf_counter() - t0, 4)
         complete = h.complete_steps()
         out = {}
         metas = {}
@@ -658,7 +661,9 @@ class CheckpointEngine(ABC):
                 continue
             for s in range(h.num_slots):
                 if s not in metas:
+                    t1 = time.perf_counter()
                     metas[s] = h.get_meta(s)
+                    sub[f"meta{s}"] = round(time.perf_counter() - t1, 4)
                 cfg = metas[s].get(DLROVER_CKPT_CONFIG_KEY)
                 if cfg is not None and cfg.step == st and cfg.num_slices == self._num_slices:
                     out[st] = s
@@ -687,6 +692,8 @@ class CheckpointEngine(ABC):
         cands = dict(hbm_only)
         cands.update(complete)
         lap("hbm_scan")
+        for k, v in (getattr(self, "hbm_scan_breakdown", None) or {}).items():
+            tb["hbm_scan." + k] = v
         step = agree_on_step(self._ctl_group, list(cands) if holds else None)
         slot = cands.get(step, -1) if (step > 0 and holds) else -1
         if step <= 0 or not check_all_rank_ready(self._ctl_group, slot >= 0 or not holds):
