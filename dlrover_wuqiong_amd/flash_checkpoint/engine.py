@@ -659,7 +659,15 @@ class CheckpointEngine(ABC):
             st, pid, _nb = h.hbm_stamp(self._slice_idx, b)
             if st <= 0 or pid != os.getpid() or st in complete:
                 continue
+            from .shm_handler import META_WORDS
+
+            hdr = getattr(h, "_header", None)
             for s in range(h.num_slots):
+                # the slot's header step word (written with its metadata at
+                # save time) names the candidate: unpickle only that slot's
+                # metadata, not every slot's
+                if hdr is not None and int(hdr[META_WORDS + 2 * s]) not in (0, st):
+                    continue
                 if s not in metas:
                     t1 = time.perf_counter()
                     metas[s] = h.get_meta(s)
