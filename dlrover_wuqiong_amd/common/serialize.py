@@ -43,39 +43,74 @@ import io  # noqa: E402
 import pickle  # noqa: E402
 
 _SAFE_BUILTINS = {"set", "frozenset", "dict", "list", "tuple", "int", "float", "complex", "bytes", "bytearray",
-                  "str", "bool", "slice", "range", "object", "NoneType", "Ellipsis"}
-_CLASS_MODULES = ("collections", "torch", "numpy", "argparse", "enum", "datetime", "decimal", "fractions",
-                  "megatron", "deepspeed", "transformers", "dlrover_wuqiong_amd", "dlrover", "atorch", "pathlib",
-                  "types", "typing", "uuid")
-_SAFE_FUNCS = {("copyreg", "_reconstructor"), ("_codecs", "encode"), ("torch._tensor", "_rebuild_from_type_v2"),
-               ("numpy.core.multiarray", "_reconstruct"), ("numpy._core.multiarray", "_reconstruct"),
-               ("numpy.core.multiarray", "scalar"), ("numpy._core.multiarray", "scalar"),
-               ("numpy.random._pickle", "__randomstate_ctor"), ("numpy.random._pickle", "__bit_generator_ctor"),
-               ("numpy.random._pickle", "__generator_ctor"), ("torch", "device"), ("torch", "Size"),
-               ("collections", "OrderedDict"), ("torch.serialization", "_get_layout")}
+                  "str", "bool", "slice", "range", "NoneType", "Ellipsis"}
+# exact (module, name) pairs: plain data classes and the reconstruction
+# helpers torch / numpy pickles reference.  Everything not listed here or
+# under _CLASS_PREFIXES is refused -- in particular nothing from ``types``
+# (bar the plain-data SimpleNamespace), ``typing``, ``functools``, ``operator``, ``pathlib``, ``os`` or ``sys``, so a
+# payload cannot build a CodeType / FunctionType and REDUCE on it.
+_SAFE_PAIRS = {
+    ("collections", "OrderedDict"), ("collections", "defaultdict"), ("collections", "deque"),
+    ("collections", "Counter"), ("argparse", "Namespace"), ("copyreg", "_reconstructor"), ("_codecs", "encode"),
+    ("datetime", "datetime"), ("datetime", "date"), ("datetime", "time"), ("datetime", "timedelta"),
+    ("datetime", "timezone"), ("decimal", "Decimal"), ("fractions", "Fraction"), ("uuid", "UUID"),
+    ("enum", "Enum"), ("enum", "IntEnum"), ("types", "SimpleNamespace"),
+    ("torch", "device"), ("torch", "Size"), ("torch", "dtype"), ("torch", "layout"), ("torch", "memory_format"),
+    ("torch", "Tensor"), ("torch._tensor", "_rebuild_from_type_v2"), ("torch.nn.parameter", "Parameter"),
+    ("torch.serialization", "_get_layout"), ("torch.storage", "UntypedStorage"), ("torch.storage", "TypedStorage"),
+    ("torch", "UntypedStorage"), ("torch.distributed.checkpoint.filesystem", "_StorageInfo"),
+    ("numpy", "ndarray"), ("numpy", "dtype"), ("numpy.core.multiarray", "_reconstruct"),
+    ("numpy._core.multiarray", "_reconstruct"), ("numpy.core.multiarray", "scalar"),
+    ("numpy._core.multiarray", "scalar"), ("numpy.random._pickle", "__randomstate_ctor"),
+    ("numpy.random._pickle", "__bit_generator_ctor"), ("numpy.random._pickle", "__generator_ctor"),
+    ("numpy.random.mtrand", "RandomState"), ("numpy.random._generator", "Generator"),
+    ("numpy.random._mt19937", "MT19937"), ("numpy.random._pcg64", "PCG64"),
+}
+# modules whose *classes* (never functions) may resolve: checkpoint metadata
+# and framework config objects.  Metaclasses and callable-wrapping types are
+# still refused (see _class_ok).
+_CLASS_PREFIXES = ("torch.distributed.checkpoint.metadata", "torch.distributed.checkpoint.planner",
+                   "torch.distributed._shard.metadata", "torch.distributed._shard.sharded_tensor.metadata",
+                   "torch.distributed._shard.sharding_spec", "numpy.dtypes", "megatron", "deepspeed",
+                   "transformers.training_args", "transformers.trainer_utils", "transformers.trainer_callback",
+                   "dlrover_wuqiong_amd", "dlrover", "atorch")
 
 
-def _module_ok(module: str) -> bool:
-    return module in ("builtins", "copyreg", "_codecs") or any(
-        module == m or module.startswith(m + ".") for m in _CLASS_MODULES)
+def _under(module: str, prefixes) -> bool:
+    return any(module == m or module.startswith(m + ".") for m in prefixes)
+
+
+def _class_ok(obj) -> bool:
+    import types as _t
+
+    if not isinstance(obj, type) or issubclass(obj, type):
+        return False  # metaclasses build arbitrary classes
+    bad = (_t.FunctionType, _t.CodeType, _t.ModuleType, _t.MethodType, _t.BuiltinFunctionType)
+    return not issubclass(obj, bad)
 
 
 class RestrictedUnpickler(pickle.Unpickler):
     def find_class(self, module, name):
-        if not _module_ok(module):
-            raise pickle.UnpicklingError(f"refusing to unpickle {module}.{name}")
-        if module == "builtins" and name not in _SAFE_BUILTINS:
-            raise pickle.UnpicklingError(f"refusing to unpickle builtins.{name}")
-        obj = super().find_class(module, name)
-        if isinstance(obj, type):
-            return obj
-        if (module, name) in _SAFE_FUNCS or (module == "torch._utils" and name.startswith("_rebuild")):
-            return obj
+        if module == "builtins":
+            if name not in _SAFE_BUILTINS:
+                raise pickle.UnpicklingError(f"refusing to unpickle builtins.{name}")
+            return super().find_class(module, name)
         import torch
 
-        if isinstance(obj, (torch.dtype, torch.layout, torch.memory_format)):
-            return obj
-        raise pickle.UnpicklingError(f"refusing to unpickle callable {module}.{name}")
+        if (module, name) in _SAFE_PAIRS:
+            return super().find_class(module, name)
+        if module == "torch._utils" and name.startswith("_rebuild"):
+            return super().find_class(module, name)
+        if module == "torch" and (name.endswith("Storage") or isinstance(getattr(torch, name, None),
+                                                                          (torch.dtype, torch.layout,
+                                                                           torch.memory_format))):
+            return super().find_class(module, name)
+        if _under(module, _CLASS_PREFIXES):
+            obj = super().find_class(module, name)
+            if _class_ok(obj):
+                return obj
+            raise pickle.UnpicklingError(f"refusing to unpickle non-class {module}.{name}")
+        raise pickle.UnpicklingError(f"refusing to unpickle {module}.{name}")
 
 
 def restricted_loads(data: bytes):

@@ -43,3 +43,28 @@ def test_safe_torch_load_falls_back_to_allow_list(tmp_path):
     bad.seek(0)
     with pytest.raises(Exception):
         safe_torch_load(bad)
+
+
+@pytest.mark.parametrize("module,name", [("types", "CodeType"), ("types", "FunctionType"), ("typing", "cast"),
+                                         ("functools", "partial"), ("builtins", "getattr"), ("builtins", "type"),
+                                         ("builtins", "object"), ("pathlib", "Path"), ("operator", "attrgetter"),
+                                         ("torch", "load"), ("numpy", "load"), ("torch.hub", "load")])
+def test_restricted_loads_refuses_callable_builders(module, name):
+    # GLOBAL <module> <name> ; EMPTY_TUPLE ; REDUCE ; STOP -- the shape of a
+    # CodeType/FunctionType chain that would execute attacker bytecode
+    payload = b"c" + module.encode() + b"\n" + name.encode() + b"\n)R."
+    with pytest.raises(pickle.UnpicklingError):
+        restricted_loads(payload)
+
+
+def test_restricted_loads_dcp_metadata():
+    from torch.distributed.checkpoint.metadata import (ChunkStorageMetadata, Metadata, MetadataIndex,
+                                                       TensorProperties, TensorStorageMetadata)
+
+    md = Metadata(state_dict_metadata={"w": TensorStorageMetadata(
+        properties=TensorProperties(dtype=torch.bfloat16), size=torch.Size([4, 4]),
+        chunks=[ChunkStorageMetadata(offsets=torch.Size([0, 0]), sizes=torch.Size([4, 4]))])},
+        storage_data={MetadataIndex("w", torch.Size([0, 0]), 0): "x"})
+    out = restricted_loads(pickle.dumps(md))
+    assert out.state_dict_metadata["w"].size == torch.Size([4, 4])
+    assert out.state_dict_metadata["w"].properties.dtype is torch.bfloat16
