@@ -110,6 +110,7 @@ def _declare_runtime(lib):
         "dw_memcpy_parallel": (i32, [vp, vp, u64, i32]),
         "dw_write_file": (i32, [cp, vp, u64, u64, i32, i32]),
         "dw_read_file": (i32, [cp, vp, u64, u64, i32]),
+        "dw_read_file_direct": (i32, [cp, vp, u64, u64, i32, i32]),
         "dw_crc32c": (u32, [vp, u64, u32]),
         "dw_ctl_open": (vp, [cp, i32, u32, u64, u64]),
         "dw_ctl_close": (i32, [vp]),

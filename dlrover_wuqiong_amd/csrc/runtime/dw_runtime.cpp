@@ -19,6 +19,7 @@
 // C ABI only (loaded through ctypes) so it has no Python/PyTorch ABI coupling.
 
 #include <errno.h>
+#include <stdio.h>
 #include <fcntl.h>
 #include <pthread.h>
 #include <signal.h>
@@ -232,6 +233,68 @@ int dw_read_file(const char* path, void* buf, uint64_t n, uint64_t file_off, int
   return 0;
 }
 
+// Cold read of a persisted checkpoint range into host memory.
+// flags bit0: O_DIRECT (bypass the page cache: what a restore after a node
+// replacement sees); the 4 KiB-aligned body is read with nthreads concurrent
+// O_DIRECT streams and the unaligned tail (or everything, when the file system
+// refuses O_DIRECT or buf/off are unaligned) through the page cache.
+// flags bit1: posix_fadvise(DONTNEED) over the range first (drops clean cached
+// pages: a buffered read then also comes from the device).
+// Returns 1 if O_DIRECT was used for the body, 0 if buffered, -1 on error.
+int dw_read_file_direct(const char* path, void* buf, uint64_t n, uint64_t file_off, int nthreads, int flags) {
+  const uint64_t A = 4096;
+  if (flags & 2) {
+    int fd0 = open(path, O_RDONLY);
+    if (fd0 >= 0) { posix_fadvise(fd0, (off_t)file_off, (off_t)n, POSIX_FADV_DONTNEED); close(fd0); }
+  }
+  uint64_t body = 0;
+  int dfd = -1;
+  if ((flags & 1) && ((uintptr_t)buf % A) == 0 && (file_off % A) == 0) {
+    dfd = open(path, O_RDONLY | O_DIRECT);
+    if (dfd >= 0) body = n / A * A;
+  }
+  nthreads = std::max(1, nthreads);
+  std::atomic<int> failed{0};
+  if (body > 0) {
+    // 8 MiB-granular work items handed out dynamically: O_DIRECT streams keep
+    // the device queue deep without one slow thread holding the tail
+    const uint64_t item = 8ull << 20;
+    std::atomic<uint64_t> next{0};
+    int nt = (int)std::min<uint64_t>((uint64_t)nthreads, (body + item - 1) / item);
+    std::vector<std::thread> ts;
+    for (int t = 0; t < nt; ++t) {
+      ts.emplace_back([&]() {
+        for (;;) {
+          uint64_t b = next.fetch_add(item);
+          if (b >= body || failed.load()) break;
+          uint64_t e = std::min(body, b + item);
+          char* dst = (char*)buf + b;
+          uint64_t m = e - b, off = file_off + b;
+          while (m > 0) {
+            ssize_t r = pread(dfd, dst, (size_t)m, (off_t)off);
+            if (r < 0) { if (errno == EINTR) continue; failed = 1; break; }
+            if (r == 0) { errno = EIO; failed = 1; break; }
+            dst += r; m -= (uint64_t)r; off += (uint64_t)r;
+            if (m % A) break;  // short read at EOF: the buffered tail path finishes it
+          }
+        }
+      });
+    }
+    for (auto& t : ts) t.join();
+    close(dfd);
+    if (failed) {
+      if (errno == EINVAL) { body = 0; failed = 0; }  // O_DIRECT refused mid-way: redo buffered
+      else { set_err("pread(O_DIRECT)"); return -1; }
+    }
+  } else if (dfd >= 0) {
+    close(dfd);
+  }
+  if (body < n) {
+    if (dw_read_file(path, (char*)buf + body, n - body, file_off + body, nthreads) != 0) return -1;
+  }
+  return body > 0 ? 1 : 0;
+}
+
 // CRC32C (Castagnoli), slicing-by-1 table; used to verify persisted shards.
 static uint32_t g_crc_table[256];
 static std::atomic<int> g_crc_init{0};
@@ -403,10 +466,32 @@ int dw_ctl_close(void* p) {
 // The "held" flag is separate from the pthread mutex so that acquire/release
 // may happen from different threads (the reference's SharedLock semantics).
 // timeout < 0 blocks forever; returns 1 acquired, 0 not acquired.
+// A lock holder that no longer runs: gone (ESRCH) or a zombie / dying task
+// whose exit has not been reaped yet.  A SIGKILLed worker with tens of GB of
+// mappings stays a zombie for ~1 s while its address space is torn down; its
+// locks must be reclaimable at once, or the restarted worker's first saves
+// see every slot "held".
+static bool pid_gone(pid_t pid) {
+  if (kill(pid, 0) != 0) return errno == ESRCH;
+  char path[64];
+  snprintf(path, sizeof(path), "/proc/%d/stat", (int)pid);
+  int fd = open(path, O_RDONLY);
+  if (fd < 0) return false;
+  char buf[512];
+  ssize_t n = read(fd, buf, sizeof(buf) - 1);
+  close(fd);
+  if (n <= 0) return false;
+  buf[n] = 0;
+  const char* rp = strrchr(buf, ')');  // comm may contain spaces / parens
+  if (!rp || rp[1] != ' ') return false;
+  char st = rp[2];
+  return st == 'Z' || st == 'X' || st == 'x';
+}
+
 int dw_lock_acquire(void* p, int blocking, double timeout) {
   CtlHeader* h = (CtlHeader*)p;
   if (robust_lock(h) != 0) return 0;
-  if (h->held && h->holder_pid > 0 && kill(h->holder_pid, 0) != 0 && errno == ESRCH) {
+  if (h->held && h->holder_pid > 0 && pid_gone(h->holder_pid)) {
     h->held = 0;  // holder died without releasing
   }
   if (!blocking) {
@@ -426,7 +511,7 @@ int dw_lock_acquire(void* p, int blocking, double timeout) {
       if (left < slice) slice = left;
     }
     if (seq_wait_unlocked(h, &h->seq_not_full, slice) != 0) return 0;
-    if (h->held && h->holder_pid > 0 && kill(h->holder_pid, 0) != 0 && errno == ESRCH) h->held = 0;
+    if (h->held && h->holder_pid > 0 && pid_gone(h->holder_pid)) h->held = 0;
   }
   h->held = 1;
   h->holder_pid = getpid();
@@ -447,7 +532,7 @@ int dw_lock_release(void* p) {
 int dw_lock_locked(void* p) {
   CtlHeader* h = (CtlHeader*)p;
   if (robust_lock(h) != 0) return 0;
-  if (h->held && h->holder_pid > 0 && kill(h->holder_pid, 0) != 0 && errno == ESRCH) h->held = 0;
+  if (h->held && h->holder_pid > 0 && pid_gone(h->holder_pid)) h->held = 0;
   int r = h->held;
   pthread_mutex_unlock(&h->mu);
   return r;

@@ -58,6 +58,37 @@ def test_lock_reclaimed_from_dead_holder():
     lk.unlink()
 
 
+def test_lock_reclaimed_from_zombie_holder(_isolated_shm):
+    """A SIGKILLed holder that is not reaped yet (a zombie: its parent, like
+    the agent reaping in the background, has not waited) no longer owns the
+    lock: a non-blocking acquire succeeds at once."""
+    import signal
+    import subprocess
+    import sys
+
+    lk = SharedLock("lz", create=True)
+    code = ("import os, signal, sys; sys.path.insert(0, %r)\n"
+            "from dlrover_wuqiong_amd.common.multi_process import SharedLock\n"
+            "lk = SharedLock('lz'); lk.acquire(); print('held', flush=True); signal.pause()") % os.getcwd()
+    p = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True)
+    try:
+        assert p.stdout.readline().strip() == "held"
+        assert not lk.acquire(blocking=False)
+        os.kill(p.pid, signal.SIGKILL)
+        deadline = time.time() + 10
+        while time.time() < deadline:  # wait for the zombie state, without reaping it
+            with open(f"/proc/{p.pid}/stat") as f:
+                if f.read().rsplit(")", 1)[1].split()[0] == "Z":
+                    break
+            time.sleep(0.01)
+        assert lk.acquire(blocking=False)
+        lk.release()
+    finally:
+        p.kill()
+        p.wait()
+        lk.unlink()
+
+
 def _producer(name, n):
     q = SharedQueue(name)
     for i in range(n):
