@@ -187,7 +187,8 @@ class CheckpointEngine(ABC):
         self._prep_pool = None
         self._prepped_for = None
         self._last_save_blocking = 0.0
-        self.last_restore_source = None  # "hbm" | "shm" after an in-place restore
+        self.last_restore_source = None  # "hbm" | "shm" | "storage" after an in-place restore
+        self.last_storage_load_stats: Dict[str, float] = {}
         self.speculation_misses = 0  # speculative snapshots redone after the state dict changed
         self.last_restore_breakdown: Dict[str, float] = {}  # host seconds per restore phase
         self._notify_agent_to_create_saver()
@@ -913,10 +914,30 @@ class FullCheckpointEngine(CheckpointEngine):
             if len(keys) == 1:
                 return sd[keys[0]]
             return sd
-        return self._load_from_storage(resume_path)
+        return self._load_from_storage(resume_path, target)
 
-    def _load_from_storage(self, resume_path=""):
-        read = lambda p: torch.load(p, map_location="cpu", weights_only=True)  # noqa: E731
+    def _load_from_storage(self, resume_path="", target=None):
+        """Persisted checkpoint -> state dict.  With ``target`` (live tensors)
+        the archive streams into them (O_DIRECT parallel reads + pipelined
+        H2D, ``storage_loader.py``) instead of ``torch.load`` + copy."""
+        inner = target.get(CheckpointConstant.MODEL_STATES_NAME, target) if isinstance(target, dict) else None
+
+        def read(p):
+            if inner is not None and os.environ.get("DWAMD_FAST_STORAGE_LOAD", "1") == "1":
+                from .storage_loader import load_archive_into
+
+                st = {}
+                try:
+                    out = load_archive_into(p, inner, direct=os.environ.get("DWAMD_STORAGE_DIRECT", "1") == "1",
+                                            stats=st)
+                    self.last_restore_source = "storage"
+                    self.last_storage_load_stats = st
+                    return out
+                except (KeyError, ValueError) as e:  # structure differs from the target: plain load
+                    logger.info(f"fast storage load not applicable ({e}); using torch.load")
+            self.last_restore_source = "storage(torch.load)"
+            return torch.load(p, map_location="cpu", weights_only=True)
+
         if resume_path:
             return self.storage.read_state_dict(resume_path, read)
         tracker = os.path.join(self.checkpoint_dir, CheckpointConstant.TRACER_FILE_NAME)

@@ -133,6 +133,46 @@ def test_save_to_storage_and_reload(tmp_path):
     ck2.close()
 
 
+def test_storage_restore_into_live_tensors(tmp_path):
+    """Memory gone (node replaced): the persisted archive streams straight
+    into the live tensors (O_DIRECT reads where the file system allows) and
+    equals what torch.load returns."""
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+    from dlrover_wuqiong_amd.flash_checkpoint.shm_handler import SharedMemoryHandler
+    from dlrover_wuqiong_amd.flash_checkpoint.storage_loader import drop_file_cache
+
+    d = tmp_path / "ck"
+    flat = torch.randn(1 << 21)
+    sd = {"model": {"w": flat[: 1 << 20].view(1024, 1024), "b": flat[1 << 20:]},
+          "optimizer": {"state": {0: {"exp_avg": torch.randn(300, dtype=torch.bfloat16)}},
+                        "param_groups": [{"lr": 0.5, "params": [0]}]},
+          "t": torch.randn(6, 4).t(), "step": 9}
+    ck = DdpCheckpointer(str(d))
+    assert ck.save_checkpoint(9, sd, storage_type=StorageType.DISK)
+    deadline = time.time() + 30
+    while time.time() < deadline and not ((d / "dlrover_latest.txt").exists()
+                                          and (d / "dlrover_latest.txt").read_text() == "9"):
+        time.sleep(0.05)
+    ck.close()
+    SharedMemoryHandler(0).unlink()
+    drop_file_cache(str(d / "9" / "rank_0.pt"))
+    target = {"model": {"w": torch.zeros(1024, 1024), "b": torch.zeros(1 << 20)},
+              "optimizer": {"state": {0: {"exp_avg": torch.zeros(300, dtype=torch.bfloat16)}},
+                            "param_groups": [{"lr": 0.0, "params": [0]}]},
+              "t": torch.zeros(4, 6), "step": 0}
+    ck2 = DdpCheckpointer(str(d))
+    out = ck2.load_checkpoint(target=target)
+    assert ck2.engine.last_restore_source == "storage"
+    assert out["model"]["w"] is target["model"]["w"]  # restored in place
+    assert torch.equal(target["model"]["w"], sd["model"]["w"]) and torch.equal(target["model"]["b"], sd["model"]["b"])
+    assert torch.equal(target["optimizer"]["state"][0]["exp_avg"], sd["optimizer"]["state"][0]["exp_avg"])
+    assert torch.equal(target["t"], sd["t"]) and out["step"] == 9
+    assert out["optimizer"]["param_groups"] == [{"lr": 0.5, "params": [0]}]
+    assert ck2.engine.last_storage_load_stats["bytes_read"] >= flat.numel() * 4
+    ck2.close()
+
+
 def _split_worker(rank, world, port, root, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
