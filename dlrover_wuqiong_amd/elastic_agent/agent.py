@@ -376,6 +376,8 @@ class ElasticTrainingAgent:
         env = dict(os.environ)
         env.update(self.config.extra_env)
         env.setdefault("OMP_NUM_THREADS", "1")
+        env["DWAMD_AGENT_CTL_DIR"] = self.ctl_dir
+        env["DWAMD_STANDBY_LOCAL_RANK"] = str(local_rank)
         if self.config.standby_mode == "deep":
             from .standby import STANDBY_ENV
 

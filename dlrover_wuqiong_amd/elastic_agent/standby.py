@@ -212,6 +212,10 @@ def main():
             return 3
         return 0
     _preload()
+    # import mode: torch + this package are imported; tell the agent (and
+    # anyone waiting on the control dir) this standby can take over now
+    _mark(os.environ.get("DWAMD_AGENT_CTL_DIR", ""), READY_PREFIX, os.environ.get("DWAMD_STANDBY_LOCAL_RANK", "0"),
+          f"{os.getpid()} {time.time()}\n")
     line = sys.stdin.readline()
     if not line.strip():
         return 0  # agent discarded the standby

@@ -465,6 +465,11 @@ class GpuCopier:
             f.result()
             self._futures[self._next_stage] = None
 
+    def rewind_stage(self, idx: int):
+        """The next snapshot reuses staging buffer ``idx`` (a discarded
+        speculative snapshot already took it; no flush was queued for it)."""
+        self._next_stage = idx % max(1, self._nbuf)
+
     def stage_busy_eta(self) -> float:
         """Seconds until the staging buffer the next snapshot uses is free:
         0 when idle; its flush's remaining bytes at the measured D2H rate when
@@ -591,6 +596,11 @@ class GpuCopier:
                 if on_snapshot is not None:
                     _check(_kern().dw_event_sync(ctypes.c_void_p(ev.cuda_event)), "snapshot sync")
                     on_snapshot()
+                    delay = float(os.environ.get("DWAMD_FAULT_FLUSH_DELAY_S", "0") or 0)
+                    if delay > 0:
+                        # fault injection: a slow PCIe flush, so a kill lands
+                        # after the snapshot and before the shm copy completes
+                        time.sleep(delay)
                 if prep is not None:
                     prep.wait(shm_payload_addr + lo, n)  # this range's prefault + registration
                 # registering here (flush thread), not in the training pause:
@@ -862,6 +872,19 @@ class GpuCopier:
         descs = build_descs([(base + off, dst, n) for off, dst, n in _merge_pieces(pieces_gpu)], self.device)
         launch_multi_copy(descs, cur)
         del full
+
+    def write_back(self, dev_src: int, host_dst: int, nbytes: int):
+        """D2H of ``nbytes`` from a device address into (shm) host memory,
+        synchronous (pinned in chunks like the flush)."""
+        if nbytes <= 0:
+            return
+        cur = torch.cuda.current_stream(self.device)
+        sp = ctypes.c_void_p(cur.cuda_stream)
+        pinned = self.pinned.ensure(host_dst, nbytes)
+        for a, c, p in (self.pinned.split(host_dst, nbytes) if pinned else [(host_dst, nbytes, False)]):
+            _check(_kern().dw_memcpy_async(ctypes.c_void_p(a), ctypes.c_void_p(dev_src + (a - host_dst)), c,
+                                           1 if p else 3, sp), "D2H write-back")
+        _check(_kern().dw_stream_sync(sp), "D2H write-back sync")
 
     def _pipelined_h2d(self, copies: List[Tuple[int, int, int]], stream, chunk: int = 512 << 20):
         """H2D of (host_src, dev_dst, nbytes) ranges.  Pinning (hipHostRegister,

@@ -169,6 +169,7 @@ class CheckpointEngine(ABC):
                              if self._local_rank == 0 else None)
         self._ctl_group = None
         self._gather_group = None
+        self._gather_on_host = False
         self._init_groups(comm_backend)
         self._copier = None
         self._layout: Optional[Layout] = None
@@ -210,14 +211,18 @@ class CheckpointEngine(ABC):
         # intra-node group for the replicated all-gather restore
         if self._replicated and self._local_world > 1:
             n_nodes = self._world // self._local_world
+            gb = comm_backend or backend
             if n_nodes <= 1:
                 self._gather_group = dist.group.WORLD if backend != "gloo" else None
             else:
                 for node in range(n_nodes):
                     ranks = list(range(node * self._local_world, (node + 1) * self._local_world))
-                    g = dist.new_group(ranks=ranks, backend=comm_backend or backend)
-                    if self._rank in ranks:
+                    g = dist.new_group(ranks=ranks, backend=gb)
+                    if self._rank in ranks and gb != "gloo":
                         self._gather_group = g
+            # a gloo world (CPU rehearsal, ranks sharing one GPU) has no device
+            # all-gather: slices meet in the node's shm instead
+            self._gather_on_host = self._gather_group is None
 
     def _ctl_barrier(self):
         if dist.is_available() and dist.is_initialized():
@@ -475,6 +480,10 @@ class CheckpointEngine(ABC):
         layout = self._plan(state_dict)
         if snap is not None and layout.extents is not spec.extents:
             self.speculation_misses += 1
+            if "idx" in stage:
+                # redo into the SAME staging buffer: the other one still holds
+                # the previous complete step (HBM-tier recovery stays possible)
+                copier.rewind_stage(stage["idx"])
             stage.clear()
             snap = None  # the speculative copy is stream-ordered before the real one below
         self._ensure_shm(layout.total_bytes)
@@ -645,8 +654,8 @@ class CheckpointEngine(ABC):
 
         if not hbm_tier.OWNED or os.environ.get("DWAMD_HBM_TIER", "1") != "1":
             return {}
-        if self._replicated and self._num_slices > 1 and self._gather_group is None:
-            return {}  # that restore path reads every slice from shm
+        if self._replicated and self._num_slices > 1 and self._gather_group is None and not self._gather_on_host:
+            return {}  # no way to combine the slices: every byte from shm
         h = self._shm_handler
         t0 = time.perf_counter()
         sub = self.hbm_scan_breakdown = {}
@@ -698,6 +707,16 @@ class CheckpointEngine(ABC):
         # a snapshot still in (standby-owned) HBM when the last worker died
         # counts too -- only for an in-place GPU restore
         hbm_only = self._hbm_only_steps() if (holds and target is not None) else {}
+        out = self._restore_step(h, holds, complete, hbm_only, target, lap, tb)
+        if out is None:
+            # the agreed step existed only in HBM and some rank's targets
+            # cannot take the D2D path: the newest step complete in shm
+            out = self._restore_step(h, holds, complete, {}, target, lap, tb)
+        return out if out is not None else (0, {})
+
+    def _restore_step(self, h, holds, complete, hbm_only, target, lap, tb):
+        """Agree on a step among the candidates and restore it.  None: the
+        step was HBM-only and the in-place restore was refused (collective)."""
         cands = dict(hbm_only)
         cands.update(complete)
         lap("hbm_scan")
@@ -709,6 +728,9 @@ class CheckpointEngine(ABC):
             return 0, {}
         lap("agree")
         if not holds:
+            # mirror the holders' collective votes in _restore_into
+            if target is not None and self._vote_retry(not check_all_rank_ready(self._ctl_group, True), False):
+                return None
             return 0, {}
         from_hbm_only = step not in complete
         logger.info(f"rank {self._rank}: restoring step {step} from memory slot {slot} "
@@ -721,6 +743,8 @@ class CheckpointEngine(ABC):
         if target is not None:
             sd = self._restore_into(tree, target, slot, step, require_hbm=from_hbm_only)
             lap("copy_enqueue")
+            if self._vote_retry(sd is None, from_hbm_only):
+                return None
             if sd is not None:
                 return step, sd
         if from_hbm_only:
@@ -729,6 +753,20 @@ class CheckpointEngine(ABC):
         if isinstance(sd, dict):
             sd.pop(DLROVER_CKPT_CONFIG_KEY, None)
         return step, sd
+
+    def _vote_retry(self, refused: bool, hbm_only: bool) -> bool:
+        """After a (collectively) refused in-place restore: retry with the
+        shm-complete steps only if the refused step was HBM-only on any rank.
+        ``refused`` is the same on every rank, so the vote is skipped by all
+        or taken by all."""
+        if not refused:
+            return False
+        v = 1 if hbm_only else 0
+        if dist.is_available() and dist.is_initialized():
+            t = torch.tensor([v], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self._ctl_group)
+            v = int(t)
+        return v == 1
 
     def _hbm_source(self, step: int, lo: int, hi: int) -> Optional[int]:
         """Device address of an HBM-tier buffer owned by this process that
@@ -753,10 +791,13 @@ class CheckpointEngine(ABC):
 
         pairs, ok = match_targets(tree, target)
         if require_hbm:
+            # the shm slot never received this step's GPU bytes: every tensor
+            # saved from the GPU must land in a contiguous GPU target (the
+            # D2D path from the HBM buffer); otherwise refuse on every rank
             total = self._shm_handler.payload_size
             s_lo, s_hi = split_ranges(total, self._num_slices)[self._slice_idx]
-            ok = ok and self._hbm_source(step, s_lo, s_hi) is not None and any(
-                t.is_cuda for _m, t in pairs)
+            ok = ok and self._hbm_source(step, s_lo, s_hi) is not None and all(
+                t.is_cuda and t.is_contiguous() for m, t in pairs if m.device == "cuda" and m.numel > 0)
         ok_all = check_all_rank_ready(self._ctl_group, ok)
         if not ok_all:
             return None
@@ -766,7 +807,9 @@ class CheckpointEngine(ABC):
         for m, t in pairs:
             if m.numel == 0:
                 continue
-            if t.is_cuda and t.is_contiguous():
+            # tensors saved from the CPU were written to shm synchronously at
+            # save time and are never in the HBM staging buffers: shm always
+            if t.is_cuda and t.is_contiguous() and m.device == "cuda":
                 gpu_pieces.append((m.offset, t.data_ptr(), m.numel * m.element_size))
             else:
                 src = torch.frombuffer(h.shared_memory.buf, dtype=m.dtype, count=m.numel,
@@ -789,7 +832,18 @@ class CheckpointEngine(ABC):
         elif self._num_slices <= 1:
             copier.restore(gpu_pieces, base, total, 0, total, hbm_src=hbm_src)
         else:
-            # replicated but no gather group (gloo world): every byte from shm
+            # replicated, no device all-gather (gloo world): slices meet in
+            # shm.  An HBM-only step is first written back slice by slice
+            # from each rank's HBM buffer (completing the shm slot), then
+            # every rank reads the whole payload from shm.
+            if require_hbm:
+                if hbm_src is not None:
+                    copier.write_back(hbm_src, base + s_lo, s_hi - s_lo)
+                    h.set_slice_step(slot, self._slice_idx, step)
+                self._ctl_barrier()
+                self.last_restore_source = "hbm->shm"
+            else:
+                self.last_restore_source = "shm"
             copier.restore(gpu_pieces, base, total, 0, total)
         it = iter([t for _, t in pairs])
 
@@ -928,8 +982,13 @@ class FullCheckpointEngine(CheckpointEngine):
 
                 st = {}
                 try:
+                    # replicated state, one file per node: each local rank
+                    # reads 1/L of it and the slices meet over xGMI
+                    sliced = self._replicated and self._num_slices > 1 and self._gather_group is not None
                     out = load_archive_into(p, inner, direct=os.environ.get("DWAMD_STORAGE_DIRECT", "1") == "1",
-                                            stats=st)
+                                            stats=st, slice_idx=self._slice_idx if sliced else 0,
+                                            num_slices=self._num_slices if sliced else 1,
+                                            gather_group=self._gather_group if sliced else None)
                     self.last_restore_source = "storage"
                     self.last_storage_load_stats = st
                     return out

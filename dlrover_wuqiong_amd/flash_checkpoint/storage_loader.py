@@ -222,12 +222,52 @@ class _Reader:
             self.buffered_bytes += nbytes
 
 
+def _regions(pairs, arc):
+    """Merge (lazy, target) pairs into regions that are contiguous both in the
+    file and in one destination storage (e.g. every parameter view of a flat
+    buffer -> one region).  Returns [(file_off, nbytes, dst uint8 tensor)]
+    sorted by file offset, plus the non-contiguous leftovers."""
+    items, slow = [], []
+    for lz, t in pairs:
+        if lz.numel == 0:
+            continue
+        if not lz.contiguous() or not t.is_contiguous():
+            slow.append((lz, t))
+            continue
+        lo, n = arc.file_range(lz)
+        st = t.untyped_storage()
+        items.append((lo, n, st, t.storage_offset() * t.element_size()))
+    items.sort(key=lambda x: x[0])
+    regions = []
+    for lo, n, st, doff in items:
+        if regions:
+            plo, pn, pst, pdoff = regions[-1]
+            if pst.data_ptr() == st.data_ptr() and lo == plo + pn and doff == pdoff + pn:
+                regions[-1] = (plo, pn + n, pst, pdoff)
+                continue
+            if pst.data_ptr() == st.data_ptr() and lo >= plo and lo + n <= plo + pn and doff - pdoff == lo - plo:
+                continue  # a view inside the region already covered
+        regions.append((lo, n, st, doff))
+    out = []
+    for lo, n, st, doff in regions:
+        dst = torch.empty(0, dtype=torch.uint8, device=st.device).set_(st, doff, (n,))
+        out.append((lo, n, dst))
+    return out, slow
+
+
 def load_archive_into(path: str, target: Any = None, chunk_bytes: int = 256 << 20, direct: bool = True,
-                      drop_cache: bool = False, threads: int = 16, stats: Optional[dict] = None) -> Any:
+                      drop_cache: bool = False, threads: int = 16, stats: Optional[dict] = None,
+                      slice_idx: int = 0, num_slices: int = 1, gather_group=None,
+                      min_gather_bytes: int = 64 << 20) -> Any:
     """Load a ``torch.save`` archive.  With ``target`` (the saved structure
     with live tensors at tensor leaves) tensors are restored in place --
     H2D for GPU targets -- and the target-backed tree is returned; without,
-    CPU tensors are returned (like ``torch.load(weights_only=True)``)."""
+    CPU tensors are returned (like ``torch.load(weights_only=True)``).
+
+    ``num_slices > 1`` with a device ``gather_group`` (replicated state, one
+    file for the node): every large region is read 1/num_slices per rank and
+    completed with an all-gather over the group (RCCL over xGMI), so the node
+    reads the file once instead of once per rank."""
     t0 = time.perf_counter()
     arc = TorchArchive(path)
     t_parse = time.perf_counter()
@@ -249,16 +289,22 @@ def load_archive_into(path: str, target: Any = None, chunk_bytes: int = 256 << 2
         return out
     pairs: List[Tuple[LazyTensor, torch.Tensor]] = []
     result = _pair(arc.tree, target, pairs)
-    pieces = []  # (file_off, nbytes, dst byte tensor or (tensor, lazy) for the slow path)
-    slow = []
-    for lz, t in pairs:
-        if lz.numel == 0:
-            continue
-        if not lz.contiguous() or not t.is_contiguous():
-            slow.append((lz, t))
-            continue
-        lo, n = arc.file_range(lz)
-        dst = t.detach().reshape(-1).view(torch.uint8)
+    regions, slow = _regions(pairs, arc)
+    gathers = []  # (region dst, per-rank bytes) all-gathered after the reads
+    mine = []
+    for lo, n, dst in regions:
+        if num_slices > 1 and gather_group is not None and dst.is_cuda and n >= min_gather_bytes:
+            per = n // (num_slices * _ALIGN) * _ALIGN
+            body = per * num_slices
+            a0 = slice_idx * per
+            mine.append((lo + a0, per, dst[a0: a0 + per]))
+            if body < n:
+                mine.append((lo + body, n - body, dst[body:]))  # short tail: every rank reads it
+            gathers.append((dst[:body], per))
+        else:
+            mine.append((lo, n, dst))
+    pieces = []
+    for lo, n, dst in mine:
         o = 0
         while o < n:  # split so every piece fits one bounce buffer
             c = min(chunk_bytes, n - o)
@@ -320,6 +366,17 @@ def load_archive_into(path: str, target: Any = None, chunk_bytes: int = 256 << 2
         del esz
     if stream is not None:
         stream.synchronize()
+    if gathers:
+        import torch.distributed as dist
+
+        t_g = time.perf_counter()
+        for full, per in gathers:
+            a0 = slice_idx * per
+            dist.all_gather_into_tensor(full, full[a0: a0 + per].clone(), group=gather_group)
+        torch.cuda.current_stream(gathers[0][0].device).synchronize()
+        if stats is not None:
+            stats["gather_s"] = round(time.perf_counter() - t_g, 4)
+            stats["gather_bytes"] = sum(f.numel() for f, _ in gathers)
     _fill_stats(stats, arc, reader, t0, t_parse, time.perf_counter())
     return result
 

@@ -14,7 +14,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_bench_two_ranks_real_kill(tmp_path):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--model", "gpt2-tiny", "--micro-batch",
-           "2", "--seq", "64", "--steps", "8", "--warmup", "2", "--fault-window", "16", "--ckpt-dir", str(tmp_path / "ckpt"), "--timeout",
+           "2", "--seq", "64", "--steps", "8", "--warmup", "2", "--fault-window", "16", "--import-window", "12", "--ckpt-dir", str(tmp_path / "ckpt"), "--timeout",
            "240"]
     r = subprocess.run(cmd, env=env, cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                        timeout=300)
@@ -29,3 +29,15 @@ def test_bench_two_ranks_real_kill(tmp_path):
     assert 0 < res["goodput_pct"] < 100
     assert res["lost_steps"] >= 0 and res["recover_sec"] > 0
     assert res["persist_sec"] is not None
+    # every timed save produced a checkpoint; skipped saves are reported
+    assert res["timed_saves_ok"] is True and res["skipped_saves_timed"] == 0
+    assert res["first_save_sec"] is not None and res["skipped_saves_fault_window"] >= 0
+    assert "goodput_pct_1fail_per_hour_modelled" in res and "goodput_pct_1fail_per_hour" not in res
+    # node-replacement restore from the persisted file, verified against memory
+    assert res["load_sec_storage"] > 0 and res["load_storage_verified"] is True
+    # the failure again under the default --standby-mode import: cold
+    # replacement process, restore from host shm (reference semantics)
+    imp = res["import_mode"]
+    assert imp["standby_mode"] == "import" and imp["restarts"] == 1 and imp["load_verified_after_restart"]
+    assert res["load_sec_shm"] == imp["load_sec"] and res["goodput_pct_import"] == imp["goodput_pct"]
+    assert res["recover_sec_import"] > 0 and imp["recovery_breakdown_s"]["process_to_model_built"] is not None

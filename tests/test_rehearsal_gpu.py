@@ -1,0 +1,45 @@
+"""N>1 fault path rehearsed on ONE GPU (bench.py --rehearse-shared-device):
+2 ranks share cuda:0 over gloo (RCCL refuses two ranks per device) with
+2 deep standbys, per-slice HBM-tier staging, a SIGKILL of rank 1 mid-step
+while the last checkpoint's shm flush is still running (fault injection),
+agent restart, and a restore of the HBM-only step whose slices meet in shm
+-- then the same failure under the default import standbys.  Never an
+N-GPU measurement: the JSON says ``rehearsal: true``."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.timeout(400)
+def test_gpu_rehearse_two_ranks_shared_device(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    cmd = [sys.executable, "-u", os.path.join(REPO, "bench.py"), "--gpus", "2", "--rehearse-shared-device",
+           "--model", "gpt2", "--micro-batch", "2", "--seq", "256", "--steps", "8", "--warmup", "3",
+           "--fault-window", "16", "--import-window", "12", "--inject-slow-flush", "3",
+           "--ckpt-dir", str(tmp_path / "ckpt"), "--timeout", "300"]
+    r = subprocess.run(cmd, env=env, cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=380)
+    sys.stderr.write(r.stderr[-6000:])
+    assert r.returncode == 0, r.stderr[-20000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    print(json.dumps(res))
+    assert res["rehearsal"] is True and res["n_gpus"] == 1 and res["rccl_world"] == 2
+    assert res["backend"] == "gloo" and "rehearsal" in res["config"]["parallelism"]
+    assert res["load_verified"] and res["replicas_identical"] and res["timed_saves_ok"]
+    assert res["restarts"] == 1 and res["load_verified_after_restart"]
+    # the killed step's checkpoint existed only in the standbys' HBM: each
+    # rank wrote its slice back to shm, then both restored the whole payload
+    assert res["restore_source"] == "hbm->shm", res["restore_source"]
+    assert res["load_storage_verified"] is True
+    imp = res["import_mode"]
+    assert imp["restarts"] == 1 and imp["load_verified_after_restart"]
