@@ -101,6 +101,14 @@ OPTIONAL = {
     "dw_attn_fwd_varlen": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, i32, f32, vp]),
     "dw_attn_bwd_varlen": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32,
                                  i32, vp, i32, f32, vp]),
+    # extended masks (window / GLM prefix / bias / ALiBi / dropout): last vp = AttnExtArgs*
+    "dw_attn_fwd_ext": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, f32, vp, vp]),
+    "dw_attn_bwd_ext": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, f32, vp, vp]),
+    "dw_attn_fwd_varlen_ext": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, f32, vp,
+                                     vp]),
+    "dw_attn_bwd_varlen_ext": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32,
+                                     i32, i32, vp, i32, f32, vp, vp]),
+    "dw_attn_dropout_mask": (i32, [vp, i32, i32, i32, f32, u64, u64, vp]),
 }
 
 

@@ -6,10 +6,12 @@ MFMA flash-attention kernels.
 model (and every sub-config) to it, so LlamaAttention / MistralAttention /
 Qwen2Attention ... call ``ops.attention.flash_attn_func`` (BSHD, GQA, causal,
 head_dim 64/128) instead of SDPA; padded batches (left or right padding)
-run the varlen kernels on the unpadded tokens.  Cases the kernels do not
-cover -- dropout, head_dim not in {64, 128}, sliding windows, KV-cache
-decoding (q_len != k_len), non-bf16 or CPU tensors -- fall back to
-transformers' own SDPA path for that call.
+run the varlen kernels on the unpadded tokens; attention dropout and
+sliding windows (Mistral / Mixtral / Qwen2 ``sliding_window``: a key is
+visible iff q - W < k <= q) run on the same kernels.  Cases the kernels do
+not cover -- head_dim not in {64, 128}, KV-cache decoding (q_len != k_len),
+non-bf16 or CPU tensors -- fall back to transformers' own SDPA path for that
+call.
 
 ``auto_accelerate``'s ``module_replace`` applies it to any
 ``PreTrainedModel`` together with the fused norm replacement.
@@ -40,8 +42,10 @@ def dwamd_attention_forward(module, query: torch.Tensor, key: torch.Tensor, valu
     causal = is_causal if is_causal is not None else getattr(module, "is_causal", True)
     D = query.shape[-1]
     q_len, k_len = query.shape[2], key.shape[2]
-    usable = (_hip.use_hip(query) and query.dtype == torch.bfloat16 and D in (64, 128) and dropout == 0.0
-              and q_len == k_len and causal and kwargs.get("sliding_window") is None)
+    usable = (_hip.use_hip(query) and query.dtype == torch.bfloat16 and D in (64, 128)
+              and q_len == k_len and causal)
+    sw = kwargs.get("sliding_window")
+    window = (int(sw) - 1, 0) if sw is not None and k_len > int(sw) else (-1, -1)
     key_valid = None
     if usable and attention_mask is not None:
         if attention_mask.dim() != 4 or attention_mask.shape[-1] != k_len:
@@ -61,8 +65,9 @@ def dwamd_attention_forward(module, query: torch.Tensor, key: torch.Tensor, valu
     if key_valid is not None:
         from ..ops.attention import flash_attn_padded_func
 
-        return flash_attn_padded_func(q, k, v, key_valid, causal=True, softmax_scale=scaling), None
-    return flash_attn_func(q, k, v, causal=True, softmax_scale=scaling), None
+        return flash_attn_padded_func(q, k, v, key_valid, causal=True, softmax_scale=scaling, dropout_p=dropout,
+                                      window_size=window), None
+    return flash_attn_func(q, k, v, dropout_p=dropout, causal=True, softmax_scale=scaling, window_size=window), None
 
 
 def register() -> str:

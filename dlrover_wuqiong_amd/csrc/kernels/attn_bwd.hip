@@ -116,13 +116,13 @@ struct DkvCfg {
   static constexpr int VIMG = BKB * D * 2;            // the block's V rows (LDS-resident)
 };
 
-template <int D, bool CAUSAL, bool PARTIAL>
+template <int D, bool CAUSAL, bool PARTIAL, bool EXT>
 __global__ void __launch_bounds__(64 * DkvCfg<D>::WAVES, 2)
 attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
                      const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
                      bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, float* __restrict__ dKp,
                      float* __restrict__ dVp, int S, int H, int HKV, float scale, float scale_log2,
-                     AttnStrides st, AttnVarlen vl) {
+                     AttnStrides st, AttnVarlen vl, AttnExt ex) {
   using C = DkvCfg<D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -170,8 +170,21 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
     }
 
   // first query that sees key kb0: key <= q + co
-  const int q_lo = CAUSAL ? (max(0, kb0 - co) / C::BQT) * C::BQT : 0;
-  const int n_it = max(0, (SQ - q_lo + C::BQT - 1) / C::BQT);
+  const int pre = EXT && ex.prefix ? min(SK, ex.prefix[b]) : 0;
+  int q_lo = CAUSAL ? (max(0, kb0 - co) / C::BQT) * C::BQT : 0;
+  int q_end = SQ;  // EXT: queries past the last window that reaches these keys see none of them
+  if (EXT) {
+    if (kb0 < pre) {
+      q_lo = 0;  // prefix keys in the block: every query sees them
+    } else {
+      // query q sees key k iff -win_l <= k - (q + co) <= win_r
+      if (ex.win_r >= 0) q_lo = (max(0, kb0 - co - ex.win_r) / C::BQT) * C::BQT;
+      if (ex.win_l >= 0) q_end = max(0, min(SQ, kb0 + C::BKB - 1 - co + ex.win_l + 1));
+    }
+  }
+  const int n_it = max(0, (q_end - q_lo + C::BQT - 1) / C::BQT);
+  const long long bh = vl.cu_q ? (long long)h : (long long)b * H + h;  // dropout hash row
+  const float al2 = EXT ? ext_alibi2(ex, b, h) : 0.f;
   u32x4 q_st[C::VPT], do_st[C::VPT];
   float lse_st = INFINITY, del_st = 0.f;
   auto issue = [&](int it) {
@@ -191,7 +204,9 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
     }
     if (tid < C::BQT) {
       const int q = q0 + tid;
-      lse_st = q < SQ ? lse_b[q] * 1.4426950408889634f : INFINITY;
+      const float l = q < SQ ? lse_b[q] : -INFINITY;
+      // a row that saw no key (lse = -inf) contributes nothing: p = 2^-inf
+      lse_st = l > -INFINITY ? l * 1.4426950408889634f : INFINITY;
       del_st = q < SQ ? del_b[q] : 0.f;
     }
   };
@@ -224,8 +239,8 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
     const char* dl = ql + C::TILE;
     const float* stl = (const float*)(dl + C::TILE);
     // all queries of this tile precede this wave's keys: nothing to add
-    if (!CAUSAL || q0 + C::BQT - 1 + co >= kw0) {
-      const bool need_mask = (q0 + C::BQT > SQ) || (kw0 + 32 > SK) || (CAUSAL && kw0 + 31 > q0 + co);
+    if (!CAUSAL || q0 + C::BQT - 1 + co >= kw0 || (EXT && kw0 < pre)) {
+      const bool need_mask = EXT || (q0 + C::BQT > SQ) || (kw0 + 32 > SK) || (CAUSAL && kw0 + 31 > q0 + co);
 #pragma unroll
       for (int qs = 0; qs < C::BQT / 32; ++qs) {
         // S = Q K^T, dP = dO V^T for 32 queries: key on the lane, query in the registers
@@ -257,6 +272,27 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int i = 4 * g + j;
+            if (EXT) {
+              const int q = q0 + qi + j;
+              const bool vis = (q < SQ) && ext_visible(ex, CAUSAL, q, key, co, SK, pre);
+              float add = (vis && ex.bias)
+                  ? ex.bias[(int64_t)b * ex.bias_bs + (int64_t)h * ex.bias_hs + (int64_t)q * ex.bias_qs + key] *
+                        1.4426950408889634f
+                  : 0.f;
+              add -= al2 * fabsf((float)(key - q - co));
+              const float p = vis ? __builtin_amdgcn_exp2f(s[i] + add) : 0.f;
+              if (ex.dropout) {
+                // dV takes the dropped probabilities; dS = P (Z dP / (1-p) - delta)
+                const float del = stl[C::BQT + qi + j];
+                const bool kp = attn_keep(ex, bh, (long long)sr.q_off + q, (long long)sr.k_off + key);
+                s[i] = kp ? p * ex.inv_keep : 0.f;
+                dp[i] = p * (kp ? (dp[i] + del) * ex.inv_keep - del : -del);
+              } else {
+                s[i] = p;
+                dp[i] = p * dp[i];
+              }
+              continue;
+            }
             float p = __builtin_amdgcn_exp2f(s[i]);
             if (need_mask) {
               const int q = q0 + qi + j;
@@ -384,12 +420,12 @@ struct DqCfg {
   static constexpr int VPT = BK * NCH / (64 * WAVES);
 };
 
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool EXT>
 __global__ void __launch_bounds__(64 * DqCfg<D>::WAVES, 1)
 attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
                    const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
                    bf16_t* __restrict__ dQ, int S, int H, int HKV, float scale, float scale_log2, AttnStrides st,
-                   AttnVarlen vl) {
+                   AttnVarlen vl, AttnExt ex) {
   using C = DqCfg<D>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -424,7 +460,8 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
     }
   }
   const int64_t so = sr.lse_base + q;
-  const float lse2 = q < SQ ? LSE[so] * 1.4426950408889634f : INFINITY;
+  const float lse_v = q < SQ ? LSE[so] : -INFINITY;
+  const float lse2 = lse_v > -INFINITY ? lse_v * 1.4426950408889634f : INFINITY;  // no visible key: p = 0
   const float dl = q < SQ ? DELTA[so] : 0.f;
 
   f32x16 acc[C::DT];
@@ -434,10 +471,23 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
     for (int i = 0; i < 16; ++i) acc[dt][i] = 0.f;
 
   int n_tiles = (SK + C::BK - 1) / C::BK;
-  if (CAUSAL) {
-    const int last = min(SK - 1, min(SQ - 1, q_blk0 + C::BQ - 1) + co);
+  int t_begin = 0;
+  const int pre = EXT && ex.prefix ? min(SK, ex.prefix[b]) : 0;
+  if (CAUSAL || EXT) {
+    const int q_last = min(SQ - 1, q_blk0 + C::BQ - 1);
+    int last = SK - 1;
+    if (CAUSAL) last = min(last, q_last + co);
+    if (EXT && ex.win_r >= 0) last = min(last, q_last + co + ex.win_r);
+    if (EXT && pre > 0) last = max(last, pre - 1);
     n_tiles = last < 0 ? 0 : min(n_tiles, last / C::BK + 1);
+    if (EXT && ex.win_l >= 0 && pre == 0) t_begin = min(n_tiles, max(0, q_blk0 + co - ex.win_l) / C::BK);
   }
+  const int n_run = n_tiles - t_begin;
+  const long long bh = vl.cu_q ? (long long)h : (long long)b * H + h;
+  const float al2 = EXT ? ext_alibi2(ex, b, h) : 0.f;
+  const float* brow = nullptr;
+  if (EXT && ex.bias && q < SQ)
+    brow = ex.bias + (int64_t)b * ex.bias_bs + (int64_t)h * ex.bias_hs + (int64_t)q * ex.bias_qs;
 
   u32x4 kst[C::VPT], vst[C::VPT];
   auto issue_load = [&](int t) {
@@ -466,17 +516,24 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
       *(u32x4*)(vl + img_off<D>(row, c)) = vst[i];
     }
   };
-  issue_load(0);
+  issue_load(t_begin);
   write_lds(0);
-  if (n_tiles > 1) issue_load(1);
+  if (n_run > 1) issue_load(t_begin + 1);
   __syncthreads();
   const int g4 = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
 
-  for (int t = 0; t < n_tiles; ++t) {
+  for (int tt = 0; tt < n_run; ++tt) {
+    const int t = t_begin + tt;
     const int k0 = t * C::BK;
-    const char* kl = smem + (t & 1) * 2 * C::TILE;
+    const char* kl = smem + (tt & 1) * 2 * C::TILE;
     const char* vl = kl + C::TILE;
-    if (!CAUSAL || k0 <= q0 + 31 + co) {
+    bool active = !CAUSAL || k0 <= q0 + 31 + co;
+    if (EXT) {
+      if (k0 < pre) active = true;
+      if (ex.win_r >= 0) active = active && (k0 <= q0 + 31 + co + ex.win_r);
+      if (ex.win_l >= 0 && k0 >= pre) active = active && (k0 + C::BK - 1 >= q0 + co - ex.win_l);
+    }
+    if (active) {
       const bool need_mask = (k0 + C::BK > SK) || (CAUSAL && (k0 + C::BK - 1 > q0 + co));
       const int lim = CAUSAL ? min(SK, q + co + 1) : SK;  // keys < lim are visible to this lane's query
       // one 32-key subtile at a time keeps S^T / dP^T at 32 registers
@@ -499,6 +556,18 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
+          if (EXT) {
+            const int key = k0 + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            const bool vis = (q < SQ) && ext_visible(ex, CAUSAL, q, key, co, SK, pre);
+            float add = (vis && brow) ? brow[key] * 1.4426950408889634f : 0.f;
+            add -= al2 * fabsf((float)(key - q - co));
+            const float p = vis ? __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], scale_log2, add - lse2)) : 0.f;
+            float dpe = dp[i];
+            if (ex.dropout)
+              dpe = attn_keep(ex, bh, (long long)sr.q_off + q, (long long)sr.k_off + key) ? dpe * ex.inv_keep : 0.f;
+            s[i] = p * (dpe - dl);
+            continue;
+          }
           float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], scale_log2, -lse2));
           if (need_mask) {
             const int key = k0 + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hh;
@@ -525,9 +594,9 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
         }
       }
     }
-    if (t + 1 < n_tiles) {
-      write_lds((t + 1) & 1);
-      if (t + 2 < n_tiles) issue_load(t + 2);
+    if (tt + 1 < n_run) {
+      write_lds((tt + 1) & 1);
+      if (tt + 2 < n_run) issue_load(t + 2);
     }
     __syncthreads();
   }
@@ -584,7 +653,10 @@ static bool bwd_concurrent() {
 template <int D>
 static void launch_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const void* lse,
                        char* ws, void* dq, void* dk, void* dv, int B, int Sq, int Sk, int H, int HKV, int causal,
-                       float softmax_scale, const AttnStrides& st, const AttnVarlen& vl, hipStream_t s) {
+                       float softmax_scale, const AttnStrides& st, const AttnVarlen& vl, hipStream_t s,
+                       const AttnExt* ext = nullptr) {
+  const AttnExt none = {};
+  const AttnExt& ex = ext ? *ext : none;
   // workspace layout (dw_attn_bwd_workspace with S = max(Sq, Sk)): delta, then
   // the GQA partials; packed batches use [H, total_q] / [total_k, H, D] inside
   const int Smax = Sq > Sk ? Sq : Sk;
@@ -607,14 +679,20 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
   float* pv = pk + (int64_t)B * Smax * H * D;
   dim3 gk((unsigned)((Sk + KC::BKB - 1) / KC::BKB * H * B));  // 1-D: xcd_block()
   const int lk = 2 * KC::BUF + KC::VIMG;
-#define DKDV(CA, PA)                                                                                          \
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CA, PA>), gk, dim3(64 * KC::WAVES), lk, s, (const bf16_t*)q,   \
-                     (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta,      \
-                     (bf16_t*)dk, (bf16_t*)dv, pk, pv, Sk, H, HKV, softmax_scale, scale_log2, st, vl)
-  if (causal) {
-    if (partial) DKDV(true, true); else DKDV(true, false);
+#define DKDV(CA, PA, EX)                                                                                      \
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CA, PA, EX>), gk, dim3(64 * KC::WAVES), lk, s, (const bf16_t*)q, \
+                     (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta,        \
+                     (bf16_t*)dk, (bf16_t*)dv, pk, pv, Sk, H, HKV, softmax_scale, scale_log2, st, vl, ex)
+  if (ext) {
+    if (causal) {
+      if (partial) DKDV(true, true, true); else DKDV(true, false, true);
+    } else {
+      if (partial) DKDV(false, true, true); else DKDV(false, false, true);
+    }
+  } else if (causal) {
+    if (partial) DKDV(true, true, false); else DKDV(true, false, false);
   } else {
-    if (partial) DKDV(false, true); else DKDV(false, false);
+    if (partial) DKDV(false, true, false); else DKDV(false, false, false);
   }
 #undef DKDV
   if (partial) {
@@ -629,14 +707,18 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
   using DC = DqCfg<D>;
   dim3 gq((unsigned)((Sq + DC::BQ - 1) / DC::BQ * H * B));  // 1-D: xcd_block()
   const int lq = 4 * DC::TILE;
-  if (causal)
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, true>), gq, dim3(64 * DC::WAVES), lq, sq, (const bf16_t*)q,
-                       (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta,
-                       (bf16_t*)dq, Sq, H, HKV, softmax_scale, scale_log2, st, vl);
-  else
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, false>), gq, dim3(64 * DC::WAVES), lq, sq, (const bf16_t*)q,
-                       (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta,
-                       (bf16_t*)dq, Sq, H, HKV, softmax_scale, scale_log2, st, vl);
+#define DQ(CA, EX)                                                                                            \
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CA, EX>), gq, dim3(64 * DC::WAVES), lq, sq, (const bf16_t*)q,      \
+                     (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta,        \
+                     (bf16_t*)dq, Sq, H, HKV, softmax_scale, scale_log2, st, vl, ex)
+  if (ext) {
+    if (causal) DQ(true, true); else DQ(false, true);
+  } else if (causal) {
+    DQ(true, false);
+  } else {
+    DQ(false, false);
+  }
+#undef DQ
   if (sq != s) {  // join: the caller's stream continues after both
     hipEventRecord(side->join, sq);
     hipStreamWaitEvent(s, side->join, 0);
@@ -695,4 +777,50 @@ extern "C" int dw_attn_bwd(const void* q, const void* k, const void* v, const vo
   const long long st[16] = {qs, qr, ks, kr, ks, kr, qs, qr, qs, qr, qs, qr, ks, kr, ks, kr};
   return dw_attn_bwd_strided(q, k, v, o, dout, lse, dq, dk, dv, workspace, B, S, H, HKV, D, st, causal,
                              softmax_scale, flags, stream);
+}
+
+// Extended masks (attn_common.h AttnExtArgs); dense layout as dw_attn_bwd_strided.
+extern "C" int dw_attn_bwd_ext(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                               const void* lse, void* dq, void* dk, void* dv, void* workspace, int B, int S, int H,
+                               int HKV, int D, const long long* strides, int causal, float softmax_scale,
+                               const AttnExtArgs* args, void* stream) {
+  if (H % HKV != 0 || (D != 64 && D != 128)) return (int)hipErrorInvalidValue;
+  AttnStrides st;
+  long long* f = &st.q_bs;
+  for (int i = 0; i < 16; ++i) f[i] = strides[i];
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  const AttnVarlen vl = {nullptr, nullptr, 0, 0};
+  const AttnExt ex = make_ext(args, S, S);
+  const AttnExt* ep = ext_active(args) ? &ex : nullptr;
+  if (D == 128)
+    launch_bwd<128>(q, k, v, o, dout, lse, ws, dq, dk, dv, B, S, S, H, HKV, causal, softmax_scale, st, vl, s, ep);
+  else
+    launch_bwd<64>(q, k, v, o, dout, lse, ws, dq, dk, dv, B, S, S, H, HKV, causal, softmax_scale, st, vl, s, ep);
+  DW_LAUNCH_RET;
+}
+
+extern "C" int dw_attn_bwd_varlen_ext(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                                      const void* lse, void* dq, void* dk, void* dv, void* workspace, const void* cu_q,
+                                      const void* cu_k, int B, int max_seqlen_q, int max_seqlen_k, int total_q,
+                                      int total_k, int H, int HKV, int D, const long long* row_strides, int causal,
+                                      float softmax_scale, const AttnExtArgs* args, void* stream) {
+  if (H % HKV != 0 || (D != 64 && D != 128) || !cu_q || !cu_k ||
+      (args && (args->bias || args->prefix || (args->alibi && args->alibi_bs))))
+    return (int)hipErrorInvalidValue;
+  AttnStrides st = {};
+  st.q_rs = row_strides[0]; st.k_rs = row_strides[1]; st.v_rs = row_strides[2]; st.o_rs = row_strides[3];
+  st.do_rs = row_strides[4]; st.dq_rs = row_strides[5]; st.dk_rs = row_strides[6]; st.dv_rs = row_strides[7];
+  const AttnVarlen vl = {(const int*)cu_q, (const int*)cu_k, total_q, total_k};
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  const AttnExt ex = make_ext(args, total_q, total_k);
+  const AttnExt* ep = ext_active(args) ? &ex : nullptr;
+  if (D == 128)
+    launch_bwd<128>(q, k, v, o, dout, lse, ws, dq, dk, dv, B, max_seqlen_q, max_seqlen_k, H, HKV, causal,
+                    softmax_scale, st, vl, s, ep);
+  else
+    launch_bwd<64>(q, k, v, o, dout, lse, ws, dq, dk, dv, B, max_seqlen_q, max_seqlen_k, H, HKV, causal,
+                   softmax_scale, st, vl, s, ep);
+  DW_LAUNCH_RET;
 }

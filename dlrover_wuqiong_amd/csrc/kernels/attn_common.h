@@ -82,3 +82,107 @@ __device__ __forceinline__ u32x4 join_tr(const V& a, const V& b) {
 __device__ __forceinline__ unsigned int pack_s16(short a, short b) {
   return (unsigned int)(unsigned short)a | ((unsigned int)(unsigned short)b << 16);
 }
+
+// ---------------------------------------------------------------------------
+// Extended masking for the attention kernels (instantiated only when EXT is a
+// template parameter of true; the plain causal / full kernels never see it):
+//   * sliding window: key visible iff -win_l <= key - (q + co) <= win_r
+//     (flash-attn window_size; < 0 = unbounded on that side);
+//   * GLM prefix ("break point"): keys < prefix[b] are visible to every query
+//     of batch b on top of the causal mask (ATorch fa2_with_glm_mask);
+//   * additive bias / mask [B|1, H|1, Sq|1, Sk] fp32 (strides 0 broadcast),
+//     added to the scaled scores (-inf = masked); no gradient;
+//   * ALiBi: -slope[b, h] * |key - (q + co)| added to the scaled scores
+//     (flash-attn alibi_slopes [H] or [B, H], fp32);
+//   * dropout on the probabilities used for O (LSE over the undropped ones,
+//     FA2 semantics) with a counter-based hash of (seed, head, query, key):
+//     stateless, so the backward regenerates the identical mask.
+// Host ABI (ctypes, ops/attention.py): AttnExtArgs.
+struct AttnExtArgs {
+  long long bias_bs, bias_hs, bias_qs;
+  const float* bias;
+  const int* prefix;
+  unsigned long long seed, offset;
+  int win_l, win_r;
+  float p_drop;
+  int pad_;
+  const float* alibi;
+  long long alibi_bs;  // 0: slopes [H] shared by the batch
+};
+
+struct AttnExt {
+  const float* bias;
+  long long bias_bs, bias_hs, bias_qs;
+  const int* prefix;
+  const float* alibi;
+  long long alibi_bs;
+  unsigned long long seed, offset;
+  long long tq, tk;  // rows of the query / key index space of the hash
+  unsigned int drop_thresh;  // keep iff hash >= thresh
+  float inv_keep;            // 1 / (1 - p)
+  int win_l, win_r;
+  bool dropout;
+};
+
+static inline AttnExt make_ext(const AttnExtArgs* a, long long tq, long long tk) {
+  AttnExt e = {};
+  e.win_l = e.win_r = -1;
+  e.inv_keep = 1.f;
+  if (!a) return e;
+  e.bias = a->bias;
+  e.bias_bs = a->bias_bs;
+  e.bias_hs = a->bias_hs;
+  e.bias_qs = a->bias_qs;
+  e.prefix = a->prefix;
+  e.alibi = a->alibi;
+  e.alibi_bs = a->alibi_bs;
+  e.seed = a->seed;
+  e.offset = a->offset;
+  e.tq = tq;
+  e.tk = tk;
+  e.win_l = a->win_l;
+  e.win_r = a->win_r;
+  e.dropout = a->p_drop > 0.f;
+  if (e.dropout) {
+    const double t = (double)a->p_drop * 4294967296.0;
+    e.drop_thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (unsigned int)t;
+    e.inv_keep = 1.f / (1.f - a->p_drop);
+  }
+  return e;
+}
+
+static inline bool ext_active(const AttnExtArgs* a) {
+  return a && (a->bias || a->prefix || a->alibi || a->win_l >= 0 || a->win_r >= 0 || a->p_drop > 0.f);
+}
+
+// splitmix64 finalizer over (seed, element index): the keep decision of one
+// attention probability.  Identical in the forward, both backward kernels and
+// dw_attn_dropout_mask (the test / reference mask).
+__device__ __forceinline__ unsigned int attn_hash(unsigned long long seed, unsigned long long idx) {
+  unsigned long long z = seed + (idx + 1ull) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return (unsigned int)((z ^ (z >> 31)) >> 32);
+}
+
+// element index of (head row bh, global query qg, global key kg)
+__device__ __forceinline__ bool attn_keep(const AttnExt& e, long long bh, long long qg, long long kg) {
+  const unsigned long long idx = ((unsigned long long)bh * e.tq + qg) * e.tk + kg + e.offset;
+  return attn_hash(e.seed, idx) >= e.drop_thresh;
+}
+
+// key visibility beyond the plain causal / length checks
+__device__ __forceinline__ bool ext_visible(const AttnExt& e, bool causal, int q, int key, int co, int SK, int pre) {
+  if (key >= SK) return false;
+  if (key < pre) return true;  // GLM prefix: bidirectional
+  const int d = key - (q + co);
+  bool v = !causal || d <= 0;
+  if (e.win_r >= 0) v = v && d <= e.win_r;
+  if (e.win_l >= 0) v = v && d >= -e.win_l;
+  return v;
+}
+
+// ALiBi slope of (b, h) pre-multiplied by log2(e) (0 without ALiBi)
+__device__ __forceinline__ float ext_alibi2(const AttnExt& e, int b, int h) {
+  return e.alibi ? e.alibi[(long long)b * e.alibi_bs + h] * 1.4426950408889634f : 0.f;
+}

@@ -56,11 +56,11 @@ __device__ __forceinline__ unsigned int pack2(float a, float b) {
   return __builtin_bit_cast(unsigned int, __builtin_convertvector((f32x2_v){a, b}, bf16x2_v));
 }
 
-template <int D, bool CAUSAL, int W = 8, int MINW = 1>
+template <int D, bool CAUSAL, bool EXT, int W = 8, int MINW = 1>
 __global__ void __launch_bounds__(64 * W, MINW)
 attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
                 bf16_t* __restrict__ O, float* __restrict__ LSE, int S, int H, int HKV, float scale_log2,
-                AttnStrides st, AttnVarlen vl) {
+                AttnStrides st, AttnVarlen vl, AttnExt ex) {
   using C = Fwd2Cfg<D, W>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -118,10 +118,23 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   bool seeded = false;  // the row's offset was set from its first visible scores
 
   int n_tiles = (SK + C::BK - 1) / C::BK;
-  if (CAUSAL) {
-    const int last = min(SK - 1, min(SQ - 1, q_blk0 + C::BQ - 1) + co);  // last key the block's queries see
+  int t_begin = 0;  // EXT sliding window: tiles left of every query's window are skipped
+  const int pre = EXT && ex.prefix ? min(SK, ex.prefix[b]) : 0;
+  if (CAUSAL || EXT) {
+    const int q_last = min(SQ - 1, q_blk0 + C::BQ - 1);
+    int last = SK - 1;  // last key the block's queries see
+    if (CAUSAL) last = min(last, q_last + co);
+    if (EXT && ex.win_r >= 0) last = min(last, q_last + co + ex.win_r);
+    if (EXT && pre > 0) last = max(last, pre - 1);
     n_tiles = last < 0 ? 0 : min(n_tiles, last / C::BK + 1);
+    if (EXT && ex.win_l >= 0 && pre == 0) t_begin = min(n_tiles, max(0, q_blk0 + co - ex.win_l) / C::BK);
   }
+  const int n_run = n_tiles - t_begin;
+  const long long bh = vl.cu_q ? (long long)h : (long long)b * H + h;  // dropout hash row
+  const float al2 = EXT ? ext_alibi2(ex, b, h) : 0.f;
+  const float* brow = nullptr;  // this lane's query row of the additive bias
+  if (EXT && ex.bias && q0 + r < SQ)
+    brow = ex.bias + (int64_t)b * ex.bias_bs + (int64_t)h * ex.bias_hs + (int64_t)(q0 + r) * ex.bias_qs;
 
   u32x4 kst[C::VPT], vst[C::VPT];
   auto issue_load = [&](int t) {
@@ -151,19 +164,25 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
     }
   };
 
-  issue_load(0);
+  issue_load(t_begin);
   write_lds(0);
-  if (n_tiles > 1) issue_load(1);
+  if (n_run > 1) issue_load(t_begin + 1);
   __syncthreads();
 
   const int g4 = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
 
-  for (int t = 0; t < n_tiles; ++t) {
+  for (int tt = 0; tt < n_run; ++tt) {
+    const int t = t_begin + tt;
     const int k0 = t * C::BK;
-    const char* kl = smem + (t & 1) * 2 * C::TILE;
+    const char* kl = smem + (tt & 1) * 2 * C::TILE;
     const char* vl = kl + C::TILE;
     // a wave whose 32 queries all lie before this tile has nothing to do here
-    const bool active = !CAUSAL || (k0 <= q0 + 31 + co);
+    bool active = !CAUSAL || (k0 <= q0 + 31 + co);
+    if (EXT) {
+      if (k0 < pre) active = true;
+      if (ex.win_r >= 0) active = active && (k0 <= q0 + 31 + co + ex.win_r);
+      if (ex.win_l >= 0 && k0 >= pre) active = active && (k0 + C::BK - 1 >= q0 + co - ex.win_l);
+    }
     if (active) {
       // ---- S'^T = K Q'^T - m : two 32-key subtiles; the accumulator starts at
       // -m_i (row constant as the initial accumulator), so p = exp2(S') needs
@@ -183,7 +202,19 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
       // ---- online softmax: lane = query q0 + r, its 32 keys in registers
       const int q = q0 + r;
       const bool need_mask = (k0 + C::BK > SK) || (CAUSAL && (k0 + C::BK - 1 > q0 + co));
-      if (need_mask) {
+      if (EXT) {
+        // window / prefix visibility and the additive bias (exp2 domain)
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = k0 + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            const bool vis = ext_visible(ex, CAUSAL, q, key, co, SK, pre);
+            float add = (brow && vis) ? brow[key] * 1.4426950408889634f : 0.f;
+            add -= al2 * fabsf((float)(key - q - co));
+            s[sb][i] = vis ? s[sb][i] + add : -INFINITY;
+          }
+      } else if (need_mask) {
         // keys < lim are visible to this lane's query (branch-free selects)
         const int lim = CAUSAL ? min(SK, q + co + 1) : SK;
 #pragma unroll
@@ -228,6 +259,17 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
           rs += p;
         }
       l_i += rs;
+      if (EXT && ex.dropout) {
+        // O accumulates the dropped probabilities; l (hence LSE) the full ones
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = k0 + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            const bool keep = attn_keep(ex, bh, (long long)sr.q_off + q, (long long)sr.k_off + key);
+            s[sb][i] = keep ? s[sb][i] * ex.inv_keep : 0.f;
+          }
+      }
 
       // ---- O^T += V^T P^T : 4 k-steps of 16 keys
 #pragma unroll
@@ -251,9 +293,9 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
         }
       }
     }
-    if (t + 1 < n_tiles) {
-      write_lds((t + 1) & 1);
-      if (t + 2 < n_tiles) issue_load(t + 2);
+    if (tt + 1 < n_run) {
+      write_lds((tt + 1) & 1);
+      if (tt + 2 < n_run) issue_load(t + 2);
     }
     __syncthreads();
   }
@@ -280,25 +322,32 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   }
 }
 
-template <int D, bool CAUSAL, int W, int MINW>
+template <int D, bool CAUSAL, bool EXT, int W, int MINW>
 static void launch_fwd_v(const void* q, const void* k, const void* v, void* o, void* lse, int B, int S, int H,
-                         int HKV, float scale_log2, const AttnStrides& st, const AttnVarlen& vl, hipStream_t s) {
+                         int HKV, float scale_log2, const AttnStrides& st, const AttnVarlen& vl, const AttnExt& ex,
+                         hipStream_t s) {
   using C = Fwd2Cfg<D, W>;
   dim3 grid((unsigned)((S + C::BQ - 1) / C::BQ * H * B)), block(64 * W);  // 1-D: xcd_block()
-  hipLaunchKernelGGL((attn_fwd_kernel<D, CAUSAL, W, MINW>), grid, block, 4 * C::TILE, s, (const bf16_t*)q,
-                     (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st, vl);
+  hipLaunchKernelGGL((attn_fwd_kernel<D, CAUSAL, EXT, W, MINW>), grid, block, 4 * C::TILE, s, (const bf16_t*)q,
+                     (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st, vl, ex);
 }
 
 template <int D>
 static void launch_fwd(const void* q, const void* k, const void* v, void* o, void* lse, int B, int S, int H, int HKV,
-                       int causal, float scale_log2, const AttnStrides& st, const AttnVarlen& vl, hipStream_t s) {
+                       int causal, float scale_log2, const AttnStrides& st, const AttnVarlen& vl, hipStream_t s,
+                       const AttnExt* ext = nullptr) {
   // D=64: 4 waves (128 queries per block, 184 VGPRs, two blocks per CU):
   // twice the blocks of the 8-wave form for a finer causal balance; measured
   // against 8 waves capped at 128 VGPRs (spills) / uncapped and 4 waves
   // capped: 289-311 vs 239-288 TF/s (profiles/r2/attn_fwd64_variants.jsonl)
   constexpr int W = D == 64 ? 4 : 8;
-  return causal ? launch_fwd_v<D, true, W, 1>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, s)
-                : launch_fwd_v<D, false, W, 1>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, s);
+  if (ext) {
+    return causal ? launch_fwd_v<D, true, true, W, 1>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, *ext, s)
+                  : launch_fwd_v<D, false, true, W, 1>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, *ext, s);
+  }
+  const AttnExt none = {};
+  return causal ? launch_fwd_v<D, true, false, W, 1>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s)
+                : launch_fwd_v<D, false, false, W, 1>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s);
 }
 
 // strides: int64[8] = q_bs, q_rs, k_bs, k_rs, v_bs, v_rs, o_bs, o_rs (elements)
@@ -343,4 +392,67 @@ extern "C" int dw_attn_fwd(const void* q, const void* k, const void* v, void* o,
   const long long st[8] = {(long long)S * H * D, (long long)H * D, (long long)S * HKV * D, (long long)HKV * D,
                            (long long)S * HKV * D, (long long)HKV * D, (long long)S * H * D, (long long)H * D};
   return dw_attn_fwd_strided(q, k, v, o, lse, B, S, H, HKV, D, st, causal, softmax_scale, flags, stream);
+}
+
+// Extended masks (window / GLM prefix / additive bias / dropout; attn_common.h
+// AttnExtArgs).  Dense: strides as dw_attn_fwd_strided, Sq = Sk = S.
+extern "C" int dw_attn_fwd_ext(const void* q, const void* k, const void* v, void* o, void* lse, int B, int S, int H,
+                               int HKV, int D, const long long* strides, int causal, float softmax_scale,
+                               const AttnExtArgs* args, void* stream) {
+  if (H % HKV != 0) return (int)hipErrorInvalidValue;
+  AttnStrides st = {};
+  st.q_bs = strides[0]; st.q_rs = strides[1]; st.k_bs = strides[2]; st.k_rs = strides[3];
+  st.v_bs = strides[4]; st.v_rs = strides[5]; st.o_bs = strides[6]; st.o_rs = strides[7];
+  const float scale_log2 = softmax_scale * 1.4426950408889634f;
+  hipStream_t s = (hipStream_t)stream;
+  const AttnVarlen vl = {nullptr, nullptr, 0, 0};
+  const AttnExt ex = make_ext(args, S, S);
+  const AttnExt* ep = ext_active(args) ? &ex : nullptr;
+  if (D == 128) launch_fwd<128>(q, k, v, o, lse, B, S, H, HKV, causal, scale_log2, st, vl, s, ep);
+  else if (D == 64) launch_fwd<64>(q, k, v, o, lse, B, S, H, HKV, causal, scale_log2, st, vl, s, ep);
+  else return (int)hipErrorInvalidValue;
+  DW_LAUNCH_RET;
+}
+
+// Packed batches with window / dropout (no bias / prefix: their indexing is dense).
+extern "C" int dw_attn_fwd_varlen_ext(const void* q, const void* k, const void* v, void* o, void* lse,
+                                      const void* cu_q, const void* cu_k, int B, int max_seqlen_q, int total_q,
+                                      int total_k, int H, int HKV, int D, const long long* row_strides, int causal,
+                                      float softmax_scale, const AttnExtArgs* args, void* stream) {
+  if (H % HKV != 0 || !cu_q || !cu_k || (args && (args->bias || args->prefix || (args->alibi && args->alibi_bs))))
+    return (int)hipErrorInvalidValue;
+  AttnStrides st = {};
+  st.q_rs = row_strides[0]; st.k_rs = row_strides[1]; st.v_rs = row_strides[2]; st.o_rs = row_strides[3];
+  const AttnVarlen vl = {(const int*)cu_q, (const int*)cu_k, total_q, total_k};
+  const float scale_log2 = softmax_scale * 1.4426950408889634f;
+  hipStream_t s = (hipStream_t)stream;
+  const AttnExt ex = make_ext(args, total_q, total_k);
+  const AttnExt* ep = ext_active(args) ? &ex : nullptr;
+  if (D == 128) launch_fwd<128>(q, k, v, o, lse, B, max_seqlen_q, H, HKV, causal, scale_log2, st, vl, s, ep);
+  else if (D == 64) launch_fwd<64>(q, k, v, o, lse, B, max_seqlen_q, H, HKV, causal, scale_log2, st, vl, s, ep);
+  else return (int)hipErrorInvalidValue;
+  DW_LAUNCH_RET;
+}
+
+// The dropout keep-mask the kernels use, materialised (tests / references):
+// out uint8 [B, H, S, S] (dense index space, tq = tk = S), 1 = kept.
+__global__ void attn_dropout_mask_kernel(unsigned char* out, int B, int H, int S, AttnExt ex) {
+  const long long n = (long long)B * H * S * S;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long key = i % S, q = (i / S) % S, bh = i / ((long long)S * S);
+    out[i] = attn_keep(ex, bh, q, key) ? 1 : 0;
+  }
+}
+
+extern "C" int dw_attn_dropout_mask(void* out, int B, int H, int S, float p, unsigned long long seed,
+                                    unsigned long long offset, void* stream) {
+  AttnExtArgs a = {};
+  a.win_l = a.win_r = -1;
+  a.p_drop = p;
+  a.seed = seed;
+  a.offset = offset;
+  const AttnExt ex = make_ext(&a, S, S);
+  hipLaunchKernelGGL(attn_dropout_mask_kernel, dim3(1024), dim3(256), 0, (hipStream_t)stream, (unsigned char*)out, B,
+                     H, S, ex);
+  DW_LAUNCH_RET;
 }
