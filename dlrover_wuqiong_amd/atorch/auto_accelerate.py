@@ -60,9 +60,9 @@ from . import distributed as adist
 
 ORDER = ["parallel_mode", "module_replace", "half", "amp_native", "tensor_parallel", "sequence_parallel",
          "context_parallel",
-         "checkpoint", "pipeline_parallel", "fsdp", "zero2", "zero1", "ddp"]
+         "checkpoint", "mixed_parallel", "pipeline_parallel", "fsdp", "zero2", "zero1", "ddp"]
 ALIASES = {"amp": "amp_native", "amp_native_bf16": "amp_native", "fsdp2": "fsdp", "zero3": "fsdp",
-           "pipe": "pipeline_parallel", "pipeline": "pipeline_parallel", "ds_3d_parallel": "pipeline_parallel"}
+           "pipe": "pipeline_parallel", "pipeline": "pipeline_parallel", "ds_3d_parallel": "mixed_parallel", "3d_parallel": "mixed_parallel"}
 
 
 @dataclass
@@ -377,6 +377,62 @@ def _apply_pipeline_parallel(ctx, cfg):
                 f"layers {[(c.start, c.end) for c in pipe.chunks]} schedule {pipe.schedule_name}")
 
 
+def _apply_mixed_parallel(ctx, cfg):
+    """TP x PP x DP in one strategy (ATorch ``MixedParallelOptimization`` /
+    ``ds_3d_parallel``; reference auto/opt_lib/mixed_parallel_optimization.py:32,
+    ds_3d_parallel_optimization.py:55): ``{"tensor": t, "pipeline": p,
+    "data": d, "chunks": m, "schedule": "1f1b", "virtual_stages": v}``.
+
+    Rank layout tensor -> pipeline -> data (TP inside one node's xGMI mesh,
+    PP / DP across).  The unsharded model is rebuilt with the framework's
+    Megatron-style TP layers (fused QKV / gate|up regrouped per rank,
+    vocab-parallel embedding, LM head and cross-entropy), cut into pipeline
+    stages at decoder-layer boundaries, and the stage's gradients average
+    over the data group after every pipeline step.  Train with
+    ``result.model.train_step(ids, targets)``."""
+    from ..models.llama import Llama, shard_llama_state_dict
+    from ..parallel.pipeline import PipelineModule
+
+    cfg = dict(cfg) if isinstance(cfg, dict) else {}
+    t, p = int(cfg.get("tensor", 1)), int(cfg.get("pipeline", 1))
+    if not dist.is_initialized():
+        raise RuntimeError("mixed_parallel needs torch.distributed")
+    world = dist.get_world_size()
+    d = int(cfg.get("data", world // max(1, t * p)))
+    if t * p * d != world:
+        raise ValueError(f"mixed_parallel: tensor {t} x pipeline {p} x data {d} != world {world}")
+    if adist.parallel_config() is None:
+        adist.create_parallel_group(([("tensor", t), ("pipeline", p), ("data", d)], None))
+    model = ctx["model"]
+    if t > 1:
+        if not isinstance(model, Llama):
+            raise TypeError(f"mixed_parallel tensor sharding supports Llama models, got {type(model).__name__}")
+        tg = adist.parallel_group("tensor")
+        tr = adist.parallel_rank("tensor")
+        dtype = next(model.parameters()).dtype
+        full = {k: v.detach() for k, v in model.state_dict().items()}
+        tp_model = Llama(model.cfg, tp_group=tg).to(dtype)
+        tp_model.load_state_dict(shard_llama_state_dict(full, model.cfg, tr, t))
+        model = tp_model
+    if p > 1:
+        group, ranks = adist.parallel_group_and_ranks("pipeline")
+        me = dist.get_rank()
+        emb_group = None
+        for _g, rk in adist._DistributedContext.PARALLEL_GROUPS_AND_RANKS["pipeline"]:
+            eg = dist.new_group(sorted({rk[0], rk[-1]}))
+            if me in rk:
+                emb_group = eg
+        model = PipelineModule(model, p, ranks.index(me), num_microbatches=cfg.get("chunks", p),
+                               schedule=cfg.get("schedule", "1f1b"), virtual_stages=cfg.get("virtual_stages", 1),
+                               group=group, embedding_group=emb_group)
+        model.amp_dtype = ctx.get("amp_dtype")
+        ctx["pipeline"] = True
+    ctx["model"] = model
+    ctx["dp_group"] = adist.parallel_group("data")
+    ctx["tp_group"] = adist.parallel_group("tensor")
+    logger.info(f"mixed_parallel: tensor {t} x pipeline {p} x data {d}")
+
+
 def _hsdp_mesh(ctx):
     """Hybrid sharding (HSDP): with ``parallel_mode`` groups ("zero", z) and
     ("data", d), both > 1, parameters are sharded inside each zero group and
@@ -411,8 +467,17 @@ def _apply_fsdp(ctx, cfg, reshard=True):
     dtype = ctx.get("amp_dtype")
     mp = MixedPrecisionPolicy(param_dtype=dtype, reduce_dtype=torch.float32) if dtype else MixedPrecisionPolicy()
     mesh = _hsdp_mesh(ctx)
+    local_sgd = isinstance(cfg, dict) and cfg.get("use_local_sgd")
+    if local_sgd:
+        if mesh is None:
+            raise RuntimeError("use_local_sgd requires hybrid sharding (parallel_mode zero x data)")
+        # every replica is its own FSDP group over the shard dimension: no
+        # per-step all-reduce across replicas at all; HSDPLocalSGD merges the
+        # shards every sync_interval steps (and averages gradients in warm-up)
+        ctx["local_sgd"] = (mesh.get_group("replicate"), cfg)
+        mesh = mesh["shard"]
     dpg = ctx.get("dp_group")
-    if mesh is None and dpg is not None and dist.get_world_size(dpg) != dist.get_world_size():
+    if mesh is None and not local_sgd and dpg is not None and dist.get_world_size(dpg) != dist.get_world_size():
         from torch.distributed.device_mesh import DeviceMesh
 
         _g, ranks = adist.parallel_group_and_ranks("data")
@@ -465,7 +530,7 @@ def _apply_ddp(ctx, cfg):
 APPLY = {"parallel_mode": _apply_parallel_mode, "module_replace": _apply_module_replace, "half": _apply_half,
          "amp_native": _apply_amp_native, "tensor_parallel": _apply_tensor_parallel,
          "sequence_parallel": _apply_sequence_parallel, "context_parallel": _apply_context_parallel,
-         "checkpoint": _apply_checkpoint,
+         "checkpoint": _apply_checkpoint, "mixed_parallel": _apply_mixed_parallel,
          "pipeline_parallel": _apply_pipeline_parallel,
          "fsdp": _apply_fsdp, "zero2": functools.partial(_apply_fsdp, reshard=False),
          "zero1": lambda ctx, cfg: ctx.__setitem__("zero1", True), "ddp": _apply_ddp}
@@ -510,6 +575,11 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
     if included:
         have = set(strategy.names())
         strategy = Strategy.from_spec(strategy.opts + [(n, None) for n in included if n not in have])
+    if world > 1 and "mixed_parallel" in strategy.names() and "parallel_mode" not in strategy.names():
+        mcfg = strategy.config("mixed_parallel") or {}
+        t, p = int(mcfg.get("tensor", 1)), int(mcfg.get("pipeline", 1))
+        dims = [("tensor", t), ("pipeline", p), ("data", int(mcfg.get("data", world // max(1, t * p))))]
+        strategy = Strategy.from_spec([("parallel_mode", (dims, None))] + strategy.opts)
     if world > 1 and "parallel_mode" not in strategy.names():
         strategy = Strategy.from_spec([("parallel_mode", None)] + strategy.opts)
     if world > 1 and not {"ddp", "fsdp", "zero2", "zero1"} & set(strategy.names()):
@@ -521,7 +591,7 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
     for name, cfg in strategy.opts:
         if name == "parallel_mode":
             APPLY[name](ctx, cfg)
-            if dev.type == "cuda" and "pipeline_parallel" not in strategy.names():
+            if dev.type == "cuda" and not {"pipeline_parallel", "mixed_parallel"} & set(strategy.names()):
                 ctx["model"] = ctx["model"].to(dev)  # a pipeline moves only its own stage later
             continue
         APPLY[name](ctx, cfg)
@@ -554,6 +624,24 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
                                             **args)
         else:
             optim = optim_func(params, **args)
+        if ctx.get("local_sgd"):
+            from .local_sgd import GTAReducer, HSDPLocalSGD, LinearReducer
+
+            rg, lcfg = ctx["local_sgd"]
+            red = None
+            if lcfg.get("reducer") == "gta":
+                red = GTAReducer(rg, consensus_method=lcfg.get("consensus_method", "sum"),
+                                 sparsification_method=lcfg.get("sparsification_method"),
+                                 normalize=lcfg.get("normalize", True), density=lcfg.get("density", 1.0))
+            elif lcfg.get("reducer") in (None, "linear"):
+                red = LinearReducer(rg)
+            optim = HSDPLocalSGD(model, optim, rg, sync_interval=lcfg.get("local_sgd_sync_interval", 1),
+                                 warmup_steps=lcfg.get("local_sgd_warmup_steps", 0),
+                                 outer_optim_class=lcfg.get("outer_optim_class"),
+                                 outer_optim_kwargs=lcfg.get("outer_optim_kwargs"), reducer=red,
+                                 cpu_offload=lcfg.get("outer_optim_cpu_offload", False))
+            logger.info(f"fsdp: local SGD over the replicate dimension (sync every "
+                        f"{optim.sync_interval} steps after {optim.warmup_steps} warm-up steps)")
     sched = lr_scheduler_cls(optim, **(lr_scheduler_args or {})) if (lr_scheduler_cls and optim) else None
 
     dataloader = None

@@ -179,3 +179,133 @@ class LocalSGD:
         self.local_step = sd["local_step"]
         if self.momentum_buf is not None and sd.get("momentum") is not None:
             self.momentum_buf.copy_(sd["momentum"])
+
+
+class HSDPLocalSGD:
+    """Local SGD inside hybrid sharding (FSDP2 on a (replicate, shard) mesh).
+
+    Each replica is an FSDP2 group over the shard dimension (one node's xGMI
+    mesh): gradients are reduce-scattered inside it every step and -- after
+    ``warmup_steps`` steps whose sharded gradients this wrapper averages
+    across replicas (plain HSDP) -- NOT all-reduced across the replicate
+    dimension (the inter-node hop) at all.  Every
+    ``sync_interval`` steps the local parameter SHARDS are merged across the
+    replicate group: the pseudo-gradient ``anchor - shard`` goes through the
+    reducer (linear mean or GTA) and an optional outer optimizer (e.g.
+    Nesterov SGD, DiLoCo) updates the anchor, which every replica then
+    adopts.  Only shards travel (1/shard_size of the model per replica).
+
+    Parity: ATorch ``local_sgd/HSDP`` (``_runtime_utils.py:143,268``: outer
+    optimizer over ``last_synced_params``, per-handle averaging) enabled by
+    ``use_local_sgd`` in the FSDP config (``auto/opt_lib/zero_optimization.py:405-412``).
+    """
+
+    def __init__(self, model, optimizer, replicate_group, sync_interval: int = 1, warmup_steps: int = 0,
+                 outer_optim_class=None, outer_optim_kwargs: Optional[dict] = None,
+                 reducer: Optional[TensorReducer] = None, cpu_offload: bool = False):
+        self.model = model
+        self.optimizer = optimizer
+        self.group = replicate_group
+        self.sync_interval = max(1, int(sync_interval))
+        self.warmup_steps = max(0, int(warmup_steps))
+        self.reducer = reducer or LinearReducer(replicate_group)
+        self.outer_optim_class, self.outer_optim_kwargs = outer_optim_class, dict(outer_optim_kwargs or {})
+        self.cpu_offload = cpu_offload
+        self.step_count = 0
+        self.syncs = 0
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        self.anchor = None
+        self.outer_optimizer = None
+        if self.warmup_steps == 0:
+            self._start_local()
+
+    # the wrapper is handed out as "the optimizer"
+    @property
+    def param_groups(self):
+        return self.optimizer.param_groups
+
+    @property
+    def state(self):
+        return self.optimizer.state
+
+    def zero_grad(self, set_to_none: bool = True):
+        self.optimizer.zero_grad(set_to_none=set_to_none)
+
+    @staticmethod
+    def _local(p):
+        return p.to_local() if hasattr(p, "to_local") else p
+
+    def _flat(self) -> torch.Tensor:
+        return torch.cat([self._local(p.data).reshape(-1).float() for p in self.params])
+
+    @torch.no_grad()
+    def _allreduce_grads(self):
+        """Warm-up steps: average the sharded gradients across replicas."""
+        grads = [self._local(p.grad) for p in self.params if p.grad is not None]
+        if not grads or _ws(self.group) <= 1:
+            return
+        flat = torch.cat([g.reshape(-1).float() for g in grads])
+        dist.all_reduce(flat, group=self.group)
+        flat.div_(_ws(self.group))
+        o = 0
+        for g in grads:
+            g.copy_(flat[o:o + g.numel()].view_as(g))
+            o += g.numel()
+
+    @torch.no_grad()
+    def _start_local(self):
+        a = self._flat()
+        if self.cpu_offload:  # the anchor (+ outer optimizer state) lives in host memory
+            a = a.cpu().pin_memory() if torch.cuda.is_available() else a.cpu()
+        self.anchor = torch.nn.Parameter(a)
+        if self.outer_optim_class is not None:
+            self.outer_optimizer = self.outer_optim_class([self.anchor], **self.outer_optim_kwargs)
+
+    @torch.no_grad()
+    def sync(self):
+        cur = self._flat()
+        anchor = self.anchor.data.to(cur.device)
+        delta = anchor - cur  # pseudo-gradient of this replica's shard
+        delta = self.reducer.reduce_tensor(delta)
+        if self.outer_optimizer is not None:
+            self.anchor.grad = delta.to(self.anchor.device)
+            self.outer_optimizer.step()
+            self.anchor.grad = None
+        else:
+            self.anchor.data.copy_((anchor - delta).to(self.anchor.device))
+        new = self.anchor.data.to(cur.device)
+        o = 0
+        for p in self.params:
+            loc = self._local(p.data)
+            n = loc.numel()
+            loc.copy_(new[o:o + n].view_as(loc))
+            o += n
+        self.syncs += 1
+
+    def step(self, closure=None):
+        if self.anchor is None:
+            self._allreduce_grads()
+        loss = self.optimizer.step(closure)
+        self.step_count += 1
+        if self.anchor is None:
+            if self.step_count >= self.warmup_steps:
+                self._start_local()  # replicas are identical here: all-reduce ran until now
+            return loss
+        if (self.step_count - self.warmup_steps) % self.sync_interval == 0:
+            self.sync()
+        return loss
+
+    def state_dict(self):
+        return {"inner": self.optimizer.state_dict(), "step_count": self.step_count,
+                "anchor": None if self.anchor is None else self.anchor.data,
+                "outer": None if self.outer_optimizer is None else self.outer_optimizer.state_dict()}
+
+    def load_state_dict(self, sd):
+        self.optimizer.load_state_dict(sd["inner"])
+        self.step_count = sd["step_count"]
+        if sd.get("anchor") is not None:
+            if self.anchor is None:
+                self._start_local()
+            self.anchor.data.copy_(sd["anchor"])
+            if self.outer_optimizer is not None and sd.get("outer") is not None:
+                self.outer_optimizer.load_state_dict(sd["outer"])
