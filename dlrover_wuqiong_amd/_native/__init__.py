@@ -79,12 +79,17 @@ def kernels(required: bool = True):
 def _stale(lib_path: str, which: str) -> bool:
     if os.environ.get("DWAMD_NO_REBUILD", "0") == "1":
         return False
-    from .build import sources_for
+    from .build import sources_digest, sources_for
 
     try:
         lib_m = os.path.getmtime(lib_path)
     except OSError:
         return True
+    try:
+        with open(lib_path + ".srcsha") as f:
+            return f.read().strip() != sources_digest(which)  # content decides when recorded
+    except OSError:
+        pass
     for s in sources_for(which):
         try:
             if os.path.getmtime(s) > lib_m:

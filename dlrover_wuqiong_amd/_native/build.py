@@ -55,7 +55,53 @@ def _atomic_replace(tmp, dst):
     os.replace(tmp, dst)
 
 
+def sources_digest(which) -> str:
+    """Content hash of a library's sources: a copied tree (tar, rsync) keeps
+    the library fresh even when file times change."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for s in sources_for(which):
+        h.update(os.path.basename(s).encode())
+        with open(s, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _write_digest(lib_path, which):
+    with open(lib_path + ".srcsha.tmp", "w") as f:
+        f.write(sources_digest(which))
+    os.replace(lib_path + ".srcsha.tmp", lib_path + ".srcsha")
+
+
+class _BuildLock:
+    """One builder per tree: concurrent processes (workers + standbys that
+    find the library stale) wait instead of racing on the same objects."""
+
+    def __init__(self):
+        os.makedirs(BUILD_DIR, exist_ok=True)
+        self.path = os.path.join(BUILD_DIR, ".lock")
+
+    def __enter__(self):
+        import fcntl
+
+        self.f = open(self.path, "w")
+        fcntl.flock(self.f, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *a):
+        import fcntl
+
+        fcntl.flock(self.f, fcntl.LOCK_UN)
+        self.f.close()
+
+
 def build_runtime(verbose=False):
+    with _BuildLock():
+        return _build_runtime(verbose)
+
+
+def _build_runtime(verbose=False):
     os.makedirs(BUILD_DIR, exist_ok=True)
     srcs = [s for s in sources_for("runtime") if s.endswith(".cpp")]
     out = runtime_lib_path()
@@ -67,6 +113,7 @@ def build_runtime(verbose=False):
     if verbose and o:
         print(o)
     _atomic_replace(tmp, out)
+    _write_digest(out, "runtime")
     return out
 
 
@@ -78,13 +125,18 @@ def _compile_hip(src):
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
            "-mcode-object-version=5", "-munsafe-fp-atomics", "-ffp-contract=fast",
            "-Wno-unused-result", "-I", os.path.join(CSRC, "kernels"), "-c", src,
-           "-o", obj + ".tmp"]
+           "-o", obj + f".tmp{os.getpid()}"]
     _run(cmd)
-    os.replace(obj + ".tmp", obj)
+    os.replace(obj + f".tmp{os.getpid()}", obj)
     return obj
 
 
 def build_kernels(verbose=False, jobs=None):
+    with _BuildLock():
+        return _build_kernels(verbose, jobs)
+
+
+def _build_kernels(verbose=False, jobs=None):
     os.makedirs(BUILD_DIR, exist_ok=True)
     srcs = [s for s in sources_for("kernels") if s.endswith(".hip")]
     jobs = jobs or min(8, max(1, len(srcs)))
@@ -98,6 +150,7 @@ def build_kernels(verbose=False, jobs=None):
     if verbose and o:
         print(o)
     _atomic_replace(tmp, out)
+    _write_digest(out, "kernels")
     return out
 
 
