@@ -109,6 +109,8 @@ OPTIONAL = {
     "dw_attn_bwd_varlen_ext": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32,
                                      i32, i32, vp, i32, f32, vp, vp]),
     "dw_attn_dropout_mask": (i32, [vp, i32, i32, i32, f32, u64, u64, vp]),
+    # moe_permute.hip
+    "dw_moe_regroup": (i32, [vp, vp, vp, i32, i32, i64, i32, i32, vp]),
 }
 
 

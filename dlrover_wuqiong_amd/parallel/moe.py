@@ -7,7 +7,9 @@ Token path (per MoE layer):
      builds a contiguous, expert-grouped activation buffer;
   3. expert parallel: the buffer is exchanged with ONE variable-split
      ``all_to_all_single`` over the EP group (RCCL; the per-expert counts go
-     first in a tiny all_to_all) and regrouped by local expert;
+     first in a tiny all_to_all; the split sizes are the layer's only host
+     read) and regrouped by local expert in ONE permutation launch driven by
+     the device counts (``csrc/kernels/moe_permute.hip``);
   4. the local experts run as grouped GEMMs over the contiguous groups
      (``grouped_mlp`` -> ``ops.grouped_gemm``: one MFMA launch per projection
      for all experts, group offsets on the device -- no host sync, no
@@ -54,6 +56,60 @@ class _AllToAllV(torch.autograd.Function):
 
 def all_to_all_v(x, out_splits, in_splits, group):
     return _AllToAllV.apply(x, out_splits, in_splits, group)
+
+
+def _regroup_index(counts: torch.Tensor, n: int) -> torch.Tensor:
+    """dst[i] of every received row i (torch ops; the CPU path and the
+    reference of ``csrc/kernels/moe_permute.hip``)."""
+    ep, L = counts.shape
+    flat = counts.reshape(-1)
+    src_off = torch.cumsum(flat, 0) - flat                       # (s, e) source-major
+    t = counts.t().reshape(-1)
+    exp_off = (torch.cumsum(t, 0) - t).view(L, ep).t().reshape(-1)  # [s * L + e] expert-major
+    seg = torch.repeat_interleave(torch.arange(ep * L, device=counts.device), flat, output_size=n)
+    return exp_off[seg] + torch.arange(n, device=counts.device) - src_off[seg]
+
+
+def _regroup(x: torch.Tensor, counts: torch.Tensor, direction: int) -> torch.Tensor:
+    from ..ops import _hip
+
+    n = x.shape[0]
+    row_bytes = x[0].numel() * x.element_size() if n else 0
+    if _hip.use_hip(x) and x.is_contiguous() and row_bytes % 16 == 0 and counts.numel() <= 1024:
+        import ctypes
+
+        out = torch.empty_like(x)
+        c = counts.to(torch.int64).contiguous()
+        _hip.check(_hip.lib().dw_moe_regroup(_hip.ptr(x), _hip.ptr(out), _hip.ptr(c), counts.shape[0],
+                                             counts.shape[1], ctypes.c_longlong(n), row_bytes, direction,
+                                             _hip.stream()), "moe_regroup")
+        return out
+    dst = _regroup_index(counts, n)
+    if direction == 0:
+        return torch.empty_like(x).index_copy_(0, dst, x)
+    return x.index_select(0, dst)
+
+
+class _Regroup(torch.autograd.Function):
+    """(source rank, expert) -> (expert, source rank) row order and back; the
+    backward is the opposite direction of the same permutation."""
+
+    @staticmethod
+    def forward(ctx, x, counts, direction: int):
+        ctx.save_for_backward(counts)
+        ctx.direction = direction
+        return _regroup(x.contiguous(), counts, direction)
+
+    @staticmethod
+    def backward(ctx, g):
+        (counts,) = ctx.saved_tensors
+        return _regroup(g.contiguous(), counts, 1 - ctx.direction), None, None
+
+
+def moe_regroup(x: torch.Tensor, counts: torch.Tensor, direction: int = 0) -> torch.Tensor:
+    """``counts`` [ep, L] rows per (source rank, local expert), on the device.
+    direction 0: received order -> expert-grouped; 1: back."""
+    return _Regroup.apply(x, counts, direction)
 
 
 class TopKGate(nn.Module):
@@ -170,24 +226,13 @@ class MoELayer(nn.Module):
             send_counts = counts.view(self.ep, self.num_local)  # [dst rank, local expert]
             recv_counts = torch.empty_like(send_counts)
             dist.all_to_all_single(recv_counts, send_counts.contiguous(), group=self.ep_group)
-            send_c = send_counts.tolist()
-            recv_c = recv_counts.tolist()  # [src rank, local expert]
-            in_splits = [sum(r) for r in send_c]
-            out_splits = [sum(r) for r in recv_c]
+            # the ONE host read per layer: the all-to-all split sizes
+            in_splits, out_splits = torch.stack([send_counts.sum(1), recv_counts.sum(1)]).tolist()
             xr = all_to_all_v(xs, out_splits, in_splits, self.ep_group)
-            # received rows are (src rank, expert)-ordered: regroup by local expert
-            seg, off = [], 0
-            for src in range(self.ep):
-                for e in range(self.num_local):
-                    seg.append((e, src, off, recv_c[src][e]))
-                    off += recv_c[src][e]
-            perm = [torch.arange(o, o + n, device=x.device) for e, src, o, n in sorted(seg)]
-            perm = torch.cat(perm) if perm else torch.zeros(0, dtype=torch.long, device=x.device)
-            local_counts = [sum(recv_c[s][e] for s in range(self.ep)) for e in range(self.num_local)]
-            y = self.experts(xr.index_select(0, perm), local_counts)
-            inv = torch.empty_like(perm)
-            inv[perm] = torch.arange(perm.numel(), device=x.device)
-            y = all_to_all_v(y.index_select(0, inv), in_splits, out_splits, self.ep_group)
+            # received rows are (src rank, expert)-ordered: one permutation
+            # launch (device counts) groups them by local expert
+            y = self.experts(moe_regroup(xr, recv_counts, 0), recv_counts.sum(0))
+            y = all_to_all_v(moe_regroup(y, recv_counts, 1), in_splits, out_splits, self.ep_group)
         else:
             y = self.experts(xs, counts)  # device counts: no host sync on the GPU path
         # un-permute and combine the k expert outputs per token

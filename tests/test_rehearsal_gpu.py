@@ -24,13 +24,15 @@ def test_gpu_rehearse_two_ranks_shared_device(tmp_path):
         pytest.skip("no GPU")
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
     cmd = [sys.executable, "-u", os.path.join(REPO, "bench.py"), "--gpus", "2", "--rehearse-shared-device",
-           "--model", "gpt2", "--micro-batch", "2", "--seq", "256", "--steps", "8", "--warmup", "3",
-           "--fault-window", "16", "--import-window", "12", "--inject-slow-flush", "3",
+           "--model", "gpt2", "--micro-batch", "2", "--seq", "256", "--steps", "4", "--warmup", "2",
+           "--fault-window", "12", "--import-window", "8", "--inject-slow-flush", "3",
            "--ckpt-dir", str(tmp_path / "ckpt"), "--timeout", "300"]
-    r = subprocess.run(cmd, env=env, cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
-                       timeout=380)
-    sys.stderr.write(r.stderr[-6000:])
-    assert r.returncode == 0, r.stderr[-20000:]
+    log = tmp_path / "bench.err"
+    with open(log, "w") as err:
+        r = subprocess.run(cmd, env=env, cwd=REPO, stdout=subprocess.PIPE, stderr=err, text=True, timeout=380)
+    tail = log.read_text()[-20000:]
+    sys.stderr.write(tail[-6000:])
+    assert r.returncode == 0, tail
     res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     print(json.dumps(res))
     assert res["rehearsal"] is True and res["n_gpus"] == 1 and res["rccl_world"] == 2
