@@ -17,8 +17,38 @@ class HipKernelError(RuntimeError):
     pass
 
 
+_TIMER = None  # utils.xpu_timer.XpuTimer timing this framework's own kernels (install(kernels=True))
+_NO_LAUNCH = ("workspace", "error", "_size", "mem_get_info", "ipc_", "device_malloc", "device_free",
+              "event_sync", "stream_sync", "_xt_")
+
+
+class _TimedLib:
+    """The kernel library with every launching ``dw_*`` entry point bracketed
+    by xpu_timer events on torch's current stream (the stream every launcher
+    of ``ops/*`` passes), so the framework's own HIP kernels -- attention,
+    norms, fused Adam, hipBLASLt epilogue GEMMs -- show up next to the
+    torch-level GEMMs and collectives (the reference gets this from an
+    LD_PRELOAD hook of the vendor libraries: atorch/dev/xpu_timer)."""
+
+    def __init__(self, lib_, timer):
+        self._lib, self._timer = lib_, timer
+
+    def __getattr__(self, name):
+        f = getattr(self._lib, name)
+        if not name.startswith("dw_") or any(t in name for t in _NO_LAUNCH):
+            return f
+        timer = self._timer
+
+        def call(*args):
+            with timer.kernel(name):
+                return f(*args)
+
+        return call
+
+
 def lib():
-    return kernels(required=True)
+    L = kernels(required=True)
+    return _TimedLib(L, _TIMER) if _TIMER is not None else L
 
 
 def stream() -> ctypes.c_void_p:

@@ -8,9 +8,14 @@ export and device-hang detection.
     print(timer.report())
 
 Interposition: a ``TorchFunctionMode`` catches ``mm/bmm/matmul/addmm/linear``
-(key = kind + m/n/k, work = 2mnk FLOPs) and the ``torch.distributed``
+(key = kind + m/n/k, work = 2mnk FLOPs), the ``torch.distributed``
 collectives are wrapped (key = collective + dtype + bytes, work = bytes,
-reported as algorithm and bus bandwidth).  On a GPU, each op is bracketed by
+reported as algorithm and bus bandwidth), and every launch of the
+framework's own HIP kernel library (flash attention, norms, RoPE, fused
+optimizers, grouped GEMM, hipBLASLt epilogue GEMMs, checkpoint copies) is
+bracketed at its single entry point (``ops/_hip.lib()``; key = ``kernel:``
++ entry point, i.e. ``kernel|dw_attn_fwd_strided``) -- the same coverage the reference gets from LD_PRELOAD
+hooks of the vendor libraries, without a preload.  On a GPU, each op is bracketed by
 two pooled hipEvents recorded on the current stream (``csrc/kernels/
 xpu_timer.hip``); a native poller thread turns them into statistics without
 ever synchronising the training stream, and flags a device hang when an op
@@ -61,6 +66,8 @@ class OpStat:
         return self.key.split("|", 1)[0]
 
     def rate(self) -> Dict[str, float]:
+        if self.kind == "kernel":
+            return {}  # framework kernels: latency statistics only
         if self.kind in ("mm", "bmm", "linear", "matmul", "addmm"):
             return {"tflops": self.work_per_us * 1e-6}
         return {"algbw_gbps": self.work_per_us * 1e-3}
@@ -265,9 +272,17 @@ class XpuTimer:
     def timed(self, key: str, work: float = 0.0, like: Optional[torch.Tensor] = None):
         return _Timed(self, key, work, like)
 
+    def kernel(self, name: str):
+        """Bracket one launch of a framework kernel on torch's current stream."""
+        return _TimedStream(self, "kernel|" + name)
+
     # ------------------------------------------------------------ install
-    def install(self, gemm: bool = True, collectives: bool = True) -> "XpuTimer":
+    def install(self, gemm: bool = True, collectives: bool = True, kernels: bool = True) -> "XpuTimer":
         self.backend.start(self.hang_timeout, self.poll_ms)
+        if kernels:
+            from ..ops import _hip
+
+            _hip._TIMER = self
         if gemm and self._mode is None:
             self._mode = _GemmMode(self)
             self._mode.__enter__()
@@ -280,6 +295,10 @@ class XpuTimer:
         return self
 
     def uninstall(self):
+        from ..ops import _hip
+
+        if _hip._TIMER is self:
+            _hip._TIMER = None
         if self._mode is not None:
             self._mode.__exit__(None, None, None)
             self._mode = None
@@ -359,7 +378,7 @@ class XpuTimer:
             r = s.rate()
             if "tflops" in r:
                 fams["tflops"].append((base, r["tflops"]))
-            else:
+            elif "algbw_gbps" in r:
                 fams["algbw_gbps"].append((base, r["algbw_gbps"]))
                 n = _ws_from_key(s.key)
                 factor = {"all_reduce": 2.0 * (n - 1) / n}.get(kind, (n - 1) / n if n > 1 else 1.0)
@@ -454,6 +473,28 @@ class _Timed:
     def __exit__(self, *exc):
         if self.tok is not None and self.tok >= 0:
             self.timer.backend.end(self.tok, self.work, self.stream)
+        return False
+
+
+class _TimedStream:
+    """Like _Timed, on torch's current stream (framework kernel launches)."""
+
+    __slots__ = ("timer", "key", "tok", "stream")
+
+    def __init__(self, timer, key):
+        self.timer, self.key, self.tok = timer, key, -1
+
+    def __enter__(self):
+        b = self.timer.backend
+        self.stream = None
+        if isinstance(b, _HipBackend):
+            self.stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        self.tok = b.begin(b.key(self.key), self.stream)
+        return self
+
+    def __exit__(self, *exc):
+        if self.tok is not None and self.tok >= 0:
+            self.timer.backend.end(self.tok, 0.0, self.stream)
         return False
 
 

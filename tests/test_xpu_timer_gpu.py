@@ -48,3 +48,36 @@ def test_gemm_timing_and_hang_detection():
         assert t.hang_status()[0] == 0  # cleared once the op finished
     finally:
         t.uninstall()
+
+
+def test_framework_kernels_are_timed():
+    """The framework's own HIP launches (attention, norms, fused Adam, ...)
+    appear as ``kernel|dw_*`` records next to the torch GEMMs."""
+    from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
+    from dlrover_wuqiong_amd.optimizers.fused import FusedAdamW
+    from dlrover_wuqiong_amd.parallel.flat import FlatParams
+    from dlrover_wuqiong_amd.utils.xpu_timer import XpuTimer
+
+    t = XpuTimer(hang_timeout=60, poll_ms=10).install(collectives=False)
+    try:
+        torch.manual_seed(0)
+        with torch.device("cuda"):
+            model = GPT2(GPT2Config.named("gpt2-tiny"))
+        model.to(torch.bfloat16)
+        flat = FlatParams(model)
+        opt = FusedAdamW(flat, lr=1e-3)
+        x = torch.randint(0, 1024, (2, 129), device="cuda")
+        for _ in range(3):
+            model(x[:, :-1], x[:, 1:]).backward()
+            opt.step()
+            flat.zero_grad()
+        torch.cuda.synchronize()
+        assert t.flush(10)
+        st = {s.key: s for s in t.stats()}
+        kern = {k: s for k, s in st.items() if k.startswith("kernel|")}
+        assert any("attn_fwd" in k for k in kern) and any("attn_bwd" in k for k in kern), sorted(st)
+        assert any("adam" in k.lower() for k in kern), sorted(kern)
+        assert all(s.count > 0 and s.avg_us > 0 for s in kern.values())
+        assert "kind=\"kernel\"" in t.prometheus_text()
+    finally:
+        t.uninstall()
