@@ -362,7 +362,7 @@ def _apply_pipeline_parallel(ctx, cfg):
     me = dist.get_rank()
     emb_group = None
     # first + last stage of every pipeline group (created by every rank, same order)
-    for _g, rk in adist._DistributedContext.PARALLEL_GROUPS_AND_RANKS["pipeline"]:
+    for _g, rk in adist.parallel_groups_and_ranks_all("pipeline"):
         eg = dist.new_group(sorted({rk[0], rk[-1]}))
         if me in rk:
             emb_group = eg
@@ -418,7 +418,7 @@ def _apply_mixed_parallel(ctx, cfg):
         group, ranks = adist.parallel_group_and_ranks("pipeline")
         me = dist.get_rank()
         emb_group = None
-        for _g, rk in adist._DistributedContext.PARALLEL_GROUPS_AND_RANKS["pipeline"]:
+        for _g, rk in adist.parallel_groups_and_ranks_all("pipeline"):
             eg = dist.new_group(sorted({rk[0], rk[-1]}))
             if me in rk:
                 emb_group = eg
@@ -447,8 +447,8 @@ def _hsdp_mesh(ctx):
         raise ValueError("HSDP needs zero x data == world size (no other parallel dimensions)")
     from torch.distributed.device_mesh import DeviceMesh
 
-    rows = sorted(sorted(r) for _g, r in adist._DistributedContext.PARALLEL_GROUPS_AND_RANKS["zero"])
-    data_groups = {tuple(sorted(r)) for _g, r in adist._DistributedContext.PARALLEL_GROUPS_AND_RANKS["data"]}
+    rows = sorted(sorted(r) for _g, r in adist.parallel_groups_and_ranks_all("zero"))
+    data_groups = {tuple(sorted(r)) for _g, r in adist.parallel_groups_and_ranks_all("data")}
     cols = {tuple(sorted(row[j] for row in rows)) for j in range(len(rows[0]))}
     if cols != data_groups:
         raise ValueError(f"zero groups {rows} and data groups {sorted(data_groups)} do not form a 2-D grid")

@@ -27,6 +27,8 @@ import torch.distributed as dist
 class _DistributedContext:
     INITIALIZED = False
     PARALLEL_CONFIG = None
+    PARALLEL_CONFIGS: Dict[str, object] = {}  # per group-name prefix (ParallelGroupContextManager)
+    PG_NAME_PREFIX = ""
     PARALLEL_GROUP: Dict[str, object] = {}
     PARALLEL_GROUPS_AND_RANKS: Dict[str, List[Tuple[object, List[int]]]] = {}
     PARALLEL_RANK: Dict[str, int] = {}
@@ -120,11 +122,15 @@ def create_parallel_group(parallel_config, timeout: Optional[timedelta] = None):
     if not multi and total != world_size():
         raise ValueError(f"product of parallel sizes ({total}) != world size ({world_size()}): {parallel_config}")
     rank_order = list(range(world_size())) if rank_order is None else list(rank_order)
-    _DistributedContext.PARALLEL_CONFIG = (slicing_dim, rank_order, multi)
+    pre = _DistributedContext.PG_NAME_PREFIX
+    _DistributedContext.PARALLEL_CONFIGS[pre] = (slicing_dim, rank_order, multi)
+    if not pre:
+        _DistributedContext.PARALLEL_CONFIG = (slicing_dim, rank_order, multi)
     _DistributedContext.PARALLEL_INSTANCE_NUM = world_size() // total
     _DistributedContext.PARALLEL_INSTANCE_INDEX = rank() // total if rank() < world_size() // total * total else None
     all_pg = get_pg_ranks(slicing_dim, rank_order)
-    for name, size in slicing_dim:
+    for dim_name, size in slicing_dim:
+        name = pre + dim_name
         if len(slicing_dim) == 1 and total == world_size():
             _DistributedContext.PARALLEL_GROUP[name] = dist.group.WORLD
             _DistributedContext.PARALLEL_RANK[name] = rank()
@@ -133,7 +139,7 @@ def create_parallel_group(parallel_config, timeout: Optional[timedelta] = None):
             continue
         groups = []
         for inst in all_pg:
-            for ranks in inst[name]:
+            for ranks in inst[dim_name]:
                 g = dist.new_group(ranks, timeout=timeout) if timeout else dist.new_group(ranks)
                 groups.append((g, ranks))
                 if rank() in ranks:
@@ -145,6 +151,7 @@ def create_parallel_group(parallel_config, timeout: Optional[timedelta] = None):
 
 def destroy_parallel_group():
     _DistributedContext.PARALLEL_CONFIG = None
+    _DistributedContext.PARALLEL_CONFIGS = {}
     _DistributedContext.PARALLEL_GROUP = {}
     _DistributedContext.PARALLEL_GROUPS_AND_RANKS = {}
     _DistributedContext.PARALLEL_RANK = {}
@@ -152,29 +159,59 @@ def destroy_parallel_group():
     destroy_sequence_parallel_group()
 
 
+class ParallelGroupContextManager:
+    """Named parallel groups per model (ATorch ``ParallelGroupContextManager``,
+    reference distributed/distributed.py:48): inside ``with
+    ParallelGroupContextManager("actor"):`` every group this module creates or
+    looks up is namespaced ``actor`` + name, so e.g. an RLHF actor (TP x DP)
+    and critic (pure DP) keep independent parallel layouts in one job."""
+
+    def __init__(self, name: str = ""):
+        self.name = name
+        self.old = ""
+
+    def __enter__(self):
+        self.old = _DistributedContext.PG_NAME_PREFIX
+        _DistributedContext.PG_NAME_PREFIX = self.name
+        return self
+
+    def __exit__(self, *exc):
+        _DistributedContext.PG_NAME_PREFIX = self.old
+        return False
+
+
+def _pn(name: str) -> str:
+    return _DistributedContext.PG_NAME_PREFIX + name
+
+
 def parallel_config():
-    return _DistributedContext.PARALLEL_CONFIG
+    return _DistributedContext.PARALLEL_CONFIGS.get(_DistributedContext.PG_NAME_PREFIX)
+
+
+def parallel_groups_and_ranks_all(name: str):
+    """[(group, ranks)] of every group of parallel dimension ``name``."""
+    return _DistributedContext.PARALLEL_GROUPS_AND_RANKS.get(_pn(name), [])
 
 
 def parallel_group(name: str):
-    return _DistributedContext.PARALLEL_GROUP.get(name)
+    return _DistributedContext.PARALLEL_GROUP.get(_pn(name))
 
 
 def parallel_group_and_ranks(name: str):
-    if name not in _DistributedContext.PARALLEL_GROUP:
+    if _pn(name) not in _DistributedContext.PARALLEL_GROUP:
         return None, None
-    for g, ranks in _DistributedContext.PARALLEL_GROUPS_AND_RANKS.get(name, []):
+    for g, ranks in _DistributedContext.PARALLEL_GROUPS_AND_RANKS.get(_pn(name), []):
         if rank() in ranks:
             return g, ranks
     return None, None
 
 
 def parallel_rank(name: str) -> Optional[int]:
-    return _DistributedContext.PARALLEL_RANK.get(name)
+    return _DistributedContext.PARALLEL_RANK.get(_pn(name))
 
 
 def parallel_group_size(name: str) -> Optional[int]:
-    return _DistributedContext.PARALLEL_GROUP_SIZE.get(name)
+    return _DistributedContext.PARALLEL_GROUP_SIZE.get(_pn(name))
 
 
 def parallel_instance_num() -> int:

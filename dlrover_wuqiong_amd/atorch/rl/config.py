@@ -36,3 +36,5 @@ class PPOConfig:
     actor_lr: float = 1e-5
     critic_lr: float = 1e-5
     seed: int = 0
+    # Safe-RLHF style: reward - cost_coef * cost when the engine has a cost model
+    cost_coef: float = 1.0

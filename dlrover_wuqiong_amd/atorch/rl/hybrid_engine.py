@@ -19,7 +19,12 @@ optional vLLM backend):
     per layer.  Sampling stays outside the graph.
 
 Works with ``models.llama.Llama`` (dense FFN for graph capture; MoE runs
-eagerly).  Parity: ATorch ``atorch/rl/ds_hybrid_engine/hybrid_engine.py``
+eagerly), including tensor-parallel actors (each rank caches its own KV
+heads, the TP layers do their own RCCL collectives, the vocab-parallel LM
+head's logits are all-gathered before sampling; decoded eagerly: no graph
+around collectives) and sequence-parallel actors (weights are replicated
+over the SP group, so generation runs with SP switched off and every SP rank
+produces the same rollout).  Parity: ATorch ``atorch/rl/ds_hybrid_engine/hybrid_engine.py``
 (generate with gathered ZeRO-3 params, inference containers, KV cache) and
 ``rl/inference_backend/vllm_backend.py``.
 """
@@ -83,12 +88,14 @@ class HybridEngine:
         self.llama = find_llama(actor)
         if self.llama is None:
             raise TypeError("HybridEngine drives models.llama.Llama actors")
-        if getattr(self.llama, "tp_group", None) is not None or getattr(self.llama, "sp_group", None) is not None:
-            raise NotImplementedError("HybridEngine: tensor / sequence parallel actors generate via sample()")
+        from ...models.llama import _ws
+
+        self.tp_group = getattr(self.llama, "tp_group", None)
+        self.tp = _ws(self.tp_group)
         cfg = self.llama.cfg
         self.cfg = cfg
         self.max_batch, self.max_len = max_batch, max_len
-        self.use_graph = use_graph and cfg.num_experts == 0
+        self.use_graph = use_graph and cfg.num_experts == 0 and self.tp == 1
         self.cache: Optional[KVCache] = None
         self._graph = None
         self._graph_key = None
@@ -100,8 +107,9 @@ class HybridEngine:
         c = self.cache
         if c is None or c.k.shape[1] != B or c.k.device != device or c.k.dtype != dtype:
             cfg = self.cfg
-            self.cache = KVCache(cfg.num_hidden_layers, B, self.max_len, cfg.num_key_value_heads, cfg.head_dim,
-                                 device, dtype)
+            # this rank's KV heads (all of them without tensor parallelism)
+            self.cache = KVCache(cfg.num_hidden_layers, B, self.max_len, cfg.num_key_value_heads // self.tp,
+                                 cfg.head_dim, device, dtype)
             self._graph = None
             logger.info(f"hybrid engine: KV cache {self.cache.nbytes / 2**30:.2f} GiB "
                         f"({B} x {self.max_len} tokens)")
@@ -145,6 +153,13 @@ class HybridEngine:
         x = m.norm.add_forward(x, r)[0]
         x = x[:, -1]
         logits = F.linear(x, m.embed_tokens.weight) if m.lm_head is None else m.lm_head(x)
+        if self.tp > 1:
+            # vocab-parallel head: every rank samples from the full vocabulary
+            import torch.distributed as dist
+
+            parts = [torch.empty_like(logits) for _ in range(self.tp)]
+            dist.all_gather(parts, logits.contiguous(), group=self.tp_group)
+            logits = torch.cat(parts, -1)[:, :cfg.vocab_size]
         if prefill:
             self.cache.lens.fill_(S)
         else:
@@ -190,12 +205,20 @@ class HybridEngine:
         was_training = self.actor.training
         self.actor.eval()
         out = [prompts]
+        sp_saved = getattr(self.llama, "sp_group", None)
+        if sp_saved is not None:
+            self.llama.set_sp(1, 0, None)  # replicated weights: decode without the SP all-to-alls
         try:
             with gathered_params(self.actor):
                 self._graph = None
                 logits = self.prefill(prompts)
                 for t in range(max_new_tokens):
                     nxt = _sample(logits.float(), temperature, top_k, generator)
+                    if self.tp > 1:
+                        # one sample per TP group: the ranks decode the same sequence
+                        import torch.distributed as dist
+
+                        dist.broadcast(nxt, dist.get_global_rank(self.tp_group, 0), group=self.tp_group)
                     out.append(nxt)
                     if t == max_new_tokens - 1:
                         break
@@ -209,6 +232,10 @@ class HybridEngine:
                 # captured against this call's weights / cache: never replayed later
                 self._graph = None
         finally:
+            if sp_saved is not None:
+                import torch.distributed as dist
+
+                self.llama.set_sp(dist.get_world_size(sp_saved), dist.get_rank(sp_saved), sp_saved)
             self.actor.train(was_training)
         return torch.cat(out, 1)
 

@@ -9,6 +9,8 @@ The file layout follows ATorch's so its example configs load unchanged:
       critic:     {...}          # an LM trunk gets a scalar value head (ValueModel)
       ref_model:  {model_cls, model_path, model_params, inference_strategy}
       reward_model: {...}        # LM / value trunk -> score of the last token
+      cost_model: {...}          # optional (Safe-RLHF): score subtracted from the reward
+      actor_critic_ref: {...}    # optional: ONE model for actor + critic (shared trunk) + frozen ref
     method:   {PPOConfig: {ppo_epoch, init_kl_coef, gamma, lam, cliprange, cliprange_value, vf_coef, ...}}
     train:    {seq_length, batch_size, epoch, num_rollouts, max_grad_norm, checkpoint_dir, ...}
     generation: {batch_size, gen_kwargs, gen_experience_kwargs: {max_new_tokens, temperature, top_k, ...}}
@@ -39,7 +41,7 @@ from typing import Any, Dict, List, Optional
 import torch
 import torch.nn as nn
 
-TRAINABLE_ROLES = ("actor", "critic")
+TRAINABLE_ROLES = ("actor", "critic", "actor_critic_ref")
 
 
 def is_trainable_model(role: str) -> bool:
@@ -360,36 +362,53 @@ def _strategy(s) -> Optional[list]:
 
 
 def build_engine(config: AtorchRLConfig, device: Optional[torch.device] = None, reward_fn=None):
-    """ModelEngine for the config's four roles.  ``reward_fn`` (ids -> [B])
-    replaces a configured reward model (rule-based rewards)."""
+    """ModelEngine for the config's roles.  ``reward_fn`` (ids -> [B])
+    replaces a configured reward model (rule-based rewards).  Every role's
+    ``train_strategy`` (trainable) / ``inference_strategy`` (frozen) is
+    applied under its own parallel-group namespace."""
     from .engine import ModelEngine, ValueModel
 
     mm = config.model.model
+    shared = "actor_critic_ref" in mm
     models = {}
-    for role in ("actor", "critic", "ref_model", "reward_model"):
+    roles = ("actor_critic_ref",) if shared else ("actor", "critic")
+    for role in roles + ("ref_model", "reward_model", "cost_model"):
         if role == "reward_model" and reward_fn is not None:
             models[role] = reward_fn
             continue
         if role not in mm:
             if role == "ref_model":
-                models[role] = build_role_model(mm["actor"])
-                models[role].load_state_dict(models["actor"].state_dict())
+                src = models["actor_critic_ref" if shared else "actor"]
+                models[role] = build_role_model(mm["actor_critic_ref" if shared else "actor"])
+                models[role].load_state_dict(src.state_dict())
+                continue
+            if role == "cost_model":
                 continue
             raise ValueError(f"config.model has no {role!r} entry")
         m = build_role_model(mm[role])
         if role == "critic" and not isinstance(m, ValueModel):
             m = ValueModel(m, _out_width(m))
-        if role == "reward_model":
+        if role in ("reward_model", "cost_model"):
             m = LastTokenScorer(m)
         models[role] = m
     if device is not None:
         for role, m in models.items():
             if isinstance(m, nn.Module):
                 m.to(device)
-    optim = {r: (mm[r].optimizer.resolve(), dict(mm[r].optimizer.kwargs)) for r in TRAINABLE_ROLES}
-    strategies = {r: s for r in TRAINABLE_ROLES if (s := _strategy(mm[r].train_strategy)) is not None}
-    return ModelEngine(models["actor"], models["critic"], models["ref_model"], models["reward_model"],
-                       strategies=strategies or None, role_optimizers=optim)
+    if shared:
+        models["actor"] = models.pop("actor_critic_ref")
+        mm = dict(mm)
+        mm["actor"] = mm["critic"] = mm["actor_critic_ref"]
+    optim = {r: (mm[r].optimizer.resolve(), dict(mm[r].optimizer.kwargs)) for r in ("actor", "critic")}
+    strategies = {r: s for r in ("actor", "critic") if (s := _strategy(mm[r].train_strategy)) is not None}
+    for r in ("ref_model", "reward_model", "cost_model"):
+        if r in config.model.model and (s := _strategy(config.model.model[r].inference_strategy)) is not None:
+            strategies[r] = s
+    if shared:
+        strategies.pop("critic", None)
+    return ModelEngine(models["actor"], models.get("critic"), models["ref_model"], models["reward_model"],
+                       strategies=strategies or None, role_optimizers=optim, cost_model=models.get("cost_model"),
+                       shared_actor_critic=shared, value_width=_out_width(models["actor"]) if shared else None)
 
 
 class PromptDataset(torch.utils.data.Dataset):

@@ -158,8 +158,7 @@ class PPOTrainer(RLTrainer):
             from .hybrid_engine import HybridEngine, find_llama
 
             llama = find_llama(self.engine.actor)
-            if llama is None or getattr(llama, "tp_group", None) is not None or \
-                    getattr(llama, "sp_group", None) is not None:
+            if llama is None:  # not a Llama-family actor: full-forward sampling
                 self.config.use_hybrid_engine = False
                 return None
             hy = self._hy = HybridEngine(self.engine.actor, need[0], need[1])
@@ -186,6 +185,10 @@ class PPOTrainer(RLTrainer):
         _, ref_logprobs, _ = self._response_stats(e.ref_model, seq, P)
         values = e.critic(seq)[:, P - 1:-1].float()
         scores = e.reward_model(seq).float()
+        if e.cost_model is not None:
+            cost = e.cost_model(seq).float()
+            self._cost = float(cost.mean())
+            scores = scores - c.cost_coef * cost
         rewards, mean_kl = kl_penalised_rewards(logprobs, ref_logprobs, scores, mask, self.kl_ctl.value)
         adv, ret = gae_advantages_and_returns(values, rewards, mask, c.gamma, c.lam, c.whiten_advantages)
         self.buffer.push(Experience(seq, logprobs, values, adv, ret, mask, scores))
@@ -209,8 +212,8 @@ class PPOTrainer(RLTrainer):
                 e.critic_optimizer.zero_grad(set_to_none=True)
                 loss.backward()
                 if c.max_grad_norm:
-                    torch.nn.utils.clip_grad_norm_(e.actor.parameters(), c.max_grad_norm)
-                    torch.nn.utils.clip_grad_norm_(e.critic.parameters(), c.max_grad_norm)
+                    torch.nn.utils.clip_grad_norm_(e.trainable_parameters("actor"), c.max_grad_norm)
+                    torch.nn.utils.clip_grad_norm_(e.trainable_parameters("critic"), c.max_grad_norm)
                 e.actor_optimizer.step()
                 e.critic_optimizer.step()
                 for k, v in st.items():

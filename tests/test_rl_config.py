@@ -193,3 +193,45 @@ def test_atorch_compat_import_paths():
     assert ln(x).shape == x.shape
     c, p = CUDAQuantizer().quantize(torch.randn(8000))
     assert c.dtype == torch.int8 and p.shape[1] == 2
+
+
+def test_actor_critic_ref_cost_model_and_role_strategies(tmp_path):
+    """One ``actor_critic_ref`` model (critic = value head on the actor's
+    trunk, frozen ref snapshot), a cost model subtracted from the reward,
+    and per-role strategies (a frozen role transformed by its
+    inference_strategy) -- reference model_engine.py:94-188,463-481."""
+    import torch.nn as nn
+
+    from dlrover_wuqiong_amd.atorch.rl.config import PPOConfig
+    from dlrover_wuqiong_amd.atorch.rl.engine import SharedCritic
+    from dlrover_wuqiong_amd.atorch.rl.rl_config import AtorchRLConfig, build_engine
+    from dlrover_wuqiong_amd.atorch.rl.trainer import PPOTrainer
+
+    role = {"model_cls": "dlrover_wuqiong_amd.models.llama.Llama", "model_params": {"config": {
+        "vocab_size": 64, "hidden_size": 32, "intermediate_size": 64, "num_hidden_layers": 1,
+        "num_attention_heads": 2, "num_key_value_heads": 1, "max_position_embeddings": 64}}}
+    cfg = {"model": {"actor_critic_ref": dict(role, optimizer={"name": "AdamW", "kwargs": {"lr": 1e-3}}),
+                     "cost_model": dict(role, inference_strategy=["half"])},
+           "train": {"batch_size": 4}, "method": {"PPOConfig": {"ppo_epoch": 1}}}
+    c = AtorchRLConfig.from_dict(cfg)
+    eng = build_engine(c, reward_fn=lambda ids: (ids[:, -3:] % 2).float().mean(-1))
+    assert isinstance(eng.critic, SharedCritic) and eng.actor_critic_ref is not None
+    # the critic's optimizer owns only the value head; the trunk is the actor's
+    head = {id(p) for p in eng.critic.v_head.parameters()}
+    assert {id(p) for g in eng.critic_optimizer.param_groups for p in g["params"]} == head
+    trunk = {id(p) for g in eng.actor_optimizer.param_groups for p in g["params"]}
+    assert not (trunk & head) and len(trunk) == len(list(eng.actor.parameters()))
+    assert not any(p.requires_grad for p in eng.ref_model.parameters())
+    assert next(eng.cost_model.parameters()).dtype == torch.bfloat16  # its inference strategy ran
+    assert isinstance(eng.actor_critic_ref, nn.Module)
+
+    torch.manual_seed(0)
+    prompts = torch.randint(1, 64, (4, 5))
+    tr = PPOTrainer(eng, [prompts[i] for i in range(4)], PPOConfig(max_new_tokens=3, rollout_batch_size=4,
+                                                                   mini_batch_size=2, ppo_epochs=1, cost_coef=0.5))
+    before = [p.detach().clone() for p in eng.actor.parameters()]
+    tr.make_experience(prompts)
+    assert hasattr(tr, "_cost")
+    stats = tr.rl_training()
+    assert all(v == v for v in stats.values())
+    assert any(not torch.equal(a, b) for a, b in zip(before, eng.actor.parameters()))
