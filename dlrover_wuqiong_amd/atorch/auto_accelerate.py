@@ -256,8 +256,19 @@ def _apply_tensor_parallel(ctx, cfg):
         return
     mesh = DeviceMesh("cuda" if torch.cuda.is_available() else "cpu", ranks, mesh_dim_names=("tensor",))
     plan = (cfg or {}).get("plan") if isinstance(cfg, dict) else None
+    heads = {}
+    if plan is None and not (isinstance(cfg, dict) and cfg.get("planner") == "names"):
+        # structural plan (torch.fx): Megatron column -> row blocks whatever
+        # the layers are called; the name table only as a fallback
+        from .tp_planner import auto_tp_plan
+
+        plan = auto_tp_plan(ctx["model"], heads) or None
     plan = plan or _tp_plan_for(ctx["model"])
     parallelize_module(ctx["model"], mesh, plan)
+    if heads:
+        from .tp_planner import shrink_head_attributes
+
+        shrink_head_attributes(ctx["model"], heads, len(ranks))
     _fix_attention_heads(ctx["model"], len(ranks))
     ctx["tp_mesh"] = mesh
     logger.info(f"tensor_parallel: {len(plan)} linear layers sharded over {len(ranks)} ranks")
