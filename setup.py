@@ -23,6 +23,7 @@ setup(
         "dwamd-run = dlrover_wuqiong_amd.trainer.run:main",
         "dwamd-master = dlrover_wuqiong_amd.master.master:main",
         "dwamd-brain = dlrover_wuqiong_amd.brain.service:main",
+        "dwamd-brain-k8s-monitor = dlrover_wuqiong_amd.brain.k8s_monitor:main",
         "dwamd-operator = dlrover_wuqiong_amd.platform.k8s:main",
     ]},
 )
