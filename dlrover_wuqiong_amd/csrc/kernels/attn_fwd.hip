@@ -233,11 +233,14 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));  // the row's max above its offset
       // move the offset of the rows that outgrew it, and seed it from the
       // first visible scores of a row (they may sit far below 0); O and l follow
-      const bool shift = (mx > RESCALE_T) || (!seeded && mx > -INFINITY);
+      const bool fresh = !seeded && mx > -INFINITY;
+      const bool shift = (mx > RESCALE_T) || fresh;
       seeded = seeded || (mx > -INFINITY);
       if (__any(shift)) {
         const float d = shift ? mx : 0.f;
-        const float alpha = __builtin_amdgcn_exp2f(-d);
+        // a fresh row has l = O = 0; its seed may lie far below 0 (ALiBi over
+        // a long distance) where exp2(-d) overflows and 0 * inf would be NaN
+        const float alpha = fresh ? 1.f : __builtin_amdgcn_exp2f(-d);
         m_i += d;
         l_i *= alpha;
 #pragma unroll
