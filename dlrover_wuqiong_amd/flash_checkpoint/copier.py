@@ -365,6 +365,13 @@ class GpuCopier:
         self.staging_mode = os.environ.get("DWAMD_STAGING", "auto")  # auto | full | ring
         self.ring_slots = max(2, int(os.environ.get("DWAMD_RING_SLOTS", "4")))
         self.ring_chunk = max(1 << 20, int(os.environ.get("DWAMD_RING_CHUNK_MB", "1024")) << 20)
+        # HBM the ring may use in total: the part of the slice that fits in it
+        # leaves the live tensors at HBM speed, only the rest drains at PCIe
+        # speed before the next optimizer step (the fence).  0 = auto: in
+        # ``auto`` staging the free HBM minus the reserve, in forced ``ring``
+        # mode K x C
+        self.ring_hbm = int(float(os.environ.get("DWAMD_RING_HBM_GB", "0")) * (1 << 30))
+        self._ring_auto = 0
         self._ring: Optional[torch.Tensor] = None
         self._ring_free: List[torch.cuda.Event] = []
         self._ring_decision: Optional[Tuple[int, bool]] = None
@@ -670,15 +677,28 @@ class GpuCopier:
                 free, _total = torch.cuda.mem_get_info(self.device)
                 have = sum(t.numel() for t in self._stagings if t is not None)
                 ring = free + have < n + self.staging_reserve
+                self._ring_auto = max(0, free + have - self.staging_reserve)
             except Exception:
                 ring = False
         self._ring_decision = (n, ring)
         if ring:
             self.wait()
             self._stagings = [None, None]  # give full-size buffers back
+            K, C = self._ring_shape(n)
             logger.info(f"checkpoint staging: {n / 2**30:.1f} GiB slice does not fit in HBM next to the model; "
-                        f"bounded ring of {self.ring_slots} x {self.ring_chunk >> 20} MiB")
+                        f"bounded ring of {K} x {C >> 20} MiB")
         return ring
+
+    def _ring_shape(self, n: int) -> Tuple[int, int]:
+        """(slots K, chunk bytes C) of the ring for an n-byte slice: at least
+        DWAMD_RING_SLOTS x DWAMD_RING_CHUNK_MB, grown to the HBM budget (never
+        beyond the slice)."""
+        K, C = self.ring_slots, self.ring_chunk
+        C = min(C, max(16, (n + K - 1) // K + 15 & ~15))  # tiny slices: no oversized ring
+        budget = self.ring_hbm or (self._ring_auto if self.staging_mode == "auto" else 0)
+        if budget > K * C:
+            K = max(K, min(budget, n) // C)
+        return K, C
 
     @property
     def staging_hbm_bytes(self) -> int:
@@ -711,8 +731,7 @@ class GpuCopier:
         n = hi - lo
         self.wait()  # one ring: the previous pipeline must have drained
         self.fence()
-        K, C = self.ring_slots, self.ring_chunk
-        C = min(C, max(16, (n + K - 1) // K + 15 & ~15))  # tiny slices: no oversized ring
+        K, C = self._ring_shape(n)
         if self._ring is None or self._ring.numel() < K * C:
             self._ring = None
             self._ring = torch.empty(K * C, dtype=torch.uint8, device=self.device)

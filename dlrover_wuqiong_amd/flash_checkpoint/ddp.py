@@ -46,6 +46,12 @@ class DdpCheckpointer(Checkpointer):
             return self._engine.save_to_storage(step, sd, paths)
         raise ValueError(f"unsupported storage type {storage_type}")
 
+    def prepare(self, state_dict) -> bool:
+        """Set up the shm slots for ``state_dict`` in the background (see
+        ``CheckpointEngine.prepare_memory``), e.g. right after the first
+        optimizer step, so the first memory save flushes at full speed."""
+        return self._engine.prepare_memory({CheckpointConstant.MODEL_STATES_NAME: state_dict})
+
     def load_checkpoint(self, resume_path="", target=None):
         """Returns the state dict (from memory if possible, else storage).
 

@@ -425,6 +425,23 @@ class CheckpointEngine(ABC):
         self._prechecked = not skip
         return skip
 
+    def prepare_memory(self, state_dict: Dict) -> bool:
+        """Start the one-time shm set-up for ``state_dict`` now, in the
+        background: create the segment and prefault + hipHostRegister this
+        rank's slot slices (~15 GB/s of host page zeroing: a 124 GB TP-shard
+        checkpoint needs ~16 s for its two slots).  Call it once the model and
+        the optimizer state exist -- it then overlaps the first training steps
+        instead of delaying the first save's flush.  Collective for replicated
+        engines (same call on every local rank).  Returns False for ranks that
+        never save (data-parallel replicas of a shard)."""
+        if not self._replicated and self._local_rank != self.local_shard_id:
+            return False
+        layout = self._plan(state_dict)
+        if layout.total_bytes <= 0:
+            return False
+        self._ensure_shm(layout.total_bytes)
+        return True
+
     def _save_state_dict_to_memory(self, state_dict: Dict, conf: CheckpointConfig) -> bool:
         if getattr(self, "_prechecked", False):
             self._prechecked = False
@@ -508,7 +525,8 @@ class CheckpointEngine(ABC):
             marks.append(("slot", time.perf_counter()))
         if slot < 0:
             logger.info(f"rank {self._rank} skips the memory checkpoint of step {conf.step}: "
-                        "the agent is persisting the in-memory checkpoints")
+                        "its shm slots are busy (the agent persisting them, a replica transfer, or the "
+                        "previous flush)")
             return False
         if self._is_shard_owner:
             self._held_slots.add(slot)

@@ -12,8 +12,10 @@ training peak + 115 GiB staging), ``--staging ring`` forces the bounded
 staging ring (``copier._save_slice_ring``: K x C bytes of HBM, the next
 optimizer step fenced on the ring) used when it does not.
 
-Reports: step time, memory-save pause, the fenced step after a save, time to
-durable (all bytes in shm), HBM used for staging, peak HBM, and a verified
+Reports: step time, the training stall per save (the save call plus the
+fence the next optimizer step waits on while the ring drains), time to
+durable (all bytes in shm), the one-time shm set-up overlapped with training
+by ``Checkpointer.prepare`` (and the step time while it runs), HBM used for staging, peak HBM, and a verified
 in-place restore.  Synthetic tokens, random-init weights, one GPU.
 """
 import argparse
@@ -33,13 +35,19 @@ def main():
     p.add_argument("--model", default="llama3-70b-tp8-shard")
     p.add_argument("--seq", type=int, default=4096)
     p.add_argument("--micro-batch", type=int, default=1)
-    p.add_argument("--steps", type=int, default=9)
-    p.add_argument("--ckpt-interval", type=int, default=3)
+    p.add_argument("--steps", type=int, default=21)
+    p.add_argument("--ckpt-interval", type=int, default=10)
     p.add_argument("--ckpt-dir", default="/tmp/dwamd_tp_shard_ckpt")
     p.add_argument("--staging", choices=["auto", "full", "ring"], default="auto",
                    help="auto: full-size HBM staging when it fits next to the model, else the bounded ring")
+    p.add_argument("--no-prepare", dest="prepare", action="store_false",
+                   help="skip Checkpointer.prepare(): the first save creates and pins the shm slots itself")
+    p.add_argument("--ring-hbm-gb", type=float, default=0.0,
+                   help="HBM the ring may use (DWAMD_RING_HBM_GB; 0 = 4 x 1 GiB when forced, free HBM in auto)")
     a = p.parse_args()
     os.environ["DWAMD_STAGING"] = a.staging
+    if a.ring_hbm_gb:
+        os.environ["DWAMD_RING_HBM_GB"] = str(a.ring_hbm_gb)
     os.environ.setdefault("DWAMD_SHM_PREFIX", f"tpring{os.getpid()}")
     cuda = torch.cuda.is_available()
     dev = torch.device("cuda", 0) if cuda else torch.device("cpu")
@@ -83,6 +91,22 @@ def main():
     sync()
     gb = 1 << 30
     mem_train = torch.cuda.max_memory_allocated() / gb if cuda else 0
+    # one-time segment set-up (create + prefault + pin both slots, ~16 s for
+    # 2 x 124 GB of host pages) started as soon as the optimizer state exists;
+    # training keeps stepping while it runs (``--no-prepare``: the first save
+    # pays it, the round-2 behaviour)
+    prep_steps, prep_wall = [], 0.0
+    if a.prepare:
+        t0 = time.perf_counter()
+        ck.prepare(state())
+        i = 0
+        while ck.engine._shm_prep is not None and not ck.engine._shm_prep.done():
+            t1 = time.perf_counter()
+            step(i)
+            sync()
+            prep_steps.append(time.perf_counter() - t1)
+            i += 1
+        prep_wall = time.perf_counter() - t0
     t0 = time.perf_counter()
     ck.save_checkpoint(0, state(), storage_type=StorageType.MEMORY)
     sync()
@@ -90,9 +114,6 @@ def main():
     ck.wait_latest_checkpoint()
     first_durable = time.perf_counter() - t0
     cp = ck.engine._copier
-    # one-time segment set-up: the other slot's prefault + registration runs
-    # in the background (in production it overlaps the first minutes of
-    # training); the loop below measures the steady state
     t0 = time.perf_counter()
     if ck.engine._shm_prep is not None:
         ck.engine._shm_prep.result()
@@ -100,6 +121,7 @@ def main():
     print(f"first save {first:.3f} s (durable {first_durable:.2f} s, rest of the segment set-up {prep_rest:.1f} s), "
           f"mode={getattr(cp, 'last_snapshot_mode', '')}", file=sys.stderr, flush=True)
     steps, after_save, pauses, durables, losses = [], [], [], [], []
+    skipped = 0
     saved_next = False
     for i in range(a.steps):
         t0 = time.perf_counter()
@@ -110,10 +132,13 @@ def main():
         saved_next = False
         if i % a.ckpt_interval == 0:
             t0 = time.perf_counter()
-            ck.save_checkpoint(i + 1, state(), storage_type=StorageType.MEMORY)
+            ok_save = ck.save_checkpoint(i + 1, state(), storage_type=StorageType.MEMORY)
             sync()
-            pauses.append(time.perf_counter() - t0)
-            saved_next = True
+            if ok_save:
+                pauses.append(time.perf_counter() - t0)
+                saved_next = True
+            else:  # previous save still draining (interval < time to durable): not a pause
+                skipped += 1
     # time to durable of one more save (pause + ring drain to shm)
     ck.wait_latest_checkpoint()
     t0 = time.perf_counter()
@@ -139,8 +164,14 @@ def main():
     got = [float(t.float().sum()) for t in model.state_dict().values()]
     ok = got == want and float(opt.flat_state_buffers()[dev]["exp_avg"].sum()) == want_m
     med = statistics.median(steps)
+    fence = (statistics.mean(after_save) - med) if after_save else 0.0
+    # the ring's save call returns after enqueueing, but the next optimizer
+    # step waits until the ring drained the state over PCIe: the training
+    # stall of a save is the call plus that fence
+    stall = statistics.mean(pauses) + max(0.0, fence)
     print(json.dumps({
-        "metric": "tp-shard flash ckpt pause s (model resident + training)", "value": round(statistics.mean(pauses), 4),
+        "metric": "tp-shard flash ckpt training stall s per save (model resident + training)",
+        "value": round(stall, 4),
         "unit": "s", "higher_is_better": False, "n_gpus": 1, "dtype": "bf16 params, fp32 master/Adam",
         "data": "synthetic tokens, random-init weights",
         "config": {"model": a.model, "params": nparams, "seq_len": a.seq, "micro_batch": a.micro_batch,
@@ -149,12 +180,15 @@ def main():
         "ckpt_interval_steps": a.ckpt_interval,
         "staging_hbm_gb": round(staging / gb, 2), "hbm_training_peak_gb": round(mem_train, 1),
         "hbm_peak_gb": round(torch.cuda.max_memory_allocated() / gb, 1) if cuda else None,
-        "save_sec": [round(x, 4) for x in pauses], "first_save_sec": round(first, 3),
+        "save_call_sec": [round(x, 4) for x in pauses], "skipped_saves": skipped, "stall_incl_fence_sec": round(stall, 4),
+        "first_save_sec": round(first, 3), "prepared": a.prepare, "prepare_overlap_sec": round(prep_wall, 1),
+        "steps_during_prepare": len(prep_steps),
+        "step_ms_during_prepare": round(1000 * statistics.median(prep_steps), 1) if prep_steps else None,
         "first_save_durable_sec": round(first_durable, 2), "segment_setup_rest_sec": round(prep_rest, 1),
         "time_to_durable_sec": round(durable, 3),
         "train_step_ms": round(1000 * med, 1),
         "step_after_save_ms": [round(1000 * x, 1) for x in after_save],
-        "fence_cost_ms": round(1000 * (statistics.mean(after_save) - med), 1) if after_save else None,
+        "fence_cost_ms": round(1000 * fence, 1) if after_save else None,
         "tokens_per_s": round(a.micro_batch * a.seq / med, 1), "load_sec": round(load_s, 3),
         "load_verified": bool(ok), "losses": [round(x, 3) for x in losses]}), flush=True)
     ck.close()

@@ -48,6 +48,27 @@ def test_single_process_memory_roundtrip(tmp_path):
     ck.close()
 
 
+def test_prepare_sets_up_shm_before_first_save(tmp_path):
+    """Checkpointer.prepare creates the segment and pins / prefaults the
+    slots in the background; the first save then reuses it (no re-create)."""
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+
+    m = torch.nn.Linear(64, 64)
+    ck = DdpCheckpointer(str(tmp_path / "ck"))
+    sd = {"model": m.state_dict(), "step": 1}
+    assert ck.prepare(sd)
+    eng = ck.engine
+    assert eng._shm_prep is not None
+    eng._shm_prep.result(timeout=60)
+    ino, size = eng._shm_handler.shared_memory.ino, eng._shm_handler.payload_size
+    assert size > 64 * 64 * 4
+    assert ck.save_checkpoint(2, {"model": m.state_dict(), "step": 2}, storage_type=StorageType.MEMORY)
+    assert eng._shm_handler.shared_memory.ino == ino and eng._shm_handler.payload_size == size
+    assert ck.load_checkpoint()["step"] == 2
+    ck.close()
+
+
 def test_double_buffer_survives_torn_save(tmp_path):
     """A process dying mid-snapshot must leave the previous checkpoint intact."""
     from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType

@@ -172,17 +172,21 @@ def test_gpu_overlapped_snapshot_copies_forward_written_buffers_first(tmp_path, 
     ck.close()
 
 
-@pytest.mark.parametrize("stepped", [True, False])
-def test_gpu_staging_ring_snapshot(tmp_path, monkeypatch, stepped):
-    """DWAMD_STAGING=ring: the slice streams through 4 x 1 MiB of HBM.  The
-    next optimizer step is fenced on the ring; forward-written buffers are
-    copied before save returns; before any optimizer step (nothing known to
-    be step-only) the save blocks until the ring has drained."""
+@pytest.mark.parametrize("stepped,ring_mb", [(True, 0), (False, 0), (True, 8)])
+def test_gpu_staging_ring_snapshot(tmp_path, monkeypatch, stepped, ring_mb):
+    """DWAMD_STAGING=ring: the slice streams through 4 x 1 MiB of HBM (or
+    DWAMD_RING_HBM_GB worth of 1 MiB slots).  The next optimizer step is
+    fenced on the ring; forward-written buffers are copied before save
+    returns; before any optimizer step (nothing known to be step-only) the
+    save blocks until the ring has drained."""
     from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
     from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
 
     monkeypatch.setenv("DWAMD_STAGING", "ring")
     monkeypatch.setenv("DWAMD_RING_CHUNK_MB", "1")
+    if ring_mb:
+        monkeypatch.setenv("DWAMD_RING_HBM_GB", str(ring_mb / 1024))
+    ring_bytes = (ring_mb or 4) << 20
     torch.manual_seed(0)
     model = torch.nn.Sequential(torch.nn.Linear(256, 1024), torch.nn.BatchNorm1d(1024),
                                 torch.nn.Linear(1024, 512)).cuda()
@@ -203,7 +207,8 @@ def test_gpu_staging_ring_snapshot(tmp_path, monkeypatch, stepped):
         want_opt = [s["exp_avg"].clone() for s in opt.state.values()]
         assert ck.save_checkpoint(step, state(), storage_type=StorageType.MEMORY)
         cp = ck.engine._copier
-        assert cp.last_snapshot_mode == "ring" and cp.staging_hbm_bytes <= 4 * (1 << 20) + (1 << 20) * 2
+        assert cp.last_snapshot_mode == "ring" and cp.staging_hbm_bytes <= ring_bytes + (1 << 20) * 2
+        assert cp._ring.numel() <= ring_bytes and (cp._ring.numel() == ring_bytes or not stepped)
         train()  # forward writes BN stats; the step waits for the ring (fence)
         ck.wait_latest_checkpoint()
     torch.cuda.synchronize()
@@ -213,7 +218,7 @@ def test_gpu_staging_ring_snapshot(tmp_path, monkeypatch, stepped):
         assert torch.equal(v, want[k]), k
     for s, w in zip(opt.state.values(), want_opt):
         assert torch.equal(s["exp_avg"], w)
-    assert ck.engine._shm_handler.payload_size > 4 * (1 << 20)  # really more than the ring
+    assert ck.engine._shm_handler.payload_size > ring_bytes  # really more than the ring
     ck.close()
 
 

@@ -92,8 +92,13 @@ def _stress_worker(rank, world, port, root, prefix, q):
         rm.chunk = 256 << 10  # many small chunks: transfers overlap the saves that follow
         base = torch.arange(2_000_000, dtype=torch.float32) + 1000 * rank
         last = 16
+        saved = 0
         for step in range(1, last + 1):  # back-to-back saves while earlier ones replicate
-            ck.save_checkpoint(step, {"w": base + step, "step": step}, storage_type=StorageType.MEMORY)
+            # a save finding both slots busy (one pinned by an outgoing
+            # replica, the other still flushing) is skipped, on every rank
+            if ck.save_checkpoint(step, {"w": base + step, "step": step}, storage_type=StorageType.MEMORY):
+                saved = step
+        last = saved
         ck.wait_latest_checkpoint()
         rm.wait()
         dist.barrier()
@@ -104,7 +109,7 @@ def _stress_worker(rank, world, port, root, prefix, q):
         del hdr
         meta = restricted_loads(bytes(seg.buf[_HDR + n: _HDR + n + m]))
         w = tensors_from_payload(meta["tree"], seg.buf, _HDR)["model_states"]["w"].clone()
-        ok = s_step == last and torch.equal(w, torch.arange(2_000_000, dtype=torch.float32) + 1000 * peer + s_step)
+        ok = last > 0 and s_step == last and torch.equal(w, torch.arange(2_000_000, dtype=torch.float32) + 1000 * peer + s_step)
         del w
         seg.close()
         q.put((rank, bool(ok), rm.coalesced))
