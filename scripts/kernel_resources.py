@@ -1,6 +1,8 @@
 """Per-kernel register / scratch usage of a .hip file for gfx950
 (hipcc -Rpass-analysis=kernel-resource-usage), one line per kernel:
-    python scripts/kernel_resources.py dlrover_wuqiong_amd/csrc/kernels/attn_fwd.hip [filter]"""
+    python scripts/kernel_resources.py dlrover_wuqiong_amd/csrc/kernels/attn_fwd.hip [filter]
+extra compiler flags via KRES_FLAGS (e.g. "-mllvm -amdgpu-mfma-vgpr-form")."""
+import os
 import re
 import subprocess
 import sys
@@ -9,8 +11,9 @@ import sys
 def main():
     src = sys.argv[1]
     flt = sys.argv[2] if len(sys.argv) > 2 else ""
+    extra = os.environ.get("KRES_FLAGS", "").split()
     r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-c", src, "-o",
-                        "/tmp/_kres.o", "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True)
+                        "/tmp/_kres.o", "-Rpass-analysis=kernel-resource-usage"] + extra, capture_output=True, text=True)
     cur, rows = None, []
     for ln in r.stderr.splitlines():
         m = re.search(r"remark:\s+(Function Name|VGPRs|AGPRs|ScratchSize \[bytes/lane\]|VGPRs Spill|SGPRs Spill|"
