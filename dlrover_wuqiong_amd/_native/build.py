@@ -124,6 +124,11 @@ def _compile_hip(src):
         return obj
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
            "-mcode-object-version=5", "-munsafe-fp-atomics", "-ffp-contract=fast",
+           # MFMA accumulators in arch VGPRs: with a 512-register budget (one
+           # wave per SIMD allowed by the launch bounds) the default AGPR form
+           # costs v_accvgpr_read/write copies around every softmax
+           # (attention D=64: 176 extra VALU ops per 64-key tile)
+           "-mllvm", "-amdgpu-mfma-vgpr-form",
            "-Wno-unused-result", "-I", os.path.join(CSRC, "kernels"), "-c", src,
            "-o", obj + f".tmp{os.getpid()}"]
     _run(cmd)

@@ -265,14 +265,36 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
           s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(qa), as_bf(kf[kk]), s, 0, 0, 0);
           dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(da), as_bf(vb), dp, 0, 0, 0);
         }
+        if (!EXT) {
+          // P, then (diagonal / ragged tiles only) the mask, then dS: the
+          // empty volatile asm keeps the mask a scalar branch (need_mask is
+          // wave-uniform) instead of per-element selects or branches
+#pragma unroll
+          for (int i = 0; i < 16; ++i) s[i] = __builtin_amdgcn_exp2f(s[i]);
+          if (need_mask) {
+            __asm__ volatile("");
+            // register i holds query q0 + 4 hh + c, c = 32 qs + 8 (i >> 2) + (i & 3)
+            const int base = q0 + 4 * hh;
+            const int qlim = key < SK ? SQ - base : -1;  // c < qlim: a real query (and a real key)
+            const int kmin = key - co - base;            // c >= kmin: causal, the key is visible
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int c = 32 * qs + 8 * (i >> 2) + (i & 3);
+              const bool keep = (c < qlim) && (!CAUSAL || c >= kmin);
+              s[i] = keep ? s[i] : 0.f;
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < 16; ++i) dp[i] = s[i] * dp[i];  // dS (scale applied in the epilogue)
+        }
         // rows of register group g: queries 32 qs + 8 g + 4 hh + 0..3
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
+        for (int g = 0; g < 4 && EXT; ++g) {
           const int qi = 32 * qs + 8 * g + 4 * hh;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int i = 4 * g + j;
-            if (EXT) {
+            {
               const int q = q0 + qi + j;
               const bool vis = (q < SQ) && ext_visible(ex, CAUSAL, q, key, co, SK, pre);
               float add = (vis && ex.bias)
@@ -291,16 +313,7 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                 s[i] = p;
                 dp[i] = p * dp[i];
               }
-              continue;
             }
-            float p = __builtin_amdgcn_exp2f(s[i]);
-            if (need_mask) {
-              const int q = q0 + qi + j;
-              const bool keep = (q < SQ) & (key < SK) & (!CAUSAL | (key <= q + co));
-              p = keep ? p : 0.f;
-            }
-            s[i] = p;
-            dp[i] = p * dp[i];  // dS (scale applied in the epilogue)
           }
         }
         // dV^T += dO^T P ; dK^T += Q^T dS : 2 k-steps of 16 queries
@@ -554,9 +567,21 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
           s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(kf), as_bf(qf[kk]), s, 0, 0, 0);
           dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(vf), as_bf(dof[kk]), dp, 0, 0, 0);
         }
+        if (!EXT) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          if (EXT) {
+          for (int i = 0; i < 16; ++i) s[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], scale_log2, -lse2));
+          if (need_mask) {
+            __asm__ volatile("");  // a scalar branch: diagonal / ragged tiles only
+            const int rel = lim - k0 - 32 * sb - 4 * hh;  // register i's key offset must be < rel
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s[i] = ((i & 3) + 8 * (i >> 2)) < rel ? s[i] : 0.f;
+          }
+#pragma unroll
+          for (int i = 0; i < 16; ++i) s[i] = s[i] * (dp[i] - dl);  // dS^T (scale applied in the epilogue)
+        }
+#pragma unroll
+        for (int i = 0; i < 16 && EXT; ++i) {
+          {
             const int key = k0 + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hh;
             const bool vis = (q < SQ) && ext_visible(ex, CAUSAL, q, key, co, SK, pre);
             float add = (vis && brow) ? brow[key] * 1.4426950408889634f : 0.f;
@@ -566,14 +591,7 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
             if (ex.dropout)
               dpe = attn_keep(ex, bh, (long long)sr.q_off + q, (long long)sr.k_off + key) ? dpe * ex.inv_keep : 0.f;
             s[i] = p * (dpe - dl);
-            continue;
           }
-          float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], scale_log2, -lse2));
-          if (need_mask) {
-            const int key = k0 + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hh;
-            p = key < lim ? p : 0.f;
-          }
-          s[i] = p * (dp[i] - dl);  // dS^T (scale applied in the epilogue)
         }
         // dQ^T += K^T dS^T : 2 k-steps of 16 keys, K^T from transposed reads
 #pragma unroll

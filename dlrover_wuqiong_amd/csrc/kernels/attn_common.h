@@ -79,6 +79,21 @@ __device__ __forceinline__ u32x4 join_tr(const V& a, const V& b) {
   return (u32x4){x[0], x[1], y[0], y[1]};
 }
 
+// max over lanes i and i ^ 32 (a row split across the two wave halves):
+// v_permlane32_swap exchanges the halves in one VALU op, where __shfl_xor
+// goes through ds_bpermute (address math + an LDS round trip)
+__device__ __forceinline__ float half_max(float x) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+
+__device__ __forceinline__ float half_sum(float x) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+
 __device__ __forceinline__ unsigned int pack_s16(short a, short b) {
   return (unsigned int)(unsigned short)a | ((unsigned int)(unsigned short)b << 16);
 }

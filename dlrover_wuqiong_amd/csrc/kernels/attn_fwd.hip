@@ -189,14 +189,34 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
       // no subtraction
       f32x16 s[2];
 #pragma unroll
-      for (int sb = 0; sb < 2; ++sb) {
+      for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) s[sb][i] = -m_i;
+      // the two subtiles' chains interleaved: no MFMA waits on its predecessor
+      if constexpr (D == 64) {
+        // all 8 K fragments (32 VGPRs) in flight at once: one LDS latency per
+        // tile instead of one per MFMA
+        u32x4 kf[C::KK][2];
 #pragma unroll
-        for (int kk = 0; kk < C::KK; ++kk) {
-          const u32x4 kf = *(const u32x4*)(kl + img_off<D>(32 * sb + r, 2 * kk + hh));
-          s[sb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf), as_bf16x8(qf[kk]), s[sb], 0, 0, 0);
-        }
+        for (int kk = 0; kk < C::KK; ++kk)
+#pragma unroll
+          for (int sb = 0; sb < 2; ++sb) kf[kk][sb] = *(const u32x4*)(kl + img_off<D>(32 * sb + r, 2 * kk + hh));
+#pragma unroll
+        for (int kk = 0; kk < C::KK; ++kk)
+#pragma unroll
+          for (int sb = 0; sb < 2; ++sb)
+            s[sb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf[kk][sb]), as_bf16x8(qf[kk]), s[sb], 0, 0, 0);
+        // the machine scheduler would sink each read next to its MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * C::KK, 0);  // DS reads
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * C::KK, 0);  // then the MFMAs
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < C::KK; ++kk)
+#pragma unroll
+          for (int sb = 0; sb < 2; ++sb) {
+            const u32x4 kf = *(const u32x4*)(kl + img_off<D>(32 * sb + r, 2 * kk + hh));
+            s[sb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf), as_bf16x8(qf[kk]), s[sb], 0, 0, 0);
+          }
       }
 
       // ---- online softmax: lane = query q0 + r, its 32 keys in registers
@@ -215,22 +235,25 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
             s[sb][i] = vis ? s[sb][i] + add : -INFINITY;
           }
       } else if (need_mask) {
-        // keys < lim are visible to this lane's query (branch-free selects)
-        const int lim = CAUSAL ? min(SK, q + co + 1) : SK;
+        // diagonal / ragged-end tiles only (need_mask is wave-uniform): the
+        // empty volatile asm keeps this a scalar branch -- if-converted, the
+        // 64 compares + selects would run on every tile
+        __asm__ volatile("");
+        // keys < lim are visible to this lane's query; the register's key
+        // offset within the tile is a compile-time constant
+        const int rel = (CAUSAL ? min(SK, q + co + 1) : SK) - k0 - 4 * hh;
 #pragma unroll
         for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int key = k0 + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hh;
-            s[sb][i] = key < lim ? s[sb][i] : -INFINITY;
-          }
+          for (int i = 0; i < 16; ++i)
+            s[sb][i] = (32 * sb + (i & 3) + 8 * (i >> 2)) < rel ? s[sb][i] : -INFINITY;
       }
       float mx = -INFINITY;
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[sb][i]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));  // the row's max above its offset
+      mx = half_max(mx);  // the row's max above its offset
       // move the offset of the rows that outgrew it, and seed it from the
       // first visible scores of a row (they may sit far below 0); O and l follow
       const bool fresh = !seeded && mx > -INFINITY;
@@ -304,7 +327,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   }
 
   // ---- epilogue: O = O^T / l ; lse
-  const float l_tot = l_i + __shfl_xor(l_i, 32, 64);
+  const float l_tot = half_sum(l_i);
   const int q = q0 + r;
   if (q < SQ) {
     bf16_t* Oq = O + (int64_t)b * st.o_bs + (int64_t)h * D + (int64_t)(sr.q_off + q) * st.o_rs;
@@ -338,7 +361,7 @@ static void launch_fwd_v(const void* q, const void* k, const void* v, void* o, v
 template <int D>
 static void launch_fwd(const void* q, const void* k, const void* v, void* o, void* lse, int B, int S, int H, int HKV,
                        int causal, float scale_log2, const AttnStrides& st, const AttnVarlen& vl, hipStream_t s,
-                       const AttnExt* ext = nullptr) {
+                       const AttnExt* ext = nullptr, int variant = 0) {
   // D=64: 4 waves (128 queries per block, 184 VGPRs, two blocks per CU):
   // twice the blocks of the 8-wave form for a finer causal balance; measured
   // against 8 waves capped at 128 VGPRs (spills) / uncapped and 4 waves
@@ -349,6 +372,11 @@ static void launch_fwd(const void* q, const void* k, const void* v, void* o, voi
                   : launch_fwd_v<D, false, true, W, 1>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, *ext, s);
   }
   const AttnExt none = {};
+  // tuning A/B (flags): D=64 capped at 168 VGPRs for three 4-wave blocks per
+  // CU -- measured 8 % slower than the uncapped two (343 vs 371 TF/s, GPT2 shape)
+  if (D == 64 && variant == 1)
+    return causal ? launch_fwd_v<D, true, false, W, 3>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s)
+                  : launch_fwd_v<D, false, false, W, 3>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s);
   return causal ? launch_fwd_v<D, true, false, W, 1>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s)
                 : launch_fwd_v<D, false, false, W, 1>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s);
 }
@@ -364,8 +392,9 @@ extern "C" int dw_attn_fwd_strided(const void* q, const void* k, const void* v, 
   const float scale_log2 = softmax_scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
   const AttnVarlen vl = {nullptr, nullptr, 0, 0};
-  if (D == 128) launch_fwd<128>(q, k, v, o, lse, B, S, H, HKV, causal, scale_log2, st, vl, s);
-  else if (D == 64) launch_fwd<64>(q, k, v, o, lse, B, S, H, HKV, causal, scale_log2, st, vl, s);
+  // flags: kernel variant for tuning A/B runs (0 = the default choice)
+  if (D == 128) launch_fwd<128>(q, k, v, o, lse, B, S, H, HKV, causal, scale_log2, st, vl, s, nullptr, flags);
+  else if (D == 64) launch_fwd<64>(q, k, v, o, lse, B, S, H, HKV, causal, scale_log2, st, vl, s, nullptr, flags);
   else return (int)hipErrorInvalidValue;
   DW_LAUNCH_RET;
 }
