@@ -149,7 +149,8 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
   // dP, row-read per k-step) -- registers for 2 waves per SIMD.
   char* v_img = smem + 2 * C::BUF;
   for (int v = tid; v < C::BKB * C::NCH; v += 64 * C::WAVES) {
-    const int row = v / C::NCH, c = v % C::NCH;
+    int row, c;
+    stage_rc<D>(v, row, c);
     const int kv = kb0 + row;
     *(u32x4*)(v_img + img_off<D>(row, c)) =
         kv < SK ? *(const u32x4*)(Vb + (int64_t)kv * st.v_rs + c * 8) : (u32x4){0, 0, 0, 0};
@@ -192,7 +193,8 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
 #pragma unroll
     for (int i = 0; i < C::VPT; ++i) {
       const int v = tid + 64 * C::WAVES * i;
-      const int row = v / C::NCH, c = v % C::NCH;
+      int row, c;
+      stage_rc<D>(v, row, c);
       const int q = q0 + row;
       if (q < SQ) {
         q_st[i] = *(const u32x4*)(Qb + (int64_t)q * st.q_rs + c * 8);
@@ -217,7 +219,8 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
 #pragma unroll
     for (int i = 0; i < C::VPT; ++i) {
       const int v = tid + 64 * C::WAVES * i;
-      const int row = v / C::NCH, c = v % C::NCH;
+      int row, c;
+      stage_rc<D>(v, row, c);
       *(u32x4*)(ql + img_off<D>(row, c)) = q_st[i];
       *(u32x4*)(dl + img_off<D>(row, c)) = do_st[i];
     }
@@ -507,7 +510,8 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
 #pragma unroll
     for (int i = 0; i < C::VPT; ++i) {
       const int v = tid + 64 * C::WAVES * i;
-      const int row = v / C::NCH, c = v % C::NCH;
+      int row, c;
+      stage_rc<D>(v, row, c);
       const int key = t * C::BK + row;
       if (key < SK) {
         kst[i] = *(const u32x4*)(Kb + (int64_t)key * st.k_rs + c * 8);
@@ -524,7 +528,8 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
 #pragma unroll
     for (int i = 0; i < C::VPT; ++i) {
       const int v = tid + 64 * C::WAVES * i;
-      const int row = v / C::NCH, c = v % C::NCH;
+      int row, c;
+      stage_rc<D>(v, row, c);
       *(u32x4*)(kl + img_off<D>(row, c)) = kst[i];
       *(u32x4*)(vl + img_off<D>(row, c)) = vst[i];
     }

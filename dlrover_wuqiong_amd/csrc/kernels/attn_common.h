@@ -14,6 +14,20 @@ __device__ __forceinline__ int img_off(int row, int ch) {
   return (D * 16) * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
 }
 
+// (row, 16-byte chunk) that staged vector v (0 .. rows * D/8 - 1) carries in
+// a tile written through img_off: 8 consecutive lanes take 2 rows x 4 chunks
+// of one 8x32 subtile = 128 contiguous LDS bytes, so a ds_write_b128 lane
+// group (8 lanes) hits every bank once.  Row-major lanes (a row's chunks on
+// 8 consecutive lanes) put the row's two subtiles 512 B apart: 2-way
+// conflicts on every staging store, all the bank conflicts of these kernels.
+template <int D>
+__device__ __forceinline__ void stage_rc(int v, int& row, int& c) {
+  constexpr int CG = D / 32;  // 4-chunk groups per row
+  const int rest = v >> 3;
+  row = (rest / CG) * 2 + ((v >> 2) & 1);
+  c = (rest % CG) * 4 + (v & 3);
+}
+
 // Block coordinates of a 1-D launch over nx * ny * nz workgroups (x fastest).
 // Hardware hands consecutive workgroup ids to the 8 XCDs round-robin, and each
 // XCD has a private L2; the remap gives every XCD a contiguous chunk of the
