@@ -155,6 +155,9 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
     *(u32x4*)(v_img + img_off<D>(row, c)) =
         kv < SK ? *(const u32x4*)(Vb + (int64_t)kv * st.v_rs + c * 8) : (u32x4){0, 0, 0, 0};
   }
+  // D=64: this wave's V fragments (16 VGPRs) live in registers too
+  constexpr bool VREG = false;  // D=64 V fragments in registers measured 10 % slower (bwd 334 -> 300 TF/s)
+  u32x4 vr[VREG ? C::KK : 1];
   // K (only used for S here) prescaled by softmax_scale * log2(e)
   u32x4 kf[C::KK];
 #pragma unroll
@@ -187,7 +190,8 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
   const long long bh = vl.cu_q ? (long long)h : (long long)b * H + h;  // dropout hash row
   const float al2 = EXT ? ext_alibi2(ex, b, h) : 0.f;
   u32x4 q_st[C::VPT], do_st[C::VPT];
-  float lse_st = INFINITY, del_st = 0.f;
+  // row constants staged NEGATED: they are the initial accumulators of S' and dP'
+  float lse_st = -INFINITY, del_st = 0.f;
   auto issue = [&](int it) {
     const int q0 = q_lo + it * C::BQT;
 #pragma unroll
@@ -208,8 +212,8 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
       const int q = q0 + tid;
       const float l = q < SQ ? lse_b[q] : -INFINITY;
       // a row that saw no key (lse = -inf) contributes nothing: p = 2^-inf
-      lse_st = l > -INFINITY ? l * 1.4426950408889634f : INFINITY;
-      del_st = q < SQ ? del_b[q] : 0.f;
+      lse_st = l > -INFINITY ? -l * 1.4426950408889634f : -INFINITY;
+      del_st = q < SQ ? -del_b[q] : 0.f;
     }
   };
   auto write = [&](int buf) {
@@ -235,6 +239,10 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
     if (n_it > 1) issue(1);
   }
   __syncthreads();
+  if constexpr (VREG) {
+#pragma unroll
+    for (int kk = 0; kk < C::KK; ++kk) vr[kk] = *(const u32x4*)(v_img + img_off<D>(32 * wid + r, 2 * kk + hh));
+  }
 
   for (int it = 0; it < n_it; ++it) {
     const int q0 = q_lo + it * C::BQT;
@@ -256,15 +264,15 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
           const f32x4 d4 = *(const f32x4*)(stl + C::BQT + qi);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            s[4 * g + j] = -l4[j];
-            dp[4 * g + j] = -d4[j];
+            s[4 * g + j] = l4[j];
+            dp[4 * g + j] = d4[j];
           }
         }
 #pragma unroll
         for (int kk = 0; kk < C::KK; ++kk) {
           const u32x4 qa = *(const u32x4*)(ql + img_off<D>(32 * qs + r, 2 * kk + hh));
           const u32x4 da = *(const u32x4*)(dl + img_off<D>(32 * qs + r, 2 * kk + hh));
-          const u32x4 vb = *(const u32x4*)(v_img + img_off<D>(32 * wid + r, 2 * kk + hh));
+          const u32x4 vb = VREG ? vr[VREG ? kk : 0] : *(const u32x4*)(v_img + img_off<D>(32 * wid + r, 2 * kk + hh));
           s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(qa), as_bf(kf[kk]), s, 0, 0, 0);
           dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(da), as_bf(vb), dp, 0, 0, 0);
         }
@@ -272,8 +280,6 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
           // P, then (diagonal / ragged tiles only) the mask, then dS: the
           // empty volatile asm keeps the mask a scalar branch (need_mask is
           // wave-uniform) instead of per-element selects or branches
-#pragma unroll
-          for (int i = 0; i < 16; ++i) s[i] = __builtin_amdgcn_exp2f(s[i]);
           if (need_mask) {
             __asm__ volatile("");
             // register i holds query q0 + 4 hh + c, c = 32 qs + 8 (i >> 2) + (i & 3)
@@ -284,11 +290,14 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
             for (int i = 0; i < 16; ++i) {
               const int c = 32 * qs + 8 * (i >> 2) + (i & 3);
               const bool keep = (c < qlim) && (!CAUSAL || c >= kmin);
-              s[i] = keep ? s[i] : 0.f;
+              s[i] = keep ? s[i] : -INFINITY;  // p = 2^-inf = 0
             }
           }
 #pragma unroll
-          for (int i = 0; i < 16; ++i) dp[i] = s[i] * dp[i];  // dS (scale applied in the epilogue)
+          for (int i = 0; i < 16; ++i) {
+            s[i] = __builtin_amdgcn_exp2f(s[i]);
+            dp[i] = s[i] * dp[i];  // dS (scale applied in the epilogue)
+          }
         }
         // rows of register group g: queries 32 qs + 8 g + 4 hh + 0..3
 #pragma unroll
@@ -308,7 +317,7 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
               const float p = vis ? __builtin_amdgcn_exp2f(s[i] + add) : 0.f;
               if (ex.dropout) {
                 // dV takes the dropped probabilities; dS = P (Z dP / (1-p) - delta)
-                const float del = stl[C::BQT + qi + j];
+                const float del = -stl[C::BQT + qi + j];
                 const bool kp = attn_keep(ex, bh, (long long)sr.q_off + q, (long long)sr.k_off + key);
                 s[i] = kp ? p * ex.inv_keep : 0.f;
                 dp[i] = p * (kp ? (dp[i] + del) * ex.inv_keep - del : -del);
@@ -426,7 +435,10 @@ __global__ void gqa_reduce_kernel(const float* __restrict__ pk, const float* __r
 // gone at the price of recomputing S and dP here.
 template <int D>
 struct DqCfg {
-  static constexpr int WAVES = 8;
+  // D=64: 4 waves (128 queries): twice the blocks of the 8-wave form, two per
+  // CU -- the causal tail of a short sequence (GPT2: 4 query blocks of 256
+  // per head) left the 8-wave form at 200 us vs 123 for the dK/dV kernel
+  static constexpr int WAVES = D == 64 ? 4 : 8;
   static constexpr int BQ = 32 * WAVES;
   static constexpr int BK = 64;
   static constexpr int NCH = D / 8;
@@ -485,6 +497,7 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
   for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[dt][i] = 0.f;
+  constexpr bool DPI = D == 64 && !EXT;  // dP^T initialised with -delta
 
   int n_tiles = (SK + C::BK - 1) / C::BK;
   int t_begin = 0;
@@ -557,13 +570,13 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
       // one 32-key subtile at a time keeps S^T / dP^T at 32 registers
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb) {
-        // (row-constant accumulator init as in the dK/dV kernel costs this
-        // kernel 40+ spilled VGPRs at D=128: kept on the plain form)
+        // dP^T starts at -delta (row constant as the initial accumulator) at
+        // D=64; at D=128 that form cost this kernel 40+ spilled VGPRs
         f32x16 s, dp;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           s[i] = 0.f;
-          dp[i] = 0.f;
+          dp[i] = DPI ? -dl : 0.f;
         }
 #pragma unroll
         for (int kk = 0; kk < C::KK; ++kk) {
@@ -573,16 +586,17 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
           dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(vf), as_bf(dof[kk]), dp, 0, 0, 0);
         }
         if (!EXT) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) s[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], scale_log2, -lse2));
           if (need_mask) {
             __asm__ volatile("");  // a scalar branch: diagonal / ragged tiles only
             const int rel = lim - k0 - 32 * sb - 4 * hh;  // register i's key offset must be < rel
 #pragma unroll
-            for (int i = 0; i < 16; ++i) s[i] = ((i & 3) + 8 * (i >> 2)) < rel ? s[i] : 0.f;
+            for (int i = 0; i < 16; ++i) s[i] = ((i & 3) + 8 * (i >> 2)) < rel ? s[i] : -INFINITY;  // p = 0
           }
 #pragma unroll
-          for (int i = 0; i < 16; ++i) s[i] = s[i] * (dp[i] - dl);  // dS^T (scale applied in the epilogue)
+          for (int i = 0; i < 16; ++i) {
+            const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], scale_log2, -lse2));
+            s[i] = p * (DPI ? dp[i] : dp[i] - dl);  // dS^T (scale applied in the epilogue)
+          }
         }
 #pragma unroll
         for (int i = 0; i < 16 && EXT; ++i) {

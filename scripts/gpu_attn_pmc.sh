@@ -1,14 +1,15 @@
 #!/bin/bash
-# PMC counters of the flash-attention forward (two passes, counters per
-# pass within the SQ block limit), then per-kernel CSV summaries.
+# PMC counters of the flash-attention kernels (two passes, counters per pass
+# within the SQ block limit), fwd + bwd, one shape per argument group.
 set -u
-mkdir -p gpurun_out/pmc_attn
+OUT=${1:-gpurun_out/pmc_attn}
+mkdir -p $OUT
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-P1="SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES"
+P1="SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES"
 P2="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_VALU_TRANS_F32 SQ_WAVES SQ_ACTIVE_INST_ANY"
-timeout -s KILL 120 rocprofv3 --pmc $P1 --output-format csv -d gpurun_out/pmc_attn/p1 -o run -- \
-  python3 scripts/attn_prof_run.py --fwd 1,8192,32,8,128 8,1024,25,25,64 > gpurun_out/pmc_attn/p1.log 2>&1 || exit 1
-timeout -s KILL 120 rocprofv3 --pmc $P2 --output-format csv -d gpurun_out/pmc_attn/p2 -o run -- \
-  python3 scripts/attn_prof_run.py --fwd 1,8192,32,8,128 8,1024,25,25,64 > gpurun_out/pmc_attn/p2.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc $P1 --output-format csv -d $OUT/p1 -o run -- \
+  python3 scripts/attn_prof_run.py 1,8192,32,8,128 8,1024,25,25,64 > $OUT/p1.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc $P2 --output-format csv -d $OUT/p2 -o run -- \
+  python3 scripts/attn_prof_run.py 1,8192,32,8,128 8,1024,25,25,64 > $OUT/p2.log 2>&1 || exit 1
 echo done
