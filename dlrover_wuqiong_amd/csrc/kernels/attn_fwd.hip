@@ -33,13 +33,14 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 
-template <int D, int W = 8>
+template <int D, int W = 8, int BKT = 64>
 struct Fwd2Cfg {
   // W waves share each K/V tile.  D=128: 8 waves (236 VGPRs, one block per
   // CU); D=64: 4 waves (see launch_fwd).
   static constexpr int WAVES = W;
   static constexpr int BQ = 32 * WAVES;  // queries per block
-  static constexpr int BK = 64;          // keys per tile
+  static constexpr int BK = BKT;         // keys per tile
+  static constexpr int NSB = BK / 32;    // 32-key subtiles (S^T accumulators)
   static constexpr int NCH = D / 8;      // 16-byte chunks per row
   static constexpr int KK = D / 16;      // MFMA k-steps over the head dim
   static constexpr int DT = D / 32;      // 32-wide d tiles of O^T
@@ -56,12 +57,12 @@ __device__ __forceinline__ unsigned int pack2(float a, float b) {
   return __builtin_bit_cast(unsigned int, __builtin_convertvector((f32x2_v){a, b}, bf16x2_v));
 }
 
-template <int D, bool CAUSAL, bool EXT, int W = 8, int MINW = 1>
+template <int D, bool CAUSAL, bool EXT, int W = 8, int MINW = 1, int BKT = 64>
 __global__ void __launch_bounds__(64 * W, MINW)
 attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
                 bf16_t* __restrict__ O, float* __restrict__ LSE, int S, int H, int HKV, float scale_log2,
                 AttnStrides st, AttnVarlen vl, AttnExt ex) {
-  using C = Fwd2Cfg<D, W>;
+  using C = Fwd2Cfg<D, W, BKT>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -189,24 +190,24 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
       // ---- S'^T = K Q'^T - m : two 32-key subtiles; the accumulator starts at
       // -m_i (row constant as the initial accumulator), so p = exp2(S') needs
       // no subtraction
-      f32x16 s[2];
+      f32x16 s[C::NSB];
 #pragma unroll
-      for (int sb = 0; sb < 2; ++sb)
+      for (int sb = 0; sb < C::NSB; ++sb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) s[sb][i] = -m_i;
       // the two subtiles' chains interleaved: no MFMA waits on its predecessor
-      if constexpr (D == 64) {
+      if constexpr (D == 64 && C::NSB == 2) {
         // all 8 K fragments (32 VGPRs) in flight at once: one LDS latency per
         // tile instead of one per MFMA
         u32x4 kf[C::KK][2];
 #pragma unroll
         for (int kk = 0; kk < C::KK; ++kk)
 #pragma unroll
-          for (int sb = 0; sb < 2; ++sb) kf[kk][sb] = *(const u32x4*)(kl + img_off<D>(32 * sb + r, 2 * kk + hh));
+          for (int sb = 0; sb < C::NSB; ++sb) kf[kk][sb] = *(const u32x4*)(kl + img_off<D>(32 * sb + r, 2 * kk + hh));
 #pragma unroll
         for (int kk = 0; kk < C::KK; ++kk)
 #pragma unroll
-          for (int sb = 0; sb < 2; ++sb)
+          for (int sb = 0; sb < C::NSB; ++sb)
             s[sb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf[kk][sb]), as_bf16x8(qf[kk]), s[sb], 0, 0, 0);
         // the machine scheduler would sink each read next to its MFMA
         __builtin_amdgcn_sched_group_barrier(0x100, 2 * C::KK, 0);  // DS reads
@@ -215,7 +216,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
 #pragma unroll
         for (int kk = 0; kk < C::KK; ++kk)
 #pragma unroll
-          for (int sb = 0; sb < 2; ++sb) {
+          for (int sb = 0; sb < C::NSB; ++sb) {
             const u32x4 kf = *(const u32x4*)(kl + img_off<D>(32 * sb + r, 2 * kk + hh));
             s[sb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf), as_bf16x8(qf[kk]), s[sb], 0, 0, 0);
           }
@@ -227,7 +228,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
       if (EXT) {
         // window / prefix visibility and the additive bias (exp2 domain)
 #pragma unroll
-        for (int sb = 0; sb < 2; ++sb)
+        for (int sb = 0; sb < C::NSB; ++sb)
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int key = k0 + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hh;
@@ -245,14 +246,14 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
         // offset within the tile is a compile-time constant
         const int rel = (CAUSAL ? min(SK, q + co + 1) : SK) - k0 - 4 * hh;
 #pragma unroll
-        for (int sb = 0; sb < 2; ++sb)
+        for (int sb = 0; sb < C::NSB; ++sb)
 #pragma unroll
           for (int i = 0; i < 16; ++i)
             s[sb][i] = (32 * sb + (i & 3) + 8 * (i >> 2)) < rel ? s[sb][i] : -INFINITY;
       }
       float mx = -INFINITY;
 #pragma unroll
-      for (int sb = 0; sb < 2; ++sb)
+      for (int sb = 0; sb < C::NSB; ++sb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[sb][i]);
       mx = half_max(mx);  // the row's max above its offset
@@ -273,13 +274,13 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
 #pragma unroll
           for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
 #pragma unroll
-        for (int sb = 0; sb < 2; ++sb)
+        for (int sb = 0; sb < C::NSB; ++sb)
 #pragma unroll
           for (int i = 0; i < 16; ++i) s[sb][i] -= d;
       }
       float rs = 0.f;
 #pragma unroll
-      for (int sb = 0; sb < 2; ++sb)
+      for (int sb = 0; sb < C::NSB; ++sb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const float p = __builtin_amdgcn_exp2f(s[sb][i]);
@@ -290,7 +291,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
       if (EXT && ex.dropout) {
         // O accumulates the dropped probabilities; l (hence LSE) the full ones
 #pragma unroll
-        for (int sb = 0; sb < 2; ++sb)
+        for (int sb = 0; sb < C::NSB; ++sb)
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int key = k0 + 32 * sb + (i & 3) + 8 * (i >> 2) + 4 * hh;
@@ -301,7 +302,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
 
       // ---- O^T += V^T P^T : 4 k-steps of 16 keys
 #pragma unroll
-      for (int sb = 0; sb < 2; ++sb) {
+      for (int sb = 0; sb < C::NSB; ++sb) {
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           const f32x16& a = s[sb];
@@ -350,275 +351,13 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   }
 }
 
-// Software-pipelined forward (plain causal / full masks, cdna_hip_programming.md
-// T15): the QK^T MFMAs of tile t+1 are issued before the softmax of tile t,
-// so within one wave the matrix pipe works on the next scores while the VALU
-// exponentiates the current ones; then P_t V_t.  K runs one tile ahead of V
-// in LDS (two K and two V buffers, the same 4 tiles as attn_fwd_kernel): in
-// iteration t the waves read K_{t+1} and V_t, and the stores at its end go
-// to the other two buffers (K_{t+2}, V_{t+1}), so one barrier per tile still
-// suffices.  The next tile's scores are accumulated against the row offset
-// m_i of before the current softmax; a rescale of the current tile shifts
-// them by the same amount.  Two score tiles live in registers (named sA / sB,
-// the loop unrolled by two so they swap roles without copies).
-template <int D, bool CAUSAL, int W>
-__global__ void __launch_bounds__(64 * W, 1)
-attn_fwd_pipe_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
-                     bf16_t* __restrict__ O, float* __restrict__ LSE, int S, int H, int HKV, float scale_log2,
-                     AttnStrides st, AttnVarlen vl) {
-  using C = Fwd2Cfg<D, W>;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 31, hh = lane >> 5;
-  const int nqb = (S + C::BQ - 1) / C::BQ;
-  const BlockXYZ bc = xcd_block(nqb, H);
-  const int b = bc.z, h = bc.y;
-  const int hk = h / (H / HKV);
-  const int qblk = CAUSAL ? nqb - 1 - bc.x : bc.x;
-  const int q_blk0 = qblk * C::BQ;
-  const SeqRange sr = seq_range(vl, b, h, H, S);
-  if (q_blk0 >= sr.sq) return;
-  const int SQ = sr.sq, SK = sr.sk, co = SK - SQ;
-  const int q0 = q_blk0 + wid * 32;
-  const int q = q0 + r;
-  const bf16_t* Qb = Q + (int64_t)b * st.q_bs + (int64_t)sr.q_off * st.q_rs + (int64_t)h * D;
-  const bf16_t* Kb = K + (int64_t)b * st.k_bs + (int64_t)sr.k_off * st.k_rs + (int64_t)hk * D;
-  const bf16_t* Vb = V + (int64_t)b * st.v_bs + (int64_t)sr.k_off * st.v_rs + (int64_t)hk * D;
-
-  u32x4 qf[C::KK];
-#pragma unroll
-  for (int kk = 0; kk < C::KK; ++kk) {
-    const u32x4 raw =
-        (q < SQ) ? *(const u32x4*)(Qb + (int64_t)q * st.q_rs + 16 * kk + 8 * hh) : (u32x4){0, 0, 0, 0};
-    float f[8];
-    unpack8(raw, f);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] *= scale_log2;
-    qf[kk] = (u32x4){pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7])};
-  }
-  f32x16 o[C::DT];
-#pragma unroll
-  for (int dt = 0; dt < C::DT; ++dt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
-  constexpr float RESCALE_T = 8.f;  // deferred rescale, as attn_fwd_kernel
-  float m_i = 0.f, l_i = 0.f;
-  bool seeded = false;
-
-  int n = (SK + C::BK - 1) / C::BK;
-  if (CAUSAL) {
-    const int last = min(SK - 1, min(SQ - 1, q_blk0 + C::BQ - 1) + co);
-    n = last < 0 ? 0 : min(n, last / C::BK + 1);
-  }
-
-  char* kbuf = smem;                // K tiles t & 1
-  char* vbuf = smem + 2 * C::TILE;  // V tiles t & 1
-  u32x4 kst[C::VPT], vst[C::VPT];
-  auto load = [&](u32x4* dst, const bf16_t* base, int64_t rs, int t) {
-#pragma unroll
-    for (int i = 0; i < C::VPT; ++i) {
-      int row, c;
-      stage_rc<D>(tid + 64 * C::WAVES * i, row, c);
-      const int key = t * C::BK + row;
-      dst[i] = key < SK ? *(const u32x4*)(base + (int64_t)key * rs + c * 8) : (u32x4){0, 0, 0, 0};
-    }
-  };
-  auto put = [&](char* img, const u32x4* src) {
-#pragma unroll
-    for (int i = 0; i < C::VPT; ++i) {
-      int row, c;
-      stage_rc<D>(tid + 64 * C::WAVES * i, row, c);
-      *(u32x4*)(img + img_off<D>(row, c)) = src[i];
-    }
-  };
-
-  // S'^T = K Q'^T - m_i for the 64 keys of tile t (two 32-key subtiles)
-  auto qk = [&](f32x16* sc, int t) {
-    const char* kl = kbuf + (t & 1) * C::TILE;
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sc[sb][i] = -m_i;
-    // K fragments: D=64 all 8 in flight (32 VGPRs); D=128 two per k-step
-    constexpr int PRE = D == 64 ? C::KK : 1;
-#pragma unroll
-    for (int k0 = 0; k0 < C::KK; k0 += PRE) {
-      u32x4 kf[PRE][2];
-#pragma unroll
-      for (int kk = 0; kk < PRE; ++kk)
-#pragma unroll
-        for (int sb = 0; sb < 2; ++sb)
-          kf[kk][sb] = *(const u32x4*)(kl + img_off<D>(32 * sb + r, 2 * (k0 + kk) + hh));
-#pragma unroll
-      for (int kk = 0; kk < PRE; ++kk)
-#pragma unroll
-        for (int sb = 0; sb < 2; ++sb)
-          sc[sb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf[kk][sb]), as_bf16x8(qf[k0 + kk]), sc[sb], 0,
-                                                           0, 0);
-    }
-  };
-
-  const int g4 = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
-  // mask + row max + (rare) rescale of tile t's scores
-  auto softmax_max = [&](f32x16* sc, int t) {
-    const int k0 = t * C::BK;
-    const bool need_mask = (k0 + C::BK > SK) || (CAUSAL && (k0 + C::BK - 1 > q0 + co));
-    if (need_mask) {
-      __asm__ volatile("");  // scalar branch: diagonal / ragged tiles only
-      const int rel = (CAUSAL ? min(SK, q + co + 1) : SK) - k0 - 4 * hh;
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          sc[sb][i] = (32 * sb + (i & 3) + 8 * (i >> 2)) < rel ? sc[sb][i] : -INFINITY;
-    }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sc[sb][i]);
-    mx = half_max(mx);
-    const bool fresh = !seeded && mx > -INFINITY;
-    const bool shift = (mx > RESCALE_T) || fresh;
-    seeded = seeded || (mx > -INFINITY);
-    if (__any(shift)) {
-      const float d = shift ? mx : 0.f;
-      const float alpha = fresh ? 1.f : __builtin_amdgcn_exp2f(-d);
-      m_i += d;
-      l_i *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < C::DT; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
-#pragma unroll
-      for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sc[sb][i] -= d;
-    }
-  };
-  // p = exp2(s'), row sum; with NEXT the next tile's QK^T MFMAs (against the
-  // now final offset m_i) are interleaved with the exponentials in one block
-  auto exp_tile = [&](f32x16* sc) {
-    float rs = 0.f;
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(sc[sb][i]);
-        sc[sb][i] = p;
-        rs += p;
-      }
-    l_i += rs;
-  };
-  auto pv = [&](f32x16* sc, int t) {
-    const char* vl_ = vbuf + (t & 1) * C::TILE;
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const f32x16& a = sc[sb];
-        const u32x4 pf = {pack2(a[8 * s2 + 0], a[8 * s2 + 1]), pack2(a[8 * s2 + 2], a[8 * s2 + 3]),
-                          pack2(a[8 * s2 + 4], a[8 * s2 + 5]), pack2(a[8 * s2 + 6], a[8 * s2 + 7])};
-        const int kb = 32 * sb + 16 * s2 + 4 * hh + tq;
-#pragma unroll
-        for (int dt = 0; dt < C::DT; ++dt) {
-          const int ch = (32 * dt + 16 * (g4 & 1)) / 8 + (tp >> 1);
-          const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_s16x4*)LDS_PTR(vl_ + img_off<D>(kb, ch) + 8 * (tp & 1)));
-          const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_s16x4*)LDS_PTR(vl_ + img_off<D>(kb + 8, ch) + 8 * (tp & 1)));
-          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(join_tr(v0, v1)), as_bf16x8(pf), o[dt], 0, 0, 0);
-        }
-      }
-    }
-  };
-
-  if (n > 0) {
-    load(kst, Kb, st.k_rs, 0);
-    load(vst, Vb, st.v_rs, 0);
-    put(kbuf, kst);
-    put(vbuf, vst);
-    if (n > 1) {
-      load(kst, Kb, st.k_rs, 1);
-      put(kbuf + C::TILE, kst);
-      load(vst, Vb, st.v_rs, 1);
-    }
-    if (n > 2) load(kst, Kb, st.k_rs, 2);
-  }
-  __syncthreads();
-  f32x16 sA[2], sB[2];
-  // tiles this wave has work in (causal: a prefix of the block's tiles)
-  const int n_w = CAUSAL ? max(0, min(n, (q0 + 31 + co) / C::BK + 1)) : n;
-  if (n_w > 0) qk(sA, 0);
-  // one iteration: softmax max of t; QK^T of t+1 interleaved with exp of t
-  // in one straight block (on a wave's last tile this QK^T reads a stale
-  // buffer and is discarded: cheaper than a branch, which makes the compiler
-  // hoist the exponentials out of the interleave); PV of t; then the stores
-  // of K_{t+2} / V_{t+1} and the loads of K_{t+3} / V_{t+2}
-  auto step = [&](f32x16* sc, f32x16* sn, int t) {
-    if (t < n_w) {
-      softmax_max(sc, t);
-      qk(sn, t + 1);
-      exp_tile(sc);
-      if constexpr (D == 64) {
-        // the 8 K reads first, then each MFMA followed by a few VALU ops
-        __builtin_amdgcn_sched_group_barrier(0x100, 2 * C::KK, 0);
-#pragma unroll
-        for (int g = 0; g < 2 * C::KK; ++g) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
-        }
-      } else {
-        // per k-step: its 2 K reads, 2 MFMAs, each followed by 2 VALU ops
-#pragma unroll
-        for (int g = 0; g < C::KK; ++g) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-        }
-      }
-      pv(sc, t);
-    }
-    if (t + 1 < n) {
-      if (t + 2 < n) put(kbuf + (t & 1) * C::TILE, kst);
-      put(vbuf + ((t + 1) & 1) * C::TILE, vst);
-      if (t + 3 < n) load(kst, Kb, st.k_rs, t + 3);
-      if (t + 2 < n) load(vst, Vb, st.v_rs, t + 2);
-    }
-    __syncthreads();
-  };
-  for (int t = 0; t < n; t += 2) {
-    step(sA, sB, t);
-    if (t + 1 < n) step(sB, sA, t + 1);
-  }
-
-  const float l_tot = half_sum(l_i);
-  if (q < SQ) {
-    bf16_t* Oq = O + (int64_t)b * st.o_bs + (int64_t)h * D + (int64_t)(sr.q_off + q) * st.o_rs;
-    const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-#pragma unroll
-    for (int dt = 0; dt < C::DT; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        uint2 w;
-        w.x = pack2(o[dt][4 * g + 0] * inv, o[dt][4 * g + 1] * inv);
-        w.y = pack2(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
-        *(uint2*)(Oq + 32 * dt + 8 * g + 4 * hh) = w;
-      }
-    if (hh == 0 && LSE) LSE[sr.lse_base + q] = (l_tot > 0.f) ? (m_i + log2f(l_tot)) * 0.6931471805599453f : -INFINITY;
-  }
-}
-
-template <int D, bool CAUSAL, bool EXT, int W, int MINW>
+template <int D, bool CAUSAL, bool EXT, int W, int MINW, int BKT = 64>
 static void launch_fwd_v(const void* q, const void* k, const void* v, void* o, void* lse, int B, int S, int H,
                          int HKV, float scale_log2, const AttnStrides& st, const AttnVarlen& vl, const AttnExt& ex,
                          hipStream_t s) {
-  using C = Fwd2Cfg<D, W>;
+  using C = Fwd2Cfg<D, W, BKT>;
   dim3 grid((unsigned)((S + C::BQ - 1) / C::BQ * H * B)), block(64 * W);  // 1-D: xcd_block()
-  hipLaunchKernelGGL((attn_fwd_kernel<D, CAUSAL, EXT, W, MINW>), grid, block, 4 * C::TILE, s, (const bf16_t*)q,
+  hipLaunchKernelGGL((attn_fwd_kernel<D, CAUSAL, EXT, W, MINW, BKT>), grid, block, 4 * C::TILE, s, (const bf16_t*)q,
                      (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st, vl, ex);
 }
 
@@ -626,7 +365,7 @@ template <int D>
 static void launch_fwd(const void* q, const void* k, const void* v, void* o, void* lse, int B, int S, int H, int HKV,
                        int causal, float scale_log2, const AttnStrides& st, const AttnVarlen& vl, hipStream_t s,
                        const AttnExt* ext = nullptr, int variant = 0) {
-  // D=64: 4 waves (128 queries per block, 184 VGPRs, two blocks per CU):
+  // D=64: 4 waves (128 queries per block, two blocks per CU):
   // twice the blocks of the 8-wave form for a finer causal balance; measured
   // against 8 waves capped at 128 VGPRs (spills) / uncapped and 4 waves
   // capped: 289-311 vs 239-288 TF/s (profiles/r2/attn_fwd64_variants.jsonl)
@@ -636,24 +375,16 @@ static void launch_fwd(const void* q, const void* k, const void* v, void* o, voi
                   : launch_fwd_v<D, false, true, W, 1>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, *ext, s);
   }
   const AttnExt none = {};
-  // tuning A/B (flags): D=64 capped at 168 VGPRs for three 4-wave blocks per
-  // CU -- measured 8 % slower than the uncapped two (343 vs 371 TF/s, GPT2 shape)
+  // D=64: 128-key tiles -- twice the MFMAs per barrier and per staging pass,
+  // 252 VGPRs: +4-8 % over 64-key tiles (GPT2 shape 354 -> 369 TF/s, S=4096
+  // 578 -> 626; profiles/r3/attn_fwd64_bk128_ab.jsonl).  D=128 keeps 64 (128
+  // spills).  flags=1 selects the 64-key form for A/B runs.
+  constexpr int BKT = D == 64 ? 128 : 64;
   if (D == 64 && variant == 1)
-    return causal ? launch_fwd_v<D, true, false, W, 3>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s)
-                  : launch_fwd_v<D, false, false, W, 3>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s);
-  if (variant == 2) {  // the software-pipelined kernel
-    using C = Fwd2Cfg<D, W>;
-    dim3 grid((unsigned)((S + C::BQ - 1) / C::BQ * H * B)), block(64 * W);
-    if (causal)
-      hipLaunchKernelGGL((attn_fwd_pipe_kernel<D, true, W>), grid, block, 4 * C::TILE, s, (const bf16_t*)q,
-                         (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st, vl);
-    else
-      hipLaunchKernelGGL((attn_fwd_pipe_kernel<D, false, W>), grid, block, 4 * C::TILE, s, (const bf16_t*)q,
-                         (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st, vl);
-    return;
-  }
-  return causal ? launch_fwd_v<D, true, false, W, 1>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s)
-                : launch_fwd_v<D, false, false, W, 1>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s);
+    return causal ? launch_fwd_v<D, true, false, W, 1, 64>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s)
+                  : launch_fwd_v<D, false, false, W, 1, 64>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s);
+  return causal ? launch_fwd_v<D, true, false, W, 1, BKT>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s)
+                : launch_fwd_v<D, false, false, W, 1, BKT>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s);
 }
 
 // strides: int64[8] = q_bs, q_rs, k_bs, k_rs, v_bs, v_rs, o_bs, o_rs (elements)
