@@ -35,6 +35,10 @@ SHAPES = {
     "llama3-70b": dict(vocab=128256, hidden=8192, ffn=28672, layers=80, heads=64, kv_heads=8, head_dim=128),
     "llama3-8b": dict(vocab=128256, hidden=4096, ffn=14336, layers=32, heads=32, kv_heads=8, head_dim=128),
     "llama-tiny": dict(vocab=1024, hidden=256, ffn=688, layers=2, heads=8, kv_heads=8, head_dim=32),
+    # the reference's Megatron-LM row (GPT-1.5B, BASELINE.md: 1.2 s save / 2.1 s load): learned positions,
+    # LayerNorm / linear biases, plain GELU MLP, vocab padded to 50304
+    "gpt2-1.5b": dict(vocab=50304, hidden=1600, ffn=6400, layers=48, heads=25, kv_heads=25, head_dim=64,
+                      gated=False, bias=True, positions=1024),
 }
 
 
@@ -42,16 +46,32 @@ def shard_param_shapes(m, tp):
     """Megatron-core GPTModel parameter names -> TP-rank shard shapes."""
     h, hd = m["hidden"], m["head_dim"]
     qkv = (m["heads"] + 2 * m["kv_heads"]) * hd // tp
+    fc1 = (2 if m.get("gated", True) else 1) * m["ffn"] // tp
+    bias = m.get("bias", False)
     out = {"embedding.word_embeddings.weight": (m["vocab"] // tp, h)}
+    if m.get("positions"):
+        out["embedding.position_embeddings.weight"] = (m["positions"], h)
     for i in range(m["layers"]):
         p = f"decoder.layers.{i}."
         out[p + "self_attention.linear_qkv.layer_norm_weight"] = (h,)
+        if bias:
+            out[p + "self_attention.linear_qkv.layer_norm_bias"] = (h,)
+            out[p + "self_attention.linear_qkv.bias"] = (qkv,)
         out[p + "self_attention.linear_qkv.weight"] = (qkv, h)
         out[p + "self_attention.linear_proj.weight"] = (h, m["heads"] * hd // tp)
+        if bias:
+            out[p + "self_attention.linear_proj.bias"] = (h,)
         out[p + "mlp.linear_fc1.layer_norm_weight"] = (h,)
-        out[p + "mlp.linear_fc1.weight"] = (2 * m["ffn"] // tp, h)
+        if bias:
+            out[p + "mlp.linear_fc1.layer_norm_bias"] = (h,)
+            out[p + "mlp.linear_fc1.bias"] = (fc1,)
+        out[p + "mlp.linear_fc1.weight"] = (fc1, h)
         out[p + "mlp.linear_fc2.weight"] = (h, m["ffn"] // tp)
+        if bias:
+            out[p + "mlp.linear_fc2.bias"] = (h,)
     out["decoder.final_layernorm.weight"] = (h,)
+    if bias:
+        out["decoder.final_layernorm.bias"] = (h,)
     out["output_layer.weight"] = (m["vocab"] // tp, h)
     return out
 
