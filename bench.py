@@ -364,6 +364,7 @@ def _fault_summary(a, ev, agent, step_sec, save_sec):
             # import mode only (a deep standby built its model long before)
             "process_to_model_built": (round(inc1["t_model"] - inc1["t_proc"], 3)
                                        if inc1.get("standby") == "import" else None),
+            "model_build_marks": inc1.get("build_marks") if inc1.get("standby") == "import" else None,
             "activate_to_pg_ready": round(inc1["t_pg"] - inc1["t_activated"], 3),
             "ckpt_engine_init": round(inc1["t_ckpt"] - inc1["t_pg"], 3),
             "restore": round(inc1["restore_sec"], 3),
@@ -430,6 +431,7 @@ def worker(a) -> int:
     from dlrover_wuqiong_amd.parallel.flat import FlatParams
 
     dtype = torch.bfloat16 if cuda else torch.float32
+    marks = {"imports": time.time()}  # model-build phases (import-mode restarts build the model cold)
     torch.manual_seed(1234)
     if a.model.startswith("llama") or a.model.startswith("mixtral"):
         from dlrover_wuqiong_amd.models.llama import Llama, LlamaConfig
@@ -449,9 +451,15 @@ def worker(a) -> int:
             model = GPT2(cfg)
         desc = ("GPT2-1.5B (gpt2-xl: 48L, 1600H, 25 heads)" if a.model == "gpt2-1.5b" else
                 f"{a.model} ({cfg.n_layer}L, {cfg.n_embd}H, {cfg.n_head} heads)")
+    if cuda:
+        torch.cuda.synchronize()
+    marks["init"] = time.time()
     model.to(dtype)
     nparams = model.num_params()
     flat = FlatParams(model, dtype=dtype, device=device)
+    if cuda:
+        torch.cuda.synchronize()
+    marks["flat"] = time.time()
     opt = FusedAdamW(flat, lr=a.lr, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0)
     B, S = a.micro_batch, a.seq
     if cuda:
@@ -785,6 +793,7 @@ def worker(a) -> int:
         emit({"event": "start", "incarnation": incarnation, "t": time.time(), "restored_step": step,
               "restore_sec": restore_sec, "restore_ok": restore_ok, "t_proc": t_proc, "t_model": t_model,
               "t_activated": t_act, "t_pg": t_pg, "t_ckpt": t_ckpt, "t_restored": t_restored,
+              "build_marks": {k: round(v - t_proc, 3) for k, v in marks.items()},
               "prepin_s": info.get("prepin_s") if info else None, "standby": "deep" if info else "import",
               "restore_source": getattr(ckpt.engine, "last_restore_source", None),
               "restore_phases": dict(getattr(ckpt.engine, "last_restore_breakdown", {}) or {},

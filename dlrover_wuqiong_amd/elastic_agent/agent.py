@@ -465,6 +465,18 @@ class ElasticTrainingAgent:
                     pass
         self._standby = {}
 
+    @staticmethod
+    def _teardown_overlap_ok() -> bool:
+        """May new workers start while the old ones are still exiting?  Yes
+        when every GPU of the node uses at most DWAMD_OVERLAP_TEARDOWN_MAX_USED
+        (default 0.5: a second copy fits) of its HBM right now (amdgpu sysfs: the agent never
+        initialises HIP); no readable GPU -> wait."""
+        from .monitor import ResourceMonitor
+
+        frac = float(os.getenv("DWAMD_OVERLAP_TEARDOWN_MAX_USED", "0.5"))
+        stats = ResourceMonitor.gpu_stats()
+        return bool(stats) and all(g.used_memory_mb <= frac * g.total_memory_mb for g in stats)
+
     def _stop_workers(self, timeout: Optional[float] = None, wait: bool = True):
         """SIGTERM every live worker group, SIGKILL after ``timeout``.
         ``wait=False``: return at once and reap in the background (the next
@@ -631,8 +643,12 @@ class ElasticTrainingAgent:
 
                 level = max((classify_failure(f.get("message", "")) for f in res.failures.values()),
                             key=lambda lv: lv == TrainingExceptionLevel.NODE_ERROR)
+                # deep standbys already hold their memory; import-mode
+                # replacements allocate theirs, so they start before the failed
+                # processes are torn down (~1-1.5 s for tens of GB of mappings)
+                # only when every GPU has room for a second copy
                 self._stop_workers(timeout=self.config.failure_stop_timeout,
-                                   wait=self.config.standby_mode != "deep")
+                                   wait=self.config.standby_mode != "deep" and not self._teardown_overlap_ok())
                 self._event("workers_stopped")
                 if level == TrainingExceptionLevel.NODE_ERROR and self.config.exit_on_node_error:
                     # hardware signature: let the platform replace this node

@@ -6,10 +6,16 @@ checkpoint shm before the first useful step.  The agent therefore keeps one
 *standby* process per local rank ready.  Two modes:
 
 ``import`` (default, safe for any script)
-    The standby imports torch and this package (nothing that touches the
-    GPU) and blocks on stdin.  On (re)start the agent sends one JSON line
-    -- worker environment, argv, entrypoint, log file -- and the standby
-    turns into the worker in place (``runpy``, ``__main__`` semantics).
+    The standby imports torch and this package, initialises the HIP runtime
+    on its local rank's GPU and keeps this rank's part of the node's
+    checkpoint shm pinned (``DWAMD_STANDBY_GPU_INIT=0``: touch no GPU, for
+    scripts that choose their visible devices in-process), and blocks on
+    stdin.  On (re)start the agent sends one JSON line -- worker
+    environment, argv, entrypoint, log file -- and the standby turns into
+    the worker in place (``runpy``, ``__main__`` semantics).  The script
+    still builds its model and restores from host shm: the reference's
+    restart semantics, minus interpreter start, imports, HIP init and the
+    pinning of the restore source.
 
 ``deep`` (opt-in: ``dwamd-run --standby-mode deep``; the script must call
 :func:`standby_point`)
@@ -60,6 +66,14 @@ def _preload():
             importlib.import_module(m)
         except Exception as e:  # a missing optional module must not kill the standby
             print(f"[standby] preload {m} failed: {e}", file=sys.stderr)
+    try:
+        # the first torch.optim.Optimizer of a process imports torch._dynamo
+        # (~900 modules, ~1.1 s): pay it here, not inside the restart
+        import torch
+
+        torch.optim.SGD([torch.zeros(1, requires_grad=True)], lr=0.1)
+    except Exception as e:
+        print(f"[standby] optimizer warm-up failed: {e}", file=sys.stderr)
 
 
 def _redirect(log_path: str):
@@ -194,6 +208,90 @@ def _run_entry(entry: str, args, module: bool):
         runpy.run_path(entry, run_name="__main__")
 
 
+def _gpu_init(lr: str) -> bool:
+    """HIP runtime + a context on this rank's device (import mode)."""
+    try:
+        import torch
+
+        if not torch.cuda.is_available():
+            return False
+        torch.cuda.set_device(int(lr) % max(1, torch.cuda.device_count()))
+        x = torch.ones(64, 64, device="cuda", dtype=torch.bfloat16)
+        (x @ x).float().sum().item()  # BLAS handle + a first kernel launch
+        from .._native import kernels
+
+        kernels(required=False)  # this package's HIP kernel library (code objects registered)
+        for m in os.environ.get("DWAMD_STANDBY_PRELOAD_GPU", "dlrover_wuqiong_amd.models.gpt2,"
+                                "dlrover_wuqiong_amd.models.llama,dlrover_wuqiong_amd.optimizers.fused,"
+                                "dlrover_wuqiong_amd.parallel.ddp,dlrover_wuqiong_amd.parallel.flat").split(","):
+            if m.strip():
+                try:
+                    importlib.import_module(m.strip())
+                except Exception as e:
+                    print(f"[standby] preload {m} failed: {e}", file=sys.stderr)
+        torch.cuda.synchronize()
+        return True
+    except Exception as e:  # never fatal: the worker initialises on its own
+        print(f"[standby] GPU pre-init skipped: {e}", file=sys.stderr)
+        return False
+
+
+def _reserve_state_memory() -> int:
+    """Fill PyTorch's caching allocator with about the HBM the worker's model
+    + optimizer will take (the checkpoint payload size, once a save made it
+    known) and leave it cached: the driver's allocation of fresh VRAM (it
+    clears every new buffer) is then paid while waiting, not inside the
+    restart (~1.9 s for the 19 GB of GPT2-1.5B Adam state).  Bounded by the
+    free HBM; DWAMD_STANDBY_RESERVE=0 disables it.  Returns bytes reserved."""
+    if os.environ.get("DWAMD_STANDBY_RESERVE", "1") != "1":
+        return -1
+    try:
+        import torch
+
+        from ..flash_checkpoint.prewarm import local_state_bytes
+
+        want = int(local_state_bytes() * float(os.environ.get("DWAMD_STANDBY_RESERVE_FACTOR", "1.25")))
+        if want <= 0:
+            return 0
+        free, _total = torch.cuda.mem_get_info()
+        n = min(want, int(free * 0.8) - (8 << 30))
+        if n <= (1 << 30):
+            return -1  # no room next to the live worker: skip for good
+        t = torch.empty(n, dtype=torch.uint8, device="cuda")
+        del t  # stays in the allocator's cache for the worker this process becomes
+        return n
+    except Exception as e:  # never fatal
+        print(f"[standby] HBM reserve skipped: {e}", file=sys.stderr)
+        return -1
+
+
+def _wait_command(pin: bool, ctl: str, lr: str, interval: float = 0.25) -> bytes:
+    """Block until the agent's activation line arrives on stdin; meanwhile
+    keep this rank's checkpoint shm pinned (segments appear, or are
+    re-created at a new size, while the standby waits).  b"" = discarded."""
+    import select
+
+    buf = b""
+    fd = sys.stdin.fileno()
+    pinned_marked = False
+    reserved = 0
+    while b"\n" not in buf:
+        if pin:
+            _prepin_checkpoint_shm()
+            if not pinned_marked and _pinned_bytes() > 0:
+                _mark(ctl, PINNED_PREFIX, lr, f"{_pinned_bytes()}\n")
+                pinned_marked = True
+            if not reserved:
+                reserved = _reserve_state_memory()
+        r, _, _ = select.select([fd], [], [], interval)
+        if r:
+            chunk = os.read(fd, 1 << 20)
+            if not chunk:
+                return b""
+            buf += chunk
+    return buf.split(b"\n", 1)[0]
+
+
 def main():
     spec = os.environ.get(SPEC_ENV, "")
     if spec:
@@ -212,11 +310,15 @@ def main():
             return 3
         return 0
     _preload()
+    ctl = os.environ.get("DWAMD_AGENT_CTL_DIR", "")
+    lr = os.environ.get("DWAMD_STANDBY_LOCAL_RANK", "0")
+    gpu = os.environ.get("DWAMD_STANDBY_GPU_INIT", "1") == "1" and _gpu_init(lr)
+    if gpu:
+        os.environ.setdefault("LOCAL_RANK", lr)  # the shm pre-pin pins this rank's ranges
     # import mode: torch + this package are imported; tell the agent (and
     # anyone waiting on the control dir) this standby can take over now
-    _mark(os.environ.get("DWAMD_AGENT_CTL_DIR", ""), READY_PREFIX, os.environ.get("DWAMD_STANDBY_LOCAL_RANK", "0"),
-          f"{os.getpid()} {time.time()}\n")
-    line = sys.stdin.readline()
+    _mark(ctl, READY_PREFIX, lr, f"{os.getpid()} {time.time()}\n")
+    line = _wait_command(gpu, ctl, lr)
     if not line.strip():
         return 0  # agent discarded the standby
     cmd = json.loads(line)

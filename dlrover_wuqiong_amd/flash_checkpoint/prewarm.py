@@ -27,6 +27,7 @@ from .shm_handler import (_ADOPTABLE, DLROVER_CKPT_CONFIG_KEY, HEADER_BYTES, MAG
 
 _PINNED_BYTES: Dict[str, int] = {}
 _SLICE_BYTES: Dict[str, int] = {}  # segment -> this rank's slice bytes (layout known)
+_STATE_BYTES: Dict[str, int] = {}  # segment -> its whole payload (the state the worker rebuilds)
 
 
 def _slot_ranges(shm: SharedMemory, shard: int, local_rank: int) -> Tuple[List[Tuple[int, int]], bool]:
@@ -68,6 +69,12 @@ def prepinned_bytes() -> int:
     return sum(_PINNED_BYTES.values())
 
 
+def local_state_bytes() -> int:
+    """Payload bytes of the checkpoint this local rank restores (0: none yet):
+    about the model + optimizer state its worker allocates."""
+    return max(_STATE_BYTES.values(), default=0)
+
+
 def local_slice_bytes() -> int:
     """Bytes of the payload slice this local rank snapshots (0: unknown yet)."""
     return max(_SLICE_BYTES.values(), default=0)
@@ -93,6 +100,7 @@ def prepin_local_checkpoint_shm() -> float:
             _ADOPTABLE.pop(name, None)
             _PINNED_BYTES.pop(name, None)
             _SLICE_BYTES.pop(name, None)
+            _STATE_BYTES.pop(name, None)
             shm.close()
             shm = None
         if shm is None:
@@ -105,6 +113,9 @@ def prepin_local_checkpoint_shm() -> float:
         ranges, known = _slot_ranges(shm, shard, lr)
         if known and ranges:
             _SLICE_BYTES[name] = ranges[0][1]
+            import numpy as np
+
+            _STATE_BYTES[name] = int(np.frombuffer(shm.buf, dtype=np.int64, count=2)[1])
         if not ranges:
             if name not in _ADOPTABLE:
                 shm.close()
