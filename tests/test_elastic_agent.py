@@ -100,3 +100,37 @@ def test_network_check_then_train(tmp_path):
     assert p.returncode == 0, log[-3000:]
     assert "network check round 0: ok=True" in log
     assert _results(out)[0]["restart"] == 0
+
+
+def test_teardown_overlap_decision(monkeypatch):
+    """Import-mode replacements start during the killed processes' teardown
+    only when every GPU has room for a second copy (amdgpu sysfs numbers)."""
+    from dlrover_wuqiong_amd.common.comm import GPUStats
+    from dlrover_wuqiong_amd.elastic_agent import monitor
+    from dlrover_wuqiong_amd.elastic_agent.agent import ElasticTrainingAgent
+
+    def stats(*used):
+        return lambda: [GPUStats(index=i, total_memory_mb=1000, used_memory_mb=u, gpu_utilization=0.0)
+                        for i, u in enumerate(used)]
+
+    monkeypatch.setattr(monitor.ResourceMonitor, "gpu_stats", staticmethod(stats(300, 450)))
+    assert ElasticTrainingAgent._teardown_overlap_ok()
+    monkeypatch.setattr(monitor.ResourceMonitor, "gpu_stats", staticmethod(stats(300, 600)))
+    assert not ElasticTrainingAgent._teardown_overlap_ok()
+    monkeypatch.setattr(monitor.ResourceMonitor, "gpu_stats", staticmethod(stats()))
+    assert not ElasticTrainingAgent._teardown_overlap_ok()  # nothing readable: wait
+    monkeypatch.setenv("DWAMD_OVERLAP_TEARDOWN_MAX_USED", "0.7")
+    monkeypatch.setattr(monitor.ResourceMonitor, "gpu_stats", staticmethod(stats(600)))
+    assert ElasticTrainingAgent._teardown_overlap_ok()
+
+
+def test_import_standby_helpers_without_gpu(monkeypatch):
+    """The import standby's GPU warm-ups are no-ops (never fatal) on a host
+    without a GPU; the optimizer warm-up leaves torch._dynamo imported."""
+    from dlrover_wuqiong_amd.elastic_agent import standby
+
+    monkeypatch.setenv("DWAMD_STANDBY_PRELOAD", "torch")
+    standby._preload()
+    assert "torch._dynamo" in sys.modules
+    assert standby._gpu_init("0") is False
+    assert standby._reserve_state_memory() in (0, -1)
