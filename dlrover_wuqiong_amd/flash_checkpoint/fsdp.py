@@ -419,6 +419,15 @@ class FsdpShardCheckpointer(Checkpointer):
         sd.update(extra_sd or {})
         return sd
 
+    def prepare(self, model, optimizer, extra_sd=None) -> bool:
+        """Start the one-time shm set-up (segment + prefault + pin of both
+        slots) for this model / optimizer in the background, e.g. right after
+        the first optimizer step (``CheckpointEngine.prepare_memory``)."""
+        sd = self._state(model, optimizer, extra_sd)
+        _, _, payload = self._engine._payload(sd)
+        payload.pop("_views", None)
+        return self._engine.prepare_memory({DCP_KEY: payload})
+
     def save_checkpoint(self, step, model, optimizer, extra_sd=None, path="", storage_type=StorageType.DISK):
         path = path or os.path.join(self.checkpoint_dir, str(step))
         if storage_type == StorageType.MEMORY and self._engine.precheck_skip():
