@@ -266,3 +266,20 @@ def test_overlapped_snapshot_fence_runs_before_any_optimizer_step():
     assert _Pending.fenced == 1 and len(copier._FENCED) == 0
     opt.step()
     assert _Pending.fenced == 1
+
+
+def test_staging_ring_shape_follows_hbm_budget():
+    """The staging ring grows from K x C to the HBM budget (never past the
+    slice): explicit DWAMD_RING_HBM_GB, or the free HBM in auto mode."""
+    from dlrover_wuqiong_amd.flash_checkpoint.copier import GpuCopier
+
+    c = GpuCopier.__new__(GpuCopier)  # sizing logic only: no device needed
+    c.ring_slots, c.ring_chunk, c.ring_hbm, c._ring_auto = 4, 1 << 30, 0, 0
+    c.staging_mode = "ring"
+    assert c._ring_shape(100 << 30) == (4, 1 << 30)  # forced ring: K x C
+    c.ring_hbm = 64 << 30
+    assert c._ring_shape(100 << 30) == (64, 1 << 30)
+    assert c._ring_shape(10 << 30) == (10, 1 << 30)  # never beyond the slice
+    c.ring_hbm, c.staging_mode, c._ring_auto = 0, "auto", 40 << 30
+    assert c._ring_shape(100 << 30) == (40, 1 << 30)  # auto: the free HBM
+    assert c._ring_shape(1 << 20)[0] == 4  # a tiny slice keeps the minimal ring

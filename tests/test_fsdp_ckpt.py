@@ -47,7 +47,10 @@ def _fsdp_worker(rank, world, port, root, q):
         _train(model, opt, 1)
         ck = FsdpShardCheckpointer(root)
         proj = torch.arange(12.0).view(3, 4)  # saved through a non-contiguous view
+        # one-time shm set-up ahead of the first save, with the same layout
+        assert ck.prepare(model, opt, {"epoch": 7, "proj": proj.t()})
         assert ck.save_checkpoint(2, model, opt, {"epoch": 7, "proj": proj.t()}, storage_type=StorageType.MEMORY)
+        assert ck.engine._planner.fast_hits >= 1  # the save reused prepare()'s DCP plan
         ck.wait_latest_checkpoint()
         want = _local(model)
         want_m = {k: v.to_local().clone() for k, v in opt.state_dict()["state"][0].items()
