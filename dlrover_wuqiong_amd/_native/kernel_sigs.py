@@ -6,6 +6,9 @@ vp, i64, i32, u32, u64, f32, cp = (c.c_void_p, c.c_int64, c.c_int, c.c_uint32, c
                                    c.c_float, c.c_char_p)
 
 SIGS = {
+    # fp8.hip
+    "dw_fp8_cast_amax": (i32, [vp, i32, vp, vp, vp, i64, i32, vp]),
+    "dw_fp8_update_scales": (i32, [vp, vp, vp, vp, vp, i32, i32, f32, vp]),
     # ckpt_copy.hip
     "dw_multi_copy": (i32, [vp, i64, vp]),
     "dw_gemm_dgelu": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),

@@ -58,7 +58,7 @@ import torch.nn as nn
 from ..common.log import logger
 from . import distributed as adist
 
-ORDER = ["parallel_mode", "module_replace", "half", "amp_native", "tensor_parallel", "sequence_parallel",
+ORDER = ["parallel_mode", "module_replace", "half", "amp_native", "fp8", "tensor_parallel", "sequence_parallel",
          "context_parallel",
          "checkpoint", "mixed_parallel", "pipeline_parallel", "fsdp", "zero2", "zero1", "ddp"]
 ALIASES = {"amp": "amp_native", "amp_native_bf16": "amp_native", "fsdp2": "fsdp", "zero3": "fsdp",
@@ -216,6 +216,25 @@ def _apply_amp_native(ctx, cfg):
     ctx["amp_dtype"] = dtype
     if dtype == torch.float16:
         ctx["grad_scaler"] = torch.amp.GradScaler("cuda" if torch.cuda.is_available() else "cpu")
+
+
+def _apply_fp8(ctx, cfg):
+    """ATorch ``fp8`` (amp_optimization.py Fp8Optimization): eligible
+    ``nn.Linear`` layers -> ``ops.fp8.Fp8Linear`` (FP8 GEMMs on the CDNA4
+    matrix cores, delayed scaling advanced after every optimizer step)."""
+    from ..ops import fp8
+
+    cfg = cfg if isinstance(cfg, dict) else {}
+    if ctx.get("tp_like"):
+        logger.warning("fp8: not combined with tensor / sequence / mixed parallelism here; fp8 skipped")
+        return
+    fp8.configure(history_len=int(cfg.get("amax_history_len", 1024)), margin=int(cfg.get("margin", 0)),
+                  algo=cfg.get("amax_compute_algo", "max"), reduce_amax=bool(cfg.get("reduce_amax", True)),
+                  interval=int(cfg.get("interval", 1)), group=ctx.get("dp_group"))
+    done = fp8.replace_linears(ctx["model"], include=cfg.get("include"), exclude=cfg.get("exclude"),
+                               fp8_format=cfg.get("fp8_format", "HYBRID"))
+    ctx["fp8"] = done
+    logger.info(f"fp8: {len(done)} nn.Linear -> Fp8Linear ({cfg.get('fp8_format', 'HYBRID')})")
 
 
 def _tp_plan_for(model: nn.Module):
@@ -539,7 +558,7 @@ def _apply_ddp(ctx, cfg):
 
 
 APPLY = {"parallel_mode": _apply_parallel_mode, "module_replace": _apply_module_replace, "half": _apply_half,
-         "amp_native": _apply_amp_native, "tensor_parallel": _apply_tensor_parallel,
+         "amp_native": _apply_amp_native, "fp8": _apply_fp8, "tensor_parallel": _apply_tensor_parallel,
          "sequence_parallel": _apply_sequence_parallel, "context_parallel": _apply_context_parallel,
          "checkpoint": _apply_checkpoint, "mixed_parallel": _apply_mixed_parallel,
          "pipeline_parallel": _apply_pipeline_parallel,
@@ -598,7 +617,9 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
     if "zero1" in strategy.names() and "ddp" not in strategy.names():
         strategy = Strategy.from_spec(strategy.opts + [("ddp", None)])
 
-    ctx: Dict[str, Any] = {"model": model, "find_unused_parameters": find_unused_parameters}
+    ctx: Dict[str, Any] = {"model": model, "find_unused_parameters": find_unused_parameters,
+                           "tp_like": bool({"tensor_parallel", "sequence_parallel", "mixed_parallel"}
+                                           & set(strategy.names()))}
     for name, cfg in strategy.opts:
         if name == "parallel_mode":
             APPLY[name](ctx, cfg)
@@ -653,6 +674,15 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
                                  cpu_offload=lcfg.get("outer_optim_cpu_offload", False))
             logger.info(f"fsdp: local SGD over the replicate dimension (sync every "
                         f"{optim.sync_interval} steps after {optim.warmup_steps} warm-up steps)")
+    if ctx.get("fp8") and optim is not None:
+        # delayed scaling: the step's recorded amaxes become the next scales
+        from ..ops.fp8 import fp8_update
+
+        inner = getattr(optim, "optimizer", optim)
+        if hasattr(inner, "register_step_post_hook"):
+            inner.register_step_post_hook(lambda *_a, **_k: fp8_update())
+        else:
+            logger.warning("fp8: optimizer has no step hooks; call ops.fp8.fp8_update() after each step")
     sched = lr_scheduler_cls(optim, **(lr_scheduler_args or {})) if (lr_scheduler_cls and optim) else None
 
     dataloader = None

@@ -1,0 +1,137 @@
+// FP8 training support for gfx950 (OCP e4m3 / e5m2, the formats the CDNA4
+// MFMA consumes natively; ops/fp8.py).
+//
+//  * dw_fp8_cast_amax: one pass over a bf16 / fp32 tensor that (a) scales
+//    it by the tensor's current delayed-scaling factor, saturates to the
+//    format's range and converts 8 values per lane with v_cvt_pk_fp8_f32 /
+//    v_cvt_pk_bf8_f32 (16-byte loads, 8-byte stores), and (b) records the
+//    tensor's amax of THIS pass (block max, one vector atomic per block on
+//    the float bits -- non-negative floats order like their bit patterns)
+//    for the next iteration's scale.
+//  * dw_fp8_update_scales: after an iteration, for every registered tensor
+//    at once: push the recorded amax into its history, scale = fmax /
+//    (max(history) * 2^margin) (unchanged while the history is all zero),
+//    inv_scale = 1 / scale for the GEMM, and clear the recorded amax.  One
+//    launch per training step for the whole model (delayed scaling, as
+//    Transformer Engine's DelayedScaling recipe).
+//
+// The GEMMs themselves are hipBLASLt's FP8 kernels (torch._scaled_mm).
+#include "dw_common.h"
+
+template <bool E5M2>
+__device__ __forceinline__ unsigned cvt4(float a, float b, float c, float d) {
+  unsigned w = 0;
+  if (E5M2) {
+    w = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, w, false);
+    w = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, w, true);
+  } else {
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, w, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  }
+  return w;
+}
+
+template <bool BF16_IN, bool E5M2>
+__global__ void __launch_bounds__(256) fp8_cast_amax_kernel(const void* __restrict__ x, const float* __restrict__ scale,
+                                                            unsigned char* __restrict__ out,
+                                                            unsigned* __restrict__ amax, long long n) {
+  constexpr float LIM = E5M2 ? 57344.f : 448.f;
+  const float s = *scale;
+  float m = 0.f;
+  const long long nvec = n >> 3;
+  for (long long v = blockIdx.x * 256ll + threadIdx.x; v < nvec; v += (long long)gridDim.x * 256) {
+    float f[8];
+    if (BF16_IN) {
+      unpack8(((const u32x4*)x)[v], f);
+    } else {
+      const f32x4 a = ((const f32x4*)x)[2 * v], b = ((const f32x4*)x)[2 * v + 1];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f[i] = a[i];
+        f[4 + i] = b[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      m = fmaxf(m, fabsf(f[i]));
+      f[i] = fminf(fmaxf(f[i] * s, -LIM), LIM);
+    }
+    uint2 w;
+    w.x = cvt4<E5M2>(f[0], f[1], f[2], f[3]);
+    w.y = cvt4<E5M2>(f[4], f[5], f[6], f[7]);
+    ((uint2*)out)[v] = w;
+  }
+  // tail (n % 8 elements): one value per thread of the first block
+  if (blockIdx.x == 0 && threadIdx.x < (n & 7)) {
+    const long long i = (nvec << 3) + threadIdx.x;
+    const float f = BF16_IN ? bf2f(((const bf16_t*)x)[i]) : ((const float*)x)[i];
+    m = fmaxf(m, fabsf(f));
+    const float c = fminf(fmaxf(f * s, -LIM), LIM);
+    out[i] = (unsigned char)(cvt4<E5M2>(c, 0.f, 0.f, 0.f) & 0xff);
+  }
+  __shared__ float red[4];
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (!(bm == bm)) {  // NaN / inf input: record +inf so the next scale backs off
+      atomicMax(amax, 0x7f800000u);
+    } else if (bm > 0.f) {
+      atomicMax(amax, __float_as_uint(bm));
+    }
+  }
+}
+
+// x: fp32 (in_bf16 = 0) or bf16 (1), 16-byte aligned; out: n bytes; scale /
+// amax: device float / uint (float bits) of this tensor.
+extern "C" int dw_fp8_cast_amax(const void* x, int in_bf16, const float* scale, void* out, unsigned* amax,
+                                long long n, int e5m2, void* stream) {
+  if (n <= 0) return 0;
+  const int grid = dw_grid_for((n >> 3) > 0 ? (n >> 3) : 1, 256, 4096);
+  hipStream_t s = (hipStream_t)stream;
+#define L(B, E)                                                                                                 \
+  hipLaunchKernelGGL((fp8_cast_amax_kernel<B, E>), dim3(grid), dim3(256), 0, s, x, scale, (unsigned char*)out, \
+                     amax, n)
+  if (in_bf16) {
+    if (e5m2) L(true, true); else L(true, false);
+  } else {
+    if (e5m2) L(false, true); else L(false, false);
+  }
+#undef L
+  DW_LAUNCH_RET;
+}
+
+// meta arrays of m tensors: amax_bits [m] (cleared here), history [m, h]
+// (slot 0 = newest), fmax [m] (448 or 57344), scale / inv_scale [m].
+__global__ void fp8_update_scales_kernel(unsigned* __restrict__ amax_bits, float* __restrict__ hist,
+                                         const float* __restrict__ fmax_, float* __restrict__ scale,
+                                         float* __restrict__ inv_scale, int m, int h, float margin_pow2) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= m) return;
+  float* hh = hist + (long long)t * h;
+  const float cur = __uint_as_float(amax_bits[t]);
+  float best = cur;
+  for (int j = h - 1; j > 0; --j) {
+    hh[j] = hh[j - 1];
+    best = fmaxf(best, hh[j]);
+  }
+  hh[0] = cur;
+  amax_bits[t] = 0u;
+  if (best > 0.f && best < INFINITY) {
+    const float sc = fmax_[t] / (best * margin_pow2);
+    scale[t] = sc;
+    inv_scale[t] = 1.f / sc;
+  } else if (best == INFINITY) {  // overflowed: shrink hard
+    scale[t] *= 0.5f;
+    inv_scale[t] = 1.f / scale[t];
+  }
+}
+
+extern "C" int dw_fp8_update_scales(unsigned* amax_bits, float* hist, const float* fmax_, float* scale,
+                                    float* inv_scale, int m, int h, float margin_pow2, void* stream) {
+  if (m <= 0) return 0;
+  hipLaunchKernelGGL(fp8_update_scales_kernel, dim3((m + 255) / 256), dim3(256), 0, (hipStream_t)stream, amax_bits,
+                     hist, fmax_, scale, inv_scale, m, h, margin_pow2);
+  DW_LAUNCH_RET;
+}

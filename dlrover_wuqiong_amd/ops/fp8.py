@@ -1,0 +1,277 @@
+"""FP8 linear layers with delayed scaling on the CDNA4 FP8 matrix cores.
+
+MI355X's MFMA consumes OCP e4m3 / e5m2 at twice the bf16 rate.  An
+``Fp8Linear`` runs its three GEMMs in FP8 (hipBLASLt kernels through
+``torch._scaled_mm``):
+
+    forward   y  = x8 @ w8^T            x8, w8: e4m3
+    backward  dx = g8 @ w8              g8: e5m2 ("HYBRID") or e4m3 ("E4M3")
+              dw = g8^T @ x8
+
+Every FP8 operand comes from ``dw_fp8_cast_amax`` (``csrc/kernels/fp8.hip``):
+one pass that scales by the tensor's current factor, saturates, converts 8
+values per lane with the gfx950 ``v_cvt_pk_fp8/bf8_f32`` instructions and
+records this pass's amax.  The factors follow Transformer Engine's delayed
+scaling: after each optimizer step ONE kernel (``Fp8State.update``) pushes
+every tensor's recorded amax into its history and sets ``scale = fmax /
+(max(history) * 2^margin)`` for the next step -- no host sync anywhere.
+``reduce_amax`` takes the MAX of the recorded amaxes over the data-parallel
+group first (one all-reduce per step), so every rank quantises alike.
+
+CPU tensors run the same math with torch's float8 dtypes (the numerics
+oracle of the tests).
+
+Parity: ATorch ``auto/opt_lib/amp_optimization.py`` ``Fp8Optimization``
+(Transformer Engine ``te.Linear`` + ``fp8_autocast(DelayedScaling)``);
+include / exclude / margin / interval / fp8_format / amax_history_len /
+amax_compute_algo / reduce_amax keep their meaning.
+"""
+
+import math
+from typing import Dict, Iterable, List, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _hip
+
+FP8_MAX = {"e4m3": 448.0, "e5m2": 57344.0}
+_TORCH_DT = {"e4m3": torch.float8_e4m3fn, "e5m2": torch.float8_e5m2}
+
+
+class Fp8State:
+    """Delayed-scaling metadata of every FP8 tensor role on one device, in
+    contiguous buffers so one kernel updates all of them."""
+
+    def __init__(self, device, history_len: int = 1024, margin: int = 0, algo: str = "max",
+                 capacity: int = 8192, group=None, reduce_amax: bool = True, interval: int = 1):
+        self.device = torch.device(device)
+        self.h = history_len if algo == "max" else 1
+        self.margin = margin
+        self.cap = capacity
+        self.group = group
+        self.reduce_amax = reduce_amax
+        self.interval = max(1, int(interval))
+        d = self.device
+        self.amax_bits = torch.zeros(capacity, dtype=torch.int32, device=d)  # float bits, this step
+        self.hist = torch.zeros(capacity, self.h, dtype=torch.float32, device=d)
+        self.fmax = torch.ones(capacity, dtype=torch.float32, device=d)
+        self.scale = torch.ones(capacity, dtype=torch.float32, device=d)
+        self.inv_scale = torch.ones(capacity, dtype=torch.float32, device=d)
+        self.n = 0
+        self.steps = 0
+
+    def register(self, fmt: str) -> int:
+        if self.n >= self.cap:
+            raise RuntimeError(f"Fp8State: more than {self.cap} FP8 tensors")
+        i = self.n
+        self.n += 1
+        self.fmax[i] = FP8_MAX[fmt]
+        return i
+
+    @torch.no_grad()
+    def update(self):
+        """Amax of the finished step -> history -> next scales (every
+        ``interval`` steps; call after ``optimizer.step()``)."""
+        self.steps += 1
+        if self.n == 0 or self.steps % self.interval:
+            return
+        amax = self.amax_bits[: self.n]
+        if self.reduce_amax and self.group is not False:
+            import torch.distributed as dist
+
+            if dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1:
+                # non-negative float bits order like the floats: MAX on int32
+                dist.all_reduce(amax, op=dist.ReduceOp.MAX, group=self.group)
+        mp = float(2.0 ** self.margin)
+        if _hip.use_hip(self.amax_bits):
+            _hip.check(_hip.lib().dw_fp8_update_scales(
+                _hip.ptr(self.amax_bits), _hip.ptr(self.hist), _hip.ptr(self.fmax), _hip.ptr(self.scale),
+                _hip.ptr(self.inv_scale), self.n, self.h, mp, _hip.stream()), "fp8_update_scales")
+            return
+        n = self.n
+        cur = amax.view(torch.float32).clone()
+        self.hist[:n] = torch.cat([cur[:, None], self.hist[:n, :-1]], 1)
+        best = self.hist[:n].amax(1)
+        ok = (best > 0) & torch.isfinite(best)
+        sc = torch.where(ok, self.fmax[:n] / (best * mp), self.scale[:n])
+        sc = torch.where(torch.isinf(best), self.scale[:n] * 0.5, sc)
+        self.scale[:n] = sc
+        self.inv_scale[:n] = 1.0 / sc
+        amax.zero_()
+
+
+_STATES: Dict[torch.device, Fp8State] = {}
+_DEFAULTS: dict = {}
+
+
+def fp8_state(device, **kw) -> Fp8State:
+    d = torch.device(device)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    st = _STATES.get(d)
+    if st is None:
+        st = _STATES[d] = Fp8State(d, **dict(_DEFAULTS, **kw))
+    return st
+
+
+def configure(**kw):
+    """Defaults (history_len, margin, algo, group, reduce_amax, interval) for
+    states created after this call."""
+    _DEFAULTS.update(kw)
+
+
+def fp8_update():
+    """Advance every device's delayed scaling (after ``optimizer.step()``)."""
+    for st in _STATES.values():
+        st.update()
+
+
+@torch.no_grad()
+def cast_to_fp8(x: torch.Tensor, st: Fp8State, idx: int, fmt: str) -> torch.Tensor:
+    """x (bf16 / fp32) -> float8 tensor scaled by ``st.scale[idx]``; records
+    amax(|x|) of this call into ``st.amax_bits[idx]``."""
+    x = x.contiguous()
+    if _hip.use_hip(x) and x.dtype in (torch.bfloat16, torch.float32):
+        out = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+        _hip.check(_hip.lib().dw_fp8_cast_amax(
+            _hip.ptr(x), int(x.dtype == torch.bfloat16), _hip.ptr(st.scale[idx:]), _hip.ptr(out),
+            _hip.ptr(st.amax_bits[idx:]), x.numel(), int(fmt == "e5m2"), _hip.stream()), "fp8_cast_amax")
+        return out.view(_TORCH_DT[fmt])
+    xf = x.float()
+    a = xf.abs().max() if xf.numel() else xf.new_zeros(())
+    cur = st.amax_bits[idx: idx + 1].view(torch.float32)
+    cur.copy_(torch.maximum(cur, a.reshape(1)))
+    lim = FP8_MAX[fmt]
+    return (xf * st.scale[idx]).clamp(-lim, lim).to(_TORCH_DT[fmt])
+
+
+def _scaled_mm(a8, b8, inv_a, inv_b, bias, out_dtype):
+    """a8 [M, K] row-major @ b8 [K, N] (column-major) with per-tensor inverse
+    scales; hipBLASLt FP8 GEMM on the GPU."""
+    if a8.is_cuda:
+        return torch._scaled_mm(a8, b8, scale_a=inv_a, scale_b=inv_b, bias=bias, out_dtype=out_dtype)
+    y = (a8.float() * inv_a) @ (b8.float() * inv_b)
+    if bias is not None:
+        y = y + bias.float()
+    return y.to(out_dtype)
+
+
+def _gemm_ok(*dims) -> bool:
+    return all(d % 16 == 0 and d > 0 for d in dims)
+
+
+class _Fp8LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, mod):
+        st = mod._state(x.device)
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        out_dtype = x.dtype if x.dtype in (torch.bfloat16, torch.float16, torch.float32) else torch.bfloat16
+        x8 = cast_to_fp8(x2, st, mod._ix, "e4m3")
+        w8 = cast_to_fp8(weight, st, mod._iw, "e4m3")
+        b = bias.to(out_dtype) if bias is not None else None
+        y = _scaled_mm(x8, w8.t(), st.inv_scale[mod._ix], st.inv_scale[mod._iw], b, out_dtype)
+        ctx.save_for_backward(x8, w8)
+        ctx.mod, ctx.shape, ctx.has_bias = mod, shape, bias is not None
+        ctx.wdtype, ctx.xdtype = weight.dtype, x.dtype
+        return y.reshape(*shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x8, w8 = ctx.saved_tensors
+        mod = ctx.mod
+        st = mod._state(gy.device)
+        g2 = gy.reshape(-1, gy.shape[-1])
+        T = g2.shape[0]
+        g8 = cast_to_fp8(g2, st, mod._ig, mod.grad_fmt)
+        inv_g, inv_w, inv_x = st.inv_scale[mod._ig], st.inv_scale[mod._iw], st.inv_scale[mod._ix]
+        gdt = ctx.xdtype if ctx.xdtype in (torch.bfloat16, torch.float16, torch.float32) else torch.bfloat16
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            # dx [T, in] = g [T, out] @ w [out, in]   (w column-major: transposed copy)
+            dx = _scaled_mm(g8, w8.t().contiguous().t(), inv_g, inv_w, None, gdt).reshape(ctx.shape)
+        if ctx.needs_input_grad[1]:
+            # dw [out, in] = g^T [out, T] @ x [T, in]
+            wdt = ctx.wdtype if ctx.wdtype in (torch.bfloat16, torch.float16, torch.float32) else torch.float32
+            if _gemm_ok(T):
+                dw = _scaled_mm(g8.t().contiguous(), x8.t().contiguous().t(), inv_g, inv_x, None, wdt)
+            else:  # token count not a multiple of 16: the dequantised GEMM
+                dw = ((g8.float() * inv_g).t() @ (x8.float() * inv_x)).to(wdt)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = g2.float().sum(0).to(ctx.wdtype)
+        return dx, dw, db, None
+
+
+class Fp8Linear(nn.Module):
+    """Drop-in for ``nn.Linear`` (shares the parameters of ``linear``) whose
+    GEMMs run in FP8.  Inputs whose token count is not a multiple of 16 (or
+    no-grad calls of non-eligible shapes) use the bf16 path."""
+
+    def __init__(self, linear: nn.Linear, fp8_format: str = "HYBRID"):
+        super().__init__()
+        self.in_features, self.out_features = linear.in_features, linear.out_features
+        self.weight = linear.weight
+        self.bias = linear.bias
+        fmt = fp8_format.upper()
+        if fmt not in ("HYBRID", "E4M3"):
+            raise ValueError(f"fp8_format must be HYBRID or E4M3, not {fp8_format}")
+        self.fp8_format = fmt
+        self.grad_fmt = "e5m2" if fmt == "HYBRID" else "e4m3"
+        self._dev = None
+        self._ix = self._iw = self._ig = -1
+
+    def _state(self, device) -> Fp8State:
+        d = torch.device(device)
+        if self._dev != d:
+            st = fp8_state(d)
+            self._ix, self._iw, self._ig = st.register("e4m3"), st.register("e4m3"), st.register(self.grad_fmt)
+            self._dev = d
+        return fp8_state(d)
+
+    def forward(self, x):
+        T = x.numel() // max(1, x.shape[-1])
+        if not _gemm_ok(self.in_features, self.out_features, T):
+            return F.linear(x, self.weight, self.bias)
+        return _Fp8LinearFn.apply(x, self.weight, self.bias, self)
+
+    def extra_repr(self):
+        return f"in_features={self.in_features}, out_features={self.out_features}, fp8_format={self.fp8_format}"
+
+
+def eligible(name: str, module: nn.Module, include: Optional[Iterable[str]] = None,
+             exclude: Optional[Iterable[str]] = None) -> bool:
+    """The reference's include / exclude name filters plus the FP8 GEMM
+    shape rule (both weight dims multiples of 16, as for the transposed
+    weight of the backward)."""
+    if type(module) is not nn.Linear:
+        return False
+    if exclude and any(e in name for e in exclude):
+        return False
+    if include is not None and not any(i in name for i in include):
+        return False
+    return _gemm_ok(module.in_features, module.out_features)
+
+
+def replace_linears(model: nn.Module, include=None, exclude=None, fp8_format: str = "HYBRID") -> List[str]:
+    """Swap every eligible ``nn.Linear`` of ``model`` for an ``Fp8Linear``
+    (parameters shared, so optimizers / checkpoints see the same tensors).
+    Returns the replaced names."""
+    done = []
+    for name, mod in list(model.named_modules()):
+        for cname, child in list(mod.named_children()):
+            full = f"{name}.{cname}" if name else cname
+            if eligible(full, child, include, exclude):
+                setattr(mod, cname, Fp8Linear(child, fp8_format))
+                done.append(full)
+    return done
+
+
+def fp8_stats(device=None) -> dict:
+    st = fp8_state(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+    n = st.n
+    return {"tensors": n, "scale_min": float(st.scale[:n].min()) if n else None,
+            "scale_max": float(st.scale[:n].max()) if n else None,
+            "history": st.h, "steps": st.steps, "log2_margin": st.margin,
+            "fmax_e4m3": FP8_MAX["e4m3"], "unit_scale": math.isclose(float(st.scale[:n].mean()), 1.0) if n else None}
