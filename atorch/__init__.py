@@ -14,3 +14,14 @@ def coworker_size() -> int:
     """This framework runs no CPU co-worker processes (data preprocessing is
     done by the shm data loaders inside each rank)."""
     return 0
+
+
+def __getattr__(name):
+    # ``atorch.optimizers.AGD`` / ``atorch.auto`` etc. without an explicit
+    # submodule import, as the reference's package allows
+    import importlib
+
+    if name in ("optimizers", "auto", "distributed", "data", "modules", "utils", "trainer", "rl", "mup", "ops",
+                "local_sgd", "normalization", "fault_tolerance", "common"):
+        return importlib.import_module(f"{__name__}.{name}")
+    raise AttributeError(f"module 'atorch' has no attribute {name!r}")

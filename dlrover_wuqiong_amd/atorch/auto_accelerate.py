@@ -62,7 +62,8 @@ ORDER = ["parallel_mode", "module_replace", "half", "amp_native", "fp8", "tensor
          "context_parallel",
          "checkpoint", "mixed_parallel", "pipeline_parallel", "fsdp", "zero2", "zero1", "ddp"]
 ALIASES = {"amp": "amp_native", "amp_native_bf16": "amp_native", "fsdp2": "fsdp", "zero3": "fsdp",
-           "pipe": "pipeline_parallel", "pipeline": "pipeline_parallel", "ds_3d_parallel": "mixed_parallel", "3d_parallel": "mixed_parallel"}
+           "pipe": "pipeline_parallel", "pipeline": "pipeline_parallel", "ds_3d_parallel": "mixed_parallel",
+           "deepspeed_3d_parallel": "mixed_parallel", "3d_parallel": "mixed_parallel"}
 
 
 @dataclass
@@ -195,7 +196,11 @@ def _apply_module_replace(ctx, cfg):
 
 
 def _apply_half(ctx, cfg):
-    dtype = (cfg or {}).get("dtype", torch.bfloat16) if isinstance(cfg, dict) else torch.bfloat16
+    # ("half", "fp16" | "bf16") as in the reference, or {"dtype": ...}
+    if isinstance(cfg, str):
+        dtype = torch.float16 if cfg.lower() in ("fp16", "float16", "half") else torch.bfloat16
+    else:
+        dtype = (cfg or {}).get("dtype", torch.bfloat16) if isinstance(cfg, dict) else torch.bfloat16
     ctx["model"].to(dtype)
 
 
@@ -209,6 +214,15 @@ class _AutocastModule(nn.Module):
         dev = "cuda" if torch.cuda.is_available() else "cpu"
         with torch.autocast(dev, dtype=self.dtype):
             return self.module(*a, **kw)
+
+
+def _autocast_fn(fn, dtype):
+    @functools.wraps(fn)
+    def run(*a, **kw):
+        with torch.autocast("cuda" if torch.cuda.is_available() else "cpu", dtype=dtype):
+            return fn(*a, **kw)
+
+    return run
 
 
 def _apply_amp_native(ctx, cfg):
@@ -365,7 +379,7 @@ def _apply_context_parallel(ctx, cfg):
 def _wrap_cls(ctx, cfg):
     cls = None
     if isinstance(cfg, dict):
-        cls = cfg.get("wrap_cls") or cfg.get("atorch_wrap_cls")
+        cls = cfg.get("wrap_cls") or cfg.get("wrap_class") or cfg.get("atorch_wrap_cls")
     elif isinstance(cfg, (list, tuple)):
         cls = cfg
     if cls is None:
@@ -407,6 +421,25 @@ def _apply_pipeline_parallel(ctx, cfg):
                 f"layers {[(c.start, c.end) for c in pipe.chunks]} schedule {pipe.schedule_name}")
 
 
+def _mixed_cfg(cfg) -> Dict[str, Any]:
+    """mixed_parallel config as a dict: a dict, or a config object such as
+    the reference's ``DeepSpeed3DParallelConfig`` (its ``ds_config`` -- dict
+    or JSON path -- supplies ``gradient_accumulation_steps`` as the
+    micro-batch count)."""
+    if cfg is None:
+        return {}
+    out = dict(cfg) if isinstance(cfg, dict) else {k: v for k, v in vars(cfg).items() if not k.startswith("_")}
+    ds = out.get("ds_config")
+    if isinstance(ds, str) and os.path.exists(ds):
+        import json
+
+        with open(ds) as f:
+            ds = json.load(f)
+    if isinstance(ds, dict) and "chunks" not in out and ds.get("gradient_accumulation_steps"):
+        out["chunks"] = int(ds["gradient_accumulation_steps"])
+    return out
+
+
 def _apply_mixed_parallel(ctx, cfg):
     """TP x PP x DP in one strategy (ATorch ``MixedParallelOptimization`` /
     ``ds_3d_parallel``; reference auto/opt_lib/mixed_parallel_optimization.py:32,
@@ -423,12 +456,14 @@ def _apply_mixed_parallel(ctx, cfg):
     from ..models.llama import Llama, shard_llama_state_dict
     from ..parallel.pipeline import PipelineModule
 
-    cfg = dict(cfg) if isinstance(cfg, dict) else {}
-    t, p = int(cfg.get("tensor", 1)), int(cfg.get("pipeline", 1))
+    cfg = _mixed_cfg(cfg)
     if not dist.is_initialized():
         raise RuntimeError("mixed_parallel needs torch.distributed")
     world = dist.get_world_size()
-    d = int(cfg.get("data", world // max(1, t * p)))
+    # sizes from the config, else from the parallel_mode groups
+    t = int(cfg.get("tensor") or adist.parallel_group_size("tensor") or 1)
+    p = int(cfg.get("pipeline") or adist.parallel_group_size("pipeline") or 1)
+    d = int(cfg.get("data") or world // max(1, t * p))
     if t * p * d != world:
         raise ValueError(f"mixed_parallel: tensor {t} x pipeline {p} x data {d} != world {world}")
     if adist.parallel_config() is None:
@@ -456,6 +491,7 @@ def _apply_mixed_parallel(ctx, cfg):
                                schedule=cfg.get("schedule", "1f1b"), virtual_stages=cfg.get("virtual_stages", 1),
                                group=group, embedding_group=emb_group)
         model.amp_dtype = ctx.get("amp_dtype")
+        model.batch_fn = cfg.get("batch_fn")
         ctx["pipeline"] = True
     ctx["model"] = model
     ctx["dp_group"] = adist.parallel_group("data")
@@ -513,6 +549,13 @@ def _apply_fsdp(ctx, cfg, reshard=True):
         _g, ranks = adist.parallel_group_and_ranks("data")
         mesh = DeviceMesh("cuda" if torch.cuda.is_available() else "cpu", ranks, mesh_dim_names=("data",))
     model = ctx["model"]
+    extra = {}
+    if isinstance(cfg, dict) and cfg.get("cpu_offload"):
+        # parameters, gradients and optimizer state live on the host; the
+        # optimizer step runs there (reference zero_optimization cpu_offload)
+        from torch.distributed.fsdp import CPUOffloadPolicy
+
+        extra["offload_policy"] = CPUOffloadPolicy()
     n = 0
     # activation checkpointing runs first: shard the CheckpointWrapper, not
     # the layer inside it.  FSDP(CheckpointWrapper(layer)) casts the layer
@@ -529,9 +572,9 @@ def _apply_fsdp(ctx, cfg, reshard=True):
             continue
         inner = getattr(m, "_checkpoint_wrapped_module", None)
         if isinstance(m, classes) or (inner is not None and isinstance(inner, classes)):
-            fully_shard(m, mesh=mesh, mp_policy=mp, reshard_after_forward=reshard)
+            fully_shard(m, mesh=mesh, mp_policy=mp, reshard_after_forward=reshard, **extra)
             n += 1
-    fully_shard(model, mesh=mesh, mp_policy=mp, reshard_after_forward=reshard)
+    fully_shard(model, mesh=mesh, mp_policy=mp, reshard_after_forward=reshard, **extra)
     ctx["fsdp"] = True
     ctx.pop("amp_dtype_autocast", None)
     logger.info(f"fsdp: {n} layers sharded (reshard_after_forward={reshard})")
@@ -564,6 +607,43 @@ APPLY = {"parallel_mode": _apply_parallel_mode, "module_replace": _apply_module_
          "pipeline_parallel": _apply_pipeline_parallel,
          "fsdp": _apply_fsdp, "zero2": functools.partial(_apply_fsdp, reshard=False),
          "zero1": lambda ctx, cfg: ctx.__setitem__("zero1", True), "ddp": _apply_ddp}
+
+
+_PARTITION: List[int] = []  # [rank, size] of the last auto_accelerate's data partition
+
+
+def _data_partition(ctx) -> Tuple[int, int]:
+    """(rank, size) of this process among the replicas that read distinct
+    batches: the data-parallel group, with SP groups sharing a batch and
+    zero (sharding) ranks each reading their own."""
+    init = dist.is_initialized()
+    dpg = ctx.get("dp_group")
+    dp_size = dist.get_world_size(dpg) if (init and dpg is not None) else (dist.get_world_size() if init else 1)
+    dp_rank = dist.get_rank(dpg) if (init and dpg is not None) else (dist.get_rank() if init else 0)
+    if ctx.get("sp") and init and dp_size == dist.get_world_size():
+        # the data group spans the SP groups (ATorch: SP is independent of
+        # DP): the ranks of one SP group share a batch -> one sampler
+        # replica per group (gradients still average over every rank)
+        sp = ctx["sp"][0]
+        dp_size, dp_rank = dp_size // sp, dp_rank // sp
+    zg = ctx.get("zero_group")
+    if zg is not None and dist.get_world_size(zg) > 1:
+        # zero (sharding) ranks are data parallel too: each reads its own batch
+        dp_rank = dp_rank * dist.get_world_size(zg) + dist.get_rank(zg)
+        dp_size = dp_size * dist.get_world_size(zg)
+    return dp_rank, dp_size
+
+
+def get_data_partition_rank_and_size() -> Tuple[int, int]:
+    """Data-partition (rank, size) chosen by the last ``auto_accelerate`` call
+    -- what a user-built DataLoader's sampler needs (reference:
+    atorch/atorch/auto/model_context.py ``get_data_partition_rank_and_size``).
+    Before any call: the global rank / world size."""
+    if _PARTITION:
+        return _PARTITION[0], _PARTITION[1]
+    if dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
 
 
 def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=None, prepare_input=None,
@@ -606,7 +686,7 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
         have = set(strategy.names())
         strategy = Strategy.from_spec(strategy.opts + [(n, None) for n in included if n not in have])
     if world > 1 and "mixed_parallel" in strategy.names() and "parallel_mode" not in strategy.names():
-        mcfg = strategy.config("mixed_parallel") or {}
+        mcfg = _mixed_cfg(strategy.config("mixed_parallel"))
         t, p = int(mcfg.get("tensor", 1)), int(mcfg.get("pipeline", 1))
         dims = [("tensor", t), ("pipeline", p), ("data", int(mcfg.get("data", world // max(1, t * p))))]
         strategy = Strategy.from_spec([("parallel_mode", (dims, None))] + strategy.opts)
@@ -685,25 +765,11 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
             logger.warning("fp8: optimizer has no step hooks; call ops.fp8.fp8_update() after each step")
     sched = lr_scheduler_cls(optim, **(lr_scheduler_args or {})) if (lr_scheduler_cls and optim) else None
 
+    dp_rank, dp_size = _data_partition(ctx)
+    _PARTITION[:] = [dp_rank, dp_size]
     dataloader = None
     if dataset is not None:
         dl_args = dict(dataloader_args or {})
-        dpg = ctx.get("dp_group")
-        dp_size = dist.get_world_size(dpg) if (dist.is_initialized() and dpg is not None) else \
-            (dist.get_world_size() if dist.is_initialized() else 1)
-        dp_rank = dist.get_rank(dpg) if (dist.is_initialized() and dpg is not None) else \
-            (dist.get_rank() if dist.is_initialized() else 0)
-        if ctx.get("sp") and dist.is_initialized() and dp_size == dist.get_world_size():
-            # the data group spans the SP groups (ATorch: SP is independent of
-            # DP): the ranks of one SP group share a batch -> one sampler
-            # replica per group (gradients still average over every rank)
-            sp = ctx["sp"][0]
-            dp_size, dp_rank = dp_size // sp, dp_rank // sp
-        zg = ctx.get("zero_group")
-        if zg is not None and dist.get_world_size(zg) > 1:
-            # zero (sharding) ranks are data parallel too: each reads its own batch
-            dp_rank = dp_rank * dist.get_world_size(zg) + dist.get_rank(zg)
-            dp_size = dp_size * dist.get_world_size(zg)
         if dp_size > 1:
             bs = dl_args.get("batch_size", 1)
             dl_args["batch_size"] = max(1, bs // dp_size)  # batch_size is the global batch
@@ -714,6 +780,10 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
                                      shuffle=dl_args.pop("shuffle", True), seed=sampler_seed)
         dataloader = torch.utils.data.DataLoader(dataset, **dl_args)
 
+    if loss_func is not None and ctx.get("amp_dtype") is not None:
+        # the loss runs under the same autocast as the forward (reference
+        # amp_optimization.py:73-78): mixed bf16 outputs / fp32 labels
+        loss_func = _autocast_fn(loss_func, ctx["amp_dtype"])
     prep = prepare_input or _default_prepare_input
     if ctx.get("sp") and ctx["sp"][2] is not None:
         sp_size, sp_rank, sp_fn = ctx["sp"]

@@ -85,6 +85,30 @@ class AtorchTrainingArgs(TrainingArguments):
     async_save: bool = field(default=True, metadata={"help": "persist flash checkpoints asynchronously"})
     shuffle: bool = field(default=True, metadata={"help": "shuffle the training data"})
     skip_if_nonfinite: bool = field(default=True, metadata={"help": "skip steps with non-finite grad norm"})
+    # the rest of the reference's AtorchArguments (trainer/atorch_args.py:21-190)
+    ignore_dryrun_on_load_strategy: bool = field(default=True, metadata={"help": "no dry run of a loaded strategy"})
+    save_load_by_streaming: bool = field(default=False, metadata={"help": "accepted; saves stream through the "
+                                                                          "flash-checkpoint engine anyway"})
+    save_base_model: bool = field(default=False, metadata={"help": "PEFT: also save the base model"})
+    use_atorch_dataloader: bool = field(default=True, metadata={"help": "dataloader built by auto_accelerate"})
+    distributed_sampler_cls: Optional[Callable] = field(default=None, metadata={"help": "custom sampler class"})
+    excluded: Optional[List[str]] = field(default=None, metadata={"help": "optimizations never used"})
+    included: Optional[List[str]] = field(default=None, metadata={"help": "optimizations always used"})
+    finetune_strategy: bool = field(default=False, metadata={"help": "accepted (no strategy search on load)"})
+    save_strategy_to_file: Optional[str] = field(default=None, metadata={"help": "write the strategy as JSON"})
+    use_default_data_collator: bool = field(default=False, metadata={"help": "pad batches with "
+                                                                              "DataCollatorWithPadding"})
+    ignore_write_errors: bool = field(default=False, metadata={"help": "log and continue on checkpoint write errors"})
+    atorch_lr_scheduler_type: Optional[str] = field(default=None, metadata={"help": "overrides lr_scheduler_type"})
+    cpu_offload: bool = field(default=False, metadata={"help": "FSDP: parameters / optimizer state on the host"})
+    use_orig_params: bool = field(default=True, metadata={"help": "FSDP2 always keeps the original parameters"})
+    wrap_trainable_outmost: bool = field(default=False, metadata={"help": "accepted"})
+    sync_module_states: bool = field(default=True, metadata={"help": "FSDP: broadcast rank 0's initial weights"})
+    limit_all_gathers: bool = field(default=True, metadata={"help": "accepted (FSDP2 bounds all-gathers itself)"})
+    forward_prefetch: bool = field(default=True, metadata={"help": "accepted (FSDP2 prefetches the next layer)"})
+    max_shard_size: str = field(default="10GB", metadata={"help": "save_pretrained shard size"})
+    logit_names: Optional[List[str]] = field(default=None, metadata={"help": "output keys holding the logits"})
+    logit_index: int = field(default=-1, metadata={"help": "tuple-output index of the logits"})
 
     def __post_init__(self):
         if not self.report_to:
@@ -155,9 +179,15 @@ class AtorchTrainer:
         if a.atorch_checkpoint_cls:
             s.append(("checkpoint", {"wrap_cls": tuple(a.atorch_checkpoint_cls)}))
         opt = (a.atorch_opt or "none").lower()
-        if opt in ("fsdp", "zero2", "zero1", "ddp"):
-            cfg = {"wrap_cls": tuple(a.atorch_wrap_cls)} if (a.atorch_wrap_cls and opt in ("fsdp", "zero2")) else None
-            s.append((opt, cfg) if cfg else opt)
+        if opt in ("fsdp", "zero2"):
+            cfg = {"sync_module_states": a.sync_module_states, "use_orig_params": a.use_orig_params,
+                   "limit_all_gathers": a.limit_all_gathers, "forward_prefetch": a.forward_prefetch,
+                   "cpu_offload": a.cpu_offload}
+            if a.atorch_wrap_cls:
+                cfg["wrap_cls"] = tuple(a.atorch_wrap_cls)
+            s.append((opt, cfg))
+        elif opt in ("zero1", "ddp"):
+            s.append(opt)
         return s
 
     def _atorch_init(self):
@@ -175,15 +205,26 @@ class AtorchTrainer:
         dl_args = {"batch_size": a.per_device_train_batch_size * self._world_hint(), "shuffle": a.shuffle,
                    "num_workers": a.dataloader_num_workers, "drop_last": a.dataloader_drop_last,
                    "pin_memory": torch.cuda.is_available()}
+        if self.data_collator is None and a.use_default_data_collator and self.tokenizer is not None:
+            from transformers import DataCollatorWithPadding
+
+            self.data_collator = DataCollatorWithPadding(self.tokenizer)
         if self.data_collator is not None:
             dl_args["collate_fn"] = self.data_collator
         ok, res, strategy = auto_accelerate(
             self.model, optim_func if self.optimizer is None else None, dataset=self.train_dataset,
             loss_func=a.loss_func, prepare_input=a.prepare_input, model_input_format=a.model_input_format,
             optim_args=optim_args, optim_param_func=a.optim_param_func, dataloader_args=dl_args,
-            load_strategy=self._build_strategy(), sampler_seed=a.seed)
+            load_strategy=self._build_strategy(), sampler_seed=a.seed, excluded=a.excluded, included=a.included,
+            distributed_sampler_cls=a.distributed_sampler_cls)
         if not ok:
             raise RuntimeError("auto_accelerate failed")
+        if a.save_strategy_to_file and self._rank() == 0:
+            import json
+
+            with open(os.path.join(a.output_dir, a.save_strategy_to_file) if not os.path.isabs(
+                    a.save_strategy_to_file) else a.save_strategy_to_file, "w") as f:
+                json.dump([[n, repr(c) if c is not None else None] for n, c in strategy.opts], f, indent=1)
         self.model = res.model
         self.optimizer = self.optimizer or res.optim
         self.train_dataloader = res.dataloader
@@ -204,7 +245,8 @@ class AtorchTrainer:
         from transformers import get_scheduler
 
         if self.lr_scheduler is None:
-            self.lr_scheduler = get_scheduler(self.args.lr_scheduler_type, optimizer=optimizer or self.optimizer,
+            self.lr_scheduler = get_scheduler(self.args.atorch_lr_scheduler_type or self.args.lr_scheduler_type,
+                                              optimizer=optimizer or self.optimizer,
                                               num_warmup_steps=self.args.get_warmup_steps(num_training_steps),
                                               num_training_steps=num_training_steps)
         return self.lr_scheduler
@@ -349,7 +391,13 @@ class AtorchTrainer:
                 if self.control.should_evaluate and self.eval_dataset is not None:
                     self.evaluate()
                 if self.control.should_save:
-                    self._save_checkpoint()
+                    try:
+                        self._save_checkpoint()
+                    except OSError as e:
+                        if not args.ignore_write_errors:
+                            raise
+                        logger.warning(f"checkpoint write failed at step {self.state.global_step} "
+                                       f"(ignore_write_errors): {e}")
                     self.control = self.callback_handler.on_save(args, self.state, self.control)
                 if self.control.should_training_stop or self.state.global_step >= max_steps:
                     break

@@ -80,7 +80,11 @@ class MLP(nn.Module):
         self.c_proj = FusedLinear(4 * cfg.n_embd, cfg.n_embd)
 
     def forward(self, x):
-        if _FUSED_MLP and x.is_cuda:
+        if type(self.c_fc) is not FusedLinear:
+            # swapped projection (e.g. auto_accelerate fp8 -> Fp8Linear): its
+            # own GEMM with the bias, then the activation
+            return self.c_proj(bias_gelu(self.c_fc(x)))
+        if _FUSED_MLP and x.is_cuda and type(self.c_proj) is FusedLinear:
             # c_fc bias in the GEMM epilogue + GELU pass; backward: c_proj
             # dgrad GEMM, then one GELU-backward + bias-gradient pass (ops/mlp.py)
             return fused_gelu_mlp(x, self.c_fc, self.c_proj)

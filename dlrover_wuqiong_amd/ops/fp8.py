@@ -234,6 +234,10 @@ class Fp8Linear(nn.Module):
         T = x.numel() // max(1, x.shape[-1])
         if not _gemm_ok(self.in_features, self.out_features, T):
             return F.linear(x, self.weight, self.bias)
+        dt = x.device.type
+        if torch.is_autocast_enabled(dt):
+            # outputs in the autocast dtype, as the nn.Linear it replaces
+            x = x.to(torch.get_autocast_dtype(dt))
         return _Fp8LinearFn.apply(x, self.weight, self.bias, self)
 
     def extra_repr(self):
@@ -245,7 +249,7 @@ def eligible(name: str, module: nn.Module, include: Optional[Iterable[str]] = No
     """The reference's include / exclude name filters plus the FP8 GEMM
     shape rule (both weight dims multiples of 16, as for the transposed
     weight of the backward)."""
-    if type(module) is not nn.Linear:
+    if not isinstance(module, nn.Linear):  # nn.Linear and FusedLinear (ops/linear.py)
         return False
     if exclude and any(e in name for e in exclude):
         return False

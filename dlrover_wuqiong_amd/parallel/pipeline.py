@@ -616,6 +616,33 @@ class PipelineModule(nn.Module):
             self._allreduce_dp_grads()
         return loss
 
+    def train_batch(self, data_iter):
+        """DeepSpeed-engine style step (reference ds_3d_llama2.py:
+        ``loss = model.train_batch(data_iter)``): pulls ``num_microbatches``
+        micro-batches, maps each through ``batch_fn`` (default: a dict's
+        ``input_ids`` / ``labels``, or an ``(ids, targets)`` pair; a
+        ``((ids, ...), (targets, ...))`` result keeps the first of each) and
+        runs one pipeline step over their concatenation."""
+        ids, tgts = [], []
+        for _ in range(self.num_microbatches):
+            i, t = self._split_batch(next(data_iter))
+            ids.append(i)
+            tgts.append(t)
+        return self.train_step(torch.cat(ids), torch.cat(tgts))
+
+    def _split_batch(self, data):
+        fn = getattr(self, "batch_fn", None)
+        if fn is not None:
+            data = fn(data)
+        if isinstance(data, dict):
+            return data["input_ids"], data["labels"]
+        i, t = data
+        if isinstance(i, (tuple, list)):
+            i = i[0]
+        if isinstance(t, (tuple, list)):
+            t = t[0]
+        return i, t
+
     def _allreduce_dp_grads(self, bucket_bytes: int = 128 << 20):
         """Average stage gradients over the data-parallel group in coalesced
         buckets (one flat copy per bucket; ``FlatDDP`` avoids even that)."""
