@@ -1,0 +1,113 @@
+"""The user-facing examples (mirrors of the reference's atorch/examples and
+examples/pytorch) run end to end on CPU / gloo with tiny configs: they are
+the switching guide, so they must keep working as the APIs evolve."""
+
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from conftest import free_port
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EX = os.path.join(REPO, "examples")
+
+
+def _run(args, cwd, nproc=1, timeout=300):
+    env = dict(os.environ, PYTHONPATH=REPO, CUDA_VISIBLE_DEVICES="")
+    if nproc > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", str(nproc), "--master-addr",
+               "127.0.0.1", "--master-port", str(free_port())] + args
+    else:
+        cmd = [sys.executable] + args
+    p = subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    return p.stdout
+
+
+def _losses(out):
+    m = re.search(r"first_loss=([\d.]+) last_loss=([\d.]+)", out)
+    assert m, out[-2000:]
+    return float(m.group(1)), float(m.group(2))
+
+
+@pytest.mark.parametrize("flags", [
+    ["--model_type", "toy", "--load_strategy", "--epoch", "1"],
+    ["--model_type", "toy", "--user_created_dataloader", "--optim_grouped_params", "--max_steps", "6"],
+    ["--model_type", "toy", "--load_strategy", "--use_fp8", "--batchsize", "16", "--max_steps", "6"],
+    ["--model_type", "gpt2", "--load_strategy", "--use_checkpointing", "--use_amp", "--max_steps", "4",
+     "--layer_num", "2"],
+])
+def test_auto_accelerate_example_single(flags):
+    out = _run(["train.py"] + flags, os.path.join(EX, "auto_accelerate"))
+    first, last = _losses(out)
+    assert last == last and first == first
+    if flags[1] == "toy":
+        assert last < first
+
+
+def test_auto_accelerate_example_fsdp_two_ranks():
+    out = _run(["train.py", "--model_type", "llama", "--distributed", "--load_strategy", "--use_fsdp",
+                "--use_module_replace", "--max_steps", "3", "--layer_num", "2", "--log_interval", "1"],
+               os.path.join(EX, "auto_accelerate"), nproc=2)
+    assert "strategy: ['parallel_mode', 'module_replace', 'fsdp']" in out, out[-2000:]
+    _losses(out)
+
+
+def test_llama2_fsdp_example():
+    out = _run(["fsdp_llama2.py", "--max_steps", "3", "--gradient_checkpointing"], os.path.join(EX, "llama2"))
+    assert out.count("iter ") == 3
+
+
+def test_llama2_3d_example_tp2_pp2():
+    out = _run(["ds_3d_llama2.py", "--model_parallel_size", "2", "--pipeline_parallel_size", "2", "--max_steps",
+                "3", "--num_layers", "4"], os.path.join(EX, "llama2"), nproc=4)
+    assert "3D parallel: tensor 2, pipeline 2, data 1" in out
+    losses = [float(x) for x in re.findall(r"iter \d+: loss ([\d.]+)", out)]
+    assert len(losses) == 3 and all(0 < x < 20 for x in losses), out[-2000:]
+
+
+def test_nanogpt_example_saves_and_resumes(tmp_path):
+    ck = str(tmp_path / "ck")
+    cwd = os.path.join(EX, "nanogpt")
+    out = _run(["train.py", "--max_iters", "4", "--save_memory_interval", "2", "--save_storage_interval", "4",
+                "--save_dir", ck], cwd)
+    assert "flash save (memory) step 4" in out
+    assert open(os.path.join(ck, "dlrover_latest.txt")).read().strip() == "4"
+    # a fresh process resumes at the persisted step, then LoRA fine-tunes on top
+    out = _run(["train.py", "--max_iters", "6", "--save_memory_interval", "100", "--save_storage_interval", "100",
+                "--save_dir", ck, "--lora_rank", "4", "--lora_targets", "c_attn"], cwd)
+    assert "resumed at step 4" in out and "LoRA" in out and "iter 6:" in out, out[-2000:]
+
+
+def test_lora_adapter_semantics():
+    from dlrover_wuqiong_amd.atorch.lora import apply_lora, lora_state_dict, merge_lora
+    from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
+
+    torch.manual_seed(0)
+    m = GPT2(GPT2Config.named("gpt2-tiny"))
+    base_sd = {k: v.clone() for k, v in m.state_dict().items()}
+    x = torch.randint(0, 1024, (2, 17))
+    y0 = m(x).detach()
+    names = apply_lora(m, ["c_attn", "c_fc"], rank=4, alpha=8)
+    assert len(names) == 4 and torch.allclose(m(x), y0)  # B = 0: identical at start
+    trainable = [n for n, p in m.named_parameters() if p.requires_grad]
+    assert trainable and all("lora_" in n for n in trainable)
+    opt = torch.optim.AdamW([p for p in m.parameters() if p.requires_grad], lr=1e-2)
+    for _ in range(3):
+        m(x[:, :-1], x[:, 1:]).backward()
+        opt.step()
+        opt.zero_grad()
+    y1 = m(x).detach()
+    assert not torch.allclose(y1, y0)
+    merge_lora(m)
+    assert torch.allclose(m(x), y1, atol=1e-5)
+    assert set(lora_state_dict(m)) == {f"{n}.lora_{s}" for n in names for s in "AB"}
+    # a plain checkpoint loads into an adapted model
+    m2 = GPT2(GPT2Config.named("gpt2-tiny"))
+    apply_lora(m2, ["c_attn"])
+    m2.load_state_dict(base_sd)
+    assert torch.allclose(m2(x), y0)
