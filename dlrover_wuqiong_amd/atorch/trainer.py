@@ -43,7 +43,7 @@ import re
 import shutil
 import time
 from dataclasses import dataclass, field
-from typing import Any, Callable, Dict, List, Optional, Tuple
+from typing import Any, Callable, Dict, List, NamedTuple, Optional, Tuple
 
 import numpy as np
 import torch
@@ -114,6 +114,20 @@ class AtorchTrainingArgs(TrainingArguments):
         if not self.report_to:
             self.report_to = []
         super().__post_init__()
+
+
+class TrainResult(NamedTuple):
+    """HF ``TrainOutput`` (``.global_step``, ``.training_loss``, ``.metrics``)
+    that also answers ``result["train_loss"]`` / ``result["global_step"]``."""
+
+    global_step: int
+    training_loss: float
+    metrics: Dict[str, Any]
+
+    def __getitem__(self, k):
+        if isinstance(k, str):
+            return self.metrics[k]
+        return tuple.__getitem__(self, k)
 
 
 def _count_params(model: nn.Module) -> Tuple[int, int]:
@@ -222,8 +236,10 @@ class AtorchTrainer:
         if a.save_strategy_to_file and self._rank() == 0:
             import json
 
-            with open(os.path.join(a.output_dir, a.save_strategy_to_file) if not os.path.isabs(
-                    a.save_strategy_to_file) else a.save_strategy_to_file, "w") as f:
+            path = a.save_strategy_to_file if os.path.isabs(a.save_strategy_to_file) else \
+                os.path.join(a.output_dir, a.save_strategy_to_file)
+            os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+            with open(path, "w") as f:
                 json.dump([[n, repr(c) if c is not None else None] for n, c in strategy.opts], f, indent=1)
         self.model = res.model
         self.optimizer = self.optimizer or res.optim
@@ -410,7 +426,7 @@ class AtorchTrainer:
         metrics = {"train_runtime": round(runtime, 4), "train_loss": float(tr_loss) / max(1, self.state.global_step),
                    "global_step": self.state.global_step}
         self.control = self.callback_handler.on_train_end(args, self.state, self.control)
-        return metrics
+        return TrainResult(self.state.global_step, metrics["train_loss"], metrics)
 
     def log(self, logs: Dict[str, float]):
         logs = {k: v for k, v in logs.items() if v is not None}

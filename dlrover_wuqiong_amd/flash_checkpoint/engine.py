@@ -21,6 +21,7 @@ Replicated vs sharded state:
 """
 
 import gc
+import hashlib
 import os
 import threading
 import time
@@ -139,6 +140,9 @@ class CheckpointEngine(ABC):
             raise RuntimeError("checkpoint engine created in a deep standby before standby_point()")
         _LocalSaverThread.ensure()
         self.checkpoint_dir = checkpoint_dir
+        # this job's id in the shm header: 63-bit hash of the checkpoint dir
+        self._owner_id = int.from_bytes(hashlib.blake2b(os.path.realpath(checkpoint_dir or ".").encode(),
+                                                        digest_size=8).digest(), "little") >> 1 or 1
         self.storage = storage or get_checkpoint_storage()
         self._save_timeout = save_timeout
         self._replicated = replicated
@@ -294,7 +298,7 @@ class CheckpointEngine(ABC):
                 self._ctl_barrier()
                 if self._local_rank == 0:
                     h.close()
-                    h.init_shared_memory(create=True, size=total)
+                    h.init_shared_memory(create=True, size=total, owner=self._owner_id)
                 self._ctl_barrier()
                 if self._local_rank != 0:
                     h.close()
@@ -303,7 +307,7 @@ class CheckpointEngine(ABC):
                 self._next_slot = None
         elif need_resize:
             h.close()
-            h.init_shared_memory(create=True, size=total)
+            h.init_shared_memory(create=True, size=total, owner=self._owner_id)
             self._generation += 1
             self._next_slot = None
         key = (h.shared_memory.ino if h.shared_memory is not None else -1, total)
@@ -721,10 +725,20 @@ class CheckpointEngine(ABC):
         h = self._shm_handler
         holds = self._replicated or self._local_rank == self.local_shard_id
         complete = h.complete_steps() if holds else {}
+        foreign = bool(complete) and h.owner() not in (0, self._owner_id)
+        if foreign:
+            # another job's checkpoint in this shm namespace (same shard
+            # name, different checkpoint dir): not ours to restore; detach so
+            # the first save re-creates the segment under this job
+            logger.warning(f"rank {self._rank}: shm {h.shm_name} holds another job's checkpoints "
+                           f"(steps {sorted(complete)}); ignored")
+            self._quiesce_shm_users()
+            h.close()
+            complete = {}
         lap("scan_slots")
         # a snapshot still in (standby-owned) HBM when the last worker died
         # counts too -- only for an in-place GPU restore
-        hbm_only = self._hbm_only_steps() if (holds and target is not None) else {}
+        hbm_only = self._hbm_only_steps() if (holds and target is not None and not foreign) else {}
         out = self._restore_step(h, holds, complete, hbm_only, target, lap, tb)
         if out is None:
             # the agreed step existed only in HBM and some rank's targets

@@ -5,7 +5,8 @@ Segment layout (one segment per local checkpoint shard)::
     [0, HEADER)                   header: int64 words
                                     0 magic, 1 payload bytes (per slot),
                                     2 layout generation, 3 slot stride,
-                                    4 number of slots,
+                                    4 number of slots, 5 owner (hash of the
+                                    writing job's checkpoint dir, 0 = any),
                                     8 + s*MAX_SLICES + r: step of slice r of slot s
                                     META_WORDS + 2s, +1: step / slice count of
                                       slot s's metadata (read without unpickling it)
@@ -49,6 +50,7 @@ MAGIC = 0x44574B5053484D32  # "DWKPSHM2"
 MAX_SLICES = 1024
 SLOT_ALIGN = 2 << 20
 META_WORDS = 7168  # header word index of slot 0's (metadata step, num_slices)
+OWNER_WORD = 5
 DLROVER_CKPT_CONFIG_KEY = "_DLORVER_CKPT_CONFIG"
 EVENT_QUEUE_SIZE = 16  # checkpoint events buffered between workers and the saver
 
@@ -120,15 +122,21 @@ class SharedMemoryHandler:
     def _stride(size: int) -> int:
         return (size + SLOT_ALIGN - 1) // SLOT_ALIGN * SLOT_ALIGN
 
-    def init_shared_memory(self, create: bool = False, size: int = 0) -> bool:
-        """Create (``size`` payload bytes per slot) or attach the segment."""
+    def init_shared_memory(self, create: bool = False, size: int = 0, owner: int = 0) -> bool:
+        """Create (``size`` payload bytes per slot) or attach the segment.
+        ``owner`` (create only): the writing job's id; a segment another job
+        wrote is re-created instead of reused (its steps are not ours)."""
         if self.shared_memory is not None and self.shared_memory.stale():
             self.close()  # re-created by a writer (resize): drop the old mapping
         if self.shared_memory is not None:
-            if not create or (self._header is not None and int(self._header[1]) == size):
+            if not create or (self._header is not None and int(self._header[1]) == size
+                              and self._owned_by(owner)):
                 return True
             self.close()
-        if create and self.init_shared_memory(create=False) and int(self._header[1]) == size:
+        if create and self.init_shared_memory(create=False) and int(self._header[1]) == size \
+                and self._owned_by(owner):
+            if owner:
+                self._header[OWNER_WORD] = owner
             return True  # compatible segment (e.g. from before a restart): keep its checkpoints
         self.close()
         try:
@@ -151,6 +159,7 @@ class SharedMemoryHandler:
             self._header[1] = size
             self._header[3] = self._stride(size)
             self._header[4] = self.num_slots
+            self._header[OWNER_WORD] = owner
             for m in self.metas:
                 m.set({})
         elif int(self._header[0]) != MAGIC or int(self._header[4]) != self.num_slots:
@@ -159,6 +168,12 @@ class SharedMemoryHandler:
             return False
         self._need_creation = False
         return True
+
+    def _owned_by(self, owner: int) -> bool:
+        return not owner or self._header is None or int(self._header[OWNER_WORD]) in (0, owner)
+
+    def owner(self) -> int:
+        return int(self._header[OWNER_WORD]) if self._header is not None else 0
 
     def exists(self) -> bool:
         return SharedMemory.exists(self._shm_name)

@@ -71,6 +71,27 @@ def use_hip(t: torch.Tensor) -> bool:
     return t.is_cuda
 
 
+def bf16_path(t: torch.Tensor) -> bool:
+    """Whether a bf16-only kernel takes ``t``: a bf16 GPU tensor, or an fp32
+    one inside a bf16 autocast region (``amp_native`` over fp32 weights).
+    fp32 outside autocast runs the fp32 PyTorch math instead of silently
+    dropping to bf16."""
+    if not t.is_cuda:
+        return False
+    if t.dtype == torch.bfloat16:
+        return True
+    return (t.dtype == torch.float32 and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+
+
+def bf16(*ts):
+    """Operands of a bf16 kernel: floating tensors cast to bf16 (autograd
+    tracks the cast, so fp32 parameters get fp32 gradients)."""
+    out = tuple(t.to(torch.bfloat16) if (t is not None and t.is_floating_point() and t.dtype != torch.bfloat16)
+                else t for t in ts)
+    return out if len(out) != 1 else out[0]
+
+
 def dtype_code(t: torch.Tensor) -> int:
     if t.dtype == torch.float32:
         return 0

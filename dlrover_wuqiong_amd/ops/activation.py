@@ -69,8 +69,8 @@ def _gelu_tanh_ref(x):
 
 def bias_gelu(x, bias=None):
     """gelu_tanh(x + bias) — GPT-2's MLP activation."""
-    if _hip.use_hip(x):
-        return _BiasGeluFn.apply(x, bias)
+    if _hip.bf16_path(x):
+        return _BiasGeluFn.apply(*_hip.bf16(x, bias))
     y = x + bias if bias is not None else x
     return F.gelu(y, approximate="tanh")
 
@@ -103,7 +103,7 @@ class _SwiGLUFn(torch.autograd.Function):
 
 def swiglu(x):
     """silu(x[..., :C]) * x[..., C:] for x of last dim 2C (fused gate|up)."""
-    if _hip.use_hip(x):
-        return _SwiGLUFn.apply(x)
+    if _hip.bf16_path(x):
+        return _SwiGLUFn.apply(_hip.bf16(x))
     a, b = x.chunk(2, dim=-1)
     return F.silu(a) * b

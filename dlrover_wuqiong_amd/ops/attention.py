@@ -87,8 +87,8 @@ def flash_attn_qkvpacked_func(qkv, causal: bool = True, softmax_scale=None):
     """qkv: [B, S, 3, H, D] (a fused QKV projection viewed) -> [B, S, H, D]."""
     D = qkv.shape[-1]
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(D)
-    if _hip.use_hip(qkv):
-        return _FlashAttnQKVPackedFn.apply(qkv, causal, scale)
+    if _hip.bf16_path(qkv):
+        return _FlashAttnQKVPackedFn.apply(_hip.bf16(qkv), causal, scale)
     q, k, v = qkv.unbind(2)
     return flash_attn_func(q, k, v, softmax_scale=scale, causal=causal)
 
@@ -307,7 +307,8 @@ def flash_attn_func(q, k, v, dropout_p=0.0, softmax_scale=None, causal=False, wi
            or attn_bias is not None or return_attn_probs)
     if glm_mask is not None and not causal:
         raise ValueError("glm_mask requires causal=True")
-    if _hip.use_hip(q):
+    if _hip.bf16_path(q):
+        q, k, v = _hip.bf16(q, k, v)
         if not ext:
             return _FlashAttnFn.apply(q, k, v, causal, scale)
         if q.shape[1] != k.shape[1]:
@@ -523,7 +524,8 @@ def flash_attn_varlen_func(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, ma
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(D)
     window = tuple(int(w) for w in window_size)
     ext = dropout_p > 0.0 or window != (-1, -1) or alibi_slopes is not None or return_attn_probs
-    if _hip.use_hip(q):
+    if _hip.bf16_path(q):
+        q, k, v = _hip.bf16(q, k, v)
         if not ext:
             return _FlashAttnVarlenFn.apply(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, causal,
                                             scale)

@@ -60,8 +60,8 @@ def cross_entropy(logits, target, ignore_index=-100, label_smoothing=0.0, reduct
     """``inplace_grad=True`` writes dlogits over the logits buffer in the
     backward (saves T*V*2 bytes; only valid when nothing else reads the
     logits after the loss)."""
-    if _hip.use_hip(logits):
-        return _XentFn.apply(logits, target, ignore_index, label_smoothing, reduction, inplace_grad)
+    if _hip.bf16_path(logits):
+        return _XentFn.apply(_hip.bf16(logits), target, ignore_index, label_smoothing, reduction, inplace_grad)
     out = F.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), target.reshape(-1),
                           ignore_index=ignore_index, label_smoothing=label_smoothing, reduction=reduction)
     return out.reshape(target.shape) if reduction == "none" else out

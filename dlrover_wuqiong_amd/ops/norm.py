@@ -106,29 +106,29 @@ class _AddNormFn(torch.autograd.Function):
 
 def add_layer_norm(x, res, weight, bias, eps: float = 1e-5):
     """Returns (layer_norm(x + res), x + res)."""
-    if _hip.use_hip(x):
-        return _AddNormFn.apply(x, res, weight, bias, eps, False)
+    if _hip.bf16_path(x):
+        return _AddNormFn.apply(*_hip.bf16(x, res, weight, bias), eps, False)
     h = x + res
     return F.layer_norm(h, (h.shape[-1],), weight, bias, eps), h
 
 
 def add_rms_norm(x, res, weight, eps: float = 1e-6):
     """Returns (rms_norm(x + res), x + res)."""
-    if _hip.use_hip(x):
-        return _AddNormFn.apply(x, res, weight, None, eps, True)
+    if _hip.bf16_path(x):
+        return _AddNormFn.apply(*_hip.bf16(x, res, weight), None, eps, True)
     h = x + res
     return rms_norm(h, weight, eps), h
 
 
 def layer_norm(x, weight, bias, eps: float = 1e-5):
-    if _hip.use_hip(x):
-        return _NormFn.apply(x, weight, bias, eps, False)
+    if _hip.bf16_path(x):
+        return _NormFn.apply(*_hip.bf16(x, weight, bias), eps, False)
     return F.layer_norm(x, (x.shape[-1],), weight, bias, eps)
 
 
 def rms_norm(x, weight, eps: float = 1e-6):
-    if _hip.use_hip(x):
-        return _NormFn.apply(x, weight, None, eps, True)
+    if _hip.bf16_path(x):
+        return _NormFn.apply(*_hip.bf16(x, weight), None, eps, True)
     xf = x.float()
     y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
     return (y * weight.float()).to(x.dtype)
@@ -144,15 +144,16 @@ class LayerNorm(nn.Module):
         self.bias = nn.Parameter(torch.zeros(hidden, device=device, dtype=dtype)) if bias else None
 
     def forward(self, x):
-        if self.bias is None and _hip.use_hip(x):
-            zeros = torch.zeros_like(self.weight)
-            return _NormFn.apply(x, self.weight, zeros, self.eps, False)
+        if self.bias is None and _hip.bf16_path(x):
+            w = _hip.bf16(self.weight)
+            return _NormFn.apply(_hip.bf16(x), w, torch.zeros_like(w), self.eps, False)
         return layer_norm(x, self.weight, self.bias, self.eps)
 
     def add_forward(self, x, res):
         """(norm(x + res), x + res) with the residual add fused in."""
-        if self.bias is None and _hip.use_hip(x):
-            return _AddNormFn.apply(x, res, self.weight, torch.zeros_like(self.weight), self.eps, False)
+        if self.bias is None and _hip.bf16_path(x):
+            w = _hip.bf16(self.weight)
+            return _AddNormFn.apply(*_hip.bf16(x, res), w, torch.zeros_like(w), self.eps, False)
         return add_layer_norm(x, res, self.weight, self.bias, self.eps)
 
 

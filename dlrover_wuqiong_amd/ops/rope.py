@@ -86,6 +86,7 @@ def _table(t, x, pos_ids):
 
 def apply_rope(x, cos, sin, pos_ids=None):
     """x: [B, S, NH, D]; cos/sin: [>=S, D/2] (fp32; other dtypes upcast)."""
-    if _hip.use_hip(x):
+    if _hip.bf16_path(x):
+        x = _hip.bf16(x)
         return _RopeFn.apply(x, _table(cos, x, pos_ids), _table(sin, x, pos_ids), pos_ids)
     return _rope_ref(x, cos, sin, 1.0, pos_ids)

@@ -111,3 +111,50 @@ def test_lora_adapter_semantics():
     apply_lora(m2, ["c_attn"])
     m2.load_state_dict(base_sd)
     assert torch.allclose(m2(x), y0)
+
+
+def test_optimizer_example_agd_and_wsam():
+    cwd = os.path.join(EX, "optimizer")
+    for opt, base, lr in (("vanilla", "agd", "1e-3"), ("wsam", "sgd", "0.05")):
+        out = _run(["main.py", "--optimizer", opt, "--base_optimizer", base, "--lr", lr, "--max-steps", "15",
+                    "--samples", "960"], cwd)
+        first, last = _losses(out)
+        assert last < first, (opt, base, out[-500:])
+
+
+def test_mnist_elastic_example_resumes(tmp_path):
+    ck = str(tmp_path / "ck")
+    cwd = os.path.join(EX, "mnist")
+    first = _run(["cnn_train.py", "--max_steps", "20", "--save_memory_interval", "10", "--save_storage_interval",
+                  "20", "--checkpoint_dir", ck], cwd)
+    _losses(first)
+    out = _run(["cnn_train.py", "--max_steps", "25", "--checkpoint_dir", ck], cwd)
+    assert "resumed at step 20" in out, out[-1500:]
+
+
+def test_atorch_trainer_example(tmp_path):
+    out_dir = str(tmp_path / "o")
+    cwd = os.path.join(EX, "llama2_trainer")
+    out = _run(["llama2_clm_atorch_trainer.py", "--output_dir", out_dir, "--max_steps", "4", "--save_steps", "2",
+                "--lora_rank", "4"], cwd)
+    assert "global_step=4" in out, out[-1500:]
+    for f in ("model.safetensors", "adapter.pt", "strategy.json", "checkpoint-4"):
+        assert os.path.exists(os.path.join(out_dir, f)), f
+
+
+def test_shm_checkpoint_of_another_job_is_ignored(tmp_path):
+    """Two jobs in one shm namespace (no launcher run id): the second never
+    restores the first one's in-memory checkpoint."""
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+
+    m = torch.nn.Linear(8, 8)
+    a = DdpCheckpointer(str(tmp_path / "job_a"))
+    assert a.save_checkpoint(5, {"model": m.state_dict(), "step": 5}, storage_type=StorageType.MEMORY)
+    got = a.load_checkpoint()
+    assert got.get("step") == 5
+    a.close() if hasattr(a, "close") else None
+    b = DdpCheckpointer(str(tmp_path / "job_b"))
+    assert not b.load_checkpoint()  # foreign shm ignored, nothing on storage
+    assert b.save_checkpoint(7, {"model": m.state_dict(), "step": 7}, storage_type=StorageType.MEMORY)
+    assert b.load_checkpoint().get("step") == 7
