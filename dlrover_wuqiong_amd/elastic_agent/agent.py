@@ -465,17 +465,34 @@ class ElasticTrainingAgent:
                     pass
         self._standby = {}
 
-    @staticmethod
-    def _teardown_overlap_ok() -> bool:
+    def _job_pids(self) -> List[int]:
+        pids = [w.proc.pid for w in self.workers if w.proc.poll() is None]
+        return pids + [p.pid for p in self._standby.values() if p.poll() is None]
+
+    def _sample_gpu_pdevs(self):
+        """Remember which GPUs (PCI addresses) this node's workers / standbys
+        hold open: the teardown-overlap decision looks at those only."""
+        from .monitor import ResourceMonitor
+
+        found = ResourceMonitor.process_gpu_pdevs(self._job_pids())
+        if found:
+            self._gpu_pdevs = found
+
+    def _teardown_overlap_ok(self) -> bool:
         """May new workers start while the old ones are still exiting?  Yes
-        when every GPU of the node uses at most DWAMD_OVERLAP_TEARDOWN_MAX_USED
-        (default 0.5: a second copy fits) of its HBM right now (amdgpu sysfs: the agent never
-        initialises HIP); no readable GPU -> wait."""
+        when every GPU this job uses (its processes' DRM fds; all GPUs of the
+        host if unknown) uses at most DWAMD_OVERLAP_TEARDOWN_MAX_USED (default
+        0.5: a second copy fits) of its HBM right now (amdgpu sysfs: the agent
+        never initialises HIP); no readable GPU -> wait."""
         from .monitor import ResourceMonitor
 
         frac = float(os.getenv("DWAMD_OVERLAP_TEARDOWN_MAX_USED", "0.5"))
-        stats = ResourceMonitor.gpu_stats()
-        return bool(stats) and all(g.used_memory_mb <= frac * g.total_memory_mb for g in stats)
+        pdevs = getattr(self, "_gpu_pdevs", None)
+        stats = ResourceMonitor.gpu_stats(pdevs)
+        ok = bool(stats) and all(g.used_memory_mb <= frac * g.total_memory_mb for g in stats)
+        logger.info(f"teardown overlap {'on' if ok else 'off'}: GPUs {sorted(pdevs) if pdevs else 'all'} used "
+                    f"{[round(g.used_memory_mb / max(1, g.total_memory_mb), 2) for g in stats]}")
+        return ok
 
     def _stop_workers(self, timeout: Optional[float] = None, wait: bool = True):
         """SIGTERM every live worker group, SIGKILL after ``timeout``.
@@ -622,6 +639,10 @@ class ElasticTrainingAgent:
                     and time.time() - self._workers_started_at > self.config.standby_delay):
                 self._spawn_standbys()
             res = self._monitor_workers()
+            now = time.time()
+            if now - getattr(self, "_pdev_sampled_at", 0.0) > 5.0 and res.state == RunResult.HEALTHY:
+                self._pdev_sampled_at = now
+                self._sample_gpu_pdevs()
             if res.state == RunResult.SUCCEEDED:
                 self._event("succeeded")
                 self._discard_standbys()

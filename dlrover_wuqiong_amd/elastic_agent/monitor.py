@@ -12,7 +12,7 @@ import json
 import os
 import threading
 import time
-from typing import List, Tuple
+from typing import Iterable, List, Optional, Set, Tuple
 
 from ..common.comm import GPUStats
 from ..common.constants import ConfigPath
@@ -37,9 +37,14 @@ class ResourceMonitor:
         return cpu, int(mem)
 
     @staticmethod
-    def gpu_stats() -> List[GPUStats]:
+    def gpu_stats(pdevs: Optional[Set[str]] = None) -> List[GPUStats]:
+        """amdgpu sysfs counters of every GPU of the host, or only of the
+        ``pdevs`` PCI addresses (e.g. ``process_gpu_pdevs`` of this job's
+        processes: other tenants' GPUs on a shared host do not count)."""
         out = []
         for i, dev in enumerate(sorted(glob.glob("/sys/class/drm/card*/device"))):
+            if pdevs and os.path.basename(os.path.realpath(dev)) not in pdevs:
+                continue
             try:
                 total = int(open(os.path.join(dev, "mem_info_vram_total")).read())
                 used = int(open(os.path.join(dev, "mem_info_vram_used")).read())
@@ -49,6 +54,26 @@ class ResourceMonitor:
             out.append(GPUStats(index=i, total_memory_mb=total >> 20, used_memory_mb=used >> 20,
                                 gpu_utilization=busy))
         return out
+
+    @staticmethod
+    def process_gpu_pdevs(pids: Iterable[int]) -> Set[str]:
+        """PCI addresses of the GPUs the given processes hold DRM file
+        descriptors on (``drm-pdev`` of /proc/<pid>/fdinfo/*, which amdgpu
+        publishes per open render node; no HIP call)."""
+        found: Set[str] = set()
+        for pid in pids:
+            for fi in glob.glob(f"/proc/{int(pid)}/fdinfo/*"):
+                try:
+                    with open(fi) as f:
+                        txt = f.read()
+                except OSError:
+                    continue
+                if "drm-pdev" not in txt:
+                    continue
+                for line in txt.splitlines():
+                    if line.startswith("drm-pdev:"):
+                        found.add(line.split(":", 1)[1].strip())
+        return found
 
 
 class TorchTrainingMonitor:

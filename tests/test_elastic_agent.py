@@ -102,26 +102,47 @@ def test_network_check_then_train(tmp_path):
     assert _results(out)[0]["restart"] == 0
 
 
-def test_teardown_overlap_decision(monkeypatch):
+def test_teardown_overlap_decision(monkeypatch, tmp_path):
     """Import-mode replacements start during the killed processes' teardown
-    only when every GPU has room for a second copy (amdgpu sysfs numbers)."""
+    only when every GPU THIS JOB uses has room for a second copy (amdgpu
+    sysfs numbers; the job's GPUs from its processes' DRM fdinfo, so another
+    tenant's full GPU on a shared host does not block the overlap)."""
     from dlrover_wuqiong_amd.common.comm import GPUStats
     from dlrover_wuqiong_amd.elastic_agent import monitor
     from dlrover_wuqiong_amd.elastic_agent.agent import ElasticTrainingAgent
 
-    def stats(*used):
-        return lambda: [GPUStats(index=i, total_memory_mb=1000, used_memory_mb=u, gpu_utilization=0.0)
-                        for i, u in enumerate(used)]
+    seen = []
 
+    def stats(*used):
+        def f(pdevs=None):
+            seen.append(pdevs)
+            rows = [GPUStats(index=i, total_memory_mb=1000, used_memory_mb=u, gpu_utilization=0.0)
+                    for i, u in enumerate(used)]
+            return rows[:1] if pdevs else rows  # "our" GPU is card 0
+        return f
+
+    agent = ElasticTrainingAgent.__new__(ElasticTrainingAgent)
     monkeypatch.setattr(monitor.ResourceMonitor, "gpu_stats", staticmethod(stats(300, 450)))
-    assert ElasticTrainingAgent._teardown_overlap_ok()
+    assert agent._teardown_overlap_ok()
     monkeypatch.setattr(monitor.ResourceMonitor, "gpu_stats", staticmethod(stats(300, 600)))
-    assert not ElasticTrainingAgent._teardown_overlap_ok()
+    assert not agent._teardown_overlap_ok()  # job GPUs unknown: every GPU counts
+    agent._gpu_pdevs = {"0000:05:00.0"}
+    assert agent._teardown_overlap_ok() and seen[-1] == {"0000:05:00.0"}
+    del agent._gpu_pdevs
     monkeypatch.setattr(monitor.ResourceMonitor, "gpu_stats", staticmethod(stats()))
-    assert not ElasticTrainingAgent._teardown_overlap_ok()  # nothing readable: wait
+    assert not agent._teardown_overlap_ok()  # nothing readable: wait
     monkeypatch.setenv("DWAMD_OVERLAP_TEARDOWN_MAX_USED", "0.7")
     monkeypatch.setattr(monitor.ResourceMonitor, "gpu_stats", staticmethod(stats(600)))
-    assert ElasticTrainingAgent._teardown_overlap_ok()
+    assert agent._teardown_overlap_ok()
+    # fdinfo parsing: drm-pdev lines of a process's open DRM fds
+    fd = tmp_path / "fdinfo"
+    fd.mkdir()
+    (fd / "7").write_text("pos:\t0\ndrm-driver:\tamdgpu\ndrm-pdev:\t0000:75:00.0\ndrm-memory-vram:\t1 KiB\n")
+    (fd / "8").write_text("pos:\t0\nflags:\t02\n")
+    real_glob = monitor.glob.glob
+    monkeypatch.setattr(monitor.glob, "glob", lambda pat: real_glob(str(fd / "*")) if "fdinfo" in pat
+                        else real_glob(pat))
+    assert monitor.ResourceMonitor.process_gpu_pdevs([1234]) == {"0000:75:00.0"}
 
 
 def test_import_standby_helpers_without_gpu(monkeypatch):
