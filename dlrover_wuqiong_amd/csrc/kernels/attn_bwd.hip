@@ -53,15 +53,13 @@ __device__ __forceinline__ u32x4 scaled8(const u32x4& v, float c) {
 
 // row r0 + 8(j>>2) + 4h + (j&3), matching the k order of a packed 32x32
 // accumulator used as the B operand.  Two ds_read_b64_tr_b16 per fragment.
+// (r0 a multiple of 16, d0 of 32; tr[p] = tr_lane<D>(lane, p), attn_common.h)
 template <int D>
-__device__ __forceinline__ u32x4 tr_frag(const char* img, int r0, int d0, int lane) {
-  const int g4 = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3, h = lane >> 5;
-  const int row = r0 + 4 * h + tq;
-  const int ch = (d0 + 16 * (g4 & 1)) / 8 + (tp >> 1);
+__device__ __forceinline__ u32x4 tr_frag(const char* img, int r0, int d0, const int (&tr)[2]) {
   const s16x4 v0 =
-      __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)LDS_PTR(img + img_off<D>(row, ch) + 8 * (tp & 1)));
+      __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)LDS_PTR(img + tr[0] + tr_const<D>(r0, d0 / 32, 0)));
   const s16x4 v1 =
-      __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)LDS_PTR(img + img_off<D>(row + 8, ch) + 8 * (tp & 1)));
+      __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)LDS_PTR(img + tr[1] + tr_const<D>(r0, d0 / 32, 1)));
   return join_tr(v0, v1);
 }
 
@@ -239,9 +237,12 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
     if (n_it > 1) issue(1);
   }
   __syncthreads();
+  // per-lane LDS read offsets; the rest of each address is an immediate
+  const int rwl[2] = {row_lane<D>(lane, 0), row_lane<D>(lane, 1)};
+  const int trl[2] = {tr_lane<D>(lane, 0), tr_lane<D>(lane, 1)};
   if constexpr (VREG) {
 #pragma unroll
-    for (int kk = 0; kk < C::KK; ++kk) vr[kk] = *(const u32x4*)(v_img + img_off<D>(32 * wid + r, 2 * kk + hh));
+    for (int kk = 0; kk < C::KK; ++kk) vr[kk] = *(const u32x4*)(v_img + rwl[kk & 1] + row_const<D>(32 * wid, kk));
   }
 
   for (int it = 0; it < n_it; ++it) {
@@ -270,9 +271,10 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
         }
 #pragma unroll
         for (int kk = 0; kk < C::KK; ++kk) {
-          const u32x4 qa = *(const u32x4*)(ql + img_off<D>(32 * qs + r, 2 * kk + hh));
-          const u32x4 da = *(const u32x4*)(dl + img_off<D>(32 * qs + r, 2 * kk + hh));
-          const u32x4 vb = VREG ? vr[VREG ? kk : 0] : *(const u32x4*)(v_img + img_off<D>(32 * wid + r, 2 * kk + hh));
+          const u32x4 qa = *(const u32x4*)(ql + rwl[kk & 1] + row_const<D>(32 * qs, kk));
+          const u32x4 da = *(const u32x4*)(dl + rwl[kk & 1] + row_const<D>(32 * qs, kk));
+          const u32x4 vb = VREG ? vr[VREG ? kk : 0]
+                                : *(const u32x4*)(v_img + rwl[kk & 1] + row_const<D>(32 * wid, kk));
           s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(qa), as_bf(kf[kk]), s, 0, 0, 0);
           dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(da), as_bf(vb), dp, 0, 0, 0);
         }
@@ -337,12 +339,12 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                             pk2(dp[8 * s2 + 4], dp[8 * s2 + 5]), pk2(dp[8 * s2 + 6], dp[8 * s2 + 7])};
 #pragma unroll
           for (int dt = 0; dt < C::DT; ++dt) {
-            const u32x4 doT = tr_frag<D>(dl, 32 * qs + 16 * s2, 32 * dt, lane);
+            const u32x4 doT = tr_frag<D>(dl, 32 * qs + 16 * s2, 32 * dt, trl);
             dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(doT), as_bf(pf), dv[dt], 0, 0, 0);
           }
 #pragma unroll
           for (int dt = 0; dt < C::DT; ++dt) {
-            const u32x4 qT = tr_frag<D>(ql, 32 * qs + 16 * s2, 32 * dt, lane);
+            const u32x4 qT = tr_frag<D>(ql, 32 * qs + 16 * s2, 32 * dt, trl);
             dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(qT), as_bf(sf), dk[dt], 0, 0, 0);
           }
         }
@@ -551,7 +553,8 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
   write_lds(0);
   if (n_run > 1) issue_load(t_begin + 1);
   __syncthreads();
-  const int g4 = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+  const int rwl[2] = {row_lane<D>(lane, 0), row_lane<D>(lane, 1)};
+  const int trl[2] = {tr_lane<D>(lane, 0), tr_lane<D>(lane, 1)};
 
   for (int tt = 0; tt < n_run; ++tt) {
     const int t = t_begin + tt;
@@ -580,8 +583,8 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
         }
 #pragma unroll
         for (int kk = 0; kk < C::KK; ++kk) {
-          const u32x4 kf = *(const u32x4*)(kl + img_off<D>(32 * sb + r, 2 * kk + hh));
-          const u32x4 vf = *(const u32x4*)(vl + img_off<D>(32 * sb + r, 2 * kk + hh));
+          const u32x4 kf = *(const u32x4*)(kl + rwl[kk & 1] + row_const<D>(32 * sb, kk));
+          const u32x4 vf = *(const u32x4*)(vl + rwl[kk & 1] + row_const<D>(32 * sb, kk));
           s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(kf), as_bf(qf[kk]), s, 0, 0, 0);
           dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(vf), as_bf(dof[kk]), dp, 0, 0, 0);
         }
@@ -617,15 +620,9 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
         for (int s2 = 0; s2 < 2; ++s2) {
           const u32x4 pf = {pk2(s[8 * s2 + 0], s[8 * s2 + 1]), pk2(s[8 * s2 + 2], s[8 * s2 + 3]),
                             pk2(s[8 * s2 + 4], s[8 * s2 + 5]), pk2(s[8 * s2 + 6], s[8 * s2 + 7])};
-          const int kb = 32 * sb + 16 * s2 + 4 * hh + tq;
 #pragma unroll
           for (int dt = 0; dt < C::DT; ++dt) {
-            const int ch = (32 * dt + 16 * (g4 & 1)) / 8 + (tp >> 1);
-            const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_s16x4*)LDS_PTR(kl + img_off<D>(kb, ch) + 8 * (tp & 1)));
-            const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_s16x4*)LDS_PTR(kl + img_off<D>(kb + 8, ch) + 8 * (tp & 1)));
-            const u32x4 kt = join_tr(v0, v1);
+            const u32x4 kt = tr_frag<D>(kl, 32 * sb + 16 * s2, 32 * dt, trl);
             acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(kt), as_bf(pf), acc[dt], 0, 0, 0);
           }
         }

@@ -14,6 +14,41 @@ __device__ __forceinline__ int img_off(int row, int ch) {
   return (D * 16) * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
 }
 
+// img_off split into a per-lane part (computed once per kernel) and a
+// compile-time part (folded into the ds_read offset field), for the two
+// MFMA operand reads of the attention kernels -- with img_off written out
+// per read, the compiler kept ~30 per-lane offset registers and spent one
+// v_add per LDS read (~1.5 VALU per MFMA, the VALU issue slots are the
+// kernels' bound: MI355X_MICROARCH 'vector-instruction ISSUE cost').
+//  * row reads (32x32x16 A operand): lane row r = lane & 31 of the 32-row
+//    subtile at row0 (a multiple of 16), chunk 2*kk + hh:
+//      img_off(row0 + r, 2kk + hh) = row_lane(lane, kk & 1) + row_const(row0, kk)
+//  * transposed reads (ds_read_b64_tr_b16 pair of tr_frag): key rows
+//    k0 + 4hh + tq (+8 for the second read, p8), k0 a multiple of 16, d tile dt:
+//      img_off(k0 + 4hh + tq + 8p8, 4dt + 2(g4&1) + (tp>>1)) + 8(tp&1)
+//        = tr_lane(lane, p8) + tr_const(k0, dt, p8)
+template <int D>
+__device__ __forceinline__ int row_lane(int lane, int kodd) {
+  const int r = lane & 31, hh = lane >> 5;
+  return (D * 16) * (r >> 3) + 64 * (r & 7) + 16 * ((2 * kodd + hh) ^ ((r >> 2) & 3));
+}
+
+template <int D>
+__host__ __device__ constexpr int row_const(int row0, int kk) {
+  return (D * 16) * (row0 >> 3) + 512 * (kk >> 1);
+}
+
+template <int D>
+__device__ __forceinline__ int tr_lane(int lane, int p8) {
+  const int hh = lane >> 5, g4 = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  return 64 * (4 * hh + tq) + 16 * ((2 * (g4 & 1) + (tp >> 1)) ^ ((hh + 2 * p8) & 3)) + 8 * (tp & 1);
+}
+
+template <int D>
+__host__ __device__ constexpr int tr_const(int k0, int dt, int p8) {
+  return (D * 16) * ((k0 >> 3) + p8) + 512 * dt;
+}
+
 // (row, 16-byte chunk) that staged vector v (0 .. rows * D/8 - 1) carries in
 // a tile written through img_off: 8 consecutive lanes take 2 rows x 4 chunks
 // of one 8x32 subtile = 128 contiguous LDS bytes, so a ds_write_b128 lane

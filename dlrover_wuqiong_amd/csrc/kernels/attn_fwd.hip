@@ -172,7 +172,10 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   if (n_run > 1) issue_load(t_begin + 1);
   __syncthreads();
 
-  const int g4 = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+  // per-lane LDS read offsets (attn_common.h row_lane / tr_lane); the rest
+  // of every read address is a compile-time immediate
+  const int kro[2] = {row_lane<D>(lane, 0), row_lane<D>(lane, 1)};
+  const int vtr[2] = {tr_lane<D>(lane, 0), tr_lane<D>(lane, 1)};
 
   for (int tt = 0; tt < n_run; ++tt) {
     const int t = t_begin + tt;
@@ -203,7 +206,8 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
 #pragma unroll
         for (int kk = 0; kk < C::KK; ++kk)
 #pragma unroll
-          for (int sb = 0; sb < C::NSB; ++sb) kf[kk][sb] = *(const u32x4*)(kl + img_off<D>(32 * sb + r, 2 * kk + hh));
+          for (int sb = 0; sb < C::NSB; ++sb)
+            kf[kk][sb] = *(const u32x4*)(kl + kro[kk & 1] + row_const<D>(32 * sb, kk));
 #pragma unroll
         for (int kk = 0; kk < C::KK; ++kk)
 #pragma unroll
@@ -217,7 +221,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
         for (int kk = 0; kk < C::KK; ++kk)
 #pragma unroll
           for (int sb = 0; sb < C::NSB; ++sb) {
-            const u32x4 kf = *(const u32x4*)(kl + img_off<D>(32 * sb + r, 2 * kk + hh));
+            const u32x4 kf = *(const u32x4*)(kl + kro[kk & 1] + row_const<D>(32 * sb, kk));
             s[sb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf), as_bf16x8(qf[kk]), s[sb], 0, 0, 0);
           }
       }
@@ -308,14 +312,13 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
           const f32x16& a = s[sb];
           const u32x4 pf = {pack2(a[8 * s2 + 0], a[8 * s2 + 1]), pack2(a[8 * s2 + 2], a[8 * s2 + 3]),
                             pack2(a[8 * s2 + 4], a[8 * s2 + 5]), pack2(a[8 * s2 + 6], a[8 * s2 + 7])};
-          const int kb = 32 * sb + 16 * s2 + 4 * hh + tq;  // key row this lane addresses
+          const int k0 = 32 * sb + 16 * s2;  // this k-step's 16 key rows
 #pragma unroll
           for (int dt = 0; dt < C::DT; ++dt) {
-            const int ch = (32 * dt + 16 * (g4 & 1)) / 8 + (tp >> 1);
             const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_s16x4*)LDS_PTR(vl + img_off<D>(kb, ch) + 8 * (tp & 1)));
+                (lds_s16x4*)LDS_PTR(vl + vtr[0] + tr_const<D>(k0, dt, 0)));
             const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_s16x4*)LDS_PTR(vl + img_off<D>(kb + 8, ch) + 8 * (tp & 1)));
+                (lds_s16x4*)LDS_PTR(vl + vtr[1] + tr_const<D>(k0, dt, 1)));
             const u32x4 vf = join_tr(v0, v1);
             o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(vf), as_bf16x8(pf), o[dt], 0, 0, 0);
           }
