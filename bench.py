@@ -101,6 +101,9 @@ def parse(argv=None):
     p.add_argument("--no-import-fault", action="store_true",
                    help="skip the second job (failure under the default --standby-mode import)")
     p.add_argument("--import-window", type=int, default=32, help="fault-window steps of the import-mode job")
+    p.add_argument("--import-hbm-tier", action="store_true",
+                   help="import-mode job with the standby-owned HBM tier (framework default) instead of the "
+                        "reference-comparable host-shm restore")
     p.add_argument("--inject-slow-flush", type=float, default=0.0,
                    help="fault injection: from the fault window on, each shm flush sleeps this long after its "
                         "HBM snapshot (the kill then always lands mid-flush: HBM-only restore)")
@@ -166,6 +169,10 @@ def _job(a, n: int, mode: str, run_dir: str, tag: str):
     })
     if a.rehearse_shared_device:
         env["DWAMD_REHEARSE_SHARED_DEVICE"] = "1"
+    if mode == "import" and not a.import_hbm_tier:
+        # the reference's restart semantics: the replacement restores from
+        # host shm (the framework default also gives import standbys the HBM tier)
+        env["DWAMD_HBM_TIER"] = "0"
     wargs = [os.path.abspath(__file__), "--run-dir", run_dir, "--gpus", str(n), "--steps", str(a.steps),
              "--warmup", str(a.warmup), "--model", a.model, "--micro-batch", str(a.micro_batch), "--seq",
              str(a.seq), "--ckpt-interval", str(a.ckpt_interval), "--fault-window",

@@ -13,9 +13,12 @@ checkpoint shm before the first useful step.  The agent therefore keeps one
     stdin.  On (re)start the agent sends one JSON line -- worker
     environment, argv, entrypoint, log file -- and the standby turns into
     the worker in place (``runpy``, ``__main__`` semantics).  The script
-    still builds its model and restores from host shm: the reference's
-    restart semantics, minus interpreter start, imports, HIP init and the
-    pinning of the restore source.
+    still builds its model and restores: the reference's restart semantics,
+    minus interpreter start, imports, HIP init and the pinning of the restore
+    source.  Like a deep standby it owns the live worker's HBM checkpoint
+    staging buffers (HBM tier, when they fit; ``DWAMD_HBM_TIER=0``: off), so
+    a worker killed while its last snapshot was still flushing to shm
+    restores that step D2D instead of losing a checkpoint interval.
 
 ``deep`` (opt-in: ``dwamd-run --standby-mode deep``; the script must call
 :func:`standby_point`)
@@ -278,6 +281,7 @@ def _wait_command(pin: bool, ctl: str, lr: str, interval: float = 0.25) -> bytes
     while b"\n" not in buf:
         if pin:
             _prepin_checkpoint_shm()
+            _publish_hbm_staging(ctl, lr)
             if not pinned_marked and _pinned_bytes() > 0:
                 _mark(ctl, PINNED_PREFIX, lr, f"{_pinned_bytes()}\n")
                 pinned_marked = True

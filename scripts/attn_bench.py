@@ -10,17 +10,21 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dlrover_wuqiong_amd.ops.attention import flash_attn_func, flash_attn_qkvpacked_func
 
 
-def t(fn, it=20):
+def t(fn, it=20, reps=5):
+    """Median over ``reps`` runs of ``it`` back-to-back calls (ms per call)."""
     for _ in range(3):
         fn()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    s.record()
-    for _ in range(it):
-        fn()
-    e.record()
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / it
+    out = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(it):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        out.append(s.elapsed_time(e) / it)
+    return sorted(out)[reps // 2]
 
 
 def main():
