@@ -61,7 +61,10 @@ def kernels(required: bool = True):
             import torch  # noqa: F401  (bind to the HIP runtime torch loaded)
 
             path = kernels_lib_path()
-            if not os.path.exists(path) or _stale(path, "kernels"):
+            ab = os.environ.get("DWAMD_KERNELS_LIB_AB", "")  # A/B runs only (scripts/build_variant_lib.py)
+            if ab:
+                path = ab
+            elif not os.path.exists(path) or _stale(path, "kernels"):
                 try:
                     build_kernels()
                 except Exception as e:  # pragma: no cover - depends on toolchain

@@ -33,8 +33,9 @@ def sources_for(which):
     if which == "runtime":
         return sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))) + sorted(
             glob.glob(os.path.join(CSRC, "runtime", "*.h")))
+    # this file too: its compiler flags are part of what the library is
     return sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))) + sorted(
-        glob.glob(os.path.join(CSRC, "kernels", "*.h")))
+        glob.glob(os.path.join(CSRC, "kernels", "*.h"))) + [os.path.abspath(__file__)]
 
 
 def _hipcc():
@@ -117,9 +118,17 @@ def _build_runtime(verbose=False):
     return out
 
 
+# Per-file extra flags.  Attention: no SLP vectorisation -- the vectoriser
+# packs adjacent f32 multiplies / adds into v_pk_*_f32, which cost more than
+# two scalar ops when issued beside MFMAs (MI355X_MICROARCH 'price of one
+# filler'); measured GPT2-shape backward 368 -> 379 TF/s, D=128 within +-1 %
+# (profiles/r3/attn_bench_{slp,noslp}.jsonl).
+FILE_FLAGS = {"attn_bwd.hip": ["-fno-slp-vectorize"], "attn_fwd.hip": ["-fno-slp-vectorize"]}
+
+
 def _compile_hip(src):
     obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
-    deps = [src] + glob.glob(os.path.join(CSRC, "kernels", "*.h"))
+    deps = [src, os.path.abspath(__file__)] + glob.glob(os.path.join(CSRC, "kernels", "*.h"))
     if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
         return obj
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
@@ -129,8 +138,8 @@ def _compile_hip(src):
            # costs v_accvgpr_read/write copies around every softmax
            # (attention D=64: 176 extra VALU ops per 64-key tile)
            "-mllvm", "-amdgpu-mfma-vgpr-form",
-           "-Wno-unused-result", "-I", os.path.join(CSRC, "kernels"), "-c", src,
-           "-o", obj + f".tmp{os.getpid()}"]
+           "-Wno-unused-result", "-I", os.path.join(CSRC, "kernels")] + FILE_FLAGS.get(os.path.basename(src), []) + [
+           "-c", src, "-o", obj + f".tmp{os.getpid()}"]
     _run(cmd)
     os.replace(obj + f".tmp{os.getpid()}", obj)
     return obj
