@@ -471,27 +471,43 @@ class ElasticTrainingAgent:
 
     def _sample_gpu_pdevs(self):
         """Remember which GPUs (PCI addresses) this node's workers / standbys
-        hold open: the teardown-overlap decision looks at those only."""
+        hold open, and the largest worker's VRAM: the teardown-overlap
+        decision looks at those GPUs and asks for room for one more worker."""
         from .monitor import ResourceMonitor
 
-        found = ResourceMonitor.process_gpu_pdevs(self._job_pids())
+        workers = {w.proc.pid for w in self.workers if w.proc.poll() is None}
+        found, vram = ResourceMonitor.process_gpu_usage(self._job_pids())
         if found:
             self._gpu_pdevs = found
+        wv = [v for p, v in vram.items() if p in workers]
+        if wv:
+            self._worker_vram = max(wv)
 
     def _teardown_overlap_ok(self) -> bool:
-        """May new workers start while the old ones are still exiting?  Yes
-        when every GPU this job uses (its processes' DRM fds; all GPUs of the
-        host if unknown) uses at most DWAMD_OVERLAP_TEARDOWN_MAX_USED (default
-        0.5: a second copy fits) of its HBM right now (amdgpu sysfs: the agent
-        never initialises HIP); no readable GPU -> wait."""
+        """May new workers start while the old ones are still exiting (the
+        driver frees their HBM only at the end of the teardown)?  Yes when
+        every GPU this job uses (its processes' DRM fds; all GPUs of the host
+        if unknown) has free HBM for another worker of the last sampled size
+        (+ DWAMD_OVERLAP_TEARDOWN_MARGIN_GB, default 8) -- the replacement
+        may need all of it even when its standby pre-reserved part; with no
+        size known, when the GPU is at most DWAMD_OVERLAP_TEARDOWN_MAX_USED
+        (default 0.5) full.  amdgpu sysfs / fdinfo only (the agent never
+        initialises HIP); no readable GPU -> wait."""
         from .monitor import ResourceMonitor
 
-        frac = float(os.getenv("DWAMD_OVERLAP_TEARDOWN_MAX_USED", "0.5"))
         pdevs = getattr(self, "_gpu_pdevs", None)
         stats = ResourceMonitor.gpu_stats(pdevs)
-        ok = bool(stats) and all(g.used_memory_mb <= frac * g.total_memory_mb for g in stats)
-        logger.info(f"teardown overlap {'on' if ok else 'off'}: GPUs {sorted(pdevs) if pdevs else 'all'} used "
-                    f"{[round(g.used_memory_mb / max(1, g.total_memory_mb), 2) for g in stats]}")
+        need = getattr(self, "_worker_vram", 0)
+        if need > 0:
+            need_mb = (need >> 20) + int(float(os.getenv("DWAMD_OVERLAP_TEARDOWN_MARGIN_GB", "8")) * 1024)
+            ok = bool(stats) and all(g.total_memory_mb - g.used_memory_mb >= need_mb for g in stats)
+            rule = f"free >= {need_mb / 1024:.1f} GiB"
+        else:
+            frac = float(os.getenv("DWAMD_OVERLAP_TEARDOWN_MAX_USED", "0.5"))
+            ok = bool(stats) and all(g.used_memory_mb <= frac * g.total_memory_mb for g in stats)
+            rule = f"used <= {frac}"
+        logger.info(f"teardown overlap {'on' if ok else 'off'} ({rule}): GPUs {sorted(pdevs) if pdevs else 'all'} "
+                    f"free GiB {[round((g.total_memory_mb - g.used_memory_mb) / 1024, 1) for g in stats]}")
         return ok
 
     def _stop_workers(self, timeout: Optional[float] = None, wait: bool = True):

@@ -12,7 +12,7 @@ import json
 import os
 import threading
 import time
-from typing import Iterable, List, Optional, Set, Tuple
+from typing import Dict, Iterable, List, Optional, Set, Tuple
 
 from ..common.comm import GPUStats
 from ..common.constants import ConfigPath
@@ -56,11 +56,14 @@ class ResourceMonitor:
         return out
 
     @staticmethod
-    def process_gpu_pdevs(pids: Iterable[int]) -> Set[str]:
-        """PCI addresses of the GPUs the given processes hold DRM file
-        descriptors on (``drm-pdev`` of /proc/<pid>/fdinfo/*, which amdgpu
-        publishes per open render node; no HIP call)."""
+    def process_gpu_usage(pids: Iterable[int]) -> Tuple[Set[str], Dict[int, int]]:
+        """(PCI addresses of the GPUs the given processes hold DRM file
+        descriptors on, {pid: VRAM bytes}) from /proc/<pid>/fdinfo/* --
+        amdgpu publishes ``drm-pdev`` and ``drm-memory-vram`` per open render
+        node, HIP allocations included (checked on MI355X:
+        scripts/probe/drm_vram_probe.py); no HIP call."""
         found: Set[str] = set()
+        vram: Dict[int, int] = {}
         for pid in pids:
             for fi in glob.glob(f"/proc/{int(pid)}/fdinfo/*"):
                 try:
@@ -73,7 +76,19 @@ class ResourceMonitor:
                 for line in txt.splitlines():
                     if line.startswith("drm-pdev:"):
                         found.add(line.split(":", 1)[1].strip())
-        return found
+                    elif line.startswith("drm-memory-vram:"):
+                        parts = line.split()
+                        try:
+                            n = int(parts[1]) << {"KiB": 10, "MiB": 20, "GiB": 30}.get(parts[2] if len(parts) > 2
+                                                                                       else "", 0)
+                        except (IndexError, ValueError):
+                            continue
+                        vram[int(pid)] = vram.get(int(pid), 0) + n
+        return found, vram
+
+    @staticmethod
+    def process_gpu_pdevs(pids: Iterable[int]) -> Set[str]:
+        return ResourceMonitor.process_gpu_usage(pids)[0]
 
 
 class TorchTrainingMonitor:

@@ -134,15 +134,24 @@ def test_teardown_overlap_decision(monkeypatch, tmp_path):
     monkeypatch.setenv("DWAMD_OVERLAP_TEARDOWN_MAX_USED", "0.7")
     monkeypatch.setattr(monitor.ResourceMonitor, "gpu_stats", staticmethod(stats(600)))
     assert agent._teardown_overlap_ok()
+    # a sampled worker size: room for one more worker (+ margin) decides
+    monkeypatch.setenv("DWAMD_OVERLAP_TEARDOWN_MARGIN_GB", "0")
+    agent._worker_vram = 300 << 20
+    monkeypatch.setattr(monitor.ResourceMonitor, "gpu_stats", staticmethod(stats(650)))
+    assert agent._teardown_overlap_ok()  # 350 MB free >= 300
+    monkeypatch.setattr(monitor.ResourceMonitor, "gpu_stats", staticmethod(stats(750)))
+    assert not agent._teardown_overlap_ok()  # 250 MB free
+    del agent._worker_vram
     # fdinfo parsing: drm-pdev lines of a process's open DRM fds
     fd = tmp_path / "fdinfo"
     fd.mkdir()
-    (fd / "7").write_text("pos:\t0\ndrm-driver:\tamdgpu\ndrm-pdev:\t0000:75:00.0\ndrm-memory-vram:\t1 KiB\n")
+    (fd / "7").write_text("pos:\t0\ndrm-driver:\tamdgpu\ndrm-pdev:\t0000:75:00.0\ndrm-memory-vram:\t3 KiB\n")
     (fd / "8").write_text("pos:\t0\nflags:\t02\n")
     real_glob = monitor.glob.glob
     monkeypatch.setattr(monitor.glob, "glob", lambda pat: real_glob(str(fd / "*")) if "fdinfo" in pat
                         else real_glob(pat))
     assert monitor.ResourceMonitor.process_gpu_pdevs([1234]) == {"0000:75:00.0"}
+    assert monitor.ResourceMonitor.process_gpu_usage([1234])[1] == {1234: 3 << 10}
 
 
 def test_import_standby_helpers_without_gpu(monkeypatch):
