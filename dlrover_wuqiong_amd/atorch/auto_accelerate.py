@@ -596,6 +596,19 @@ def _apply_ddp(ctx, cfg):
     kw = dict(cfg) if isinstance(cfg, dict) else {}
     kw.setdefault("find_unused_parameters", ctx.get("find_unused_parameters", False))
     dev = _device()
+    eps = {getattr(m, "ep", 1) for m in ctx["model"].modules() if hasattr(m, "experts") and hasattr(m, "ep")}
+    if max(eps, default=1) > 1:
+        # expert-parallel MoE: experts differ across an EP group -- their
+        # grads go over the expert-data-parallel group, the rest through DDP
+        from ..parallel.moe_ddp import MoEDistributedDataParallel, expert_data_parallel_group
+
+        ep = max(eps)
+        edp = kw.pop("expert_dp_group", None) or expert_data_parallel_group(ep)
+        ctx["model"] = MoEDistributedDataParallel(ctx["model"], expert_dp_group=edp, process_group=dpg,
+                                                  device_ids=[dev.index] if dev.type == "cuda" else None, **kw)
+        ctx["moe_ddp"] = ctx["model"]
+        logger.info(f"ddp: MoE-aware (EP {ep}; expert grads over the expert-data-parallel group)")
+        return
     ctx["model"] = nn.parallel.DistributedDataParallel(
         ctx["model"], device_ids=[dev.index] if dev.type == "cuda" else None, process_group=dpg, **kw)
 
@@ -754,6 +767,8 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
                                  cpu_offload=lcfg.get("outer_optim_cpu_offload", False))
             logger.info(f"fsdp: local SGD over the replicate dimension (sync every "
                         f"{optim.sync_interval} steps after {optim.warmup_steps} warm-up steps)")
+    if ctx.get("moe_ddp") is not None and optim is not None:
+        ctx["moe_ddp"].attach_optimizer(getattr(optim, "optimizer", optim))
     if ctx.get("fp8") and optim is not None:
         # delayed scaling: the step's recorded amaxes become the next scales
         from ..ops.fp8 import fp8_update

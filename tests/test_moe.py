@@ -78,3 +78,72 @@ def test_moe_expert_parallel_two_ranks():
     for p in ps:
         p.join(timeout=30)
     assert res == [(0, True), (1, True)], res
+
+
+class _DenseMoE(torch.nn.Module):
+    def __init__(self, ep_group=None):
+        super().__init__()
+        from dlrover_wuqiong_amd.parallel.moe import MoELayer
+
+        self.proj = torch.nn.Linear(16, 16)
+        self.moe = MoELayer(16, 32, num_experts=4, top_k=2, ep_group=ep_group)
+
+    def forward(self, x):
+        return self.moe(self.proj(x))
+
+
+def _ddp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dlrover_wuqiong_amd.parallel.moe_ddp import MoEDistributedDataParallel, expert_data_parallel_group
+
+        torch.manual_seed(0)
+        ref = _DenseMoE()
+        xs = [torch.randn(10, 16, generator=torch.Generator().manual_seed(50 + r)) for r in range(world)]
+        # the objective: mean over the 4 data ranks of each rank's batch-mean loss
+        sum(ref(x).square().mean() for x in xs).div(world).backward()
+        ep_groups = [dist.new_group([0, 1]), dist.new_group([2, 3])]
+        ep = ep_groups[rank // 2]
+        edp = expert_data_parallel_group(2)
+        m = _DenseMoE(ep_group=ep)
+        lo = 2 * (rank % 2)
+        with torch.no_grad():
+            m.proj.load_state_dict(ref.proj.state_dict())
+            m.moe.gate.wg.weight.copy_(ref.moe.gate.wg.weight)
+            for n in ("w1", "w2", "w3"):
+                getattr(m.moe.experts, n).copy_(getattr(ref.moe.experts, n)[lo:lo + 2])
+        ddp = MoEDistributedDataParallel(m, expert_dp_group=edp)
+        opt = ddp.attach_optimizer(torch.optim.SGD(m.parameters(), lr=0.0))
+        ddp(xs[rank]).square().mean().backward()
+        opt.step()  # waits for the expert all-reduces
+        ok = torch.allclose(m.proj.weight.grad, ref.proj.weight.grad, atol=1e-5)
+        ok &= torch.allclose(m.moe.gate.wg.weight.grad, ref.moe.gate.wg.weight.grad, atol=1e-5)
+        for n in ("w1", "w2", "w3"):
+            ok &= torch.allclose(getattr(m.moe.experts, n).grad, getattr(ref.moe.experts, n).grad[lo:lo + 2],
+                                 atol=1e-5)
+        q.put((rank, bool(ok)))
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        traceback.print_exc()
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_moe_ddp_expert_grads_over_expert_dp_group_four_ranks():
+    """EP 2 x DP 2: dense grads averaged over all 4 ranks by DDP, expert
+    grads summed over the 2 replicas holding the same experts and scaled by
+    1/4 -- both equal the single-process gradient of the mean loss (plain
+    DDP over the world would average different experts together)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_ddp_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in ps)
+    for p in ps:
+        p.join(timeout=30)
+    assert res == [(r, True) for r in range(4)], res
