@@ -198,18 +198,39 @@ class Experts(nn.Module):
         return grouped_mlp(x, counts, self.w1, self.w2, self.w3, "silu" if self.w3 is not None else "gelu")
 
 
+def capacity_mask(idx: torch.Tensor, num_experts: int, capacity: int) -> torch.Tensor:
+    """[T, k] keep-mask of top-k assignments under a per-expert capacity
+    (GShard / Switch priority: every token's first choice before any second
+    choice, earlier tokens first); computed on the device."""
+    T, k = idx.shape
+    pri = idx.t().reshape(-1)  # k-major: first choices first
+    oh = F.one_hot(pri, num_experts)
+    pos = (oh.cumsum(0) * oh).sum(-1) - 1  # position of each assignment in its expert's queue
+    return (pos < capacity).view(k, T).t()
+
+
 class MoELayer(nn.Module):
-    """``num_experts`` global experts split evenly over ``ep_group``."""
+    """``num_experts`` global experts split evenly over ``ep_group``.
+
+    ``capacity_factor`` > 0: GShard / Switch capacity -- each expert takes at
+    most ceil(factor * T * k / E) assignments of a batch (T tokens on this
+    rank), the rest are dropped (their weight is 0; with a residual around
+    the layer the token passes through unchanged).  Dropped assignments go
+    to a sentinel bucket past the last expert: never sent, never computed.
+    Default 0: dropless."""
 
     def __init__(self, hidden: int, ffn: int, num_experts: int, top_k: int = 2, ep_group=None,
-                 swiglu: bool = True, dtype=None, device=None, aux_loss_coef: float = 1e-2):
+                 swiglu: bool = True, dtype=None, device=None, aux_loss_coef: float = 1e-2,
+                 capacity_factor: float = 0.0, norm_topk: bool = True):
         super().__init__()
         self.ep_group = ep_group
         self.ep = _ws(ep_group)
         assert num_experts % self.ep == 0, f"{num_experts} experts not divisible by EP {self.ep}"
         self.num_experts, self.top_k = num_experts, top_k
         self.num_local = num_experts // self.ep
-        self.gate = TopKGate(hidden, num_experts, top_k, aux_loss_coef=aux_loss_coef, dtype=dtype, device=device)
+        self.capacity_factor = float(capacity_factor)
+        self.gate = TopKGate(hidden, num_experts, top_k, aux_loss_coef=aux_loss_coef, norm_topk=norm_topk,
+                             dtype=dtype, device=device)
         self.experts = Experts(self.num_local, hidden, ffn, swiglu, dtype=dtype, device=device)
         self.aux_loss = torch.zeros(())
 
@@ -218,9 +239,15 @@ class MoELayer(nn.Module):
         x = x.reshape(-1, shape[-1])
         T, k, E = x.shape[0], self.top_k, self.num_experts
         w, idx, self.aux_loss = self.gate(x)
+        keep = None
+        if self.capacity_factor > 0:
+            cap = max(1, math.ceil(self.capacity_factor * T * k / E))
+            keep = capacity_mask(idx, E, cap)
+            idx = torch.where(keep, idx, torch.full_like(idx, E))  # sentinel bucket E
+            w = w * keep
         flat = idx.reshape(-1)
         order = torch.argsort(flat, stable=True)
-        counts = torch.bincount(flat, minlength=E)
+        counts = torch.bincount(flat, minlength=E + (keep is not None))[:E]
         xs = x.index_select(0, order // k)
         if self.ep > 1:
             send_counts = counts.view(self.ep, self.num_local)  # [dst rank, local expert]
@@ -228,18 +255,75 @@ class MoELayer(nn.Module):
             dist.all_to_all_single(recv_counts, send_counts.contiguous(), group=self.ep_group)
             # the ONE host read per layer: the all-to-all split sizes
             in_splits, out_splits = torch.stack([send_counts.sum(1), recv_counts.sum(1)]).tolist()
-            xr = all_to_all_v(xs, out_splits, in_splits, self.ep_group)
+            xr = all_to_all_v(xs[:sum(in_splits)] if keep is not None else xs, out_splits, in_splits,
+                              self.ep_group)
             # received rows are (src rank, expert)-ordered: one permutation
             # launch (device counts) groups them by local expert
             y = self.experts(moe_regroup(xr, recv_counts, 0), recv_counts.sum(0))
             y = all_to_all_v(moe_regroup(y, recv_counts, 1), in_splits, out_splits, self.ep_group)
         else:
             y = self.experts(xs, counts)  # device counts: no host sync on the GPU path
+        if keep is not None:
+            # dropped (sentinel) rows: never computed -- zero, whatever the buffer holds
+            if y.shape[0] < xs.shape[0]:
+                y = torch.cat([y, y.new_zeros(xs.shape[0] - y.shape[0], y.shape[-1])])
+            y = torch.where((flat.index_select(0, order) < E).unsqueeze(-1), y, y.new_zeros(()))
         # un-permute and combine the k expert outputs per token
         out = torch.zeros(T * k, y.shape[-1], dtype=y.dtype, device=y.device)
         out = out.index_copy(0, order, y)
         out = (out.view(T, k, -1) * w.to(y.dtype).unsqueeze(-1)).sum(1)
         return out.view(shape[:-1] + (out.shape[-1],))
+
+
+class SwitchGate(TopKGate):
+    """Switch Transformer router: top-1, the output scaled by the expert's
+    raw gate probability (reference switch_gating.py; use with a
+    ``MoELayer(top_k=1, capacity_factor=..., norm_topk=False)``)."""
+
+    def __init__(self, hidden: int, num_experts: int, **kw):
+        kw.setdefault("norm_topk", False)
+        super().__init__(hidden, num_experts, top_k=1, **kw)
+
+
+def replace_with_moe(model: nn.Module, layer_class, num_experts: int, top_k: int = 2, ep_group=None,
+                     capacity_factor: float = 0.0, noise_std: float = 0.0) -> List[str]:
+    """Sparse upcycling (reference modules/moe/inject.py ``replace_with_moe``):
+    every ``layer_class`` SwiGLU FFN of ``model`` becomes a ``MoELayer`` whose
+    experts start as copies of the dense weights (optionally + Gaussian
+    noise) and whose router starts at zero (uniform routing) -- the MoE model
+    initially computes exactly the dense model's function.  Supported FFNs:
+    this framework's ``LlamaMLP`` (fused ``gate_up_proj``) and HF-style
+    ``gate_proj`` / ``up_proj`` / ``down_proj``.  With ``ep_group`` this
+    rank keeps its slice of the experts.  Returns the replaced names."""
+    done = []
+    for name, mod in list(model.named_modules()):
+        for cname, child in list(mod.named_children()):
+            if not isinstance(child, layer_class):
+                continue
+            if hasattr(child, "gate_up_proj"):
+                gu = child.gate_up_proj.weight
+                F_ = gu.shape[0] // 2
+                gate_w, up_w = gu[:F_], gu[F_:]
+            elif hasattr(child, "gate_proj") and hasattr(child, "up_proj"):
+                gate_w, up_w = child.gate_proj.weight, child.up_proj.weight
+            else:
+                raise TypeError(f"{type(child).__name__}: not a SwiGLU FFN (gate/up/down projections)")
+            down_w = child.down_proj.weight
+            H, F_ = down_w.shape
+            moe = MoELayer(H, F_, num_experts, top_k, ep_group=ep_group, capacity_factor=capacity_factor,
+                           dtype=down_w.dtype, device=down_w.device)
+            lo = moe.num_local * (dist.get_rank(ep_group) if moe.ep > 1 else 0)
+            with torch.no_grad():
+                moe.gate.wg.weight.zero_()
+                for e in range(moe.num_local):
+                    for dst, src in ((moe.experts.w1, gate_w), (moe.experts.w3, up_w), (moe.experts.w2, down_w)):
+                        dst[e].copy_(src)
+                        if noise_std > 0:
+                            g = torch.Generator(device="cpu").manual_seed(lo + e)
+                            dst[e].add_(torch.randn(dst[e].shape, generator=g).to(dst) * noise_std)
+            setattr(mod, cname, moe)
+            done.append(f"{name}.{cname}" if name else cname)
+    return done
 
 
 def moe_aux_loss(model: nn.Module) -> torch.Tensor:

@@ -147,3 +147,50 @@ def test_moe_ddp_expert_grads_over_expert_dp_group_four_ranks():
     for p in ps:
         p.join(timeout=30)
     assert res == [(r, True) for r in range(4)], res
+
+
+def test_moe_capacity_drops_overflow_and_matches_reference():
+    """Capacity (GShard priority): dropped assignments contribute nothing,
+    kept ones equal the dropless layer's per-expert outputs."""
+    from dlrover_wuqiong_amd.parallel.moe import MoELayer, capacity_mask
+
+    idx = torch.tensor([[0, 1], [0, 2], [0, 1], [3, 0]])
+    keep = capacity_mask(idx, 4, 2)
+    # first choices in token order: t0->0, t1->0, t2->0 (3rd: dropped), t3->3;
+    # then second choices: t0->1, t1->2, t2->1, t3->0 (expert 0 full)
+    assert keep.tolist() == [[True, True], [True, True], [False, True], [True, False]]
+    torch.manual_seed(0)
+    free = MoELayer(16, 32, num_experts=4, top_k=2)
+    capped = MoELayer(16, 32, num_experts=4, top_k=2, capacity_factor=0.5)
+    capped.load_state_dict(free.state_dict())
+    x = torch.randn(24, 16, requires_grad=True)
+    y = capped(x)
+    w, idx, _ = free.gate(x)
+    keep = capacity_mask(idx, 4, 6)  # capacity ceil(0.5 * 24 * 2 / 4) = 6
+    e = free.experts
+    want = torch.zeros_like(y)
+    for t in range(24):
+        for j in range(2):
+            if keep[t, j]:
+                ex = int(idx[t, j])
+                h = torch.nn.functional.silu(x[t] @ e.w1[ex].T) * (x[t] @ e.w3[ex].T)
+                want[t] += w[t, j] * (h @ e.w2[ex].T)
+    assert int((~keep).sum()) > 0 and torch.allclose(y, want, atol=1e-5)
+    y.square().sum().backward()
+    assert torch.isfinite(x.grad).all()
+
+
+def test_replace_with_moe_upcycles_dense_ffn():
+    """Upcycled experts are copies of the dense FFN and the router starts
+    uniform: the MoE model computes the dense model's output."""
+    from dlrover_wuqiong_amd.models.llama import Llama, LlamaConfig, LlamaMLP
+    from dlrover_wuqiong_amd.parallel.moe import MoELayer, replace_with_moe
+
+    torch.manual_seed(0)
+    cfg = LlamaConfig.named("llama-tiny")
+    m = Llama(cfg)
+    ids = torch.randint(0, cfg.vocab_size, (2, 16))
+    dense = m(ids).detach()
+    names = replace_with_moe(m, LlamaMLP, num_experts=4, top_k=2)
+    assert len(names) == cfg.num_hidden_layers and all(isinstance(l.mlp, MoELayer) for l in m.layers)
+    assert torch.allclose(m(ids), dense, atol=1e-4)
