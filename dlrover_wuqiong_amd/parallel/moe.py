@@ -249,6 +249,11 @@ class MoELayer(nn.Module):
         order = torch.argsort(flat, stable=True)
         counts = torch.bincount(flat, minlength=E + (keep is not None))[:E]
         xs = x.index_select(0, order // k)
+        if keep is not None:
+            # the grouped GEMMs leave rows past the last group (the sentinel
+            # bucket) unwritten in y and dx: mask them out both ways
+            valid = (flat.index_select(0, order) < E).unsqueeze(-1)
+            xs = torch.where(valid, xs, xs.new_zeros(()))
         if self.ep > 1:
             send_counts = counts.view(self.ep, self.num_local)  # [dst rank, local expert]
             recv_counts = torch.empty_like(send_counts)
@@ -267,7 +272,7 @@ class MoELayer(nn.Module):
             # dropped (sentinel) rows: never computed -- zero, whatever the buffer holds
             if y.shape[0] < xs.shape[0]:
                 y = torch.cat([y, y.new_zeros(xs.shape[0] - y.shape[0], y.shape[-1])])
-            y = torch.where((flat.index_select(0, order) < E).unsqueeze(-1), y, y.new_zeros(()))
+            y = torch.where(valid, y, y.new_zeros(()))
         # un-permute and combine the k expert outputs per token
         out = torch.zeros(T * k, y.shape[-1], dtype=y.dtype, device=y.device)
         out = out.index_copy(0, order, y)

@@ -42,3 +42,37 @@ def test_moe_regroup_matches_reference(ep, L, H):
     e_of_row = torch.repeat_interleave(torch.arange(L, device="cuda").repeat_interleave(ep),
                                        counts.t().reshape(-1), output_size=n)
     assert torch.all(e_of_row[:-1] <= e_of_row[1:])
+
+
+@pytest.mark.parametrize("capacity_factor", [0.0, 0.5])
+def test_moe_layer_grouped_gemm_gpu_vs_fp32(capacity_factor):
+    """MoELayer on the grouped-GEMM kernels (bf16), dropless and with a
+    capacity that drops assignments (rows past the last group masked both
+    ways), vs the same layer in fp32 on the CPU per-expert path."""
+    from dlrover_wuqiong_amd.parallel.moe import MoELayer
+
+    torch.manual_seed(0)
+    ref = MoELayer(256, 512, num_experts=8, top_k=2, capacity_factor=capacity_factor)
+    m = MoELayer(256, 512, num_experts=8, top_k=2, capacity_factor=capacity_factor).cuda().bfloat16()
+    m.load_state_dict({k: v.cuda().bfloat16() for k, v in ref.state_dict().items()})
+    x = torch.randn(1024, 256)
+    xg = x.cuda().bfloat16().requires_grad_(True)
+    y = m(xg)
+    xr = x.clone().requires_grad_(True)
+    yr = ref(xr)
+    # bf16 vs fp32 gate logits may route near-ties differently (and shift the
+    # capacity queue after them): compare the tokens routed identically
+    from dlrover_wuqiong_amd.parallel.moe import capacity_mask
+
+    _w, ig, _ = m.gate(xg.detach())
+    _w, ir, _ = ref.gate(x)
+    ig = ig.cpu()
+    same = (ig == ir).all(-1)
+    if capacity_factor > 0:
+        cap = int(-(-capacity_factor * 1024 * 2 // 8))
+        same &= (capacity_mask(ig, 8, cap) == capacity_mask(ir, 8, cap)).all(-1)
+    assert same.float().mean() > 0.9, same.float().mean()
+    rel = ((y.float().cpu()[same] - yr[same]).norm() / yr[same].norm()).item()
+    assert rel < 3e-2, rel
+    y.float().square().sum().backward()
+    assert torch.isfinite(xg.grad).all() and torch.isfinite(m.experts.w1.grad.float()).all()
