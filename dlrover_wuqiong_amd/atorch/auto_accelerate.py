@@ -390,9 +390,19 @@ def _wrap_cls(ctx, cfg):
 def _apply_checkpoint(ctx, cfg):
     from torch.distributed.algorithms._checkpoint.checkpoint_wrapper import apply_activation_checkpointing
 
+    import functools as _ft
+
+    from torch.distributed.algorithms._checkpoint.checkpoint_wrapper import checkpoint_wrapper
+
+    from ..parallel.randomizer import rng_checkpoint
+
     classes = _wrap_cls(ctx, cfg)
     if classes:
-        apply_activation_checkpointing(ctx["model"], check_fn=lambda m: isinstance(m, classes))
+        # the recompute also replays the parallel randomizer / tracked RNG
+        # states (dropout inside a forked stream regenerates its mask)
+        apply_activation_checkpointing(ctx["model"], check_fn=lambda m: isinstance(m, classes),
+                                       checkpoint_wrapper_fn=_ft.partial(checkpoint_wrapper,
+                                                                         checkpoint_fn=rng_checkpoint))
         logger.info(f"checkpoint: activation checkpointing on {[c.__name__ for c in classes]}")
 
 

@@ -109,6 +109,11 @@ class MultiDimParallelRandomizer:
         return {k: {"cpu_rng": s.cpu_rng, "cuda_rng": s.cuda_rng, "offset": s.offset} for k, s in self._streams.items()}
 
     def set_states(self, states: dict):
+        """Restore a ``get_states`` snapshot.  Streams first requested after
+        the snapshot did not exist then: they go back to their initial
+        state (a checkpoint recompute replays them from the start too)."""
+        for k in [k for k in self._streams if k not in {tuple(x) for x in states}]:
+            self._streams[k] = _Stream(self._streams[k].seed)
         for k, st in states.items():
             k = tuple(k)
             if k not in self._streams:
@@ -145,5 +150,122 @@ def reset_randomizer():
     _INSTANCE = None
 
 
+# ------------------------------------------------ Megatron-style named tracker
+class CudaRNGStatesTracker:
+    """Named GPU generator states (reference activation_checkpointing.py
+    ``CudaRNGStatesTracker``): ``add(name, seed)``, ``fork(name)``,
+    ``get_states`` / ``set_states``.  On a host without a GPU the CPU
+    generator is tracked instead (the CPU / gloo execution path)."""
+
+    def __init__(self):
+        self.states_: Dict[str, torch.Tensor] = {}
+        self.seeds_ = set()
+
+    @staticmethod
+    def _get():
+        return torch.cuda.get_rng_state() if torch.cuda.is_available() else torch.get_rng_state()
+
+    @staticmethod
+    def _set(st):
+        (torch.cuda.set_rng_state if torch.cuda.is_available() else torch.set_rng_state)(st)
+
+    def reset(self):
+        self.states_, self.seeds_ = {}, set()
+
+    def get_states(self) -> Dict[str, torch.Tensor]:
+        return dict(self.states_)
+
+    def set_states(self, states: Dict[str, torch.Tensor]):
+        self.states_ = dict(states)
+
+    def add(self, name: str, seed: int):
+        if seed in self.seeds_ or name in self.states_:
+            raise RuntimeError(f"rng state {name} / seed {seed} already tracked")
+        self.seeds_.add(seed)
+        cur = self._get()
+        (torch.cuda.manual_seed if torch.cuda.is_available() else torch.manual_seed)(seed)
+        self.states_[name] = self._get()
+        self._set(cur)
+
+    @contextmanager
+    def fork(self, name: str = "model-parallel-rng"):
+        if name not in self.states_:
+            raise RuntimeError(f"rng state {name} is not tracked")
+        cur = self._get()
+        self._set(self.states_[name])
+        try:
+            yield
+        finally:
+            self.states_[name] = self._get()
+            self._set(cur)
+
+
+_TRACKER = CudaRNGStatesTracker()
+
+
+def get_cuda_rng_tracker() -> CudaRNGStatesTracker:
+    return _TRACKER
+
+
+def model_parallel_cuda_manual_seed(seed: int, group: str = "tensor"):
+    """Default generator: ``seed`` (equal across the tensor group, as the
+    replicated regions need); tracked "model-parallel-rng": seed + 2718 +
+    tensor rank (different across the tensor group, equal across data
+    replicas) for dropout inside the sharded regions."""
+    from ..atorch import distributed as adist
+
+    r = adist.parallel_rank(group) or 0
+    (torch.cuda.manual_seed if torch.cuda.is_available() else torch.manual_seed)(seed)
+    _TRACKER.reset()
+    _TRACKER.add("model-parallel-rng", seed + 2718 + r)
+
+
+# ------------------------------------------ RNG-consistent activation checkpoint
+def _rng_context():
+    """(forward, recompute) contexts for torch.utils.checkpoint: the
+    recompute replays the randomizer streams and tracked states (incl. the
+    counter offsets) exactly as the forward saw them, so dropout inside a
+    forked stream regenerates the same mask."""
+    from contextlib import nullcontext
+
+    inst = _INSTANCE
+    snap_streams = inst.get_states() if inst is not None else None
+    snap_tracker = _TRACKER.get_states()
+
+    @contextmanager
+    def recompute():
+        cur_streams = inst.get_states() if inst is not None else None
+        cur_tracker = _TRACKER.get_states()
+        if inst is not None:
+            inst.set_states(snap_streams)
+        _TRACKER.set_states(snap_tracker)
+        try:
+            yield
+        finally:
+            if inst is not None:
+                inst.set_states(cur_streams)
+            _TRACKER.set_states(cur_tracker)
+
+    return nullcontext(), recompute()
+
+
+def rng_checkpoint(function, *args, **kwargs):
+    """Non-reentrant activation checkpoint that also restores the parallel
+    randomizer / tracker states for the recompute (reference
+    ``CheckpointFunction`` / ``checkpoint``; torch's own checkpoint restores
+    only the default generators)."""
+    return torch.utils.checkpoint.checkpoint(function, *args, use_reentrant=False, context_fn=_rng_context,
+                                             **kwargs)
+
+
+def tp_wrap_fn(module: torch.nn.Module) -> torch.nn.Module:
+    """Wrap ``module`` so its forward runs under :func:`rng_checkpoint`
+    (reference ``TPCheckpointWrapper`` / ``tp_wrap_fn``)."""
+    from torch.distributed.algorithms._checkpoint.checkpoint_wrapper import checkpoint_wrapper
+
+    return checkpoint_wrapper(module, checkpoint_fn=rng_checkpoint)
+
+
 __all__ = ["MultiDimParallelRandomizer", "init_randomizer", "get_MDPRInstance", "get_randomizer",
-           "reset_randomizer"]
+           "reset_randomizer", "CudaRNGStatesTracker", "get_cuda_rng_tracker", "model_parallel_cuda_manual_seed",
+           "rng_checkpoint", "tp_wrap_fn"]

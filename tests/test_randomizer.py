@@ -74,3 +74,38 @@ def test_four_rank_parallel_randomizer():
     # different G never collide on one rank
     seeds = {by[(0, 0)][k + ("philox",)][0][0] for k in [(), ("tensor",), ("data",), ("tensor", "data")]}
     assert len(seeds) == 4
+
+
+def test_rng_checkpoint_replays_forked_streams():
+    """Dropout inside a forked randomizer stream / tracked state: the
+    checkpointed recompute regenerates the forward's masks, so gradients
+    equal the uncheckpointed ones (torch's checkpoint alone would draw new
+    masks from the advanced streams)."""
+    from dlrover_wuqiong_amd.parallel import randomizer as R
+
+    R.reset_randomizer()
+    R.init_randomizer(7, dims={"tensor": (2, 1), "data": (2, 0)})
+    tr = R.get_cuda_rng_tracker()
+    tr.reset()
+    tr.add("model-parallel-rng", 99)
+    lin = torch.nn.Linear(32, 32)
+
+    def block(x):
+        with R.get_randomizer("tensor").fork():
+            x = torch.nn.functional.dropout(lin(x), 0.5)
+        with tr.fork():
+            x = torch.nn.functional.dropout(lin(x), 0.5)
+        return x
+
+    x = torch.randn(8, 32, requires_grad=True)
+    s0 = R.get_MDPRInstance().get_states()
+    t0 = tr.get_states()
+    block(x).square().sum().backward()
+    g_ref, gx_ref = lin.weight.grad.clone(), x.grad.clone()
+    lin.weight.grad, x.grad = None, None
+    R.get_MDPRInstance().set_states(s0)
+    tr.set_states(t0)
+    R.rng_checkpoint(block, x).square().sum().backward()
+    assert torch.allclose(lin.weight.grad, g_ref) and torch.allclose(x.grad, gx_ref)
+    R.reset_randomizer()
+    tr.reset()
