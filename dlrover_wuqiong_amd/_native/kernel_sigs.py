@@ -8,7 +8,8 @@ vp, i64, i32, u32, u64, f32, cp = (c.c_void_p, c.c_int64, c.c_int, c.c_uint32, c
 SIGS = {
     # fp8.hip
     "dw_fp8_cast_amax": (i32, [vp, i32, vp, vp, vp, i64, i32, vp]),
-    "dw_fp8_update_scales": (i32, [vp, vp, vp, vp, vp, i32, i32, f32, vp]),
+    "dw_fp8_update_scales": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, f32, vp]),
+    "dw_fp8_cast_t": (i32, [vp, i32, vp, vp, vp, vp, i32, i32, i32, vp]),
     # ckpt_copy.hip
     "dw_multi_copy": (i32, [vp, i64, vp]),
     "dw_gemm_dgelu": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),

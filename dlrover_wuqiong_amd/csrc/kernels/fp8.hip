@@ -102,36 +102,155 @@ extern "C" int dw_fp8_cast_amax(const void* x, int in_bf16, const float* scale, 
   DW_LAUNCH_RET;
 }
 
-// meta arrays of m tensors: amax_bits [m] (cleared here), history [m, h]
-// (slot 0 = newest), fmax [m] (448 or 57344), scale / inv_scale [m].
-__global__ void fp8_update_scales_kernel(unsigned* __restrict__ amax_bits, float* __restrict__ hist,
-                                         const float* __restrict__ fmax_, float* __restrict__ scale,
-                                         float* __restrict__ inv_scale, int m, int h, float margin_pow2) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+// meta arrays of m tensors: amax_bits [m] (cleared here), history [m, h] as
+// a RING (slot ``head`` receives this step's amax -- no shifting), fmax [m]
+// (448 or 57344), scale / inv_scale [m].  One wave per tensor: the 64 lanes
+// stride the history (coalesced) and reduce its max in registers.  (The
+// first form -- one thread per tensor shifting h = 1024 entries serially --
+// took 121 us per step for three tensors.)
+__global__ void __launch_bounds__(256) fp8_update_scales_kernel(unsigned* __restrict__ amax_bits,
+                                                                float* __restrict__ hist,
+                                                                const float* __restrict__ fmax_,
+                                                                float* __restrict__ scale,
+                                                                float* __restrict__ inv_scale, int m, int h,
+                                                                int head, float margin_pow2) {
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (t >= m) return;
   float* hh = hist + (long long)t * h;
   const float cur = __uint_as_float(amax_bits[t]);
   float best = cur;
-  for (int j = h - 1; j > 0; --j) {
-    hh[j] = hh[j - 1];
-    best = fmaxf(best, hh[j]);
-  }
-  hh[0] = cur;
-  amax_bits[t] = 0u;
-  if (best > 0.f && best < INFINITY) {
-    const float sc = fmax_[t] / (best * margin_pow2);
-    scale[t] = sc;
-    inv_scale[t] = 1.f / sc;
-  } else if (best == INFINITY) {  // overflowed: shrink hard
-    scale[t] *= 0.5f;
-    inv_scale[t] = 1.f / scale[t];
+  for (int j = lane; j < h; j += 64)
+    if (j != head) best = fmaxf(best, hh[j]);
+  best = wave_max(best);
+  if (lane == 0) {
+    hh[head] = cur;
+    amax_bits[t] = 0u;
+    if (best > 0.f && best < INFINITY) {
+      const float sc = fmax_[t] / (best * margin_pow2);
+      scale[t] = sc;
+      inv_scale[t] = 1.f / sc;
+    } else if (best == INFINITY) {  // overflowed: shrink hard
+      scale[t] *= 0.5f;
+      inv_scale[t] = 1.f / scale[t];
+    }
   }
 }
 
 extern "C" int dw_fp8_update_scales(unsigned* amax_bits, float* hist, const float* fmax_, float* scale,
-                                    float* inv_scale, int m, int h, float margin_pow2, void* stream) {
+                                    float* inv_scale, int m, int h, int head, float margin_pow2, void* stream) {
   if (m <= 0) return 0;
-  hipLaunchKernelGGL(fp8_update_scales_kernel, dim3((m + 255) / 256), dim3(256), 0, (hipStream_t)stream, amax_bits,
-                     hist, fmax_, scale, inv_scale, m, h, margin_pow2);
+  hipLaunchKernelGGL(fp8_update_scales_kernel, dim3((m + 3) / 4), dim3(256), 0, (hipStream_t)stream, amax_bits,
+                     hist, fmax_, scale, inv_scale, m, h, head, margin_pow2);
+  DW_LAUNCH_RET;
+}
+
+// Cast + transpose in one pass: x [R, C] (bf16 / fp32, row-major) -> out
+// [R, C] fp8 and/or out_t [C, R] fp8, scaled / saturated / amax-recorded as
+// dw_fp8_cast_amax.  The FP8 GEMMs want every operand K-contiguous (A
+// row-major, B column-major), and the backward contracts over different
+// dims than the forward: the weight gradient needs x and the output
+// gradient with the TOKEN dim contiguous, dgrad needs W^T.  Writing both
+// layouts from one read replaces a separate transposed copy (torch's
+// byte-wise transpose of a float8 tensor ran at ~0.25 TB/s:
+// profiles/r3/fp8_linear_kernels.md).
+// 64x64 tiles, 256 threads: each thread converts 2 x 8 contiguous elements
+// (16-byte loads, 8-byte row-major stores), parks the bytes in LDS (row
+// pitch 68 B), then writes 16 bytes of one transposed row.
+template <bool BF16_IN, bool E5M2>
+__global__ void __launch_bounds__(256) fp8_cast_t_kernel(const void* __restrict__ x, const float* __restrict__ scale,
+                                                         unsigned char* __restrict__ out,
+                                                         unsigned char* __restrict__ out_t,
+                                                         unsigned* __restrict__ amax, int R, int C) {
+  constexpr float LIM = E5M2 ? 57344.f : 448.f;
+  constexpr int P = 68;  // LDS row pitch (bytes): 4-byte skew per row
+  __shared__ __attribute__((aligned(16))) unsigned char tile[64 * P];
+  __shared__ float red[4];
+  const float s = *scale;
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tid = threadIdx.x;
+  float m = 0.f;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int v = tid + 256 * k;  // 512 vectors of 8 per tile
+    const int rr = v >> 3, cc = (v & 7) * 8;
+    const int r = r0 + rr, c = c0 + cc;
+    uint2 w = {0u, 0u};
+    if (r < R && c < C) {  // C is a multiple of 8: whole vectors
+      float f[8];
+      const long long off = (long long)r * C + c;
+      if (BF16_IN) {
+        unpack8(*(const u32x4*)((const bf16_t*)x + off), f);
+      } else {
+        const f32x4 a = *(const f32x4*)((const float*)x + off), b = *(const f32x4*)((const float*)x + off + 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          f[i] = a[i];
+          f[4 + i] = b[i];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        m = fmaxf(m, fabsf(f[i]));
+        f[i] = fminf(fmaxf(f[i] * s, -LIM), LIM);
+      }
+      w.x = cvt4<E5M2>(f[0], f[1], f[2], f[3]);
+      w.y = cvt4<E5M2>(f[4], f[5], f[6], f[7]);
+      if (out) *(uint2*)(out + off) = w;
+    }
+    *(unsigned*)(tile + rr * P + cc) = w.x;
+    *(unsigned*)(tile + rr * P + cc + 4) = w.y;
+  }
+  if (out_t) {
+    __syncthreads();
+    // transposed row = tile column cc (C index c0 + cc), 16 bytes = tile rows rb .. rb + 15
+    const int cc = tid >> 2, rb = (tid & 3) * 16;
+    const int c = c0 + cc, r = r0 + rb;
+    if (c < C && r < R) {
+      unsigned wv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        unsigned b = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b |= (unsigned)tile[(rb + 4 * q + j) * P + cc] << (8 * j);
+        wv[q] = b;
+      }
+      unsigned char* dst = out_t + (long long)c * R + r;
+      if (r + 16 <= R) {
+        *(u32x4*)dst = (u32x4){wv[0], wv[1], wv[2], wv[3]};
+      } else {
+        for (int j = 0; j < R - r; ++j) dst[j] = (unsigned char)(wv[j >> 2] >> (8 * (j & 3)));
+      }
+    }
+  }
+  m = wave_max(m);
+  if ((tid & 63) == 0) red[tid >> 6] = m;
+  __syncthreads();
+  if (tid == 0) {
+    const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (!(bm == bm)) {
+      atomicMax(amax, 0x7f800000u);
+    } else if (bm > 0.f) {
+      atomicMax(amax, __float_as_uint(bm));
+    }
+  }
+}
+
+// x [R, C] (C % 8 == 0, 16-byte aligned rows), out [R, C] and / or out_t
+// [C, R] (either may be null; out_t rows 16-byte aligned: R % 16 == 0).
+extern "C" int dw_fp8_cast_t(const void* x, int in_bf16, const float* scale, void* out, void* out_t,
+                             unsigned* amax, int R, int C, int e5m2, void* stream) {
+  if (R <= 0 || C <= 0) return 0;
+  if (C % 8 || (out_t && R % 16)) return (int)hipErrorInvalidValue;
+  dim3 grid((C + 63) / 64, (R + 63) / 64);
+  hipStream_t s = (hipStream_t)stream;
+#define L(B, E)                                                                                                \
+  hipLaunchKernelGGL((fp8_cast_t_kernel<B, E>), grid, dim3(256), 0, s, x, scale, (unsigned char*)out,          \
+                     (unsigned char*)out_t, amax, R, C)
+  if (in_bf16) {
+    if (e5m2) L(true, true); else L(true, false);
+  } else {
+    if (e5m2) L(false, true); else L(false, false);
+  }
+#undef L
   DW_LAUNCH_RET;
 }

@@ -61,6 +61,7 @@ class Fp8State:
         self.inv_scale = torch.ones(capacity, dtype=torch.float32, device=d)
         self.n = 0
         self.steps = 0
+        self.head = 0  # ring slot of the history the next update writes
 
     def register(self, fmt: str) -> int:
         if self.n >= self.cap:
@@ -85,14 +86,16 @@ class Fp8State:
                 # non-negative float bits order like the floats: MAX on int32
                 dist.all_reduce(amax, op=dist.ReduceOp.MAX, group=self.group)
         mp = float(2.0 ** self.margin)
+        head = self.head
+        self.head = (self.head + 1) % self.h  # the history is a ring: no shifting
         if _hip.use_hip(self.amax_bits):
             _hip.check(_hip.lib().dw_fp8_update_scales(
                 _hip.ptr(self.amax_bits), _hip.ptr(self.hist), _hip.ptr(self.fmax), _hip.ptr(self.scale),
-                _hip.ptr(self.inv_scale), self.n, self.h, mp, _hip.stream()), "fp8_update_scales")
+                _hip.ptr(self.inv_scale), self.n, self.h, head, mp, _hip.stream()), "fp8_update_scales")
             return
         n = self.n
         cur = amax.view(torch.float32).clone()
-        self.hist[:n] = torch.cat([cur[:, None], self.hist[:n, :-1]], 1)
+        self.hist[:n, head] = cur
         best = self.hist[:n].amax(1)
         ok = (best > 0) & torch.isfinite(best)
         sc = torch.where(ok, self.fmax[:n] / (best * mp), self.scale[:n])
@@ -147,6 +150,25 @@ def cast_to_fp8(x: torch.Tensor, st: Fp8State, idx: int, fmt: str) -> torch.Tens
     return (xf * st.scale[idx]).clamp(-lim, lim).to(_TORCH_DT[fmt])
 
 
+@torch.no_grad()
+def cast_to_fp8_t(x: torch.Tensor, st: Fp8State, idx: int, fmt: str, row: bool = True, trans: bool = True):
+    """x [R, C] -> (x8 [R, C] or None, x8^T [C, R] contiguous or None) in ONE
+    pass (``dw_fp8_cast_t``: LDS-tiled transpose), scaled by ``st.scale[idx]``,
+    amax recorded as ``cast_to_fp8``."""
+    x = x.contiguous()
+    R, C = x.shape
+    if _hip.use_hip(x) and x.dtype in (torch.bfloat16, torch.float32) and C % 8 == 0 and R % 16 == 0:
+        out = torch.empty(R, C, dtype=torch.uint8, device=x.device) if row else None
+        out_t = torch.empty(C, R, dtype=torch.uint8, device=x.device) if trans else None
+        _hip.check(_hip.lib().dw_fp8_cast_t(
+            _hip.ptr(x), int(x.dtype == torch.bfloat16), _hip.ptr(st.scale[idx:]), _hip.ptr(out), _hip.ptr(out_t),
+            _hip.ptr(st.amax_bits[idx:]), R, C, int(fmt == "e5m2"), _hip.stream()), "fp8_cast_t")
+        dt = _TORCH_DT[fmt]
+        return (out.view(dt) if out is not None else None), (out_t.view(dt) if out_t is not None else None)
+    x8 = cast_to_fp8(x, st, idx, fmt)
+    return (x8 if row else None), (x8.t().contiguous() if trans else None)
+
+
 def _scaled_mm(a8, b8, inv_a, inv_b, bias, out_dtype):
     """a8 [M, K] row-major @ b8 [K, N] (column-major) with per-tensor inverse
     scales; hipBLASLt FP8 GEMM on the GPU."""
@@ -169,38 +191,44 @@ class _Fp8LinearFn(torch.autograd.Function):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
         out_dtype = x.dtype if x.dtype in (torch.bfloat16, torch.float16, torch.float32) else torch.bfloat16
-        x8 = cast_to_fp8(x2, st, mod._ix, "e4m3")
-        w8 = cast_to_fp8(weight, st, mod._iw, "e4m3")
+        # x8 for this GEMM, x8^T (token dim contiguous) for the weight
+        # gradient; w8 for this GEMM, w8^T for dgrad -- each from ONE pass
+        need_w = weight.requires_grad
+        x8, x8t = cast_to_fp8_t(x2, st, mod._ix, "e4m3", trans=need_w)
+        w8, w8t = cast_to_fp8_t(weight, st, mod._iw, "e4m3", trans=x.requires_grad)
         b = bias.to(out_dtype) if bias is not None else None
         y = _scaled_mm(x8, w8.t(), st.inv_scale[mod._ix], st.inv_scale[mod._iw], b, out_dtype)
-        ctx.save_for_backward(x8, w8)
+        ctx.save_for_backward(x8t, w8t)
         ctx.mod, ctx.shape, ctx.has_bias = mod, shape, bias is not None
         ctx.wdtype, ctx.xdtype = weight.dtype, x.dtype
         return y.reshape(*shape[:-1], weight.shape[0])
 
     @staticmethod
     def backward(ctx, gy):
-        x8, w8 = ctx.saved_tensors
+        x8t, w8t = ctx.saved_tensors
         mod = ctx.mod
         st = mod._state(gy.device)
-        g2 = gy.reshape(-1, gy.shape[-1])
-        T = g2.shape[0]
-        g8 = cast_to_fp8(g2, st, mod._ig, mod.grad_fmt)
+        g2 = gy.reshape(-1, gy.shape[-1]).contiguous()
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        # g8 for dgrad, g8^T (token dim contiguous) for the weight gradient: one pass
+        g8, g8t = cast_to_fp8_t(g2, st, mod._ig, mod.grad_fmt, row=need_x, trans=need_w)
         inv_g, inv_w, inv_x = st.inv_scale[mod._ig], st.inv_scale[mod._iw], st.inv_scale[mod._ix]
         gdt = ctx.xdtype if ctx.xdtype in (torch.bfloat16, torch.float16, torch.float32) else torch.bfloat16
         dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            # dx [T, in] = g [T, out] @ w [out, in]   (w column-major: transposed copy)
-            dx = _scaled_mm(g8, w8.t().contiguous().t(), inv_g, inv_w, None, gdt).reshape(ctx.shape)
-        if ctx.needs_input_grad[1]:
-            # dw [out, in] = g^T [out, T] @ x [T, in]
+        if need_x:
+            # dx [T, in] = g [T, out] @ w [out, in]: B = w8^T viewed column-major
+            dx = _scaled_mm(g8, w8t.t(), inv_g, inv_w, None, gdt).reshape(ctx.shape)
+        if need_w:
+            # dw [out, in] = g^T [out, T] @ x [T, in]: A = g8^T, B = x8^T viewed column-major
             wdt = ctx.wdtype if ctx.wdtype in (torch.bfloat16, torch.float16, torch.float32) else torch.float32
-            if _gemm_ok(T):
-                dw = _scaled_mm(g8.t().contiguous(), x8.t().contiguous().t(), inv_g, inv_x, None, wdt)
-            else:  # token count not a multiple of 16: the dequantised GEMM
-                dw = ((g8.float() * inv_g).t() @ (x8.float() * inv_x)).to(wdt)
+            dw = _scaled_mm(g8t, x8t.t(), inv_g, inv_x, None, wdt)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = g2.float().sum(0).to(ctx.wdtype)
+            if _hip.use_hip(g2) and g2.dtype == torch.bfloat16 and g2.shape[-1] % 8 == 0:
+                from .activation import colsum
+
+                db = colsum(g2, out_dtype=ctx.wdtype)  # one HIP pass, fp32 math
+            else:
+                db = g2.float().sum(0).to(ctx.wdtype)
         return dx, dw, db, None
 
 

@@ -45,6 +45,30 @@ def test_cast_kernel_matches_torch(fmt, dtype, n):
     assert st.amax_bits[i].view(torch.float32).item() == x.float().abs().max().item()
 
 
+@pytest.mark.parametrize("fmt", ["e4m3", "e5m2"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(8192, 1600), (96, 200), (48, 64)])
+def test_cast_transpose_kernel_matches_torch(fmt, dtype, shape):
+    """dw_fp8_cast_t: both layouts from one pass (partial edge tiles
+    included) equal torch's scale -> clamp -> cast, and the amax matches."""
+    from dlrover_wuqiong_amd.ops import fp8
+
+    torch.manual_seed(shape[0])
+    st = fp8.fp8_state("cuda")
+    i = st.register(fmt)
+    st.scale[i] = 3.0
+    x = (torch.randn(*shape, device="cuda") * 40).to(dtype)
+    x8, x8t = fp8.cast_to_fp8_t(x, st, i, fmt)
+    lim = fp8.FP8_MAX[fmt]
+    ref = (x.float() * 3.0).clamp(-lim, lim).to(x8.dtype)
+    assert (x8.view(torch.uint8) == ref.view(torch.uint8)).float().mean().item() > 0.999
+    assert x8t.shape == (shape[1], shape[0]) and x8t.is_contiguous()
+    assert torch.equal(x8t.view(torch.uint8), x8.view(torch.uint8).t())
+    assert st.amax_bits[i].view(torch.float32).item() == x.float().abs().max().item()
+    _r, only_t = fp8.cast_to_fp8_t(x, st, i, fmt, row=False)
+    assert _r is None and torch.equal(only_t.view(torch.uint8), x8t.view(torch.uint8))
+
+
 def test_update_scales_kernel():
     from dlrover_wuqiong_amd.ops import fp8
 
