@@ -153,26 +153,30 @@ extern "C" int dw_fp8_update_scales(unsigned* amax_bits, float* hist, const floa
 // layouts from one read replaces a separate transposed copy (torch's
 // byte-wise transpose of a float8 tensor ran at ~0.25 TB/s:
 // profiles/r3/fp8_linear_kernels.md).
-// 64x64 tiles, 256 threads: each thread converts 2 x 8 contiguous elements
-// (16-byte loads, 8-byte row-major stores), parks the bytes in LDS (row
-// pitch 68 B), then writes 16 bytes of one transposed row.
+// 128x128 tiles, 256 threads, every output row segment a whole 128-byte
+// line in both layouts (a 64-wide tile wrote half lines and ran at ~1.4
+// TB/s): phase 1 converts 8 x 8 contiguous elements per thread (16 threads
+// per 256-byte input row; 8-byte row-major stores) and parks the bytes in
+// LDS; phase 2 gives each thread a 16-row x 4-column block: 16 4-byte LDS
+// reads, a byte transpose in registers, four 16-byte stores (8 threads per
+// 128-byte transposed row).
 template <bool BF16_IN, bool E5M2>
 __global__ void __launch_bounds__(256) fp8_cast_t_kernel(const void* __restrict__ x, const float* __restrict__ scale,
                                                          unsigned char* __restrict__ out,
                                                          unsigned char* __restrict__ out_t,
                                                          unsigned* __restrict__ amax, int R, int C) {
   constexpr float LIM = E5M2 ? 57344.f : 448.f;
-  constexpr int P = 68;  // LDS row pitch (bytes): 4-byte skew per row
-  __shared__ __attribute__((aligned(16))) unsigned char tile[64 * P];
+  constexpr int T = 128, P = T + 4;  // LDS row pitch (bytes)
+  __shared__ __attribute__((aligned(16))) unsigned char tile[T * P];
   __shared__ float red[4];
   const float s = *scale;
-  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int r0 = blockIdx.y * T, c0 = blockIdx.x * T;
   const int tid = threadIdx.x;
   float m = 0.f;
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int v = tid + 256 * k;  // 512 vectors of 8 per tile
-    const int rr = v >> 3, cc = (v & 7) * 8;
+  for (int k = 0; k < 8; ++k) {
+    const int v = tid + 256 * k;  // 2048 vectors of 8 per tile
+    const int rr = v >> 4, cc = (v & 15) * 8;
     const int r = r0 + rr, c = c0 + cc;
     uint2 w = {0u, 0u};
     if (r < R && c < C) {  // C is a multiple of 8: whole vectors
@@ -197,28 +201,24 @@ __global__ void __launch_bounds__(256) fp8_cast_t_kernel(const void* __restrict_
       w.y = cvt4<E5M2>(f[4], f[5], f[6], f[7]);
       if (out) *(uint2*)(out + off) = w;
     }
-    *(unsigned*)(tile + rr * P + cc) = w.x;
-    *(unsigned*)(tile + rr * P + cc + 4) = w.y;
+    if (out_t) *(uint2*)(tile + rr * P + cc) = w;
   }
   if (out_t) {
     __syncthreads();
-    // transposed row = tile column cc (C index c0 + cc), 16 bytes = tile rows rb .. rb + 15
-    const int cc = tid >> 2, rb = (tid & 3) * 16;
-    const int c = c0 + cc, r = r0 + rb;
-    if (c < C && r < R) {
-      unsigned wv[4];
+    const int cg = tid >> 3, rg = tid & 7;  // columns 4cg .. 4cg+3, rows 16rg .. 16rg+15
+    const int c = c0 + 4 * cg, r = r0 + 16 * rg;
+    if (c < C && r < R) {  // C % 8 == 0 and R % 16 == 0: whole groups
+      unsigned w[16];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        unsigned b = 0;
+      for (int i = 0; i < 16; ++i) w[i] = *(const unsigned*)(tile + (16 * rg + i) * P + 4 * cg);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) b |= (unsigned)tile[(rb + 4 * q + j) * P + cc] << (8 * j);
-        wv[q] = b;
-      }
-      unsigned char* dst = out_t + (long long)c * R + r;
-      if (r + 16 <= R) {
-        *(u32x4*)dst = (u32x4){wv[0], wv[1], wv[2], wv[3]};
-      } else {
-        for (int j = 0; j < R - r; ++j) dst[j] = (unsigned char)(wv[j >> 2] >> (8 * (j & 3)));
+      for (int j = 0; j < 4; ++j) {
+        unsigned q[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          q[g] = ((w[4 * g] >> (8 * j)) & 0xffu) | (((w[4 * g + 1] >> (8 * j)) & 0xffu) << 8) |
+                 (((w[4 * g + 2] >> (8 * j)) & 0xffu) << 16) | (((w[4 * g + 3] >> (8 * j)) & 0xffu) << 24);
+        *(u32x4*)(out_t + (long long)(c + j) * R + r) = (u32x4){q[0], q[1], q[2], q[3]};
       }
     }
   }
@@ -241,7 +241,7 @@ extern "C" int dw_fp8_cast_t(const void* x, int in_bf16, const float* scale, voi
                              unsigned* amax, int R, int C, int e5m2, void* stream) {
   if (R <= 0 || C <= 0) return 0;
   if (C % 8 || (out_t && R % 16)) return (int)hipErrorInvalidValue;
-  dim3 grid((C + 63) / 64, (R + 63) / 64);
+  dim3 grid((C + 127) / 128, (R + 127) / 128);
   hipStream_t s = (hipStream_t)stream;
 #define L(B, E)                                                                                                \
   hipLaunchKernelGGL((fp8_cast_t_kernel<B, E>), grid, dim3(256), 0, s, x, scale, (unsigned char*)out,          \
