@@ -76,7 +76,7 @@ def bf16_path(t: torch.Tensor) -> bool:
     one inside a bf16 autocast region (``amp_native`` over fp32 weights).
     fp32 outside autocast runs the fp32 PyTorch math instead of silently
     dropping to bf16."""
-    if not t.is_cuda:
+    if not use_hip(t):
         return False
     if t.dtype == torch.bfloat16:
         return True

@@ -34,6 +34,7 @@ def main():
                         "masters inside the fused optimizer")
     p.add_argument("--torch-optim", action="store_true", help="keep torch.optim.AdamW (no multi-tensor HIP kernel)")
     p.add_argument("--no-ckpt", action="store_true", help="step time only (no flash checkpoints)")
+    p.add_argument("--fp8", action="store_true", help="auto_accelerate 'fp8' on the decoder layers' projections")
     a = p.parse_args()
     for k, v in dict(MASTER_ADDR="127.0.0.1", MASTER_PORT="29571", RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
                      LOCAL_WORLD_SIZE="1").items():
@@ -72,7 +73,7 @@ def main():
     prec = ("amp_native", {"dtype": torch.bfloat16}) if a.precision == "amp" else "half"
     ok, res, strategy = auto_accelerate(
         model, torch.optim.AdamW, optim_args={"lr": 2e-5, "betas": (0.9, 0.95), "weight_decay": 0.1},
-        load_strategy=["module_replace", prec,
+        load_strategy=["module_replace", prec] + ([("fp8", {"include": ("layers", "h.")})] if a.fp8 else []) + [
                        ("fsdp", {"wrap_cls": (layer_cls,)}), ("checkpoint", {"wrap_cls": (layer_cls,)})],
         fused_optimizer=not a.torch_optim)
     assert ok, "auto_accelerate failed"
@@ -110,7 +111,7 @@ def main():
         med = sorted(steps)[len(steps) // 2]
         if rank == 0:
             print(json.dumps({"metric": "fsdp train step", "n_gpus": world, "model": a.model, "seq_len": a.seq,
-                              "precision": a.precision, "optimizer": type(opt).__name__,
+                              "precision": a.precision + ("+fp8" if a.fp8 else ""), "optimizer": type(opt).__name__,
                               "train_step_ms": round(1000 * med, 1),
                               "tokens_per_s": round(world * a.micro_batch * a.seq / med, 1),
                               "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if cuda else None,
