@@ -27,6 +27,7 @@ MI355X layout: EP inside a node's xGMI mesh, expert-DP across nodes; the
 expert all-reduces are few and large (one per expert weight tensor).
 """
 
+import contextlib
 from typing import List, Optional
 
 import torch
@@ -66,10 +67,27 @@ class MoEDistributedDataParallel(nn.Module):
         self.expert_dp_group = expert_dp_group
         self.dp_size = data_parallel_size or dist.get_world_size(process_group)
         self._pending = []
+        self._sync = True
         for _n, p in self.expert_params:
             p.register_post_accumulate_grad_hook(self._reduce_expert)
 
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Gradient accumulation: no dense or expert all-reduce inside (as
+        DDP.no_sync); the backward after the block reduces the sums."""
+        prev, self._sync = self._sync, False
+        try:
+            if self.dense_ddp:
+                with self.module.no_sync():
+                    yield
+            else:
+                yield
+        finally:
+            self._sync = prev
+
     def _reduce_expert(self, p: torch.Tensor):
+        if not self._sync:
+            return
         # SUM over the replicas of these experts, scaled by 1 / (data ranks)
         p.grad.div_(self.dp_size)
         work = dist.all_reduce(p.grad, group=self.expert_dp_group, async_op=True)
