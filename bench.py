@@ -192,7 +192,8 @@ def _job(a, n: int, mode: str, run_dir: str, tag: str):
     # the agent's and workers' output goes to stderr: stdout carries the one JSON line
     p = subprocess.Popen(cmd, env=env, stdout=sys.stderr, stderr=sys.stderr, start_new_session=True)
     try:
-        rc = p.wait(timeout=a.timeout)
+        # the extra import-mode job must not hold the run hostage
+        rc = p.wait(timeout=a.timeout if mode == "deep" else min(a.timeout, 420.0))
     except subprocess.TimeoutExpired:
         log("bench: timeout; killing the job")
         os.killpg(p.pid, signal.SIGKILL)
@@ -246,7 +247,10 @@ def launcher(a) -> int:
                     # from host memory: compare the like-for-like number
                     res["load_vs_baseline"] = round(imp["load_sec"] / REF_LOAD_SEC, 4)
                     res["load_vs_baseline_basis"] = "load_sec_shm (restart restore from host shm)"
-            rc = rc or rc2
+            if rc2:
+                # the headline (deep-job) numbers stand; the extra job's
+                # failure is reported in the line, not as the run's status
+                res["import_mode_rc"] = rc2
         if res is not None:
             res["launcher_wall_s"] = round(time.time() - T_LAUNCH, 1)
     finally:
