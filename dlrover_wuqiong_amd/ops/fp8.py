@@ -151,6 +151,20 @@ def cast_to_fp8(x: torch.Tensor, st: Fp8State, idx: int, fmt: str) -> torch.Tens
 
 
 @torch.no_grad()
+def init_scale_from(x: torch.Tensor, st: Fp8State, idx: int):
+    """First use of a tensor role: its delayed-scaling history is empty, so
+    set the scale from THIS tensor's amax (current scaling, device-side --
+    no host sync) instead of the cold-start 1.0 that saturates or underflows
+    the first step's casts (Llama-3 8B: first-step loss 11.9 vs 0.15 in bf16
+    without this)."""
+    a = x.detach().abs().amax().float()
+    mp = float(2.0 ** st.margin)
+    sc = torch.where((a > 0) & torch.isfinite(a), st.fmax[idx] / (a * mp), st.scale[idx])
+    st.scale[idx] = sc
+    st.inv_scale[idx] = 1.0 / sc
+
+
+@torch.no_grad()
 def cast_to_fp8_t(x: torch.Tensor, st: Fp8State, idx: int, fmt: str, row: bool = True, trans: bool = True):
     """x [R, C] -> (x8 [R, C] or None, x8^T [C, R] contiguous or None) in ONE
     pass (``dw_fp8_cast_t``: LDS-tiled transpose), scaled by ``st.scale[idx]``,
@@ -194,6 +208,11 @@ class _Fp8LinearFn(torch.autograd.Function):
         # x8 for this GEMM, x8^T (token dim contiguous) for the weight
         # gradient; w8 for this GEMM, w8^T for dgrad -- each from ONE pass
         need_w = weight.requires_grad
+        if mod._fresh:  # first step: scales from the tensors themselves
+            for i, t in ((mod._ix, x2), (mod._iw, weight)):
+                if i in mod._fresh:
+                    init_scale_from(t, st, i)
+                    mod._fresh.discard(i)
         x8, x8t = cast_to_fp8_t(x2, st, mod._ix, "e4m3", trans=need_w)
         w8, w8t = cast_to_fp8_t(weight, st, mod._iw, "e4m3", trans=x.requires_grad)
         b = bias.to(out_dtype) if bias is not None else None
@@ -210,6 +229,9 @@ class _Fp8LinearFn(torch.autograd.Function):
         st = mod._state(gy.device)
         g2 = gy.reshape(-1, gy.shape[-1]).contiguous()
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if mod._ig in mod._fresh:
+            init_scale_from(g2, st, mod._ig)
+            mod._fresh.discard(mod._ig)
         # g8 for dgrad, g8^T (token dim contiguous) for the weight gradient: one pass
         g8, g8t = cast_to_fp8_t(g2, st, mod._ig, mod.grad_fmt, row=need_x, trans=need_w)
         inv_g, inv_w, inv_x = st.inv_scale[mod._ig], st.inv_scale[mod._iw], st.inv_scale[mod._ix]
@@ -249,12 +271,14 @@ class Fp8Linear(nn.Module):
         self.grad_fmt = "e5m2" if fmt == "HYBRID" else "e4m3"
         self._dev = None
         self._ix = self._iw = self._ig = -1
+        self._fresh = set()  # roles whose scale is still the cold-start 1.0
 
     def _state(self, device) -> Fp8State:
         d = torch.device(device)
         if self._dev != d:
             st = fp8_state(d)
             self._ix, self._iw, self._ig = st.register("e4m3"), st.register("e4m3"), st.register(self.grad_fmt)
+            self._fresh = {self._ix, self._iw, self._ig}
             self._dev = d
         return fp8_state(d)
 
