@@ -177,7 +177,11 @@ def grouped_mlp(x: torch.Tensor, counts, w1: torch.Tensor, w2: torch.Tensor,
         outs.append(F.linear(h, w2[e]))
         off += n
     if not outs:
-        return x.new_zeros((0, w2.shape[1])) + 0 * (w1.sum() + w2.sum() + (w3.sum() if w3 is not None else 0))
+        # no rows for any local expert (EP: this rank received nothing): keep
+        # x AND the weights in the graph, so the backward still runs the
+        # inverse all-to-all every EP peer waits for
+        return x.new_zeros((0, w2.shape[1])) + 0 * (x.sum() + w1.sum() + w2.sum() +
+                                                    (w3.sum() if w3 is not None else 0))
     return torch.cat(outs, 0)
 
 
@@ -295,8 +299,10 @@ def replace_with_moe(model: nn.Module, layer_class, num_experts: int, top_k: int
     """Sparse upcycling (reference modules/moe/inject.py ``replace_with_moe``):
     every ``layer_class`` SwiGLU FFN of ``model`` becomes a ``MoELayer`` whose
     experts start as copies of the dense weights (optionally + Gaussian
-    noise) and whose router starts at zero (uniform routing) -- the MoE model
-    initially computes exactly the dense model's function.  Supported FFNs:
+    noise) and whose router starts small and random (balanced routing; the
+    renormalised top-k weights sum to 1 over identical experts) -- without
+    noise the MoE model initially computes exactly the dense model's
+    function.  Supported FFNs:
     this framework's ``LlamaMLP`` (fused ``gate_up_proj``) and HF-style
     ``gate_proj`` / ``up_proj`` / ``down_proj``.  With ``ep_group`` this
     rank keeps its slice of the experts.  Returns the replaced names."""
@@ -319,7 +325,10 @@ def replace_with_moe(model: nn.Module, layer_class, num_experts: int, top_k: int
                            dtype=down_w.dtype, device=down_w.device)
             lo = moe.num_local * (dist.get_rank(ep_group) if moe.ep > 1 else 0)
             with torch.no_grad():
-                moe.gate.wg.weight.zero_()
+                # a zero router ties every expert and top-k then sends all
+                # tokens to the same k experts (one EP rank gets everything)
+                gen = torch.Generator(device="cpu").manual_seed(1234)
+                moe.gate.wg.weight.copy_(torch.randn(moe.gate.wg.weight.shape, generator=gen) * (0.1 / H ** 0.5))
                 for e in range(moe.num_local):
                     for dst, src in ((moe.experts.w1, gate_w), (moe.experts.w3, up_w), (moe.experts.w2, down_w)):
                         dst[e].copy_(src)

@@ -158,3 +158,15 @@ def test_shm_checkpoint_of_another_job_is_ignored(tmp_path):
     assert not b.load_checkpoint()  # foreign shm ignored, nothing on storage
     assert b.save_checkpoint(7, {"model": m.state_dict(), "step": 7}, storage_type=StorageType.MEMORY)
     assert b.load_checkpoint().get("step") == 7
+
+
+def test_moe_example_upcycled_ep2_dp2():
+    """Upcycled Llama MoE, EP 2 x DP 2 with capacity, MoE-aware DDP through
+    auto_accelerate: the step-0 loss equals the dense model's (up to the
+    expert noise) and training reduces it."""
+    out = _run(["train_moe.py", "--ep", "2", "--capacity_factor", "1.25", "--steps", "5"],
+               os.path.join(EX, "moe"), nproc=4)
+    m = re.search(r"loss dense ([\d.]+) -> MoE ([\d.]+)", out)
+    assert m and abs(float(m.group(1)) - float(m.group(2))) < 0.01, out[-1500:]
+    first, last = _losses(out)
+    assert last < first and "'ddp'" in out

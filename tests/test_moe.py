@@ -194,3 +194,37 @@ def test_replace_with_moe_upcycles_dense_ffn():
     names = replace_with_moe(m, LlamaMLP, num_experts=4, top_k=2)
     assert len(names) == cfg.num_hidden_layers and all(isinstance(l.mlp, MoELayer) for l in m.layers)
     assert torch.allclose(m(ids), dense, atol=1e-4)
+
+
+def _empty_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dlrover_wuqiong_amd.parallel.moe import MoELayer
+
+        torch.manual_seed(0)
+        layer = MoELayer(16, 32, num_experts=4, top_k=2, ep_group=dist.group.WORLD)
+        with torch.no_grad():
+            layer.gate.wg.weight.zero_()  # ties: every token to the same 2 experts -> one rank gets nothing
+        x = torch.randn(10, 16, requires_grad=True)
+        layer(x).square().sum().backward()  # must not desynchronise the inverse all-to-all
+        q.put((rank, bool(torch.isfinite(x.grad).all())))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_moe_ep_rank_receiving_no_tokens_two_ranks():
+    """An EP rank whose experts get no token still runs the backward's
+    inverse all-to-all (the empty expert output keeps its input in the graph)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_empty_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=30)
+    assert res == [(0, True), (1, True)], res
