@@ -1,0 +1,6 @@
+"""Compatibility import path (reference: atorch/atorch/optimizers/agd.py).
+
+Thin re-export onto the MI355X-native implementation; existing ATorch user code imports unchanged.
+"""
+
+from dlrover_wuqiong_amd.optimizers.agd import AGD  # noqa: F401
