@@ -582,11 +582,11 @@ def worker(a) -> int:
             # the checkpoint flush running on its own stream
             torch.cuda.current_stream().synchronize()
 
-    def wait_standbys(marks):
+    def wait_standbys(marks, timeout=600.0):
         ctl = os.environ.get("DWAMD_AGENT_CTL_DIR", "")
         if not ctl or a.no_fault:
             return
-        deadline = time.time() + 600
+        deadline = time.time() + timeout
         lw = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
         while time.time() < deadline and not all(
                 os.path.exists(os.path.join(ctl, m.format(i))) for i in range(lw) for m in marks):
@@ -608,7 +608,11 @@ def worker(a) -> int:
             sync_step()
             times.append(time.perf_counter() - ts)
         step_sec = mx(statistics.median(times))
-        wait_standbys(["standby_ready.{}"])  # the pre-imported replacements are up
+        # the pre-imported replacements are up (on a GPU: and have replayed
+        # this worker's warm profile -- recorded during the warm-up)
+        wait_standbys(["standby_ready.{}"])
+        if cuda:
+            wait_standbys(["standby_warm.{}"], timeout=90.0)
         dt, _ok = save()
         ckpt.wait_latest_checkpoint()
         sync_all()

@@ -37,6 +37,7 @@ SIGS = {
     "dw_mem_get_info": (i32, [c.POINTER(u64), c.POINTER(u64)]),
     "dw_hip_error_string": (cp, [i32]),
     "dw_kernels_abi_version": (i32, []),
+    "dw_preload_code_objects": (i32, []),  # preload.hip
     # xpu_timer.hip
     "dw_xt_start": (i32, [c.c_double, i32]),
     "dw_xt_stop": (i32, []),

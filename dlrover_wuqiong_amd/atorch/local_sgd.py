@@ -181,6 +181,17 @@ class LocalSGD:
             self.momentum_buf.copy_(sd["momentum"])
 
 
+def _like_param(p, local: torch.Tensor):
+    """Gradient for ``p`` from this rank's local piece (a DTensor parameter
+    gets a DTensor gradient with the same placements)."""
+    if hasattr(p, "to_local"):
+        from torch.distributed.tensor import DTensor
+
+        return DTensor.from_local(local, p.device_mesh, p.placements, run_check=False,
+                                  shape=p.shape, stride=p.stride())
+    return local
+
+
 class HSDPLocalSGD:
     """Local SGD inside hybrid sharding (FSDP2 on a (replicate, shard) mesh).
 
@@ -216,8 +227,25 @@ class HSDPLocalSGD:
         self.params = [p for p in model.parameters() if p.requires_grad]
         self.anchor = None
         self.outer_optimizer = None
+        self._sync_initial_shards()
         if self.warmup_steps == 0:
             self._start_local()
+
+    @torch.no_grad()
+    def _sync_initial_shards(self):
+        """Replicas start from replicate-group rank 0's shards: FSDP2 on the
+        shard sub-mesh does not sync across replicas, and with per-rank
+        random init the anchors would differ and never converge."""
+        if _ws(self.group) <= 1:
+            return
+        flat = self._flat()
+        src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
+        dist.broadcast(flat, src=src, group=self.group)
+        o = 0
+        for p in self.params:
+            loc = self._local(p.data)
+            loc.copy_(flat[o:o + loc.numel()].view_as(loc))
+            o += loc.numel()
 
     # the wrapper is handed out as "the optimizer"
     @property
@@ -241,16 +269,23 @@ class HSDPLocalSGD:
     @torch.no_grad()
     def _allreduce_grads(self):
         """Warm-up steps: average the sharded gradients across replicas."""
-        grads = [self._local(p.grad) for p in self.params if p.grad is not None]
-        if not grads or _ws(self.group) <= 1:
+        if _ws(self.group) <= 1:
             return
-        flat = torch.cat([g.reshape(-1).float() for g in grads])
+        # same layout on every rank: a parameter unused on this rank packs zeros
+        locs = [self._local(p.data) for p in self.params]
+        flat = torch.cat([(self._local(p.grad).reshape(-1).float() if p.grad is not None
+                           else torch.zeros(loc.numel(), device=loc.device))
+                          for p, loc in zip(self.params, locs)])
         dist.all_reduce(flat, group=self.group)
         flat.div_(_ws(self.group))
         o = 0
-        for g in grads:
-            g.copy_(flat[o:o + g.numel()].view_as(g))
-            o += g.numel()
+        for p, loc in zip(self.params, locs):
+            n = loc.numel()
+            if p.grad is not None:
+                self._local(p.grad).copy_(flat[o:o + n].view_as(loc))
+            else:
+                p.grad = _like_param(p, flat[o:o + n].view_as(loc).to(loc.dtype))
+            o += n
 
     @torch.no_grad()
     def _start_local(self):

@@ -858,3 +858,5 @@ extern "C" int dw_attn_bwd_varlen_ext(const void* q, const void* k, const void* 
                    softmax_scale, st, vl, s, ep);
   DW_LAUNCH_RET;
 }
+
+DW_PRELOAD(attn_bwd_pre_kernel<128>);

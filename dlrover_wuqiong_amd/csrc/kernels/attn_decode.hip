@@ -225,3 +225,5 @@ extern "C" int dw_attn_decode(const void* q, const void* k, const void* v, const
   }
   DW_LAUNCH_RET;
 }
+
+DW_PRELOAD(attn_decode_merge_kernel<128>);

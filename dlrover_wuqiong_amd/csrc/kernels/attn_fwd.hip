@@ -497,3 +497,5 @@ extern "C" int dw_attn_dropout_mask(void* out, int B, int H, int S, float p, uns
                      H, S, ex);
   DW_LAUNCH_RET;
 }
+
+DW_PRELOAD(attn_dropout_mask_kernel);

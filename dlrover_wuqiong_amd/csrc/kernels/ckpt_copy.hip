@@ -222,3 +222,5 @@ extern "C" int dw_mem_get_info(uint64_t* free_b, uint64_t* total_b) {
 extern "C" const char* dw_hip_error_string(int e) { return hipGetErrorString((hipError_t)e); }
 
 extern "C" int dw_kernels_abi_version() { return 1; }
+
+DW_PRELOAD((multi_copy_kernel<8, true>));

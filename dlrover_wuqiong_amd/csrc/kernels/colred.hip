@@ -459,3 +459,5 @@ extern "C" int dw_norm_bwd2(const void* dy, const void* x, const void* gamma, co
                        accumulate);
   DW_LAUNCH_RET;
 }
+
+DW_PRELOAD(colred_kernel<0>);

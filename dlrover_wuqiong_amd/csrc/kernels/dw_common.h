@@ -29,6 +29,20 @@ struct AttnStrides {
 
 #define DW_LAUNCH_RET return (int)hipGetLastError()
 
+// Code-object preload: with deferred loading a TU's fat binary is loaded at
+// the first launch of any of its kernels.  Every TU registers one kernel
+// (DW_PRELOAD, at static-init time of the library); dw_preload_code_objects
+// (preload.hip) queries each one's attributes, which loads every code object
+// up front -- an import-mode standby does this while it waits, so the worker
+// it becomes launches from warm modules (elastic_agent/warm_profile.py).
+extern "C" void dw_register_preload(const void* kernel);
+struct DwPreloadReg {
+  explicit DwPreloadReg(const void* k) { dw_register_preload(k); }
+};
+#define DW_PRELOAD_CAT2(a, b) a##b
+#define DW_PRELOAD_CAT(a, b) DW_PRELOAD_CAT2(a, b)
+#define DW_PRELOAD(kernel) static DwPreloadReg DW_PRELOAD_CAT(dw_preload_reg_, __LINE__)((const void*)(kernel))
+
 __device__ __forceinline__ float bf2f(bf16_t u) {
   return __uint_as_float(((unsigned int)u) << 16);
 }

@@ -200,3 +200,5 @@ extern "C" int dw_rope(const void* x, void* y, const void* cosb, const void* sin
                      backward ? -1.f : 1.f, (const int*)pos_ids, rows);
   DW_LAUNCH_RET;
 }
+
+DW_PRELOAD(gelu_bwd_kernel);

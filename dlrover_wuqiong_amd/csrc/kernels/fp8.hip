@@ -31,6 +31,11 @@ __device__ __forceinline__ unsigned cvt4(float a, float b, float c, float d) {
   return w;
 }
 
+// Saturate to the format's finite range but let NaN through (fminf / fmaxf
+// would turn it into -LIM): the converter then writes the format's NaN
+// encoding, as torch's float8 cast does, so a NaN activation stays visible.
+__device__ __forceinline__ float sat(float v, float lim) { return v != v ? v : fminf(fmaxf(v, -lim), lim); }
+
 template <bool BF16_IN, bool E5M2>
 __global__ void __launch_bounds__(256) fp8_cast_amax_kernel(const void* __restrict__ x, const float* __restrict__ scale,
                                                             unsigned char* __restrict__ out,
@@ -38,6 +43,7 @@ __global__ void __launch_bounds__(256) fp8_cast_amax_kernel(const void* __restri
   constexpr float LIM = E5M2 ? 57344.f : 448.f;
   const float s = *scale;
   float m = 0.f;
+  bool nan = false;  // fmaxf drops NaN: track it explicitly
   const long long nvec = n >> 3;
   for (long long v = blockIdx.x * 256ll + threadIdx.x; v < nvec; v += (long long)gridDim.x * 256) {
     float f[8];
@@ -53,8 +59,9 @@ __global__ void __launch_bounds__(256) fp8_cast_amax_kernel(const void* __restri
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+      nan |= f[i] != f[i];
       m = fmaxf(m, fabsf(f[i]));
-      f[i] = fminf(fmaxf(f[i] * s, -LIM), LIM);
+      f[i] = sat(f[i] * s, LIM);
     }
     uint2 w;
     w.x = cvt4<E5M2>(f[0], f[1], f[2], f[3]);
@@ -65,21 +72,19 @@ __global__ void __launch_bounds__(256) fp8_cast_amax_kernel(const void* __restri
   if (blockIdx.x == 0 && threadIdx.x < (n & 7)) {
     const long long i = (nvec << 3) + threadIdx.x;
     const float f = BF16_IN ? bf2f(((const bf16_t*)x)[i]) : ((const float*)x)[i];
+    nan |= f != f;
     m = fmaxf(m, fabsf(f));
-    const float c = fminf(fmaxf(f * s, -LIM), LIM);
+    const float c = sat(f * s, LIM);
     out[i] = (unsigned char)(cvt4<E5M2>(c, 0.f, 0.f, 0.f) & 0xff);
   }
   __shared__ float red[4];
+  if (nan) m = INFINITY;  // NaN input: record +inf so the next scale backs off
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
   if (threadIdx.x == 0) {
     const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    if (!(bm == bm)) {  // NaN / inf input: record +inf so the next scale backs off
-      atomicMax(amax, 0x7f800000u);
-    } else if (bm > 0.f) {
-      atomicMax(amax, __float_as_uint(bm));
-    }
+    if (bm > 0.f) atomicMax(amax, __float_as_uint(bm));  // +inf bits = 0x7f800000 for NaN / inf
   }
 }
 
@@ -173,6 +178,7 @@ __global__ void __launch_bounds__(256) fp8_cast_t_kernel(const void* __restrict_
   const int r0 = blockIdx.y * T, c0 = blockIdx.x * T;
   const int tid = threadIdx.x;
   float m = 0.f;
+  bool nan = false;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int v = tid + 256 * k;  // 2048 vectors of 8 per tile
@@ -194,8 +200,9 @@ __global__ void __launch_bounds__(256) fp8_cast_t_kernel(const void* __restrict_
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
+        nan |= f[i] != f[i];
         m = fmaxf(m, fabsf(f[i]));
-        f[i] = fminf(fmaxf(f[i] * s, -LIM), LIM);
+        f[i] = sat(f[i] * s, LIM);
       }
       w.x = cvt4<E5M2>(f[0], f[1], f[2], f[3]);
       w.y = cvt4<E5M2>(f[4], f[5], f[6], f[7]);
@@ -222,16 +229,13 @@ __global__ void __launch_bounds__(256) fp8_cast_t_kernel(const void* __restrict_
       }
     }
   }
+  if (nan) m = INFINITY;
   m = wave_max(m);
   if ((tid & 63) == 0) red[tid >> 6] = m;
   __syncthreads();
   if (tid == 0) {
     const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    if (!(bm == bm)) {
-      atomicMax(amax, 0x7f800000u);
-    } else if (bm > 0.f) {
-      atomicMax(amax, __float_as_uint(bm));
-    }
+    if (bm > 0.f) atomicMax(amax, __float_as_uint(bm));
   }
 }
 
@@ -254,3 +258,5 @@ extern "C" int dw_fp8_cast_t(const void* x, int in_bf16, const float* scale, voi
 #undef L
   DW_LAUNCH_RET;
 }
+
+DW_PRELOAD(fp8_update_scales_kernel);

@@ -312,3 +312,5 @@ extern "C" int dw_grouped_gemm(int mode, const void* A, const void* B, void* C, 
   }
   DW_LAUNCH_RET;
 }
+
+DW_PRELOAD(grouped_gemm_kernel<MODE_TN>);

@@ -69,3 +69,5 @@ extern "C" int dw_moe_regroup(const void* x, void* out, const void* counts, int 
                      (char*)out, (const long long*)counts, ep, L, N, row_bytes, dir);
   DW_LAUNCH_RET;
 }
+
+DW_PRELOAD(moe_regroup_kernel);

@@ -276,3 +276,5 @@ extern "C" int dw_norm_bwd(const void* dy, const void* x, const void* gamma, con
                        H, (bf16_t*)dgamma, (bf16_t*)dbeta);
   DW_LAUNCH_RET;
 }
+
+DW_PRELOAD(norm_bwd_reduce_kernel<float>);

@@ -275,3 +275,5 @@ extern "C" int dw_scale_flat(void* x, int dtype, int64_t n, const void* scale, v
                        (float*)x, n, (const float*)scale);
   DW_LAUNCH_RET;
 }
+
+DW_PRELOAD((adam_flat_kernel<float, bf16_t>));

@@ -183,3 +183,5 @@ extern "C" int dw_qadamw(void* p, const void* g, void* mq, void* vq, void* ms, v
 #undef QL
   DW_LAUNCH_RET;
 }
+
+DW_PRELOAD((qadamw_kernel<8, float, float>));

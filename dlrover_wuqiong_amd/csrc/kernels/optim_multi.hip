@@ -215,3 +215,5 @@ extern "C" int dw_mt_sumsq(const void* descs, const void* chunks, int64_t nchunk
 
 extern "C" int dw_mt_hyper_size() { return (int)sizeof(MTHyper); }
 extern "C" int dw_mt_chunk() { return MT_CHUNK; }
+
+DW_PRELOAD(mt_sumsq_kernel);

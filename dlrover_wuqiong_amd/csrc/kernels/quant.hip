@@ -212,3 +212,5 @@ extern "C" int dw_dequant_reduce(const void* q, const void* params, void* out, i
   return bits == 8 ? launch_dqr<float, 8>(q, params, out, n_src, elems, gs, chunk_bytes, gpc, accumulate, s)
                    : launch_dqr<float, 4>(q, params, out, n_src, elems, gs, chunk_bytes, gpc, accumulate, s);
 }
+
+DW_PRELOAD((quant_kernel<float, 8, true>));

@@ -116,3 +116,5 @@ extern "C" int dw_xent_bwd(const void* logits, const void* target, const void* l
                      dloss_per_row, (bf16_t*)dlogits, T, V, ignore_index, vocab_start, smoothing);
   DW_LAUNCH_RET;
 }
+
+DW_PRELOAD(xent_fwd_kernel);

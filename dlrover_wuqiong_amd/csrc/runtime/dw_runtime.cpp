@@ -163,6 +163,14 @@ int dw_memcpy_parallel(void* dst, const void* src, uint64_t n, int nthreads) {
   return 0;
 }
 
+// Record the calling worker thread's errno in the shared slot (first failure
+// wins; a zero errno still marks failure as EIO).  errno is thread-local, so
+// the joining thread must read the workers' value from here.
+static void keep_errno(std::atomic<int>& slot) {
+  int expect = 0;
+  slot.compare_exchange_strong(expect, errno ? errno : EIO);
+}
+
 static int pwrite_all(int fd, const char* buf, uint64_t n, uint64_t off) {
   while (n > 0) {
     size_t chunk = (size_t)std::min<uint64_t>(n, 1ull << 30);
@@ -192,7 +200,7 @@ int dw_write_file(const char* path, const void* buf, uint64_t n, uint64_t file_o
   int fd = open(path, flags, 0644);
   if (fd < 0) { set_err("open(write)"); return -1; }
   nthreads = std::max(1, nthreads);
-  std::atomic<int> failed{0};
+  std::atomic<int> failed{0};  // errno of the first failing worker (errno is per thread)
   if (n < (16ull << 20)) nthreads = 1;
   uint64_t per = (n + nthreads - 1) / nthreads;
   per = (per + 4095) / 4096 * 4096;
@@ -201,11 +209,11 @@ int dw_write_file(const char* path, const void* buf, uint64_t n, uint64_t file_o
     uint64_t b = t * per, e = std::min(n, b + per);
     if (b >= e) break;
     ts.emplace_back([&, b, e]() {
-      if (pwrite_all(fd, (const char*)buf + b, e - b, file_off + b) != 0) failed = 1;
+      if (pwrite_all(fd, (const char*)buf + b, e - b, file_off + b) != 0) keep_errno(failed);
     });
   }
   for (auto& t : ts) t.join();
-  if (failed) { set_err("pwrite"); close(fd); return -1; }
+  if (failed) { errno = failed.load(); set_err("pwrite"); close(fd); return -1; }
   if ((mode & 2) && fsync(fd) != 0) { set_err("fsync"); close(fd); return -1; }
   close(fd);
   return 0;
@@ -224,12 +232,12 @@ int dw_read_file(const char* path, void* buf, uint64_t n, uint64_t file_off, int
     uint64_t b = t * per, e = std::min(n, b + per);
     if (b >= e) break;
     ts.emplace_back([&, b, e]() {
-      if (pread_all(fd, (char*)buf + b, e - b, file_off + b) != 0) failed = 1;
+      if (pread_all(fd, (char*)buf + b, e - b, file_off + b) != 0) keep_errno(failed);
     });
   }
   for (auto& t : ts) t.join();
   close(fd);
-  if (failed) { set_err("pread"); return -1; }
+  if (failed) { errno = failed.load(); set_err("pread"); return -1; }
   return 0;
 }
 
@@ -272,8 +280,8 @@ int dw_read_file_direct(const char* path, void* buf, uint64_t n, uint64_t file_o
           uint64_t m = e - b, off = file_off + b;
           while (m > 0) {
             ssize_t r = pread(dfd, dst, (size_t)m, (off_t)off);
-            if (r < 0) { if (errno == EINTR) continue; failed = 1; break; }
-            if (r == 0) { errno = EIO; failed = 1; break; }
+            if (r < 0) { if (errno == EINTR) continue; keep_errno(failed); break; }
+            if (r == 0) { errno = EIO; keep_errno(failed); break; }
             dst += r; m -= (uint64_t)r; off += (uint64_t)r;
             if (m % A) break;  // short read at EOF: the buffered tail path finishes it
           }
@@ -283,8 +291,9 @@ int dw_read_file_direct(const char* path, void* buf, uint64_t n, uint64_t file_o
     for (auto& t : ts) t.join();
     close(dfd);
     if (failed) {
-      if (errno == EINVAL) { body = 0; failed = 0; }  // O_DIRECT refused mid-way: redo buffered
-      else { set_err("pread(O_DIRECT)"); return -1; }
+      const int e = failed.load();
+      if (e == EINVAL) { body = 0; failed = 0; }  // O_DIRECT refused mid-way: redo buffered
+      else { errno = e; set_err("pread(O_DIRECT)"); return -1; }
     }
   } else if (dfd >= 0) {
     close(dfd);

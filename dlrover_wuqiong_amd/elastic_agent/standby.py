@@ -100,6 +100,7 @@ def _apply(cmd: dict):
 
 
 PINNED_PREFIX = "standby_pinned."
+WARM_PREFIX = "standby_warm."  # the warm profile was replayed (value: bytes reserved)
 
 
 def _prepin_checkpoint_shm() -> float:
@@ -239,33 +240,78 @@ def _gpu_init(lr: str) -> bool:
         return False
 
 
-def _reserve_state_memory() -> int:
-    """Fill PyTorch's caching allocator with about the HBM the worker's model
-    + optimizer will take (the checkpoint payload size, once a save made it
-    known) and leave it cached: the driver's allocation of fresh VRAM (it
-    clears every new buffer) is then paid while waiting, not inside the
-    restart (~1.9 s for the 19 GB of GPT2-1.5B Adam state).  Bounded by the
-    free HBM; DWAMD_STANDBY_RESERVE=0 disables it.  Returns bytes reserved."""
+def _reserve_state_memory(reserved: int = 0, prof: Optional[dict] = None) -> int:
+    """Fill PyTorch's caching allocator with about the HBM the worker will
+    take -- its recorded peak footprint (warm profile: model + optimizer +
+    activations), else the checkpoint payload size once a save made it known
+    -- and leave it cached: the driver's allocation of fresh VRAM (it clears
+    every new buffer) is then paid while waiting, not inside the restart
+    (~1.9 s for the 19 GB of GPT2-1.5B Adam state alone).  ``reserved``:
+    bytes already held (only the increment is allocated).  Bounded by the
+    free HBM; DWAMD_STANDBY_RESERVE=0 disables it.  Returns bytes reserved
+    (-1: skipped for good)."""
     if os.environ.get("DWAMD_STANDBY_RESERVE", "1") != "1":
         return -1
     try:
         import torch
 
         from ..flash_checkpoint.prewarm import local_state_bytes
+        from .warm_profile import reserve_bytes
 
-        want = int(local_state_bytes() * float(os.environ.get("DWAMD_STANDBY_RESERVE_FACTOR", "1.25")))
-        if want <= 0:
-            return 0
+        want = reserve_bytes(prof, local_state_bytes(), float(os.environ.get("DWAMD_STANDBY_RESERVE_FACTOR", "1.25")))
+        if want <= reserved:
+            return reserved
         free, _total = torch.cuda.mem_get_info()
-        n = min(want, int(free * 0.8) - (8 << 30))
+        n = min(want - reserved, int(free * 0.8) - (8 << 30))
         if n <= (1 << 30):
-            return -1  # no room next to the live worker: skip for good
+            return reserved or -1  # no room next to the live worker
         t = torch.empty(n, dtype=torch.uint8, device="cuda")
         del t  # stays in the allocator's cache for the worker this process becomes
-        return n
+        return reserved + n
     except Exception as e:  # never fatal
         print(f"[standby] HBM reserve skipped: {e}", file=sys.stderr)
-        return -1
+        return reserved or -1
+
+
+def _apply_warm_profile(ctl: str, lr: str) -> Optional[dict]:
+    """Replay the live worker's warm profile (its GEMMs) once it exists."""
+    from . import warm_profile
+
+    prof = warm_profile.load(ctl, lr) if ctl else None
+    if prof is None:
+        return None
+    try:
+        warm_profile.preload_kernel_library()
+        r = warm_profile.replay(prof)
+        print(f"[standby] warm profile replayed: {r['gemms']} GEMMs ({r['failed']} failed) in {r['sec']} s",
+              file=sys.stderr)
+    except Exception as e:  # never fatal
+        print(f"[standby] warm profile replay failed: {e}", file=sys.stderr)
+    return prof
+
+
+def _release_under_pressure(reserved: int) -> int:
+    """The reservation lives next to the LIVE worker on the same GPU: when
+    the device's free HBM drops under ``DWAMD_STANDBY_RELEASE_GB`` (default
+    max(16 GiB, 6 % of the card)) -- the worker's eval / activation peak /
+    its staging buffers want it -- hand the cached blocks back to the driver
+    and stop reserving.  Returns the new reservation state (-1 = released
+    for good)."""
+    if reserved <= 0:
+        return reserved
+    try:
+        import torch
+
+        free, total = torch.cuda.mem_get_info()
+        floor = float(os.environ.get("DWAMD_STANDBY_RELEASE_GB", "0")) * (1 << 30) or max(16 << 30, 0.06 * total)
+        if free < floor:
+            torch.cuda.empty_cache()
+            print(f"[standby] released {reserved / 2**30:.1f} GiB reserved HBM (device free "
+                  f"{free / 2**30:.1f} GiB < {floor / 2**30:.1f} GiB)", file=sys.stderr)
+            return -1
+    except Exception as e:  # never fatal
+        print(f"[standby] release check failed: {e}", file=sys.stderr)
+    return reserved
 
 
 def _wait_command(pin: bool, ctl: str, lr: str, interval: float = 0.25) -> bytes:
@@ -278,6 +324,7 @@ def _wait_command(pin: bool, ctl: str, lr: str, interval: float = 0.25) -> bytes
     fd = sys.stdin.fileno()
     pinned_marked = False
     reserved = 0
+    prof = None
     while b"\n" not in buf:
         if pin:
             _prepin_checkpoint_shm()
@@ -285,8 +332,16 @@ def _wait_command(pin: bool, ctl: str, lr: str, interval: float = 0.25) -> bytes
             if not pinned_marked and _pinned_bytes() > 0:
                 _mark(ctl, PINNED_PREFIX, lr, f"{_pinned_bytes()}\n")
                 pinned_marked = True
-            if not reserved:
+            if prof is None:
+                prof = _apply_warm_profile(ctl, lr)
+                if prof is not None:
+                    if reserved >= 0:
+                        reserved = _reserve_state_memory(reserved, prof)
+                    _mark(ctl, WARM_PREFIX, lr, f"{reserved}\n")
+            if reserved == 0:
                 reserved = _reserve_state_memory()
+            else:
+                reserved = _release_under_pressure(reserved)
         r, _, _ = select.select([fd], [], [], interval)
         if r:
             chunk = os.read(fd, 1 << 20)

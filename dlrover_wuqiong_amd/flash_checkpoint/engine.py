@@ -398,6 +398,12 @@ class CheckpointEngine(ABC):
                 self._gc_frozen = True
             if enabled:
                 gc.enable()
+            # under the agent: record what a replacement's first step needs
+            # (GEMMs of the next optimizer step + allocator peak) for the
+            # import-mode standby to replay (elastic_agent/warm_profile.py)
+            from ..elastic_agent import warm_profile
+
+            warm_profile.on_save()
 
     def _skip_busy(self) -> bool:
         """Reference semantics (a save is skipped while the previous one is
@@ -1026,6 +1032,10 @@ class FullCheckpointEngine(CheckpointEngine):
                     return out
                 except (KeyError, ValueError) as e:  # structure differs from the target: plain load
                     logger.info(f"fast storage load not applicable ({e}); using torch.load")
+                except OSError as e:
+                    if sliced:  # the peers are already in the slice all-gather: no private fallback
+                        raise
+                    logger.warning(f"fast storage load failed ({e}); using torch.load")
             self.last_restore_source = "storage(torch.load)"
             return torch.load(p, map_location="cpu", weights_only=True)
 
@@ -1056,7 +1066,13 @@ class ShardCheckpointEngine(FullCheckpointEngine):
         return CommonDirCheckpointSaver
 
     def load(self, resume_path="", target=None):
+        """Memory first; then ``resume_path`` (this rank's persisted shard
+        file -- shard layouts are framework-chosen, so there is no default
+        file name to fall back to)."""
         step, sd = self.get_state_dict_from_memory(target=target)
         if sd:
             return sd
+        if resume_path:
+            return self._load_from_storage(resume_path, target)
+        logger.warning(f"rank {self._rank}: no complete checkpoint in memory and no resume_path: nothing restored")
         return {}

@@ -314,7 +314,12 @@ def load_archive_into(path: str, target: Any = None, chunk_bytes: int = 256 << 2
     cuda = any(p[2].is_cuda for p in pieces) or any(t.is_cuda for _l, t in slow)
     dev = next((p[2].device for p in pieces if p[2].is_cuda), None)
     stream = torch.cuda.Stream(dev) if cuda and dev is not None else None
-    bufs = [_aligned_host(chunk_bytes + 2 * _ALIGN, pinned=cuda) for _ in range(2)]
+    if stream is not None:
+        # work still queued on the caller's stream (init kernels of a model
+        # just built, .to(device), zeroed optimizer state) writes the same
+        # tensors: order the restore copies after it
+        stream.wait_stream(torch.cuda.current_stream(dev))
+    bufs =[_aligned_host(chunk_bytes + 2 * _ALIGN, pinned=cuda) for _ in range(2)]
     events = [None, None]
     nb = 0
     i = 0

@@ -144,6 +144,7 @@ def cast_to_fp8(x: torch.Tensor, st: Fp8State, idx: int, fmt: str) -> torch.Tens
         return out.view(_TORCH_DT[fmt])
     xf = x.float()
     a = xf.abs().max() if xf.numel() else xf.new_zeros(())
+    a = torch.where(torch.isnan(a), torch.full_like(a, float("inf")), a)  # as the kernels: NaN records +inf
     cur = st.amax_bits[idx: idx + 1].view(torch.float32)
     cur.copy_(torch.maximum(cur, a.reshape(1)))
     lim = FP8_MAX[fmt]

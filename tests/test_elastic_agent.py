@@ -164,3 +164,20 @@ def test_import_standby_helpers_without_gpu(monkeypatch):
     assert "torch._dynamo" in sys.modules
     assert standby._gpu_init("0") is False
     assert standby._reserve_state_memory() in (0, -1)
+
+
+def test_import_standby_releases_reservation_under_pressure(monkeypatch):
+    """The standby's cached HBM goes back to the driver once the live
+    worker's allocations push device free memory under the floor."""
+    import torch
+
+    from dlrover_wuqiong_amd.elastic_agent import standby
+
+    freed = []
+    free = {"v": 100 << 30}
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda *a: (free["v"], 288 << 30))
+    monkeypatch.setattr(torch.cuda, "empty_cache", lambda: freed.append(1))
+    assert standby._release_under_pressure(20 << 30) == 20 << 30 and not freed
+    free["v"] = 10 << 30  # the worker grew: 10 GiB left < max(16 GiB, 6 % of 288)
+    assert standby._release_under_pressure(20 << 30) == -1 and freed == [1]
+    assert standby._release_under_pressure(-1) == -1 and freed == [1]  # released for good

@@ -283,3 +283,25 @@ def test_staging_ring_shape_follows_hbm_budget():
     c.ring_hbm, c.staging_mode, c._ring_auto = 0, "auto", 40 << 30
     assert c._ring_shape(100 << 30) == (40, 1 << 30)  # auto: the free HBM
     assert c._ring_shape(1 << 20)[0] == 4  # a tiny slice keeps the minimal ring
+
+
+def test_shard_engine_load_falls_back_to_resume_path(tmp_path):
+    """ShardCheckpointEngine with nothing in memory reads this rank's
+    persisted shard from ``resume_path`` (it used to return {} silently)."""
+    from dlrover_wuqiong_amd.flash_checkpoint.engine import ShardCheckpointEngine
+    from dlrover_wuqiong_amd.flash_checkpoint.shm_handler import SharedMemoryHandler
+
+    SharedMemoryHandler(0).unlink()
+    p = tmp_path / "shard_0.pt"
+    ref = {"w": torch.randn(257, 3), "step": 4}
+    torch.save(ref, p)
+    eng = ShardCheckpointEngine(str(tmp_path / "ck"))
+    try:
+        assert eng.load() == {}
+        out = eng.load(resume_path=str(p))
+        assert torch.equal(out["w"], ref["w"]) and out["step"] == 4
+        tgt = {"w": torch.zeros(257, 3), "step": 0}
+        out = eng.load(resume_path=str(p), target=tgt)
+        assert torch.equal(tgt["w"], ref["w"])
+    finally:
+        eng.close()

@@ -455,3 +455,25 @@ def test_gpu_busy_save_is_skipped(tmp_path, monkeypatch):
     torch.cuda.synchronize()
     assert target["w"].abs().sum().item() > 0
     ck.close()
+
+
+def test_gpu_storage_restore_orders_after_queued_writes(tmp_path):
+    """load_archive_into's side-stream H2D copies must wait for work still
+    queued on the caller's stream: a long chain of kernels that writes the
+    target right before the load must not overwrite the restored values."""
+    from dlrover_wuqiong_amd.flash_checkpoint.storage_loader import load_archive_into
+
+    torch.manual_seed(0)
+    ref = {"w": torch.randn(64 << 20, dtype=torch.float32)}  # 256 MB
+    path = str(tmp_path / "a.pt")
+    torch.save(ref, path)
+    tgt = {"w": torch.empty(64 << 20, dtype=torch.float32, device="cuda")}
+    big = torch.randn(4096, 4096, device="cuda")
+    torch.cuda.synchronize()
+    for _ in range(20):  # tens of ms of queued work ending in a write to the target
+        big = big @ big
+        big.div_(big.norm())
+    tgt["w"].fill_(7.0)
+    load_archive_into(path, target=tgt)
+    torch.cuda.synchronize()
+    assert torch.equal(tgt["w"].cpu(), ref["w"])

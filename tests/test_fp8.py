@@ -105,3 +105,21 @@ def test_auto_accelerate_fp8_strategy_trains():
     assert losses[-1] < 0.5 * losses[0]
     st = fp8.fp8_state("cpu")
     assert st.steps == 30 and float(st.scale[: st.n].min()) != 1.0
+
+
+def test_cast_nan_stays_nan_and_amax_backs_off():
+    """NaN survives the saturating cast (so loss-spike / NaN checks see it),
+    and the recorded amax is +inf, so the next update halves the scale --
+    the contract the GPU kernels follow (tests/test_fp8_gpu.py)."""
+    from dlrover_wuqiong_amd.ops import fp8
+
+    st = fp8.fp8_state("cpu", history_len=4)
+    i = st.register("e4m3")
+    x = torch.randn(16, 8)
+    x[2, 3] = float("nan")
+    x[4, 4] = float("inf")
+    x8 = fp8.cast_to_fp8(x, st, i, "e4m3").float()
+    assert torch.isnan(x8[2, 3]) and x8[4, 4].item() == 448.0
+    assert st.amax_bits[i].view(torch.float32).item() == float("inf")
+    st.update()
+    assert st.scale[i].item() == pytest.approx(0.5)

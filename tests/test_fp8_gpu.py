@@ -129,3 +129,53 @@ def test_auto_accelerate_fp8_gpt2_trains():
         res.optim.zero_grad()
         losses.append(float(loss))
     assert all(map(lambda v: v == v, losses)) and losses[-1] < losses[0] - 0.5, losses
+
+
+@pytest.mark.parametrize("fmt", ["e4m3", "e5m2"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_cast_keeps_nan_and_records_inf_amax(fmt, dtype):
+    """A NaN input stays NaN in both cast kernels (fmaxf / fminf would turn
+    it into -fmax), +-inf saturates, and the recorded amax is +inf so the
+    next delayed-scaling update backs off -- the same as the CPU path."""
+    from dlrover_wuqiong_amd.ops import fp8
+
+    st = fp8.fp8_state("cuda")
+    i = st.register(fmt)
+    x = torch.randn(256, 64, device="cuda").to(dtype)
+    x[3, 5] = float("nan")
+    x[7, 9] = float("inf")
+    x[100, 63] = -float("inf")
+    lim = fp8.FP8_MAX[fmt]
+    for cast in ("flat", "t"):
+        st.amax_bits.zero_()
+        if cast == "flat":
+            x8 = fp8.cast_to_fp8(x, st, i, fmt).float().view(256, 64)
+            x8t = None
+        else:
+            x8, x8t = fp8.cast_to_fp8_t(x, st, i, fmt)
+            x8, x8t = x8.float(), x8t.float()
+        assert torch.isnan(x8[3, 5]) and x8[7, 9].item() == lim and x8[100, 63].item() == -lim
+        assert torch.isnan(x8).sum().item() == 1
+        if x8t is not None:
+            assert torch.isnan(x8t[5, 3]) and torch.isnan(x8t).sum().item() == 1
+        assert st.amax_bits[i].view(torch.float32).item() == float("inf")
+    cpu_st = fp8.Fp8State(torch.device("cpu"))
+    j = cpu_st.register(fmt)
+    ref = fp8.cast_to_fp8(x.cpu(), cpu_st, j, fmt)
+    assert torch.equal(torch.isnan(ref.float()), torch.isnan(x8.cpu()))
+    assert cpu_st.amax_bits[j].view(torch.float32).item() == float("inf")
+
+
+def test_fp8_linear_propagates_nan():
+    from dlrover_wuqiong_amd.ops import fp8
+
+    torch.manual_seed(0)
+    lin = nn.Linear(256, 512, device="cuda", dtype=torch.bfloat16)
+    f8 = fp8.Fp8Linear(lin, "HYBRID")
+    x = torch.randn(4, 64, 256, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    with torch.no_grad():
+        x[0, 0, 0] = float("nan")
+    y = f8(x)
+    assert torch.isnan(y.float()).any()
+    y.float().sum().backward()
+    assert not torch.isfinite(lin.weight.grad.float()).all()

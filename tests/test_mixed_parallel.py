@@ -94,7 +94,7 @@ def test_eight_rank_tp2_pp2_dp2_loss_parity():
     assert got[1] < got[0]
 
 
-def _lsgd_worker(rank, world, port, q):
+def _lsgd_worker(rank, world, port, q, warmup=1, per_rank_init=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
     from dlrover_wuqiong_amd.atorch import distributed as adist
@@ -105,16 +105,23 @@ def _lsgd_worker(rank, world, port, q):
 
         adist.init_distributed("gloo")
         model = _llama()
+        if per_rank_init:  # every rank its own random init: the wrapper must sync the replicas
+            torch.manual_seed(1000 + rank)
+            for p_ in model.parameters():
+                p_.data.normal_(0, 0.02)
         ok, res, strat = auto_accelerate(
             model, torch.optim.AdamW, optim_args={"lr": 1e-2}, fused_optimizer=False,
             load_strategy=[("parallel_mode", ([("zero", 2), ("data", 2)], None)),
                            ("fsdp", {"wrap_cls": (LlamaDecoderLayer,), "use_local_sgd": True,
-                                     "local_sgd_sync_interval": 2, "local_sgd_warmup_steps": 1,
+                                     "local_sgd_sync_interval": 2, "local_sgd_warmup_steps": warmup,
                                      "outer_optim_class": torch.optim.SGD,
                                      "outer_optim_kwargs": {"lr": 0.7, "momentum": 0.9, "nesterov": True}})])
         opt = res.optim
         rg = opt.group
-        states = []
+        flat = opt._flat()
+        other = [torch.zeros_like(flat) for _ in range(dist.get_world_size(rg))]
+        dist.all_gather(other, flat, group=rg)
+        states = [(0, all(torch.equal(o, other[0]) for o in other), 0, False)]
         for step in range(5):
             ids, tgt = _batch(step)
             ids, tgt = ids[rank: rank + 1], tgt[rank: rank + 1]  # every rank its own sample
@@ -154,5 +161,23 @@ def test_four_rank_hsdp_local_sgd():
         assert isinstance(states, list), res
         # step 1: warm-up (HSDP all-reduce) -> replicas equal; then local
         # steps 2 (drift), 3 (sync), 4 (drift), 5 (sync)
-        assert [s[1] for s in states] == [True, False, True, False, True], states
+        assert [s[1] for s in states] == [True, True, False, True, False, True], states
         assert states[-1][2] == 2
+
+
+def test_four_rank_hsdp_local_sgd_per_rank_init_no_warmup():
+    """warmup_steps=0 and a different random init on every rank: the
+    replicas still start from one model and agree after every sync."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_lsgd_worker, args=(r, 4, port, q, 0, True)) for r in range(4)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in ps), key=lambda x: x[0])
+    for p in ps:
+        p.join(timeout=60)
+    for _r, states in res:
+        assert isinstance(states, list), res
+        # init synced; local steps 1 (drift), 2 (sync), 3 (drift), 4 (sync), 5 (drift)
+        assert [s[1] for s in states] == [True, False, True, False, True, False], states
