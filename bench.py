@@ -101,9 +101,9 @@ def parse(argv=None):
     p.add_argument("--no-import-fault", action="store_true",
                    help="skip the second job (failure under the default --standby-mode import)")
     p.add_argument("--import-window", type=int, default=32, help="fault-window steps of the import-mode job")
-    p.add_argument("--import-hbm-tier", action="store_true",
-                   help="import-mode job with the standby-owned HBM tier (framework default) instead of the "
-                        "reference-comparable host-shm restore")
+    p.add_argument("--no-import-hbm", action="store_true",
+                   help="skip the third job (failure under the framework default: import standbys that own the "
+                        "HBM tier); the second job always restores from host shm (reference semantics)")
     p.add_argument("--inject-slow-flush", type=float, default=0.0,
                    help="fault injection: from the fault window on, each shm flush sleeps this long after its "
                         "HBM snapshot (the kill then always lands mid-flush: HBM-only restore)")
@@ -111,7 +111,7 @@ def parse(argv=None):
                    help="N ranks share cuda:0 over gloo: rehearses the N>1 fault path on one GPU")
     # worker-only
     p.add_argument("--run-dir", default="", help=argparse.SUPPRESS)
-    p.add_argument("--phase", default="deep", choices=["deep", "import"], help=argparse.SUPPRESS)
+    p.add_argument("--phase", default="deep", choices=["deep", "import", "import_hbm"], help=argparse.SUPPRESS)
     return p.parse_args(argv)
 
 
@@ -169,15 +169,18 @@ def _job(a, n: int, mode: str, run_dir: str, tag: str):
     })
     if a.rehearse_shared_device:
         env["DWAMD_REHEARSE_SHARED_DEVICE"] = "1"
-    if mode == "import" and not a.import_hbm_tier:
+    if mode == "import":
         # the reference's restart semantics: the replacement restores from
-        # host shm (the framework default also gives import standbys the HBM tier)
+        # host shm (the framework default -- job "import_hbm" -- also gives
+        # import standbys the HBM tier)
         env["DWAMD_HBM_TIER"] = "0"
+    phase = mode
+    mode = "import" if mode == "import_hbm" else mode
     wargs = [os.path.abspath(__file__), "--run-dir", run_dir, "--gpus", str(n), "--steps", str(a.steps),
              "--warmup", str(a.warmup), "--model", a.model, "--micro-batch", str(a.micro_batch), "--seq",
              str(a.seq), "--ckpt-interval", str(a.ckpt_interval), "--fault-window",
              str(a.fault_window if mode == "deep" else a.import_window), "--ckpt-dir", ckpt_dir, "--lr", str(a.lr),
-             "--phase", mode]
+             "--phase", phase]
     if a.inject_slow_flush > 0 and mode == "deep":
         wargs += ["--inject-slow-flush", str(a.inject_slow_flush)]
     for flag in ("no_fault", "no_persist", "act_ckpt"):
@@ -230,27 +233,36 @@ def launcher(a) -> int:
             res = summarize(a, run_dir, n, wall)
         finally:
             _cleanup(prefix, ck)
+        jobs = []
         if res is not None and not a.no_fault and not a.no_import_fault:
-            idir = os.path.join(run_dir, "import")
-            rc2, wall2, prefix2, ck2 = _job(a, n, "import", idir, "i")
+            jobs.append(("import", "i", "import_mode"))
+            if not a.no_import_hbm:
+                jobs.append(("import_hbm", "h", "import_mode_hbm"))
+        for mode, tag, key in jobs:
+            idir = os.path.join(run_dir, mode)
+            rc2, wall2, prefix2, ck2 = _job(a, n, mode, idir, tag)
             try:
-                imp = summarize_import(a, idir, wall2)
+                imp = summarize_import(a, idir, wall2, mode)
             finally:
                 _cleanup(prefix2, ck2)
-            res["import_mode"] = imp
-            if imp is not None:
-                res["load_sec_shm"] = imp.get("load_sec")
-                res["recover_sec_import"] = imp.get("recover_sec")
-                res["goodput_pct_import"] = imp.get("goodput_pct")
-                if imp.get("load_sec") is not None and a.model == "gpt2-1.5b":
-                    # the reference's 3.7 s is a restarted process restoring
-                    # from host memory: compare the like-for-like number
-                    res["load_vs_baseline"] = round(imp["load_sec"] / REF_LOAD_SEC, 4)
-                    res["load_vs_baseline_basis"] = "load_sec_shm (restart restore from host shm)"
+            res[key] = imp
             if rc2:
-                # the headline (deep-job) numbers stand; the extra job's
+                # the headline (deep-job) numbers stand; an extra job's
                 # failure is reported in the line, not as the run's status
-                res["import_mode_rc"] = rc2
+                res[key + "_rc"] = rc2
+            if imp is None or imp.get("load_sec") is None:
+                continue
+            src = imp.get("restore_source") or "unknown"
+            sfx = "" if mode == "import" else "_hbm_tier"
+            # keys follow where the bytes really came from
+            res[("load_sec_" if mode == "import" else "load_sec_import_") + src.replace("->", "_to_")] = imp["load_sec"]
+            res["recover_sec_import" + sfx] = imp.get("recover_sec")
+            res["goodput_pct_import" + sfx] = imp.get("goodput_pct")
+            if mode == "import" and src == "shm" and a.model == "gpt2-1.5b":
+                # the reference's 3.7 s is a restarted process restoring
+                # from host memory: compare the like-for-like number
+                res["load_vs_baseline"] = round(imp["load_sec"] / REF_LOAD_SEC, 4)
+                res["load_vs_baseline_basis"] = "load_sec_shm (restarted process, restore from host shm)"
         if res is not None:
             res["launcher_wall_s"] = round(time.time() - T_LAUNCH, 1)
     finally:
@@ -311,6 +323,11 @@ def summarize(a, run_dir, n, wall):
         "loss": phase0["loss"],
         "rccl_world": phase0["world"],
         "backend": phase0.get("backend"),
+        # replicated state split 1/N across the node's ranks (each snapshots
+        # and restores its slice; restores meet in an all-gather)
+        "ckpt_slices": phase0.get("slices"),
+        "restore_gather_group": phase0.get("gather"),
+        "hbm_plan": phase0.get("hbm_plan"),  # per-GPU budget preflight (flash_checkpoint/hbm_budget.py)
         "launcher_wall_s": round(wall, 1),
     }
     persist = next((e for e in ev if e["event"] == "persisted"), None)
@@ -383,6 +400,7 @@ def _fault_summary(a, ev, agent, step_sec, save_sec):
         },
         "standby_prepin_s": inc1.get("prepin_s"),
         "restore_source": inc1.get("restore_source"),
+        "restore_gather": inc1.get("restore_gather"),
         "restore_phases_s": inc1.get("restore_phases"),
         "restarts": len(started) - 1,
     }
@@ -395,15 +413,16 @@ def _fault_summary(a, ev, agent, step_sec, save_sec):
     return out
 
 
-def summarize_import(a, run_dir, wall):
+def summarize_import(a, run_dir, wall, mode="import"):
     """The failure under the agent's default ``--standby-mode import``: the
-    replacement runs the script from the top and restores from host shm."""
+    replacement runs the script from the top and restores from host shm
+    (``import``) or from its own HBM-tier buffers (``import_hbm``)."""
     ev = _read_jsonl(os.path.join(run_dir, "steps.jsonl"))
     agent = _read_jsonl(os.path.join(run_dir, "agent.jsonl"))
     phase0 = next((e for e in ev if e["event"] == "phase0"), None)
     if phase0 is None:
         return None
-    out = {"standby_mode": "import", "train_step_ms": round(1000 * phase0["step_sec"], 2),
+    out = {"standby_mode": "import", "hbm_tier": mode == "import_hbm", "train_step_ms": round(1000 * phase0["step_sec"], 2),
            "first_save_sec": round(phase0["first_save_sec"], 4) if phase0.get("first_save_sec") else None,
            "launcher_wall_s": round(wall, 1)}
     fs = _fault_summary(a, ev, agent, phase0["step_sec"], phase0.get("save_sec_mean", 0.0))
@@ -592,7 +611,7 @@ def worker(a) -> int:
                 os.path.exists(os.path.join(ctl, m.format(i))) for i in range(lw) for m in marks):
             time.sleep(0.05)
 
-    if incarnation == 0 and a.phase == "import":
+    if incarnation == 0 and a.phase in ("import", "import_hbm"):
         # ---------------- import-standby job: warm-up, step time, then the fault window
         first_save = None
         for _ in range(a.warmup):
@@ -612,7 +631,8 @@ def worker(a) -> int:
         # this worker's warm profile -- recorded during the warm-up)
         wait_standbys(["standby_ready.{}"])
         if cuda:
-            wait_standbys(["standby_warm.{}"], timeout=90.0)
+            wait_standbys(["standby_warm.{}"] + (["hbm_staging.{}.json"] if a.phase == "import_hbm" else []),
+                          timeout=90.0)
         dt, _ok = save()
         ckpt.wait_latest_checkpoint()
         sync_all()
@@ -715,7 +735,8 @@ def worker(a) -> int:
               "load_sec_warm": load_warm, "load_ok": load_ok, "replicas_identical": replicas_identical,
               "ckpt_bytes": ckpt_bytes, "first_save_sec": first_save, "timed_saves": len(save_times),
               "timed_saves_ok": timed_ok, "skipped_saves_timed": skipped_timed, "rehearsal": rehearsal,
-              "backend": backend})
+              "backend": backend, "slices": ckpt.engine._num_slices, "hbm_plan": getattr(ckpt.engine, "hbm_plan", None),
+              "gather": ckpt.engine._gather_group is not None})
 
         # ---------------- DISK persist (agent: torch.save archive written from
         # shm with parallel pwrite) while training continues: persist time and
@@ -811,6 +832,7 @@ def worker(a) -> int:
               "build_marks": {k: round(v - t_proc, 3) for k, v in marks.items()},
               "prepin_s": info.get("prepin_s") if info else None, "standby": "deep" if info else "import",
               "restore_source": getattr(ckpt.engine, "last_restore_source", None),
+              "restore_gather": getattr(ckpt.engine._copier, "last_restore_gather", None),
               "restore_phases": dict(getattr(ckpt.engine, "last_restore_breakdown", {}) or {},
                                      device_wait=round(restore_dev, 4))})
         if not restore_ok:

@@ -294,6 +294,7 @@ class ElasticTrainingAgent:
             NodeEnv.DLROVER_MASTER_ADDR: self.client.master_addr,
             "HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
             "DWAMD_AGENT_CTL_DIR": self.ctl_dir,
+            "DWAMD_STANDBY_MODE": self.config.standby_mode,  # the HBM-budget preflight sizes for it
         })
         env.setdefault("OMP_NUM_THREADS", "1")
         return env

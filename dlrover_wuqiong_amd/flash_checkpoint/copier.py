@@ -447,11 +447,12 @@ class GpuCopier:
             return
         nb = 1
         if os.environ.get("DWAMD_STAGING_BUFFERS", "auto") != "1":
+            from .hbm_budget import staging_buffers
+
             try:
                 free, _total = torch.cuda.mem_get_info(self.device)
                 have = sum(t.numel() for t in self._stagings if t is not None)
-                if free + have >= 2 * nbytes + self.staging_reserve:
-                    nb = 2
+                nb = staging_buffers(free, have, nbytes, self.staging_reserve)
             except Exception:
                 nb = 1
         self._nbuf = nb
@@ -676,7 +677,9 @@ class GpuCopier:
             try:
                 free, _total = torch.cuda.mem_get_info(self.device)
                 have = sum(t.numel() for t in self._stagings if t is not None)
-                ring = free + have < n + self.staging_reserve
+                from .hbm_budget import use_ring
+
+                ring = use_ring(free, have, n, self.staging_reserve)
                 self._ring_auto = max(0, free + have - self.staging_reserve)
             except Exception:
                 ring = False
@@ -873,24 +876,47 @@ class GpuCopier:
             return
         import torch.distributed as dist
 
+        from .gather import all_gather_slices
+        from .hbm_budget import gather_chunk
+
         per = hi - lo
-        # a temporary buffer, never the staging buffers: with the HBM tier they
-        # hold the checkpoint being restored
-        full = torch.empty(per * world, dtype=torch.uint8, device=self.device)
-        # every rank's slice has the same size `per` (last one may be short in
-        # payload terms but is padded): copy what exists.
-        real = max(0, min(hi, payload_bytes) - lo)
-        if real > 0:
-            if hbm_src is not None:
-                launch_multi_copy(build_descs([(hbm_src, full.data_ptr() + lo, real)], self.device), cur)
-            else:
-                self._pipelined_h2d([(shm_payload_addr + lo, full.data_ptr() + lo, real)], cur)
-        mine = full[lo: lo + per]
-        dist.all_gather_into_tensor(full, mine, group=gather_group)
-        base = full.data_ptr()
-        descs = build_descs([(base + off, dst, n) for off, dst, n in _merge_pieces(pieces_gpu)], self.device)
-        launch_multi_copy(descs, cur)
-        del full
+        rank = dist.get_rank(gather_group)
+        try:
+            free, _t = torch.cuda.mem_get_info(self.device)
+        except Exception:
+            free = 0
+        # the gather's temporary (never the staging buffers: with the HBM tier
+        # they hold the checkpoint being restored) is bounded: world x c bytes
+        # per round (hbm_budget.gather_chunk), the whole payload in one round
+        # when it fits
+        c = min(per, gather_chunk(per, world, free))
+        tmp = torch.empty(c * world, dtype=torch.uint8, device=self.device)
+        merged = _merge_pieces(pieces_gpu)
+        self.last_restore_gather = {"rounds": -(-per // c) if per else 0, "chunk": c, "temp_bytes": c * world}
+        for o in range(0, per, c):
+            n = min(c, per - o)
+            buf = tmp[: n * world]
+            # every rank's slice has the same size ``per`` (the last one may be
+            # short in payload terms, padded): copy what exists of this round
+            real = max(0, min(lo + o + n, payload_bytes) - (lo + o))
+            dst0 = buf.data_ptr() + rank * n
+            if real > 0:
+                if hbm_src is not None:
+                    launch_multi_copy(build_descs([(hbm_src + o, dst0, real)], self.device), cur)
+                else:
+                    self._pipelined_h2d([(shm_payload_addr + lo + o, dst0, real)], cur)
+            self.last_restore_gather["transport"] = all_gather_slices(buf, buf[rank * n: (rank + 1) * n],
+                                                                      gather_group)
+            base = buf.data_ptr()
+            scatter = []
+            for r in range(world):
+                a, b = r * per + o, r * per + o + n  # payload bytes of rank r's part of this round
+                for off, dst, m in merged:
+                    x0, x1 = max(a, off), min(b, off + m)
+                    if x0 < x1:
+                        scatter.append((base + r * n + (x0 - a), dst + (x0 - off), x1 - x0))
+            launch_multi_copy(build_descs(scatter, self.device), cur)
+        del tmp
 
     def write_back(self, dev_src: int, host_dst: int, nbytes: int):
         """D2H of ``nbytes`` from a device address into (shm) host memory,

@@ -212,20 +212,23 @@ class CheckpointEngine(ABC):
             self._ctl_group = None
         else:
             self._ctl_group = dist.new_group(backend="gloo", timeout=timedelta(seconds=120))
-        # intra-node group for the replicated all-gather restore
+        # intra-node group for the replicated all-gather restore.  RCCL over
+        # xGMI on MI355X; a gloo world (CPU rehearsal, ranks sharing one GPU)
+        # takes the SAME sliced-restore branches with the gather staged through
+        # pinned host memory (gather.py).  DWAMD_GLOO_GATHER=shm: the older
+        # gloo-only path where slices meet in the node's shm instead.
         if self._replicated and self._local_world > 1:
             n_nodes = self._world // self._local_world
             gb = comm_backend or backend
+            host_meet = gb == "gloo" and os.environ.get("DWAMD_GLOO_GATHER", "staged") == "shm"
             if n_nodes <= 1:
-                self._gather_group = dist.group.WORLD if backend != "gloo" else None
+                self._gather_group = None if host_meet else dist.group.WORLD
             else:
                 for node in range(n_nodes):
                     ranks = list(range(node * self._local_world, (node + 1) * self._local_world))
                     g = dist.new_group(ranks=ranks, backend=gb)
-                    if self._rank in ranks and gb != "gloo":
+                    if self._rank in ranks and not host_meet:
                         self._gather_group = g
-            # a gloo world (CPU rehearsal, ranks sharing one GPU) has no device
-            # all-gather: slices meet in the node's shm instead
             self._gather_on_host = self._gather_group is None
 
     def _ctl_barrier(self):
@@ -310,12 +313,34 @@ class CheckpointEngine(ABC):
             h.init_shared_memory(create=True, size=total, owner=self._owner_id)
             self._generation += 1
             self._next_slot = None
+        if need_resize:
+            self._log_hbm_plan(total)
         key = (h.shared_memory.ino if h.shared_memory is not None else -1, total)
         if self._prepped_for != key:
             # new segment, or an existing one this process attached (restart):
             # make sure every slot this rank writes is pinned before its flush
             self._prepped_for = key
             self._start_shm_prep(total, prefault=need_resize)
+
+    def _log_hbm_plan(self, payload: int):
+        """HBM-budget preflight (hbm_budget.py) for this GPU, logged once per
+        payload size: staging, standby, restore-gather temporary."""
+        self.hbm_plan = None
+        if not torch.cuda.is_available() or payload <= 0:
+            return
+        try:
+            from .hbm_budget import plan
+
+            dev = torch.cuda.current_device()
+            _free, total = torch.cuda.mem_get_info(dev)
+            state = int(torch.cuda.memory_allocated(dev))
+            p = plan(total, worker_state=state, worker_peak=max(state, int(torch.cuda.max_memory_reserved(dev))),
+                     payload=payload, world_local=self._num_slices if self._replicated else self._local_world,
+                     replicated=self._replicated, standby=os.environ.get("DWAMD_STANDBY_MODE", "import"))
+            self.hbm_plan = p.as_dict()
+            logger.info(f"rank {self._rank}: HBM budget {self.hbm_plan}")
+        except Exception as e:  # a log line must never fail a save
+            logger.warning(f"HBM budget preflight skipped: {e}")
 
     def _quiesce_shm_users(self):
         """Before this process unmaps its segment (resize, a stale mapping
@@ -857,6 +882,7 @@ class CheckpointEngine(ABC):
         total = h.payload_size
         copier = self._device_copier() if gpu_pieces else None
         if copier is None:
+            self.last_restore_source = "shm"  # host tensors: copied straight from the slot
             it = iter([t for _, t in pairs])
             return traverse(tree, lambda v: next(it) if isinstance(v, TensorMeta) else v)
         s_lo, s_hi = split_ranges(total, self._num_slices)[self._slice_idx]

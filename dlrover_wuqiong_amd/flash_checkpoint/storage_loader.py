@@ -375,9 +375,13 @@ def load_archive_into(path: str, target: Any = None, chunk_bytes: int = 256 << 2
         import torch.distributed as dist
 
         t_g = time.perf_counter()
+        from .gather import all_gather_slices
+
         for full, per in gathers:
             a0 = slice_idx * per
-            dist.all_gather_into_tensor(full, full[a0: a0 + per].clone(), group=gather_group)
+            stats_t = all_gather_slices(full, full[a0: a0 + per], gather_group)
+            if stats is not None:
+                stats["gather_transport"] = stats_t
         torch.cuda.current_stream(gathers[0][0].device).synchronize()
         if stats is not None:
             stats["gather_s"] = round(time.perf_counter() - t_g, 4)

@@ -41,3 +41,26 @@ def test_bench_two_ranks_real_kill(tmp_path):
     assert imp["standby_mode"] == "import" and imp["restarts"] == 1 and imp["load_verified_after_restart"]
     assert res["load_sec_shm"] == imp["load_sec"] and res["goodput_pct_import"] == imp["goodput_pct"]
     assert res["recover_sec_import"] > 0 and imp["recovery_breakdown_s"]["process_to_model_built"] is not None
+    # and under the framework default (import standbys owning the HBM tier)
+    hbm = res["import_mode_hbm"]
+    assert hbm["hbm_tier"] is True and hbm["restarts"] == 1 and hbm["load_verified_after_restart"]
+    assert res["goodput_pct_import_hbm_tier"] == hbm["goodput_pct"]
+
+
+def test_bench_eight_ranks_sliced(tmp_path):
+    """The N=8 path the driver runs on a whole node, rehearsed on CPU/gloo:
+    8 ranks, the replicated checkpoint split 8 ways (each rank snapshots and
+    restores 1/8; the restore all-gathers), a real SIGKILL and a restart
+    from deep standbys."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "8", "--model", "gpt2-tiny", "--micro-batch",
+           "1", "--seq", "32", "--steps", "4", "--warmup", "1", "--fault-window", "12", "--no-import-fault",
+           "--no-persist", "--ckpt-dir", str(tmp_path / "ckpt"), "--timeout", "400"]
+    r = subprocess.run(cmd, env=env, cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=480)
+    assert r.returncode == 0, r.stderr[-20000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["n_gpus"] == 8 and res["rccl_world"] == 8 and res["config"]["parallelism"] == "dp8"
+    assert res["ckpt_slices"] == 8 and res["restore_gather_group"] is True
+    assert res["load_verified"] and res["replicas_identical"] and res["timed_saves_ok"]
+    assert res["restarts"] == 1 and res["load_verified_after_restart"]
