@@ -111,6 +111,12 @@ def _device() -> torch.device:
     return torch.device("cpu")
 
 
+def _meta_model(model) -> bool:
+    from .meta_init import is_meta
+
+    return is_meta(model)
+
+
 def _default_prepare_input(data, device):
     if torch.is_tensor(data):
         return data.to(device, non_blocking=True)
@@ -559,6 +565,31 @@ def _apply_fsdp(ctx, cfg, reshard=True):
         _g, ranks = adist.parallel_group_and_ranks("data")
         mesh = DeviceMesh("cuda" if torch.cuda.is_available() else "cpu", ranks, mesh_dim_names=("data",))
     model = ctx["model"]
+    cfgd = dict(cfg) if isinstance(cfg, dict) else {}
+    # meta-device model (init_empty_weights / torch.device("meta")): shard
+    # first, then materialise only this rank's shards (atorch/meta_init.py)
+    from . import meta_init
+
+    here_meta = meta_init.is_meta(model)
+    flags = torch.tensor([int(here_meta), int(not here_meta and dist.get_rank() == 0)], dtype=torch.int64)
+    flags_dev = flags.to(_device()) if dist.get_backend() != "gloo" else flags
+    dist.all_reduce(flags_dev, op=dist.ReduceOp.MAX)
+    any_meta, rank0_real = (bool(x) for x in flags_dev.cpu().tolist())
+    sync = bool(cfgd.get("sync_module_states"))
+    full_rank0 = None
+    if any_meta:
+        if here_meta is False and dist.get_rank() != 0:
+            raise RuntimeError("meta-device init: a rank other than 0 holds a real model while others are meta")
+        if rank0_real and not sync:
+            raise ValueError("rank 0 holds a real model and the other ranks a meta one: pass "
+                             "sync_module_states=True to scatter rank 0's weights")
+        if rank0_real:
+            full_rank0 = meta_init.capture_full_states(model) if dist.get_rank() == 0 else None
+            cfgd["_rank0_real"] = True
+    elif sync:
+        # every rank built the full model: rank 0's initial weights win
+        meta_init.sync_full_module_states(model, src=0)
+        logger.info("fsdp: sync_module_states -- parameters and buffers broadcast from rank 0")
     extra = {}
     if isinstance(cfg, dict) and cfg.get("cpu_offload"):
         # parameters, gradients and optimizer state live on the host; the
@@ -585,6 +616,12 @@ def _apply_fsdp(ctx, cfg, reshard=True):
             fully_shard(m, mesh=mesh, mp_policy=mp, reshard_after_forward=reshard, **extra)
             n += 1
     fully_shard(model, mesh=mesh, mp_policy=mp, reshard_after_forward=reshard, **extra)
+    if any_meta:
+        dev = torch.device("cpu") if cfgd.get("cpu_offload") else _device()
+        how = meta_init.materialize_sharded(model, dev, cfgd, full_rank0)
+        del full_rank0
+        logger.info(f"fsdp: meta-device model materialised per shard on {dev} ({how})")
+        ctx["meta_init"] = how
     ctx["fsdp"] = True
     ctx.pop("amp_dtype_autocast", None)
     logger.info(f"fsdp: {n} layers sharded (reshard_after_forward={reshard})")
@@ -726,12 +763,15 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
     for name, cfg in strategy.opts:
         if name == "parallel_mode":
             APPLY[name](ctx, cfg)
-            if dev.type == "cuda" and not {"pipeline_parallel", "mixed_parallel"} & set(strategy.names()):
+            if (dev.type == "cuda" and not {"pipeline_parallel", "mixed_parallel"} & set(strategy.names())
+                    and not _meta_model(ctx["model"])):
                 ctx["model"] = ctx["model"].to(dev)  # a pipeline moves only its own stage later
             continue
         APPLY[name](ctx, cfg)
     model = ctx["model"]
-    if dev.type == "cuda":
+    if _meta_model(model):
+        raise RuntimeError("a meta-device model needs the fsdp / zero2 strategy (it materialises per shard)")
+    if dev.type == "cuda" and not ctx.get("meta_init"):
         model = model.to(dev)
     if ctx.get("amp_dtype") is not None and not ctx.get("fsdp") and not ctx.get("pipeline"):
         model = _AutocastModule(model, ctx["amp_dtype"])

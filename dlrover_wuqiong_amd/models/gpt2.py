@@ -127,6 +127,13 @@ class GPT2(nn.Module):
             if n.endswith("c_proj.weight"):
                 nn.init.normal_(p, 0.0, 0.02 / math.sqrt(2 * cfg.n_layer))
 
+    def init_spec(self, name: str):
+        """Distribution of parameter ``name`` for sharded meta-device init
+        (atorch/meta_init.py); None: by module type."""
+        if name.endswith("c_proj.weight"):
+            return ("normal", 0.0, 0.02 / math.sqrt(2 * self.cfg.n_layer))
+        return None
+
     @staticmethod
     def _init(m):
         if isinstance(m, nn.Linear):

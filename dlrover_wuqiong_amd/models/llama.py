@@ -215,6 +215,14 @@ class Llama(nn.Module):
             if n.endswith("o_proj.weight") or n.endswith("down_proj.weight"):
                 nn.init.normal_(p, 0.0, std)
 
+    def init_spec(self, name: str):
+        """Distribution of parameter ``name`` for sharded meta-device init
+        (atorch/meta_init.py); None: by module type (normal(0, 0.02) for
+        Linear / Embedding, ones for norms)."""
+        if name.endswith("o_proj.weight") or name.endswith("down_proj.weight"):
+            return ("normal", 0.0, 0.02 / math.sqrt(2 * self.cfg.num_hidden_layers))
+        return None
+
     @staticmethod
     def _init(m):
         if isinstance(m, nn.Linear) or type(m).__name__ in ("ColumnParallelLinear", "RowParallelLinear"):
