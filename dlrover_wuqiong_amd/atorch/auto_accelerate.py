@@ -286,14 +286,12 @@ def _fix_attention_heads(model: nn.Module, tp: int):
             m.hidden_size = m.hidden_size // tp
 
 
-def _apply_tensor_parallel(ctx, cfg):
-    from torch.distributed.device_mesh import DeviceMesh
+def _dtensor_tp(model, mesh, tp: int, cfg=None) -> int:
+    """Shard ``model``'s Megatron blocks over ``mesh`` with DTensor
+    (colwise -> rowwise: one all-reduce per block each way); returns the
+    number of Linear layers sharded."""
     from torch.distributed.tensor.parallel import parallelize_module
 
-    _g, ranks = adist.parallel_group_and_ranks("tensor")
-    if not ranks or len(ranks) == 1:
-        return
-    mesh = DeviceMesh("cuda" if torch.cuda.is_available() else "cpu", ranks, mesh_dim_names=("tensor",))
     plan = (cfg or {}).get("plan") if isinstance(cfg, dict) else None
     heads = {}
     if plan is None and not (isinstance(cfg, dict) and cfg.get("planner") == "names"):
@@ -301,16 +299,70 @@ def _apply_tensor_parallel(ctx, cfg):
         # the layers are called; the name table only as a fallback
         from .tp_planner import auto_tp_plan
 
-        plan = auto_tp_plan(ctx["model"], heads) or None
-    plan = plan or _tp_plan_for(ctx["model"])
-    parallelize_module(ctx["model"], mesh, plan)
+        plan = auto_tp_plan(model, heads) or None
+    plan = plan or _tp_plan_for(model)
+    parallelize_module(model, mesh, plan)
     if heads:
         from .tp_planner import shrink_head_attributes
 
-        shrink_head_attributes(ctx["model"], heads, len(ranks))
-    _fix_attention_heads(ctx["model"], len(ranks))
+        shrink_head_attributes(model, heads, tp)
+    _fix_attention_heads(model, tp)
+    return len(plan)
+
+
+def _megatron_tp(model, group, tp: int, cfg=None) -> int:
+    """Swap ``model``'s Megatron blocks (found structurally by the fx
+    planner, else by layer names) for this package's Column / Row parallel
+    Linears over ``group``: blocking autograd collectives on the tensor
+    group (RCCL over xGMI), deterministic on gloo too.  Returns the number
+    of Linear layers swapped."""
+    from torch.distributed.tensor.parallel import ColwiseParallel
+
+    from ..parallel.tensor_parallel import ColumnParallelLinear, RowParallelLinear
+
+    plan = (cfg or {}).get("plan") if isinstance(cfg, dict) else None
+    heads = {}
+    if plan is None:
+        from .tp_planner import auto_tp_plan
+
+        plan = dict(auto_tp_plan(model, heads) or {})
+        # blocks the tracer could not prove (e.g. HF attention with control
+        # flow): the name table, for parents with no structural entry that
+        # hold both a column and a row Linear of it
+        by_parent = {}
+        for name, style in _tp_plan_for(model).items():
+            by_parent.setdefault(name.rsplit(".", 1)[0] if "." in name else "", {})[name] = style
+        for parent, entries in by_parent.items():
+            if any(k.startswith(parent + ".") or (not parent) for k in plan if k.rsplit(".", 1)[0] == parent):
+                continue
+            kinds = {isinstance(v, ColwiseParallel) for v in entries.values()}
+            if kinds == {True, False}:
+                plan.update(entries)
+    plan = plan or _tp_plan_for(model)
+    for name, style in plan.items():
+        lin = model.get_submodule(name)
+        parent = model.get_submodule(name.rsplit(".", 1)[0]) if "." in name else model
+        col = isinstance(style, ColwiseParallel) or style == "colwise"
+        new = (ColumnParallelLinear if col else RowParallelLinear).from_linear(lin, group)
+        setattr(parent, name.rsplit(".", 1)[-1], new)
+    if heads:
+        from .tp_planner import shrink_head_attributes
+
+        shrink_head_attributes(model, heads, tp)
+    _fix_attention_heads(model, tp)
+    return len(plan)
+
+
+def _apply_tensor_parallel(ctx, cfg):
+    from torch.distributed.device_mesh import DeviceMesh
+
+    _g, ranks = adist.parallel_group_and_ranks("tensor")
+    if not ranks or len(ranks) == 1:
+        return
+    mesh = DeviceMesh("cuda" if torch.cuda.is_available() else "cpu", ranks, mesh_dim_names=("tensor",))
+    n = _dtensor_tp(ctx["model"], mesh, len(ranks), cfg)
     ctx["tp_mesh"] = mesh
-    logger.info(f"tensor_parallel: {len(plan)} linear layers sharded over {len(ranks)} ranks")
+    logger.info(f"tensor_parallel: {n} linear layers sharded over {len(ranks)} ranks")
 
 
 def _apply_sequence_parallel(ctx, cfg):
@@ -486,15 +538,23 @@ def _apply_mixed_parallel(ctx, cfg):
         adist.create_parallel_group(([("tensor", t), ("pipeline", p), ("data", d)], None))
     model = ctx["model"]
     if t > 1:
-        if not isinstance(model, Llama):
-            raise TypeError(f"mixed_parallel tensor sharding supports Llama models, got {type(model).__name__}")
-        tg = adist.parallel_group("tensor")
-        tr = adist.parallel_rank("tensor")
-        dtype = next(model.parameters()).dtype
-        full = {k: v.detach() for k, v in model.state_dict().items()}
-        tp_model = Llama(model.cfg, tp_group=tg).to(dtype)
-        tp_model.load_state_dict(shard_llama_state_dict(full, model.cfg, tr, t))
-        model = tp_model
+        tg, tranks = adist.parallel_group_and_ranks("tensor")
+        if isinstance(model, Llama):
+            # this package's Llama: Megatron TP layers (fused QKV / gate|up
+            # regrouped per rank, vocab-parallel embedding + head + CE)
+            tr = adist.parallel_rank("tensor")
+            dtype = next(model.parameters()).dtype
+            full = {k: v.detach() for k, v in model.state_dict().items()}
+            tp_model = Llama(model.cfg, tp_group=tg).to(dtype)
+            tp_model.load_state_dict(shard_llama_state_dict(full, model.cfg, tr, t))
+            model = tp_model
+        else:
+            # any other model: the structural (torch.fx) Megatron plan,
+            # realised with this package's Column / Row parallel Linears on
+            # the existing tensor group (no new communicators)
+            n = _megatron_tp(model, tg, t, cfg.get("tp_cfg"))
+            if n == 0:
+                raise ValueError(f"mixed_parallel: no tensor-parallel block found in {type(model).__name__}")
     if p > 1:
         group, ranks = adist.parallel_group_and_ranks("pipeline")
         me = dist.get_rank()
@@ -503,9 +563,10 @@ def _apply_mixed_parallel(ctx, cfg):
             eg = dist.new_group(sorted({rk[0], rk[-1]}))
             if me in rk:
                 emb_group = eg
+        split_kw = {k: cfg[k] for k in ("loss_fn", "boundary_shape") if k in cfg}
         model = PipelineModule(model, p, ranks.index(me), num_microbatches=cfg.get("chunks", p),
                                schedule=cfg.get("schedule", "1f1b"), virtual_stages=cfg.get("virtual_stages", 1),
-                               group=group, embedding_group=emb_group)
+                               group=group, embedding_group=emb_group, **split_kw)
         model.amp_dtype = ctx.get("amp_dtype")
         model.batch_fn = cfg.get("batch_fn")
         ctx["pipeline"] = True

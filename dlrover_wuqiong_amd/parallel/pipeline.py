@@ -225,12 +225,188 @@ class LlamaStage(PipelineStage):
         return cross_entropy(logits, targets, inplace_grad=True)
 
 
+class DecoderParts:
+    """The pieces of a generic decoder-only LM (any transformers causal LM --
+    Llama, Qwen2, Mistral, GPT-NeoX, GPT-2, Phi ... -- or a user model of
+    the same shape), found structurally rather than by class:
+
+    * ``layers``: the longest ``nn.ModuleList`` of same-class blocks that
+      hold parameters (the decoder layers); its parent is the backbone;
+    * ``embed``: the backbone's token ``nn.Embedding`` (vocabulary-sized, or
+      the first Embedding registered before the layers); ``pos_embed``: a
+      second Embedding before the layers (learned positions, GPT-2);
+      ``drop``: a Dropout registered before the layers;
+    * ``norm``: the first module registered after the layers;
+    * ``rotary``: a backbone child whose class name mentions "Rotary"
+      (``forward(x, position_ids) -> (cos, sin)``);
+    * ``head``: the top-level ``nn.Linear`` producing vocabulary logits
+      (tied when its weight IS the embedding's)."""
+
+    def __init__(self, model: nn.Module):
+        lists = [(n, m) for n, m in model.named_modules() if isinstance(m, nn.ModuleList) and len(m) > 0
+                 and len({type(x) for x in m}) == 1 and any(True for _ in m[0].parameters())]
+        if not lists:
+            raise TypeError(f"no decoder layer stack found in {type(model).__name__}")
+        lname, layers = max(lists, key=lambda x: len(x[1]))
+        self.layers = layers
+        bname = lname.rsplit(".", 1)[0] if "." in lname else ""
+        self.backbone = model.get_submodule(bname) if bname else model
+        self.config = getattr(model, "config", None) or getattr(self.backbone, "config", None)
+        kids = list(self.backbone.named_children())
+        li = next(i for i, (_n, m) in enumerate(kids) if m is layers)
+        before, after = kids[:li], kids[li + 1:]
+        vocab = getattr(self.config, "vocab_size", None)
+        embs = [m for _n, m in before if isinstance(m, nn.Embedding)]
+        if not embs:
+            raise TypeError(f"{type(model).__name__}: no token embedding before the decoder layers")
+        tok = [m for m in embs if vocab is not None and m.num_embeddings == vocab]
+        self.embed = tok[0] if tok else embs[0]
+        others = [m for m in embs if m is not self.embed]
+        self.pos_embed = others[0] if others else None
+        drops = [m for _n, m in before if isinstance(m, nn.Dropout)]
+        self.drop = drops[0] if drops else None
+        norms = [m for _n, m in after if "rotary" not in type(m).__name__.lower()]
+        self.norm = norms[0] if norms else None
+        rot = [m for _n, m in kids if "rotary" in type(m).__name__.lower()]
+        self.rotary = rot[0] if rot else None
+        heads = [m for _n, m in model.named_children() if isinstance(m, nn.Linear)
+                 and (vocab is None or m.out_features == vocab)]
+        if not heads:
+            raise TypeError(f"{type(model).__name__}: no LM head (Linear to the vocabulary) at the top level")
+        self.head = heads[0]
+        self.tied = self.head.weight is self.embed.weight
+        self.hidden = self.embed.embedding_dim
+        self.vocab = self.head.out_features
+        if self.config is not None and getattr(self.config, "_attn_implementation", None) == "eager":
+            # eager attention needs an explicit causal mask; sdpa / flash
+            # take attention_mask=None as causal
+            self.config._attn_implementation = "sdpa"
+
+
+class DecoderStackStage(PipelineStage):
+    """A contiguous range of decoder layers of any :class:`DecoderParts`
+    model.  One tensor crosses each boundary: the hidden states."""
+
+    def __init__(self, parts: DecoderParts, start: int, end: int, is_first: bool, is_last: bool):
+        super().__init__()
+        self.parts_cfg = parts.config
+        self.hidden = parts.hidden
+        self.is_first, self.is_last = is_first, is_last
+        self.start, self.end = start, end
+        self.layers = nn.ModuleList(list(parts.layers[start:end]))
+        self.rotary = parts.rotary
+        self.tied = parts.tied
+        if is_first:
+            self.embed = parts.embed
+            self.pos_embed = parts.pos_embed
+            self.drop = parts.drop
+        if is_last:
+            self.norm = parts.norm
+            if parts.tied and not is_first:
+                self.head_weight = nn.Parameter(parts.embed.weight.detach().clone())
+            elif not parts.tied:
+                self.head = parts.head
+
+    def tied_parameters(self):
+        if not self.tied or (self.is_first and self.is_last):
+            return []
+        if self.is_first:
+            return [self.embed.weight]
+        if self.is_last:
+            return [self.head_weight]
+        return []
+
+    def act_meta(self, micro_batch: int, seq: int):
+        dt = next(p.dtype for p in self.parameters() if p.is_floating_point())
+        return [(dt, (micro_batch, seq, self.hidden))]
+
+    def _masks(self, x, pos):
+        cfg = self.parts_cfg
+        try:
+            from transformers.masking_utils import create_causal_mask, create_sliding_window_causal_mask
+        except Exception:
+            return {"full_attention": None}
+        kw = dict(config=cfg, inputs_embeds=x, attention_mask=None, past_key_values=None, position_ids=pos)
+        out = {"full_attention": create_causal_mask(**kw)}
+        if "sliding_attention" in (getattr(cfg, "layer_types", None) or []):
+            out["sliding_attention"] = create_sliding_window_causal_mask(**kw)
+        return out
+
+    def forward(self, *acts, targets=None):
+        import torch.nn.functional as F
+
+        from ..ops.cross_entropy import cross_entropy
+
+        if self.is_first:
+            ids = acts[0]
+            x = self.embed(ids)
+            if self.pos_embed is not None:
+                x = x + self.pos_embed(torch.arange(ids.shape[1], device=ids.device))[None]
+            if self.drop is not None:
+                x = self.drop(x)
+        else:
+            x = acts[0]
+        pos = torch.arange(x.shape[1], device=x.device)[None]
+        masks = self._masks(x, pos) if self.parts_cfg is not None else {"full_attention": None}
+        kw = {"position_ids": pos}
+        if self.rotary is not None:
+            kw["position_embeddings"] = self.rotary(x, pos)
+        types = getattr(self.parts_cfg, "layer_types", None)
+        for i, layer in enumerate(self.layers):
+            t = types[self.start + i] if types else "full_attention"
+            out = layer(x, attention_mask=masks.get(t), **kw)
+            x = out[0] if isinstance(out, (tuple, list)) else out
+        if not self.is_last:
+            return (x,)
+        if self.norm is not None:
+            x = self.norm(x)
+        if self.tied:
+            logits = F.linear(x, self.embed.weight if self.is_first else self.head_weight)
+        else:
+            logits = self.head(x)
+        if hasattr(logits, "to_local"):  # a DTensor-parallel head
+            logits = logits.full_tensor()
+        if targets is None:
+            return logits
+        return cross_entropy(logits, targets, inplace_grad=True)
+
+
+class SequentialStage(PipelineStage):
+    """A contiguous range of an ``nn.Sequential`` (one tensor between
+    children); the last stage applies ``loss_fn(output, targets)``."""
+
+    def __init__(self, seq: nn.Sequential, start: int, end: int, is_first: bool, is_last: bool, loss_fn=None,
+                 boundary_shape=None):
+        super().__init__()
+        self.body = nn.Sequential(*list(seq)[start:end])
+        self.is_first, self.is_last = is_first, is_last
+        self.loss_fn = loss_fn
+        self.boundary_shape = boundary_shape  # fn(micro_batch, seq) -> (dtype, shape)
+
+    def act_meta(self, micro_batch: int, seq: int):
+        if self.boundary_shape is None:
+            raise ValueError("SequentialStage needs boundary_shape(micro_batch, seq) -> (dtype, shape)")
+        return [self.boundary_shape(micro_batch, seq)]
+
+    def forward(self, *acts, targets=None):
+        y = self.body(acts[0])
+        if not self.is_last:
+            return (y,)
+        if targets is None or self.loss_fn is None:
+            return y
+        return self.loss_fn(y, targets)
+
+
 def split_model(model: nn.Module, num_stages: int, stage: int, bounds: Optional[List[Tuple[int, int]]] = None,
-                virtual_chunk: Optional[Tuple[int, int]] = None) -> PipelineStage:
-    """Cut a GPT2 / Llama model at decoder-layer boundaries and return the
-    piece for pipeline ``stage``.  With ``virtual_chunk=(chunk, v)`` the
-    layers are cut into ``num_stages * v`` pieces and piece
-    ``chunk * num_stages + stage`` is returned (interleaved schedule)."""
+                virtual_chunk: Optional[Tuple[int, int]] = None, **kw) -> PipelineStage:
+    """Cut a model at decoder-layer boundaries and return the piece for
+    pipeline ``stage``: this package's GPT-2 / Llama, any decoder-only LM
+    whose layer stack :class:`DecoderParts` finds (transformers Qwen2,
+    Mistral, GPT-NeoX, GPT-2, Llama ...), or an ``nn.Sequential`` (cut
+    between children; pass ``loss_fn`` and ``boundary_shape``).  With
+    ``virtual_chunk=(chunk, v)`` the layers are cut into ``num_stages * v``
+    pieces and piece ``chunk * num_stages + stage`` is returned
+    (interleaved schedule)."""
     from ..models.gpt2 import GPT2
     from ..models.llama import Llama
 
@@ -240,8 +416,20 @@ def split_model(model: nn.Module, num_stages: int, stage: int, bounds: Optional[
     elif isinstance(model, Llama):
         n, cls = model.cfg.num_hidden_layers, LlamaStage
         vocab, hidden = model.cfg.vocab_size, model.cfg.hidden_size
+    elif isinstance(model, nn.Sequential):
+        chunks, piece = num_stages, stage
+        if virtual_chunk is not None:
+            c, v = virtual_chunk
+            chunks, piece = num_stages * v, c * num_stages + stage
+        a, b = (bounds or partition_layers(len(model), chunks))[piece]
+        return SequentialStage(model, a, b, is_first=(piece == 0), is_last=(piece == chunks - 1),
+                               loss_fn=kw.get("loss_fn"), boundary_shape=kw.get("boundary_shape"))
     else:
-        raise TypeError(f"no pipeline splitter for {type(model).__name__}")
+        parts = DecoderParts(model)
+        n, vocab, hidden = len(parts.layers), parts.vocab, parts.hidden
+
+        def cls(_m, a, b, is_first, is_last):
+            return DecoderStackStage(parts, a, b, is_first, is_last)
     chunks, piece = num_stages, stage
     if virtual_chunk is not None:
         c, v = virtual_chunk
@@ -571,11 +759,11 @@ def _as_tuple(x) -> Tensors:
 
 
 def build_pipeline(model: nn.Module, num_stages: int, stage: int, virtual_stages: int = 1,
-                   bounds: Optional[List[Tuple[int, int]]] = None) -> Union[PipelineStage, List[PipelineStage]]:
+                   bounds: Optional[List[Tuple[int, int]]] = None, **kw) -> Union[PipelineStage, List[PipelineStage]]:
     """This rank's stage (or its ``virtual_stages`` interleaved chunks)."""
     if virtual_stages == 1:
-        return split_model(model, num_stages, stage, bounds)
-    return [split_model(model, num_stages, stage, bounds, virtual_chunk=(c, virtual_stages))
+        return split_model(model, num_stages, stage, bounds, **kw)
+    return [split_model(model, num_stages, stage, bounds, virtual_chunk=(c, virtual_stages), **kw)
             for c in range(virtual_stages)]
 
 
@@ -586,9 +774,9 @@ class PipelineModule(nn.Module):
 
     def __init__(self, model: nn.Module, num_stages: int, stage: int, num_microbatches: int,
                  schedule: str = "1f1b", virtual_stages: int = 1, group=None, embedding_group=None,
-                 bounds: Optional[List[Tuple[int, int]]] = None):
+                 bounds: Optional[List[Tuple[int, int]]] = None, **split_kw):
         super().__init__()
-        chunks = build_pipeline(model, num_stages, stage, virtual_stages, bounds)
+        chunks = build_pipeline(model, num_stages, stage, virtual_stages, bounds, **split_kw)
         self.chunks = nn.ModuleList(chunks if isinstance(chunks, list) else [chunks])
         self.num_stages, self.stage = num_stages, stage
         self.num_microbatches = num_microbatches
@@ -649,7 +837,9 @@ class PipelineModule(nn.Module):
         from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
 
         n = dist.get_world_size(self.dp_group)
-        grads = [p.grad for p in self.parameters() if p.grad is not None]
+        # DTensor (tensor-parallel) parameters: their local gradient shards
+        grads = [p.grad.to_local() if hasattr(p.grad, "to_local") else p.grad
+                 for p in self.parameters() if p.grad is not None]
         bucket, size = [], 0
         for g in grads + [None]:
             if g is not None:
@@ -669,5 +859,5 @@ class PipelineModule(nn.Module):
         return self.chunks[0](ids, targets=targets)
 
 
-__all__ = ["partition_layers", "PipelineStage", "GPT2Stage", "LlamaStage", "split_model", "build_pipeline",
-           "PipelineSchedule", "PipelineModule"]
+__all__ = ["partition_layers", "PipelineStage", "GPT2Stage", "LlamaStage", "DecoderParts", "DecoderStackStage",
+           "SequentialStage", "split_model", "build_pipeline", "PipelineSchedule", "PipelineModule"]
