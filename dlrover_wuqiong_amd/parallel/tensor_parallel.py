@@ -23,6 +23,7 @@ and ``mappings.py`` (copy / reduce / scatter / gather regions), Megatron
 ``core/tensor_parallel``.
 """
 
+import os
 from typing import Optional
 
 import torch
@@ -197,6 +198,82 @@ def scatter_to_sequence_parallel_region(x, group=None):
     return _ScatterToSequenceRegion.apply(x, group)
 
 
+class _ColumnLinearOverlap(torch.autograd.Function):
+    """Column-parallel Linear with its communication overlapped with GEMMs
+    (ATorch ``LinearWithGradAccumulationAndAsyncCommunication``,
+    ``modules/distributed_modules/layers.py:90-158``; Megatron's
+    ``async_tensor_model_parallel_allreduce``).
+
+    Forward, sequence parallel: the all-gather of the sequence shards is
+    issued async and this rank's own rows are multiplied while the other
+    ranks' rows are in flight; the rest follows once they landed.
+    Backward: dX = dY W is computed first and its all-reduce (or, with SP,
+    reduce-scatter) is issued async; the weight-gradient GEMM dW = dY^T X
+    (plus db) runs underneath it -- on MI355X the RCCL kernel on its own
+    stream shares the CUs with the hipBLASLt GEMM instead of serialising.
+    With SP the input is re-gathered in backward (only the local shard is
+    saved: 1/tp of the activation memory), that gather overlapping dX."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, group, sp):
+        ctx.group, ctx.sp, ctx.has_bias = group, sp, bias is not None
+        if sp:
+            n, r = _ws(group), _rk(group)
+            xc = x.contiguous()
+            full = torch.empty((n * xc.shape[0],) + tuple(xc.shape[1:]), dtype=xc.dtype, device=xc.device)
+            work = dist.all_gather_into_tensor(full, xc, group=group, async_op=True)
+            rows = xc.shape[0]
+            y_own = F.linear(xc, weight, bias)  # under the gather
+            work.wait()
+            y = torch.empty((full.shape[0],) + tuple(y_own.shape[1:]), dtype=y_own.dtype, device=y_own.device)
+            y[r * rows:(r + 1) * rows] = y_own
+            if r > 0:
+                y[:r * rows] = F.linear(full[:r * rows], weight, bias)
+            if r < n - 1:
+                y[(r + 1) * rows:] = F.linear(full[(r + 1) * rows:], weight, bias)
+            ctx.save_for_backward(xc, weight)
+            return y
+        ctx.save_for_backward(x, weight)
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight = ctx.saved_tensors
+        group, sp = ctx.group, ctx.sp
+        g = g.contiguous()
+        gather = None
+        if sp:
+            n = _ws(group)
+            total = torch.empty((n * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+            gather = dist.all_gather_into_tensor(total, x, group=group, async_op=True)
+        else:
+            total = x
+        # (under autocast the forward GEMMs ran in g's dtype: so do these)
+        dx = g.matmul(weight.to(g.dtype))
+        if gather is not None:
+            gather.wait()
+        if sp:
+            out = torch.empty((dx.shape[0] // _ws(group),) + tuple(dx.shape[1:]), dtype=dx.dtype, device=dx.device)
+            red = dist.reduce_scatter_tensor(out, dx.contiguous(), group=group, async_op=True)
+        else:
+            out = dx
+            red = dist.all_reduce(dx, group=group, async_op=True)
+        g2 = g.reshape(-1, g.shape[-1])
+        dw = g2.t().matmul(total.reshape(-1, total.shape[-1]).to(g2.dtype))  # under the collective
+        db = g2.sum(0) if ctx.has_bias else None
+        red.wait()
+        return (out.to(x.dtype), dw.to(weight.dtype), (db.to(weight.dtype) if db is not None else None), None,
+                None)
+
+
+def column_parallel_linear(x, weight, bias, group, sequence_parallel=False):
+    """Y = X W^T (+ b) for a column shard W, communication overlapped with
+    the GEMMs (see :class:`_ColumnLinearOverlap`)."""
+    if _ws(group) == 1:
+        return F.linear(x, weight, bias)
+    return _ColumnLinearOverlap.apply(x, weight, bias, group, sequence_parallel)
+
+
 def _default_tp_group():
     from . import state
 
@@ -220,6 +297,8 @@ class ColumnParallelLinear(nn.Module):
         self.gather_output = gather_output
         self.sequence_parallel = sequence_parallel
         self.skip_bias_add = skip_bias_add
+        # comm / GEMM overlap (DWAMD_TP_OVERLAP=0: the plain blocking mappings)
+        self.overlap_comm = os.environ.get("DWAMD_TP_OVERLAP", "1") == "1"
         self.weight = nn.Parameter(torch.empty(self.out_per_rank, in_features, dtype=dtype, device=device))
         self.bias = nn.Parameter(torch.zeros(self.out_per_rank, dtype=dtype, device=device)) if bias else None
         init_method(self.weight)
@@ -238,12 +317,15 @@ class ColumnParallelLinear(nn.Module):
         return m
 
     def forward(self, x):
-        if self.sequence_parallel:
-            x = gather_from_sequence_parallel_region(x, self.group)
-        else:
-            x = copy_to_tensor_parallel_region(x, self.group)
         bias = None if self.skip_bias_add else self.bias
-        y = F.linear(x, self.weight, bias)
+        if self.overlap_comm and torch.is_grad_enabled():
+            y = column_parallel_linear(x, self.weight, bias, self.group, self.sequence_parallel)
+        else:
+            if self.sequence_parallel:
+                x = gather_from_sequence_parallel_region(x, self.group)
+            else:
+                x = copy_to_tensor_parallel_region(x, self.group)
+            y = F.linear(x, self.weight, bias)
         if self.gather_output:
             y = gather_from_tensor_parallel_region(y, self.group)
         return (y, self.bias) if self.skip_bias_add else y

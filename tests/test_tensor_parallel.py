@@ -104,3 +104,88 @@ def test_tensor_and_sequence_parallel_two_ranks():
     for p in ps:
         p.join(timeout=30)
     assert res == [(0, True), (1, True)], res
+
+
+def _overlap_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    try:
+        from dlrover_wuqiong_amd.parallel import tensor_parallel as tp
+
+        dist.init_process_group("gloo")
+        group = dist.group.WORLD
+        torch.manual_seed(1)
+        fc = nn.Linear(16, 32)
+        x = torch.randn(8, 4, 16)
+        out = {}
+        for sp in (False, True):
+            grads = []
+            for overlap in (False, True):
+                c = tp.ColumnParallelLinear.from_linear(fc, group, sequence_parallel=sp)
+                c.overlap_comm = overlap
+                xi = (x.chunk(world, 0)[rank] if sp else x).clone().requires_grad_(True)
+                y = c(xi)
+                y.square().sum().backward()
+                grads.append((y.detach(), xi.grad, c.weight.grad, c.bias.grad))
+            out[sp] = all(torch.allclose(a, b, atol=1e-5) for a, b in zip(*grads))
+        # order of events in the overlapped backward: the input-gradient
+        # collective is issued BEFORE the weight-gradient GEMM and waited after
+        log = []
+
+        real_ar = dist.all_reduce
+
+        def ar(t, *a, **k):
+            log.append("all_reduce_async" if k.get("async_op") else "all_reduce")
+            w = real_ar(t, *a, **k)
+            if k.get("async_op"):
+                class W:
+                    def wait(self_):
+                        log.append("wait")
+                        return w.wait()
+                return W()
+            return w
+
+        real_mm = torch.Tensor.matmul
+
+        def mm(self_, other):
+            log.append("matmul")
+            return real_mm(self_, other)
+
+        c = tp.ColumnParallelLinear.from_linear(fc, group)
+        y = c(x.clone().requires_grad_(True))
+        dist.all_reduce, torch.Tensor.matmul = ar, mm
+        try:
+            y.square().sum().backward()
+        finally:
+            dist.all_reduce, torch.Tensor.matmul = real_ar, real_mm
+        q.put((rank, (out[False], out[True], log)))
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        traceback.print_exc()
+        q.put((rank, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_column_parallel_comm_overlap_two_ranks():
+    """The overlapped column-parallel Linear (ATorch
+    LinearWithGradAccumulationAndAsyncCommunication) gives the gradients of
+    the blocking form, with and without sequence parallelism, and issues
+    the dX all-reduce before the dW GEMM, waiting only after it."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_overlap_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in ps)
+    for p in ps:
+        p.join(timeout=30)
+    for _r, out in res:
+        assert isinstance(out, tuple), res
+        tp_ok, sp_ok, log = out
+        assert tp_ok and sp_ok, out
+        i = log.index("all_reduce_async")
+        assert "matmul" in log[i + 1:log.index("wait")], log
