@@ -340,10 +340,84 @@ class FsdpCheckpointEngine(ShardCheckpointEngine):
             ok = check_all_rank_ready(self._ctl_group, ok)
         if not ok:
             return 0
-        dist_cp.load(state_dict, storage_reader=dist_cp.FileSystemReader(path),
-                     process_group=self._ctl_group if dist.is_initialized() else None)
+        t0 = time.perf_counter()
+        plan = self._fast_storage_plan(state_dict, path) if os.environ.get("DWAMD_FAST_STORAGE_LOAD", "1") == "1" \
+            else None
+        fast = plan is not None
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            fast = check_all_rank_ready(self._ctl_group, fast)  # all ranks take the same path
+        if fast:
+            self._run_fast_storage_plan(state_dict, plan)
+            self.last_restore_source = "storage"
+        else:
+            dist_cp.load(state_dict, storage_reader=dist_cp.FileSystemReader(path),
+                         process_group=self._ctl_group if dist.is_initialized() else None)
+            self.last_restore_source = "storage(dcp)"
+        self.last_storage_load_stats = dict(getattr(self, "_fast_stats", {}) if fast else {},
+                                            sec=round(time.perf_counter() - t0, 4), fast=fast)
         base = os.path.basename(os.path.normpath(path))
         return int(base) if base.isdigit() else -1
+
+    def _fast_storage_plan(self, state_dict, path):
+        """Same DCP layout as this rank's current shards (same world size and
+        sharding): map every local item to its byte range in the ``.distcp``
+        files -- None when any item is missing or differs (resharding: the
+        stock DCP reader handles it)."""
+        from torch.distributed.checkpoint.metadata import Metadata
+
+        from .storage_loader import TorchArchive, _pair, _regions
+
+        try:
+            with open(os.path.join(path, ".metadata"), "rb") as f:
+                md = restricted_loads(f.read())
+            if not isinstance(md, Metadata):
+                return None
+            lookup = {(k.fqn, tuple(k.offset) if k.offset is not None else None): v
+                      for k, v in md.storage_data.items()}
+            planner, _plan, payload = self._payload(state_dict)
+            views = payload.pop("_views", {})
+            by_file: Dict[str, list] = {}
+            byte_items = []
+            for n, (fqn, off, _idx, _typ, _p) in enumerate(payload["index"]):
+                info = lookup.get((fqn, tuple(off) if off is not None else None))
+                if info is None:
+                    return None
+                fpath = os.path.join(path, info.relative_path)
+                v = payload["items"][str(n)]
+                if isinstance(v, (bytes, bytearray)):
+                    byte_items.append((fqn, fpath, info.offset, info.length))
+                    continue
+                arc = TorchArchive(fpath, info.offset, info.length)
+                pairs = []
+                _pair(arc.tree, v, pairs)
+                regs, slow = _regions(pairs, arc)
+                if slow:
+                    return None
+                by_file.setdefault(fpath, []).extend(regs)
+            return planner, payload, views, by_file, byte_items
+        except (OSError, KeyError, ValueError, EOFError, pickle.UnpicklingError) as e:
+            logger.info(f"fast DCP restore not applicable ({type(e).__name__}: {e}); using dist_cp.load")
+            return None
+
+    def _run_fast_storage_plan(self, state_dict, plan):
+        """Parallel O_DIRECT reads of this rank's ``.distcp`` ranges straight
+        into the live shards (pinned bounce buffers, pipelined H2D)."""
+        from torch.distributed.checkpoint._traverse import set_element
+
+        from .storage_loader import _Reader, stream_regions_into
+
+        planner, payload, views, by_file, byte_items = plan
+        direct = os.environ.get("DWAMD_STORAGE_DIRECT", "1") == "1"
+        nb = 0
+        for fpath, regs in by_file.items():
+            nb += stream_regions_into(_Reader(fpath, direct, False, 16), os.path.getsize(fpath), regs)
+        for fqn, fpath, off, length in byte_items:
+            with open(fpath, "rb") as f:
+                f.seek(off)
+                obj = safe_torch_load(io.BytesIO(f.read(length)))
+            set_element(state_dict, planner.mappings[fqn], obj)
+        restore_views(payload, views)
+        self._fast_stats = {"bytes_read": nb, "files": len(by_file)}
 
 
 # ------------------------------------------------------------ checkpointers

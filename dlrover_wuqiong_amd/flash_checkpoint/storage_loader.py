@@ -113,20 +113,53 @@ class _LazyUnpickler(RestrictedUnpickler):
         return _LazyStorage(str(key), dtype, int(numel) * esz)
 
 
+class _Window(io.RawIOBase):
+    """Read-only view of bytes [start, start + length) of an open file."""
+
+    def __init__(self, f, start: int, length: int):
+        self.f, self.start, self.length, self.pos = f, start, length, 0
+
+    def readable(self):
+        return True
+
+    def seekable(self):
+        return True
+
+    def tell(self):
+        return self.pos
+
+    def seek(self, off, whence=0):
+        self.pos = off if whence == 0 else (self.pos + off if whence == 1 else self.length + off)
+        return self.pos
+
+    def readinto(self, b):
+        n = max(0, min(len(b), self.length - self.pos))
+        self.f.seek(self.start + self.pos)
+        got = self.f.readinto(memoryview(b)[:n])
+        self.pos += got
+        return got
+
+
 class TorchArchive:
     """Directory of a ``torch.save`` zip archive: the lazy object tree and the
     absolute file offset of every storage record."""
 
-    def __init__(self, path: str):
+    def __init__(self, path: str, start: int = 0, length: Optional[int] = None):
+        """``start`` / ``length``: an archive embedded in a larger file (a DCP
+        ``.distcp`` file is a sequence of ``torch.save`` blobs); offsets
+        stay absolute file offsets."""
         self.path = str(path)
         self.file_size = os.path.getsize(self.path)
-        with open(self.path, "rb") as f, zipfile.ZipFile(f) as z:
+        self.start = start
+        with open(self.path, "rb") as f0, zipfile.ZipFile(
+                _Window(f0, start, (self.file_size - start) if length is None else length)) as z:
+            f = _Window(f0, start, (self.file_size - start) if length is None else length)
             infos = z.infolist()
             pkl = next(i for i in infos if i.filename.endswith("/data.pkl") or i.filename == "data.pkl")
             self.prefix = pkl.filename[: -len("data.pkl")]
             # records are stored uncompressed; read them by offset (archives
             # written by fast_torch_save carry no CRC, which zipfile rejects)
-            f.seek(self._data_offset(f, pkl))
+            f.seek(self._data_offset(f, pkl) - start)
             self.tree = _LazyUnpickler(io.BytesIO(f.read(pkl.compress_size))).load()
             self.data_off: Dict[str, int] = {}
             dprefix = self.prefix + "data/"
@@ -142,7 +175,7 @@ class TorchArchive:
         if hdr[:4] != b"PK\x03\x04":
             raise ValueError(f"{self.path}: bad local header for {info.filename}")
         n, m = struct.unpack("<HH", hdr[26:30])
-        return info.header_offset + 30 + n + m
+        return self.start + info.header_offset + 30 + n + m
 
     def file_range(self, t: LazyTensor) -> Tuple[int, int]:
         esz = torch.empty(0, dtype=t.dtype).element_size()
@@ -303,15 +336,52 @@ def load_archive_into(path: str, target: Any = None, chunk_bytes: int = 256 << 2
             gathers.append((dst[:body], per))
         else:
             mine.append((lo, n, dst))
+    stream_regions_into(reader, arc.file_size, mine, chunk_bytes, extra_cuda=any(t.is_cuda for _l, t in slow))
+    for lz, t in slow:  # non-contiguous views: read the storage range, copy with strides
+        lo = arc.data_off[lz.storage.key]
+        alo = lo // _ALIGN * _ALIGN
+        n = min(arc.file_size, lo + lz.storage.nbytes + _ALIGN) - alo
+        raw, pad = _aligned_host(n + _ALIGN, False)
+        reader.read(raw.data_ptr() + pad, n, alo)
+        buf = raw[pad + (lo - alo): pad + (lo - alo) + lz.storage.nbytes].view(lz.dtype)
+        src = buf.as_strided(lz.size, lz.stride, buf.storage_offset() + lz.offset)
+        with torch.no_grad():
+            t.copy_(src)
+    if gathers:
+        import torch.distributed as dist
+
+        t_g = time.perf_counter()
+        from .gather import all_gather_slices
+
+        for full, per in gathers:
+            a0 = slice_idx * per
+            stats_t = all_gather_slices(full, full[a0: a0 + per], gather_group)
+            if stats is not None:
+                stats["gather_transport"] = stats_t
+        torch.cuda.current_stream(gathers[0][0].device).synchronize()
+        if stats is not None:
+            stats["gather_s"] = round(time.perf_counter() - t_g, 4)
+            stats["gather_bytes"] = sum(f.numel() for f, _ in gathers)
+    _fill_stats(stats, arc, reader, t0, t_parse, time.perf_counter())
+    return result
+
+
+def stream_regions_into(reader: "_Reader", file_size: int, regions, chunk_bytes: int = 256 << 20,
+                        extra_cuda: bool = False) -> int:
+    """Read file ranges straight into destination tensors: ``regions`` =
+    [(file_off, nbytes, dst uint8 tensor)].  Spans of nearby ranges are read
+    with the native parallel O_DIRECT reader into two pinned bounce buffers;
+    while span k+1 is read, span k's H2D DMA runs on a side stream (ordered
+    after the caller's stream).  Returns the bytes read."""
     pieces = []
-    for lo, n, dst in mine:
+    for lo, n, dst in regions:
         o = 0
         while o < n:  # split so every piece fits one bounce buffer
             c = min(chunk_bytes, n - o)
             pieces.append((lo + o, c, dst[o: o + c]))
             o += c
     pieces.sort(key=lambda p: p[0])
-    cuda = any(p[2].is_cuda for p in pieces) or any(t.is_cuda for _l, t in slow)
+    cuda = any(p[2].is_cuda for p in pieces) or extra_cuda
     dev = next((p[2].device for p in pieces if p[2].is_cuda), None)
     stream = torch.cuda.Stream(dev) if cuda and dev is not None else None
     if stream is not None:
@@ -335,7 +405,7 @@ def load_archive_into(path: str, target: Any = None, chunk_bytes: int = 256 << 2
                 break
             j += 1
             span_hi = max(span_hi, end)
-        read_hi = min(arc.file_size, (span_hi + _ALIGN - 1) // _ALIGN * _ALIGN)
+        read_hi = min(file_size, (span_hi + _ALIGN - 1) // _ALIGN * _ALIGN)
         raw, pad = bufs[bi]
         if events[bi] is not None:
             events[bi].synchronize()  # its previous span's DMA has drained
@@ -357,37 +427,9 @@ def load_archive_into(path: str, target: Any = None, chunk_bytes: int = 256 << 2
         nb += read_hi - span_lo
         i = j + 1
         bi ^= 1
-    for lz, t in slow:  # non-contiguous views: read the storage range, copy with strides
-        esz = torch.empty(0, dtype=lz.dtype).element_size()
-        lo = arc.data_off[lz.storage.key]
-        alo = lo // _ALIGN * _ALIGN
-        n = min(arc.file_size, lo + lz.storage.nbytes + _ALIGN) - alo
-        raw, pad = _aligned_host(n + _ALIGN, False)
-        reader.read(raw.data_ptr() + pad, n, alo)
-        buf = raw[pad + (lo - alo): pad + (lo - alo) + lz.storage.nbytes].view(lz.dtype)
-        src = buf.as_strided(lz.size, lz.stride, buf.storage_offset() + lz.offset)
-        with torch.no_grad():
-            t.copy_(src)
-        del esz
     if stream is not None:
         stream.synchronize()
-    if gathers:
-        import torch.distributed as dist
-
-        t_g = time.perf_counter()
-        from .gather import all_gather_slices
-
-        for full, per in gathers:
-            a0 = slice_idx * per
-            stats_t = all_gather_slices(full, full[a0: a0 + per], gather_group)
-            if stats is not None:
-                stats["gather_transport"] = stats_t
-        torch.cuda.current_stream(gathers[0][0].device).synchronize()
-        if stats is not None:
-            stats["gather_s"] = round(time.perf_counter() - t_g, 4)
-            stats["gather_bytes"] = sum(f.numel() for f, _ in gathers)
-    _fill_stats(stats, arc, reader, t0, t_parse, time.perf_counter())
-    return result
+    return nb
 
 
 def _collect_storages(tree, out: Dict[str, _LazyStorage]):

@@ -35,6 +35,8 @@ def main():
     p.add_argument("--torch-optim", action="store_true", help="keep torch.optim.AdamW (no multi-tensor HIP kernel)")
     p.add_argument("--no-ckpt", action="store_true", help="step time only (no flash checkpoints)")
     p.add_argument("--fp8", action="store_true", help="auto_accelerate 'fp8' on the decoder layers' projections")
+    p.add_argument("--storage", action="store_true",
+                   help="also persist and time the storage restore (fast O_DIRECT reader vs stock dist_cp.load)")
     a = p.parse_args()
     for k, v in dict(MASTER_ADDR="127.0.0.1", MASTER_PORT="29571", RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
                      LOCAL_WORLD_SIZE="1").items():
@@ -173,6 +175,42 @@ def main():
     verified = extra.get("step") == last + 1 and all(
         torch.equal(v.to_local(), want[k]) for k, v in model.state_dict().items())
     nbytes = ck.engine._shm_handler.payload_size if ck.engine._shm_handler.shared_memory else 0
+    storage = {}
+    if a.storage:
+        # node replaced: the persisted DCP checkpoint read back (page cache
+        # dropped) -- this framework's O_DIRECT range reader into the live
+        # shards vs torch's stock dist_cp.load (FileSystemReader)
+        import glob as _glob
+
+        from dlrover_wuqiong_amd.flash_checkpoint.fsdp import _set_model_optim_state, wait_for_persist
+        from dlrover_wuqiong_amd.flash_checkpoint.storage_loader import drop_file_cache
+
+        sstep = last + 2
+        ck.save_checkpoint(sstep, model, opt, storage_type=StorageType.DISK)
+        if rank == 0:
+            wait_for_persist(a.ckpt_dir, sstep, timeout=600)
+        dist.barrier()
+        want = {k: v.to_local().clone() for k, v in model.state_dict().items()}
+        path = os.path.join(a.ckpt_dir, str(sstep))
+        for mode in ("fast", "dcp"):
+            os.environ["DWAMD_FAST_STORAGE_LOAD"] = "1" if mode == "fast" else "0"
+            with torch.no_grad():
+                for v in model.state_dict().values():
+                    v.to_local().zero_()
+            for f in _glob.glob(os.path.join(path, "*.distcp")):
+                drop_file_cache(f)
+            sync()
+            t0 = time.perf_counter()
+            sd = ck._state(model, opt, None)
+            got = ck.engine._load_from_storage_dcp(sd, path)
+            _set_model_optim_state(model, opt, sd.pop("model"), sd.pop("optim", None), full=False)
+            sync()
+            sec = time.perf_counter() - t0
+            ok = got == sstep and all(torch.equal(v.to_local(), want[k]) for k, v in model.state_dict().items())
+            storage[mode] = {"sec": round(sec, 3), "verified": bool(ok),
+                             "source": ck.engine.last_restore_source,
+                             "stats": ck.engine.last_storage_load_stats}
+        os.environ["DWAMD_FAST_STORAGE_LOAD"] = "1"
     if rank == 0:
         print(json.dumps({
             "metric": "fsdp flash ckpt pause s", "unit": "s",
@@ -189,6 +227,9 @@ def main():
             "flush_gbps": round(sum(n for n, _ in ck.engine._copier.flush_stats) / max(1e-9, sum(
                 t for _, t in ck.engine._copier.flush_stats)) / 1e9, 1) if getattr(ck.engine, "_copier", None) else None,
             "load_sec": round(load_s, 3), "load_verified": bool(verified), "ckpt_bytes_per_rank": nbytes,
+            "load_sec_storage": storage.get("fast", {}).get("sec"),
+            "load_sec_storage_stock_dcp": storage.get("dcp", {}).get("sec"), "storage_restores": storage,
+            "reference_fsdp_gpt2_1.5b_ssd_read_s": 18.0,
             "train_step_ms": round(1000 * sorted(steps)[len(steps) // 2], 1),
             "tokens_per_s": round(world * a.micro_batch * a.seq / sorted(steps)[len(steps) // 2], 1),
             "losses": [round(x, 3) for x in losses]}))

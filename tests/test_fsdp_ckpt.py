@@ -87,6 +87,12 @@ def _fsdp_worker(rank, world, port, root, q):
         sd2 = ck._state(model, opt, {"epoch": 0})
         step = ck.engine._load_from_storage_dcp(sd2)
         ok = ok and step == 5 and sd2["epoch"] == 8
+        # same world size and sharding: the fast reader (O_DIRECT ranges of
+        # the .distcp files straight into the live shards), not dist_cp.load
+        ok = ok and ck.engine.last_restore_source == "storage"
+        ok = ok and ck.engine.last_storage_load_stats.get("fast") is True
+        got5 = _local(model)
+        ok = ok and all(torch.equal(got5[k], want5[k]) for k in want5)
         ck.close()
         q.put((rank, bool(ok)))
     except Exception as e:  # pragma: no cover - surfaced through the queue
