@@ -496,6 +496,8 @@ def _mixed_cfg(cfg) -> Dict[str, Any]:
     micro-batch count)."""
     if cfg is None:
         return {}
+    if isinstance(cfg, str):
+        return {"auto": True} if cfg == "auto" else {}
     out = dict(cfg) if isinstance(cfg, dict) else {k: v for k, v in vars(cfg).items() if not k.startswith("_")}
     ds = out.get("ds_config")
     if isinstance(ds, str) and os.path.exists(ds):
@@ -806,6 +808,24 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
     if included:
         have = set(strategy.names())
         strategy = Strategy.from_spec(strategy.opts + [(n, None) for n in included if n not in have])
+    if world > 1 and "mixed_parallel" in strategy.names():
+        mcfg = _mixed_cfg(strategy.config("mixed_parallel"))
+        if mcfg.get("auto") or not (mcfg.get("tensor") or mcfg.get("pipeline")):
+            # automatic tensor x pipeline x data sizing (atorch/shard_planner.py)
+            from .shard_planner import Hardware, plan_3d
+
+            plans = plan_3d(model, world, seq=int(mcfg.get("seq_len", 4096)),
+                            micro_batch=int(mcfg.get("micro_batch", 1)), global_batch=mcfg.get("global_batch"),
+                            hw=Hardware(gpus_per_node=int(mcfg.get("gpus_per_node", min(8, world)))),
+                            act_ckpt=bool(mcfg.get("act_ckpt", False)))
+            best = next((x for x in plans if x.feasible), plans[0])
+            mcfg = dict(mcfg, **best.as_strategy_cfg())
+            mcfg.pop("auto", None)
+            logger.info(f"mixed_parallel auto plan: tensor {best.tensor} x pipeline {best.pipeline} x data "
+                        f"{best.data} ({best.chunks} micro-batches), ~{best.mem_gb} GB / GPU, est. "
+                        f"{best.step_s:.3f} s / step; runner-up "
+                        f"{[(x.tensor, x.pipeline, x.data) for x in plans[1:3]]}")
+            strategy = Strategy.from_spec([(n, mcfg if n == "mixed_parallel" else c) for n, c in strategy.opts])
     if world > 1 and "mixed_parallel" in strategy.names() and "parallel_mode" not in strategy.names():
         mcfg = _mixed_cfg(strategy.config("mixed_parallel"))
         t, p = int(mcfg.get("tensor", 1)), int(mcfg.get("pipeline", 1))
