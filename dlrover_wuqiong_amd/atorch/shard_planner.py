@@ -54,6 +54,7 @@ class Hardware:
     xgmi_busbw_gbs: float = 300.0
     nic_gbs: float = 50.0  # per GPU, across nodes (400 Gb/s)
     reserve_gb: float = 24.0  # staging buffers / allocator slack
+    coll_latency_us: float = 20.0  # fixed cost of one RCCL call (launch + sync)
 
 
 @dataclass
@@ -129,9 +130,9 @@ def estimate(shape: ModelShape, t: int, p: int, d: int, seq: int, micro_batch: i
     # parameters of the heaviest stage (the first holds the embedding, the last the head)
     stage_params = (shape.layer_params * (L / p) + shape.vocab * H * (2 if p == 1 else 1)) / t
     state = stage_params * 16
-    # activations per layer per micro-batch (bf16): ~34 H + 5 heads*seq bytes per token (Megatron
-    # estimate, attention scores recomputed by the flash kernel: drop the 5 a s term); TP shards
-    # the MLP / attention intermediates
+    # activations per layer per micro-batch (bf16 bytes per token): 10 H + 24 H / t (Megatron's
+    # 34 H + 5 a s with TP sharding the attention / MLP intermediates; the flash kernel recomputes
+    # the scores, so no 5 a s term)
     per_layer = tokens_mb * H * (10 + 24 / t) if not act_ckpt else tokens_mb * H * 2
     in_flight = min(p, m)
     acts = per_layer * (L / p) * in_flight
@@ -141,14 +142,16 @@ def estimate(shape: ModelShape, t: int, p: int, d: int, seq: int, micro_batch: i
     flops = (8 if act_ckpt else 6) * shape.params * seq * global_batch
     compute = flops / (world * hw.bf16_tflops * 1e12 * hw.efficiency)
     # TP: 4 all-reduces per layer per micro-batch on xGMI (ring over t GPUs)
-    tp = _ring_allreduce_s(tokens_mb * H * 2, t, hw.xgmi_busbw_gbs) * 4 * (L / p) * m
+    lat = hw.coll_latency_us * 1e-6
+    tp = (_ring_allreduce_s(tokens_mb * H * 2, t, hw.xgmi_busbw_gbs) + lat) * 4 * (L / p) * m if t > 1 else 0.0
     bubble = compute * (p - 1) / (m + p - 1) if p > 1 else 0.0
     # PP boundary: activation + gradient per micro-batch; one neighbour link (xGMI in-node, NIC across)
     pp_bw = hw.xgmi_link_gbs if t * p <= hw.gpus_per_node else hw.nic_gbs
-    pp = (2 * m * tokens_mb * H * 2 / (pp_bw * GB)) if p > 1 else 0.0
+    pp = 2 * m * (tokens_mb * H * 2 / (pp_bw * GB) + lat) if p > 1 else 0.0
     # DP: gradient all-reduce of the stage's parameters (bf16), half hidden under the backward
     dp_bw = hw.xgmi_busbw_gbs if world <= hw.gpus_per_node else hw.nic_gbs
-    dp = 0.5 * _ring_allreduce_s(stage_params * 2, d, dp_bw)
+    buckets = max(1.0, stage_params * 2 / (256 << 20))
+    dp = 0.5 * _ring_allreduce_s(stage_params * 2, d, dp_bw) + (buckets * lat if d > 1 else 0.0)
     step = compute + tp + bubble + pp + dp
     return Plan(tensor=t, pipeline=p, data=d, chunks=m, mem_gb=round(mem, 2), step_s=step, feasible=feasible,
                 parts={"compute": compute, "tp": tp, "bubble": bubble, "pp": pp, "dp": dp,
