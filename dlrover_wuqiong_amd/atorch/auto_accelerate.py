@@ -810,7 +810,8 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
         strategy = Strategy.from_spec(strategy.opts + [(n, None) for n in included if n not in have])
     if world > 1 and "mixed_parallel" in strategy.names():
         mcfg = _mixed_cfg(strategy.config("mixed_parallel"))
-        if mcfg.get("auto") or not (mcfg.get("tensor") or mcfg.get("pipeline")):
+        sized_elsewhere = "parallel_mode" in strategy.names() or adist.parallel_config() is not None
+        if mcfg.get("auto") or not (mcfg.get("tensor") or mcfg.get("pipeline") or sized_elsewhere):
             # automatic tensor x pipeline x data sizing (atorch/shard_planner.py)
             from .shard_planner import Hardware, plan_3d
 
