@@ -27,6 +27,11 @@
 #include "attn_common.h"
 
 #include <cstdlib>
+#include <type_traits>
+
+#ifndef DWAMD_DQ_RI
+#define DWAMD_DQ_RI 1  // A/B: -DDWAMD_DQ_RI=0 builds the previous dQ form
+#endif
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -477,12 +482,20 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
   const bf16_t* Kb = K + (int64_t)b * st.k_bs + (int64_t)sr.k_off * st.k_rs + (int64_t)hk * D;
   const bf16_t* Vb = V + (int64_t)b * st.v_bs + (int64_t)sr.k_off * st.v_rs + (int64_t)hk * D;
 
+  // Row constants as the accumulators' INITIAL VALUES (RI, dense masks):
+  // Q is prescaled by softmax_scale * log2(e) so S^T leaves the MFMA in the
+  // exp2 domain, and the first MFMA of each chain takes a loop-invariant C
+  // operand holding -lse2 (resp. -delta) -- a lane's 16 registers all belong
+  // to its query -- so P = exp2(S'), dS = P * dP' cost one exp and one mul
+  // per element instead of fma + exp + sub + mul.
+  constexpr bool RI = DWAMD_DQ_RI && !EXT;
   // Q and dO fragments (B operands): lane holds row q, d = 16 kk + 8 hh .. +7
   u32x4 qf[C::KK], dof[C::KK];
 #pragma unroll
   for (int kk = 0; kk < C::KK; ++kk) {
     if (q < SQ) {
       qf[kk] = *(const u32x4*)(Qb + (int64_t)q * st.q_rs + 16 * kk + 8 * hh);
+      if (RI) qf[kk] = scaled8(qf[kk], scale_log2);
       dof[kk] = *(const u32x4*)(dOb + (int64_t)q * st.do_rs + 16 * kk + 8 * hh);
     } else {
       qf[kk] = (u32x4){0, 0, 0, 0};
@@ -499,7 +512,13 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
   for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[dt][i] = 0.f;
-  constexpr bool DPI = D == 64 && !EXT;  // dP^T initialised with -delta
+  constexpr bool DPI = D == 64 && !EXT && !RI;  // dP^T initialised with -delta
+  f32x16 s_init, dp_init;  // RI: the loop-invariant C operands
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    s_init[i] = -lse2;
+    dp_init[i] = -dl;
+  }
 
   int n_tiles = (SK + C::BK - 1) / C::BK;
   int t_begin = 0;
@@ -570,35 +589,52 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
     if (active) {
       const bool need_mask = (k0 + C::BK > SK) || (CAUSAL && (k0 + C::BK - 1 > q0 + co));
       const int lim = CAUSAL ? min(SK, q + co + 1) : SK;  // keys < lim are visible to this lane's query
+      // The tile body is instantiated twice -- with and without the mask --
+      // so an interior tile (most of them) is ONE basic block over both
+      // subtiles and the scheduler can overlap subtile 1's S / dP MFMAs with
+      // subtile 0's softmax (a runtime mask branch split them).
+      // (D=64 only: at D=128 the overlap needs ~200 more VGPRs than the 256 of
+      // two waves per SIMD and spills; there the mask stays a runtime branch.)
+      constexpr bool SPLIT = D == 64;
+      auto tile = [&](auto mask_c) {
+        constexpr bool MASK = decltype(mask_c)::value;
       // one 32-key subtile at a time keeps S^T / dP^T at 32 registers
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb) {
         // dP^T starts at -delta (row constant as the initial accumulator) at
         // D=64; at D=128 that form cost this kernel 40+ spilled VGPRs
         f32x16 s, dp;
+        if (!RI) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          s[i] = 0.f;
-          dp[i] = DPI ? -dl : 0.f;
+          for (int i = 0; i < 16; ++i) {
+            s[i] = 0.f;
+            dp[i] = DPI ? -dl : 0.f;
+          }
         }
 #pragma unroll
         for (int kk = 0; kk < C::KK; ++kk) {
           const u32x4 kf = *(const u32x4*)(kl + rwl[kk & 1] + row_const<D>(32 * sb, kk));
           const u32x4 vf = *(const u32x4*)(vl + rwl[kk & 1] + row_const<D>(32 * sb, kk));
-          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(kf), as_bf(qf[kk]), s, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(vf), as_bf(dof[kk]), dp, 0, 0, 0);
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(kf), as_bf(qf[kk]), (RI && kk == 0) ? s_init : s, 0,
+                                                      0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(vf), as_bf(dof[kk]), (RI && kk == 0) ? dp_init : dp,
+                                                       0, 0, 0);
         }
         if (!EXT) {
-          if (need_mask) {
-            __asm__ volatile("");  // a scalar branch: diagonal / ragged tiles only
+          if (MASK || (!SPLIT && need_mask)) {  // diagonal / ragged tiles only
+            if (!SPLIT) __asm__ volatile("");  // keep the runtime test a scalar branch
             const int rel = lim - k0 - 32 * sb - 4 * hh;  // register i's key offset must be < rel
 #pragma unroll
             for (int i = 0; i < 16; ++i) s[i] = ((i & 3) + 8 * (i >> 2)) < rel ? s[i] : -INFINITY;  // p = 0
           }
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], scale_log2, -lse2));
-            s[i] = p * (DPI ? dp[i] : dp[i] - dl);  // dS^T (scale applied in the epilogue)
+            if (RI) {
+              s[i] = __builtin_amdgcn_exp2f(s[i]) * dp[i];  // dS^T (scale applied in the epilogue)
+            } else {
+              const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], scale_log2, -lse2));
+              s[i] = p * (DPI ? dp[i] : dp[i] - dl);
+            }
           }
         }
 #pragma unroll
@@ -627,6 +663,11 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
           }
         }
       }
+      };
+      if (SPLIT && (need_mask || EXT))
+        tile(std::true_type{});
+      else
+        tile(std::false_type{});
     }
     if (tt + 1 < n_run) {
       write_lds((tt + 1) & 1);
