@@ -116,6 +116,12 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   // lane-half's partial row sum.
   constexpr float RESCALE_T = 8.f;
   float m_i = 0.f, l_i = 0.f;
+  // -m_i in all 16 registers: the loop-invariant C operand of each S chain's
+  // first MFMA (a lane's registers all belong to its query), rewritten only
+  // when m_i moves -- instead of 16 v_mov per subtile per tile
+  f32x16 minit;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) minit[i] = 0.f;
   bool seeded = false;  // the row's offset was set from its first visible scores
 
   int n_tiles = (SK + C::BK - 1) / C::BK;
@@ -194,10 +200,12 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
       // -m_i (row constant as the initial accumulator), so p = exp2(S') needs
       // no subtraction
       f32x16 s[C::NSB];
+      if (EXT) {  // (the EXT instances keep the explicit init: minit would spill them)
 #pragma unroll
-      for (int sb = 0; sb < C::NSB; ++sb)
+        for (int sb = 0; sb < C::NSB; ++sb)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) s[sb][i] = -m_i;
+          for (int i = 0; i < 16; ++i) s[sb][i] = -m_i;
+      }
       // the two subtiles' chains interleaved: no MFMA waits on its predecessor
       if constexpr (D == 64 && C::NSB == 2) {
         // all 8 K fragments (32 VGPRs) in flight at once: one LDS latency per
@@ -212,7 +220,8 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
         for (int kk = 0; kk < C::KK; ++kk)
 #pragma unroll
           for (int sb = 0; sb < C::NSB; ++sb)
-            s[sb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf[kk][sb]), as_bf16x8(qf[kk]), s[sb], 0, 0, 0);
+            s[sb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf[kk][sb]), as_bf16x8(qf[kk]),
+                                                            (kk == 0 && !EXT) ? minit : s[sb], 0, 0, 0);
         // the machine scheduler would sink each read next to its MFMA
         __builtin_amdgcn_sched_group_barrier(0x100, 2 * C::KK, 0);  // DS reads
         __builtin_amdgcn_sched_group_barrier(0x008, 2 * C::KK, 0);  // then the MFMAs
@@ -222,7 +231,8 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
 #pragma unroll
           for (int sb = 0; sb < C::NSB; ++sb) {
             const u32x4 kf = *(const u32x4*)(kl + kro[kk & 1] + row_const<D>(32 * sb, kk));
-            s[sb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf), as_bf16x8(qf[kk]), s[sb], 0, 0, 0);
+            s[sb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf), as_bf16x8(qf[kk]),
+                                                            (kk == 0 && !EXT) ? minit : s[sb], 0, 0, 0);
           }
       }
 
@@ -272,6 +282,10 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
         // a long distance) where exp2(-d) overflows and 0 * inf would be NaN
         const float alpha = fresh ? 1.f : __builtin_amdgcn_exp2f(-d);
         m_i += d;
+        if (!EXT) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) minit[i] = -m_i;
+        }
         l_i *= alpha;
 #pragma unroll
         for (int dt = 0; dt < C::DT; ++dt)
