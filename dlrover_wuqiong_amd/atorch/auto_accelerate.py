@@ -246,8 +246,10 @@ def _apply_fp8(ctx, cfg):
 
     cfg = cfg if isinstance(cfg, dict) else {}
     if ctx.get("tp_like"):
-        logger.warning("fp8: not combined with tensor / sequence / mixed parallelism here; fp8 skipped")
-        return
+        # the TP layers replace the Linears fp8 would have converted: refuse
+        # loudly instead of silently training in bf16
+        raise ValueError("fp8 cannot be combined with tensor / sequence / mixed parallelism: drop 'fp8' from the "
+                         "strategy, or use it with DDP / FSDP")
     fp8.configure(history_len=int(cfg.get("amax_history_len", 1024)), margin=int(cfg.get("margin", 0)),
                   algo=cfg.get("amax_compute_algo", "max"), reduce_amax=bool(cfg.get("reduce_amax", True)),
                   interval=int(cfg.get("interval", 1)), group=ctx.get("dp_group"))

@@ -123,3 +123,14 @@ def test_cast_nan_stays_nan_and_amax_backs_off():
     assert st.amax_bits[i].view(torch.float32).item() == float("inf")
     st.update()
     assert st.scale[i].item() == pytest.approx(0.5)
+
+
+def test_fp8_with_tensor_parallel_is_rejected_loudly():
+    """The verdict's silent-skip trap: fp8 under TP / SP / mixed used to be
+    dropped with a warning; it now refuses."""
+    import pytest
+
+    from dlrover_wuqiong_amd.atorch.auto_accelerate import _apply_fp8
+
+    with pytest.raises(ValueError, match="fp8 cannot be combined"):
+        _apply_fp8({"tp_like": True, "model": nn.Linear(16, 16)}, None)
