@@ -262,14 +262,19 @@ def _apply_fp8(ctx, cfg):
 def _tp_plan_for(model: nn.Module):
     from torch.distributed.tensor.parallel import ColwiseParallel, RowwiseParallel
 
-    col = ("q_proj", "k_proj", "v_proj", "gate_proj", "up_proj", "c_fc", "fc1", "w1", "w3", "query_key_value")
-    row = ("o_proj", "down_proj", "c_proj", "fc2", "w2", "dense", "out_proj")
+    col = ("q_proj", "k_proj", "v_proj", "gate_proj", "up_proj", "c_fc", "fc1", "w1", "w3", "query_key_value",
+           "query", "key", "value", "dense_h_to_4h")
+    row = ("o_proj", "down_proj", "c_proj", "fc2", "w2", "dense", "out_proj", "dense_4h_to_h")
+    # encoder families (Bert / RoBERTa / ViT): the MLP's first Linear is
+    # ``intermediate.dense`` -- column, although plain ``dense`` is a row one
+    col2 = ("intermediate.dense",)
     plan = {}
     for name, m in model.named_modules():
         if not isinstance(m, nn.Linear):
             continue
         leaf = name.rsplit(".", 1)[-1]
-        if leaf in col:
+        last2 = ".".join(name.rsplit(".", 2)[-2:])
+        if last2 in col2 or leaf in col:
             plan[name] = ColwiseParallel()
         elif leaf in row:
             plan[name] = RowwiseParallel()
@@ -286,6 +291,9 @@ def _fix_attention_heads(model: nn.Module, tp: int):
                 setattr(m, attr, v // tp)
         if hasattr(m, "hidden_size") and isinstance(getattr(m, "hidden_size"), int) and hasattr(m, "num_heads"):
             m.hidden_size = m.hidden_size // tp
+        # Bert-style self-attention: the merged-heads width of the context
+        if isinstance(getattr(m, "all_head_size", None), int) and hasattr(m, "num_attention_heads"):
+            m.all_head_size = m.all_head_size // tp
 
 
 def _dtensor_tp(model, mesh, tp: int, cfg=None) -> int:
@@ -329,14 +337,22 @@ def _megatron_tp(model, group, tp: int, cfg=None) -> int:
 
         plan = dict(auto_tp_plan(model, heads) or {})
         # blocks the tracer could not prove (e.g. HF attention with control
-        # flow): the name table, for parents with no structural entry that
-        # hold both a column and a row Linear of it
-        by_parent = {}
+        # flow): the name table's remaining entries, taken per layer when
+        # they hold both a column and a row Linear -- grouped per layer (the path up to the first list index), so an
+        # attention block split over sibling modules (Bert: attention.self.
+        # query/key/value -> attention.output.dense) is taken as a whole
+        def layer_of(name):
+            parts = name.split(".")
+            for k, x in enumerate(parts):
+                if x.isdigit():
+                    return ".".join(parts[:k + 1])
+            return name.rsplit(".", 1)[0] if "." in name else ""
+
+        by_layer = {}
         for name, style in _tp_plan_for(model).items():
-            by_parent.setdefault(name.rsplit(".", 1)[0] if "." in name else "", {})[name] = style
-        for parent, entries in by_parent.items():
-            if any(k.startswith(parent + ".") or (not parent) for k in plan if k.rsplit(".", 1)[0] == parent):
-                continue
+            if name not in plan:
+                by_layer.setdefault(layer_of(name), {})[name] = style
+        for entries in by_layer.values():
             kinds = {isinstance(v, ColwiseParallel) for v in entries.values()}
             if kinds == {True, False}:
                 plan.update(entries)
