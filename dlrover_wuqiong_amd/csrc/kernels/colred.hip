@@ -345,6 +345,156 @@ __global__ void __launch_bounds__(256) norm_bwd_fused_kernel(
   if (threadIdx.x == 0) __hip_atomic_exchange(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Norm backward for SMALL H (<= 2048, VPL <= 4), one pass over dy / x:
+// every wave takes RPW rows (all their loads issued before any math, so a
+// wave has 2 rows of HBM latency in flight), writes dx like norm_dx_kernel,
+// and keeps per-lane dgamma / dbeta sums; the block's 4 waves combine them
+// in LDS and store ONE fp32 partial row [2H] per block -- plain stores, no
+// atomics (the atomic-combined fused kernel above, 512 blocks of 4-row
+// waves, was latency-bound at H = 1600: 2048 waves for 8192 rows).  The
+// [blocks, 2H] partials are summed by colsum_f32_kernel.
+template <int VPL, bool RMS, int RPW>
+__global__ void __launch_bounds__(256) norm_bwd_part_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ gamma,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const bf16_t* __restrict__ dres,
+    bf16_t* __restrict__ dx, float* __restrict__ part, int64_t rows, int H) {
+  static_assert(VPL <= 4, "small-H norm backward");
+  __shared__ float red[2][4][512 + 4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nv = H >> 3;
+  const int64_t row0 = ((int64_t)blockIdx.x * 4 + wid) * RPW;
+  float ag[VPL][8], ab[VPL][8];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ag[j][k] = ab[j][k] = 0.f;
+  u32x4 xv[RPW][VPL], dv[RPW][VPL], gv[VPL];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nv) gv[j] = *(const u32x4*)(gamma + c * 8);
+  }
+#pragma unroll
+  for (int u = 0; u < RPW; ++u)
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nv && row0 + u < rows) {
+        xv[u][j] = *(const u32x4*)(x + (row0 + u) * H + c * 8);
+        dv[u][j] = *(const u32x4*)(dy + (row0 + u) * H + c * 8);
+      }
+    }
+#pragma unroll
+  for (int u = 0; u < RPW; ++u) {
+    const int64_t row = row0 + u;
+    if (row >= rows) break;  // wave-uniform
+    const float mu = RMS ? 0.f : mean_in[row];
+    const float rstd = rstd_in[row];
+    float xh[VPL][8], g[VPL][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nv) {
+        float xf[8], df[8], gm[8];
+        unpack8(xv[u][j], xf);
+        unpack8(dv[u][j], df);
+        unpack8(gv[j], gm);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float a = (xf[k] - mu) * rstd, b = df[k] * gm[k];
+          xh[j][k] = a;
+          g[j][k] = b;
+          ag[j][k] += df[k] * a;
+          if constexpr (!RMS) ab[j][k] += df[k];
+          s1 += b;
+          s2 += b * a;
+        }
+      }
+    }
+    const float m1 = RMS ? 0.f : wave_sum(s1) / (float)H;
+    const float m2 = wave_sum(s2) / (float)H;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nv) {
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = rstd * (g[j][k] - m1 - xh[j][k] * m2);
+        if (dres) {
+          float r[8];
+          unpack8(*(const u32x4*)(dres + row * H + c * 8), r);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] += r[k];
+        }
+        *(u32x4*)(dx + row * H + c * 8) = pack8(o);
+      }
+    }
+  }
+  float* prow = part + (int64_t)blockIdx.x * 2 * H;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[0][wid][lane * 8 + k] = ag[j][k];
+      if constexpr (!RMS) red[1][wid][lane * 8 + k] = ab[j][k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int cl = threadIdx.x + 256 * h;
+      const int c = 512 * j + cl;
+      if (c < H) {
+        prow[c] = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+        if constexpr (!RMS) prow[H + c] = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Column sums of fp32 partials [R, 2H] into out0 (columns 0..H-1) and out1
+// (H..2H-1, may be null): thread = column, grid.y splits the rows; one
+// atomic per (column, row-split) into ws, the last row-split block of each
+// 256-column strip converts (+ accumulates) and clears -- colred_kernel's
+// completion protocol.  ws: fp32 [2H + ceil(2H/256)], zero on entry and exit.
+__global__ void __launch_bounds__(256) colsum_f32_kernel(const float* __restrict__ part, int R, int H2,
+                                                         int rows_per_blk, float* __restrict__ ws,
+                                                         void* __restrict__ out0, void* __restrict__ out1,
+                                                         int is_fp32, int accumulate) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int r0 = blockIdx.y * rows_per_blk, r1 = min(R, r0 + rows_per_blk);
+  if (c < H2) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int r = r0;
+    for (; r + 4 <= r1; r += 4) {
+      a0 += part[(int64_t)r * H2 + c];
+      a1 += part[(int64_t)(r + 1) * H2 + c];
+      a2 += part[(int64_t)(r + 2) * H2 + c];
+      a3 += part[(int64_t)(r + 3) * H2 + c];
+    }
+    for (; r < r1; ++r) a0 += part[(int64_t)r * H2 + c];
+    atomicAdd(ws + c, (a0 + a1) + (a2 + a3));
+  }
+  __shared__ int is_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  unsigned* cnt = (unsigned*)(ws + H2) + blockIdx.x;
+  if (threadIdx.x == 0)
+    is_last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.y - 1;
+  __syncthreads();
+  if (!is_last) return;
+  if (c < H2) {
+    const float v = __hip_atomic_exchange(ws + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int H = H2 / 2;
+    if (c < H)
+      colred_store(out0, c, v, is_fp32, accumulate);
+    else
+      colred_store(out1, c - H, v, is_fp32, accumulate);
+  }
+  if (threadIdx.x == 0) __hip_atomic_exchange(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 static int colred_rows_per_blk(int64_t rows, int C, int dflt_blocks) {
   // Grid-size target per kernel flavour (DWAMD_COLRED_BLOCKS overrides all,
   // for A/B).  Fewer row blocks = fewer same-address atomics per column; the
@@ -457,6 +607,42 @@ extern "C" int dw_norm_bwd2(const void* dy, const void* x, const void* gamma, co
     hipLaunchKernelGGL(colred_kernel<1>, cg, dim3(256), 0, s, (const bf16_t*)dy, (const bf16_t*)x,
                        (const float*)mean, (const float*)rstd, (float*)ws, rows, H, per, dgamma, dbeta, out_fp32,
                        accumulate);
+  DW_LAUNCH_RET;
+}
+
+// Norm backward v3: v2, plus the small-H one-pass path (H < 2048) when the
+// caller provides fp32 scratch ``part`` of at least part_floats =
+// ceil(rows / 8) * 2H floats (any content).  ws as v2 but sized
+// 2H + ceil(2H / 256) + ceil(H / 512) floats.
+extern "C" int dw_norm_bwd3(const void* dy, const void* x, const void* gamma, const void* mean, const void* rstd,
+                            const void* dres, void* dx, void* dgamma, void* dbeta, void* ws, void* part,
+                            int64_t part_floats, int64_t rows, int H, int rms, int out_fp32, int accumulate,
+                            void* stream) {
+  constexpr int RPW = 2;
+  const int64_t nb = (rows + 4 * RPW - 1) / (4 * RPW);
+  static const bool off = getenv_flag("DWAMD_NORM_BWD_PART_OFF");  // A/B switch
+  if (off || !part || !(dgamma || dbeta) || H % 8 != 0 || H >= 2048 || nb * 2 * H > part_floats)
+    return dw_norm_bwd2(dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, ws, rows, H, rms, out_fp32, accumulate,
+                        stream);
+  hipStream_t s = (hipStream_t)stream;
+  DISPATCH_VPL2(H, {
+    if constexpr (VPL <= 4) {
+      if (rms)
+        hipLaunchKernelGGL((norm_bwd_part_kernel<VPL, true, RPW>), dim3((unsigned)nb), dim3(256), 0, s,
+                           (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)gamma, nullptr, (const float*)rstd,
+                           (const bf16_t*)dres, (bf16_t*)dx, (float*)part, rows, H);
+      else
+        hipLaunchKernelGGL((norm_bwd_part_kernel<VPL, false, RPW>), dim3((unsigned)nb), dim3(256), 0, s,
+                           (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)gamma, (const float*)mean,
+                           (const float*)rstd, (const bf16_t*)dres, (bf16_t*)dx, (float*)part, rows, H);
+    }
+  });
+  const int H2 = 2 * H;
+  const int splits = (int)std::max<int64_t>(1, std::min<int64_t>(64, nb / 16));
+  const int per = (int)((nb + splits - 1) / splits);
+  dim3 g((H2 + 255) / 256, (unsigned)((nb + per - 1) / per));
+  hipLaunchKernelGGL(colsum_f32_kernel, g, dim3(256), 0, s, (const float*)part, (int)nb, H2, per, (float*)ws,
+                     dgamma, rms ? nullptr : dbeta, out_fp32, accumulate);
   DW_LAUNCH_RET;
 }
 

@@ -26,7 +26,11 @@ def _norm_backward(ctx, dy, dres):
         dres = dres.contiguous().view(-1, H)
         if dres.dtype != torch.bfloat16:
             dres = dres.to(torch.bfloat16)
-    ws = _hip.zeroed_workspace(2 * H + (H + 511) // 512, x2.device)  # sums + strip counters
+    # sums + strip counters (of the 512-column fused path and of the small-H colsum)
+    ws = _hip.zeroed_workspace(2 * H + max((H + 511) // 512, (2 * H + 255) // 256), x2.device)
+    # small H: one-pass kernel writes per-block fp32 dgamma/dbeta partials here
+    nparts = (R + 7) // 8 * 2 * H if H < 2048 else 0
+    part = torch.empty(nparts, device=x2.device, dtype=torch.float32) if nparts else None
     dx = torch.empty_like(x2)
     wp, bp = ctx.weight_param, ctx.bias_param
     gd, bd = direct_grad(wp), direct_grad(bp) if ctx.has_bias else None
@@ -36,10 +40,11 @@ def _norm_backward(ctx, dy, dres):
     else:
         dgamma = torch.empty(H, device=x2.device, dtype=weight.dtype)
         dbeta = torch.empty(H, device=x2.device, dtype=weight.dtype) if ctx.has_bias else None
-    _hip.check(_hip.lib().dw_norm_bwd2(_hip.ptr(dy2), _hip.ptr(x2), _hip.ptr(weight), _hip.ptr(mean),
+    _hip.check(_hip.lib().dw_norm_bwd3(_hip.ptr(dy2), _hip.ptr(x2), _hip.ptr(weight), _hip.ptr(mean),
                                        _hip.ptr(rstd), _hip.ptr(dres), _hip.ptr(dx), _hip.ptr(dgamma),
-                                       _hip.ptr(dbeta), _hip.ptr(ws), R, H, int(ctx.rms),
-                                       int(dgamma.dtype == torch.float32), int(direct), _hip.stream()), "norm_bwd")
+                                       _hip.ptr(dbeta), _hip.ptr(ws), _hip.ptr(part), nparts, R, H,
+                                       int(ctx.rms), int(dgamma.dtype == torch.float32), int(direct),
+                                       _hip.stream()), "norm_bwd")
     if direct:
         notify(wp)
         notify(bp)

@@ -39,9 +39,29 @@ int probe(hipblasLtHandle_t h, hipblasLtEpilogue_t epi, bool aux, hipDataType bi
   return st == HIPBLAS_STATUS_SUCCESS ? found : -(int)st;
 }
 
-int main() {
+int main(int argc, char** argv) {
   hipblasLtHandle_t h;
   hipblasLtCreate(&h);
+  if (argc > 1) {
+    // bias-gradient epilogues on the WEIGHT-gradient GEMM of a Linear:
+    // dW^T[K_in, N_out] = X^T[K_in, M] . dY[M, N_out] (column-major view of
+    // row-major dW), db = sum_M dY = reduction of B over the GEMM's K
+    struct E { const char* n; hipblasLtEpilogue_t e; };
+    E es[] = {{"BGRADA", HIPBLASLT_EPILOGUE_BGRADA}, {"BGRADB", HIPBLASLT_EPILOGUE_BGRADB}};
+    int shapes[][3] = {{1600, 6400, 8192}, {6400, 1600, 8192}, {1600, 4800, 8192}, {1600, 1600, 8192},
+                       {4096, 4096, 4096}};
+    for (auto& e : es)
+      for (auto& sh : shapes)
+        for (int bt = 0; bt < 2; ++bt)
+          for (int ta = 0; ta < 2; ++ta)
+            for (int tb = 0; tb < 2; ++tb) {
+              int f = probe(h, e.e, false, bt ? HIP_R_32F : HIP_R_16BF, false, sh[0], sh[1], sh[2],
+                            ta ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb ? HIPBLAS_OP_T : HIPBLAS_OP_N);
+              printf("%-7s m=%d n=%d k=%d bias=%s transA=%d transB=%d -> %d\n", e.n, sh[0], sh[1], sh[2],
+                     bt ? "f32" : "bf16", ta, tb, f);
+            }
+    return 0;
+  }
   struct E { const char* n; hipblasLtEpilogue_t e; bool aux; };
   E es[] = {{"BIAS", HIPBLASLT_EPILOGUE_BIAS, false}, {"GELU", HIPBLASLT_EPILOGUE_GELU, false},
             {"GELU_BIAS", HIPBLASLT_EPILOGUE_GELU_BIAS, false}, {"GELU_AUX", HIPBLASLT_EPILOGUE_GELU_AUX, true},

@@ -25,7 +25,7 @@ def _need_gpu():
     kernels(required=True)
 
 
-@pytest.mark.parametrize("H,R", [(256, 777), (1600, 777), (4096, 777), (8192, 777), (1600, 9000)])
+@pytest.mark.parametrize("H,R", [(256, 777), (1000, 333), (1600, 777), (4096, 777), (8192, 777), (1600, 9000)])
 @pytest.mark.parametrize("rms", [False, True])
 def test_norm_fwd_bwd(H, R, rms):
     """H <= 4096: one-pass backward (dx + weight grads, row-striding waves,
