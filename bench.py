@@ -109,6 +109,8 @@ def parse(argv=None):
                         "HBM snapshot (the kill then always lands mid-flush: HBM-only restore)")
     p.add_argument("--rehearse-shared-device", action="store_true",
                    help="N ranks share cuda:0 over gloo: rehearses the N>1 fault path on one GPU")
+    p.add_argument("--no-step-overlap", action="store_true",
+                   help="run the optimizer update on the compute stream instead of under the next forward")
     # worker-only
     p.add_argument("--run-dir", default="", help=argparse.SUPPRESS)
     p.add_argument("--phase", default="deep", choices=["deep", "import", "import_hbm"], help=argparse.SUPPRESS)
@@ -183,7 +185,7 @@ def _job(a, n: int, mode: str, run_dir: str, tag: str):
              "--phase", phase]
     if a.inject_slow_flush > 0 and mode == "deep":
         wargs += ["--inject-slow-flush", str(a.inject_slow_flush)]
-    for flag in ("no_fault", "no_persist", "act_ckpt"):
+    for flag in ("no_fault", "no_persist", "act_ckpt", "no_step_overlap"):
         if getattr(a, flag):
             wargs.append("--" + flag.replace("_", "-"))
     cmd = [sys.executable, "-u", "-m", "dlrover_wuqiong_amd.trainer.run", "--nnodes", "1", "--nproc-per-node",
@@ -320,6 +322,7 @@ def summarize(a, run_dir, n, wall):
         "params": phase0["params"],
         "train_step_ms": round(1000 * step_sec, 2),
         "tokens_per_s": round(a.micro_batch * a.seq * phase0["world"] / step_sec, 1),
+        "optimizer_update": phase0.get("optimizer_update"),
         "loss": phase0["loss"],
         "rccl_world": phase0["world"],
         "backend": phase0.get("backend"),
@@ -491,6 +494,10 @@ def worker(a) -> int:
         torch.cuda.synchronize()
     marks["flat"] = time.time()
     opt = FusedAdamW(flat, lr=a.lr, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0)
+    if cuda and not a.no_step_overlap:
+        # the update runs under the next forward (optimizers/overlap.py); the
+        # timed region's closing device-wide synchronize includes all of it
+        opt.overlap_with_forward(model)
     B, S = a.micro_batch, a.seq
     if cuda:
         torch.cuda.synchronize()
@@ -585,6 +592,7 @@ def worker(a) -> int:
             os.kill(os.getpid(), signal.SIGKILL)
 
     def state_sums():
+        opt.join()
         third = opt.master if opt.master is not None else opt.exp_avg_sq
         return [float(flat.data.float().sum()), float(opt.exp_avg.sum()), float(third.sum())]
 
@@ -736,7 +744,8 @@ def worker(a) -> int:
               "ckpt_bytes": ckpt_bytes, "first_save_sec": first_save, "timed_saves": len(save_times),
               "timed_saves_ok": timed_ok, "skipped_saves_timed": skipped_timed, "rehearsal": rehearsal,
               "backend": backend, "slices": ckpt.engine._num_slices, "hbm_plan": getattr(ckpt.engine, "hbm_plan", None),
-              "gather": ckpt.engine._gather_group is not None})
+              "gather": ckpt.engine._gather_group is not None,
+              "optimizer_update": "under next forward" if opt._overlap is not None else "compute stream"})
 
         # ---------------- DISK persist (agent: torch.save archive written from
         # shm with parallel pwrite) while training continues: persist time and

@@ -270,6 +270,14 @@ def _covered(ranges: List[Tuple[int, int]], starts: List[int], a: int, n: int) -
     return i >= 0 and a + n <= ranges[i][1]
 
 
+def _pending_updates(device) -> list:
+    """Events of optimizer updates still running on a side stream
+    (``optimizers/overlap.py``): a snapshot must read after them."""
+    from ..optimizers.overlap import pending_events
+
+    return pending_events(device)
+
+
 def _install_fence_hook():
     global _FENCED, _OPTIMIZERS
     if _FENCED is None:
@@ -546,6 +554,12 @@ class GpuCopier:
                 self._snap_stream = torch.cuda.Stream(device=self.device)
             copy_stream = self._snap_stream
             copy_stream.wait_stream(cur)  # the state as of this save call
+            for e in _pending_updates(self.device):  # ... after an overlapped update
+                copy_stream.wait_event(e)
+        else:
+            from ..optimizers.overlap import join_all
+
+            join_all(cur)
         stg = None
         if n > 0:
             stg = self._alloc(idx, n)
@@ -803,6 +817,10 @@ class GpuCopier:
                                          ctypes.c_void_p(e.src_ptr + (a - e.offset)), b - a, 4)
         ev_start = torch.cuda.Event()
         ev_start.record(cur)
+        # parameters / optimizer state after an overlapped update; waited on
+        # by the flush thread before the gate opens (the next step, which
+        # re-records these events, is fenced on the gate)
+        pend = _pending_updates(self.device)
         prep = self.pending_prep
         gate = threading.Event()
         holder = self._ring_last
@@ -818,6 +836,8 @@ class GpuCopier:
                 sp = ctypes.c_void_p(self.side_stream.cuda_stream)
                 t0 = time.perf_counter()
                 cstream.wait_event(ev_start)
+                for e in pend:
+                    cstream.wait_event(e)
                 for j, (r0, r1, c0, c1) in enumerate(bounds):
                     if j >= K:
                         cstream.wait_event(free[j % K])  # slot's previous D2H has landed
@@ -866,6 +886,9 @@ class GpuCopier:
         """
         self.fence()  # the restore overwrites the state a pending snapshot still reads
         cur = torch.cuda.current_stream(self.device)
+        from ..optimizers.overlap import join_all
+
+        join_all(cur)  # ... and a pending overlapped optimizer update would overwrite it
         if gather_group is None or world <= 1:
             merged = _merge_pieces(pieces_gpu)
             if hbm_src is not None:

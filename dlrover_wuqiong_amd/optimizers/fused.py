@@ -87,6 +87,34 @@ class _FlatOptimizer(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = False):
         self.flat.zero_grad()
 
+    # ------------------------------------------------- overlapped update
+    _overlap = None
+
+    def overlap_with_forward(self, model, chunks: int = 24):
+        """Run each ``step()``'s update on a side stream, in forward order,
+        under the next forward pass (``optimizers/overlap.py``).  Parameters
+        and optimizer state are complete once that forward has returned, or
+        after :meth:`join`."""
+        from .overlap import StepOverlap
+
+        if self._overlap is not None:
+            self._overlap.remove()
+        self._overlap = StepOverlap(self, model, chunks) if chunks > 0 else None
+        return self._overlap
+
+    def join(self):
+        """Order the current stream after a pending overlapped update."""
+        if self._overlap is not None:
+            self._overlap.join()
+
+    def _run_update(self, launch_range):
+        """The update over the whole buffer: one launch, or piecewise on the
+        overlap side stream."""
+        if self._overlap is not None:
+            self._overlap.launch(launch_range)
+        else:
+            launch_range(0, self.flat.numel)
+
     def checkpoint_safe_tensors(self):
         """Tensors only ``step()`` writes (an overlapped flash-checkpoint
         snapshot may still be reading them after the save call returns)."""
@@ -149,12 +177,20 @@ class FusedAdamW(_FlatOptimizer):
         bc2 = 1.0 - b2 ** self.step_count
         f = self.flat
         if f.data.is_cuda:
+            if self._overlap is not None:
+                self._overlap.join()  # the previous update, if no forward ran since
             gs = self._gscale_ptr()
-            _hip.check(_hip.lib().dw_adam_flat(
-                _hip.ptr(f.data), _hip.dtype_code(f.data), _hip.ptr(self.master), _hip.ptr(f.grad),
-                _hip.dtype_code(f.grad), _hip.ptr(self.exp_avg), _hip.ptr(self.exp_avg_sq), _hip.ptr(gs),
-                f.numel, 0, float(g["lr"]), float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]),
-                float(bc1), float(bc2), int(self.adamw), _hip.ptr(f.decay_mask), _hip.stream()), "adam")
+            ms = self.master
+
+            def launch(lo, hi):
+                _hip.check(_hip.lib().dw_adam_flat(
+                    _hip.ptr(f.data[lo:hi]), _hip.dtype_code(f.data), _hip.ptr(None if ms is None else ms[lo:hi]),
+                    _hip.ptr(f.grad[lo:hi]), _hip.dtype_code(f.grad), _hip.ptr(self.exp_avg[lo:hi]),
+                    _hip.ptr(self.exp_avg_sq[lo:hi]), _hip.ptr(gs), hi - lo, 0, float(g["lr"]), float(b1),
+                    float(b2), float(g["eps"]), float(g["weight_decay"]), float(bc1), float(bc2), int(self.adamw),
+                    _hip.ptr(f.decay_mask[lo // 64:]), _hip.stream()), "adam")
+
+            self._run_update(launch)
             return loss
         # CPU path (reference math)
         scale = self._cpu_gscale()
@@ -195,12 +231,20 @@ class FusedAGD(_FlatOptimizer):
         clip = float(g["clip"]) if g["clip"] is not None else 0.0
         f = self.flat
         if f.data.is_cuda:
+            if self._overlap is not None:
+                self._overlap.join()
             gs = self._gscale_ptr()
-            _hip.check(_hip.lib().dw_agd_flat(
-                _hip.ptr(f.data), _hip.dtype_code(f.data), _hip.ptr(self.master), _hip.ptr(f.grad),
-                _hip.dtype_code(f.grad), _hip.ptr(self.exp_avg), _hip.ptr(self.exp_avg_sq), _hip.ptr(gs),
-                f.numel, 0, float(g["lr"]), float(b1), float(b2), float(g["delta"]), float(g["weight_decay"]),
-                float(bc1), float(bc1_prev), float(bc2), clip, _hip.ptr(f.decay_mask), _hip.stream()), "agd")
+            ms = self.master
+
+            def launch(lo, hi):
+                _hip.check(_hip.lib().dw_agd_flat(
+                    _hip.ptr(f.data[lo:hi]), _hip.dtype_code(f.data), _hip.ptr(None if ms is None else ms[lo:hi]),
+                    _hip.ptr(f.grad[lo:hi]), _hip.dtype_code(f.grad), _hip.ptr(self.exp_avg[lo:hi]),
+                    _hip.ptr(self.exp_avg_sq[lo:hi]), _hip.ptr(gs), hi - lo, 0, float(g["lr"]), float(b1),
+                    float(b2), float(g["delta"]), float(g["weight_decay"]), float(bc1), float(bc1_prev), float(bc2),
+                    clip, _hip.ptr(f.decay_mask[lo // 64:]), _hip.stream()), "agd")
+
+            self._run_update(launch)
             return loss
         scale = self._cpu_gscale()
         grad = f.grad.float() * scale

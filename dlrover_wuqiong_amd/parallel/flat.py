@@ -76,6 +76,10 @@ class FlatParams:
         return self._index[id(p)]
 
     def zero_grad(self):
+        ovl = getattr(self, "_step_overlap", None)
+        if ovl is not None and ovl.pending:  # an overlapped optimizer update still reads them
+            ovl.zero_grad()
+            return
         self.grad.zero_()
 
     def reattach_grads(self):

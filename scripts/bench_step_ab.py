@@ -1,0 +1,79 @@
+"""GPT2-1.5B training step A/B (1 GPU, B=8 x 1024, bf16, FusedAdamW with
+clipping): one process per variant, K timed steps between device-wide syncs.
+
+  python scripts/bench_step_ab.py --steps 10                     # overlap off / on
+  python scripts/bench_step_ab.py --variant on --env DWAMD_NORM_BWD_PART_OFF=1
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def run(variant, steps, model_name):
+    import torch
+
+    from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
+    from dlrover_wuqiong_amd.optimizers.fused import FusedAdamW
+    from dlrover_wuqiong_amd.parallel.flat import FlatParams
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    cfg = GPT2Config.named(model_name)
+    with torch.device(dev):
+        model = GPT2(cfg)
+    model.to(torch.bfloat16)
+    flat = FlatParams(model, dtype=torch.bfloat16, device=dev)
+    opt = FusedAdamW(flat, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0)
+    if variant == "on":
+        opt.overlap_with_forward(model)
+    data = torch.randint(0, cfg.vocab_size, (8, 1025), device=dev)
+    losses = []
+
+    def step():
+        loss = model(data[:, :-1], data[:, 1:])
+        loss.backward()
+        opt.step()
+        flat.zero_grad()
+        losses.append(loss.detach())
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    ms = 1000 * (time.perf_counter() - t0) / steps
+    print(json.dumps({"variant": variant, "step_ms": round(ms, 2), "tok_s": round(8 * 1024 / ms * 1000),
+                      "loss_last": round(float(losses[-1]), 4),
+                      "env": {k: v for k, v in os.environ.items() if k.startswith("DWAMD_")}}), flush=True)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--model", default="gpt2-1.5b")
+    p.add_argument("--variant", default="", help="off | on (one process); default: both")
+    p.add_argument("--env", action="append", default=[], help="KEY=VAL for the child processes")
+    a = p.parse_args()
+    if a.variant:
+        run(a.variant, a.steps, a.model)
+        return
+    env = dict(os.environ)
+    for kv in a.env:
+        k, v = kv.split("=", 1)
+        env[k] = v
+    for v in ("off", "on"):
+        rc = subprocess.call([sys.executable, __file__, "--steps", str(a.steps), "--model", a.model, "--variant", v],
+                             env=env)
+        if rc:
+            sys.exit(rc)
+
+
+if __name__ == "__main__":
+    main()

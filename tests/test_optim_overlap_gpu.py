@@ -1,0 +1,98 @@
+"""Optimizer update overlapped with the next forward (optimizers/overlap.py)
+on the GPU: bitwise the same training trajectory as the one-launch update,
+for AdamW and AGD, with grad clipping; checkpoint snapshots taken while an
+update is pending read the updated state."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from dlrover_wuqiong_amd._native import kernels
+
+    kernels(required=True)
+
+
+def _run(overlap: bool, opt_name: str, steps: int = 4):
+    from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
+    from dlrover_wuqiong_amd.optimizers.fused import FusedAdamW, FusedAGD
+    from dlrover_wuqiong_amd.parallel.flat import FlatParams
+
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    cfg = GPT2Config.named("gpt2-tiny")
+    with torch.device(dev):
+        model = GPT2(cfg)
+    model.to(torch.bfloat16)
+    flat = FlatParams(model)
+    if opt_name == "adamw":
+        opt = FusedAdamW(flat, lr=1e-3, weight_decay=0.1, max_grad_norm=1.0)
+    else:
+        opt = FusedAGD(flat, lr=1e-3, weight_decay=0.1, max_grad_norm=1.0)
+    if overlap:
+        ov = opt.overlap_with_forward(model, chunks=5)
+        assert len(ov.pieces) >= 3
+    g = torch.Generator(device="cpu").manual_seed(1)
+    x = torch.randint(0, cfg.vocab_size, (steps, 2, 129), generator=g).to(dev)
+    losses = []
+    for s in range(steps):
+        loss = model(x[s, :, :-1], x[s, :, 1:])
+        loss.backward()
+        opt.step()
+        flat.zero_grad()
+        losses.append(loss.detach())
+    opt.join()
+    torch.cuda.synchronize()
+    return ([float(v) for v in losses], flat.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(),
+            None if opt.master is None else opt.master.clone(), float(flat.grad.abs().sum()))
+
+
+@pytest.mark.parametrize("opt_name", ["adamw", "agd"])
+def test_overlapped_update_bitwise_equal(opt_name):
+    _need_gpu()
+    a = _run(False, opt_name)
+    b = _run(True, opt_name)
+    assert a[0] == b[0], (a[0], b[0])
+    for ta, tb in zip(a[1:5], b[1:5]):
+        if ta is not None:
+            assert torch.equal(ta, tb)
+    assert a[5] == 0.0 and b[5] == 0.0  # zero_grad deferred onto the side stream still zeroes
+
+
+def test_snapshot_orders_after_pending_update(tmp_path):
+    """A GpuCopier snapshot enqueued while the update is pending copies the
+    UPDATED parameters (its copy stream waits for the update's event)."""
+    _need_gpu()
+    from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
+    from dlrover_wuqiong_amd.optimizers.fused import FusedAdamW
+    from dlrover_wuqiong_amd.optimizers.overlap import pending_events
+    from dlrover_wuqiong_amd.parallel.flat import FlatParams
+
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    cfg = GPT2Config.named("gpt2-tiny")
+    with torch.device(dev):
+        model = GPT2(cfg)
+    model.to(torch.bfloat16)
+    flat = FlatParams(model)
+    opt = FusedAdamW(flat, lr=1e-2, max_grad_norm=1.0)
+    opt.overlap_with_forward(model, chunks=4)
+    x = torch.randint(0, cfg.vocab_size, (2, 65), device=dev)
+    model(x[:, :-1], x[:, 1:]).backward()
+    opt.step()
+    assert pending_events(dev)
+    # what a checkpoint copy stream does: wait for the pending update, then read
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    for e in pending_events(dev):
+        s.wait_event(e)
+    with torch.cuda.stream(s):
+        snap = flat.data.clone()
+    s.synchronize()
+    opt.join()
+    torch.cuda.synchronize()
+    assert torch.equal(snap, flat.data)
