@@ -32,6 +32,9 @@
 #ifndef DWAMD_DQ_RI
 #define DWAMD_DQ_RI 1  // A/B: -DDWAMD_DQ_RI=0 builds the previous dQ form
 #endif
+#ifndef DWAMD_DQ_SPLIT
+#define DWAMD_DQ_SPLIT 1  // A/B: 0 keeps the D=64 mask a runtime branch inside one tile body
+#endif
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -595,7 +598,7 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
       // subtile 0's softmax (a runtime mask branch split them).
       // (D=64 only: at D=128 the overlap needs ~200 more VGPRs than the 256 of
       // two waves per SIMD and spills; there the mask stays a runtime branch.)
-      constexpr bool SPLIT = D == 64;
+      constexpr bool SPLIT = DWAMD_DQ_SPLIT && D == 64;
       auto tile = [&](auto mask_c) {
         constexpr bool MASK = decltype(mask_c)::value;
       // one 32-key subtile at a time keeps S^T / dP^T at 32 registers

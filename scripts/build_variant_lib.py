@@ -21,7 +21,8 @@ def main():
         obj = os.path.join(odir, os.path.basename(src) + ".o")
         cmd = [b._hipcc(), f"--offload-arch={b.ARCH}", "-O3", "-std=c++17", "-fPIC", "-mcode-object-version=5",
                "-munsafe-fp-atomics", "-ffp-contract=fast", "-mllvm", "-amdgpu-mfma-vgpr-form",
-               "-Wno-unused-result", "-I", os.path.join(b.CSRC, "kernels")] + extra + ["-c", src, "-o", obj]
+               "-Wno-unused-result", "-I", os.path.join(b.CSRC, "kernels")] + b.FILE_FLAGS.get(
+                   os.path.basename(src), []) + extra + ["-c", src, "-o", obj]
         procs.append(subprocess.Popen(cmd))
         objs.append(obj)
     assert all(p.wait() == 0 for p in procs)

@@ -40,6 +40,7 @@ int probe(hipblasLtHandle_t h, hipblasLtEpilogue_t epi, bool aux, hipDataType bi
 }
 
 int main(int argc, char** argv) {
+  setvbuf(stdout, nullptr, _IONBF, 0);  // partial results survive a timeout
   hipblasLtHandle_t h;
   hipblasLtCreate(&h);
   if (argc > 1) {
