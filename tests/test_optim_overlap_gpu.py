@@ -52,14 +52,50 @@ def _run(overlap: bool, opt_name: str, steps: int = 4):
 
 
 @pytest.mark.parametrize("opt_name", ["adamw", "agd"])
-def test_overlapped_update_bitwise_equal(opt_name):
+def test_piecewise_update_bitwise_equal(opt_name):
+    """The same gradients through the one-launch update and the piecewise
+    side-stream update: bitwise the same parameters, masters and moments."""
+    _need_gpu()
+    from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
+    from dlrover_wuqiong_amd.optimizers.fused import FusedAdamW, FusedAGD
+    from dlrover_wuqiong_amd.parallel.flat import FlatParams
+
+    dev = torch.device("cuda:0")
+    outs = []
+    for overlap in (False, True):
+        torch.manual_seed(0)
+        with torch.device(dev):
+            model = GPT2(GPT2Config.named("gpt2-tiny"))
+        model.to(torch.bfloat16)
+        flat = FlatParams(model)
+        cls = FusedAdamW if opt_name == "adamw" else FusedAGD
+        opt = cls(flat, lr=1e-3, weight_decay=0.1, max_grad_norm=1.0)
+        if overlap:
+            opt.overlap_with_forward(model, chunks=7)
+        g = torch.Generator(device="cpu").manual_seed(3)
+        for _ in range(3):
+            flat.grad.copy_(torch.randn(flat.numel, generator=g).to(dev, flat.grad.dtype))
+            opt.step()
+            opt.join()
+        torch.cuda.synchronize()
+        outs.append([flat.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(), opt.master])
+    for ta, tb in zip(*outs):
+        if ta is not None:
+            assert torch.equal(ta, tb)
+
+
+@pytest.mark.parametrize("opt_name", ["adamw", "agd"])
+def test_overlapped_training_matches(opt_name):
+    """Training with the update under the next forward follows the plain
+    run (the backward's float-atomic column sums make neither run bitwise
+    reproducible, so: equal within run-to-run noise)."""
     _need_gpu()
     a = _run(False, opt_name)
     b = _run(True, opt_name)
-    assert a[0] == b[0], (a[0], b[0])
+    assert all(abs(x - y) <= 1e-3 * abs(x) for x, y in zip(a[0], b[0])), (a[0], b[0])
     for ta, tb in zip(a[1:5], b[1:5]):
         if ta is not None:
-            assert torch.equal(ta, tb)
+            torch.testing.assert_close(ta.float(), tb.float(), rtol=2e-2, atol=1e-5)
     assert a[5] == 0.0 and b[5] == 0.0  # zero_grad deferred onto the side stream still zeroes
 
 
