@@ -124,7 +124,7 @@ def _build_runtime(verbose=False):
 # filler'); measured GPT2-shape backward 368 -> 379 TF/s, D=128 within +-1 %
 # (profiles/r3/attn_bench_{slp,noslp}.jsonl).
 FILE_FLAGS = {"attn_bwd.hip": ["-fno-slp-vectorize"], "attn_fwd.hip": ["-fno-slp-vectorize"],
-              "attn_bwd_dq2.hip": ["-fno-slp-vectorize"]}
+              "attn_bwd_dq2.hip": ["-fno-slp-vectorize"], "attn_fwd2.hip": ["-fno-slp-vectorize"]}
 
 
 def _compile_hip(src):

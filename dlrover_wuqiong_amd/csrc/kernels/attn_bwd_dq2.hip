@@ -55,7 +55,8 @@ attn_bwd_dq2_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, 
                     AttnVarlen vl) {
   using C = Dq2Cfg;
   constexpr int D = C::D, G = C::G;
-  constexpr bool RI = DWAMD_DQ2_RI;
+  constexpr bool RI = DWAMD_DQ2_RI == 1;
+  constexpr bool RID = DWAMD_DQ2_RI == 2;  // -delta only as dP's initial accumulator
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -168,7 +169,10 @@ attn_bwd_dq2_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, 
 #pragma unroll
             for (int g = 0; g < G; ++g)
 #pragma unroll
-              for (int i = 0; i < 16; ++i) s[g][i] = dp[g][i] = 0.f;
+              for (int i = 0; i < 16; ++i) {
+                s[g][i] = 0.f;
+                if (!RID) dp[g][i] = 0.f;
+              }
           }
 #pragma unroll
           for (int kk = 0; kk < C::KK; ++kk) {
@@ -179,7 +183,7 @@ attn_bwd_dq2_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, 
               s[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(kf), as_bf(qf[g][kk]),
                                                              (RI && kk == 0) ? s_init[g] : s[g], 0, 0, 0);
               dp[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(vf), as_bf(dof[g][kk]),
-                                                              (RI && kk == 0) ? dp_init[g] : dp[g], 0, 0, 0);
+                                                              ((RI || RID) && kk == 0) ? dp_init[g] : dp[g], 0, 0, 0);
             }
           }
 #pragma unroll
@@ -197,7 +201,7 @@ attn_bwd_dq2_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, 
                 s[g][i] = __builtin_amdgcn_exp2f(s[g][i]) * dp[g][i];  // dS^T (scale in the epilogue)
               } else {
                 const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[g][i], scale_log2, -lse2[g]));
-                s[g][i] = p * (dp[g][i] - dl[g]);
+                s[g][i] = p * (RID ? dp[g][i] : dp[g][i] - dl[g]);
               }
             }
           }

@@ -378,10 +378,16 @@ static void launch_fwd_v(const void* q, const void* k, const void* v, void* o, v
                      (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, (float*)lse, S, H, HKV, scale_log2, st, vl, ex);
 }
 
+// one-wave-per-SIMD D = 128 forward (attn_fwd2.hip); false: not taken
+bool launch_fwd2(const void* q, const void* k, const void* v, void* o, void* lse, int B, int S, int H, int HKV,
+                 int causal, float scale_log2, const AttnStrides& st, const AttnVarlen& vl, hipStream_t s);
+
 template <int D>
 static void launch_fwd(const void* q, const void* k, const void* v, void* o, void* lse, int B, int S, int H, int HKV,
                        int causal, float scale_log2, const AttnStrides& st, const AttnVarlen& vl, hipStream_t s,
                        const AttnExt* ext = nullptr, int variant = 0) {
+  if (D == 128 && !ext && variant == 0 && launch_fwd2(q, k, v, o, lse, B, S, H, HKV, causal, scale_log2, st, vl, s))
+    return;
   // D=64: 4 waves (128 queries per block, two blocks per CU):
   // twice the blocks of the 8-wave form for a finer causal balance; measured
   // against 8 waves capped at 128 VGPRs (spills) / uncapped and 4 waves
