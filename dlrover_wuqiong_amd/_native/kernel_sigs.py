@@ -81,7 +81,7 @@ SIGS = {
     "dw_colsum_acc": (i32, [vp, i64, i32, vp, vp, i32, i32, vp]),
     "dw_gelu_bwd_dbias": (i32, [vp, vp, vp, i64, i32, vp, vp, i32, i32, vp]),
     "dw_norm_bwd2": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp]),
-    "dw_norm_bwd3": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32, i32, i32, i32, vp]),
+    "dw_norm_bwd3": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32, i32, i32, i32, vp, vp, vp]),
     "dw_add_norm_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, f32, i32, vp]),
     "dw_swiglu_fwd": (i32, [vp, vp, i64, i32, vp]),
     "dw_swiglu_bwd": (i32, [vp, vp, vp, i64, i32, vp]),

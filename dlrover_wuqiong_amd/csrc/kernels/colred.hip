@@ -244,11 +244,11 @@ __global__ void __launch_bounds__(256) norm_bwd_fused_kernel(
   __shared__ float red[2][4][512 + 4];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nv = H >> 3;
-  float ag[VPL][8], ab[VPL][8];
+  float ag[VPL][8], ab[VPL][8], ad[VPL][8];
 #pragma unroll
   for (int j = 0; j < VPL; ++j)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) ag[j][k] = ab[j][k] = 0.f;
+    for (int k = 0; k < 8; ++k) ag[j][k] = ab[j][k] = ad[j][k] = 0.f;
   for (int64_t row = (int64_t)blockIdx.x * 4 + wid; row < rows; row += (int64_t)gridDim.x * 4) {
     const float mu = RMS ? 0.f : mean_in[row];
     const float rstd = rstd_in[row];
@@ -353,7 +353,9 @@ __global__ void __launch_bounds__(256) norm_bwd_fused_kernel(
 // atomics (the atomic-combined fused kernel above, 512 blocks of 4-row
 // waves, was latency-bound at H = 1600: 2048 waves for 8192 rows).  The
 // [blocks, 2H] partials are summed by colsum_f32_kernel.
-template <int VPL, bool RMS, int RPW>
+// DS: also the column sums of dx itself (the bias gradient of the Linear
+// whose output is this add-norm's residual input): partial rows [3H].
+template <int VPL, bool RMS, int RPW, bool DS = false>
 __global__ void __launch_bounds__(256) norm_bwd_part_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ gamma,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const bf16_t* __restrict__ dres,
@@ -363,11 +365,11 @@ __global__ void __launch_bounds__(256) norm_bwd_part_kernel(
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nv = H >> 3;
   const int64_t row0 = ((int64_t)blockIdx.x * 4 + wid) * RPW;
-  float ag[VPL][8], ab[VPL][8];
+  float ag[VPL][8], ab[VPL][8], ad[VPL][8];
 #pragma unroll
   for (int j = 0; j < VPL; ++j)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) ag[j][k] = ab[j][k] = 0.f;
+    for (int k = 0; k < 8; ++k) ag[j][k] = ab[j][k] = ad[j][k] = 0.f;
   u32x4 xv[RPW][VPL], dv[RPW][VPL], gv[VPL];
 #pragma unroll
   for (int j = 0; j < VPL; ++j) {
@@ -427,11 +429,15 @@ __global__ void __launch_bounds__(256) norm_bwd_part_kernel(
 #pragma unroll
           for (int k = 0; k < 8; ++k) o[k] += r[k];
         }
+        if constexpr (DS) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) ad[j][k] += o[k];
+        }
         *(u32x4*)(dx + row * H + c * 8) = pack8(o);
       }
     }
   }
-  float* prow = part + (int64_t)blockIdx.x * 2 * H;
+  float* prow = part + (int64_t)blockIdx.x * (DS ? 3 : 2) * H;
 #pragma unroll
   for (int j = 0; j < VPL; ++j) {
 #pragma unroll
@@ -446,10 +452,22 @@ __global__ void __launch_bounds__(256) norm_bwd_part_kernel(
       const int c = 512 * j + cl;
       if (c < H) {
         prow[c] = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
-        if constexpr (!RMS) prow[H + c] = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+        prow[H + c] = RMS ? 0.f : red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
       }
     }
     __syncthreads();
+    if constexpr (DS) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[0][wid][lane * 8 + k] = ad[j][k];
+      __syncthreads();
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int cl = threadIdx.x + 256 * h;
+        const int c = 512 * j + cl;
+        if (c < H) prow[2 * H + c] = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -461,7 +479,8 @@ __global__ void __launch_bounds__(256) norm_bwd_part_kernel(
 __global__ void __launch_bounds__(256) colsum_f32_kernel(const float* __restrict__ part, int R, int H2,
                                                          int rows_per_blk, float* __restrict__ ws,
                                                          void* __restrict__ out0, void* __restrict__ out1,
-                                                         int is_fp32, int accumulate) {
+                                                         int is_fp32, int accumulate, int H,
+                                                         void* __restrict__ out2) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   const int r0 = blockIdx.y * rows_per_blk, r1 = min(R, r0 + rows_per_blk);
   if (c < H2) {
@@ -486,11 +505,12 @@ __global__ void __launch_bounds__(256) colsum_f32_kernel(const float* __restrict
   if (!is_last) return;
   if (c < H2) {
     const float v = __hip_atomic_exchange(ws + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int H = H2 / 2;
     if (c < H)
       colred_store(out0, c, v, is_fp32, accumulate);
-    else
+    else if (c < 2 * H)
       colred_store(out1, c - H, v, is_fp32, accumulate);
+    else
+      colred_store(out2, c - 2 * H, v, is_fp32, 1);  // a bias gradient: always accumulated
   }
   if (threadIdx.x == 0) __hip_atomic_exchange(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -614,35 +634,45 @@ extern "C" int dw_norm_bwd2(const void* dy, const void* x, const void* gamma, co
 // caller provides fp32 scratch ``part`` of at least part_floats =
 // ceil(rows / 8) * 2H floats (any content).  ws as v2 but sized
 // 2H + ceil(2H / 256) + ceil(H / 512) floats.
+//
+// dsum (nullable, small-H path only): column sums of dx accumulated into it
+// (same dtype as dgamma) -- the bias gradient of the Linear that produced
+// the residual input; returns 1 when it was written, 0 when not (fallback
+// path: the caller keeps the Linear's own bias reduction).
 extern "C" int dw_norm_bwd3(const void* dy, const void* x, const void* gamma, const void* mean, const void* rstd,
                             const void* dres, void* dx, void* dgamma, void* dbeta, void* ws, void* part,
                             int64_t part_floats, int64_t rows, int H, int rms, int out_fp32, int accumulate,
-                            void* stream) {
+                            void* dsum, int* dsum_done, void* stream) {
   constexpr int RPW = 2;
   const int64_t nb = (rows + 4 * RPW - 1) / (4 * RPW);
+  const int pw = dsum ? 3 : 2;
+  if (dsum_done) *dsum_done = 0;
   static const bool off = getenv_flag("DWAMD_NORM_BWD_PART_OFF");  // A/B switch
-  if (off || !part || !(dgamma || dbeta) || H % 8 != 0 || H >= 2048 || nb * 2 * H > part_floats)
+  if (off || !part || !(dgamma || dbeta) || H % 8 != 0 || H >= 2048 || nb * pw * H > part_floats)
     return dw_norm_bwd2(dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, ws, rows, H, rms, out_fp32, accumulate,
                         stream);
   hipStream_t s = (hipStream_t)stream;
+#define NBP(RM, DSV)                                                                                          \
+  hipLaunchKernelGGL((norm_bwd_part_kernel<VPL, RM, RPW, DSV>), dim3((unsigned)nb), dim3(256), 0, s,         \
+                     (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)gamma, RM ? nullptr : (const float*)mean, \
+                     (const float*)rstd, (const bf16_t*)dres, (bf16_t*)dx, (float*)part, rows, H)
   DISPATCH_VPL2(H, {
     if constexpr (VPL <= 4) {
-      if (rms)
-        hipLaunchKernelGGL((norm_bwd_part_kernel<VPL, true, RPW>), dim3((unsigned)nb), dim3(256), 0, s,
-                           (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)gamma, nullptr, (const float*)rstd,
-                           (const bf16_t*)dres, (bf16_t*)dx, (float*)part, rows, H);
-      else
-        hipLaunchKernelGGL((norm_bwd_part_kernel<VPL, false, RPW>), dim3((unsigned)nb), dim3(256), 0, s,
-                           (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)gamma, (const float*)mean,
-                           (const float*)rstd, (const bf16_t*)dres, (bf16_t*)dx, (float*)part, rows, H);
+      if (rms) {
+        if (dsum) NBP(true, true); else NBP(true, false);
+      } else {
+        if (dsum) NBP(false, true); else NBP(false, false);
+      }
     }
   });
-  const int H2 = 2 * H;
+#undef NBP
+  if (dsum_done) *dsum_done = dsum ? 1 : 0;
+  const int H2 = pw * H;
   const int splits = (int)std::max<int64_t>(1, std::min<int64_t>(64, nb / 16));
   const int per = (int)((nb + splits - 1) / splits);
   dim3 g((H2 + 255) / 256, (unsigned)((nb + per - 1) / per));
   hipLaunchKernelGGL(colsum_f32_kernel, g, dim3(256), 0, s, (const float*)part, (int)nb, H2, per, (float*)ws,
-                     dgamma, rms ? nullptr : dbeta, out_fp32, accumulate);
+                     dgamma, rms ? nullptr : dbeta, out_fp32, accumulate, H, dsum);
   DW_LAUNCH_RET;
 }
 

@@ -39,6 +39,10 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.weight_param, ctx.bias_param = weight, bias
+        # a following add-norm may take over this bias's gradient (ops/norm.py
+        # _fold_target: the column sums of the residual gradient it computes
+        # anyway); it sets out_bias_folded before this backward runs
+        ctx.out_bias, ctx.out_bias_folded = bias, False
         return F.linear(x, weight, bias)
 
     @staticmethod
@@ -47,7 +51,7 @@ class _LinearFn(torch.autograd.Function):
         N, K = w.shape
         dy2 = dy.reshape(-1, N)
         x2 = x.reshape(-1, K)
-        b = ctx.bias_param
+        b = None if ctx.out_bias_folded else ctx.bias_param
         gw = direct_grad(ctx.weight_param)
         gb = direct_grad(b) if b is not None else None
         if (_WGRAD_STREAM and dy2.is_cuda and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]

@@ -63,6 +63,7 @@ class _FusedMLPFn(torch.autograd.Function):
         ctx.save_for_backward(x2, w1, pre, g, w2)
         ctx.params = (w1, b1, w2, b2)
         ctx.shape = shape
+        ctx.out_bias, ctx.out_bias_folded = b2, False  # see ops/linear.py
         return y.view(*shape[:-1], w2.shape[0])
 
     @staticmethod
@@ -75,8 +76,8 @@ class _FusedMLPFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, N2).contiguous().to(x2.dtype)
         M = dy2.shape[0]
         dw2 = _acc(p_w2, lambda gb: gb.addmm_(dy2.t(), g) if gb is not None else dy2.t() @ g)
-        db2 = _acc(p_b2, lambda gb: colsum(dy2, out=gb, accumulate=True) if gb is not None else
-                   colsum(dy2, p_b2.dtype))
+        db2 = None if ctx.out_bias_folded else _acc(
+            p_b2, lambda gb: colsum(dy2, out=gb, accumulate=True) if gb is not None else colsum(dy2, p_b2.dtype))
         key = (M, N1, N2)
         dh = torch.empty(M, N1, device=dy.device, dtype=x2.dtype)
         db1_f = None

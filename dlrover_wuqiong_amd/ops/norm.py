@@ -4,12 +4,32 @@ Parity: reference ``atorch/atorch/normalization/layernorm.py``
 (``AtorchLayerNorm``) and the RMSNorm of its Llama modules.
 """
 
+import ctypes
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _hip
 from ._grad import direct_grad, notify
+
+_FOLD = os.environ.get("DWAMD_NORM_FOLD_BIAS", "1") != "0"
+
+
+def _fold_target(res, H):
+    """The producer of an add-norm's residual input whose output bias
+    gradient this norm's backward can take over: a fused Linear / MLP node
+    (``ctx.out_bias``) whose bias accumulates into flat gradient storage.
+    d(bias) = column sums of d(res) = of the norm's dx, which the small-H
+    backward kernel reduces anyway -- one fewer pass over [rows, H]."""
+    if not _FOLD or H >= 2048 or H % 8:
+        return None
+    node = getattr(res, "grad_fn", None)
+    b = getattr(node, "out_bias", None)
+    if b is None or direct_grad(b) is None:
+        return None
+    return (node, b)
 
 
 def _norm_backward(ctx, dy, dres):
@@ -27,10 +47,7 @@ def _norm_backward(ctx, dy, dres):
         if dres.dtype != torch.bfloat16:
             dres = dres.to(torch.bfloat16)
     # sums + strip counters (of the 512-column fused path and of the small-H colsum)
-    ws = _hip.zeroed_workspace(2 * H + max((H + 511) // 512, (2 * H + 255) // 256), x2.device)
-    # small H: one-pass kernel writes per-block fp32 dgamma/dbeta partials here
-    nparts = (R + 7) // 8 * 2 * H if H < 2048 else 0
-    part = torch.empty(nparts, device=x2.device, dtype=torch.float32) if nparts else None
+    ws = _hip.zeroed_workspace(3 * H + max((H + 511) // 512, (3 * H + 255) // 256), x2.device)
     dx = torch.empty_like(x2)
     wp, bp = ctx.weight_param, ctx.bias_param
     gd, bd = direct_grad(wp), direct_grad(bp) if ctx.has_bias else None
@@ -40,11 +57,24 @@ def _norm_backward(ctx, dy, dres):
     else:
         dgamma = torch.empty(H, device=x2.device, dtype=weight.dtype)
         dbeta = torch.empty(H, device=x2.device, dtype=weight.dtype) if ctx.has_bias else None
+    # the residual producer's bias gradient (ops/linear.py out_bias): same
+    # flags as dgamma (accumulated into direct storage of the same dtype)
+    fold = getattr(ctx, "fold", None)
+    dsum = direct_grad(fold[1]) if (fold is not None and direct) else None
+    if dsum is not None and dsum.dtype != dgamma.dtype:
+        dsum = None
+    # small H: one-pass kernel writes per-block fp32 dgamma/dbeta (/dsum) partials here
+    nparts = (R + 7) // 8 * (3 if dsum is not None else 2) * H if H < 2048 else 0
+    part = torch.empty(nparts, device=x2.device, dtype=torch.float32) if nparts else None
+    done = ctypes.c_int(0)
     _hip.check(_hip.lib().dw_norm_bwd3(_hip.ptr(dy2), _hip.ptr(x2), _hip.ptr(weight), _hip.ptr(mean),
                                        _hip.ptr(rstd), _hip.ptr(dres), _hip.ptr(dx), _hip.ptr(dgamma),
                                        _hip.ptr(dbeta), _hip.ptr(ws), _hip.ptr(part), nparts, R, H,
                                        int(ctx.rms), int(dgamma.dtype == torch.float32), int(direct),
-                                       _hip.stream()), "norm_bwd")
+                                       _hip.ptr(dsum), ctypes.byref(done), _hip.stream()), "norm_bwd")
+    if done.value:
+        fold[0].out_bias_folded = True  # the producer's backward (later) skips its own reduction
+        notify(fold[1])
     if direct:
         notify(wp)
         notify(bp)
@@ -87,7 +117,8 @@ class _AddNormFn(torch.autograd.Function):
     res receive the same gradient."""
 
     @staticmethod
-    def forward(ctx, x, res, weight, bias, eps, rms):
+    def forward(ctx, x, res, weight, bias, eps, rms, fold=None):
+        ctx.fold = fold
         H = x.shape[-1]
         x2 = x.contiguous().view(-1, H)
         r2 = res.contiguous().view(-1, H)
@@ -106,13 +137,14 @@ class _AddNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, dh):
         dx, dgamma, dbeta = _norm_backward(ctx, dy, dh)
-        return dx, dx, dgamma, dbeta, None, None
+        return dx, dx, dgamma, dbeta, None, None, None
 
 
 def add_layer_norm(x, res, weight, bias, eps: float = 1e-5):
     """Returns (layer_norm(x + res), x + res)."""
     if _hip.bf16_path(x):
-        return _AddNormFn.apply(*_hip.bf16(x, res, weight, bias), eps, False)
+        x, res, weight, bias = _hip.bf16(x, res, weight, bias)
+        return _AddNormFn.apply(x, res, weight, bias, eps, False, _fold_target(res, x.shape[-1]))
     h = x + res
     return F.layer_norm(h, (h.shape[-1],), weight, bias, eps), h
 
@@ -120,7 +152,8 @@ def add_layer_norm(x, res, weight, bias, eps: float = 1e-5):
 def add_rms_norm(x, res, weight, eps: float = 1e-6):
     """Returns (rms_norm(x + res), x + res)."""
     if _hip.bf16_path(x):
-        return _AddNormFn.apply(*_hip.bf16(x, res, weight), None, eps, True)
+        x, res, weight = _hip.bf16(x, res, weight)
+        return _AddNormFn.apply(x, res, weight, None, eps, True, _fold_target(res, x.shape[-1]))
     h = x + res
     return rms_norm(h, weight, eps), h
 
@@ -158,7 +191,8 @@ class LayerNorm(nn.Module):
         """(norm(x + res), x + res) with the residual add fused in."""
         if self.bias is None and _hip.bf16_path(x):
             w = _hip.bf16(self.weight)
-            return _AddNormFn.apply(*_hip.bf16(x, res), w, torch.zeros_like(w), self.eps, False)
+            x, res = _hip.bf16(x, res)
+            return _AddNormFn.apply(x, res, w, torch.zeros_like(w), self.eps, False, _fold_target(res, x.shape[-1]))
         return add_layer_norm(x, res, self.weight, self.bias, self.eps)
 
 
