@@ -1,7 +1,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r4
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_ops_gpu.py tests/test_optim_overlap_gpu.py -m gpu -k "overlap" > gpurun_out/r4/g3_norm_overlap.log 2>&1 &&
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_optim_overlap_gpu.py tests/test_norm_fold_gpu.py -m gpu > gpurun_out/r4/g3_norm_overlap.log 2>&1 &&
 timeout -k 10 300 python -u scripts/bench_step_ab.py --steps 10 > gpurun_out/r4/g3_step_ab.log 2>&1 &&
 DWAMD_NORM_BWD_PART_OFF=1 timeout -k 10 200 python -u scripts/bench_step_ab.py --steps 10 --variant on > gpurun_out/r4/g3_step_nopart.log 2>&1 &&
 timeout -k 10 120 python -u scripts/bench_norm.py > gpurun_out/r4/g3_bench_norm_part.log 2>&1 &&
