@@ -141,78 +141,67 @@ attn_fwd2_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, con
     const char* vl2 = kl + C::TILE;
     if (!CAUSAL || k0 <= q0 + 32 * G - 1 + co) {
       const bool need_mask = (k0 + C::BK > SK) || (CAUSAL && (k0 + C::BK - 1 > q0 + co));
+      // one 32-key subtile at a time (S of both groups = 32 registers): the
+      // online softmax steps per 32 keys, which keeps O (128) + S + the
+      // fragments inside the 256 arch VGPRs
       auto tile = [&](auto mask_c) {
         constexpr bool MASK = decltype(mask_c)::value;
-        // ---- S^T = K Q'^T for both groups, 2 subtiles of 32 keys
-        f32x16 s[G][C::NSB];
 #pragma unroll
-        for (int kk = 0; kk < C::KK; ++kk)
+        for (int sb = 0; sb < C::NSB; ++sb) {
+          f32x16 s[G];
 #pragma unroll
-          for (int sb = 0; sb < C::NSB; ++sb) {
+          for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s[g][i] = 0.f;
+#pragma unroll
+          for (int kk = 0; kk < C::KK; ++kk) {
             const u32x4 kf = *(const u32x4*)(kl + kro[kk & 1] + row_const<D>(32 * sb, kk));
 #pragma unroll
-            for (int g = 0; g < G; ++g) {
-              if (kk == 0) {
+            for (int g = 0; g < G; ++g)
+              s[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf8(kf), bf8(qf[g][kk]), s[g], 0, 0, 0);
+          }
 #pragma unroll
-                for (int i = 0; i < 16; ++i) s[g][sb][i] = 0.f;
-              }
-              s[g][sb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf8(kf), bf8(qf[g][kk]), s[g][sb], 0, 0, 0);
+          for (int g = 0; g < G; ++g) {
+            if (MASK) {
+              const int q = q0 + 32 * g + r;
+              const int rel = (CAUSAL ? min(SK, q + co + 1) : SK) - k0 - 32 * sb - 4 * hh;
+#pragma unroll
+              for (int i = 0; i < 16; ++i) s[g][i] = ((i & 3) + 8 * (i >> 2)) < rel ? s[g][i] : -INFINITY;
             }
-          }
-        // ---- online softmax per group
+            float mx = -INFINITY;
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-          if (MASK) {
-            const int q = q0 + 32 * g + r;
-            const int rel = (CAUSAL ? min(SK, q + co + 1) : SK) - k0 - 4 * hh;
+            for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[g][i]);
+            mx = half_max(mx) - m_i[g];  // the row's max above its offset
+            const bool fresh = !seeded[g] && mx > -INFINITY;
+            const bool shift = (mx > RESCALE_T) || fresh;
+            seeded[g] = seeded[g] || (mx > -INFINITY);
+            if (__any(shift)) {
+              const float d = shift ? mx : 0.f;
+              const float alpha = fresh ? 1.f : __builtin_amdgcn_exp2f(-d);
+              m_i[g] += d;
+              l_i[g] *= alpha;
 #pragma unroll
-            for (int sb = 0; sb < C::NSB; ++sb)
+              for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
-              for (int i = 0; i < 16; ++i)
-                s[g][sb][i] = (32 * sb + (i & 3) + 8 * (i >> 2)) < rel ? s[g][sb][i] : -INFINITY;
-          }
-          float mx = -INFINITY;
-#pragma unroll
-          for (int sb = 0; sb < C::NSB; ++sb)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[g][sb][i]);
-          mx = half_max(mx) - m_i[g];  // the row's max above its offset
-          const bool fresh = !seeded[g] && mx > -INFINITY;
-          const bool shift = (mx > RESCALE_T) || fresh;
-          seeded[g] = seeded[g] || (mx > -INFINITY);
-          if (__any(shift)) {
-            const float d = shift ? mx : 0.f;
-            const float alpha = fresh ? 1.f : __builtin_amdgcn_exp2f(-d);
-            m_i[g] += d;
-            l_i[g] *= alpha;
-#pragma unroll
-            for (int dt = 0; dt < C::DT; ++dt)
-#pragma unroll
-              for (int i = 0; i < 16; ++i) o[g][dt][i] *= alpha;
-          }
-          float rs = 0.f;
-#pragma unroll
-          for (int sb = 0; sb < C::NSB; ++sb)
+                for (int i = 0; i < 16; ++i) o[g][dt][i] *= alpha;
+            }
+            float rs = 0.f;
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-              const float p = __builtin_amdgcn_exp2f(s[g][sb][i] - m_i[g]);
-              s[g][sb][i] = p;
+              const float p = __builtin_amdgcn_exp2f(s[g][i] - m_i[g]);
+              s[g][i] = p;
               rs += p;
             }
-          l_i[g] += rs;
-        }
-        // ---- O^T += V^T P^T: 4 k-steps of 16 keys; each V^T fragment feeds both groups
-#pragma unroll
-        for (int sb = 0; sb < C::NSB; ++sb)
+            l_i[g] += rs;
+          }
+          // O^T += V^T P^T over this subtile's 32 keys; each V^T fragment feeds both groups
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2) {
             u32x4 pf[G];
 #pragma unroll
-            for (int g = 0; g < G; ++g) {
-              const f32x16& a = s[g][sb];
-              pf[g] = (u32x4){pk2f(a[8 * s2 + 0], a[8 * s2 + 1]), pk2f(a[8 * s2 + 2], a[8 * s2 + 3]),
-                              pk2f(a[8 * s2 + 4], a[8 * s2 + 5]), pk2f(a[8 * s2 + 6], a[8 * s2 + 7])};
-            }
+            for (int g = 0; g < G; ++g)
+              pf[g] = (u32x4){pk2f(s[g][8 * s2 + 0], s[g][8 * s2 + 1]), pk2f(s[g][8 * s2 + 2], s[g][8 * s2 + 3]),
+                              pk2f(s[g][8 * s2 + 4], s[g][8 * s2 + 5]), pk2f(s[g][8 * s2 + 6], s[g][8 * s2 + 7])};
             const int kr = 32 * sb + 16 * s2;
 #pragma unroll
             for (int dt = 0; dt < C::DT; ++dt) {
@@ -226,6 +215,7 @@ attn_fwd2_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, con
                 o[g][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf8(vf), bf8(pf[g]), o[g][dt], 0, 0, 0);
             }
           }
+        }
       };
       if (need_mask)
         tile(std::true_type{});
