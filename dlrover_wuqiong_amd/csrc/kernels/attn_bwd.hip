@@ -757,11 +757,9 @@ static void launch_bwd(const void* q, const void* k, const void* v, const void* 
                      (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta,        \
                      (bf16_t*)dq, Sq, H, HKV, softmax_scale, scale_log2, st, vl, ex)
   bool dq_done = false;
-  if constexpr (D == 128) {  // dense masks: the one-wave-per-SIMD form (attn_bwd_dq2.hip)
-    if (!ext)
-      dq_done = launch_dq2(q, k, v, dout, lse, delta, dq, B, Sq, H, HKV, causal, softmax_scale, scale_log2, st, vl,
-                           sq);
-  }
+  if (!ext)  // dense masks: the 4-wave, 64-queries-per-wave form (attn_bwd_dq2.hip)
+    dq_done = launch_dq2(q, k, v, dout, lse, delta, dq, B, Sq, H, HKV, D, causal, softmax_scale, scale_log2, st, vl,
+                         sq);
   if (dq_done) {
   } else if (ext) {
     if (causal) DQ(true, true); else DQ(false, true);

@@ -38,8 +38,8 @@ __device__ __forceinline__ u32x4 tr_frag(const char* img, int r0, int d0, const 
   return join_tr(v0, v1);
 }
 
-// One-wave-per-SIMD dQ kernel for D = 128 (attn_bwd_dq2.hip): returns false
+// One-wave-per-SIMD dQ kernel (attn_bwd_dq2.hip): returns false
 // when it does not apply (then the caller launches attn_bwd_dq_kernel).
 bool launch_dq2(const void* q, const void* k, const void* v, const void* dout, const void* lse, const float* delta,
-                void* dq, int B, int Sq, int H, int HKV, int causal, float softmax_scale, float scale_log2,
+                void* dq, int B, int Sq, int H, int HKV, int D, int causal, float softmax_scale, float scale_log2,
                 const AttnStrides& st, const AttnVarlen& vl, hipStream_t s);

@@ -29,13 +29,18 @@
 #endif
 #ifndef DWAMD_DQ2_RI
 // row constants as loop-invariant MFMA C operands (attn_bwd_dq_kernel's RI):
-// off -- its 64 extra registers crash the ROCm 7.2 register allocator here
+// off -- at D = 128 its 64 extra registers crash the ROCm 7.2 register
+// allocator; at D = 64 the allocator trades the saved fma / sub for as many
+// AGPR copies (148 per tile).  1 on; 2 -delta only
 #define DWAMD_DQ2_RI 0
 #endif
 
 namespace {
+template <int DD>
 struct Dq2Cfg {
-  static constexpr int D = 128;
+  static constexpr int D = DD;
+  // one wave per SIMD (D = 64 at two per SIMD spills 112 registers)
+  static constexpr int MINW = 1;
   static constexpr int WAVES = 4;
   static constexpr int G = 2;  // 32-query groups per wave
   static constexpr int BQ = 32 * G * WAVES;
@@ -47,13 +52,13 @@ struct Dq2Cfg {
 };
 }  // namespace
 
-template <bool CAUSAL>
-__global__ void __launch_bounds__(64 * Dq2Cfg::WAVES, 1)
+template <int DD, bool CAUSAL>
+__global__ void __launch_bounds__(64 * Dq2Cfg<DD>::WAVES, Dq2Cfg<DD>::MINW)
 attn_bwd_dq2_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
                     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
                     bf16_t* __restrict__ dQ, int S, int H, int HKV, float scale, float scale_log2, AttnStrides st,
                     AttnVarlen vl) {
-  using C = Dq2Cfg;
+  using C = Dq2Cfg<DD>;
   constexpr int D = C::D, G = C::G;
   constexpr bool RI = DWAMD_DQ2_RI == 1;
   constexpr bool RID = DWAMD_DQ2_RI == 2;  // -delta only as dP's initial accumulator
@@ -249,26 +254,43 @@ attn_bwd_dq2_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, 
   }
 }
 
-bool launch_dq2(const void* q, const void* k, const void* v, const void* dout, const void* lse, const float* delta,
-                void* dq, int B, int Sq, int H, int HKV, int causal, float softmax_scale, float scale_log2,
-                const AttnStrides& st, const AttnVarlen& vl, hipStream_t s) {
-  static const bool off = [] {
-    const char* e = std::getenv("DWAMD_ATTN_DQ2");  // A/B: 0 = the 8-wave kernel
-    return e && e[0] == '0';
-  }();
-  if (off) return false;
-  using C = Dq2Cfg;
+template <int DD>
+static void launch_dq2_d(const void* q, const void* k, const void* v, const void* dout, const void* lse,
+                         const float* delta, void* dq, int B, int Sq, int H, int HKV, int causal, float softmax_scale,
+                         float scale_log2, const AttnStrides& st, const AttnVarlen& vl, hipStream_t s) {
+  using C = Dq2Cfg<DD>;
   dim3 grid((unsigned)((Sq + C::BQ - 1) / C::BQ * H * B));  // 1-D: xcd_block()
   if (causal)
-    hipLaunchKernelGGL(attn_bwd_dq2_kernel<true>, grid, dim3(64 * C::WAVES), 4 * C::TILE, s, (const bf16_t*)q,
+    hipLaunchKernelGGL((attn_bwd_dq2_kernel<DD, true>), grid, dim3(64 * C::WAVES), 4 * C::TILE, s, (const bf16_t*)q,
                        (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta, (bf16_t*)dq,
                        Sq, H, HKV, softmax_scale, scale_log2, st, vl);
   else
-    hipLaunchKernelGGL(attn_bwd_dq2_kernel<false>, grid, dim3(64 * C::WAVES), 4 * C::TILE, s, (const bf16_t*)q,
+    hipLaunchKernelGGL((attn_bwd_dq2_kernel<DD, false>), grid, dim3(64 * C::WAVES), 4 * C::TILE, s, (const bf16_t*)q,
                        (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, (const float*)lse, delta, (bf16_t*)dq,
                        Sq, H, HKV, softmax_scale, scale_log2, st, vl);
-  return true;
 }
 
-DW_PRELOAD(attn_bwd_dq2_kernel<true>);
-DW_PRELOAD(attn_bwd_dq2_kernel<false>);
+bool launch_dq2(const void* q, const void* k, const void* v, const void* dout, const void* lse, const float* delta,
+                void* dq, int B, int Sq, int H, int HKV, int D, int causal, float softmax_scale, float scale_log2,
+                const AttnStrides& st, const AttnVarlen& vl, hipStream_t s) {
+  // DWAMD_ATTN_DQ2: unset = D 128 only; 0 = never; 2 = D 64 and 128 (A/B)
+  static const int mode = [] {
+    const char* e = std::getenv("DWAMD_ATTN_DQ2");
+    return e ? std::atoi(e) : 1;
+  }();
+  if (mode == 0) return false;
+  if (D == 128) {
+    launch_dq2_d<128>(q, k, v, dout, lse, delta, dq, B, Sq, H, HKV, causal, softmax_scale, scale_log2, st, vl, s);
+    return true;
+  }
+  if (D == 64 && mode == 2) {
+    launch_dq2_d<64>(q, k, v, dout, lse, delta, dq, B, Sq, H, HKV, causal, softmax_scale, scale_log2, st, vl, s);
+    return true;
+  }
+  return false;
+}
+
+DW_PRELOAD((attn_bwd_dq2_kernel<128, true>));
+DW_PRELOAD((attn_bwd_dq2_kernel<128, false>));
+DW_PRELOAD((attn_bwd_dq2_kernel<64, true>));
+DW_PRELOAD((attn_bwd_dq2_kernel<64, false>));
