@@ -32,6 +32,12 @@
 #ifndef DWAMD_DQ_RI
 #define DWAMD_DQ_RI 1  // A/B: -DDWAMD_DQ_RI=0 builds the previous dQ form
 #endif
+#ifndef DWAMD_DKDV_W1
+// A/B: dK/dV at D = 128 with one wave per SIMD, V fragments in registers and
+// each S / dP chain's Q / dO fragments read ahead of its MFMAs (the 2-wave form
+// waits on an LDS read before every MFMA)
+#define DWAMD_DKDV_W1 0
+#endif
 #ifndef DWAMD_DQ_SPLIT
 #define DWAMD_DQ_SPLIT 1  // A/B: 0 keeps the D=64 mask a runtime branch inside one tile body
 #endif
@@ -90,7 +96,7 @@ struct DkvCfg {
 };
 
 template <int D, bool CAUSAL, bool PARTIAL, bool EXT>
-__global__ void __launch_bounds__(64 * DkvCfg<D>::WAVES, 2)
+__global__ void __launch_bounds__(64 * DkvCfg<D>::WAVES, (DWAMD_DKDV_W1 && D == 128 && !EXT) ? 1 : 2)
 attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
                      const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
                      bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, float* __restrict__ dKp,
@@ -129,7 +135,9 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
         kv < SK ? *(const u32x4*)(Vb + (int64_t)kv * st.v_rs + c * 8) : (u32x4){0, 0, 0, 0};
   }
   // D=64: this wave's V fragments (16 VGPRs) live in registers too
-  constexpr bool VREG = false;  // D=64 V fragments in registers measured 10 % slower (bwd 334 -> 300 TF/s)
+  // D=64 V fragments in registers measured 10 % slower (bwd 334 -> 300 TF/s)
+  constexpr bool W1 = DWAMD_DKDV_W1 && D == 128 && !EXT;
+  constexpr bool VREG = W1;
   u32x4 vr[VREG ? C::KK : 1];
   // K (only used for S here) prescaled by softmax_scale * log2(e)
   u32x4 kf[C::KK];
@@ -244,14 +252,31 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
             dp[4 * g + j] = d4[j];
           }
         }
+        if constexpr (W1) {
+          // every Q / dO fragment of the chain in flight before its MFMAs
+          u32x4 qa[C::KK], da[C::KK];
 #pragma unroll
-        for (int kk = 0; kk < C::KK; ++kk) {
-          const u32x4 qa = *(const u32x4*)(ql + rwl[kk & 1] + row_const<D>(32 * qs, kk));
-          const u32x4 da = *(const u32x4*)(dl + rwl[kk & 1] + row_const<D>(32 * qs, kk));
-          const u32x4 vb = VREG ? vr[VREG ? kk : 0]
-                                : *(const u32x4*)(v_img + rwl[kk & 1] + row_const<D>(32 * wid, kk));
-          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(qa), as_bf(kf[kk]), s, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(da), as_bf(vb), dp, 0, 0, 0);
+          for (int kk = 0; kk < C::KK; ++kk) {
+            qa[kk] = *(const u32x4*)(ql + rwl[kk & 1] + row_const<D>(32 * qs, kk));
+            da[kk] = *(const u32x4*)(dl + rwl[kk & 1] + row_const<D>(32 * qs, kk));
+          }
+#pragma unroll
+          for (int kk = 0; kk < C::KK; ++kk) {
+            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(qa[kk]), as_bf(kf[kk]), s, 0, 0, 0);
+            dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(da[kk]), as_bf(vr[VREG ? kk : 0]), dp, 0, 0, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x100, 2 * C::KK, 0);  // the DS reads first
+          __builtin_amdgcn_sched_group_barrier(0x008, 2 * C::KK, 0);  // then the MFMAs
+        } else {
+#pragma unroll
+          for (int kk = 0; kk < C::KK; ++kk) {
+            const u32x4 qa = *(const u32x4*)(ql + rwl[kk & 1] + row_const<D>(32 * qs, kk));
+            const u32x4 da = *(const u32x4*)(dl + rwl[kk & 1] + row_const<D>(32 * qs, kk));
+            const u32x4 vb = VREG ? vr[VREG ? kk : 0]
+                                  : *(const u32x4*)(v_img + rwl[kk & 1] + row_const<D>(32 * wid, kk));
+            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(qa), as_bf(kf[kk]), s, 0, 0, 0);
+            dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(da), as_bf(vb), dp, 0, 0, 0);
+          }
         }
         if (!EXT) {
           // P, then (diagonal / ragged tiles only) the mask, then dS: the
