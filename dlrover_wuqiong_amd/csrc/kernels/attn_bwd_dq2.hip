@@ -35,7 +35,20 @@
 #define DWAMD_DQ2_RI 0
 #endif
 
+#ifndef DWAMD_DQ2_AACC
+// dQ accumulators in the accumulator (AGPR) file through inline-asm MFMAs:
+// frees 128 arch VGPRs at D = 128 for the S / dP side.  hipcc pads nothing
+// inside asm: the packed dS operand is fresh from v_cvt_pk (VALU -> MFMA
+// operand: s_nop 1 in the string), and the accumulators are read only after
+// an s_nop pad that covers the last MFMA's 8-pass latency.
+#define DWAMD_DQ2_AACC 0
+#endif
+
 namespace {
+__device__ __forceinline__ void mfma_acc_agpr(f32x16& acc, const u32x4& a, const u32x4& b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
 template <int DD>
 struct Dq2Cfg {
   static constexpr int D = DD;
@@ -224,7 +237,10 @@ attn_bwd_dq2_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, 
               const u32x4 kt = tr_frag<D>(kl, 32 * sb + 16 * s2, 32 * dt, trl);
 #pragma unroll
               for (int g = 0; g < G; ++g)
-                acc[g][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(kt), as_bf(pf[g]), acc[g][dt], 0, 0, 0);
+                if constexpr (DWAMD_DQ2_AACC)
+                  mfma_acc_agpr(acc[g][dt], kt, pf[g]);
+                else
+                  acc[g][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(kt), as_bf(pf[g]), acc[g][dt], 0, 0, 0);
             }
           }
         }
@@ -236,6 +252,7 @@ attn_bwd_dq2_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, 
     }
     __syncthreads();  // tile t + 1 landed (vmcnt(0)), buffer t & 1 free
   }
+  if constexpr (DWAMD_DQ2_AACC) asm volatile("s_nop 15\n\ts_nop 3" ::: "memory");  // last MFMA's result lands
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const int q = q0 + 32 * g + r;
