@@ -109,8 +109,8 @@ def parse(argv=None):
                         "HBM snapshot (the kill then always lands mid-flush: HBM-only restore)")
     p.add_argument("--rehearse-shared-device", action="store_true",
                    help="N ranks share cuda:0 over gloo: rehearses the N>1 fault path on one GPU")
-    p.add_argument("--no-step-overlap", action="store_true",
-                   help="run the optimizer update on the compute stream instead of under the next forward")
+    p.add_argument("--step-overlap", action="store_true",
+                   help="run the optimizer update under the next forward (optimizers/overlap.py)")
     # worker-only
     p.add_argument("--run-dir", default="", help=argparse.SUPPRESS)
     p.add_argument("--phase", default="deep", choices=["deep", "import", "import_hbm"], help=argparse.SUPPRESS)
@@ -185,7 +185,7 @@ def _job(a, n: int, mode: str, run_dir: str, tag: str):
              "--phase", phase]
     if a.inject_slow_flush > 0 and mode == "deep":
         wargs += ["--inject-slow-flush", str(a.inject_slow_flush)]
-    for flag in ("no_fault", "no_persist", "act_ckpt", "no_step_overlap"):
+    for flag in ("no_fault", "no_persist", "act_ckpt", "step_overlap"):
         if getattr(a, flag):
             wargs.append("--" + flag.replace("_", "-"))
     cmd = [sys.executable, "-u", "-m", "dlrover_wuqiong_amd.trainer.run", "--nnodes", "1", "--nproc-per-node",
@@ -494,9 +494,13 @@ def worker(a) -> int:
         torch.cuda.synchronize()
     marks["flat"] = time.time()
     opt = FusedAdamW(flat, lr=a.lr, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0)
-    if cuda and not a.no_step_overlap:
+    if cuda and a.step_overlap:
         # the update runs under the next forward (optimizers/overlap.py); the
-        # timed region's closing device-wide synchronize includes all of it
+        # timed region's closing device-wide synchronize includes all of it.
+        # Off by default: +0.2 % on this step (114.83 -> 114.61 ms,
+        # profiles/r4/step_ab.jsonl) -- GEMM workgroups leave no room beside
+        # them -- and its side stream shares one of the 4 hardware queues
+        # with the checkpoint flush, so a forward could wait behind a D2H chunk
         opt.overlap_with_forward(model)
     B, S = a.micro_batch, a.seq
     if cuda:

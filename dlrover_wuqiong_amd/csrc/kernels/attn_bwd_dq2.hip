@@ -290,10 +290,15 @@ static void launch_dq2_d(const void* q, const void* k, const void* v, const void
 bool launch_dq2(const void* q, const void* k, const void* v, const void* dout, const void* lse, const float* delta,
                 void* dq, int B, int Sq, int H, int HKV, int D, int causal, float softmax_scale, float scale_log2,
                 const AttnStrides& st, const AttnVarlen& vl, hipStream_t s) {
-  // DWAMD_ATTN_DQ2: unset = D 128 only; 0 = never; 2 = D 64 and 128 (A/B)
+  // DWAMD_ATTN_DQ2: unset / 0 = never (the 8-wave kernel); 1 = D 128; 2 = D
+  // 64 and 128.  Opt-in: measured SLOWER than the 8-wave kernel -- GQA S=8192
+  // backward 659 vs 715 TF/s, S=4096 569 vs 632, GPT2 shape (D=64) 315 vs 347
+  // (profiles/r4/attn_dq2_ab.md): with one wave per SIMD the exp / multiply /
+  // pack VALU (7.9 VALU per MFMA after the compiler's AGPR copies) is no
+  // longer hidden behind a partner wave's MFMAs.
   static const int mode = [] {
     const char* e = std::getenv("DWAMD_ATTN_DQ2");
-    return e ? std::atoi(e) : 1;
+    return e ? std::atoi(e) : 0;
   }();
   if (mode == 0) return false;
   if (D == 128) {

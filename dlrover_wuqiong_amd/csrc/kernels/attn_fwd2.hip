@@ -249,7 +249,9 @@ attn_fwd2_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, con
 
 bool launch_fwd2(const void* q, const void* k, const void* v, void* o, void* lse, int B, int S, int H, int HKV,
                  int causal, float scale_log2, const AttnStrides& st, const AttnVarlen& vl, hipStream_t s) {
-  // opt-in until it beats the 8-wave kernel (DWAMD_ATTN_FWD2=1)
+  // opt-in (DWAMD_ATTN_FWD2=1): measured SLOWER than the 8-wave kernel, GQA
+  // S=8192 forward 636 vs 979 TF/s (profiles/r4/attn_dq2_ab.md): the branchy
+  // per-group rescale makes the allocator shuttle O between AGPRs and VGPRs
   static const bool off = [] {
     const char* e = std::getenv("DWAMD_ATTN_FWD2");
     return !(e && e[0] == '1');

@@ -500,6 +500,10 @@ class ElasticTrainingAgent:
         stats = ResourceMonitor.gpu_stats(pdevs)
         need = getattr(self, "_worker_vram", 0)
         if need > 0:
+            # the replacement is the standby: what it already holds in its
+            # allocator cache (standby_warm marker = bytes reserved after the
+            # warm-profile replay) it does not allocate again
+            need = max(0, need - self._standby_reserved())
             need_mb = (need >> 20) + int(float(os.getenv("DWAMD_OVERLAP_TEARDOWN_MARGIN_GB", "8")) * 1024)
             ok = bool(stats) and all(g.total_memory_mb - g.used_memory_mb >= need_mb for g in stats)
             rule = f"free >= {need_mb / 1024:.1f} GiB"
@@ -510,6 +514,24 @@ class ElasticTrainingAgent:
         logger.info(f"teardown overlap {'on' if ok else 'off'} ({rule}): GPUs {sorted(pdevs) if pdevs else 'all'} "
                     f"free GiB {[round((g.total_memory_mb - g.used_memory_mb) / 1024, 1) for g in stats]}")
         return ok
+
+    def _standby_reserved(self) -> int:
+        """Smallest HBM reservation among this node's waiting standbys (0 if
+        any has not reported one): standby.py writes it into its
+        ``standby_warm.<local rank>`` marker once the warm profile ran."""
+        from .standby import WARM_PREFIX
+
+        standby = getattr(self, "_standby", None)
+        if not standby:
+            return 0
+        vals = []
+        for lr in standby:
+            try:
+                with open(os.path.join(self.ctl_dir, WARM_PREFIX + str(lr))) as f:
+                    vals.append(max(0, int(f.read().strip() or 0)))
+            except (OSError, ValueError):
+                return 0
+        return min(vals) if vals else 0
 
     def _stop_workers(self, timeout: Optional[float] = None, wait: bool = True):
         """SIGTERM every live worker group, SIGKILL after ``timeout``.

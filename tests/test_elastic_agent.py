@@ -141,6 +141,14 @@ def test_teardown_overlap_decision(monkeypatch, tmp_path):
     assert agent._teardown_overlap_ok()  # 350 MB free >= 300
     monkeypatch.setattr(monitor.ResourceMonitor, "gpu_stats", staticmethod(stats(750)))
     assert not agent._teardown_overlap_ok()  # 250 MB free
+    # ... unless the standby that replaces the worker already holds part of it
+    agent.ctl_dir = str(tmp_path)
+    agent._standby = {0: None}
+    (tmp_path / "standby_warm.0").write_text(f"{100 << 20}\n")
+    assert agent._teardown_overlap_ok()  # needs 300 - 100 = 200 MB <= 250 free
+    (tmp_path / "standby_warm.0").write_text("-1\n")  # reservation skipped
+    assert not agent._teardown_overlap_ok()
+    agent._standby = {}
     del agent._worker_vram
     # fdinfo parsing: drm-pdev lines of a process's open DRM fds
     fd = tmp_path / "fdinfo"
