@@ -463,9 +463,15 @@ def worker(a) -> int:
     from dlrover_wuqiong_amd.parallel.ddp import FlatDDP
     from dlrover_wuqiong_amd.parallel.flat import FlatParams
 
+    from dlrover_wuqiong_amd.flash_checkpoint.deferred_init import deferred_init
+
     dtype = torch.bfloat16 if cuda else torch.float32
     marks = {"imports": time.time()}  # model-build phases (import-mode restarts build the model cold)
     torch.manual_seed(1234)
+    # a restarted process restores every parameter: its random init is only
+    # recorded (replayed if nothing was restored)
+    defer = deferred_init()
+    di = defer.__enter__()
     if a.model.startswith("llama") or a.model.startswith("mixtral"):
         from dlrover_wuqiong_amd.models.llama import Llama, LlamaConfig
 
@@ -484,6 +490,7 @@ def worker(a) -> int:
             model = GPT2(cfg)
         desc = ("GPT2-1.5B (gpt2-xl: 48L, 1600H, 25 heads)" if a.model == "gpt2-1.5b" else
                 f"{a.model} ({cfg.n_layer}L, {cfg.n_embd}H, {cfg.n_head} heads)")
+    defer.__exit__(None, None, None)
     if cuda:
         torch.cuda.synchronize()
     marks["init"] = time.time()
@@ -832,6 +839,10 @@ def worker(a) -> int:
         restore_sec = mx(time.perf_counter() - t0)
         step = int(restored.get("step", 0)) if restored else 0
         restore_ok = bool(restored) and step > 0
+        if restore_ok:
+            di.discard()
+        else:
+            di.replay()  # nothing restored: the parameters still need their init
         # bit-exact check against the sums incarnation 0 logged right after
         # that save (the last one before the kill)
         want = [e for e in _read_jsonl(step_log) if e["event"] == "saved_sums" and e["rank"] == rank
