@@ -345,17 +345,17 @@ __global__ void __launch_bounds__(256) norm_bwd_fused_kernel(
   if (threadIdx.x == 0) __hip_atomic_exchange(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Norm backward for SMALL H (<= 2048, VPL <= 4), one pass over dy / x:
-// every wave takes RPW rows (all their loads issued before any math, so a
-// wave has 2 rows of HBM latency in flight), writes dx like norm_dx_kernel,
-// and keeps per-lane dgamma / dbeta sums; the block's 4 waves combine them
-// in LDS and store ONE fp32 partial row [2H] per block -- plain stores, no
-// atomics (the atomic-combined fused kernel above, 512 blocks of 4-row
-// waves, was latency-bound at H = 1600: 2048 waves for 8192 rows).  The
-// [blocks, 2H] partials are summed by colsum_f32_kernel.
+// Norm backward for SMALL H (< 2048, VPL <= 4), one pass over dy / x (/ dres):
+// every wave strides over rows (grid = the resident workgroups), loading the
+// next row before computing the current one, writes dx like norm_dx_kernel
+// and keeps per-lane dgamma / dbeta sums; at the end the block's 4 waves
+// combine them in LDS and store ONE fp32 partial row per block -- plain
+// stores, no atomics (the atomic-combined fused kernel above, 512 blocks of
+// 4-row waves, was latency-bound at H = 1600).  The [blocks, 2H] partials
+// are summed by colsum_f32_kernel.
 // DS: also the column sums of dx itself (the bias gradient of the Linear
 // whose output is this add-norm's residual input): partial rows [3H].
-template <int VPL, bool RMS, int RPW, bool DS = false>
+template <int VPL, bool RMS, bool DS = false>
 __global__ void __launch_bounds__(256) norm_bwd_part_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ gamma,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const bf16_t* __restrict__ dres,
@@ -364,53 +364,56 @@ __global__ void __launch_bounds__(256) norm_bwd_part_kernel(
   __shared__ float red[2][4][512 + 4];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nv = H >> 3;
-  const int64_t row0 = ((int64_t)blockIdx.x * 4 + wid) * RPW;
   float ag[VPL][8], ab[VPL][8], ad[VPL][8];
 #pragma unroll
   for (int j = 0; j < VPL; ++j)
 #pragma unroll
     for (int k = 0; k < 8; ++k) ag[j][k] = ab[j][k] = ad[j][k] = 0.f;
-  u32x4 xv[RPW][VPL], dv[RPW][VPL], gv[VPL];
+  u32x4 gv[VPL];
 #pragma unroll
   for (int j = 0; j < VPL; ++j) {
     const int c = lane + 64 * j;
     if (c < nv) gv[j] = *(const u32x4*)(gamma + c * 8);
   }
-#pragma unroll
-  for (int u = 0; u < RPW; ++u)
+  // grid-stride over rows, one row per wave per step, the next row's x / dy
+  // / dres (and mean / rstd) loaded before the current one is computed: two
+  // named register sets, the loop unrolled by two so nothing is copied
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  struct Row {
+    u32x4 x[VPL], d[VPL], r[VPL];
+    float mu, rs;
+  };
+  auto load = [&](Row& b, int64_t row) {
+    if (row >= rows) return;
 #pragma unroll
     for (int j = 0; j < VPL; ++j) {
       const int c = lane + 64 * j;
-      if (c < nv && row0 + u < rows) {
-        xv[u][j] = *(const u32x4*)(x + (row0 + u) * H + c * 8);
-        dv[u][j] = *(const u32x4*)(dy + (row0 + u) * H + c * 8);
+      if (c < nv) {
+        b.x[j] = *(const u32x4*)(x + row * H + c * 8);
+        b.d[j] = *(const u32x4*)(dy + row * H + c * 8);
+        if (dres) b.r[j] = *(const u32x4*)(dres + row * H + c * 8);
       }
     }
-#pragma unroll
-  for (int u = 0; u < RPW; ++u) {
-    const int64_t row = row0 + u;
-    if (row >= rows) break;  // wave-uniform
-    const float mu = RMS ? 0.f : mean_in[row];
-    const float rstd = rstd_in[row];
-    float xh[VPL][8], g[VPL][8];
+    b.mu = RMS ? 0.f : mean_in[row];
+    b.rs = rstd_in[row];
+  };
+  auto process = [&](const Row& b, int64_t row) {
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < VPL; ++j) {
       const int c = lane + 64 * j;
       if (c < nv) {
         float xf[8], df[8], gm[8];
-        unpack8(xv[u][j], xf);
-        unpack8(dv[u][j], df);
+        unpack8(b.x[j], xf);
+        unpack8(b.d[j], df);
         unpack8(gv[j], gm);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const float a = (xf[k] - mu) * rstd, b = df[k] * gm[k];
-          xh[j][k] = a;
-          g[j][k] = b;
+          const float a = (xf[k] - b.mu) * b.rs, g = df[k] * gm[k];
           ag[j][k] += df[k] * a;
           if constexpr (!RMS) ab[j][k] += df[k];
-          s1 += b;
-          s2 += b * a;
+          s1 += g;
+          s2 += g * a;
         }
       }
     }
@@ -420,12 +423,15 @@ __global__ void __launch_bounds__(256) norm_bwd_part_kernel(
     for (int j = 0; j < VPL; ++j) {
       const int c = lane + 64 * j;
       if (c < nv) {
-        float o[8];
+        float xf[8], df[8], gm[8], o[8];
+        unpack8(b.x[j], xf);  // recomputed: cheaper than 64 more live registers
+        unpack8(b.d[j], df);
+        unpack8(gv[j], gm);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = rstd * (g[j][k] - m1 - xh[j][k] * m2);
+        for (int k = 0; k < 8; ++k) o[k] = b.rs * (df[k] * gm[k] - m1 - (xf[k] - b.mu) * b.rs * m2);
         if (dres) {
           float r[8];
-          unpack8(*(const u32x4*)(dres + row * H + c * 8), r);
+          unpack8(b.r[j], r);
 #pragma unroll
           for (int k = 0; k < 8; ++k) o[k] += r[k];
         }
@@ -436,6 +442,18 @@ __global__ void __launch_bounds__(256) norm_bwd_part_kernel(
         *(u32x4*)(dx + row * H + c * 8) = pack8(o);
       }
     }
+  };
+  Row A, B;
+  int64_t row = (int64_t)blockIdx.x * 4 + wid;
+  load(A, row);
+  while (row < rows) {
+    load(B, row + stride);
+    process(A, row);
+    row += stride;
+    if (row >= rows) break;
+    load(A, row + stride);
+    process(B, row);
+    row += stride;
   }
   float* prow = part + (int64_t)blockIdx.x * (DS ? 3 : 2) * H;
 #pragma unroll
@@ -643,8 +661,9 @@ extern "C" int dw_norm_bwd3(const void* dy, const void* x, const void* gamma, co
                             const void* dres, void* dx, void* dgamma, void* dbeta, void* ws, void* part,
                             int64_t part_floats, int64_t rows, int H, int rms, int out_fp32, int accumulate,
                             void* dsum, int* dsum_done, void* stream) {
-  constexpr int RPW = 2;
-  const int64_t nb = (rows + 4 * RPW - 1) / (4 * RPW);
+  // every workgroup resident at once, each wave striding over rows: H > 1024
+  // (VPL 4) needs ~310-370 VGPRs, one workgroup per CU; smaller H two
+  const int64_t nb = std::min<int64_t>((rows + 3) / 4, H > 1024 ? 256 : 512);
   const int pw = dsum ? 3 : 2;
   if (dsum_done) *dsum_done = 0;
   static const bool off = getenv_flag("DWAMD_NORM_BWD_PART_OFF");  // A/B switch
@@ -653,7 +672,7 @@ extern "C" int dw_norm_bwd3(const void* dy, const void* x, const void* gamma, co
                         stream);
   hipStream_t s = (hipStream_t)stream;
 #define NBP(RM, DSV)                                                                                          \
-  hipLaunchKernelGGL((norm_bwd_part_kernel<VPL, RM, RPW, DSV>), dim3((unsigned)nb), dim3(256), 0, s,         \
+  hipLaunchKernelGGL((norm_bwd_part_kernel<VPL, RM, DSV>), dim3((unsigned)nb), dim3(256), 0, s,              \
                      (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)gamma, RM ? nullptr : (const float*)mean, \
                      (const float*)rstd, (const bf16_t*)dres, (bf16_t*)dx, (float*)part, rows, H)
   DISPATCH_VPL2(H, {

@@ -64,7 +64,7 @@ def _norm_backward(ctx, dy, dres):
     if dsum is not None and dsum.dtype != dgamma.dtype:
         dsum = None
     # small H: one-pass kernel writes per-block fp32 dgamma/dbeta (/dsum) partials here
-    nparts = (R + 7) // 8 * (3 if dsum is not None else 2) * H if H < 2048 else 0
+    nparts = min(512, (R + 3) // 4) * (3 if dsum is not None else 2) * H if H < 2048 else 0
     part = torch.empty(nparts, device=x2.device, dtype=torch.float32) if nparts else None
     done = ctypes.c_int(0)
     _hip.check(_hip.lib().dw_norm_bwd3(_hip.ptr(dy2), _hip.ptr(x2), _hip.ptr(weight), _hip.ptr(mean),
