@@ -283,8 +283,8 @@ def _apply_warm_profile(ctl: str, lr: str) -> Optional[dict]:
     try:
         warm_profile.preload_kernel_library()
         r = warm_profile.replay(prof)
-        print(f"[standby] warm profile replayed: {r['gemms']} GEMMs ({r['failed']} failed) in {r['sec']} s",
-              file=sys.stderr)
+        print(f"[standby] warm profile replayed: {r['gemms']} GEMMs, {r.get('ops', 0)} other ops "
+              f"({r['failed']} failed) in {r['sec']} s", file=sys.stderr)
     except Exception as e:  # never fatal
         print(f"[standby] warm profile replay failed: {e}", file=sys.stderr)
     return prof

@@ -78,6 +78,23 @@ def _enc(x, device_type: str = "cuda"):
     return None  # not replayable
 
 
+# Non-GEMM aten ops are recorded too (their kernels' code objects load at the
+# first launch) -- except ops whose replay on scratch data could do harm or
+# is pointless: random number generation, host syncs, pure views /
+# metadata, collectives (other namespaces are never recorded).
+_SKIP_WORDS = ("rand", "normal", "uniform", "bernoulli", "dropout", "exponential", "multinomial", "random",
+               "_local_scalar_dense", "nonzero", "unique", "masked_select", "item", "resize", "set_",
+               "record_stream", "_foreach")
+_VIEW_OPS = {"view", "_unsafe_view", "as_strided", "t", "transpose", "permute", "expand", "slice", "select",
+             "unsqueeze", "squeeze", "reshape", "alias", "detach", "unbind", "split", "split_with_sizes",
+             "chunk", "narrow", "lift_fresh", "view_as_real", "view_as_complex", "_reshape_alias",
+             "empty", "empty_like", "empty_strided", "new_empty", "new_empty_strided", "is_same_size"}
+
+
+def _warm_op(name: str) -> bool:
+    return name not in _VIEW_OPS and not any(w in name for w in _SKIP_WORDS)
+
+
 def _make_recorder(device_type: str = "cuda"):
     import torch
     from torch.utils._python_dispatch import TorchDispatchMode
@@ -90,19 +107,27 @@ def _make_recorder(device_type: str = "cuda"):
         def __init__(self):
             super().__init__()
             self.seen: Dict[str, dict] = {}
+            self.other: Dict[str, dict] = {}
             self.calls = 0
 
         def __torch_dispatch__(self, func, types, args=(), kwargs=None):
             kwargs = kwargs or {}
             name = ops.get(func)
+            gemm = name is not None
+            if name is None and getattr(func, "namespace", "") == "aten":
+                pk = func._overloadpacket.__name__
+                name = (pk, func._overloadname) if _warm_op(pk) else None
             if name is not None and name[1] != "out":
-                self.calls += 1
+                self.calls += gemm
                 ea = [_enc(a, device_type) for a in args]
                 ek = {k: _enc(v, device_type) for k, v in kwargs.items()}
-                if all(e is not None for e in ea) and all(e is not None for e in ek.values()):
+                # at least one device tensor (a kernel runs), everything encodable
+                dev = any(isinstance(e, dict) and "t" in e for e in ea + list(ek.values()))
+                if dev and all(e is not None for e in ea) and all(e is not None for e in ek.values()):
                     key = json.dumps([name, ea, ek], sort_keys=True)
-                    if key not in self.seen:
-                        self.seen[key] = {"op": name[0], "ov": name[1], "args": ea, "kwargs": ek}
+                    table = self.seen if gemm else self.other
+                    if key not in table:
+                        table[key] = {"op": name[0], "ov": name[1], "args": ea, "kwargs": ek}
             return func(*args, **kwargs)
 
     return GemmRecorder()
@@ -115,7 +140,7 @@ def _write(rec, t0: float):
     lr = os.environ.get("LOCAL_RANK", "0")
     dev = torch.cuda.current_device()
     prof = {"version": _VERSION, "pid": os.getpid(), "device": dev, "recorded_s": round(time.time() - t0, 3),
-            "gemm_calls": rec.calls, "gemms": list(rec.seen.values()),
+            "gemm_calls": rec.calls, "gemms": list(rec.seen.values()), "ops": list(rec.other.values()),
             "max_reserved": int(torch.cuda.max_memory_reserved(dev)),
             "reserved": int(torch.cuda.memory_reserved(dev)),
             "max_allocated": int(torch.cuda.max_memory_allocated(dev))}
@@ -200,14 +225,26 @@ def _dec(e, device):
 
 
 def replay(prof: dict, device=None, repeats: int = 2) -> dict:
-    """Run every recorded GEMM ``repeats`` times on scratch tensors (loads
-    the GEMM library's heuristics and kernel code objects in this process).
-    Returns ``{"gemms": n, "failed": k, "sec": s}``."""
+    """Run every recorded GEMM ``repeats`` times, and every other recorded
+    op once, on scratch tensors (floats random, integers zero -- so index
+    operands stay in range): loads the GEMM library's heuristics and the
+    kernels' code objects in this process.
+    Returns ``{"gemms": n, "ops": m, "failed": k, "sec": s}``."""
     import torch
 
     device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
     t0 = time.perf_counter()
-    n = failed = 0
+    n = failed = m = 0
+    for g in prof.get("ops", []):
+        try:
+            op = getattr(getattr(torch.ops.aten, g["op"]), g.get("ov", "default"))
+            args = [_dec(a, device) for a in g["args"]]
+            kwargs = {k: _dec(v, device) for k, v in g["kwargs"].items()}
+            op(*args, **kwargs)
+            m += 1
+            del args, kwargs
+        except Exception:
+            failed += 1
     for g in prof.get("gemms", []):
         try:
             op = getattr(getattr(torch.ops.aten, g["op"]), g.get("ov", "default"))
@@ -225,7 +262,7 @@ def replay(prof: dict, device=None, repeats: int = 2) -> dict:
             failed += 1
     if torch.device(device).type == "cuda":
         torch.cuda.synchronize(device)
-    return {"gemms": n, "failed": failed, "sec": round(time.perf_counter() - t0, 3)}
+    return {"gemms": n, "ops": m, "failed": failed, "sec": round(time.perf_counter() - t0, 3)}
 
 
 def preload_kernel_library() -> float:
