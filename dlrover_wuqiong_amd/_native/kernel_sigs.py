@@ -14,6 +14,7 @@ SIGS = {
     "dw_multi_copy": (i32, [vp, i64, vp]),
     "dw_gemm_dgelu": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),
     "dw_gemm_dgelu_bgrad": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, vp]),
+    "dw_gemm_wgrad_bgradb": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, vp]),
     "dw_multi_copy_grid": (i32, [vp, i64, i32, vp]),
     "dw_multi_copy_variant": (i32, [vp, i64, i32, i32, vp]),
     "dw_fill_u32": (i32, [vp, i64, u32, vp]),

@@ -4,6 +4,7 @@
 //  * dw_gemm_dgelu_bgrad     dh = (dy W2) * gelu'(pre), db = sum_rows dh
 //      (HIPBLASLT_EPILOGUE_DGELU_BGRAD on the c_proj dgrad GEMM)
 //  * dw_gemm_dgelu           dh = (dy W2) * gelu'(pre)   (HIPBLASLT_EPILOGUE_DGELU)
+//  * dw_gemm_wgrad_bgradb    dW (+)= dy^T x, db = sum_rows dy  (HIPBLASLT_EPILOGUE_BGRADB)
 //
 // Probed on gfx950 / ROCm 7.2 (scripts/probe/epi_probe.cpp,
 // profiles/r2/hipblaslt_epilogue_probe.txt): GELU_AUX(_BIAS) has no bf16
@@ -68,10 +69,10 @@ struct Plan {
     if ((x) != HIPBLAS_STATUS_SUCCESS) return -1; \
   } while (0)
 
-// D[m, n] (col-major, ld m) = op(A) op(B) with the given epilogue
+// D[m, n] (col-major, ld m) = op(A) op(B) (+ D when beta = 1) with the given epilogue
 int run(int kind, hipblasOperation_t ta, hipblasOperation_t tb, int m, int n, int k, const void* A, int lda,
         const void* B, int ldb, void* D, hipblasLtEpilogue_t epi, const void* bias, hipDataType bias_type,
-        const void* aux, int64_t aux_ld, hipStream_t stream) {
+        const void* aux, int64_t aux_ld, hipStream_t stream, float beta = 0.f) {
   std::lock_guard<std::mutex> lk(g_mu);
   Dev* dv = dev_state();
   if (!dv) return -1;
@@ -114,7 +115,7 @@ int run(int kind, hipblasOperation_t ta, hipblasOperation_t tb, int m, int n, in
     it = g_algo.emplace(key, std::make_pair(true, res[0].algo)).first;
   }
   if (!it->second.first) return DW_EPI_UNSUPPORTED;
-  const float alpha = 1.f, beta = 0.f;
+  const float alpha = 1.f;
   CK(hipblasLtMatmul(dv->h, p.op, &alpha, A, p.a, B, p.b, &beta, D, p.c, D, p.c, &it->second.second, dv->ws,
                      dv->ws_bytes, stream));
   return 0;
@@ -135,4 +136,17 @@ extern "C" int dw_gemm_dgelu(const void* dy, const void* w2, const void* pre, vo
                              void* stream) {
   return run(2, HIPBLAS_OP_N, HIPBLAS_OP_N, N1, M, N2, w2, N1, dy, N2, dh, HIPBLASLT_EPILOGUE_DGELU, nullptr,
              HIP_R_16BF, pre, N1, (hipStream_t)stream);
+}
+
+// Weight gradient of a Linear with its bias gradient in the epilogue:
+// dW [N, K] (+)= dy^T x, db [N] fp32 = sum over the M rows of dy
+// (HIPBLASLT_EPILOGUE_BGRADB: the reduction of B over the GEMM's k).  In the
+// library's column-major view dW^T [K, N] = x^T [K, M] . (dy^T [N, M])^T, i.e.
+// transA = N, transB = T -- the one combination the gfx950 probe finds
+// algorithms for (profiles/r4/hipblaslt_bgrad_probe.txt).  accumulate: beta 1
+// on dW (direct flat-gradient storage); db is always written.
+extern "C" int dw_gemm_wgrad_bgradb(const void* x, const void* dy, void* dw, void* db, int M, int K, int N,
+                                    int accumulate, void* stream) {
+  return run(3, HIPBLAS_OP_N, HIPBLAS_OP_T, K, N, M, x, K, dy, N, dw, HIPBLASLT_EPILOGUE_BGRADB, db, HIP_R_32F,
+             nullptr, 0, (hipStream_t)stream, accumulate ? 1.f : 0.f);
 }

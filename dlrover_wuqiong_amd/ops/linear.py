@@ -25,6 +25,12 @@ from ._grad import direct_grad, notify
 # rather than filling each other's tail waves).
 _WGRAD_STREAM = os.environ.get("DWAMD_WGRAD_STREAM", "0") == "1"
 _SIDE = {}
+# The bias gradient as the wgrad GEMM's hipBLASLt BGRADB epilogue (one pass
+# over dY fewer); per shape it falls back to the column-sum kernel when the
+# library has no algorithm.  DWAMD_WGRAD_BGRAD=0 disables it.
+_WGRAD_BGRAD = os.environ.get("DWAMD_WGRAD_BGRAD", "1") == "1"
+_EPI_UNSUPPORTED = -100
+_BGRAD_OFF = set()  # (M, K, N) without an algorithm
 
 
 def _side_stream(device) -> torch.cuda.Stream:
@@ -59,6 +65,21 @@ class _LinearFn(torch.autograd.Function):
             return _backward_two_streams(ctx, dy2, x2, w, x.shape, gw, gb, N)
         dx = (dy2 @ w).view(x.shape) if ctx.needs_input_grad[0] else None
         dw = db = None
+        if (_WGRAD_BGRAD and gw is not None and gb is not None and ctx.needs_input_grad[1] and ctx.needs_input_grad[2]
+                and _hip.use_hip(dy2) and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
+                and gw.dtype == torch.bfloat16 and dy2.is_contiguous() and x2.is_contiguous()
+                and (dy2.shape[0], K, N) not in _BGRAD_OFF):
+            db32 = torch.empty(N, device=dy2.device, dtype=torch.float32)
+            rc = _hip.lib().dw_gemm_wgrad_bgradb(_hip.ptr(x2), _hip.ptr(dy2), _hip.ptr(gw), _hip.ptr(db32),
+                                                 dy2.shape[0], K, N, 1, _hip.stream())
+            if rc == _EPI_UNSUPPORTED:
+                _BGRAD_OFF.add((dy2.shape[0], K, N))
+            else:
+                _hip.check(rc, "gemm_wgrad_bgradb")
+                gb.add_(db32)
+                notify(ctx.weight_param)
+                notify(b)
+                return dx, None, None
         if ctx.needs_input_grad[1]:
             if gw is not None:
                 gw.addmm_(dy2.t(), x2)
