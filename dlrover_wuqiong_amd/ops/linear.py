@@ -27,8 +27,11 @@ _WGRAD_STREAM = os.environ.get("DWAMD_WGRAD_STREAM", "0") == "1"
 _SIDE = {}
 # The bias gradient as the wgrad GEMM's hipBLASLt BGRADB epilogue (one pass
 # over dY fewer); per shape it falls back to the column-sum kernel when the
-# library has no algorithm.  DWAMD_WGRAD_BGRAD=0 disables it.
-_WGRAD_BGRAD = os.environ.get("DWAMD_WGRAD_BGRAD", "1") == "1"
+# library has no algorithm.  Opt-in (DWAMD_WGRAD_BGRAD=1): on gfx950 / ROCm
+# 7.2 the only BGRADB solutions are 32x32-tile kernels -- GPT2-1.5B's qkv
+# wgrad 1013 us vs ~100 us plain + 19 us column sum, step 159 vs 116 ms
+# (profiles/r4/wgrad_bgradb_ab.md)
+_WGRAD_BGRAD = os.environ.get("DWAMD_WGRAD_BGRAD", "0") == "1"
 _EPI_UNSUPPORTED = -100
 _BGRAD_OFF = set()  # (M, K, N) without an algorithm
 

@@ -23,6 +23,8 @@ def test_wgrad_bgradb_matches_fp32(M, K, N):
     from dlrover_wuqiong_amd.ops import linear as L
     from dlrover_wuqiong_amd.parallel.flat import FlatParams
 
+    L._WGRAD_BGRAD = True  # opt-in path (slow on ROCm 7.2, still exact)
+
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     m = nn.Module()
@@ -41,3 +43,4 @@ def test_wgrad_bgradb_matches_fp32(M, K, N):
     rel = lambda a, b: ((a.float() - b).norm() / b.norm()).item()  # noqa: E731
     assert rel(m.fc.weight.grad, ref_w.grad) < 2e-2
     assert rel(m.fc.bias.grad, ref_b.grad) < 2e-2
+    L._WGRAD_BGRAD = False
