@@ -181,14 +181,23 @@ class LayerNorm(nn.Module):
         self.weight = nn.Parameter(torch.ones(hidden, device=device, dtype=dtype))
         self.bias = nn.Parameter(torch.zeros(hidden, device=device, dtype=dtype)) if bias else None
 
-    def forward(self, x):
+    def forward(self, x, res=None):
+        """norm(x); with ``res``: (norm(x + res), x + res), the residual add
+        fused in (``add_forward``)."""
+        if res is not None:
+            return self._add_forward(x, res)
         if self.bias is None and _hip.bf16_path(x):
             w = _hip.bf16(self.weight)
             return _NormFn.apply(_hip.bf16(x), w, torch.zeros_like(w), self.eps, False)
         return layer_norm(x, self.weight, self.bias, self.eps)
 
     def add_forward(self, x, res):
-        """(norm(x + res), x + res) with the residual add fused in."""
+        """(norm(x + res), x + res) with the residual add fused in.  Goes
+        through ``__call__`` so module hooks see the parameter use (e.g. the
+        overlapped optimizer update's per-module waits)."""
+        return self(x, res)
+
+    def _add_forward(self, x, res):
         if self.bias is None and _hip.bf16_path(x):
             w = _hip.bf16(self.weight)
             x, res = _hip.bf16(x, res)
@@ -202,11 +211,13 @@ class RMSNorm(nn.Module):
         self.eps = eps
         self.weight = nn.Parameter(torch.ones(hidden, device=device, dtype=dtype))
 
-    def forward(self, x):
+    def forward(self, x, res=None):
+        if res is not None:
+            return add_rms_norm(x, res, self.weight, self.eps)
         return rms_norm(x, self.weight, self.eps)
 
     def add_forward(self, x, res):
-        return add_rms_norm(x, res, self.weight, self.eps)
+        return self(x, res)  # through __call__: module hooks see the parameter use
 
 
 AtorchLayerNorm = LayerNorm  # reference-compatible name

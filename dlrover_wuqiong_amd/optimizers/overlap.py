@@ -14,7 +14,9 @@ GEMM-bound and touches the parameters layer by layer, so the update can run
 * a forward pre-hook on every module that owns parameters makes the compute
   stream wait for the event of the last piece holding them -- layer 0 starts
   once its own parameters are updated, while the side stream keeps streaming
-  the rest;
+  the rest.  A module's parameters must be read inside its own ``__call__``
+  (this package's norms route ``add_forward`` through it); a parameter read
+  elsewhere is only ordered by the final join;
 * ``zero_grad`` during a pending update is enqueued on the side stream after
   the last piece (the update still reads the gradients);
 * the top-level forward's post-hook joins the side stream, so the backward
