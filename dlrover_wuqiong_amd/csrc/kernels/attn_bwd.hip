@@ -38,6 +38,11 @@
 // waits on an LDS read before every MFMA)
 #define DWAMD_DKDV_W1 0
 #endif
+#ifndef DWAMD_DKDV64_W3
+// A/B: dK/dV at D = 64 capped at 168 VGPRs -- three workgroups (12 waves)
+// per CU instead of two (the kernel waits 47 % of its wave cycles, PMC)
+#define DWAMD_DKDV64_W3 0
+#endif
 #ifndef DWAMD_DQ_SPLIT
 #define DWAMD_DQ_SPLIT 1  // A/B: 0 keeps the D=64 mask a runtime branch inside one tile body
 #endif
@@ -96,7 +101,8 @@ struct DkvCfg {
 };
 
 template <int D, bool CAUSAL, bool PARTIAL, bool EXT>
-__global__ void __launch_bounds__(64 * DkvCfg<D>::WAVES, (DWAMD_DKDV_W1 && D == 128 && !EXT) ? 1 : 2)
+__global__ void __launch_bounds__(64 * DkvCfg<D>::WAVES,
+                                  (DWAMD_DKDV_W1 && D == 128 && !EXT) ? 1 : ((DWAMD_DKDV64_W3 && D == 64 && !EXT) ? 3 : 2))
 attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
                      const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
                      bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, float* __restrict__ dKp,
