@@ -39,9 +39,11 @@
 #define DWAMD_DKDV_W1 0
 #endif
 #ifndef DWAMD_DKDV64_W3
-// A/B: dK/dV at D = 64 capped at 168 VGPRs -- three workgroups (12 waves)
-// per CU instead of two (the kernel waits 47 % of its wave cycles, PMC)
-#define DWAMD_DKDV64_W3 0
+// dK/dV at D = 64 capped at 168 VGPRs -- three workgroups (12 waves) per CU
+// instead of two (the 2-workgroup form waits 47 % of its wave cycles, PMC):
+// GPT2 shape backward 323 -> 334 TF/s packed, 354 -> 371 unpacked
+// (profiles/r4/attn_dkdv64_w3_ab.jsonl).  -DDWAMD_DKDV64_W3=0: the 2-wave form
+#define DWAMD_DKDV64_W3 1
 #endif
 #ifndef DWAMD_DQ_SPLIT
 #define DWAMD_DQ_SPLIT 1  // A/B: 0 keeps the D=64 mask a runtime branch inside one tile body

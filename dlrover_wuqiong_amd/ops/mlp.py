@@ -81,6 +81,7 @@ class _FusedMLPFn(torch.autograd.Function):
         key = (M, N1, N2)
         dh = torch.empty(M, N1, device=dy.device, dtype=x2.dtype)
         db1_f = None
+        db1_done = False
         mode = _BWD_MODE.get(key, _BWD_DEFAULT)
         if mode == "bgrad":
             db1_f = torch.empty(N1, device=dy.device, dtype=torch.float32)
@@ -101,14 +102,28 @@ class _FusedMLPFn(torch.autograd.Function):
         if mode == "unfused":
             # dgrad GEMM, then ONE pass: dh = dg * gelu'(pre) and db1 = colsum(dh)
             dg = (dy2 @ w2).contiguous()
-            db1_f = torch.empty(N1, device=dy.device, dtype=torch.float32)
             ws = _hip.zeroed_workspace(N1 + (N1 + 511) // 512, dy.device)
-            _hip.check(_hip.lib().dw_gelu_bwd_dbias(_hip.ptr(dg), _hip.ptr(pre), _hip.ptr(dh), M, N1, _hip.ptr(ws),
-                                                    _hip.ptr(db1_f), 1, 0, _hip.stream()), "gelu_bwd_dbias")
+            gb1 = direct_grad(p_b1)
+            if gb1 is not None and gb1.dtype in (torch.bfloat16, torch.float32):
+                # the finish kernel adds db1 into the flat gradient itself (no
+                # fp32 temporary + cast + add_ launches)
+                _hip.check(_hip.lib().dw_gelu_bwd_dbias(_hip.ptr(dg), _hip.ptr(pre), _hip.ptr(dh), M, N1,
+                                                        _hip.ptr(ws), _hip.ptr(gb1),
+                                                        int(gb1.dtype == torch.float32), 1, _hip.stream()),
+                           "gelu_bwd_dbias")
+                notify(p_b1)
+                db1_done = True
+            else:
+                db1_f = torch.empty(N1, device=dy.device, dtype=torch.float32)
+                _hip.check(_hip.lib().dw_gelu_bwd_dbias(_hip.ptr(dg), _hip.ptr(pre), _hip.ptr(dh), M, N1,
+                                                        _hip.ptr(ws), _hip.ptr(db1_f), 1, 0, _hip.stream()),
+                           "gelu_bwd_dbias")
         _BWD_MODE.setdefault(key, mode)
-        if db1_f is None:
-            db1_f = colsum(dh, torch.float32)
-        db1 = _acc(p_b1, lambda gb: gb.add_(db1_f.to(gb.dtype)) if gb is not None else db1_f.to(p_b1.dtype))
+        db1 = None
+        if not db1_done:
+            if db1_f is None:
+                db1_f = colsum(dh, torch.float32)
+            db1 = _acc(p_b1, lambda gb: gb.add_(db1_f.to(gb.dtype)) if gb is not None else db1_f.to(p_b1.dtype))
         dw1 = _acc(p_w1, lambda gb: gb.addmm_(dh.t(), x2) if gb is not None else dh.t() @ x2)
         dx = (dh @ w1).view(ctx.shape)
         return dx, dw1, db1, dw2, db2
