@@ -2,7 +2,6 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r4
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 120 ./scripts/probe/adam_probe > gpurun_out/r4/g11_adam_probe.jsonl 2>&1 &&
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_adam_kernel_gpu.py tests/test_ops_gpu.py tests/test_norm_fold_gpu.py tests/test_fused_mlp_gpu.py tests/test_optim_overlap_gpu.py -m gpu > gpurun_out/r4/g12_pytest.log 2>&1 &&
 DWAMD_NORM_FWD_BLOCKS=0 DWAMD_GELU_UNROLL=1 timeout -k 10 120 python -u scripts/bench_norm_fwd.py > gpurun_out/r4/g12_normfwd.jsonl 2>&1 &&
 timeout -k 10 120 python -u scripts/bench_norm_fwd.py >> gpurun_out/r4/g12_normfwd.jsonl 2>&1 &&
