@@ -13,8 +13,6 @@
 // a device scalar that the update kernel reads.
 #include "dw_common.h"
 
-#include <cstdlib>
-
 template <typename T> __device__ __forceinline__ float ld(const T* p, int64_t i);
 template <> __device__ __forceinline__ float ld<float>(const float* p, int64_t i) { return p[i]; }
 template <> __device__ __forceinline__ float ld<bf16_t>(const bf16_t* p, int64_t i) { return bf2f(p[i]); }
@@ -109,108 +107,6 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(P* __restrict__ param, f
   }
 }
 
-typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
-
-// 4-element loads / stores (i multiple of 4)
-template <typename T> __device__ __forceinline__ void ld4(const T* p, int64_t i, float* f);
-template <> __device__ __forceinline__ void ld4<bf16_t>(const bf16_t* p, int64_t i, float* f) {
-  const u32x2 v = *(const u32x2*)(p + i);
-  f[0] = bf2f(v[0] & 0xffff); f[1] = bf2f(v[0] >> 16); f[2] = bf2f(v[1] & 0xffff); f[3] = bf2f(v[1] >> 16);
-}
-template <> __device__ __forceinline__ void ld4<float>(const float* p, int64_t i, float* f) {
-  const f32x4 a = *(const f32x4*)(p + i);
-  f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3];
-}
-template <typename T> __device__ __forceinline__ void st4(T* p, int64_t i, const float* f);
-template <> __device__ __forceinline__ void st4<bf16_t>(bf16_t* p, int64_t i, const float* f) {
-  *(u32x2*)(p + i) = (u32x2){(unsigned)f2bf(f[0]) | ((unsigned)f2bf(f[1]) << 16),
-                             (unsigned)f2bf(f[2]) | ((unsigned)f2bf(f[3]) << 16)};
-}
-template <> __device__ __forceinline__ void st4<float>(float* p, int64_t i, const float* f) {
-  *(f32x4*)(p + i) = (f32x4){f[0], f[1], f[2], f[3]};
-}
-
-// Slab layout: a wave owns 512 consecutive elements per trip, lane l the 4 at
-// 4l and the 4 at 256 + 4l -- every load / store instruction of the wave
-// covers one contiguous 1 KiB (fp32) / 512 B (bf16) span, where the 8-per-lane
-// form above splits each fp32 stream over two half-filled instructions.  Both
-// halves' loads are issued before the math.  The ragged tail (< 512) runs the
-// scalar loop.
-template <typename G, typename P>
-__global__ void __launch_bounds__(256) adam_slab_kernel(P* __restrict__ param, float* __restrict__ master,
-                                                        const G* __restrict__ grad, float* __restrict__ m,
-                                                        float* __restrict__ v, const float* __restrict__ gscale,
-                                                        AdamArgs a) {
-  const float gs = gscale ? *gscale : 1.f;
-  const float step_size = a.lr / a.bc1;
-  const float rbc2 = rsqrtf(a.bc2);
-  const int lane = threadIdx.x & 63;
-  const int64_t nslab = a.n >> 9;
-  const int64_t nw = (int64_t)gridDim.x * 4;
-  for (int64_t sl = blockIdx.x * 4ll + (threadIdx.x >> 6); sl < nslab; sl += nw) {
-    float g[2][4], w[2][4], mm[2][4], vv[2][4];
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-      const int64_t i = (sl << 9) + 256 * hf + 4 * lane;
-      ld4<G>(grad, i, g[hf]);
-      if (master) ld4<float>(master, i, w[hf]); else ld4<P>(param, i, w[hf]);
-      ld4<float>(m, i, mm[hf]);
-      ld4<float>(v, i, vv[hf]);
-    }
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-      const int64_t i = (sl << 9) + 256 * hf + 4 * lane;
-      const bool dblk = decays(a.decay_mask, a.n_decay, i);  // 4-vector never straddles a 64-block
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool decay = a.decay_mask ? dblk : (i + k) < a.n_decay;
-        float gk = g[hf][k] * gs;
-        if (!a.adamw && decay) gk += a.wd * w[hf][k];
-        mm[hf][k] = a.beta1 * mm[hf][k] + (1.f - a.beta1) * gk;
-        vv[hf][k] = a.beta2 * vv[hf][k] + (1.f - a.beta2) * gk * gk;
-        const float denom = sqrtf(vv[hf][k]) * rbc2 + a.eps;
-        if (a.adamw && decay) w[hf][k] -= a.lr * a.wd * w[hf][k];
-        w[hf][k] -= step_size * mm[hf][k] / denom;
-      }
-      st4<float>(m, i, mm[hf]);
-      st4<float>(v, i, vv[hf]);
-      if (master) st4<float>(master, i, w[hf]);
-      st4<P>(param, i, w[hf]);
-    }
-  }
-  for (int64_t i = (nslab << 9) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const bool decay = decays(a.decay_mask, a.n_decay, i);
-    float gk = ld<G>(grad, i) * gs;
-    float w = master ? master[i] : ld<P>(param, i);
-    if (!a.adamw && decay) gk += a.wd * w;
-    float mk = a.beta1 * m[i] + (1.f - a.beta1) * gk;
-    float vk = a.beta2 * v[i] + (1.f - a.beta2) * gk * gk;
-    if (a.adamw && decay) w -= a.lr * a.wd * w;
-    w -= step_size * mk / (sqrtf(vk) * rbc2 + a.eps);
-    m[i] = mk; v[i] = vk;
-    if (master) master[i] = w;
-    st<P>(param, i, w);
-  }
-}
-
-static int adam_slab_grid() {
-  static const int g = [] {
-    const char* e = getenv("DWAMD_ADAM_GRID");
-    return e ? atoi(e) : 4096;
-  }();
-  return g;
-}
-
-static int adam_layout() {
-  // 0: 8 consecutive elements per lane; 1: slab layout (A/B: DWAMD_ADAM_SLAB)
-  static const int l = [] {
-    const char* e = getenv("DWAMD_ADAM_SLAB");
-    return e ? atoi(e) : 1;
-  }();
-  return l;
-}
-
 // dtype codes: 0 fp32, 1 bf16
 extern "C" int dw_adam_flat(void* param, int param_dtype, void* master, const void* grad,
                             int grad_dtype, void* m, void* v, const void* gscale, int64_t n,
@@ -218,20 +114,12 @@ extern "C" int dw_adam_flat(void* param, int param_dtype, void* master, const vo
                             float wd, float bc1, float bc2, int adamw, const void* decay_mask,
                             void* stream) {
   AdamArgs a{lr, beta1, beta2, eps, wd, bc1, bc2, n, n_decay, adamw, (const unsigned char*)decay_mask};
+  // up to 8192 blocks: 8.60 -> 8.30 ms at GPT2-1.5B size, where a pure
+  // 28 B/element copy takes 8.24 ms -- the update runs at the HBM ceiling;
+  // a contiguous-per-instruction layout and non-temporal accesses measured
+  // within +-2 % (profiles/r4/adam_layout_probe.jsonl, scripts/probe/adam_probe.hip)
+  int grid = dw_grid_for((n + 7) / 8, 256, 8192);
   hipStream_t s = (hipStream_t)stream;
-  if (adam_layout() == 1 && n >= 512) {
-    const int grid = dw_grid_for((n + 511) / 512, 4, adam_slab_grid());
-#define DW_SLAB(G, P)                                                                                         \
-  hipLaunchKernelGGL((adam_slab_kernel<G, P>), dim3(grid), dim3(256), 0, s, (P*)param, (float*)master,       \
-                     (const G*)grad, (float*)m, (float*)v, (const float*)gscale, a)
-    if (param_dtype == 1 && grad_dtype == 1) DW_SLAB(bf16_t, bf16_t);
-    else if (param_dtype == 1 && grad_dtype == 0) DW_SLAB(float, bf16_t);
-    else if (param_dtype == 0 && grad_dtype == 0) DW_SLAB(float, float);
-    else DW_SLAB(bf16_t, float);
-#undef DW_SLAB
-    DW_LAUNCH_RET;
-  }
-  int grid = dw_grid_for((n + 7) / 8, 256, 4096);
   if (param_dtype == 1 && grad_dtype == 1) {
     hipLaunchKernelGGL((adam_flat_kernel<bf16_t, bf16_t>), dim3(grid), dim3(256), 0, s,
                        (bf16_t*)param, (float*)master, (const bf16_t*)grad, (float*)m, (float*)v,

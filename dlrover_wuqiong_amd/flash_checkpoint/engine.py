@@ -804,7 +804,7 @@ class CheckpointEngine(ABC):
         tree = (scanned.get(slot) or h.get_meta(slot))["tree"]
         lap("meta")
         if target is not None:
-            sd = self._restore_into(tree, target, slot, step, require_hbm=from_hbm_only)
+            sd = self._restore_into(tree, target, slot, step, require_hbm=from_hbm_only, lap=lap)
             lap("copy_enqueue")
             if self._vote_retry(sd is None, from_hbm_only):
                 return None
@@ -845,14 +845,17 @@ class CheckpointEngine(ABC):
                 return buf.ptr
         return None
 
-    def _restore_into(self, tree, target, slot: int, step: int = 0, require_hbm: bool = False):
+    def _restore_into(self, tree, target, slot: int, step: int = 0, require_hbm: bool = False, lap=None):
         """Fast path: H2D (sliced + all-gather for replicated) straight into
         the live tensors of ``target`` (same structure as the saved dict).
         ``require_hbm``: the shm slot is incomplete -- every rank must copy
-        its slice from its HBM-tier buffer."""
+        its slice from its HBM-tier buffer.  ``lap``: phase timer of the
+        caller (sub-phases ``copy_enqueue.*``)."""
         from .copier import match_targets
 
+        lap = lap or (lambda name: None)
         pairs, ok = match_targets(tree, target)
+        lap("copy_enqueue.match")
         if require_hbm:
             # the shm slot never received this step's GPU bytes: every tensor
             # saved from the GPU must land in a contiguous GPU target (the
@@ -862,6 +865,7 @@ class CheckpointEngine(ABC):
             ok = ok and self._hbm_source(step, s_lo, s_hi) is not None and all(
                 t.is_cuda and t.is_contiguous() for m, t in pairs if m.device == "cuda" and m.numel > 0)
         ok_all = check_all_rank_ready(self._ctl_group, ok)
+        lap("copy_enqueue.vote")
         if not ok_all:
             return None
         h = self._shm_handler
@@ -880,13 +884,16 @@ class CheckpointEngine(ABC):
                 with torch.no_grad():
                     t.copy_(src.view(t.shape))
         total = h.payload_size
+        lap("copy_enqueue.pieces")
         copier = self._device_copier() if gpu_pieces else None
+        lap("copy_enqueue.copier")
         if copier is None:
             self.last_restore_source = "shm"  # host tensors: copied straight from the slot
             it = iter([t for _, t in pairs])
             return traverse(tree, lambda v: next(it) if isinstance(v, TensorMeta) else v)
         s_lo, s_hi = split_ranges(total, self._num_slices)[self._slice_idx]
         hbm_src = self._hbm_source(step, s_lo, s_hi) if step > 0 else None
+        lap("copy_enqueue.hbm_source")
         self.last_restore_source = "hbm" if hbm_src is not None else "shm"
         if self._replicated and self._num_slices > 1 and self._gather_group is not None:
             per = split_ranges(total, self._num_slices)[0][1]

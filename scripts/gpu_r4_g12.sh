@@ -8,4 +8,5 @@ timeout -k 10 120 python -u scripts/bench_norm_fwd.py >> gpurun_out/r4/g12_normf
 DWAMD_NORM_FWD_BLOCKS=512 DWAMD_GELU_UNROLL=2 timeout -k 10 120 python -u scripts/bench_norm_fwd.py >> gpurun_out/r4/g12_normfwd.jsonl 2>&1 &&
 DWAMD_NORM_FWD_BLOCKS=1024 timeout -k 10 120 python -u scripts/bench_norm_fwd.py >> gpurun_out/r4/g12_normfwd.jsonl 2>&1 &&
 timeout -k 10 300 python -u scripts/bench_step_ab.py --steps 10 --variant off > gpurun_out/r4/g12_step.log 2>&1 &&
-DWAMD_ADAM_SLAB=0 DWAMD_NORM_FWD_BLOCKS=0 DWAMD_GELU_UNROLL=1 timeout -k 10 300 python -u scripts/bench_step_ab.py --steps 10 --variant off > gpurun_out/r4/g12_step_old.log 2>&1
+DWAMD_NORM_FWD_BLOCKS=0 DWAMD_GELU_UNROLL=1 timeout -k 10 300 python -u scripts/bench_step_ab.py --steps 10 --variant off > gpurun_out/r4/g12_step_old.log 2>&1 &&
+timeout -k 10 400 python -u bench.py --out-dir gpurun_out/r4/bench_run12 > gpurun_out/r4/g12_bench.json 2> gpurun_out/r4/g12_bench.err

@@ -1,4 +1,4 @@
-"""GPU: the flat AdamW kernel (optim.hip, slab layout by default) against an
+"""GPU: the flat AdamW kernel (optim.hip) against an
 fp32 PyTorch reference of the same update -- bf16 params with fp32 master
 weights, a per-64-block decay mask, ragged lengths (scalar tail) and an
 offset slice (the overlapped update launches sub-ranges)."""
