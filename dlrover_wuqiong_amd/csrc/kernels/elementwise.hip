@@ -6,10 +6,10 @@
 // rotary embedding; llama SwiGLU MLP).
 #include "dw_common.h"
 
-#include <cstdlib>
-
 // y = gelu(x + bias); x:[R, C] bf16, bias [C] bf16 (nullable). Optionally
-// writes the biased pre-activation (pre) for the backward.
+// writes the biased pre-activation (pre) for the backward.  The bias-free
+// GPT2-1.5B pass (8192 x 6400) runs at 6.3 TB/s; 2 / 4 vectors per thread per
+// trip measured the same (profiles/r4/norm_fwd_gelu_ab.jsonl).
 __global__ void __launch_bounds__(256) bias_gelu_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ bias,
                                                             bf16_t* __restrict__ y, bf16_t* __restrict__ pre,
                                                             int64_t n, int C) {
@@ -47,54 +47,9 @@ __global__ void __launch_bounds__(256) gelu_bwd_kernel(const bf16_t* __restrict_
   }
 }
 
-// The bias-free GELU pass of the fused MLP forward (ops/mlp.py: the bias is
-// the GEMM's epilogue): U 16-byte vectors per thread per trip, all loads
-// issued before the tanh math, so each wave keeps U loads in flight instead
-// of one (the U = 1 loop measured 4.4 TB/s at 8192 x 6400 in the step,
-// profiles/r4/gpt2_1.5b_step_kernels.md).
-template <int U>
-__global__ void __launch_bounds__(256) gelu_fwd_unr_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
-                                                           int64_t n) {
-  const int64_t nv = n >> 3, stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t v0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v0 < nv; v0 += U * stride) {
-    u32x4 raw[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (v0 + u * stride < nv) raw[u] = *(const u32x4*)(x + ((v0 + u * stride) << 3));
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (v0 + u * stride >= nv) break;
-      float a[8], o[8];
-      unpack8(raw[u], a);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = gelu_tanh(a[k]);
-      *(u32x4*)(y + ((v0 + u * stride) << 3)) = pack8(o);
-    }
-  }
-}
-
-static int gelu_unroll() {
-  static const int u = [] {
-    const char* e = getenv("DWAMD_GELU_UNROLL");
-    return e ? atoi(e) : 4;
-  }();
-  return u;
-}
-
 extern "C" int dw_bias_gelu_fwd(const void* x, const void* bias, void* y, void* pre, int64_t n, int C,
                                 void* stream) {
   if (n % 8 || C % 8) return (int)hipErrorInvalidValue;
-  if (!bias && !pre && gelu_unroll() > 1) {
-    const int u = gelu_unroll() >= 4 ? 4 : 2;
-    const int grid = dw_grid_for((n / 8 + u - 1) / u, 256, 4096);
-    if (u == 4)
-      hipLaunchKernelGGL(gelu_fwd_unr_kernel<4>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
-                         (bf16_t*)y, n);
-    else
-      hipLaunchKernelGGL(gelu_fwd_unr_kernel<2>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
-                         (bf16_t*)y, n);
-    DW_LAUNCH_RET;
-  }
   hipLaunchKernelGGL(bias_gelu_fwd_kernel, dim3(dw_grid_for(n / 8, 256, 4096)), dim3(256), 0,
                      (hipStream_t)stream, (const bf16_t*)x, (const bf16_t*)bias, (bf16_t*)y,
                      (bf16_t*)pre, n, C);

@@ -13,8 +13,6 @@
 // fused LayerNorm) and the RMSNorm used by its Llama modules.
 #include "dw_common.h"
 
-#include <cstdlib>
-
 // ADD: fused residual add -- h = x + res is formed in registers, rounded to
 // bf16 (exactly what a separate bf16 add would store), written to h_out and
 // normalized; the residual stream is read once instead of three times.
@@ -89,115 +87,9 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(const bf16_t* __restrict_
   }
 }
 
-// Forward, grid-stride form: a wave walks rows gid, gid + nw, ... and issues
-// the NEXT row's x (/ res) loads before it normalises the current one, with
-// gamma / beta loaded once per wave before the first row.  The one-row-per-
-// wave kernel above waits a full HBM latency per row twice (x, then gamma /
-// beta after the reductions): GPT2-1.5B add+norm (8192 x 1600) ran at
-// 3.2 TB/s in the training step (profiles/r4/gpt2_1.5b_step_kernels.md).
-template <int VPL, bool RMS, bool ADD>
-__global__ void __launch_bounds__(256) norm_fwd_gs_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ gamma,
-                                                          const bf16_t* __restrict__ beta, bf16_t* __restrict__ y,
-                                                          float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                          int64_t rows, int H, float eps,
-                                                          const bf16_t* __restrict__ res, bf16_t* __restrict__ h_out) {
-  const int lane = threadIdx.x & 63;
-  const int64_t nw = (int64_t)gridDim.x * 4;
-  int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const int nv = H >> 3;
-  u32x4 xa[VPL], ra[ADD ? VPL : 1];
-  auto load = [&](int64_t rw) {
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) {
-      const int c = lane + 64 * j;
-      if (c < nv) {
-        xa[j] = *(const u32x4*)(x + rw * H + c * 8);
-        if constexpr (ADD) ra[j] = *(const u32x4*)(res + rw * H + c * 8);
-      }
-    }
-  };
-  load(row);
-  u32x4 gm[VPL], bt[RMS ? 1 : VPL];
-#pragma unroll
-  for (int j = 0; j < VPL; ++j) {
-    const int c = lane + 64 * j;
-    if (c < nv) {
-      gm[j] = *(const u32x4*)(gamma + c * 8);
-      if constexpr (!RMS) bt[j] = *(const u32x4*)(beta + c * 8);
-    }
-  }
-  for (; row < rows; row += nw) {
-    float v[VPL][8];
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) {
-      const int c = lane + 64 * j;
-      if (c < nv) {
-        unpack8(xa[j], v[j]);
-        if constexpr (ADD) {
-          float r[8];
-          unpack8(ra[j], r);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) r[k] += v[j][k];
-          const u32x4 hv = pack8(r);
-          *(u32x4*)(h_out + row * H + c * 8) = hv;
-          unpack8(hv, v[j]);  // normalise the bf16-rounded sum
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) s += v[j][k];
-      } else {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[j][k] = 0.f;
-      }
-    }
-    if (row + nw < rows) load(row + nw);  // the registers are free again: next row in flight
-    float mu = 0.f;
-    if (!RMS) mu = wave_sum(s) / (float)H;
-    float ss = 0.f;
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) {
-      const int c = lane + 64 * j;
-      if (c < nv) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float d = v[j][k] - mu;
-          ss += d * d;
-        }
-      }
-    }
-    const float rstd = rsqrtf(wave_sum(ss) / (float)H + eps);
-    if (lane == 0) {
-      if (!RMS) mean_out[row] = mu;
-      rstd_out[row] = rstd;
-    }
-#pragma unroll
-    for (int j = 0; j < VPL; ++j) {
-      const int c = lane + 64 * j;
-      if (c < nv) {
-        float g[8], b[8], o[8];
-        unpack8(gm[j], g);
-        if constexpr (!RMS) unpack8(bt[j], b);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = (v[j][k] - mu) * rstd * g[k] + (RMS ? 0.f : b[k]);
-        *(u32x4*)(y + row * H + c * 8) = pack8(o);
-      }
-    }
-  }
-}
-
-static int norm_fwd_gs_blocks(int64_t rows, int H) {
-  // 0: the one-row-per-wave kernel (A/B); default: ~2 rows per wave at
-  // 8k rows, never more blocks than rows / 4
-  static const int env = [] {
-    const char* e = getenv("DWAMD_NORM_FWD_BLOCKS");
-    return e ? atoi(e) : -1;
-  }();
-  if (env == 0 || H > 8 * 64 * 4) return 0;  // VPL > 4: keep the register-light form
-  const int64_t want = env > 0 ? env : 768;  // 166 VGPRs: 3 waves per SIMD, 3 blocks per CU
-  const int64_t cap = (rows + 3) / 4;
-  return (int)(want < cap ? want : cap);
-}
+// (A grid-stride form that prefetches the next row and loads gamma / beta
+// once per wave measured the same: 25.1 vs 24.9 us for the GPT2-1.5B add+norm,
+// 8192 x 1600 -- profiles/r4/norm_fwd_gelu_ab.jsonl; one row per wave stays.)
 
 // Backward. partial: [gridDim.x, 2, H] fp32 (dgamma, dbeta) per block.
 // Two passes over each row (the second hits L1/L2): pass 1 forms the row
@@ -320,32 +212,11 @@ __global__ void __launch_bounds__(256) norm_bwd_reduce_kernel(const float* __res
     else { constexpr int VPL = 16; __VA_ARGS__; }    \
   } while (0)
 
-#define DISPATCH_VPL4(H, ...)                          \
-  do {                                                 \
-    int nv_ = (H) / 8;                                 \
-    if (nv_ <= 64) { constexpr int VPL = 1; __VA_ARGS__; } \
-    else if (nv_ <= 128) { constexpr int VPL = 2; __VA_ARGS__; } \
-    else { constexpr int VPL = 4; __VA_ARGS__; }      \
-  } while (0)
-
 extern "C" int dw_norm_fwd(const void* x, const void* gamma, const void* beta, void* y, void* mean,
                            void* rstd, int64_t rows, int H, float eps, int rms, void* stream) {
   if (H % 8 != 0 || H > 8 * 64 * 16) return (int)hipErrorInvalidValue;
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   hipStream_t s = (hipStream_t)stream;
-  if (const int gb = norm_fwd_gs_blocks(rows, H)) {
-    DISPATCH_VPL4(H, {
-      if (rms)
-        hipLaunchKernelGGL((norm_fwd_gs_kernel<VPL, true, false>), dim3(gb), block, 0, s, (const bf16_t*)x,
-                           (const bf16_t*)gamma, nullptr, (bf16_t*)y, nullptr, (float*)rstd, rows, H, eps, nullptr,
-                           nullptr);
-      else
-        hipLaunchKernelGGL((norm_fwd_gs_kernel<VPL, false, false>), dim3(gb), block, 0, s, (const bf16_t*)x,
-                           (const bf16_t*)gamma, (const bf16_t*)beta, (bf16_t*)y, (float*)mean, (float*)rstd, rows,
-                           H, eps, nullptr, nullptr);
-    });
-    DW_LAUNCH_RET;
-  }
   DISPATCH_VPL(H, {
     if (rms)
       hipLaunchKernelGGL((norm_fwd_kernel<VPL, true>), grid, block, 0, s, (const bf16_t*)x,
@@ -365,19 +236,6 @@ extern "C" int dw_add_norm_fwd(const void* x, const void* res, const void* gamma
   if (H % 8 != 0 || H > 8 * 64 * 16) return (int)hipErrorInvalidValue;
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   hipStream_t s = (hipStream_t)stream;
-  if (const int gb = norm_fwd_gs_blocks(rows, H)) {
-    DISPATCH_VPL4(H, {
-      if (rms)
-        hipLaunchKernelGGL((norm_fwd_gs_kernel<VPL, true, true>), dim3(gb), block, 0, s, (const bf16_t*)x,
-                           (const bf16_t*)gamma, nullptr, (bf16_t*)y, nullptr, (float*)rstd, rows, H, eps,
-                           (const bf16_t*)res, (bf16_t*)h_out);
-      else
-        hipLaunchKernelGGL((norm_fwd_gs_kernel<VPL, false, true>), dim3(gb), block, 0, s, (const bf16_t*)x,
-                           (const bf16_t*)gamma, (const bf16_t*)beta, (bf16_t*)y, (float*)mean, (float*)rstd, rows,
-                           H, eps, (const bf16_t*)res, (bf16_t*)h_out);
-    });
-    DW_LAUNCH_RET;
-  }
   DISPATCH_VPL(H, {
     if (rms)
       hipLaunchKernelGGL((norm_fwd_kernel<VPL, true, true>), grid, block, 0, s, (const bf16_t*)x,

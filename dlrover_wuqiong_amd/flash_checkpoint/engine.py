@@ -743,14 +743,20 @@ class CheckpointEngine(ABC):
 
     def get_state_dict_from_memory(self, target: Any = None):
         """Returns (step, state_dict) from shm, or (0, {})."""
-        t0 = time.perf_counter()
+        t0, c0 = time.perf_counter(), time.thread_time()
         tb = self.last_restore_breakdown = {}
+        # other threads alive in this process during the restore (a phase
+        # whose wall time far exceeds its own CPU time was blocked: lock,
+        # GIL or the mm lock a concurrent hipHostRegister holds)
+        tb["threads"] = sorted(t.name for t in threading.enumerate() if t is not threading.current_thread())
 
         def lap(name):
-            nonlocal t0
-            t1 = time.perf_counter()
+            nonlocal t0, c0
+            t1, c1 = time.perf_counter(), time.thread_time()
             tb[name] = round(t1 - t0, 4)
-            t0 = t1
+            if t1 - t0 > 0.01:
+                tb["cpu." + name] = round(c1 - c0, 4)
+            t0, c0 = t1, c1
 
         self._restore_memory_from_replica()
         h = self._shm_handler
