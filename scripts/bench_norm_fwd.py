@@ -1,8 +1,9 @@
 """Norm forward micro-benchmark: fused add + LayerNorm / RMSNorm and plain
-norm at the GPT2-1.5B / Llama shapes.  ``DWAMD_NORM_FWD_BLOCKS`` selects the
-kernel (0: one row per wave; N: grid-stride over N blocks; unset: default),
-so run once per setting.  Prints one JSON line per shape with the HBM rate
-(x, res read; h, y written for the add form)."""
+norm at the GPT2-1.5B / Llama shapes, and the MLP's GELU pass.  Prints one
+JSON line per shape with the HBM rate (x, res read; h, y written for the add
+form).  profiles/r4/norm_fwd_gelu_ab.jsonl holds the round-4 A/B of the
+grid-stride norm / unrolled GELU variants it was written for (both equal to
+the kept kernels, since removed)."""
 import json
 import os
 import sys
