@@ -742,7 +742,31 @@ class CheckpointEngine(ABC):
         return out
 
     def get_state_dict_from_memory(self, target: Any = None):
-        """Returns (step, state_dict) from shm, or (0, {})."""
+        """Returns (step, state_dict) from shm, or (0, {}).
+
+        A restart's restore is the first allocation-heavy Python work of a
+        fresh process (unpickled meta trees, leaf lists) next to a model's
+        worth of live objects: a 0.12-0.21 s stall moved between its
+        Python-only phases from run to run (``hbm_scan.meta1``,
+        ``copy_enqueue.match``), the signature of a generation-2 collection.
+        Collection is deferred past the restore, and everything alive then
+        (model, optimizer, restored state) is frozen out of later full
+        collections, as after a save.  ``DWAMD_RESTORE_GC=1`` keeps the
+        collector on (A/B)."""
+        if os.environ.get("DWAMD_RESTORE_GC", "0") == "1":
+            return self._get_state_dict_from_memory(target)
+        enabled = gc.isenabled()
+        gc.disable()
+        try:
+            return self._get_state_dict_from_memory(target)
+        finally:
+            if not self._gc_frozen:
+                gc.freeze()
+                self._gc_frozen = True
+            if enabled:
+                gc.enable()
+
+    def _get_state_dict_from_memory(self, target: Any = None):
         t0, c0 = time.perf_counter(), time.thread_time()
         tb = self.last_restore_breakdown = {}
         # other threads alive in this process during the restore (a phase
