@@ -379,9 +379,14 @@ def _fault_summary(a, ev, agent, step_sec, save_sec):
     # that step's own compute: the time with no forward progress
     recovery = first_step_end - kill["t"] - step_sec
     skipped = [e for e in ev if e["event"] == "window_skipped"]
+    late = next((e for e in ev if e["event"] == "restore_late" and e.get("resident_sec") is not None), None)
+    load_sec = inc1["restore_sec"] if inc1.get("restore_sec") is not None else (late or {}).get("resident_sec")
+    load_ok = inc1["restore_ok"] if inc1.get("restore_ok") is not None else (late or {}).get("restore_ok")
     out = {
-        "load_sec": round(inc1["restore_sec"], 4),
-        "load_verified_after_restart": inc1["restore_ok"],
+        "load_sec": round(load_sec, 4) if load_sec is not None else None,
+        "load_verified_after_restart": load_ok,
+        "load_blocking_sec": inc1.get("restore_blocking_sec"),
+        "optim_restore_deferred": late is not None,
         "goodput_pct": round(goodput, 2),
         "goodput_window_s": round(window, 3),
         "goodput_window_steps": productive_steps,
@@ -398,7 +403,7 @@ def _fault_summary(a, ev, agent, step_sec, save_sec):
             "model_build_marks": inc1.get("build_marks") if inc1.get("standby") == "import" else None,
             "activate_to_pg_ready": round(inc1["t_pg"] - inc1["t_activated"], 3),
             "ckpt_engine_init": round(inc1["t_ckpt"] - inc1["t_pg"], 3),
-            "restore": round(inc1["restore_sec"], 3),
+            "restore": round(inc1["restore_blocking_sec"] if late is not None else inc1["restore_sec"], 3),
             "first_step": round(first_step_end - inc1["t_restored"], 3),
         },
         "standby_prepin_s": inc1.get("prepin_s"),
@@ -606,6 +611,24 @@ def worker(a) -> int:
         opt.join()
         third = opt.master if opt.master is not None else opt.exp_avg_sq
         return [float(flat.data.float().sum()), float(opt.exp_avg.sum()), float(third.sum())]
+
+    def state_sums_behind(deferred):
+        """state_sums() computed on a side stream after a deferred restore's
+        optimizer-state copies (flash_checkpoint/deferred_restore.py) and
+        ordered before the first optimizer update; returns a callable that
+        yields the sums (call it after that update was enqueued)."""
+        from dlrover_wuqiong_amd.flash_checkpoint import deferred_restore
+
+        opt.join()
+        vs = torch.cuda.Stream()
+        vs.wait_stream(torch.cuda.current_stream())
+        deferred.wait(vs)
+        third = opt.master if opt.master is not None else opt.exp_avg_sq
+        with torch.cuda.stream(vs):
+            t = torch.stack([flat.data.float().sum(), opt.exp_avg.sum(), third.sum()])
+        ev = vs.record_event()
+        deferred_restore.add_event(ev)  # the update waits for these reads
+        return lambda: (torch.cuda.current_stream().wait_event(ev), [float(x) for x in t.tolist()])[1]
 
     def save(st=None):
         t0 = time.perf_counter()
@@ -833,10 +856,13 @@ def worker(a) -> int:
         t0 = time.perf_counter()
         restored = ckpt.load_checkpoint(target=state())
         t_host = time.perf_counter()
+        deferred = getattr(ckpt.engine, "last_deferred_restore", None)
         if cuda:
-            torch.cuda.synchronize()
+            # with a deferred optimizer-state restore only the compute
+            # stream's copies (model) block; the rest lands during step 1
+            (torch.cuda.current_stream() if deferred is not None else torch.cuda).synchronize()
         restore_dev = time.perf_counter() - t_host
-        restore_sec = mx(time.perf_counter() - t0)
+        restore_block = time.perf_counter() - t0
         step = int(restored.get("step", 0)) if restored else 0
         restore_ok = bool(restored) and step > 0
         if restore_ok:
@@ -847,11 +873,19 @@ def worker(a) -> int:
         # that save (the last one before the kill)
         want = [e for e in _read_jsonl(step_log) if e["event"] == "saved_sums" and e["rank"] == rank
                 and e["step"] == step]
+        late_sums = None
         if restore_ok and want:
-            restore_ok = state_sums() == want[-1]["sums"]
+            if deferred is not None:
+                late_sums = state_sums_behind(deferred)  # checked after step 1
+            else:
+                restore_ok = state_sums() == want[-1]["sums"]
+        # load_sec: until every byte is resident (a deferred restore's last
+        # copy included; it overlaps step 1, and is collected after it)
+        restore_sec = mx(restore_block) if deferred is None else None
         t_restored = time.time()
         emit({"event": "start", "incarnation": incarnation, "t": time.time(), "restored_step": step,
-              "restore_sec": restore_sec, "restore_ok": restore_ok, "t_proc": t_proc, "t_model": t_model,
+              "restore_sec": restore_sec, "restore_ok": restore_ok if late_sums is None else None,
+              "restore_blocking_sec": round(restore_block, 4), "t_proc": t_proc, "t_model": t_model,
               "t_activated": t_act, "t_pg": t_pg, "t_ckpt": t_ckpt, "t_restored": t_restored,
               "build_marks": {k: round(v - t_proc, 3) for k, v in marks.items()},
               "prepin_s": info.get("prepin_s") if info else None, "standby": "deep" if info else "import",
@@ -862,6 +896,10 @@ def worker(a) -> int:
         if not restore_ok:
             log(f"[rank {rank}] restore from memory failed: starting over")
         start_step = step
+    if incarnation > 0:
+        pending_check = (late_sums, want[-1]["sums"] if want else None, deferred)
+    else:
+        pending_check = None
         s0 = next(e for e in _read_jsonl(step_log) if e["event"] == "fault_start")["s0"]
 
     # ---------------- fault window: train + save every interval; rank n-1 dies mid-step
@@ -874,6 +912,16 @@ def worker(a) -> int:
     while step < s_end:
         train_step(True)
         sync_step()
+        if pending_check is not None:
+            # the deferred restore: residency time and the bit-exact check,
+            # both settled behind step 1
+            late, wanted, dres = pending_check
+            pending_check = None
+            res_sec = dres.resident_sec() if dres is not None else None
+            ok = (late() == wanted) if late is not None else None
+            res_sec = mx(res_sec if res_sec is not None else -1.0)  # collective on every rank
+            emit({"event": "restore_late", "rank": rank, "restore_ok": ok,
+                  "resident_sec": res_sec if res_sec >= 0 else None})
         if (step - s0) % a.ckpt_interval == 0:
             _dt, ok = save()
             if not ok:

@@ -274,8 +274,10 @@ def _pending_updates(device) -> list:
     """Events of optimizer updates still running on a side stream
     (``optimizers/overlap.py``): a snapshot must read after them."""
     from ..optimizers.overlap import pending_events
+    from . import deferred_restore
 
-    return pending_events(device)
+    # ... and optimizer state a restart's restore is still copying in
+    return pending_events(device) + deferred_restore.events(device)
 
 
 def _install_fence_hook():
@@ -889,6 +891,9 @@ class GpuCopier:
         from ..optimizers.overlap import join_all
 
         join_all(cur)  # ... and a pending overlapped optimizer update would overwrite it
+        from . import deferred_restore
+
+        deferred_restore.wait_all(cur, self.device)  # ... as would a previous restore's late copies
         if gather_group is None or world <= 1:
             merged = _merge_pieces(pieces_gpu)
             if hbm_src is not None:
@@ -940,6 +945,25 @@ class GpuCopier:
                         scatter.append((base + r * n + (x0 - a), dst + (x0 - off), x1 - x0))
             launch_multi_copy(build_descs(scatter, self.device), cur)
         del tmp
+
+    def restore_deferred(self, pieces_gpu: List[Tuple[int, int, int]], shm_payload_addr: int, t0: float):
+        """H2D of ``pieces_gpu`` (payload_off, dst_addr, nbytes) from the shm
+        slot on a side stream, ordered after everything queued on the current
+        stream so far (the restore() of the other pieces included), enqueued
+        by a helper thread (pinning of a cold range must not hold up the
+        training thread).  Returns the registered
+        ``deferred_restore.DeferredRestore``."""
+        from . import deferred_restore
+
+        cur = torch.cuda.current_stream(self.device)
+        if getattr(self, "_restore_stream", None) is None:
+            self._restore_stream = torch.cuda.Stream(device=self.device)
+        merged = _merge_pieces(pieces_gpu)
+        copies = [(shm_payload_addr + off, dst, n) for off, dst, n in merged]
+        d = deferred_restore.DeferredRestore(self.device, self._restore_stream, cur.record_event(),
+                                             lambda stream: self._pipelined_h2d(copies, stream), t0)
+        deferred_restore.add(d)
+        return d
 
     def write_back(self, dev_src: int, host_dst: int, nbytes: int):
         """D2H of ``nbytes`` from a device address into (shm) host memory,

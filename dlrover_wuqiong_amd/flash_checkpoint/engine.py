@@ -193,6 +193,10 @@ class CheckpointEngine(ABC):
         self._prepped_for = None
         self._last_save_blocking = 0.0
         self.last_restore_source = None  # "hbm" | "shm" | "storage" after an in-place restore
+        self.last_deferred_restore = None  # deferred_restore.DeferredRestore of the last restore
+        # checkpointers whose restores feed straight into training (DDP) let
+        # optimizer state land behind the first step (deferred_restore.py)
+        self.defer_optimizer_restore = False
         self.last_storage_load_stats: Dict[str, float] = {}
         self.speculation_misses = 0  # speculative snapshots redone after the state dict changed
         self.last_restore_breakdown: Dict[str, float] = {}  # host seconds per restore phase
@@ -768,6 +772,7 @@ class CheckpointEngine(ABC):
 
     def _get_state_dict_from_memory(self, target: Any = None):
         t0, c0 = time.perf_counter(), time.thread_time()
+        self._restore_t0 = t0
         tb = self.last_restore_breakdown = {}
         # other threads alive in this process during the restore (a phase
         # whose wall time far exceeds its own CPU time was blocked: lock,
@@ -900,14 +905,16 @@ class CheckpointEngine(ABC):
             return None
         h = self._shm_handler
         base = h.payload_addr(slot)
-        gpu_pieces = []
-        for m, t in pairs:
+        gpu_pieces, late_pieces = [], []
+        late = self._late_leaf_flags(tree)
+        for i, (m, t) in enumerate(pairs):
             if m.numel == 0:
                 continue
             # tensors saved from the CPU were written to shm synchronously at
             # save time and are never in the HBM staging buffers: shm always
             if t.is_cuda and t.is_contiguous() and m.device == "cuda":
-                gpu_pieces.append((m.offset, t.data_ptr(), m.numel * m.element_size))
+                (late_pieces if late and late[i] else gpu_pieces).append(
+                    (m.offset, t.data_ptr(), m.numel * m.element_size))
             else:
                 src = torch.frombuffer(h.shared_memory.buf, dtype=m.dtype, count=m.numel,
                                        offset=m.offset + h.payload_offset(slot))
@@ -915,7 +922,7 @@ class CheckpointEngine(ABC):
                     t.copy_(src.view(t.shape))
         total = h.payload_size
         lap("copy_enqueue.pieces")
-        copier = self._device_copier() if gpu_pieces else None
+        copier = self._device_copier() if (gpu_pieces or late_pieces) else None
         lap("copy_enqueue.copier")
         if copier is None:
             self.last_restore_source = "shm"  # host tensors: copied straight from the slot
@@ -925,6 +932,11 @@ class CheckpointEngine(ABC):
         hbm_src = self._hbm_source(step, s_lo, s_hi) if step > 0 else None
         lap("copy_enqueue.hbm_source")
         self.last_restore_source = "hbm" if hbm_src is not None else "shm"
+        self.last_deferred_restore = None
+        if late_pieces and (hbm_src is not None or self._num_slices > 1):
+            # D2D restores take milliseconds and sliced ones meet in one
+            # gather: only a single-slice restore from host shm defers
+            gpu_pieces, late_pieces = gpu_pieces + late_pieces, []
         if self._replicated and self._num_slices > 1 and self._gather_group is not None:
             per = split_ranges(total, self._num_slices)[0][1]
             lo = self._slice_idx * per
@@ -932,6 +944,8 @@ class CheckpointEngine(ABC):
                            hbm_src=hbm_src)
         elif self._num_slices <= 1:
             copier.restore(gpu_pieces, base, total, 0, total, hbm_src=hbm_src)
+            if late_pieces:
+                self.last_deferred_restore = copier.restore_deferred(late_pieces, base, self._restore_t0)
         else:
             # replicated, no device all-gather (gloo world): slices meet in
             # shm.  An HBM-only step is first written back slice by slice
@@ -954,6 +968,32 @@ class CheckpointEngine(ABC):
             return v
 
         return traverse(tree, pick)
+
+    def _late_leaf_flags(self, tree):
+        """Per TensorMeta leaf of ``tree`` (``iter_leaves`` order, as in
+        ``match_targets``): may it land after the restore returns
+        (``deferred_restore``: optimizer state -- a dict key naming it in the
+        first two levels, e.g. ``{"model_states": {"optimizer": ...}}``)?
+        None: nothing deferrable, or the checkpointer did not opt in."""
+        from . import deferred_restore
+
+        if not (self.defer_optimizer_restore and isinstance(tree, dict) and deferred_restore.enabled()
+                and torch.cuda.is_available()):
+            return None
+        flags = []
+
+        def walk(v, late, depth):
+            if isinstance(v, dict):
+                for k, x in v.items():
+                    walk(x, late or (depth < 2 and deferred_restore.is_deferred_key(k)), depth + 1)
+            elif isinstance(v, (list, tuple)) and not hasattr(v, "_fields"):
+                for x in v:
+                    walk(x, late, depth + 1)
+            elif isinstance(v, TensorMeta):
+                flags.append(late)
+
+        walk(tree, False, 0)
+        return flags if any(flags) else None
 
     def _restore_memory_from_replica(self):
         if self._replica_manager.has_replica():

@@ -477,3 +477,61 @@ def test_gpu_storage_restore_orders_after_queued_writes(tmp_path):
     load_archive_into(path, target=tgt)
     torch.cuda.synchronize()
     assert torch.equal(tgt["w"].cpu(), ref["w"])
+
+
+@pytest.mark.parametrize("defer", [True, False])
+def test_gpu_deferred_optimizer_restore_orders_the_first_step(tmp_path, monkeypatch, defer):
+    """The optimizer state restored behind the first step (deferred_restore.py):
+    the side-stream copies are held back by a GPU spin, and the first
+    forward / backward / optimizer step issued right after load_checkpoint
+    (no host sync) must still produce exactly the state of a step taken from
+    the fully restored checkpoint (up to summation order)."""
+    from dlrover_wuqiong_amd.flash_checkpoint import copier as cp
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+
+    if not defer:
+        monkeypatch.setenv("DWAMD_DEFER_OPTIM_RESTORE", "0")
+    orig = cp.GpuCopier._pipelined_h2d
+
+    def slow(self, copies, stream, *a, **k):
+        if stream != torch.cuda.current_stream(self.device):
+            with torch.cuda.stream(stream):
+                torch.cuda._sleep(200_000_000)  # ~0.1 s of GPU cycles before the late copies
+        return orig(self, copies, stream, *a, **k)
+
+    monkeypatch.setattr(cp.GpuCopier, "_pipelined_h2d", slow)
+    model, opt, flat = _model_and_opt()
+    ck = DdpCheckpointer(str(tmp_path / "ck"))
+    state = lambda: {"model": model.state_dict(), "optimizer": opt.state_dict()}  # noqa
+    assert ck.save_checkpoint(5, state(), storage_type=StorageType.MEMORY)
+    ck.wait_latest_checkpoint()
+    x = torch.randint(0, model.cfg.vocab_size if hasattr(model, "cfg") else 50257, (2, 65), device="cuda",
+                      generator=torch.Generator("cuda").manual_seed(7))
+
+    def step():
+        model(x[:, :-1], x[:, 1:]).backward()
+        opt.step()
+        flat.zero_grad()
+
+    ck.load_checkpoint(target=state())
+    torch.cuda.synchronize()
+    step()
+    torch.cuda.synchronize()
+    want = flat.data.clone(), opt.exp_avg.clone(), opt.master.clone()
+    # corrupt, restore (no sync), step at once
+    flat.data.zero_()
+    opt.exp_avg.fill_(3.0)
+    opt.master.fill_(-1.0)
+    ck.load_checkpoint(target=state())
+    d = ck.engine.last_deferred_restore
+    assert (d is not None) == defer
+    step()
+    torch.cuda.synchronize()
+    # (embedding backward uses atomics: equal up to summation order; a step
+    # that read the corrupted state would be off by O(1))
+    for got, ref in zip((flat.data.float(), opt.exp_avg, opt.master), want):
+        torch.testing.assert_close(got, ref.float(), rtol=1e-2, atol=1e-3)
+    if defer:
+        assert d.resident_sec(timeout=30) > 0
+    ck.close()
