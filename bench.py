@@ -896,11 +896,11 @@ def worker(a) -> int:
         if not restore_ok:
             log(f"[rank {rank}] restore from memory failed: starting over")
         start_step = step
+        s0 = next(e for e in _read_jsonl(step_log) if e["event"] == "fault_start")["s0"]
     if incarnation > 0:
         pending_check = (late_sums, want[-1]["sums"] if want else None, deferred)
     else:
         pending_check = None
-        s0 = next(e for e in _read_jsonl(step_log) if e["event"] == "fault_start")["s0"]
 
     # ---------------- fault window: train + save every interval; rank n-1 dies mid-step
     if incarnation == 0 and a.inject_slow_flush > 0:
