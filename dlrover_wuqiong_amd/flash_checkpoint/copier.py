@@ -949,10 +949,8 @@ class GpuCopier:
     def restore_deferred(self, pieces_gpu: List[Tuple[int, int, int]], shm_payload_addr: int, t0: float):
         """H2D of ``pieces_gpu`` (payload_off, dst_addr, nbytes) from the shm
         slot on a side stream, ordered after everything queued on the current
-        stream so far (the restore() of the other pieces included), enqueued
-        by a helper thread (pinning of a cold range must not hold up the
-        training thread).  Returns the registered
-        ``deferred_restore.DeferredRestore``."""
+        stream so far (the restore() of the other pieces included).  Returns
+        the registered ``deferred_restore.DeferredRestore``."""
         from . import deferred_restore
 
         cur = torch.cuda.current_stream(self.device)

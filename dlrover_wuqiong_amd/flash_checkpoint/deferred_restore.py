@@ -6,8 +6,10 @@ optimizer state (fp32 master weights, exp_avg, exp_avg_sq) that nothing
 reads until the optimizer update at the END of the first step.  The engine
 therefore copies the model (and every non-optimizer leaf) on the compute
 stream as before, and the leaves under an ``optim*`` / ``opt`` key (first two
-levels) of the checkpointed dict on a side stream, enqueued by a helper thread; the first
-forward / backward runs while those DMAs land (SDMA engines, no CU time).
+levels) of the checkpointed dict on a side stream; the restore returns once
+they are enqueued, and the first forward / backward runs while those DMAs
+land (SDMA engines, no CU time).  A ``torch.cuda.synchronize()`` after the
+load still waits for everything.
 
 Ordering is enforced on the device, never by host waits:
   * every ``torch.optim.Optimizer.step`` (a global step pre-hook, installed
@@ -52,55 +54,40 @@ def is_deferred_key(key) -> bool:
 
 
 class DeferredRestore:
-    """Copies enqueued by a helper thread on ``stream`` after ``ready`` (an
-    event of the compute stream); ``event`` completes when they landed."""
+    """Copies enqueued (by the calling thread, before the restore returns:
+    a ``torch.cuda.synchronize()`` after the load still covers them) on
+    ``stream`` after ``ready`` (an event of the compute stream); ``event``
+    completes when they landed.  A helper thread only waits for that to
+    time the residency."""
 
     def __init__(self, device, stream, ready, enqueue: Callable[[object], None], t0: float):
         self.device = device
         self.stream = stream
-        self.event = None
-        self.error: Optional[BaseException] = None
         self.t0 = t0
-        self.enqueued_at: Optional[float] = None
         self.done_at: Optional[float] = None
-        self._enqueued = threading.Event()
-        self._thread = threading.Thread(target=self._run, args=(ready, enqueue), daemon=True,
-                                        name="dwamd-deferred-restore")
+        with torch.cuda.device(device):
+            stream.wait_event(ready)
+            enqueue(stream)
+            self.event = stream.record_event()
+        self.enqueued_at = time.perf_counter()
+        self._thread = threading.Thread(target=self._time, daemon=True, name="dwamd-deferred-restore")
         self._thread.start()
 
-    def _run(self, ready, enqueue):
-        try:
-            with torch.cuda.device(self.device):
-                self.stream.wait_event(ready)
-                enqueue(self.stream)
-                self.event = self.stream.record_event()
-        except BaseException as e:  # surfaced by wait()
-            self.error = e
-        finally:
-            self.enqueued_at = time.perf_counter()
-            self._enqueued.set()
-        if self.event is not None:
-            self.event.synchronize()
-            self.done_at = time.perf_counter()
+    def _time(self):
+        self.event.synchronize()
+        self.done_at = time.perf_counter()
 
     def wait(self, stream=None):
         """Order ``stream`` (default: current) after the copies (device-side
-        wait; the host only waits for the helper thread to finish enqueueing)."""
-        self._enqueued.wait()
-        if self.error is not None:
-            raise RuntimeError("deferred optimizer-state restore failed") from self.error
+        wait, the host does not block)."""
         (stream or torch.cuda.current_stream(self.device)).wait_event(self.event)
 
     def ready_event(self):
-        self._enqueued.wait()
-        if self.error is not None:
-            raise RuntimeError("deferred optimizer-state restore failed") from self.error
         return self.event
 
     @property
     def complete(self) -> bool:
-        # a failed restore stays pending: every later wait() raises
-        return self.done_at is not None
+        return self.done_at is not None or self.event.query()
 
     def resident_sec(self, timeout: Optional[float] = None) -> Optional[float]:
         """Seconds from the restore call until every deferred byte landed
