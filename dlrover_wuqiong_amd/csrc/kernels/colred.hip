@@ -498,7 +498,7 @@ __global__ void __launch_bounds__(256) colsum_f32_kernel(const float* __restrict
                                                          int rows_per_blk, float* __restrict__ ws,
                                                          void* __restrict__ out0, void* __restrict__ out1,
                                                          int is_fp32, int accumulate, int H,
-                                                         void* __restrict__ out2) {
+                                                         void* __restrict__ out2, int accumulate2) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   const int r0 = blockIdx.y * rows_per_blk, r1 = min(R, r0 + rows_per_blk);
   if (c < H2) {
@@ -528,7 +528,7 @@ __global__ void __launch_bounds__(256) colsum_f32_kernel(const float* __restrict
     else if (c < 2 * H)
       colred_store(out1, c - H, v, is_fp32, accumulate);
     else
-      colred_store(out2, c - 2 * H, v, is_fp32, 1);  // a bias gradient: always accumulated
+      colred_store(out2, c - 2 * H, v, is_fp32, accumulate2);  // the folded bias gradient
   }
   if (threadIdx.x == 0) __hip_atomic_exchange(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -661,6 +661,10 @@ extern "C" int dw_norm_bwd3(const void* dy, const void* x, const void* gamma, co
                             const void* dres, void* dx, void* dgamma, void* dbeta, void* ws, void* part,
                             int64_t part_floats, int64_t rows, int H, int rms, int out_fp32, int accumulate,
                             void* dsum, int* dsum_done, void* stream) {
+  // accumulate: bit 0 -- dgamma / dbeta accumulate; bit 1 -- dsum is
+  // OVERWRITTEN (its parameter's first gradient contribution of the step)
+  const int acc2 = (accumulate & 2) ? 0 : 1;
+  accumulate &= 1;
   // every workgroup resident at once, each wave striding over rows: H > 1024
   // (VPL 4) needs ~310-370 VGPRs, one workgroup per CU; smaller H two
   const int64_t nb = std::min<int64_t>((rows + 3) / 4, H > 1024 ? 256 : 512);
@@ -691,7 +695,7 @@ extern "C" int dw_norm_bwd3(const void* dy, const void* x, const void* gamma, co
   const int per = (int)((nb + splits - 1) / splits);
   dim3 g((H2 + 255) / 256, (unsigned)((nb + per - 1) / per));
   hipLaunchKernelGGL(colsum_f32_kernel, g, dim3(256), 0, s, (const float*)part, (int)nb, H2, per, (float*)ws,
-                     dgamma, rms ? nullptr : dbeta, out_fp32, accumulate, H, dsum);
+                     dgamma, rms ? nullptr : dbeta, out_fp32, accumulate, H, dsum, acc2);
   DW_LAUNCH_RET;
 }
 

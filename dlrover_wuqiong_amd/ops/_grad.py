@@ -2,7 +2,8 @@
 
 Parameters managed by ``parallel.flat.FlatParams`` (with
 ``direct_grads=True``) carry ``_dwamd_direct``: their ``.grad`` is a view of
-the flat gradient buffer, zeroed once per step.  The fused ops accumulate
+the flat gradient buffer, zeroed lazily once per step (``claim()``: the
+first contribution after ``zero_grad`` overwrites, ``parallel/flat.py``).  The fused ops accumulate
 into it themselves -- weight GEMMs with ``addmm_`` (beta = 1: the hipBLASLt
 epilogue does the add), bias / norm-weight reductions with an accumulating
 finish kernel -- and return ``None`` to autograd.  That removes one
@@ -27,6 +28,28 @@ def direct_grad(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     if g is None or not g.is_contiguous():
         return None
     return g
+
+
+def claim(p: Optional[torch.Tensor]) -> bool:
+    """The caller is about to write ``p``'s direct gradient: True when the
+    write must OVERWRITE (first contribution since a lazy ``zero_grad``,
+    ``parallel/flat.py``), False when it accumulates."""
+    st = getattr(p, "_dwamd_flat", None)
+    return st.claim(p._dwamd_idx) if st is not None else False
+
+
+def claim_all(*ps) -> bool:
+    """One writer for several parameters (e.g. a norm's weight and bias):
+    True (overwrite) only if all are fresh; a mixed set zeroes its fresh
+    members and accumulates."""
+    ps = [p for p in ps if p is not None]
+    fresh = [claim(p) for p in ps]
+    if all(fresh):
+        return bool(fresh)
+    for p, f in zip(ps, fresh):
+        if f:
+            p.grad.zero_()
+    return False
 
 
 def notify(p: Optional[torch.Tensor]):

@@ -6,7 +6,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _hip
-from ._grad import direct_grad, notify
+from ._grad import claim, direct_grad, notify
 
 
 def colsum(x2: torch.Tensor, out_dtype=None, out: torch.Tensor = None, accumulate: bool = False) -> torch.Tensor:
@@ -56,7 +56,8 @@ class _BiasGeluFn(torch.autograd.Function):
         ws = _hip.zeroed_workspace(C + (C + 511) // 512, pre.device)
         _hip.check(_hip.lib().dw_gelu_bwd_dbias(_hip.ptr(dy), _hip.ptr(pre), _hip.ptr(dx), pre.numel() // C, C,
                                                 _hip.ptr(ws), _hip.ptr(db), int(db.dtype == torch.float32),
-                                                int(g is not None), _hip.stream()), "gelu_bwd_dbias")
+                                                int(g is not None and not claim(ctx.bias_param)), _hip.stream()),
+                   "gelu_bwd_dbias")
         if g is not None:
             notify(ctx.bias_param)
             return dx, None

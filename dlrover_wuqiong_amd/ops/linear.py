@@ -15,7 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _hip
-from ._grad import direct_grad, notify
+from ._grad import claim, direct_grad, notify
 
 # dX = dY W (dgrad) and dW += dY^T X (wgrad) are independent GEMMs;
 # DWAMD_WGRAD_STREAM=1 runs the wgrad (+ bias colsum) on a per-device side
@@ -73,19 +73,22 @@ class _LinearFn(torch.autograd.Function):
                 and gw.dtype == torch.bfloat16 and dy2.is_contiguous() and x2.is_contiguous()
                 and (dy2.shape[0], K, N) not in _BGRAD_OFF):
             db32 = torch.empty(N, device=dy2.device, dtype=torch.float32)
+            ow = claim(ctx.weight_param)
             rc = _hip.lib().dw_gemm_wgrad_bgradb(_hip.ptr(x2), _hip.ptr(dy2), _hip.ptr(gw), _hip.ptr(db32),
-                                                 dy2.shape[0], K, N, 1, _hip.stream())
+                                                 dy2.shape[0], K, N, 0 if ow else 1, _hip.stream())
             if rc == _EPI_UNSUPPORTED:
                 _BGRAD_OFF.add((dy2.shape[0], K, N))
+                if ow:
+                    gw.zero_()  # claimed: the fallback below accumulates
             else:
                 _hip.check(rc, "gemm_wgrad_bgradb")
-                gb.add_(db32)
+                gb.copy_(db32) if claim(b) else gb.add_(db32)
                 notify(ctx.weight_param)
                 notify(b)
                 return dx, None, None
         if ctx.needs_input_grad[1]:
             if gw is not None:
-                gw.addmm_(dy2.t(), x2)
+                _wgrad(gw, dy2, x2, ctx.weight_param)
                 notify(ctx.weight_param)
             else:
                 dw = dy2.t() @ x2
@@ -93,11 +96,20 @@ class _LinearFn(torch.autograd.Function):
             if gb is not None and _hip.use_hip(dy2) and dy2.is_contiguous() and N % 8 == 0:
                 from .activation import colsum
 
-                colsum(dy2, out=gb, accumulate=True)
+                colsum(dy2, out=gb, accumulate=not claim(b))
                 notify(b)
             else:
                 db = dy2.sum(0).to(b.dtype)
         return dx, dw, db
+
+
+def _wgrad(gw, dy2, x2, param):
+    """gw (+)= dy2^T x2: overwrite (GEMM beta = 0) on the parameter's first
+    contribution since a lazy zero_grad, else accumulate (beta = 1)."""
+    if claim(param):
+        torch.mm(dy2.t(), x2, out=gw)
+    else:
+        gw.addmm_(dy2.t(), x2)
 
 
 def _backward_two_streams(ctx, dy2, x2, w, x_shape, gw, gb, N):
@@ -107,12 +119,14 @@ def _backward_two_streams(ctx, dy2, x2, w, x_shape, gw, gb, N):
     side = _side_stream(dy2.device)
     side.wait_stream(cur)
     with torch.cuda.stream(side):
-        gw.addmm_(dy2.t(), x2)
+        _wgrad(gw, dy2, x2, ctx.weight_param)
         if gb is not None:
             if _hip.use_hip(dy2) and dy2.is_contiguous() and N % 8 == 0:
                 from .activation import colsum
 
-                colsum(dy2, out=gb, accumulate=True)
+                colsum(dy2, out=gb, accumulate=not claim(ctx.bias_param))
+            elif claim(ctx.bias_param):
+                gb.copy_(dy2.sum(0).to(gb.dtype))
             else:
                 gb.add_(dy2.sum(0).to(gb.dtype))
     dx = (dy2 @ w).view(x_shape)

@@ -32,7 +32,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _hip
-from ._grad import direct_grad, notify
+from ._grad import claim, direct_grad, notify
 
 _EPI_UNSUPPORTED = -100
 _BWD_MODE = {}  # (M, N1, N2) -> "bgrad" | "dgelu" | "unfused"
@@ -40,13 +40,19 @@ _BWD_DEFAULT = os.environ.get("DWAMD_MLP_BWD_EPILOGUE", "unfused")
 
 
 def _acc(param, grad_fn):
-    """Accumulate into the flat gradient of ``param`` or return the grad."""
+    """Write into the flat gradient of ``param`` or return the grad.
+    ``grad_fn(g, overwrite)``: g is the flat view (None: return the grad);
+    overwrite on the first contribution since a lazy zero_grad."""
     g = direct_grad(param)
     if g is not None:
-        grad_fn(g)
+        grad_fn(g, claim(param))
         notify(param)
         return None
-    return grad_fn(None)
+    return grad_fn(None, False)
+
+
+def _mm_into(g, a, b, overwrite):
+    return torch.mm(a, b, out=g) if overwrite else g.addmm_(a, b)
 
 
 class _FusedMLPFn(torch.autograd.Function):
@@ -75,9 +81,9 @@ class _FusedMLPFn(torch.autograd.Function):
         N2, N1 = w2.shape
         dy2 = dy.reshape(-1, N2).contiguous().to(x2.dtype)
         M = dy2.shape[0]
-        dw2 = _acc(p_w2, lambda gb: gb.addmm_(dy2.t(), g) if gb is not None else dy2.t() @ g)
+        dw2 = _acc(p_w2, lambda gb, ow: _mm_into(gb, dy2.t(), g, ow) if gb is not None else dy2.t() @ g)
         db2 = None if ctx.out_bias_folded else _acc(
-            p_b2, lambda gb: colsum(dy2, out=gb, accumulate=True) if gb is not None else colsum(dy2, p_b2.dtype))
+            p_b2, lambda gb, ow: colsum(dy2, out=gb, accumulate=not ow) if gb is not None else colsum(dy2, p_b2.dtype))
         key = (M, N1, N2)
         dh = torch.empty(M, N1, device=dy.device, dtype=x2.dtype)
         db1_f = None
@@ -109,7 +115,8 @@ class _FusedMLPFn(torch.autograd.Function):
                 # fp32 temporary + cast + add_ launches)
                 _hip.check(_hip.lib().dw_gelu_bwd_dbias(_hip.ptr(dg), _hip.ptr(pre), _hip.ptr(dh), M, N1,
                                                         _hip.ptr(ws), _hip.ptr(gb1),
-                                                        int(gb1.dtype == torch.float32), 1, _hip.stream()),
+                                                        int(gb1.dtype == torch.float32), int(not claim(p_b1)),
+                                                        _hip.stream()),
                            "gelu_bwd_dbias")
                 notify(p_b1)
                 db1_done = True
@@ -123,8 +130,9 @@ class _FusedMLPFn(torch.autograd.Function):
         if not db1_done:
             if db1_f is None:
                 db1_f = colsum(dh, torch.float32)
-            db1 = _acc(p_b1, lambda gb: gb.add_(db1_f.to(gb.dtype)) if gb is not None else db1_f.to(p_b1.dtype))
-        dw1 = _acc(p_w1, lambda gb: gb.addmm_(dh.t(), x2) if gb is not None else dh.t() @ x2)
+            db1 = _acc(p_b1, lambda gb, ow: (gb.copy_ if ow else gb.add_)(db1_f.to(gb.dtype))
+                       if gb is not None else db1_f.to(p_b1.dtype))
+        dw1 = _acc(p_w1, lambda gb, ow: _mm_into(gb, dh.t(), x2, ow) if gb is not None else dh.t() @ x2)
         dx = (dh @ w1).view(ctx.shape)
         return dx, dw1, db1, dw2, db2
 

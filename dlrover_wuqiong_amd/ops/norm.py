@@ -12,7 +12,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _hip
-from ._grad import direct_grad, notify
+from ._grad import claim, claim_all, direct_grad, notify
 
 _FOLD = os.environ.get("DWAMD_NORM_FOLD_BIAS", "1") != "0"
 
@@ -67,11 +67,18 @@ def _norm_backward(ctx, dy, dres):
     nparts = min(512, (R + 3) // 4) * (3 if dsum is not None else 2) * H if H < 2048 else 0
     part = torch.empty(nparts, device=x2.device, dtype=torch.float32) if nparts else None
     done = ctypes.c_int(0)
+    # flags: bit 0 accumulate dgamma / dbeta (direct storage already holding
+    # this step's contributions), bit 1 overwrite dsum (first contribution to
+    # the producer's bias since a lazy zero_grad -- parallel/flat.py)
+    acc = int(direct and not claim_all(wp, bp if ctx.has_bias else None))
+    dsum_fresh = dsum is not None and claim(fold[1])
     _hip.check(_hip.lib().dw_norm_bwd3(_hip.ptr(dy2), _hip.ptr(x2), _hip.ptr(weight), _hip.ptr(mean),
                                        _hip.ptr(rstd), _hip.ptr(dres), _hip.ptr(dx), _hip.ptr(dgamma),
                                        _hip.ptr(dbeta), _hip.ptr(ws), _hip.ptr(part), nparts, R, H,
-                                       int(ctx.rms), int(dgamma.dtype == torch.float32), int(direct),
+                                       int(ctx.rms), int(dgamma.dtype == torch.float32), acc | (2 * dsum_fresh),
                                        _hip.ptr(dsum), ctypes.byref(done), _hip.stream()), "norm_bwd")
+    if dsum_fresh and not done.value:
+        dsum.zero_()  # claimed but not taken over: the producer's backward accumulates into it
     if done.value:
         fold[0].out_bias_folded = True  # the producer's backward (later) skips its own reduction
         notify(fold[1])

@@ -27,6 +27,10 @@ class _FlatOptimizer(torch.optim.Optimizer):
                  max_grad_norm: float = 0.0):
         self.flat = flat
         super().__init__(flat.params, defaults)
+        # a lazily zeroed gradient generation (parallel/flat.py) is fully
+        # defined before the update reads the whole buffer
+        if hasattr(flat, "finalize_grads"):
+            self.register_step_pre_hook(lambda opt, args, kwargs: opt.flat.finalize_grads())
         dev = flat.device
         self.master_weights = (flat.dtype != torch.float32) if master_weights is None else master_weights
         n = flat.numel

@@ -148,6 +148,7 @@ class FlatDDP(nn.Module):
         buckets holding unused parameters)."""
         if self.world <= 1:
             return
+        self.flat.finalize_grads()  # lazily zeroed grads nobody wrote (the backward-end callback did it already)
         if self._expected is None:
             self._expected = list(self._calls)
         for b in range(len(self.buckets)):
