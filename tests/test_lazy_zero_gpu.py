@@ -31,7 +31,8 @@ def _run(lazy, monkeypatch):
         ids = torch.randint(0, cfg.vocab_size, (2, 65), device="cuda", generator=g)
         flat.zero_grad()
         if lazy:
-            flat.grad.fill_(7.0)  # stale contents of the open generation
+            for p in flat.params:
+                p.grad.fill_(7.0)  # stale contents of the open generation
         m(ids[:, :-1], ids[:, 1:]).backward()
         if it == 2:
             m(ids[:, :-1], ids[:, 1:]).backward()  # accumulation
