@@ -501,7 +501,7 @@ def worker(a) -> int:
     marks["init"] = time.time()
     model.to(dtype)
     nparams = model.num_params()
-    flat = FlatParams(model, dtype=dtype, device=device)
+    flat = FlatParams(model, dtype=dtype, device=device, lazy_zero_grad=True)
     if cuda:
         torch.cuda.synchronize()
     marks["flat"] = time.time()

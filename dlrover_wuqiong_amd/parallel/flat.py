@@ -35,11 +35,18 @@ def default_no_decay(name: str, p: torch.Tensor) -> bool:
 class FlatParams:
     def __init__(self, module: nn.Module, dtype: Optional[torch.dtype] = None, device=None,
                  no_decay_fn: Callable[[str, torch.Tensor], bool] = default_no_decay,
-                 grad_dtype: Optional[torch.dtype] = None, direct_grads: bool = True):
+                 grad_dtype: Optional[torch.dtype] = None, direct_grads: bool = True,
+                 lazy_zero_grad: Optional[bool] = None):
         """``direct_grads``: the fused ops (``ops/linear.py``, norms, bias
         activations) accumulate straight into the flat ``.grad`` views
         (``ops/_grad.py``); call ``zero_grad()`` (not ``set_to_none``) once
-        per optimizer step."""
+        per optimizer step.  ``lazy_zero_grad`` (training loops that only
+        produce gradients by backward; ``DWAMD_LAZY_ZERO_GRAD=0/1``
+        overrides): ``zero_grad()`` skips the pass over the buffer and the
+        next backward's first contributions overwrite -- gradients read
+        between ``zero_grad()`` and the end of the next backward are
+        undefined, and gradients written by hand after ``zero_grad()`` need
+        the eager default."""
         named = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
         # tied weights appear once in named_parameters (dedup by identity)
         named.reverse()
@@ -72,7 +79,7 @@ class FlatParams:
                 mask[o // ALIGN:(o + c + ALIGN - 1) // ALIGN] = 0
         self.decay_mask = mask.to(self.device)
         self._index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
-        # Lazy zeroing (direct grads): zero_grad() only opens a new gradient
+        # Lazy zeroing (opt-in): zero_grad() only opens a new gradient
         # generation; the first writer of each parameter in it OVERWRITES
         # (GEMMs with beta = 0, reductions without accumulate -- claim()),
         # autograd-accumulated parameters are zeroed by a pre-hook just before
@@ -80,7 +87,9 @@ class FlatParams:
         # the backward ends (or before any flat-buffer reader).  Saves the
         # zero pass over the buffer and the C read of every weight-gradient
         # GEMM: 0.5 + 1.3 ms per GPT2-1.5B step (profiles/r4/wgrad_beta_ab.jsonl).
-        self.lazy_zero = bool(direct_grads) and os.environ.get("DWAMD_LAZY_ZERO_GRAD", "1") != "0"
+        env = os.environ.get("DWAMD_LAZY_ZERO_GRAD")
+        lazy = (env == "1") if env is not None else bool(lazy_zero_grad)
+        self.lazy_zero = bool(direct_grads) and lazy
         self._fresh = False  # a generation is open: unwritten grads hold stale values
         self._written: set = set()
         self._finalize_queued = False

@@ -62,7 +62,7 @@ def main():
     with torch.device(dev):
         model = GPT2(cfg)
     model.to(dtype)
-    flat = FlatParams(model, dtype=dtype, device=dev)
+    flat = FlatParams(model, dtype=dtype, device=dev, lazy_zero_grad=True)
     opt = FusedAdamW(flat, lr=1e-4, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0)
     ddp = FlatDDP(model, flat)
     opt.grad_scale = 1.0 / world

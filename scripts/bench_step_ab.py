@@ -27,7 +27,7 @@ def run(variant, steps, model_name):
     with torch.device(dev):
         model = GPT2(cfg)
     model.to(torch.bfloat16)
-    flat = FlatParams(model, dtype=torch.bfloat16, device=dev)
+    flat = FlatParams(model, dtype=torch.bfloat16, device=dev, lazy_zero_grad=True)
     opt = FusedAdamW(flat, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0)
     if variant == "on":
         opt.overlap_with_forward(model)

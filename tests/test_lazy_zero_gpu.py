@@ -14,16 +14,13 @@ def _run(lazy, monkeypatch):
     from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
     from dlrover_wuqiong_amd.parallel.flat import FlatParams
 
-    if lazy:
-        monkeypatch.delenv("DWAMD_LAZY_ZERO_GRAD", raising=False)
-    else:
-        monkeypatch.setenv("DWAMD_LAZY_ZERO_GRAD", "0")
+    monkeypatch.delenv("DWAMD_LAZY_ZERO_GRAD", raising=False)
     torch.manual_seed(0)
     cfg = GPT2Config.named("gpt2-tiny")
     with torch.device("cuda"):
         m = GPT2(cfg)
     m.to(torch.bfloat16)
-    flat = FlatParams(m, dtype=torch.bfloat16, device=torch.device("cuda"))
+    flat = FlatParams(m, dtype=torch.bfloat16, device=torch.device("cuda"), lazy_zero_grad=lazy)
     assert flat.lazy_zero == lazy
     g = torch.Generator("cuda").manual_seed(1)
     out = []

@@ -1,4 +1,5 @@
-"""Lazy gradient zeroing of FlatParams (parallel/flat.py): zero_grad() only
+"""Lazy gradient zeroing of FlatParams (parallel/flat.py, opt-in
+``lazy_zero_grad=True``; ``DWAMD_LAZY_ZERO_GRAD`` overrides): zero_grad() only
 opens a generation, the first contribution overwrites, autograd-accumulated
 parameters are zeroed just before their first accumulation, and unused
 parameters are zeroed when the backward ends."""
@@ -31,10 +32,9 @@ def test_lazy_zero_matches_eager(monkeypatch):
     ref_net = _Net()
     net = _Net()
     net.load_state_dict(ref_net.state_dict())
-    monkeypatch.setenv("DWAMD_LAZY_ZERO_GRAD", "0")
-    ref = FlatParams(ref_net, dtype=torch.float32)
-    monkeypatch.delenv("DWAMD_LAZY_ZERO_GRAD")
-    flat = FlatParams(net, dtype=torch.float32)
+    monkeypatch.delenv("DWAMD_LAZY_ZERO_GRAD", raising=False)
+    ref = FlatParams(ref_net, dtype=torch.float32)  # eager: the default
+    flat = FlatParams(net, dtype=torch.float32, lazy_zero_grad=True)
     assert flat.lazy_zero and not ref.lazy_zero
     for it in range(3):
         for f, m in ((ref, ref_net), (flat, net)):
@@ -53,9 +53,10 @@ def test_lazy_zero_matches_eager(monkeypatch):
         assert not flat._fresh
 
 
-def test_claim_outside_backward_and_finalize():
+def test_claim_outside_backward_and_finalize(monkeypatch):
+    monkeypatch.delenv("DWAMD_LAZY_ZERO_GRAD", raising=False)
     net = _Net()
-    flat = FlatParams(net, dtype=torch.float32)
+    flat = FlatParams(net, dtype=torch.float32, lazy_zero_grad=True)
     flat.grad.fill_(5.0)
     flat.zero_grad()
     i = flat.index_of(net.fc.weight)
@@ -66,3 +67,12 @@ def test_claim_outside_backward_and_finalize():
     for j, p in enumerate(flat.params):
         assert torch.all(p.grad == (1.0 if j == i else 0.0))
     assert flat.claim(i) is False     # generation closed: accumulate
+
+
+def test_env_overrides(monkeypatch):
+    monkeypatch.setenv("DWAMD_LAZY_ZERO_GRAD", "0")
+    assert not FlatParams(_Net(), dtype=torch.float32, lazy_zero_grad=True).lazy_zero
+    monkeypatch.setenv("DWAMD_LAZY_ZERO_GRAD", "1")
+    assert FlatParams(_Net(), dtype=torch.float32).lazy_zero
+    monkeypatch.delenv("DWAMD_LAZY_ZERO_GRAD")
+    assert not FlatParams(_Net(), dtype=torch.float32).lazy_zero

@@ -46,6 +46,7 @@ def _run(overlap: bool, opt_name: str, steps: int = 4):
         flat.zero_grad()
         losses.append(loss.detach())
     opt.join()
+    flat.finalize_grads()  # (a no-op unless the gradients are zeroed lazily, parallel/flat.py)
     torch.cuda.synchronize()
     return ([float(v) for v in losses], flat.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(),
             None if opt.master is None else opt.master.clone(), float(flat.grad.abs().sum()))
