@@ -13,7 +13,8 @@ restore then overwrites every parameter.  Around the model constructor::
         di.replay()
 
 on a restart (``TORCHELASTIC_RESTART_COUNT`` > 0) the ``torch.nn.init``
-functions only record their calls; ``replay()`` runs them later, in order,
+functions only record their calls (and the cyclic collector stays off until
+the restore or ``discard()`` / ``replay()``); ``replay()`` runs them later, in order,
 against the same Parameter objects (so it also reaches storage that
 ``FlatParams`` / ``.to()`` re-pointed them to).  Outside a restart, or with
 ``DWAMD_DEFER_INIT=0``, the context is a no-op and ``replay()`` does nothing.
@@ -24,6 +25,7 @@ agent (reference ``dlrover/python/elastic_agent/torch/training.py``).
 """
 
 import contextlib
+import gc
 import os
 from typing import Callable, List, Tuple
 
@@ -32,6 +34,29 @@ import torch.nn.init as _init
 
 _FNS = ("uniform_", "normal_", "trunc_normal_", "constant_", "ones_", "zeros_", "eye_", "dirac_",
         "xavier_uniform_", "xavier_normal_", "kaiming_uniform_", "kaiming_normal_", "orthogonal_", "sparse_")
+
+
+_GC_HELD = False
+
+
+def hold_gc():
+    """Keep the cyclic collector off through a restart's model build and
+    restore (a generation-2 pass over a model's worth of fresh objects cost
+    80-90 ms at random points of the build, profiles/r4 bench runs)."""
+    global _GC_HELD
+    if not _GC_HELD and gc.isenabled():
+        gc.disable()
+        _GC_HELD = True
+
+
+def release_gc():
+    """End :func:`hold_gc`: freeze what is alive now (model, optimizer,
+    restored state -- long-lived) out of later full collections, re-enable."""
+    global _GC_HELD
+    if _GC_HELD:
+        _GC_HELD = False
+        gc.freeze()
+        gc.enable()
 
 
 def restarting() -> bool:
@@ -50,6 +75,7 @@ class DeferredInit:
     def replay(self) -> int:
         """Run the recorded initialisers (once).  Returns how many ran."""
         if self.replayed or not self.calls:
+            release_gc()
             return 0
         self.replayed = True
         with torch.no_grad():
@@ -57,11 +83,13 @@ class DeferredInit:
                 fn(t, *args, **kwargs)
         n = len(self.calls)
         self.calls = []
+        release_gc()
         return n
 
     def discard(self):
         """The restore covered every parameter: drop the recorded calls."""
         self.calls = []
+        release_gc()
 
 
 @contextlib.contextmanager
@@ -74,6 +102,7 @@ def deferred_init(active: bool = None):
     if not active:
         yield d
         return
+    hold_gc()  # released by discard() / replay() or by the checkpoint restore
     saved = {}
     for name in _FNS:
         fn = getattr(_init, name, None)

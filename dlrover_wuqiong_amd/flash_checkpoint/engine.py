@@ -769,6 +769,9 @@ class CheckpointEngine(ABC):
                 self._gc_frozen = True
             if enabled:
                 gc.enable()
+            from .deferred_init import release_gc
+
+            release_gc()  # a restart's model build held the collector off (deferred_init.hold_gc)
 
     def _get_state_dict_from_memory(self, target: Any = None):
         t0, c0 = time.perf_counter(), time.thread_time()

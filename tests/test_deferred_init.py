@@ -51,3 +51,24 @@ def test_disabled_by_env(monkeypatch):
     with deferred_init() as di:
         GPT2(_cfg())
     assert not di.active and not di.calls
+
+
+def test_restart_build_holds_the_collector_until_the_restore():
+    import gc
+
+    from dlrover_wuqiong_amd.flash_checkpoint import deferred_init as dim
+
+    assert gc.isenabled()
+    with dim.deferred_init(active=True) as d:
+        torch.nn.Linear(4, 4)
+        assert not gc.isenabled()
+    assert not gc.isenabled()  # still held: the model build continues until the restore
+    d.discard()
+    assert gc.isenabled()
+    with dim.deferred_init(active=False):
+        assert gc.isenabled()
+    with dim.deferred_init(active=True) as d:
+        pass
+    d.replay()
+    assert gc.isenabled()
+    gc.unfreeze()
