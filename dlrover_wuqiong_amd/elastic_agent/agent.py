@@ -399,9 +399,23 @@ class ElasticTrainingAgent:
             })
         return env
 
+    def _standbys_useful(self) -> bool:
+        """A standby only ever becomes a worker at a restart: with the restart
+        budget spent on a fixed single-node job (no membership restarts
+        either) it would only compete with the live, just-recovered workers
+        -- its interpreter start, HIP context, HBM reservation (the driver
+        clears fresh VRAM) and shm pinning ran into their restore and first
+        checkpoint flushes (0.3-2.7 s save stalls, profiles/r4 bench runs)."""
+        return self.remaining_restarts > 0 or self.config.max_nodes > 1
+
     def _spawn_standbys(self):
         """Start one standby process per local rank for the next (re)start."""
         if not self.config.warm_standby:
+            return
+        if not self._standbys_useful():
+            if not getattr(self, "_standby_skip_logged", False):
+                self._standby_skip_logged = True
+                self._event("standby_skipped", reason="no restarts left")
             return
         deep = self.config.standby_mode == "deep"
         for lr in range(self.config.nproc_per_node):

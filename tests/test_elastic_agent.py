@@ -189,3 +189,16 @@ def test_import_standby_releases_reservation_under_pressure(monkeypatch):
     free["v"] = 10 << 30  # the worker grew: 10 GiB left < max(16 GiB, 6 % of 288)
     assert standby._release_under_pressure(20 << 30) == -1 and freed == [1]
     assert standby._release_under_pressure(-1) == -1 and freed == [1]  # released for good
+
+
+def test_no_standbys_once_the_restart_budget_is_spent():
+    from dlrover_wuqiong_amd.elastic_agent.agent import ElasticLaunchConfig, ElasticTrainingAgent
+
+    ag = ElasticTrainingAgent.__new__(ElasticTrainingAgent)
+    ag.config = ElasticLaunchConfig(max_nodes=1)
+    ag.remaining_restarts = 1
+    assert ag._standbys_useful()
+    ag.remaining_restarts = 0
+    assert not ag._standbys_useful()  # single node, no restart left: a standby could never run
+    ag.config = ElasticLaunchConfig(max_nodes=4)
+    assert ag._standbys_useful()  # membership changes still restart the workers
