@@ -21,7 +21,7 @@ def main():
     with torch.device(dev):
         model = GPT2(cfg)
     model.to(torch.bfloat16)
-    flat = FlatParams(model)
+    flat = FlatParams(model, lazy_zero_grad=True)
     opt = FusedAdamW(flat, lr=1e-4, max_grad_norm=1.0)
     data = torch.randint(0, cfg.vocab_size, (8, 1025), device=dev)
 
@@ -49,6 +49,17 @@ def main():
         cnt[key] += 1
     for k, v in agg.most_common(25):
         print(f"{v / 1000:8.2f} ms  x{cnt[k]:3d}  {k[0]}  {k[1]}  {k[2]}")
+    # every CPU op that launched device work, by call count (per-layer ones x48)
+    ops = collections.Counter()
+    dt = collections.Counter()
+    for e in p.events():
+        t = e.device_time_total if hasattr(e, "device_time_total") else e.cuda_time_total
+        if e.name.startswith("aten::") and t > 0:
+            ops[(e.name, str(e.input_shapes)[:90])] += 1
+            dt[(e.name, str(e.input_shapes)[:90])] += t
+    print("--- aten ops with device time, by count")
+    for k, n in ops.most_common(40):
+        print(f"x{n:4d}  {dt[k] / 1000:8.2f} ms  {k[0]}  {k[1]}")
 
 
 if __name__ == "__main__":
