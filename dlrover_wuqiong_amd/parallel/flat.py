@@ -104,7 +104,9 @@ class FlatParams:
             # runs before autograd accumulates ``grad`` into p.grad
             if self._fresh and i not in self._written:
                 self.claim(i)
-                self.params[i].grad.zero_()
+                g = self.params[i].grad
+                if g is not None:  # (detached by the user: autograd creates a fresh one)
+                    g.zero_()
             return None
         return hook
 
