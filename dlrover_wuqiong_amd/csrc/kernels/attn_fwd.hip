@@ -28,6 +28,12 @@
 //    query blocks are dispatched first.
 #include "attn_common.h"
 
+#ifndef DWAMD_FWD_DIAG_SKIP
+// causal diagonal tiles: a wave skips the QK^T / PV MFMAs of the 32-key
+// subtiles that lie wholly after its 32 queries (A/B; 0 = compute and mask)
+#define DWAMD_FWD_DIAG_SKIP 0
+#endif
+
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
@@ -200,6 +206,11 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
       // -m_i (row constant as the initial accumulator), so p = exp2(S') needs
       // no subtraction
       f32x16 s[C::NSB];
+      // subtiles [sb_hi, NSB) hold only keys after this wave's last query
+      // (causal, non-EXT): every score there is masked to -inf below
+      int sb_hi = C::NSB;
+      if (DWAMD_FWD_DIAG_SKIP && CAUSAL && !EXT && k0 + C::BK - 1 > q0 + 31 + co)
+        sb_hi = min(C::NSB, max(1, (q0 + 31 + co - k0) / 32 + 1));
       if (EXT) {  // (the EXT instances keep the explicit init: minit would spill them)
 #pragma unroll
         for (int sb = 0; sb < C::NSB; ++sb)
@@ -230,6 +241,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
         for (int kk = 0; kk < C::KK; ++kk)
 #pragma unroll
           for (int sb = 0; sb < C::NSB; ++sb) {
+            if (DWAMD_FWD_DIAG_SKIP && sb >= sb_hi) continue;  // wholly masked below
             const u32x4 kf = *(const u32x4*)(kl + kro[kk & 1] + row_const<D>(32 * sb, kk));
             s[sb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf), as_bf16x8(qf[kk]),
                                                             (kk == 0 && !EXT) ? minit : s[sb], 0, 0, 0);
@@ -321,6 +333,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
       // ---- O^T += V^T P^T : 4 k-steps of 16 keys
 #pragma unroll
       for (int sb = 0; sb < C::NSB; ++sb) {
+        if (DWAMD_FWD_DIAG_SKIP && sb >= sb_hi) continue;  // P == 0 there
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           const f32x16& a = s[sb];
