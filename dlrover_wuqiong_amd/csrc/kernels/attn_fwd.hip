@@ -30,7 +30,10 @@
 
 #ifndef DWAMD_FWD_DIAG_SKIP
 // causal diagonal tiles: a wave skips the QK^T / PV MFMAs of the 32-key
-// subtiles that lie wholly after its 32 queries (A/B; 0 = compute and mask)
+// subtiles that lie wholly after its 32 queries (A/B; 0 = compute and mask).
+// Measured SLOWER despite fewer MFMAs -- the per-subtile scalar branches
+// break the interleaved MFMA chains: GPT2 shape fwd 65.5 -> 73.1 us, D=128
+// S=4k 649 -> 702 us (profiles/r4/attn_fwd_diag_skip_ab.jsonl)
 #define DWAMD_FWD_DIAG_SKIP 0
 #endif
 
