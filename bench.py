@@ -171,6 +171,7 @@ def _job(a, n: int, mode: str, run_dir: str, tag: str):
     })
     if a.rehearse_shared_device:
         env["DWAMD_REHEARSE_SHARED_DEVICE"] = "1"
+        env["DWAMD_STANDBY_PG_BACKEND"] = "gloo"  # the standbys pre-form what the workers will ask for
     if mode == "import":
         # the reference's restart semantics: the replacement restores from
         # host shm (the framework default -- job "import_hbm" -- also gives
@@ -325,6 +326,9 @@ def summarize(a, run_dir, n, wall):
         "optimizer_update": phase0.get("optimizer_update"),
         "loss": phase0["loss"],
         "rccl_world": phase0["world"],
+        # incarnation 0 forms its world cold: the cost a restart would pay
+        # without the standbys' pre-formed group
+        "pg_init_cold_sec": (phase0.get("pg") or {}).get("init_sec"),
         "backend": phase0.get("backend"),
         # replicated state split 1/N across the node's ranks (each snapshots
         # and restores its slice; restores meet in an all-gather)
@@ -402,10 +406,15 @@ def _fault_summary(a, ev, agent, step_sec, save_sec):
                                        if inc1.get("standby") == "import" else None),
             "model_build_marks": inc1.get("build_marks") if inc1.get("standby") == "import" else None,
             "activate_to_pg_ready": round(inc1["t_pg"] - inc1["t_activated"], 3),
+            # init_process_group + first all-reduce of the restarted world
+            # (adopted: the standbys formed it while parked)
+            "pg_init": (inc1.get("pg") or {}).get("init_sec"),
             "ckpt_engine_init": round(inc1["t_ckpt"] - inc1["t_pg"], 3),
             "restore": round(inc1["restore_blocking_sec"] if late is not None else inc1["restore_sec"], 3),
             "first_step": round(first_step_end - inc1["t_restored"], 3),
         },
+        "pg_adopted_after_restart": (inc1.get("pg") or {}).get("adopted"),
+        "pg_preform_sec": (inc1.get("pg") or {}).get("preform_sec"),
         "standby_prepin_s": inc1.get("prepin_s"),
         "restore_source": inc1.get("restore_source"),
         "restore_gather": inc1.get("restore_gather"),
@@ -541,19 +550,28 @@ def worker(a) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     incarnation = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
-    if world > 1:
-        dist.init_process_group(backend, device_id=device if backend == "nccl" else None)
+    from dlrover_wuqiong_amd.elastic_agent import pg_preform
+
+    # a real RCCL world at every N (world 1 included): eager communicator
+    # init on this GPU.  A restarted standby whose set pre-formed the world
+    # while parked adopts it here (elastic_agent/pg_preform.py); otherwise
+    # this is the cold re-formation the recovery pays
+    t_pg0 = time.time()
+    pg_preform.init_process_group(backend, device_id=device if backend == "nccl" else None)
     assert world == a.gpus, f"world {world} != --gpus {a.gpus}"
     ddp = FlatDDP(model, flat, bucket_mb=128)
     opt.grad_scale = 1.0 / max(1, world)
-    if world > 1:
-        # the communicator is created lazily by the first collective: do it now
-        # so it is part of the measured re-formation, not of the first step
-        t = torch.ones(1, device=device)
-        dist.all_reduce(t)
-        if cuda:
-            torch.cuda.synchronize()
+    # the communicator answers (the first collective of an adopted group
+    # included) before the restore: part of the measured re-formation
+    t = torch.ones(1, device=device if backend == "nccl" else torch.device("cpu"))
+    dist.all_reduce(t)
+    if cuda:
+        torch.cuda.synchronize()
+    assert float(t.item()) == float(world)
     t_pg = time.time()
+    pg_info = {"adopted": pg_preform.adopted() is not None, "init_sec": round(t_pg - t_pg0, 4),
+               "preform_sec": (pg_preform.adopted() or {}).get("sec"),  # paid while parked
+               "backend": backend}
     g = torch.Generator(device="cpu").manual_seed(rank)
     data = torch.randint(0, cfg.vocab_size, (4, B, S + 1), generator=g).to(device)
     ckpt = DdpCheckpointer(a.ckpt_dir)
@@ -679,7 +697,7 @@ def worker(a) -> int:
         ckpt.wait_latest_checkpoint()
         sync_all()
         emit({"event": "phase0", "world": world, "step_sec": step_sec, "save_sec_mean": mx(dt),
-              "first_save_sec": first_save, "backend": backend})
+              "first_save_sec": first_save, "backend": backend, "pg": pg_info})
         s0 = step
         emit({"event": "fault_start", "t": time.time(), "s0": s0})
         start_step = step
@@ -778,7 +796,7 @@ def worker(a) -> int:
               "ckpt_bytes": ckpt_bytes, "first_save_sec": first_save, "timed_saves": len(save_times),
               "timed_saves_ok": timed_ok, "skipped_saves_timed": skipped_timed, "rehearsal": rehearsal,
               "backend": backend, "slices": ckpt.engine._num_slices, "hbm_plan": getattr(ckpt.engine, "hbm_plan", None),
-              "gather": ckpt.engine._gather_group is not None,
+              "gather": ckpt.engine._gather_group is not None, "pg": pg_info,
               "optimizer_update": "under next forward" if opt._overlap is not None else "compute stream"})
 
         # ---------------- DISK persist (agent: torch.save archive written from
@@ -889,6 +907,7 @@ def worker(a) -> int:
               "t_activated": t_act, "t_pg": t_pg, "t_ckpt": t_ckpt, "t_restored": t_restored,
               "build_marks": {k: round(v - t_proc, 3) for k, v in marks.items()},
               "prepin_s": info.get("prepin_s") if info else None, "standby": "deep" if info else "import",
+              "pg": pg_info,
               "restore_source": getattr(ckpt.engine, "last_restore_source", None),
               "restore_gather": getattr(ckpt.engine._copier, "last_restore_gather", None),
               "restore_phases": dict(getattr(ckpt.engine, "last_restore_breakdown", {}) or {},
@@ -940,7 +959,7 @@ def worker(a) -> int:
     ckpt.close()
     if world > 1:
         dist.barrier()
-        dist.destroy_process_group()
+    dist.destroy_process_group()
     return 0
 
 

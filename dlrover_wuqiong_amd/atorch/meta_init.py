@@ -238,6 +238,43 @@ def scatter_from_rank0(model: nn.Module, full: Optional[Dict[str, torch.Tensor]]
             p.data.copy_(t)
 
 
+def _init_meta_buffers(model: nn.Module, names, device, buffer_init_fn: Optional[Callable] = None):
+    """Buffers created under ``torch.device("meta")`` hold no values after
+    ``to_empty``.  Recompute them: ``buffer_init_fn(module)`` if given, else
+    a parameter-free module that carries its ``config`` (HF rotary
+    embeddings: ``inv_freq`` / ``original_inv_freq``) is rebuilt on the CPU
+    from that config and its buffers copied.  Anything else fails loudly --
+    training on uninitialised buffers is silent garbage."""
+    owners = {}
+    for n in names:
+        mod_name, _, buf = n.rpartition(".")
+        owners.setdefault(mod_name, []).append(buf)
+    unresolved = []
+    for mod_name, bufs in owners.items():
+        m = model.get_submodule(mod_name) if mod_name else model
+        if buffer_init_fn is not None:
+            buffer_init_fn(m)
+            continue
+        fresh = None
+        if getattr(m, "config", None) is not None and not list(m.parameters(recurse=False)):
+            try:
+                with torch.device("cpu"):
+                    fresh = type(m)(m.config)
+            except Exception:
+                fresh = None
+        if fresh is None:
+            unresolved += [f"{mod_name}.{b}" if mod_name else b for b in bufs]
+            continue
+        for b in bufs:
+            getattr(m, b).copy_(getattr(fresh, b).to(device))
+        for k, v in vars(fresh).items():  # derived scalars set next to the buffers (attention_scaling, ...)
+            if not k.startswith("_") and isinstance(v, (int, float)) and not isinstance(v, bool):
+                setattr(m, k, v)
+    if unresolved:
+        raise RuntimeError(f"buffers created on the meta device have no initialiser: {unresolved[:8]} "
+                           f"({len(unresolved)} total); pass buffer_init_fn or build them on a real device")
+
+
 @torch.no_grad()
 def materialize_sharded(model: nn.Module, device, cfg: Optional[dict] = None,
                         full_rank0: Optional[Dict[str, torch.Tensor]] = None) -> str:
@@ -245,12 +282,23 @@ def materialize_sharded(model: nn.Module, device, cfg: Optional[dict] = None,
     shards on ``device`` and fill them.  Returns the method used."""
     cfg = cfg or {}
     saved_buffers = {n: b.detach().clone() for n, b in model.named_buffers() if not b.is_meta}
+    meta_buffers = [n for n, b in model.named_buffers() if b.is_meta]
+    rank0_real = bool(cfg.get("sync_module_states") and cfg.get("_rank0_real"))
     model.to_empty(device=device)
     for n, b in model.named_buffers():
         if n in saved_buffers:
             b.copy_(saved_buffers[n])
+    if rank0_real:
+        # rank 0 built the real model: its buffers (rotary inv_freq, ...) are
+        # the truth; the other ranks' were created on meta and are garbage
+        # (reference atorch/utils/fsdp_init_util.py:340
+        # _sync_module_params_and_buffers)
+        for _n, b in model.named_buffers():
+            dist.broadcast(b.data, src=0)  # on `device` after to_empty
+    elif meta_buffers:
+        _init_meta_buffers(model, meta_buffers, device, cfg.get("buffer_init_fn"))
     init_fn: Optional[Callable] = cfg.get("param_init_fn")
-    if cfg.get("sync_module_states") and cfg.get("_rank0_real"):
+    if rank0_real:
         scatter_from_rank0(model, full_rank0, device)
         how = "scatter_from_rank0"
     elif cfg.get("init_from"):

@@ -297,6 +297,9 @@ class ElasticTrainingAgent:
             "DWAMD_STANDBY_MODE": self.config.standby_mode,  # the HBM-budget preflight sizes for it
         })
         env.setdefault("OMP_NUM_THREADS", "1")
+        # RCCL watchdog: a collective past DWAMD_COLLECTIVE_TIMEOUT_S tears the
+        # process down (the agent then restarts the group) instead of hanging
+        env.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "3")
         return env
 
     def _clear_ctl(self):
@@ -340,6 +343,7 @@ class ElasticTrainingAgent:
 
     def _start_workers(self):
         ranks, world_size = self._rendezvous()
+        adopt = self._can_adopt_pg(ranks, world_size)
         self._clear_ctl()
         self.workers = []
         warm = 0
@@ -350,16 +354,108 @@ class ElasticTrainingAgent:
                 os.makedirs(self.config.log_dir, exist_ok=True)
                 log_path = os.path.join(self.config.log_dir,
                                         f"{self.config.run_id}_r{self.restart_count}_rank{gr}.log")
-            p = self._activate_standby(lr, env, log_path)
+            p = self._activate_standby(lr, env, log_path, adopt)
+            if p is None and adopt:
+                # a standby of the pre-formed set vanished: the ones already
+                # activated wait in a group that can never complete -- stop
+                # them and start the whole local group without adoption
+                logger.warning("pre-formed group incomplete at activation: forming the world cold")
+                self._stop_workers(timeout=0)
+                self._discard_standbys()
+                self._clear_ctl()
+                self._start_group_cold(ranks, world_size)
+                return
             if p is None:
                 p = self._cold_start(env, log_path)
             else:
                 warm += 1
             self.workers.append(WorkerProcess(lr, gr, p, log_path))
         self._workers_started_at = time.time()
-        self._event("workers_started", warm=warm, n=len(self.workers))
+        self._preform_sent = False
+        self._event("workers_started", warm=warm, n=len(self.workers), pg_adopted=adopt)
         logger.info(f"started {len(self.workers)} workers (restart {self.restart_count}, "
-                    f"{warm} from warm standby)")
+                    f"{warm} from warm standby{', pre-formed process group adopted' if adopt else ''})")
+
+    def _start_group_cold(self, ranks: List[int], world_size: int):
+        self.workers = []
+        for lr, gr in enumerate(ranks):
+            env = self._worker_env(lr, gr, world_size)
+            log_path = ""
+            if self.config.log_dir:
+                log_path = os.path.join(self.config.log_dir,
+                                        f"{self.config.run_id}_r{self.restart_count}_rank{gr}.log")
+            self.workers.append(WorkerProcess(lr, gr, self._cold_start(env, log_path), log_path))
+        self._workers_started_at = time.time()
+        self._preform_sent = False
+        self._event("workers_started", warm=0, n=len(self.workers), pg_adopted=False)
+
+    # --------------------------------------- pre-formed process groups
+    def _preform_wanted(self) -> bool:
+        """Pre-form the standbys' communicator only when the world is this
+        node alone (the next world is then, barring a membership change,
+        exactly the standby set) -- see pg_preform.py."""
+        return (self.config.warm_standby and os.getenv("DWAMD_STANDBY_PREFORM", "1") == "1"
+                and len(self.world) == 1 and self.config.nproc_per_node >= 1)
+
+    def _pg_store_addr(self) -> str:
+        """The agent hosts the TCPStore the standbys rendezvous on (it never
+        touches the GPU; the store outlives every worker generation)."""
+        if getattr(self, "_pg_store", None) is None:
+            import datetime
+
+            import torch.distributed as dist
+
+            port = self._free_port()
+            self._pg_store = dist.TCPStore("127.0.0.1", port, is_master=True, wait_for_workers=False,
+                                           timeout=datetime.timedelta(seconds=300))
+            self._pg_store_port = port
+        return f"127.0.0.1:{self._pg_store_port}"
+
+    def _standbys_parked(self) -> bool:
+        from .standby import READY_PREFIX
+
+        if len(self._standby) < self.config.nproc_per_node:
+            return False
+        return all(p.poll() is None and os.path.exists(os.path.join(self.ctl_dir, READY_PREFIX + str(lr)))
+                   for lr, p in self._standby.items())
+
+    def _maybe_preform(self):
+        if getattr(self, "_preform_sent", False) or not self._preform_wanted() or not self._standbys_parked():
+            return
+        self._preform_sent = True
+        self._preform_gen = getattr(self, "_preform_gen", 0) + 1
+        spec = {"store": self._pg_store_addr(), "prefix": f"{self.config.run_id}/standby_pg/{self._preform_gen}/",
+                "world": self.config.nproc_per_node, "backend": os.getenv("DWAMD_STANDBY_PG_BACKEND", "auto"),
+                "timeout": float(os.getenv("DWAMD_STANDBY_PG_TIMEOUT", "120"))}
+        self._preform_prefix = spec["prefix"]
+        for lr, p in self._standby.items():
+            try:
+                p.stdin.write(json.dumps({"preform": spec}) + "\n")
+                p.stdin.flush()
+            except (BrokenPipeError, OSError):
+                pass
+        self._event("standby_pg_preform", world=spec["world"], gen=self._preform_gen)
+
+    def _can_adopt_pg(self, ranks: List[int], world_size: int) -> bool:
+        """Adopt the standbys' pre-formed group iff the new world is exactly
+        this node's local ranks 0..n-1 and every standby reported the group
+        of the current generation formed."""
+        from .pg_preform import PG_MARK_PREFIX
+
+        prefix = getattr(self, "_preform_prefix", None)
+        n = self.config.nproc_per_node
+        if prefix is None or world_size != n or ranks != list(range(n)) or len(self._standby) != n:
+            return False
+        for lr, p in self._standby.items():
+            if p.poll() is not None:
+                return False
+            try:
+                with open(os.path.join(self.ctl_dir, PG_MARK_PREFIX + str(lr))) as f:
+                    if f.read().split()[0] != prefix:
+                        return False
+            except (OSError, IndexError):
+                return False
+        return True
 
     def _cold_start(self, env: Dict[str, str], log_path: str) -> subprocess.Popen:
         cmd = [sys.executable, "-u"] + (["-m", self.entrypoint] if self.is_module else [self.entrypoint]) + self.args
@@ -452,14 +548,14 @@ class ElasticTrainingAgent:
                     return False
         return True
 
-    def _activate_standby(self, local_rank: int, env: Dict[str, str], log_path: str):
+    def _activate_standby(self, local_rank: int, env: Dict[str, str], log_path: str, adopt_pg: bool = False):
         p = self._standby.pop(local_rank, None)
         if p is None:
             return None
         if p.poll() is not None:
             return None
         cmd = {"env": env, "entry": self.entrypoint, "args": self.args, "module": self.is_module,
-               "log": log_path, "cwd": os.getcwd()}
+               "log": log_path, "cwd": os.getcwd(), "adopt_pg": adopt_pg}
         try:
             p.stdin.write(json.dumps(cmd) + "\n")
             p.stdin.close()
@@ -691,6 +787,8 @@ class ElasticTrainingAgent:
             if (self.config.warm_standby and not self._standby
                     and time.time() - self._workers_started_at > self.config.standby_delay):
                 self._spawn_standbys()
+            if self._standby:
+                self._maybe_preform()
             res = self._monitor_workers()
             now = time.time()
             if now - getattr(self, "_pdev_sampled_at", 0.0) > 5.0 and res.state == RunResult.HEALTHY:
@@ -863,13 +961,20 @@ def _local_ip() -> str:
 
 def launch_agent(config: ElasticLaunchConfig, entrypoint: str, args: List[str], master_addr: str,
                  is_module: bool = False) -> int:
+    global LAST_WORLD_NODES
     client = MasterClient(master_addr, node_id=config.node_rank)
     agent = ElasticTrainingAgent(config, entrypoint, args, client, is_module=is_module)
     try:
         return agent.run()
     finally:
+        # the launcher hosting the master keeps it up until every node of the
+        # FINAL world reported (an elastic job may have grown past min_nodes)
+        LAST_WORLD_NODES = len(agent.world)
         agent._stop_workers(timeout=5)
         shutil.rmtree(agent.ctl_dir, ignore_errors=True)
+
+
+LAST_WORLD_NODES = 0
 
 
 def wait_nodes_done(master_addr: str, run_id: str, nnodes: int, timeout: float = 15.0) -> bool:

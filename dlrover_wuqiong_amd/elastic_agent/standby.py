@@ -175,7 +175,8 @@ def standby_point(prepin_shm: bool = True, repin_interval: float = 0.25) -> Opti
     t0 = time.time()
     buf = b""
     fd = sys.stdin.fileno()
-    while True:
+    cmd = None
+    while cmd is None:
         if not pinned_marked and prepin_shm and _pinned_bytes() > 0:
             _mark(ctl, PINNED_PREFIX, lr, f"{_pinned_bytes()}\n")
             pinned_marked = True
@@ -187,16 +188,34 @@ def standby_point(prepin_shm: bool = True, repin_interval: float = 0.25) -> Opti
                 sys.stderr.flush()
                 os._exit(0)  # discarded by the agent (stdin closed)
             buf += chunk
-            if b"\n" in buf:
-                break
+            buf, cmd = _control_lines(buf, ctl, lr)
         elif prepin_shm:
             pin_s += _prepin_checkpoint_shm()
             _publish_hbm_staging(ctl, lr)
-    cmd = json.loads(buf.split(b"\n", 1)[0].decode())
     _apply(cmd)
+    from . import pg_preform
+
+    pg_preform.arm(bool(cmd.get("adopt_pg")))
     _activated = {"activated_at": time.time(), "waited_s": time.time() - t0, "prepin_s": pin_s,
-                  "pinned_bytes": _pinned_bytes()}
+                  "pinned_bytes": _pinned_bytes(), "pg_preformed": pg_preform.preformed()}
     return dict(_activated)
+
+
+def _control_lines(buf: bytes, ctl: str, lr: str):
+    """Consume complete JSON lines from the agent: ``preform`` requests are
+    served in place (pg_preform.py); the first other line is the activation
+    command.  Returns (rest of the buffer, activation command or None)."""
+    from . import pg_preform
+
+    while b"\n" in buf:
+        line, buf = buf.split(b"\n", 1)
+        if not line.strip():
+            continue
+        obj = json.loads(line.decode())
+        if pg_preform.handle_line(obj, ctl, lr):
+            continue
+        return buf, obj
+    return buf, None
 
 
 def activation_info() -> Optional[dict]:
@@ -314,10 +333,11 @@ def _release_under_pressure(reserved: int) -> int:
     return reserved
 
 
-def _wait_command(pin: bool, ctl: str, lr: str, interval: float = 0.25) -> bytes:
-    """Block until the agent's activation line arrives on stdin; meanwhile
-    keep this rank's checkpoint shm pinned (segments appear, or are
-    re-created at a new size, while the standby waits).  b"" = discarded."""
+def _wait_command(pin: bool, ctl: str, lr: str, interval: float = 0.25) -> Optional[dict]:
+    """Block until the agent's activation line arrives on stdin (served
+    ``preform`` requests on the way); meanwhile keep this rank's checkpoint
+    shm pinned (segments appear, or are re-created at a new size, while the
+    standby waits).  None = discarded."""
     import select
 
     buf = b""
@@ -325,7 +345,8 @@ def _wait_command(pin: bool, ctl: str, lr: str, interval: float = 0.25) -> bytes
     pinned_marked = False
     reserved = 0
     prof = None
-    while b"\n" not in buf:
+    cmd = None
+    while cmd is None:
         if pin:
             _prepin_checkpoint_shm()
             _publish_hbm_staging(ctl, lr)
@@ -346,9 +367,10 @@ def _wait_command(pin: bool, ctl: str, lr: str, interval: float = 0.25) -> bytes
         if r:
             chunk = os.read(fd, 1 << 20)
             if not chunk:
-                return b""
+                return None
             buf += chunk
-    return buf.split(b"\n", 1)[0]
+            buf, cmd = _control_lines(buf, ctl, lr)
+    return cmd
 
 
 def main():
@@ -377,11 +399,13 @@ def main():
     # import mode: torch + this package are imported; tell the agent (and
     # anyone waiting on the control dir) this standby can take over now
     _mark(ctl, READY_PREFIX, lr, f"{os.getpid()} {time.time()}\n")
-    line = _wait_command(gpu, ctl, lr)
-    if not line.strip():
+    cmd = _wait_command(gpu, ctl, lr)
+    if cmd is None:
         return 0  # agent discarded the standby
-    cmd = json.loads(line)
     _apply(cmd)
+    from . import pg_preform
+
+    pg_preform.arm(bool(cmd.get("adopt_pg")))
     _run_entry(cmd["entry"], cmd.get("args", []), cmd.get("module", False))
     return 0
 

@@ -550,6 +550,11 @@ class GpuCopier:
         if before_copy is not None:
             before_copy(idx)
         cur = torch.cuda.current_stream(self.device)
+        # a snapshot taken before the first optimizer step after a restart
+        # must not read optimizer state a deferred restore is still landing
+        from . import deferred_restore
+
+        deferred_restore.wait_all(cur, self.device)
         copy_stream = cur
         if self.overlap and n > 0:
             if self._snap_stream is None:

@@ -145,6 +145,13 @@ def wait_all(stream=None, device=None):
         d.wait(stream)
 
 
+def synchronize_all(device=None):
+    """Host-side wait until every pending deferred copy landed: before the
+    host memory they read (pinned shm) is unregistered or unmapped."""
+    for d in pending(device):
+        d.event.synchronize()
+
+
 def _step_pre_hook(optimizer, args, kwargs):
     if _PENDING:
         wait_all()

@@ -356,6 +356,11 @@ class CheckpointEngine(ABC):
             self._prepped_for = None
         if self._copier is not None:
             self._copier.wait()
+            # a deferred optimizer-state restore still DMAs from this
+            # segment's pinned pages on its side stream: let it land first
+            from . import deferred_restore
+
+            deferred_restore.synchronize_all()
             self._copier.pinned.release_all()
 
     def _start_shm_prep(self, total: int, prefault: bool):
@@ -1018,6 +1023,9 @@ class CheckpointEngine(ABC):
             if self._copier is not None:
                 self._copier.wait()
                 self._wait_own_lock_release(timeout=30)
+                from . import deferred_restore
+
+                deferred_restore.synchronize_all()  # late restore copies read the pinned shm
                 self._copier.close()
         finally:
             self._copier = None

@@ -148,15 +148,28 @@ class _FlatOptimizer(torch.optim.Optimizer):
 
     def load_state_dict(self, sd):
         st = sd["state"]
+        if self.exp_avg.is_cuda:
+            # a flash-checkpoint restore may still be landing this state on a
+            # side stream (deferred_restore.py): order these copies after it
+            from ..flash_checkpoint import deferred_restore
+
+            deferred_restore.wait_all()
+
+        def put(dst, src):
+            src = src.reshape(-1)
+            if src.data_ptr() == dst.data_ptr() and src.numel() == dst.numel() and src.dtype == dst.dtype:
+                return  # the restore wrote these views in place already
+            dst.copy_(src)
+
         with torch.no_grad():
             for i, (o, c) in enumerate(self.flat.offsets):
                 if i not in st:
                     continue
                 s = st[i]
-                self.exp_avg[o:o + c].copy_(s["exp_avg"].reshape(-1))
-                self.exp_avg_sq[o:o + c].copy_(s["exp_avg_sq"].reshape(-1))
+                put(self.exp_avg[o:o + c], s["exp_avg"])
+                put(self.exp_avg_sq[o:o + c], s["exp_avg_sq"])
                 if self.master is not None and "master_param" in s:
-                    self.master[o:o + c].copy_(s["master_param"].reshape(-1))
+                    put(self.master[o:o + c], s["master_param"])
                 self.step_count = int(float(s["step"]))
         for g, sg in zip(self.param_groups, sd.get("param_groups", [])):
             for k, v in sg.items():

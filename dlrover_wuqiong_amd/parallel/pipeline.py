@@ -327,10 +327,19 @@ class DecoderStackStage(PipelineStage):
         except Exception:
             return {"full_attention": None}
         kw = dict(config=cfg, inputs_embeds=x, attention_mask=None, past_key_values=None, position_ids=pos)
+        if self._uniform_sliding():
+            # Mistral-style: no per-layer types, every layer uses the window
+            # when the config sets one (MistralModel.forward's mask choice)
+            return {"sliding_attention": create_sliding_window_causal_mask(**kw)}
         out = {"full_attention": create_causal_mask(**kw)}
         if "sliding_attention" in (getattr(cfg, "layer_types", None) or []):
             out["sliding_attention"] = create_sliding_window_causal_mask(**kw)
         return out
+
+    def _uniform_sliding(self) -> bool:
+        cfg = self.parts_cfg
+        return (cfg is not None and not getattr(cfg, "layer_types", None)
+                and getattr(cfg, "sliding_window", None) is not None)
 
     def forward(self, *acts, targets=None):
         import torch.nn.functional as F
@@ -352,8 +361,9 @@ class DecoderStackStage(PipelineStage):
         if self.rotary is not None:
             kw["position_embeddings"] = self.rotary(x, pos)
         types = getattr(self.parts_cfg, "layer_types", None)
+        default_t = "sliding_attention" if self._uniform_sliding() else "full_attention"
         for i, layer in enumerate(self.layers):
-            t = types[self.start + i] if types else "full_attention"
+            t = types[self.start + i] if types else default_t
             out = layer(x, attention_mask=masks.get(t), **kw)
             x = out[0] if isinstance(out, (tuple, list)) else out
         if not self.is_last:

@@ -187,9 +187,9 @@ def run(a) -> int:
     finally:
         if master_proc is not None:
             if rc == 0 and cfg.max_nodes > 1:
-                from ..elastic_agent.agent import wait_nodes_done
+                from ..elastic_agent import agent as _agent
 
-                wait_nodes_done(master_addr, cfg.run_id, cfg.min_nodes)
+                _agent.wait_nodes_done(master_addr, cfg.run_id, max(cfg.min_nodes, _agent.LAST_WORLD_NODES))
             master_proc.terminate()
             try:
                 master_proc.wait(timeout=10)

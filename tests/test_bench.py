@@ -26,6 +26,10 @@ def test_bench_two_ranks_real_kill(tmp_path):
     assert res["steps"] == 8 and res["warmup"] == 2
     assert res["load_verified"] and res["replicas_identical"]
     assert res["restarts"] == 1 and res["load_verified_after_restart"]
+    # the deep standbys formed the restarted world while parked and the
+    # restarted workers adopted it (elastic_agent/pg_preform.py)
+    assert res["pg_adopted_after_restart"] is True and res["pg_preform_sec"] > 0
+    assert res["pg_init_cold_sec"] > 0 and res["recovery_breakdown_s"]["pg_init"] >= 0
     # plumbing check: on CPU a gpt2-tiny step is a few ms and the phase-0 step
     # time it is normalised by is noisy (the value itself is judged on GPUs)
     assert 0 < res["goodput_pct"] < 150
@@ -41,6 +45,7 @@ def test_bench_two_ranks_real_kill(tmp_path):
     # replacement process, restore from host shm (reference semantics)
     imp = res["import_mode"]
     assert imp["standby_mode"] == "import" and imp["restarts"] == 1 and imp["load_verified_after_restart"]
+    assert imp["pg_adopted_after_restart"] is True  # import standbys pre-form too
     assert res["load_sec_shm"] == imp["load_sec"] and res["goodput_pct_import"] == imp["goodput_pct"]
     assert res["recover_sec_import"] > 0 and imp["recovery_breakdown_s"]["process_to_model_built"] is not None
     # and under the framework default (import standbys owning the HBM tier)
@@ -66,3 +71,4 @@ def test_bench_eight_ranks_sliced(tmp_path):
     assert res["ckpt_slices"] == 8 and res["restore_gather_group"] is True
     assert res["load_verified"] and res["replicas_identical"] and res["timed_saves_ok"]
     assert res["restarts"] == 1 and res["load_verified_after_restart"]
+    assert res["pg_adopted_after_restart"] is True  # 8 standbys pre-formed the 8-rank world

@@ -535,3 +535,72 @@ def test_gpu_deferred_optimizer_restore_orders_the_first_step(tmp_path, monkeypa
     if defer:
         assert d.resident_sec(timeout=30) > 0
     ck.close()
+
+
+def _slow_late_copies(monkeypatch):
+    from dlrover_wuqiong_amd.flash_checkpoint import copier as cp
+
+    orig = cp.GpuCopier._pipelined_h2d
+
+    def slow(self, copies, stream, *a, **k):
+        if stream != torch.cuda.current_stream(self.device):
+            with torch.cuda.stream(stream):
+                torch.cuda._sleep(200_000_000)  # ~0.1 s of GPU cycles before the late copies
+        return orig(self, copies, stream, *a, **k)
+
+    monkeypatch.setattr(cp.GpuCopier, "_pipelined_h2d", slow)
+
+
+def test_gpu_deferred_restore_then_optimizer_load_state_dict(tmp_path, monkeypatch):
+    """The usual ``opt.load_state_dict(sd["optimizer"])`` right after an
+    in-place restore whose optimizer state is still landing on a side
+    stream: the views alias the live buffers, so nothing may be copied back
+    over them (stale bytes), and the first step must see the restored state."""
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+
+    _slow_late_copies(monkeypatch)
+    model, opt, flat = _model_and_opt()
+    ck = DdpCheckpointer(str(tmp_path / "ck"))
+    state = lambda: {"model": model.state_dict(), "optimizer": opt.state_dict()}  # noqa
+    assert ck.save_checkpoint(5, state(), storage_type=StorageType.MEMORY)
+    ck.wait_latest_checkpoint()
+    torch.cuda.synchronize()
+    want = flat.data.clone(), opt.exp_avg.clone(), opt.master.clone()
+    flat.data.zero_()
+    opt.exp_avg.fill_(3.0)
+    opt.master.fill_(-1.0)
+    sd = ck.load_checkpoint(target=state())
+    assert ck.engine.last_deferred_restore is not None
+    opt.load_state_dict(sd["optimizer"])
+    model.load_state_dict(sd["model"])
+    torch.cuda.synchronize()
+    for got, ref in zip((flat.data, opt.exp_avg, opt.master), want):
+        assert torch.equal(got, ref)
+    ck.close()
+
+
+def test_gpu_close_right_after_deferred_restore(tmp_path, monkeypatch):
+    """Closing the engine (unregister + unmap of the pinned shm) while a
+    deferred restore still DMAs from it: the close waits for those copies,
+    and the state lands intact."""
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+
+    _slow_late_copies(monkeypatch)
+    model, opt, flat = _model_and_opt()
+    ck = DdpCheckpointer(str(tmp_path / "ck"))
+    state = lambda: {"model": model.state_dict(), "optimizer": opt.state_dict()}  # noqa
+    assert ck.save_checkpoint(5, state(), storage_type=StorageType.MEMORY)
+    ck.wait_latest_checkpoint()
+    torch.cuda.synchronize()
+    want = opt.exp_avg.clone(), opt.master.clone()
+    opt.exp_avg.fill_(3.0)
+    opt.master.fill_(-1.0)
+    ck.load_checkpoint(target=state())
+    d = ck.engine.last_deferred_restore
+    assert d is not None and not d.complete
+    ck.close()
+    assert d.complete
+    torch.cuda.synchronize()
+    assert torch.equal(opt.exp_avg, want[0]) and torch.equal(opt.master, want[1])

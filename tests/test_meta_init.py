@@ -248,3 +248,57 @@ def _wreject(rank, world, port, q):
 def test_mixed_meta_without_sync_is_rejected_loudly():
     res = _run(_wreject, 2)
     assert [o for _r, o in res] == ["rejected", "rejected"], res
+
+
+class _RotaryLike(torch.nn.Module):
+    """Parameter-free module with a config-derived, non-persistent buffer
+    (the shape of HF rotary embeddings' ``inv_freq``)."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.config = config
+        d = config.hidden_size // config.num_attention_heads
+        self.register_buffer("inv_freq", 1.0 / (10000.0 ** (torch.arange(0, d, 2).float() / d)), persistent=False)
+
+
+def _want_inv_freq(cfg):
+    d = cfg.hidden_size // cfg.num_attention_heads
+    return 1.0 / (10000.0 ** (torch.arange(0, d, 2).float() / d))
+
+
+def _wbuf(rank, world, port, q, mode):
+    _env(rank, world, port)
+    try:
+        from dlrover_wuqiong_amd.atorch import distributed as adist
+        from dlrover_wuqiong_amd.atorch.auto_accelerate import auto_accelerate
+        from dlrover_wuqiong_amd.models.llama import Llama, LlamaDecoderLayer
+
+        adist.init_distributed("gloo")
+        cfg = _tiny()
+        real = mode == "rank0_real" and rank == 0
+        with torch.device("cpu" if real else "meta"):
+            model = Llama(cfg)
+            model.rot = _RotaryLike(cfg)
+        strat = {"wrap_cls": (LlamaDecoderLayer,)}
+        if mode == "rank0_real":
+            strat["sync_module_states"] = True
+        ok, res, _ = auto_accelerate(model, None, fused_optimizer=False, load_strategy=[("fsdp", strat)])
+        got = res.model.rot.inv_freq
+        q.put((rank, ("ok", bool(torch.equal(got.cpu(), _want_inv_freq(cfg))))))
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        traceback.print_exc()
+        q.put((rank, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["rank0_real", "all_meta"])
+def test_meta_buffers_are_initialised(mode):
+    """Buffers created on the meta device get real values on every rank:
+    rank 0's are broadcast (sync_module_states), or the owning module is
+    rebuilt from its config (all ranks meta)."""
+    res = _run(_wbuf, 2, mode)
+    assert [o for _r, o in res] == [("ok", True), ("ok", True)], res

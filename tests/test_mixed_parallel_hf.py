@@ -28,8 +28,11 @@ def _model(family):
     if family == "qwen2":
         cfg = tf.Qwen2Config(num_key_value_heads=2, **common)
         m = tf.Qwen2ForCausalLM(cfg)
-    elif family == "mistral":
-        cfg = tf.MistralConfig(num_key_value_heads=2, **common)
+    elif family in ("mistral", "mistral_sw"):
+        # mistral_sw: a 4-token window on 16-token sequences -- the stages
+        # must use the sliding-window mask the unsplit model uses
+        sw = 4 if family == "mistral_sw" else None
+        cfg = tf.MistralConfig(num_key_value_heads=2, sliding_window=sw, **common)
         m = tf.MistralForCausalLM(cfg)
     else:
         cfg = tf.GPTNeoXConfig(**common)
@@ -82,7 +85,7 @@ def _worker(rank, world, port, q, family):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("family", ["qwen2", "mistral", "gpt_neox"])
+@pytest.mark.parametrize("family", ["qwen2", "mistral", "mistral_sw", "gpt_neox"])
 def test_hf_tp2_pp2_dp2_matches_one_process(family):
     model = _model(family)
     opt = torch.optim.SGD(model.parameters(), lr=0.5)
