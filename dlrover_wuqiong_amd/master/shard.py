@@ -11,6 +11,8 @@ Parity: reference ``dlrover/python/master/shard/`` (``task_manager.py:37-297``,
 """
 
 import json
+import math
+import os
 import random
 import threading
 import time
@@ -91,31 +93,64 @@ class TextDatasetSplitter(DatasetSplitter):
 
 class StreamingDatasetSplitter(DatasetSplitter):
     """Unbounded stream: hands out the next ``shard_size`` offsets forever
-    (``dataset_size`` <= 0) or until ``dataset_size``."""
+    (``dataset_size`` <= 0) or until ``dataset_size`` records were issued.
 
-    def __init__(self, *a, **kw):
+    A stream may have several partitions (Kafka-style topics / files), each
+    with its own next unconsumed offset; shards are cut round-robin over the
+    partitions and ``ShardDef.name`` carries the partition name.  The offsets
+    are part of the checkpoint (:meth:`to_checkpoint`), so a restored master
+    resumes each partition where it stopped instead of replaying the stream
+    from offset 0 (reference ``PartitionOffsets`` +
+    ``StreamingDatasetSplitter.to_checkpoint/from_checkpoint``,
+    ``dataset_splitter.py:43-88,414-440``)."""
+
+    def __init__(self, *a, partition_offsets: Optional[Dict[str, int]] = None, shards_per_fetch: int = 16, **kw):
         super().__init__(*a, **kw)
-        self._offset = 0
+        self.partition_offsets: Dict[str, int] = dict(partition_offsets or {self.dataset_name: 0})
+        self._rr = 0  # next partition, round-robin
+        self.issued = 0  # records handed out so far (bounded streams stop at dataset_size)
+        self.shards_per_fetch = max(1, shards_per_fetch)
+
+    @property
+    def _offset(self) -> int:  # single-partition view (kept for callers/tests)
+        return sum(self.partition_offsets.values())
 
     def epoch_finished(self):
-        return self.dataset_size > 0 and self._offset >= self.dataset_size
+        return self.dataset_size > 0 and self.issued >= self.dataset_size
 
     def create_shards(self):
-        n = 16
         out = []
-        for _ in range(n):
-            if self.dataset_size > 0 and self._offset >= self.dataset_size:
+        parts = list(self.partition_offsets)
+        for _ in range(self.shards_per_fetch):
+            if self.epoch_finished():
                 break
-            end = self._offset + self.shard_size
+            name = parts[self._rr % len(parts)]
+            self._rr += 1
+            start = self.partition_offsets[name]
+            n = self.shard_size
             if self.dataset_size > 0:
-                end = min(end, self.dataset_size)
-            out.append(ShardDef(self.dataset_name, self._offset, end))
-            self._offset = end
+                n = min(n, self.dataset_size - self.issued)
+            out.append(ShardDef(name, start, start + n))
+            self.partition_offsets[name] = start + n
+            self.issued += n
         return out
+
+    def to_checkpoint(self) -> dict:
+        return {"partition_offsets": dict(self.partition_offsets), "rr": self._rr, "issued": self.issued}
+
+    def from_checkpoint(self, d: dict):
+        if d.get("partition_offsets"):
+            self.partition_offsets = {str(k): int(v) for k, v in d["partition_offsets"].items()}
+        self._rr = int(d.get("rr", 0))
+        self.issued = int(d.get("issued", 0))
+
+
+MAX_TASK_RETRIES = int(os.environ.get("DWAMD_MAX_TASK_RETRIES", "3"))
 
 
 class DatasetManager:
-    def __init__(self, task_type: int, batch_size: int, splitter: DatasetSplitter):
+    def __init__(self, task_type: int, batch_size: int, splitter: DatasetSplitter,
+                 max_task_retries: int = MAX_TASK_RETRIES):
         self.task_type = task_type
         self.batch_size = batch_size
         self.splitter = splitter
@@ -123,6 +158,8 @@ class DatasetManager:
         self.doing: Dict[int, tuple] = {}  # task_id -> (node_id, TaskDef, start_time)
         self._next_id = 0
         self.completed_steps = 0
+        self.max_task_retries = max_task_retries
+        self.failed_shards: List[ShardDef] = []  # dropped after max_task_retries failures
 
     def get_task(self, node_id: int) -> Optional[TaskDef]:
         if not self.todo and not self.splitter.epoch_finished():
@@ -138,6 +175,20 @@ class DatasetManager:
         self._next_id += 1
         return self._next_id
 
+    def _requeue(self, t: TaskDef, why: str) -> bool:
+        """Back to the todo queue unless the shard already failed
+        ``max_task_retries`` times: then it is dropped with an error (a poison
+        shard must not keep the job from ever finishing; reference
+        ``_check_exceed_max_task_retries``, batch_dataset_manager.py:140-152)."""
+        t.retry += 1
+        if t.retry > self.max_task_retries:
+            self.failed_shards.append(t.shard)
+            logger.error(f"shard {t.shard.name}[{t.shard.start}:{t.shard.end}) dropped after "
+                         f"{self.max_task_retries} retries (last: {why})")
+            return False
+        self.todo.appendleft(t)
+        return True
+
     def report_task_status(self, task_id: int, success: bool) -> Optional[TaskDef]:
         item = self.doing.pop(task_id, None)
         if item is None:
@@ -145,17 +196,16 @@ class DatasetManager:
         _node, t, _ts = item
         if success:
             n = t.shard.end - t.shard.start
-            self.completed_steps += max(1, n // max(1, self.batch_size))
+            self.completed_steps += max(1, math.ceil(n / max(1, self.batch_size)))
         else:
-            t.retry += 1
-            self.todo.appendleft(t)
+            self._requeue(t, "reported failed")
         return t
 
     def recover_tasks(self, node_id: int):
         back = [tid for tid, (n, _t, _s) in self.doing.items() if n == node_id]
         for tid in back:
             _n, t, _s = self.doing.pop(tid)
-            self.todo.appendleft(t)
+            self._requeue(t, f"worker {node_id} died")
         return len(back)
 
     def reassign_timeout_tasks(self, timeout: float):
@@ -163,25 +213,37 @@ class DatasetManager:
         late = [tid for tid, (_n, _t, s) in self.doing.items() if now - s > timeout]
         for tid in late:
             _n, t, _s = self.doing.pop(tid)
-            self.todo.appendleft(t)
+            self._requeue(t, f"not done within {timeout:.0f}s")
         return len(late)
 
     def finished(self) -> bool:
         return self.splitter.epoch_finished() and not self.todo and not self.doing
 
     def checkpoint(self) -> str:
-        shards = [[t.shard.start, t.shard.end, t.shard.record_indices] for t in self.todo]
-        shards += [[t.shard.start, t.shard.end, t.shard.record_indices] for (_n, t, _s) in self.doing.values()]
-        return json.dumps({"epoch": self.splitter.epoch, "todo": shards,
-                           "dataset_name": self.splitter.dataset_name})
+        """Unfinished shards (todo + doing, with their retry counts), the
+        epoch and the splitter's position (stream offsets)."""
+        tasks = [t for t in self.todo] + [t for (_n, t, _s) in self.doing.values()]
+        shards = [[t.shard.start, t.shard.end, t.shard.record_indices, t.shard.name, t.retry] for t in tasks]
+        d = {"epoch": self.splitter.epoch, "todo": shards, "dataset_name": self.splitter.dataset_name,
+             "completed_steps": self.completed_steps}
+        if hasattr(self.splitter, "to_checkpoint"):
+            d["splitter"] = self.splitter.to_checkpoint()
+        return json.dumps(d)
 
     def restore_checkpoint(self, content: str):
         d = json.loads(content)
         self.splitter.epoch = d.get("epoch", 0)
+        if "splitter" in d and hasattr(self.splitter, "from_checkpoint"):
+            self.splitter.from_checkpoint(d["splitter"])
+        self.completed_steps = int(d.get("completed_steps", self.completed_steps))
         self.todo.clear()
         self.doing.clear()
-        for s, e, idx in d.get("todo", []):
-            self.todo.append(TaskDef(self._alloc_id(), self.task_type, ShardDef(d["dataset_name"], s, e, idx)))
+        for item in d.get("todo", []):
+            s, e, idx = item[:3]
+            name = item[3] if len(item) > 3 else d["dataset_name"]
+            t = TaskDef(self._alloc_id(), self.task_type, ShardDef(name, s, e, idx))
+            t.retry = int(item[4]) if len(item) > 4 else 0
+            self.todo.append(t)
 
 
 class TaskManager:
@@ -196,14 +258,17 @@ class TaskManager:
 
     def new_dataset(self, batch_size: int, dataset_size: int, dataset_name: str, num_epochs: int = 1,
                     shuffle: bool = False, num_minibatches_per_shard: int = 1, task_type: int = TaskType.TRAINING,
-                    storage_type: str = "table"):
+                    storage_type: str = "table", partition_offsets: Optional[Dict[str, int]] = None):
         with self._lock:
             if dataset_name in self._datasets:
                 return
             shard_size = batch_size * max(1, num_minibatches_per_shard)
-            cls = {"text": TextDatasetSplitter, "stream": StreamingDatasetSplitter}.get(storage_type,
-                                                                                        TableDatasetSplitter)
-            splitter = cls(dataset_name, dataset_size, shard_size, num_epochs, shuffle)
+            if storage_type == "stream":
+                splitter = StreamingDatasetSplitter(dataset_name, dataset_size, shard_size, num_epochs, shuffle,
+                                                    partition_offsets=partition_offsets)
+            else:
+                cls = TextDatasetSplitter if storage_type == "text" else TableDatasetSplitter
+                splitter = cls(dataset_name, dataset_size, shard_size, num_epochs, shuffle)
             self._datasets[dataset_name] = DatasetManager(task_type, batch_size, splitter)
             logger.info(f"dataset {dataset_name}: size={dataset_size} shard={shard_size} epochs={num_epochs}")
 

@@ -215,3 +215,85 @@ def test_elastic_ps_cluster_versions(master):
     assert c.get_cluster_version(V.GLOBAL, NodeType.PS, 1) == 1
     nodes, ready, failed = c.query_ps_nodes()
     assert nodes == [] and not ready and not failed
+
+
+def test_streaming_restore_resumes_offsets_not_zero():
+    """A checkpointed streaming dataset resumes after the last issued offset
+    (the splitter position is part of the checkpoint): after the restored
+    in-flight / queued shards drain, the next shard starts where the stream
+    stopped, never at 0 again."""
+    from dlrover_wuqiong_amd.master.shard import TaskManager
+
+    tm = TaskManager()
+    tm.new_dataset(10, -1, "s", storage_type="stream")
+    done = []
+    for _ in range(20):  # consume shards up to offset 200
+        t = tm.get_dataset_task(0, "s")
+        done.append((t.shard.start, t.shard.end))
+        tm.report_dataset_task("s", t.task_id, True)
+    assert done[-1] == (190, 200)
+    ck = tm.get_dataset_checkpoint("s")
+    tm2 = TaskManager()
+    tm2.new_dataset(10, -1, "s", storage_type="stream")
+    assert tm2.restore_dataset_from_checkpoint(ck)
+    starts = [tm2.get_dataset_task(0, "s").shard.start for _ in range(40)]
+    assert min(starts) >= 200 and starts == sorted(starts) and len(set(starts)) == 40
+    assert tm2.get_dataset("s").completed_steps == 20
+
+
+def test_streaming_partitions_round_robin_and_checkpoint():
+    from dlrover_wuqiong_amd.master.shard import TaskManager
+
+    tm = TaskManager()
+    tm.new_dataset(5, 60, "p", storage_type="stream", partition_offsets={"a": 100, "b": 0})
+    got = []
+    while True:
+        t = tm.get_dataset_task(0, "p")
+        if t is None:
+            break
+        got.append((t.shard.name, t.shard.start, t.shard.end))
+        tm.report_dataset_task("p", t.task_id, True)
+        if len(got) == 4:
+            ck = tm.get_dataset_checkpoint("p")
+    assert got[:4] == [("a", 100, 105), ("b", 0, 5), ("a", 105, 110), ("b", 5, 10)]
+    assert sum(e - s for _n, s, e in got) == 60 and tm.finished()
+    tm2 = TaskManager()
+    tm2.new_dataset(5, 60, "p", storage_type="stream", partition_offsets={"a": 100, "b": 0})
+    tm2.restore_dataset_from_checkpoint(ck)
+    rest = []
+    while (t := tm2.get_dataset_task(0, "p")) is not None:
+        rest.append((t.shard.name, t.shard.start, t.shard.end))
+        tm2.report_dataset_task("p", t.task_id, True)
+    assert rest == got[4:]  # exactly the remainder, no replay
+
+
+def test_poison_shard_is_dropped_after_max_retries():
+    from dlrover_wuqiong_amd.master.shard import TaskManager
+
+    tm = TaskManager()
+    tm.new_dataset(10, 30, "d")
+    ds = tm.get_dataset("d")
+    fails = 0
+    for _ in range(200):
+        t = tm.get_dataset_task(0, "d")
+        if t is None:
+            break
+        ok = t.shard.start != 10  # the shard [10, 20) always fails
+        fails += not ok
+        tm.report_dataset_task("d", t.task_id, ok)
+    assert fails == ds.max_task_retries + 1  # first try + 3 retries, then dropped
+    assert [(s.start, s.end) for s in ds.failed_shards] == [(10, 20)]
+    assert tm.finished()
+    # dead-worker and timeout re-queues count as retries too
+    tm.new_dataset(7, 10, "e")
+    for _ in range(10):
+        t = tm.get_dataset_task(5, "e")
+        if t is None:
+            break
+        tm.recover_tasks(5)
+    assert tm.get_dataset("e").failed_shards and tm.get_dataset("e").finished()
+    # completed steps round up (7 records, batch 7 -> 1; 10 records, batch 4 -> 3)
+    tm.new_dataset(4, 10, "f", num_minibatches_per_shard=3)
+    t = tm.get_dataset_task(0, "f")
+    tm.report_dataset_task("f", t.task_id, True)
+    assert tm.get_dataset("f").completed_steps == 3
