@@ -768,6 +768,14 @@ class ElasticTrainingAgent:
                 ok = run_network_check(self.config, self.client)
                 if not ok:
                     raise NodeCheckFailedError(f"node {self.config.node_rank} failed the network check")
+            if self.config.comm_perf_test:
+                from .node_check import run_comm_perf_check
+
+                ok, rep = run_comm_perf_check(self.config, self.client)
+                self._event("comm_perf", ok=ok, allreduce_busbw_gbps=rep.get("allreduce_busbw_gbps"),
+                            slow_links=rep.get("slow_links"), slow_node=rep.get("slow_node"))
+                if not ok:
+                    raise NodeCheckFailedError(f"node {self.config.node_rank} failed the comm perf check")
             self._start_workers()
             AsyncCheckpointSaver.register_signal_handler()
             self._install_signal_handlers()
