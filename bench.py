@@ -335,6 +335,7 @@ def summarize(a, run_dir, n, wall):
         "ckpt_slices": phase0.get("slices"),
         "restore_gather_group": phase0.get("gather"),
         "hbm_plan": phase0.get("hbm_plan"),  # per-GPU budget preflight (flash_checkpoint/hbm_budget.py)
+        "host_plan": phase0.get("host_plan"),  # node host-memory (tmpfs) plan of the checkpoint shm
         "launcher_wall_s": round(wall, 1),
     }
     persist = next((e for e in ev if e["event"] == "persisted"), None)
@@ -796,6 +797,7 @@ def worker(a) -> int:
               "ckpt_bytes": ckpt_bytes, "first_save_sec": first_save, "timed_saves": len(save_times),
               "timed_saves_ok": timed_ok, "skipped_saves_timed": skipped_timed, "rehearsal": rehearsal,
               "backend": backend, "slices": ckpt.engine._num_slices, "hbm_plan": getattr(ckpt.engine, "hbm_plan", None),
+              "host_plan": getattr(ckpt.engine, "host_plan", None),
               "gather": ckpt.engine._gather_group is not None, "pg": pg_info,
               "optimizer_update": "under next forward" if opt._overlap is not None else "compute stream"})
 

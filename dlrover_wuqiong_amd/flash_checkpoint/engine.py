@@ -200,6 +200,7 @@ class CheckpointEngine(ABC):
         self.last_storage_load_stats: Dict[str, float] = {}
         self.speculation_misses = 0  # speculative snapshots redone after the state dict changed
         self.last_restore_breakdown: Dict[str, float] = {}  # host seconds per restore phase
+        self.host_plan: Optional[dict] = None  # node host-memory plan of the shm segment(s) (hbm_budget.host_plan)
         self._notify_agent_to_create_saver()
         self._update_saver_config()
         from .replica import CkptReplicaManager
@@ -304,8 +305,9 @@ class CheckpointEngine(ABC):
             if need_resize:
                 self._ctl_barrier()
                 if self._local_rank == 0:
+                    slots = self._plan_host_memory(total, segments=1)
                     h.close()
-                    h.init_shared_memory(create=True, size=total, owner=self._owner_id)
+                    h.init_shared_memory(create=True, size=total, owner=self._owner_id, slots=slots)
                 self._ctl_barrier()
                 if self._local_rank != 0:
                     h.close()
@@ -313,8 +315,9 @@ class CheckpointEngine(ABC):
                 self._generation += 1
                 self._next_slot = None
         elif need_resize:
+            slots = self._plan_host_memory(total, segments=max(1, self.local_shard_num))
             h.close()
-            h.init_shared_memory(create=True, size=total, owner=self._owner_id)
+            h.init_shared_memory(create=True, size=total, owner=self._owner_id, slots=slots)
             self._generation += 1
             self._next_slot = None
         if need_resize:
@@ -325,6 +328,36 @@ class CheckpointEngine(ABC):
             # make sure every slot this rank writes is pinned before its flush
             self._prepped_for = key
             self._start_shm_prep(total, prefault=need_resize)
+
+    def _plan_host_memory(self, payload: int, segments: int) -> Optional[int]:
+        """Host-memory preflight before the node's checkpoint segment(s) are
+        (re)created (hbm_budget.host_plan): the slot count that fits, or a
+        clean HostMemoryError instead of a SIGBUS on first touch.
+        ``DWAMD_HOST_BUDGET=off`` skips it."""
+        self.host_plan = None
+        if os.environ.get("DWAMD_HOST_BUDGET", "on") == "off":
+            return None
+        import glob
+
+        from ..common.multi_process import shm_name
+        from .hbm_budget import HostMemoryError, host_plan
+
+        prefix = shm_name("seg", CheckpointSharedObjPrefix.SHM_NAME)
+        mine = 0
+        for f in glob.glob("/dev/shm/" + prefix.lstrip("/") + "*"):
+            try:
+                mine += os.stat(f).st_blocks * 512  # pages this job's segments hold now
+            except OSError:
+                pass
+        p = host_plan(payload, segments, want_slots=self._shm_handler.max_slots, reclaimable=mine)
+        self.host_plan = p.as_dict()
+        if not p.fits:
+            raise HostMemoryError(f"flash checkpoint: {p.notes.get('slots')}; set DWAMD_HOST_RESERVE_GB lower, "
+                                  f"free host memory or save to storage only")
+        if p.notes:
+            logger.warning(f"rank {self._rank}: host memory plan: {p.notes['slots']}")
+        logger.info(f"rank {self._rank}: host memory plan {self.host_plan}")
+        return p.slots
 
     def _log_hbm_plan(self, payload: int):
         """HBM-budget preflight (hbm_budget.py) for this GPU, logged once per
@@ -495,7 +528,7 @@ class CheckpointEngine(ABC):
             # not a saving rank (e.g. a data-parallel replica of a TP/PP shard):
             # still takes part in the slot vote of the saving ranks
             if dist.is_available() and dist.is_initialized():
-                t = torch.ones(self._shm_handler.num_slots, dtype=torch.int64)
+                t = torch.ones(self._shm_handler.max_slots, dtype=torch.int64)
                 dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self._ctl_group)
             return False
         t0 = time.perf_counter()
@@ -625,7 +658,9 @@ class CheckpointEngine(ABC):
         Shard owners vote with per-slot flags (gloo MIN) so all ranks agree."""
         n = h.num_slots
         order = [self._next_slot] + [s for s in range(n) if s != self._next_slot]
-        flags = [1] * n
+        # the vote always carries max_slots flags (a 1-slot segment marks the
+        # rest unusable): every rank's tensor has the same shape
+        flags = [1] * n + [0] * (h.max_slots - n)
         acquired = {}
         if self._is_shard_owner:
             complete = h.complete_steps()
@@ -638,7 +673,7 @@ class CheckpointEngine(ABC):
                 if ok:
                     acquired[s] = True
         elif not has_state:
-            flags = [0] * n
+            flags = [0] * h.max_slots
         if dist.is_available() and dist.is_initialized():
             t = torch.tensor(flags, dtype=torch.int64)
             dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self._ctl_group)

@@ -129,3 +129,106 @@ def plan(total: int, worker_state: int, worker_peak: int, payload: int, world_lo
                    staging_bytes=st_bytes, standby=standby, standby_bytes=sb_bytes, gather_chunk=ch,
                    gather_temp_bytes=temp, restore_peak=restore_peak,
                    fits=steady <= total and restore_peak <= total, notes=notes)
+
+
+# ------------------------------------------------------------------ host side
+class HostMemoryError(RuntimeError):
+    """The node's host memory cannot hold even one checkpoint slot."""
+
+
+def read_meminfo(path: str = "/proc/meminfo") -> Dict[str, int]:
+    out = {}
+    try:
+        with open(path) as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                parts = v.split()
+                if parts:
+                    out[k.strip()] = int(parts[0]) * (1024 if len(parts) > 1 and parts[1] == "kB" else 1)
+    except OSError:
+        pass
+    return out
+
+
+def shm_free_bytes(path: str = "/dev/shm") -> int:
+    try:
+        st = os.statvfs(path)
+        return st.f_bavail * st.f_frsize
+    except OSError:
+        return 0
+
+
+def host_reserve(mem_total: int) -> int:
+    """Host RAM kept for everything that is not checkpoint shm (the
+    processes' own memory, page cache for data loading, pinned staging)."""
+    gb = os.environ.get("DWAMD_HOST_RESERVE_GB")
+    return int(float(gb) * GiB) if gb else max(8 * GiB, mem_total // 20)
+
+
+@dataclass
+class HostPlan:
+    segments: int  # checkpoint segments on this node (1 replicated, one per local shard otherwise)
+    slot_bytes: int  # per segment per slot (aligned payload)
+    slots: int  # 2 (double-buffered: a save never overwrites the latest checkpoint), 1, or 0 = does not fit
+    need_bytes: int  # segments x (header + slots x slot_bytes)
+    shm_free: int
+    mem_available: int
+    reclaimable: int  # bytes of this job's existing segments (replaced by the new ones)
+    reserve: int
+    room: int
+    pin_sec_est: float  # first-save prefault + hipHostRegister of one segment at DWAMD_PIN_GBPS
+    fits: bool
+    notes: Dict[str, str] = field(default_factory=dict)
+
+    def as_dict(self) -> dict:
+        d = asdict(self)
+        for k in list(d):
+            if k.endswith("bytes") or k in ("shm_free", "mem_available", "reclaimable", "reserve", "room"):
+                d[k + "_gib"] = round(d.pop(k) / GiB, 2)
+        return d
+
+
+def host_plan(payload: int, segments: int, want_slots: int = 2, shm_free: Optional[int] = None,
+              meminfo: Optional[Dict[str, int]] = None, reclaimable: int = 0,
+              reserve: Optional[int] = None, pin_gbps: Optional[float] = None) -> HostPlan:
+    """Node-level host memory plan of the flash-checkpoint shm (tmpfs).
+
+    tmpfs over-commits: a segment is created at any size and its pages are
+    allocated on first touch, so an undersized node dies with SIGBUS in the
+    middle of a snapshot flush instead of failing cleanly.  Sized here
+    before any segment exists: room = min(free /dev/shm, MemAvailable -
+    reserve) + this job's segments that the new ones replace.  Two slots
+    when they fit, one (with a warning: a crash during a save then loses the
+    in-memory checkpoint) when only one does, else :class:`HostMemoryError`.
+
+    Reference: ``ckpt_saver.py:140`` ``_create_shared_memory`` creates the
+    segment unconditionally."""
+    from .shm_handler import HEADER_BYTES, SLOT_ALIGN
+
+    mi = read_meminfo() if meminfo is None else meminfo
+    shm_free = shm_free_bytes() if shm_free is None else shm_free
+    mem_avail = mi.get("MemAvailable", 0)
+    reserve = host_reserve(mi.get("MemTotal", 0)) if reserve is None else reserve
+    slot = (payload + SLOT_ALIGN - 1) // SLOT_ALIGN * SLOT_ALIGN
+    room = max(0, min(shm_free, mem_avail - reserve)) + reclaimable
+    notes = {}
+    slots = 0
+    for s in range(max(1, want_slots), 0, -1):
+        if segments * (HEADER_BYTES + s * slot) <= room:
+            slots = s
+            break
+    if 0 < slots < want_slots:
+        notes["slots"] = (f"{want_slots} slots need {segments * want_slots * slot / GiB:.1f} GiB of host shm, "
+                          f"{room / GiB:.1f} GiB available: {slots} slot (a failure during a save loses the "
+                          f"in-memory checkpoint; storage is the fallback)")
+    elif slots == 0:
+        notes["slots"] = (f"one slot needs {segments * slot / GiB:.1f} GiB of host shm, only {room / GiB:.1f} GiB "
+                          f"available (/dev/shm free {shm_free / GiB:.1f}, MemAvailable {mem_avail / GiB:.1f}, "
+                          f"reserve {reserve / GiB:.1f})")
+    rate = float(os.environ.get("DWAMD_PIN_GBPS", "2.7")) if pin_gbps is None else pin_gbps
+    n_slots = max(slots, 1)
+    return HostPlan(segments=segments, slot_bytes=slot, slots=slots,
+                    need_bytes=segments * (HEADER_BYTES + n_slots * slot), shm_free=shm_free,
+                    mem_available=mem_avail, reclaimable=reclaimable, reserve=reserve, room=room,
+                    pin_sec_est=round(n_slots * slot / (rate * 1e9), 2) if rate > 0 else 0.0,
+                    fits=slots > 0, notes=notes)

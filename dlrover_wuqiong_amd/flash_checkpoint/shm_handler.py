@@ -104,7 +104,12 @@ def slot_lock_name(local_shard_id: int, slot: int) -> str:
 class SharedMemoryHandler:
     def __init__(self, local_shard_id: int, host: bool = True, num_slots: Optional[int] = None):
         self.local_shard_id = local_shard_id
-        self.num_slots = num_slots or default_num_slots()
+        # capacity (metadata dicts / slot locks exist for this many slots);
+        # ``num_slots`` is the segment's active count: the host-memory plan
+        # may create it with fewer (hbm_budget.host_plan), readers adopt the
+        # count from the segment header
+        self.max_slots = num_slots or default_num_slots()
+        self.num_slots = self.max_slots
         self._shm_name = CheckpointSharedObjPrefix.SHM_NAME + str(local_shard_id)
         self.metas = [SharedDict(f"{CheckpointSharedObjPrefix.META_NAME}{local_shard_id}_{s}", create=True)
                       for s in range(self.num_slots)]
@@ -122,10 +127,13 @@ class SharedMemoryHandler:
     def _stride(size: int) -> int:
         return (size + SLOT_ALIGN - 1) // SLOT_ALIGN * SLOT_ALIGN
 
-    def init_shared_memory(self, create: bool = False, size: int = 0, owner: int = 0) -> bool:
+    def init_shared_memory(self, create: bool = False, size: int = 0, owner: int = 0,
+                           slots: Optional[int] = None) -> bool:
         """Create (``size`` payload bytes per slot) or attach the segment.
         ``owner`` (create only): the writing job's id; a segment another job
-        wrote is re-created instead of reused (its steps are not ours)."""
+        wrote is re-created instead of reused (its steps are not ours).
+        ``slots`` (create only): active slot count of a new segment (<=
+        ``max_slots``; default all)."""
         if self.shared_memory is not None and self.shared_memory.stale():
             self.close()  # re-created by a writer (resize): drop the old mapping
         if self.shared_memory is not None:
@@ -145,6 +153,7 @@ class SharedMemoryHandler:
                     # never resize in place: a reader's mapping could fault (SIGBUS)
                     SharedMemory(self._shm_name, create=False).unlink()
                 stride = self._stride(size)
+                self.num_slots = max(1, min(self.max_slots, slots or self.max_slots))
                 self.shared_memory = SharedMemory(self._shm_name, create=True,
                                                   size=HEADER_BYTES + stride * self.num_slots)
             else:
@@ -162,10 +171,12 @@ class SharedMemoryHandler:
             self._header[OWNER_WORD] = owner
             for m in self.metas:
                 m.set({})
-        elif int(self._header[0]) != MAGIC or int(self._header[4]) != self.num_slots:
+        elif int(self._header[0]) != MAGIC or not 1 <= int(self._header[4]) <= self.max_slots:
             logger.warning(f"shm {self._shm_name}: incompatible header; ignoring it")
             self.close()
             return False
+        else:
+            self.num_slots = int(self._header[4])  # the creator's (host-memory plan) decision
         self._need_creation = False
         return True
 

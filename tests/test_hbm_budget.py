@@ -105,3 +105,93 @@ def test_chunked_gather_scatter_plan_covers_payload(per, world, chunk):
                     assert x not in dst_of
                     dst_of[x] = dst + (x - off)
     assert sorted(dst_of) == list(range(payload))
+
+
+# ----------------------------------------------------- node host-memory plan
+def _mi(total_gib, avail_gib):
+    return {"MemTotal": int(total_gib * GiB), "MemAvailable": int(avail_gib * GiB)}
+
+
+def test_host_plan_gpt2_1p5b_ddp_n8_two_slots():
+    # replicated: ONE node segment (the 8 ranks write 1/8 slices of it)
+    p = hb.host_plan(int(21.8 * GiB), segments=1, shm_free=1000 * GiB, meminfo=_mi(2048, 1900), reserve=64 * GiB)
+    assert p.fits and p.slots == 2 and not p.notes
+    assert p.need_bytes >= 2 * int(21.8 * GiB)
+    d = p.as_dict()
+    assert d["slots"] == 2 and d["need_bytes_gib"] >= 43.6
+
+
+def test_host_plan_llama3_8b_fsdp_n8():
+    # FSDP: one segment per rank, 1/8 of bf16 params + fp32 master + Adam (16 B/param)
+    shard = int(8.03e9 * 16 / 8)
+    p = hb.host_plan(shard, segments=8, shm_free=1000 * GiB, meminfo=_mi(2048, 1900), reserve=64 * GiB)
+    assert p.fits and p.slots == 2
+    # a node with 200 GiB of shm: one slot only
+    p = hb.host_plan(shard, segments=8, shm_free=200 * GiB, meminfo=_mi(2048, 1900), reserve=64 * GiB)
+    assert p.slots == 1 and "1 slot" in p.notes["slots"]
+
+
+def test_host_plan_llama3_70b_tp8():
+    shard = int(123.5 * GiB)  # per-rank TP=8 shard payload (profiles/megatron_llama3_70b_tp8_shard.log)
+    # 8 x 2 x 123.5 GiB = 1976 GiB does not fit 1.5 TiB of shm, one slot does
+    p = hb.host_plan(shard, segments=8, shm_free=1536 * GiB, meminfo=_mi(2048, 1900), reserve=64 * GiB)
+    assert p.fits and p.slots == 1
+    assert p.pin_sec_est > 40  # ~46 s measured for one 123.5 GB shard's first pinning
+    # a node whose MemAvailable (not tmpfs size) is the limit
+    p = hb.host_plan(shard, segments=8, shm_free=4096 * GiB, meminfo=_mi(1024, 900), reserve=64 * GiB)
+    assert not p.fits and p.slots == 0 and "only" in p.notes["slots"]
+    # this job's old segments are replaced, so their pages count as room
+    p = hb.host_plan(shard, segments=8, shm_free=4096 * GiB, meminfo=_mi(1024, 900), reserve=64 * GiB,
+                     reclaimable=8 * shard)
+    assert p.fits and p.slots == 1
+
+
+def test_host_plan_reads_statvfs_and_meminfo(monkeypatch, tmp_path):
+    import collections
+
+    mi = tmp_path / "meminfo"
+    mi.write_text("MemTotal:       65536000 kB\nMemAvailable:   32768000 kB\nShmem: 10 kB\n")
+    vfs = collections.namedtuple("vfs", "f_bavail f_frsize")
+    monkeypatch.setattr(hb.os, "statvfs", lambda p: vfs(10 * (GiB // 4096), 4096))
+    got = hb.read_meminfo(str(mi))
+    assert got["MemAvailable"] == 32768000 * 1024 and got["MemTotal"] == 65536000 * 1024
+    assert hb.shm_free_bytes() == 10 * GiB
+    monkeypatch.setattr(hb, "read_meminfo", lambda path="/proc/meminfo": got)
+    p = hb.host_plan(3 * GiB, segments=1)  # 2 x 3 GiB fits the 10 GiB tmpfs
+    assert p.slots == 2 and p.shm_free == 10 * GiB
+    p = hb.host_plan(7 * GiB, segments=1)
+    assert p.slots == 1
+
+
+def test_engine_creates_one_slot_segment_when_two_do_not_fit(tmp_path, monkeypatch):
+    """End to end on CPU: the engine asks the plan before creating the
+    segment; with room for one slot it creates a 1-slot segment, saves and
+    restores through it (readers adopt the slot count from the header); with
+    room for none it raises HostMemoryError instead of risking SIGBUS."""
+    from dlrover_wuqiong_amd.flash_checkpoint import engine as eng_mod
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+
+    real = hb.host_plan
+    monkeypatch.setattr(hb, "host_plan", lambda payload, segments, want_slots=2, reclaimable=0, **kw: real(
+        payload, segments, want_slots, shm_free=int(1.5 * payload) + (1 << 20), meminfo=_mi(1024, 1000),
+        reserve=0, reclaimable=0))
+    w = torch.nn.Linear(512, 512)
+    ck = DdpCheckpointer(str(tmp_path / "ck"))
+    assert ck.save_checkpoint(3, {"model": w.state_dict(), "step": 3}, storage_type=StorageType.MEMORY)
+    ck.wait_latest_checkpoint()
+    h = ck.engine._shm_handler
+    assert h.num_slots == 1 and ck.engine.host_plan["slots"] == 1
+    assert ck.save_checkpoint(4, {"model": w.state_dict(), "step": 4}, storage_type=StorageType.MEMORY)
+    ck.wait_latest_checkpoint()
+    sd = ck.load_checkpoint()
+    assert sd["step"] == 4 and torch.equal(sd["model"]["weight"], w.weight)
+    ck.close()
+    monkeypatch.setattr(hb, "host_plan", lambda payload, segments, want_slots=2, reclaimable=0, **kw: real(
+        payload, segments, want_slots, shm_free=1 << 20, meminfo=_mi(1024, 1000), reserve=0))
+    ck2 = DdpCheckpointer(str(tmp_path / "ck2"))
+    big = torch.nn.Linear(1024, 1024)  # a new size: the segment is re-created
+    with pytest.raises(hb.HostMemoryError):
+        ck2.save_checkpoint(5, {"model": big.state_dict(), "step": 5}, storage_type=StorageType.MEMORY)
+    ck2.close()
+    del eng_mod
