@@ -422,6 +422,8 @@ class AtorchTrainer:
                 break
         if self._checkpointer is not None and hasattr(self._checkpointer, "wait_latest_checkpoint"):
             self._checkpointer.wait_latest_checkpoint()
+        if args.load_best_model_at_end and self.state.best_model_checkpoint:
+            self._load_best_model()
         runtime = time.time() - start
         metrics = {"train_runtime": round(runtime, 4), "train_loss": float(tr_loss) / max(1, self.state.global_step),
                    "global_step": self.state.global_step}
@@ -437,57 +439,188 @@ class AtorchTrainer:
     # ---------------------------------------------------------------- eval
     def get_eval_dataloader(self, eval_dataset=None):
         ds = eval_dataset if eval_dataset is not None else self.eval_dataset
-        sampler = None
+        bs = self.args.per_device_eval_batch_size
         if dist.is_initialized() and dist.get_world_size() > 1:
-            sampler = torch.utils.data.distributed.DistributedSampler(ds, shuffle=False)
-        return torch.utils.data.DataLoader(ds, batch_size=self.args.per_device_eval_batch_size, sampler=sampler,
-                                           collate_fn=self.data_collator)
+            # contiguous runs of whole batches per rank: the rank-ordered
+            # gather is the dataset order, and padding batches are whole
+            # batches the loop runs (matched collectives) but does not record
+            bsm = DistributedEvalBatchSampler(len(ds), bs, dist.get_world_size(), dist.get_rank())
+            return torch.utils.data.DataLoader(ds, batch_sampler=bsm, collate_fn=self.data_collator)
+        return torch.utils.data.DataLoader(ds, batch_size=bs, collate_fn=self.data_collator)
 
-    @torch.no_grad()
-    def evaluate(self, eval_dataset=None, metric_key_prefix: str = "eval") -> Dict[str, float]:
-        dl = self.get_eval_dataloader(eval_dataset)
+    def _logits(self, out):
+        if torch.is_tensor(out):
+            return out
+        if isinstance(out, dict) or hasattr(out, "keys"):
+            for k in (self.args.logit_names or ["logits"]):
+                if k in out:
+                    return out[k]
+            return None
+        if hasattr(out, "logits"):
+            return out.logits
+        if isinstance(out, (tuple, list)) and len(out) > 1:
+            return out[self.args.logit_index]
+        return None
+
+    @staticmethod
+    def _labels(inputs):
+        if isinstance(inputs, dict):
+            for k in ("labels", "label", "label_ids", "targets"):
+                if k in inputs and torch.is_tensor(inputs[k]):
+                    return inputs[k]
+        return None
+
+    @staticmethod
+    def _batch_size(inputs) -> int:
+        if torch.is_tensor(inputs):
+            return inputs.shape[0]
+        vals = inputs.values() if isinstance(inputs, dict) else inputs if isinstance(inputs, (list, tuple)) else []
+        for v in vals:
+            if torch.is_tensor(v) and v.dim() > 0:
+                return v.shape[0]
+        return 1
+
+    def _comm_device(self):
+        return self.device if dist.is_initialized() and dist.get_backend() == "nccl" else torch.device("cpu")
+
+    def _gather(self, t: Optional[torch.Tensor], counts: List[int], pad_index=-100) -> Optional[torch.Tensor]:
+        """Rank-ordered concatenation over the data-parallel ranks of each
+        rank's first ``counts[rank]`` rows (the ranks' tensors are padded to
+        a common shape -- trailing dims with ``pad_index`` -- for the
+        all-gather, then trimmed)."""
+        world = self._world()
+        if world == 1 or t is None:
+            return t
+        dev = self._comm_device()
+        t = t.to(dev)
+        shape = torch.tensor([max(counts)] + list(t.shape[1:]), dtype=torch.int64, device=dev)
+        dist.all_reduce(shape, op=dist.ReduceOp.MAX)
+        want = [int(x) for x in shape.tolist()]
+        if want != list(t.shape):
+            out = t.new_full(want, pad_index)
+            out[tuple(slice(0, n) for n in t.shape)] = t
+            t = out
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t.contiguous())
+        return torch.cat([p[:c] for p, c in zip(parts, counts)])
+
+    def evaluation_loop(self, dataset, metric_key_prefix: str = "eval", want_preds: bool = False):
+        """Loss, predictions and labels over the WHOLE dataset: per-sample
+        losses and logits stay on the device during the loop (no host sync
+        per batch), are gathered across the data-parallel ranks once at the
+        end, and the sampler's padding is cut off (reference
+        ``evaluation_loop`` / ``_nested_gather``,
+        atorch_trainer.py:1659,1857-2043)."""
+        dl = self.get_eval_dataloader(dataset)
+        n = len(dl.dataset)
+        real_batches = getattr(dl.batch_sampler, "num_real_batches", None)
         self.model.eval()
-        tot = torch.zeros(2, dtype=torch.float64, device=self.device)
-        preds, labels = [], []
-        for inputs in dl:
-            inputs = self._prepare_inputs(inputs)
-            with self._autocast():
-                loss, out = self.compute_loss(self.model, inputs, return_outputs=True)
-            tot[0] += float(loss)
-            tot[1] += 1
-            if self.compute_metrics is not None:
-                logits = out.logits if hasattr(out, "logits") else out
-                preds.append(logits.detach().float().cpu())
-                if isinstance(inputs, dict) and "labels" in inputs:
-                    labels.append(inputs["labels"].detach().cpu())
-        if dist.is_initialized() and dist.get_world_size() > 1:
-            t = tot.to(self.device) if self.device.type == "cuda" else tot
-            dist.all_reduce(t)
-            tot = t
-        metrics = {f"{metric_key_prefix}_loss": float(tot[0] / max(1.0, float(tot[1])))}
-        if self.compute_metrics is not None and preds:
+        losses, preds, labels = [], [], []
+        collect = want_preds or self.compute_metrics is not None
+        with torch.no_grad():
+            for bi, inputs in enumerate(dl):
+                inputs = self._prepare_inputs(inputs)
+                with self._autocast():
+                    loss, out = self.compute_loss(self.model, inputs, return_outputs=True)
+                if real_batches is not None and bi >= real_batches:
+                    continue  # a padding batch (keeps FSDP / DDP collectives matched)
+                bs = self._batch_size(inputs)
+                losses.append(loss.detach().float().reshape(1).expand(bs))
+                if collect:
+                    lg = self._logits(out)
+                    if lg is not None:
+                        preds.append(lg.detach().float())
+                    lb = self._labels(inputs)
+                    if lb is not None:
+                        labels.append(lb.detach())
+        self.model.train()
+        counts = [n]
+        if self._world() > 1:
+            mine = sum(x.numel() for x in losses)
+            c = torch.zeros(self._world(), dtype=torch.int64, device=self._comm_device())
+            c[self._rank()] = mine
+            dist.all_reduce(c)
+            counts = [int(x) for x in c.tolist()]
+        loss_all = self._gather(torch.cat(losses) if losses else torch.zeros(0, device=self.device), counts)
+        preds_all = self._gather(_pad_cat(preds), counts) if preds else None
+        labels_all = self._gather(_pad_cat(labels), counts) if labels else None
+        preds_all = preds_all.cpu() if preds_all is not None else None
+        labels_all = labels_all.cpu() if labels_all is not None else None
+        metrics = {f"{metric_key_prefix}_loss": float(loss_all.mean()) if loss_all.numel() else float("nan")}
+        if self.compute_metrics is not None and preds_all is not None:
             from transformers import EvalPrediction
 
-            m = self.compute_metrics(EvalPrediction(predictions=torch.cat(preds).numpy(),
-                                                    label_ids=torch.cat(labels).numpy() if labels else None))
-            metrics.update({f"{metric_key_prefix}_{k}": v for k, v in m.items()})
+            m = self.compute_metrics(EvalPrediction(predictions=preds_all.numpy(),
+                                                    label_ids=labels_all.numpy() if labels_all is not None else None))
+            metrics.update({k if k.startswith(metric_key_prefix + "_") else f"{metric_key_prefix}_{k}": v
+                            for k, v in m.items()})
+        metrics[f"{metric_key_prefix}_samples"] = n
+        return EvalLoopOutput(preds_all, labels_all, metrics, n)
+
+    def evaluate(self, eval_dataset=None, metric_key_prefix: str = "eval") -> Dict[str, float]:
+        ds = eval_dataset if eval_dataset is not None else self.eval_dataset
+        out = self.evaluation_loop(ds, metric_key_prefix)
+        metrics = out.metrics
+        self._last_eval_metrics = dict(metrics)
         self.log(dict(metrics))
         self.control = self.callback_handler.on_evaluate(self.args, self.state, self.control, metrics)
-        self.model.train()
         return metrics
 
-    @torch.no_grad()
-    def predict(self, test_dataset) -> torch.Tensor:
-        dl = self.get_eval_dataloader(test_dataset)
-        self.model.eval()
-        outs = []
-        for inputs in dl:
-            inputs = self._prepare_inputs(inputs)
-            with self._autocast():
-                _, out = self.compute_loss(self.model, inputs, return_outputs=True)
-            outs.append((out.logits if hasattr(out, "logits") else out).detach().float().cpu())
-        self.model.train()
-        return torch.cat(outs)
+    def predict(self, test_dataset, metric_key_prefix: str = "test") -> "EvalLoopOutput":
+        """Predictions (and labels / metrics when the dataset has labels) of
+        the whole dataset, in dataset order, on every rank."""
+        return self.evaluation_loop(test_dataset, metric_key_prefix, want_preds=True)
+
+    # ---------------------------------------------------------------- best model
+    def _track_best(self, ckpt_dir: str):
+        """At a save: is the last evaluation the best so far?  (HF
+        ``_determine_best_metric``; reference atorch_trainer.py:1304
+        ``_save_checkpoint``)."""
+        a = self.args
+        metrics = getattr(self, "_last_eval_metrics", None)
+        if not metrics or not a.metric_for_best_model:
+            return
+        name = a.metric_for_best_model
+        if not name.startswith("eval_"):
+            name = f"eval_{name}"
+        if name not in metrics:
+            logger.warning(f"metric_for_best_model {name} not in the evaluation metrics {sorted(metrics)}")
+            return
+        v = float(metrics[name])
+        greater = a.greater_is_better if a.greater_is_better is not None else not name.endswith("loss")
+        best = self.state.best_metric
+        if best is None or (v > best if greater else v < best):
+            self.state.best_metric = v
+            self.state.best_model_checkpoint = ckpt_dir
+            if hasattr(self.state, "best_global_step"):
+                self.state.best_global_step = self.state.global_step
+
+    def _load_best_model(self):
+        """``load_best_model_at_end``: the weights of the best checkpoint
+        (reference atorch_trainer.py:1197)."""
+        d = self.state.best_model_checkpoint
+        if not d or not os.path.isdir(d):
+            logger.warning("load_best_model_at_end: no best checkpoint recorded")
+            return
+        if self._checkpointer is not None and hasattr(self._checkpointer, "wait_latest_checkpoint"):
+            self._checkpointer.wait_latest_checkpoint()  # its async persist may still be writing
+        if self.is_fsdp:
+            from torch.distributed.checkpoint.state_dict import get_model_state_dict, set_model_state_dict
+
+            import torch.distributed.checkpoint as dcp
+
+            msd = get_model_state_dict(self.model)
+            dcp.load({"model": msd}, checkpoint_id=os.path.join(d, "dcp"))
+            set_model_state_dict(self.model, msd)
+        else:
+            path = os.path.join(d, f"rank_{self._rank()}_{STATE_FILE}")
+            if not os.path.exists(path):  # replicated (DDP) flash checkpoints are persisted by rank 0 only
+                path = os.path.join(d, f"rank_0_{STATE_FILE}")
+            sd = torch.load(path, map_location="cpu", weights_only=True)
+            if "model_states" in sd and "model" not in sd:  # flash-checkpoint archive layout
+                sd = sd["model_states"]
+            self.model.load_state_dict(sd["model"])
+        logger.info(f"loaded the best model ({self.args.metric_for_best_model}={self.state.best_metric}) from {d}")
 
     # ---------------------------------------------------------------- checkpoint
     def _set_seed(self, seed: int):
@@ -549,6 +682,7 @@ class AtorchTrainer:
         else:
             torch.save(sd, path)
         torch.save(self._rng_state(), os.path.join(out, f"rng_state_{self._rank()}.pth"))
+        self._track_best(out)
         if self.is_world_process_zero():
             self.state.save_to_json(os.path.join(out, TRAINER_STATE_NAME))
             with open(os.path.join(self.args.output_dir, "latest_checkpoint.txt"), "w") as f:
@@ -568,6 +702,11 @@ class AtorchTrainer:
         if not limit or limit <= 0:
             return
         cks = self._sorted_checkpoints()
+        best = self.state.best_model_checkpoint
+        if best in cks:
+            # the best checkpoint is kept on top of the limit (HF semantics)
+            cks.remove(best)
+            limit = max(1, limit - 1) if self.args.load_best_model_at_end else limit
         for old in cks[:max(0, len(cks) - limit)]:
             logger.info(f"deleting old checkpoint {old} (save_total_limit={limit})")
             shutil.rmtree(old, ignore_errors=True)
@@ -641,6 +780,54 @@ class AtorchTrainer:
         if self._checkpointer is not None:
             self._checkpointer.close()
             self._checkpointer = None
+
+
+class EvalLoopOutput(NamedTuple):
+    """HF ``EvalLoopOutput`` / ``PredictionOutput``."""
+
+    predictions: Optional[torch.Tensor]
+    label_ids: Optional[torch.Tensor]
+    metrics: Dict[str, Any]
+    num_samples: int
+
+
+class DistributedEvalBatchSampler(torch.utils.data.Sampler):
+    """Evaluation batches for data-parallel ranks: the dataset's sequential
+    batches (``[0, bs), [bs, 2 bs), ...``, only the last one partial) are
+    split into contiguous runs, rank r taking batches ``[r * pb, (r + 1) *
+    pb)``; ranks with fewer real batches run whole padding batches so every
+    rank runs ``pb`` batches.  Padding never shares a batch with real samples,
+    so per-batch mean losses weight exactly like one process, and the
+    rank-ordered gather of the real rows is the dataset order."""
+
+    def __init__(self, n: int, batch_size: int, num_replicas: int, rank: int):
+        bs = max(1, batch_size)
+        batches = [list(range(i, min(i + bs, n))) for i in range(0, n, bs)]
+        pb = -(-len(batches) // num_replicas) if batches else 0
+        mine = batches[rank * pb: (rank + 1) * pb]
+        self.num_real_batches = len(mine)
+        self.num_real = sum(len(b) for b in mine)
+        self.batches = mine + [batches[0]] * (pb - len(mine))
+
+    def __iter__(self):
+        return iter(self.batches)
+
+    def __len__(self):
+        return len(self.batches)
+
+
+def _pad_cat(ts: List[torch.Tensor], pad_index=-100) -> torch.Tensor:
+    """Concatenate along dim 0, padding the other dims to the largest
+    (variable sequence lengths across batches)."""
+    if len({tuple(t.shape[1:]) for t in ts}) <= 1:
+        return torch.cat(ts)
+    shape = [max(t.shape[d] for t in ts) for d in range(1, ts[0].dim())]
+    out = ts[0].new_full([sum(t.shape[0] for t in ts)] + shape, pad_index)
+    o = 0
+    for t in ts:
+        out[(slice(o, o + t.shape[0]),) + tuple(slice(0, n) for n in t.shape[1:])] = t
+        o += t.shape[0]
+    return out
 
 
 class _null:

@@ -83,3 +83,129 @@ def test_trainer_trains_saves_rotates_and_resumes_exactly(tmp_path, flash):
 
     w = load_file(str(tmp_path / "final" / "model.safetensors"))
     assert torch.equal(w["wte.weight"], final_a["wte.weight"])
+
+
+# ------------------------------------------------ distributed evaluation
+class _ClsDS(torch.utils.data.Dataset):
+    """37 samples: not a multiple of ranks x batch, so the sampler pads."""
+
+    def __init__(self, n=37):
+        g = torch.Generator().manual_seed(3)
+        self.x = torch.randn(n, 8, generator=g)
+        self.y = (self.x.sum(-1) > 0).long()
+
+    def __len__(self):
+        return len(self.x)
+
+    def __getitem__(self, i):
+        return {"x": self.x[i], "labels": self.y[i]}
+
+
+class _Cls(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.lin = torch.nn.Linear(8, 2)
+
+    def forward(self, x, labels=None):
+        logits = self.lin(x)
+        out = {"logits": logits}
+        if labels is not None:
+            out["loss"] = torch.nn.functional.cross_entropy(logits, labels)
+        return out
+
+
+def _metrics(p):
+    import numpy as np
+
+    pred = p.predictions.argmax(-1)
+    return {"acc": float((pred == p.label_ids).mean()), "n": int(len(p.label_ids)),
+            "label_sum": int(np.sum(p.label_ids)), "logit_sum": float(np.sum(p.predictions))}
+
+
+def _cls_args(out, **kw):
+    base = dict(per_device_train_batch_size=4, per_device_eval_batch_size=3, max_steps=6, save_steps=2,
+                logging_steps=100, atorch_opt="ddp", learning_rate=0.5, flash_checkpoint=False)
+    base.update(kw)
+    return _args(out, **base)
+
+
+def _eval_worker(rank, world, port, q, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    import torch.distributed as dist
+
+    try:
+        from dlrover_wuqiong_amd.atorch.trainer import AtorchTrainer
+
+        dist.init_process_group("gloo")
+        t = AtorchTrainer(_Cls(), _cls_args(out), train_dataset=_ClsDS(), eval_dataset=_ClsDS(),
+                          compute_metrics=_metrics)
+        m = t.evaluate()
+        pr = t.predict(_ClsDS())
+        q.put((rank, ("ok", m, pr.predictions.tolist(), pr.num_samples)))
+        t.close()
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        traceback.print_exc()
+        q.put((rank, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_four_rank_evaluation_equals_single_process(tmp_path):
+    import torch.multiprocessing as mp
+
+    from conftest import free_port
+    from dlrover_wuqiong_amd.atorch.trainer import AtorchTrainer
+
+    single = AtorchTrainer(_Cls(), _cls_args(tmp_path / "s", atorch_opt="none"), train_dataset=_ClsDS(),
+                           eval_dataset=_ClsDS(), compute_metrics=_metrics)
+    want = single.evaluate()
+    want_pred = single.predict(_ClsDS()).predictions
+    assert want["eval_n"] == 37
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_eval_worker, args=(r, 4, port, q, str(tmp_path / "d"))) for r in range(4)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in ps), key=lambda x: x[0])
+    for p in ps:
+        p.join(timeout=60)
+    for _r, out in res:
+        assert isinstance(out, tuple) and out[0] == "ok", res
+        m = out[1]
+        # global metrics over exactly the 37 samples (padding stripped), equal to one process
+        assert m["eval_n"] == 37 and m["eval_label_sum"] == want["eval_label_sum"]
+        assert abs(m["eval_acc"] - want["eval_acc"]) < 1e-9
+        assert abs(m["eval_loss"] - want["eval_loss"]) < 1e-5
+        assert abs(m["eval_logit_sum"] - want["eval_logit_sum"]) < 1e-3
+        assert out[3] == 37 and torch.allclose(torch.tensor(out[2]), want_pred, atol=1e-5)
+
+
+def test_load_best_model_at_end(tmp_path):
+    from dlrover_wuqiong_amd.atorch.trainer import AtorchTrainer
+
+    snaps = {}
+    holder = {}
+
+    def metrics(p):
+        step = holder["t"].state.global_step
+        snaps[step] = {k: v.clone() for k, v in holder["t"].model.state_dict().items()}
+        return {"score": -abs(step - 4)}  # best at step 4 of 2, 4, 6
+
+    t = AtorchTrainer(_Cls(), _cls_args(tmp_path / "b", atorch_opt="none", eval_strategy="steps", eval_steps=2,
+                                        load_best_model_at_end=True, metric_for_best_model="score",
+                                        greater_is_better=True, save_total_limit=1),
+                      train_dataset=_ClsDS(), eval_dataset=_ClsDS(), compute_metrics=metrics)
+    holder["t"] = t
+    t.train()
+    assert t.state.best_model_checkpoint.endswith("checkpoint-4") and t.state.best_metric == 0
+    assert os.path.isdir(t.state.best_model_checkpoint)  # kept despite save_total_limit=1
+    for k, v in t.model.state_dict().items():
+        assert torch.equal(v, snaps[4][k]), k
+    assert not torch.equal(snaps[4]["lin.weight"], snaps[6]["lin.weight"])
+    t.close()
