@@ -79,10 +79,11 @@ SIGS = {
     "dw_qadamw": (i32, [vp, vp, vp, vp, vp, vp, i64, i64, i32, i32, i32, f32, f32, f32, f32, f32, f32, f32, f32,
                         vp]),
     # colred.hip
-    "dw_colsum_acc": (i32, [vp, i64, i32, vp, vp, i32, i32, vp]),
-    "dw_gelu_bwd_dbias": (i32, [vp, vp, vp, i64, i32, vp, vp, i32, i32, vp]),
-    "dw_norm_bwd2": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp]),
-    "dw_norm_bwd3": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32, i32, i32, i32, vp, vp, vp]),
+    "dw_colsum_acc": (i32, [vp, i64, i32, vp, vp, i32, i32, vp, vp]),
+    "dw_gelu_bwd_dbias": (i32, [vp, vp, vp, i64, i32, vp, vp, i32, i32, vp, vp]),
+    "dw_norm_bwd2": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp, vp]),
+    "dw_norm_bwd3": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i32, i32, i32, i32, vp, vp, vp, vp]),
+    "dw_colred_det_floats": (i64, [i64, i32, i32]),
     "dw_add_norm_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, f32, i32, vp]),
     "dw_swiglu_fwd": (i32, [vp, vp, i64, i32, vp]),
     "dw_swiglu_bwd": (i32, [vp, vp, vp, i64, i32, vp]),

@@ -40,6 +40,27 @@ __device__ __forceinline__ void colred_store(void* out, int c, float v, int is_f
   }
 }
 
+// Deterministic mode (``part`` != nullptr; DWAMD_DETERMINISTIC=1 or
+// torch.use_deterministic_algorithms(True) on the Python side): every block
+// stores its partial column sums instead of adding them atomically, and the
+// finishing block adds the partials in block order -- bit-identical results
+// from run to run at the cost of the partial buffer and the finishing
+// block's serial sum.  Loads are issued 8 at a time, the adds stay in order.
+__device__ __forceinline__ float ordered_sum(const float* p, int64_t stride, int n) {
+  float a = 0.f;
+  int i = 0;
+  for (; i + 8 <= n; i += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      v[u] = __hip_atomic_load(p + (int64_t)(i + u) * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a += v[u];
+  }
+  for (; i < n; ++i) a += __hip_atomic_load(p + (int64_t)i * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return a;
+}
+
 // MODE 0: acc0 += dy ;  MODE 1: acc0 += dy * xhat, acc1 += dy (LayerNorm) ;
 // MODE 2: acc0 += dy * xhat (RMSNorm) ;
 // MODE 3: dxo = dy * gelu'(x), acc0 += dxo (GELU backward fused with the
@@ -49,8 +70,10 @@ __global__ void __launch_bounds__(256) colred_kernel(const bf16_t* __restrict__ 
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      float* __restrict__ ws, int64_t rows, int C, int rows_per_blk,
                                                      void* __restrict__ out0, void* __restrict__ out1, int is_fp32,
-                                                     int accumulate, bf16_t* __restrict__ dxo = nullptr) {
+                                                     int accumulate, bf16_t* __restrict__ dxo = nullptr,
+                                                     float* __restrict__ part = nullptr) {
   __shared__ float red[2][4][512 + 4];
+  constexpr int NS = MODE == 1 ? 2 : 1;  // sums per column
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c0 = blockIdx.x * 512 + lane * 8;
   const int64_t r_beg = (int64_t)blockIdx.y * rows_per_blk;
@@ -115,10 +138,21 @@ __global__ void __launch_bounds__(256) colred_kernel(const bf16_t* __restrict__ 
     const int c = blockIdx.x * 512 + cl;
     if (c >= C) continue;
     const float s0 = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
-    atomicAdd(ws + c, s0);
+    if (part) {
+      // deterministic mode: this block's partial sums, combined in a fixed
+      // order by the finishing block (agent-scope stores: performed at the
+      // coherent level, like the atomics of the default mode)
+      __hip_atomic_store(part + (int64_t)blockIdx.y * NS * C + c, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      atomicAdd(ws + c, s0);
+    }
     if constexpr (MODE == 1) {
       const float s1 = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
-      atomicAdd(ws + C + c, s1);
+      if (part)
+        __hip_atomic_store(part + ((int64_t)blockIdx.y * NS + 1) * C + c, s1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      else
+        atomicAdd(ws + C + c, s1);
     }
   }
   // The last block of each 512-column strip converts the strip's fp32 sums
@@ -141,15 +175,26 @@ __global__ void __launch_bounds__(256) colred_kernel(const bf16_t* __restrict__ 
   __syncthreads();
   if (!is_last) return;
   float v0[2], v1[2];
+  if (part) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    // read + clear (self-cleaning) with the same atomics that built the sums:
-    // single-location atomicity, no cache maintenance; all in flight at once
-    const int c = blockIdx.x * 512 + threadIdx.x + 256 * j;
-    if (c < C) {
-      v0[j] = __hip_atomic_exchange(ws + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if constexpr (MODE == 1)
-        v1[j] = __hip_atomic_exchange(ws + C + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int j = 0; j < 2; ++j) {
+      const int c = blockIdx.x * 512 + threadIdx.x + 256 * j;
+      if (c < C) {
+        v0[j] = ordered_sum(part + c, (int64_t)NS * C, gridDim.y);
+        if constexpr (MODE == 1) v1[j] = ordered_sum(part + C + c, (int64_t)NS * C, gridDim.y);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      // read + clear (self-cleaning) with the same atomics that built the sums:
+      // single-location atomicity, no cache maintenance; all in flight at once
+      const int c = blockIdx.x * 512 + threadIdx.x + 256 * j;
+      if (c < C) {
+        v0[j] = __hip_atomic_exchange(ws + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (MODE == 1)
+          v1[j] = __hip_atomic_exchange(ws + C + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
 #pragma unroll
@@ -498,7 +543,8 @@ __global__ void __launch_bounds__(256) colsum_f32_kernel(const float* __restrict
                                                          int rows_per_blk, float* __restrict__ ws,
                                                          void* __restrict__ out0, void* __restrict__ out1,
                                                          int is_fp32, int accumulate, int H,
-                                                         void* __restrict__ out2, int accumulate2) {
+                                                         void* __restrict__ out2, int accumulate2,
+                                                         float* __restrict__ detp) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   const int r0 = blockIdx.y * rows_per_blk, r1 = min(R, r0 + rows_per_blk);
   if (c < H2) {
@@ -511,7 +557,11 @@ __global__ void __launch_bounds__(256) colsum_f32_kernel(const float* __restrict
       a3 += part[(int64_t)(r + 3) * H2 + c];
     }
     for (; r < r1; ++r) a0 += part[(int64_t)r * H2 + c];
-    atomicAdd(ws + c, (a0 + a1) + (a2 + a3));
+    if (detp)
+      __hip_atomic_store(detp + (int64_t)blockIdx.y * H2 + c, (a0 + a1) + (a2 + a3), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    else
+      atomicAdd(ws + c, (a0 + a1) + (a2 + a3));
   }
   __shared__ int is_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -522,7 +572,8 @@ __global__ void __launch_bounds__(256) colsum_f32_kernel(const float* __restrict
   __syncthreads();
   if (!is_last) return;
   if (c < H2) {
-    const float v = __hip_atomic_exchange(ws + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float v = detp ? ordered_sum(detp + c, H2, gridDim.y)
+                         : __hip_atomic_exchange(ws + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (c < H)
       colred_store(out0, c, v, is_fp32, accumulate);
     else if (c < 2 * H)
@@ -555,27 +606,55 @@ static int colred_rows_per_blk(int64_t rows, int C, int dflt_blocks) {
 }
 
 // ws: fp32 [C + ceil(C/512)] (sums + per-strip completion counters), all-zero on entry, left all-zero.  out (+)= column sums of dy [rows, C].
+// det: nullptr (atomic combine) or fp32 scratch of dw_colred_det_floats(rows, C, 0) floats (any content).
 extern "C" int dw_colsum_acc(const void* dy, int64_t rows, int C, void* ws, void* out, int out_fp32, int accumulate,
-                             void* stream) {
+                             void* stream, void* det) {
   if (C % 8 != 0) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   const int per = colred_rows_per_blk(rows, C, 256);
   dim3 grid((C + 511) / 512, (unsigned)((rows + per - 1) / per));
   hipLaunchKernelGGL(colred_kernel<0>, grid, dim3(256), 0, s, (const bf16_t*)dy, nullptr, nullptr, nullptr,
-                     (float*)ws, rows, C, per, out, nullptr, out_fp32, accumulate);
+                     (float*)ws, rows, C, per, out, nullptr, out_fp32, accumulate, nullptr, (float*)det);
   DW_LAUNCH_RET;
 }
 
 // dx = dy * gelu'(pre) [rows, C]; dbias (+)= column sums of dx.  ws as above.
+// det: as dw_colsum_acc (dw_colred_det_floats(rows, C, 1) floats).
 extern "C" int dw_gelu_bwd_dbias(const void* dy, const void* pre, void* dx, int64_t rows, int C, void* ws,
-                                 void* dbias, int out_fp32, int accumulate, void* stream) {
+                                 void* dbias, int out_fp32, int accumulate, void* stream, void* det) {
   if (C % 8 != 0) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   const int per = colred_rows_per_blk(rows, C, 2048);
   dim3 grid((C + 511) / 512, (unsigned)((rows + per - 1) / per));
   hipLaunchKernelGGL(colred_kernel<3>, grid, dim3(256), 0, s, (const bf16_t*)dy, (const bf16_t*)pre, nullptr,
-                     nullptr, (float*)ws, rows, C, per, dbias, nullptr, out_fp32, accumulate, (bf16_t*)dx);
+                     nullptr, (float*)ws, rows, C, per, dbias, nullptr, out_fp32, accumulate, (bf16_t*)dx,
+                     (float*)det);
   DW_LAUNCH_RET;
+}
+
+static int norm_colred_blocks() {
+  static const int norm_blocks = [] {
+    const char* e = getenv("DWAMD_COLRED_NORM_BLOCKS");
+    return e && atoi(e) > 0 ? atoi(e) : 1024;
+  }();
+  return norm_blocks;
+}
+
+static int64_t colsum_f32_splits(int64_t nb) { return std::max<int64_t>(1, std::min<int64_t>(64, nb / 16)); }
+
+// fp32 scratch the deterministic mode needs (kind 0: dw_colsum_acc, 1:
+// dw_gelu_bwd_dbias, 2: dw_norm_bwd3): one partial row per row-block.
+extern "C" int64_t dw_colred_det_floats(int64_t rows, int C, int kind) {
+  auto grid_y = [&](int target) {
+    const int per = colred_rows_per_blk(rows, C, target);
+    return (rows + per - 1) / per;
+  };
+  if (kind == 0) return grid_y(256) * C;
+  if (kind == 1) return grid_y(2048) * C;
+  // norm: the two-pass path (colred_kernel<1>, 2 sums per column) or the
+  // small-H partial-rows path (colsum_f32_kernel over <= 3H columns)
+  const int64_t nb = std::min<int64_t>((rows + 3) / 4, C > 1024 ? 256 : 512);
+  return std::max<int64_t>(grid_y(norm_colred_blocks()) * 2 * C, colsum_f32_splits(nb) * 3 * C);
 }
 
 #define DISPATCH_VPL2(H, ...)                          \
@@ -591,14 +670,16 @@ extern "C" int dw_gelu_bwd_dbias(const void* dy, const void* pre, void* dx, int6
 // Norm backward v2.  ws: fp32 [2H + ceil(H/512)], all-zero on entry, left all-zero.
 // dgamma/dbeta (+)= (accumulate flag).  dres (nullable): gradient of the
 // residual sum that this norm's input also feeds (fused add+norm) -> dx += dres.
+// det: nullptr, or fp32 scratch of dw_colred_det_floats(rows, H, 2) floats:
+// deterministic weight gradients (the two-pass path with ordered partials).
 extern "C" int dw_norm_bwd2(const void* dy, const void* x, const void* gamma, const void* mean, const void* rstd,
                             const void* dres, void* dx, void* dgamma, void* dbeta, void* ws, int64_t rows, int H,
-                            int rms, int out_fp32, int accumulate, void* stream) {
+                            int rms, int out_fp32, int accumulate, void* stream, void* det) {
   if (H % 8 != 0 || H > 8 * 64 * 16) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   static const bool two_pass = getenv_flag("DWAMD_NORM_BWD_2PASS");  // A/B switch
-  if ((dgamma || dbeta) && H >= 2048 && H <= 8 * 64 * 8 && !two_pass) {
+  if ((dgamma || dbeta) && H >= 2048 && H <= 8 * 64 * 8 && !two_pass && !det) {
     // one pass: dx + weight gradients (2 blocks per CU of 4 row-striding
     // waves).  Measured (scripts/bench_norm.py): RMSNorm 16k x 4096 141 ->
     // 118 us; at H = 1600 the two passes are as fast (the row pass alone
@@ -631,20 +712,17 @@ extern "C" int dw_norm_bwd2(const void* dy, const void* x, const void* gamma, co
                          (bf16_t*)dx, rows, H);
   });
   if (!dgamma && !dbeta) { DW_LAUNCH_RET; }
-  static const int norm_blocks = [] {
-    const char* e = getenv("DWAMD_COLRED_NORM_BLOCKS");
-    return e && atoi(e) > 0 ? atoi(e) : 1024;
-  }();
-  const int per = colred_rows_per_blk(rows, H, norm_blocks);
+  const int per = colred_rows_per_blk(rows, H, norm_colred_blocks());
   dim3 cg((H + 511) / 512, (unsigned)((rows + per - 1) / per));
   // both halves are consumed (and cleared) even if one output is absent
   if (rms)
     hipLaunchKernelGGL(colred_kernel<2>, cg, dim3(256), 0, s, (const bf16_t*)dy, (const bf16_t*)x, nullptr,
-                       (const float*)rstd, (float*)ws, rows, H, per, dgamma, nullptr, out_fp32, accumulate);
+                       (const float*)rstd, (float*)ws, rows, H, per, dgamma, nullptr, out_fp32, accumulate, nullptr,
+                       (float*)det);
   else
     hipLaunchKernelGGL(colred_kernel<1>, cg, dim3(256), 0, s, (const bf16_t*)dy, (const bf16_t*)x,
                        (const float*)mean, (const float*)rstd, (float*)ws, rows, H, per, dgamma, dbeta, out_fp32,
-                       accumulate);
+                       accumulate, nullptr, (float*)det);
   DW_LAUNCH_RET;
 }
 
@@ -660,7 +738,7 @@ extern "C" int dw_norm_bwd2(const void* dy, const void* x, const void* gamma, co
 extern "C" int dw_norm_bwd3(const void* dy, const void* x, const void* gamma, const void* mean, const void* rstd,
                             const void* dres, void* dx, void* dgamma, void* dbeta, void* ws, void* part,
                             int64_t part_floats, int64_t rows, int H, int rms, int out_fp32, int accumulate,
-                            void* dsum, int* dsum_done, void* stream) {
+                            void* dsum, int* dsum_done, void* stream, void* det) {
   // accumulate: bit 0 -- dgamma / dbeta accumulate; bit 1 -- dsum is
   // OVERWRITTEN (its parameter's first gradient contribution of the step)
   const int acc2 = (accumulate & 2) ? 0 : 1;
@@ -673,7 +751,7 @@ extern "C" int dw_norm_bwd3(const void* dy, const void* x, const void* gamma, co
   static const bool off = getenv_flag("DWAMD_NORM_BWD_PART_OFF");  // A/B switch
   if (off || !part || !(dgamma || dbeta) || H % 8 != 0 || H >= 2048 || nb * pw * H > part_floats)
     return dw_norm_bwd2(dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, ws, rows, H, rms, out_fp32, accumulate,
-                        stream);
+                        stream, det);
   hipStream_t s = (hipStream_t)stream;
 #define NBP(RM, DSV)                                                                                          \
   hipLaunchKernelGGL((norm_bwd_part_kernel<VPL, RM, DSV>), dim3((unsigned)nb), dim3(256), 0, s,              \
@@ -691,11 +769,11 @@ extern "C" int dw_norm_bwd3(const void* dy, const void* x, const void* gamma, co
 #undef NBP
   if (dsum_done) *dsum_done = dsum ? 1 : 0;
   const int H2 = pw * H;
-  const int splits = (int)std::max<int64_t>(1, std::min<int64_t>(64, nb / 16));
+  const int splits = (int)colsum_f32_splits(nb);
   const int per = (int)((nb + splits - 1) / splits);
   dim3 g((H2 + 255) / 256, (unsigned)((nb + per - 1) / per));
   hipLaunchKernelGGL(colsum_f32_kernel, g, dim3(256), 0, s, (const float*)part, (int)nb, H2, per, (float*)ws,
-                     dgamma, rms ? nullptr : dbeta, out_fp32, accumulate, H, dsum, acc2);
+                     dgamma, rms ? nullptr : dbeta, out_fp32, accumulate, H, dsum, acc2, (float*)det);
   DW_LAUNCH_RET;
 }
 

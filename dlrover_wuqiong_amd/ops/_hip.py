@@ -19,7 +19,7 @@ class HipKernelError(RuntimeError):
 
 _TIMER = None  # utils.xpu_timer.XpuTimer timing this framework's own kernels (install(kernels=True))
 _NO_LAUNCH = ("workspace", "error", "_size", "mem_get_info", "ipc_", "device_malloc", "device_free",
-              "event_sync", "stream_sync", "_xt_")
+              "event_sync", "stream_sync", "_xt_", "det_floats")
 
 
 class _TimedLib:
@@ -120,6 +120,34 @@ def grid_sum_ws(device) -> torch.Tensor:
     if buf is None:
         buf = _GRID_WS[key] = torch.zeros(2048 + 1, device=device, dtype=torch.float32)
     return buf
+
+
+_DET_WS = {}
+
+
+def deterministic() -> bool:
+    """Bit-reproducible gradients: ``DWAMD_DETERMINISTIC=1`` or
+    ``torch.use_deterministic_algorithms(True)``.  The column-reduction
+    kernels (bias / norm-weight gradients) then combine per-block partials in
+    a fixed order instead of with float atomics (csrc/kernels/colred.hip)."""
+    import os
+
+    return os.environ.get("DWAMD_DETERMINISTIC", "0") == "1" or torch.are_deterministic_algorithms_enabled()
+
+
+def det_scratch(rows: int, C: int, kind: int, device):
+    """Pointer to the fp32 partial-sum scratch of a deterministic column
+    reduction (``kind``: 0 colsum, 1 GELU-bias backward, 2 norm backward),
+    or a null pointer when deterministic mode is off.  Any content; one
+    buffer per (device, stream), grown on demand."""
+    if not deterministic():
+        return ctypes.c_void_p(0)
+    n = int(kernels(required=True).dw_colred_det_floats(int(rows), int(C), int(kind)))
+    key = (torch.device(device).index, torch.cuda.current_stream(device).cuda_stream)
+    buf = _DET_WS.get(key)
+    if buf is None or buf.numel() < n:
+        buf = _DET_WS[key] = torch.empty(max(n, 1 << 16), device=device, dtype=torch.float32)
+    return ptr(buf)
 
 
 def zeroed_workspace(nfloats: int, device) -> torch.Tensor:

@@ -17,7 +17,8 @@ def colsum(x2: torch.Tensor, out_dtype=None, out: torch.Tensor = None, accumulat
         out = torch.empty(C, device=x2.device, dtype=out_dtype or x2.dtype)
     ws = _hip.zeroed_workspace(C + (C + 511) // 512, x2.device)  # sums + strip counters
     _hip.check(_hip.lib().dw_colsum_acc(_hip.ptr(x2), R, C, _hip.ptr(ws), _hip.ptr(out),
-                                        int(out.dtype == torch.float32), int(accumulate), _hip.stream()), "colsum")
+                                        int(out.dtype == torch.float32), int(accumulate), _hip.stream(),
+                                        _hip.det_scratch(R, C, 0, x2.device)), "colsum")
     return out
 
 
@@ -56,7 +57,8 @@ class _BiasGeluFn(torch.autograd.Function):
         ws = _hip.zeroed_workspace(C + (C + 511) // 512, pre.device)
         _hip.check(_hip.lib().dw_gelu_bwd_dbias(_hip.ptr(dy), _hip.ptr(pre), _hip.ptr(dx), pre.numel() // C, C,
                                                 _hip.ptr(ws), _hip.ptr(db), int(db.dtype == torch.float32),
-                                                int(g is not None and not claim(ctx.bias_param)), _hip.stream()),
+                                                int(g is not None and not claim(ctx.bias_param)), _hip.stream(),
+                                                _hip.det_scratch(pre.numel() // C, C, 1, pre.device)),
                    "gelu_bwd_dbias")
         if g is not None:
             notify(ctx.bias_param)

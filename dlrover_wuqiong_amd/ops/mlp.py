@@ -116,14 +116,15 @@ class _FusedMLPFn(torch.autograd.Function):
                 _hip.check(_hip.lib().dw_gelu_bwd_dbias(_hip.ptr(dg), _hip.ptr(pre), _hip.ptr(dh), M, N1,
                                                         _hip.ptr(ws), _hip.ptr(gb1),
                                                         int(gb1.dtype == torch.float32), int(not claim(p_b1)),
-                                                        _hip.stream()),
+                                                        _hip.stream(), _hip.det_scratch(M, N1, 1, dy.device)),
                            "gelu_bwd_dbias")
                 notify(p_b1)
                 db1_done = True
             else:
                 db1_f = torch.empty(N1, device=dy.device, dtype=torch.float32)
                 _hip.check(_hip.lib().dw_gelu_bwd_dbias(_hip.ptr(dg), _hip.ptr(pre), _hip.ptr(dh), M, N1,
-                                                        _hip.ptr(ws), _hip.ptr(db1_f), 1, 0, _hip.stream()),
+                                                        _hip.ptr(ws), _hip.ptr(db1_f), 1, 0, _hip.stream(),
+                                                        _hip.det_scratch(M, N1, 1, dy.device)),
                            "gelu_bwd_dbias")
         _BWD_MODE.setdefault(key, mode)
         db1 = None

@@ -76,7 +76,8 @@ def _norm_backward(ctx, dy, dres):
                                        _hip.ptr(rstd), _hip.ptr(dres), _hip.ptr(dx), _hip.ptr(dgamma),
                                        _hip.ptr(dbeta), _hip.ptr(ws), _hip.ptr(part), nparts, R, H,
                                        int(ctx.rms), int(dgamma.dtype == torch.float32), acc | (2 * dsum_fresh),
-                                       _hip.ptr(dsum), ctypes.byref(done), _hip.stream()), "norm_bwd")
+                                       _hip.ptr(dsum), ctypes.byref(done), _hip.stream(),
+                                       _hip.det_scratch(R, H, 2, x2.device)), "norm_bwd")
     if dsum_fresh and not done.value:
         dsum.zero_()  # claimed but not taken over: the producer's backward accumulates into it
     if done.value:

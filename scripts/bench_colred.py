@@ -44,7 +44,7 @@ for C in (1600, 4800, 6400):
 
         def gb():
             _hip.check(L.dw_gelu_bwd_dbias(_hip.ptr(dy), _hip.ptr(pre), _hip.ptr(dx), R, C, _hip.ptr(ws),
-                                           _hip.ptr(out), 1, 0, _hip.stream()), "gelu_bwd_dbias")
+                                           _hip.ptr(out), 1, 0, _hip.stream(), None), "gelu_bwd_dbias")
         t = timed(gb)
         print(json.dumps({"op": "gelu_bwd_dbias", "blocks": blocks, "R": R, "C": C, "us": round(t * 1e6, 1),
                           "gbps": round(3 * R * C * 2 / t / 1e9, 1)}), flush=True)

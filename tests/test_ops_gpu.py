@@ -121,13 +121,13 @@ def test_gelu_bwd_dbias_fused(R, C):
         dx = torch.empty_like(pre)
         ws = _hip.zeroed_workspace(C + (C + 511) // 512, DEV)
         _hip.check(_hip.lib().dw_gelu_bwd_dbias(_hip.ptr(dy), _hip.ptr(pre), _hip.ptr(dx), R, C, _hip.ptr(ws),
-                                                _hip.ptr(acc), 1, 1, _hip.stream()), "gelu_bwd_dbias")
+                                                _hip.ptr(acc), 1, 1, _hip.stream(), None), "gelu_bwd_dbias")
         assert _rel(dx, ref_dx) < 1e-2
         assert _rel(acc, (it + 1) * ref_db) < 1e-3
         assert int((ws[:C + (C + 511) // 512] != 0).sum()) == 0  # left all-zero (sums + counters)
     db16 = torch.empty(C, device=DEV, dtype=torch.bfloat16)
     _hip.check(_hip.lib().dw_gelu_bwd_dbias(_hip.ptr(dy), _hip.ptr(pre), _hip.ptr(dx), R, C, _hip.ptr(ws),
-                                            _hip.ptr(db16), 0, 0, _hip.stream()), "gelu_bwd_dbias")
+                                            _hip.ptr(db16), 0, 0, _hip.stream(), None), "gelu_bwd_dbias")
     assert _rel(db16, ref_db) < 1e-2
 
 
