@@ -421,6 +421,10 @@ def _fault_summary(a, ev, agent, step_sec, save_sec):
         "restore_gather": inc1.get("restore_gather"),
         "restore_phases_s": inc1.get("restore_phases"),
         "restarts": len(started) - 1,
+        # after the restart: every save's pause and the last flushes (HBM
+        # staging -> shm) -- a save waits when its buffer's flush lags
+        "save_ms_after_restart": [e["save_ms"] for e in steps1 if e.get("save_ms") is not None],
+        "flushes_after_restart": done.get("flushes"),
     }
     # a MODEL, not a measurement: one failure per hour, a checkpoint every
     # ckpt_interval steps (mean loss: half an interval of steps)
@@ -943,20 +947,30 @@ def worker(a) -> int:
             res_sec = mx(res_sec if res_sec is not None else -1.0)  # collective on every rank
             emit({"event": "restore_late", "rank": rank, "restore_ok": ok,
                   "resident_sec": res_sec if res_sec >= 0 else None})
+        save_ms = None
         if (step - s0) % a.ckpt_interval == 0:
             _dt, ok = save()
+            save_ms = round(1000 * _dt, 2)
             if not ok:
                 emit({"event": "window_skipped", "n": 1, "step": step, "incarnation": incarnation})
             if incarnation == 0 and step == last_before_kill:
                 emit({"event": "saved_sums", "step": step, "rank": rank, "sums": state_sums()}, all_ranks=True)
-        emit({"event": "step", "step": step, "t": time.time(), "incarnation": incarnation})
+        emit({"event": "step", "step": step, "t": time.time(), "incarnation": incarnation, "save_ms": save_ms})
     del skipped_w
     # end of the window: every rank's compute done (the background flush of
     # the last checkpoint is not training time and is not waited for)
     if world > 1:
         dist.barrier()
     sync_step()
-    emit({"event": "done", "t": time.time(), "step": step, "start_step": start_step, "incarnation": incarnation})
+    cp = ckpt.engine._copier
+    # the window's flushes (HBM staging -> shm): queueing delay and duration
+    # per flush, for save-wait diagnosis (a save waits when the previous
+    # flush of its staging buffer has not landed)
+    flushes = [{"wait_ms": round(1000 * (t0 - te), 1), "ms": round(1000 * (t1 - t0), 1),
+                "gbps": round(nb / max(t1 - t0, 1e-9) / 1e9, 1)}
+               for te, t0, t1, nb in list(getattr(cp, "flush_log", []) or [])[-12:]] if cp is not None else []
+    emit({"event": "done", "t": time.time(), "step": step, "start_step": start_step, "incarnation": incarnation,
+          "flushes": flushes, "skipped_saves": ckpt.engine.skipped_saves})
     sync_all()
     ckpt.close()
     if world > 1:
