@@ -88,6 +88,7 @@ SIGS = {
     "dw_swiglu_fwd": (i32, [vp, vp, i64, i32, vp]),
     "dw_swiglu_bwd": (i32, [vp, vp, vp, i64, i32, vp]),
     "dw_rope": (i32, [vp, vp, vp, vp, i64, i32, i32, i32, i32, vp, i32, vp]),
+    "dw_qkv_rope": (i32, [vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, i32, i32, vp, i32, vp]),
     # grouped_gemm.hip
     "dw_grouped_gemm": (i32, [i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, c.c_longlong, c.c_longlong,
                               c.c_longlong, c.c_longlong, c.c_longlong, vp]),

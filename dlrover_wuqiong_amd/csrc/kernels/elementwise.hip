@@ -203,4 +203,84 @@ extern "C" int dw_rope(const void* x, void* y, const void* cosb, const void* sin
   DW_LAUNCH_RET;
 }
 
+// Fused QKV split + RoPE (Llama attention prologue).  The QKV projection's
+// output [B, S, NH + 2 NKV, D] is read ONCE: query / key heads are rotated
+// (rotate-half) and written to contiguous q [B, S, NH, D] / k [B, S, NKV, D],
+// value heads copied to v [B, S, NKV, D] -- instead of three .contiguous()
+// copies of the split views and two rope passes over q and k.  BACKWARD: the
+// inverse -- dq / dk rotated back (sin negated) and dq | dk | dv written
+// interleaved into dqkv [B, S, NH + 2 NKV, D] (the split's gradient), one
+// pass.  One thread per (row, head, 8-wide vector of the first half): loads
+// the 8 elements and their rotate-half partners 16 bytes at a time.
+template <bool BWD>
+__global__ void __launch_bounds__(256) qkv_rope_kernel(bf16_t* __restrict__ qkv, bf16_t* __restrict__ q,
+                                                       bf16_t* __restrict__ k, bf16_t* __restrict__ v,
+                                                       const float* __restrict__ cosb,
+                                                       const float* __restrict__ sinb, int64_t BS, int S, int NH,
+                                                       int NKV, int D, const int* __restrict__ pos_ids, int rows) {
+  const int half = D >> 1;
+  const int hv = half >> 3;
+  const int NT = NH + 2 * NKV;
+  const int64_t total = BS * NT * hv;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int vi = (int)(t % hv);
+    const int64_t rh = t / hv;  // (b*S + s) * NT + head
+    const int head = (int)(rh % NT);
+    const int64_t bs = rh / NT;
+    bf16_t* packed = qkv + rh * D;
+    bf16_t* sep;
+    if (head < NH)
+      sep = q + (bs * NH + head) * D;
+    else if (head < NH + NKV)
+      sep = k + (bs * NKV + head - NH) * D;
+    else
+      sep = v + (bs * NKV + head - NH - NKV) * D;
+    const bf16_t* src = BWD ? sep : packed;
+    bf16_t* dst = BWD ? packed : sep;
+    const u32x4 a4 = *(const u32x4*)(src + vi * 8), b4 = *(const u32x4*)(src + half + vi * 8);
+    if (head >= NH + NKV) {  // value head: a plain copy
+      *(u32x4*)(dst + vi * 8) = a4;
+      *(u32x4*)(dst + half + vi * 8) = b4;
+      continue;
+    }
+    const int sp = pos_ids ? min(max(pos_ids[bs], 0), rows - 1) : (int)(bs % S);
+    const float* cr = cosb + (int64_t)sp * half + vi * 8;
+    const float* sr = sinb + (int64_t)sp * half + vi * 8;
+    const f32x4 c0 = *(const f32x4*)cr, c1 = *(const f32x4*)(cr + 4);
+    const f32x4 s0 = *(const f32x4*)sr, s1 = *(const f32x4*)(sr + 4);
+    float a[8], b[8], o1[8], o2[8];
+    unpack8(a4, a);
+    unpack8(b4, b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float c = j < 4 ? c0[j] : c1[j - 4];
+      const float sn = (BWD ? -1.f : 1.f) * (j < 4 ? s0[j] : s1[j - 4]);
+      o1[j] = a[j] * c - b[j] * sn;
+      o2[j] = b[j] * c + a[j] * sn;
+    }
+    *(u32x4*)(dst + vi * 8) = pack8(o1);
+    *(u32x4*)(dst + half + vi * 8) = pack8(o2);
+  }
+}
+
+// backward = 0: qkv -> (q, k, v) rotated; 1: (dq, dk, dv) -> dqkv, inverse
+// rotation.  cos / sin: fp32 [rows, D/2]; pos_ids (nullable) int32 [B*S].
+extern "C" int dw_qkv_rope(void* qkv, void* q, void* k, void* v, const void* cosb, const void* sinb, int64_t B,
+                           int S, int NH, int NKV, int D, int backward, const void* pos_ids, int rows,
+                           void* stream) {
+  if (D % 16 || rows < 1 || (!pos_ids && rows < S) || NH < 1 || NKV < 1) return (int)hipErrorInvalidValue;
+  const int64_t total = B * S * (NH + 2 * NKV) * (D / 16);
+  const dim3 g(dw_grid_for(total, 256, 8192));
+  if (backward)
+    hipLaunchKernelGGL(qkv_rope_kernel<true>, g, dim3(256), 0, (hipStream_t)stream, (bf16_t*)qkv, (bf16_t*)q,
+                       (bf16_t*)k, (bf16_t*)v, (const float*)cosb, (const float*)sinb, B * S, S, NH, NKV, D,
+                       (const int*)pos_ids, rows);
+  else
+    hipLaunchKernelGGL(qkv_rope_kernel<false>, g, dim3(256), 0, (hipStream_t)stream, (bf16_t*)qkv, (bf16_t*)q,
+                       (bf16_t*)k, (bf16_t*)v, (const float*)cosb, (const float*)sinb, B * S, S, NH, NKV, D,
+                       (const int*)pos_ids, rows);
+  DW_LAUNCH_RET;
+}
+
 DW_PRELOAD(gelu_bwd_kernel);

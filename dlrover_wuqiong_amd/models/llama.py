@@ -31,7 +31,7 @@ from ..ops.activation import swiglu
 from ..ops.attention import flash_attn_func
 from ..ops.cross_entropy import cross_entropy
 from ..ops.norm import RMSNorm
-from ..ops.rope import apply_rope, rope_table
+from ..ops.rope import apply_rope, qkv_split_rope, rope_table
 
 
 @dataclass
@@ -120,8 +120,12 @@ class LlamaAttention(nn.Module):
     def forward(self, x, cos, sin):
         B, S, _ = x.shape
         qkv = self.qkv_proj(x).view(B, S, self.nh + 2 * self.nkv, self.hd)
-        q, k, v = qkv.split([self.nh, self.nkv, self.nkv], dim=2)
         sp = _ws(self.sp_group)
+        if sp == 1:
+            # one pass over the projection: split + RoPE on q, k (ops/rope.py)
+            q, k, v = qkv_split_rope(qkv, self.nh, self.nkv, cos, sin)
+        else:
+            q, k, v = qkv.split([self.nh, self.nkv, self.nkv], dim=2)
         if sp > 1:
             from ..atorch.distributed import seq_all_to_all
 
@@ -129,8 +133,8 @@ class LlamaAttention(nn.Module):
             q = seq_all_to_all(q.contiguous(), 2, 1, self.sp_group, sp)
             k = seq_all_to_all(k.contiguous(), 2, 1, self.sp_group, sp)
             v = seq_all_to_all(v.contiguous(), 2, 1, self.sp_group, sp)
-        q = apply_rope(q.contiguous(), cos, sin)
-        k = apply_rope(k.contiguous(), cos, sin)
+            q = apply_rope(q.contiguous(), cos, sin)
+            k = apply_rope(k.contiguous(), cos, sin)
         if self.cp_group is not None:
             from ..parallel.context_parallel import context_parallel_attention
 

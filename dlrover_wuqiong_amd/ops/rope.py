@@ -90,3 +90,54 @@ def apply_rope(x, cos, sin, pos_ids=None):
         x = _hip.bf16(x)
         return _RopeFn.apply(x, _table(cos, x, pos_ids), _table(sin, x, pos_ids), pos_ids)
     return _rope_ref(x, cos, sin, 1.0, pos_ids)
+
+
+class _QkvRopeFn(torch.autograd.Function):
+    """Split of a packed QKV projection + RoPE on q and k in one pass
+    (``dw_qkv_rope``); backward: inverse rotation + interleaved write of the
+    packed gradient in one pass."""
+
+    @staticmethod
+    def forward(ctx, qkv, nh, nkv, cos, sin, pos_ids):
+        qkv = qkv.contiguous()
+        _hip.require_bf16(qkv)
+        B, S, NT, D = qkv.shape
+        q = torch.empty(B, S, nh, D, device=qkv.device, dtype=qkv.dtype)
+        k = torch.empty(B, S, nkv, D, device=qkv.device, dtype=qkv.dtype)
+        v = torch.empty(B, S, nkv, D, device=qkv.device, dtype=qkv.dtype)
+        pid = pos_ids.to(torch.int32).contiguous() if pos_ids is not None else None
+        _hip.check(_hip.lib().dw_qkv_rope(_hip.ptr(qkv), _hip.ptr(q), _hip.ptr(k), _hip.ptr(v), _hip.ptr(cos),
+                                          _hip.ptr(sin), B, S, nh, nkv, D, 0, _hip.ptr(pid), cos.shape[0],
+                                          _hip.stream()), "qkv_rope")
+        ctx.save_for_backward(cos, sin, pid)
+        ctx.shape = (B, S, NT, D, nh, nkv)
+        return q, k, v
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        cos, sin, pid = ctx.saved_tensors
+        B, S, NT, D, nh, nkv = ctx.shape
+        dev = (dq if dq is not None else dk if dk is not None else dv).device
+
+        def g(t, heads):
+            if t is None:
+                return torch.zeros(B, S, heads, D, device=dev, dtype=torch.bfloat16)
+            return t.contiguous().to(torch.bfloat16)
+
+        dq, dk, dv = g(dq, nh), g(dk, nkv), g(dv, nkv)
+        dqkv = torch.empty(B, S, NT, D, device=dev, dtype=torch.bfloat16)
+        _hip.check(_hip.lib().dw_qkv_rope(_hip.ptr(dqkv), _hip.ptr(dq), _hip.ptr(dk), _hip.ptr(dv), _hip.ptr(cos),
+                                          _hip.ptr(sin), B, S, nh, nkv, D, 1, _hip.ptr(pid), cos.shape[0],
+                                          _hip.stream()), "qkv_rope_bwd")
+        return dqkv, None, None, None, None, None
+
+
+def qkv_split_rope(qkv, nh: int, nkv: int, cos, sin, pos_ids=None):
+    """qkv: [B, S, nh + 2 nkv, D] (a packed QKV projection, heads ordered
+    q | k | v) -> contiguous (rope(q), rope(k), v), each [B, S, heads, D]."""
+    if _hip.bf16_path(qkv):
+        qkv = _hip.bf16(qkv)
+        q4 = qkv[:, :, :nh]
+        return _QkvRopeFn.apply(qkv, nh, nkv, _table(cos, q4, pos_ids), _table(sin, q4, pos_ids), pos_ids)
+    q, k, v = qkv.split([nh, nkv, nkv], dim=2)
+    return _rope_ref(q, cos, sin, 1.0, pos_ids), _rope_ref(k, cos, sin, 1.0, pos_ids), v.contiguous()

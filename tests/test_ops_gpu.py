@@ -162,6 +162,29 @@ def test_rope():
     assert _rel(x.grad, xf.grad) < 2e-2
 
 
+@pytest.mark.parametrize("D,nh,nkv,pos", [(128, 8, 2, False), (64, 4, 4, True)])
+def test_qkv_split_rope_fused(D, nh, nkv, pos):
+    """Fused split + RoPE of a packed QKV projection (dw_qkv_rope) against
+    split views + the fp32 rope reference, forward and backward (the packed
+    gradient written in one pass, v's gradient copied through)."""
+    from dlrover_wuqiong_amd.ops.rope import _rope_ref, qkv_split_rope, rope_table
+
+    B, S = 2, 96
+    cos, sin = rope_table(S + 8, D, device=DEV)
+    pid = torch.randint(0, S + 8, (B, S), device=DEV) if pos else None
+    qkv = torch.randn(B, S, nh + 2 * nkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    q, k, v = qkv_split_rope(qkv, nh, nkv, cos, sin, pid)
+    assert q.is_contiguous() and k.is_contiguous() and v.is_contiguous()
+    qf = qkv.detach().float().requires_grad_()
+    rq, rk, rv = qf.split([nh, nkv, nkv], dim=2)
+    rq, rk = _rope_ref(rq, cos, sin, 1.0, pid), _rope_ref(rk, cos, sin, 1.0, pid)
+    assert _rel(q, rq) < 1e-2 and _rel(k, rk) < 1e-2 and torch.equal(v.float(), rv)
+    gq, gk, gv = torch.randn_like(q), torch.randn_like(k), torch.randn_like(v)
+    (q.float() * gq.float()).sum().add((k.float() * gk.float()).sum()).add((v.float() * gv.float()).sum()).backward()
+    (rq * gq.float()).sum().add((rk * gk.float()).sum()).add((rv * gv.float()).sum()).backward()
+    assert _rel(qkv.grad, qf.grad) < 2e-2
+
+
 def test_rope_bf16_table_and_bad_shape():
     """FSDP2 mixed precision casts the cos/sin layer inputs to bf16: the op
     upcasts them (never reads a bf16 table as fp32) and rejects short tables."""
