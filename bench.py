@@ -109,6 +109,8 @@ def parse(argv=None):
                         "HBM snapshot (the kill then always lands mid-flush: HBM-only restore)")
     p.add_argument("--rehearse-shared-device", action="store_true",
                    help="N ranks share cuda:0 over gloo: rehearses the N>1 fault path on one GPU")
+    p.add_argument("--no-frameworks", action="store_true",
+                   help="skip the FSDP / Megatron flash-checkpoint rows (N=1, GPT2-1.5B only)")
     p.add_argument("--step-overlap", action="store_true",
                    help="run the optimizer update under the next forward (optimizers/overlap.py)")
     # worker-only
@@ -266,6 +268,9 @@ def launcher(a) -> int:
                 # from host memory: compare the like-for-like number
                 res["load_vs_baseline"] = round(imp["load_sec"] / REF_LOAD_SEC, 4)
                 res["load_vs_baseline_basis"] = "load_sec_shm (restarted process, restore from host shm)"
+        if res is not None and not a.no_frameworks and n == 1 and a.model.startswith("gpt2") and \
+                not a.rehearse_shared_device:
+            res.update(framework_rows(a, run_dir))
         if res is not None:
             res["launcher_wall_s"] = round(time.time() - T_LAUNCH, 1)
     finally:
@@ -279,6 +284,70 @@ def launcher(a) -> int:
 
 
 T_LAUNCH = time.time()
+
+# reference rows for GPT-1.5B: flash save pause / in-memory load, seconds
+REF_FRAMEWORK = {"fsdp": (2.9, 15.1), "megatron": (1.2, 2.1)}
+
+
+def _json_tail(text: str):
+    for line in reversed(text.splitlines()):
+        line = line.strip()
+        if line.startswith("{"):
+            try:
+                return json.loads(line)
+            except ValueError:
+                pass
+    return None
+
+
+def framework_rows(a, run_dir) -> dict:
+    """The reference's other GPT-1.5B rows, measured here so the driver's run
+    carries them: FSDP (FSDP2 + FsdpShardCheckpointer, scripts/
+    bench_fsdp_llama.py) and Megatron-LM layout (MegatronCheckpointer,
+    scripts/bench_megatron_tp_shard.py at TP=1).  Each is a separate process
+    on the same GPU, after the DDP jobs; a failure is reported, never fatal."""
+    out = {}
+    env = {k: v for k, v in os.environ.items() if k not in _SCRUB}
+    env.update({"PYTHONPATH": REPO + os.pathsep + env.get("PYTHONPATH", ""),
+                "HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0")})
+    jobs = {
+        "fsdp": ([sys.executable, "-u", os.path.join(REPO, "scripts", "bench_fsdp_llama.py"), "--model", a.model,
+                  "--seq", str(a.seq), "--micro-batch", str(a.micro_batch), "--steps", "8", "--ckpt-interval", "4",
+                  "--ckpt-dir", os.path.join(a.ckpt_dir, f"fsdp_{os.getpid()}")],
+                 dict(MASTER_PORT=str(29571 + os.getpid() % 1000), DWAMD_SHM_PREFIX=f"bf{os.getpid()}")),
+        "megatron": ([sys.executable, "-u", os.path.join(REPO, "scripts", "bench_megatron_tp_shard.py"), "--model",
+                      "gpt2-1.5b" if a.model == "gpt2-1.5b" else "llama-tiny", "--tp", "1", "--saves", "3",
+                      "--work-gemms", "1200" if a.model == "gpt2-1.5b" else "2", "--ckpt-dir",
+                      os.path.join(a.ckpt_dir, f"meg_{os.getpid()}")],
+                     dict(DWAMD_SHM_PREFIX=f"bm{os.getpid()}")),
+    }
+    for name, (cmd, extra) in jobs.items():
+        e = dict(env, **extra)
+        t0 = time.time()
+        try:
+            r = subprocess.run(cmd, env=e, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240,
+                               start_new_session=True)
+            with open(os.path.join(run_dir, f"{name}.err"), "w") as f:
+                f.write(r.stderr[-20000:])
+            j = _json_tail(r.stdout) if r.returncode == 0 else None
+        except subprocess.TimeoutExpired:
+            j, r = None, None
+        prefix = extra.get("DWAMD_SHM_PREFIX", "")
+        _cleanup(prefix, cmd[cmd.index("--ckpt-dir") + 1])
+        if j is None:
+            out[f"{name}_rc"] = r.returncode if r is not None else 124
+            continue
+        ref_save, ref_load = REF_FRAMEWORK[name]
+        save = j.get("value")
+        load = j.get("load_sec")
+        ref = a.model == "gpt2-1.5b"
+        out[name] = {"save_sec": save, "load_sec": load, "load_verified": j.get("load_verified"),
+                     "save_vs_baseline": round(save / ref_save, 4) if (save and ref) else None,
+                     "load_vs_baseline": round(load / ref_load, 4) if (load and ref) else None,
+                     "ckpt_bytes": j.get("ckpt_bytes_per_rank", j.get("ckpt_bytes")),
+                     "train_step_ms": j.get("train_step_ms"), "wall_s": round(time.time() - t0, 1),
+                     "reference_s": {"save": ref_save, "load": ref_load}}
+    return out
 
 
 def summarize(a, run_dir, n, wall):

@@ -72,3 +72,20 @@ def test_bench_eight_ranks_sliced(tmp_path):
     assert res["load_verified"] and res["replicas_identical"] and res["timed_saves_ok"]
     assert res["restarts"] == 1 and res["load_verified_after_restart"]
     assert res["pg_adopted_after_restart"] is True  # 8 standbys pre-formed the 8-rank world
+
+
+def test_framework_rows_plumbing(tmp_path):
+    """The FSDP and Megatron-layout flash-checkpoint rows bench.py adds at
+    N=1 (tiny models on CPU): both measured, restored and verified."""
+    import sys as _sys
+
+    _sys.path.insert(0, REPO)
+    import bench
+
+    a = bench.parse(["--model", "gpt2-tiny", "--seq", "64", "--micro-batch", "2", "--ckpt-dir", str(tmp_path / "ck")])
+    out = bench.framework_rows(a, str(tmp_path))
+    for name in ("fsdp", "megatron"):
+        assert name in out, out
+        row = out[name]
+        assert row["load_verified"] is True and row["save_sec"] > 0 and row["load_sec"] > 0
+        assert row["save_vs_baseline"] is None  # ratios only for the reference's GPT2-1.5B
