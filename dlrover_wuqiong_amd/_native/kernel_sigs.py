@@ -56,6 +56,8 @@ SIGS = {
     # optim.hip
     "dw_adam_flat": (i32, [vp, i32, vp, vp, i32, vp, vp, vp, i64, i64, f32, f32, f32, f32, f32,
                            f32, f32, i32, vp, vp]),
+    "dw_adam_replay": (i32, [vp, i32, vp, vp, vp, i64, i32, vp, i32, vp, vp, vp, vp, f32, f32, f32, f32, i32, vp,
+                             i32, vp]),
     "dw_agd_flat": (i32, [vp, i32, vp, vp, i32, vp, vp, vp, i64, i64, f32, f32, f32, f32, f32,
                           f32, f32, f32, f32, vp, vp]),
     "dw_sumsq_flat": (i32, [vp, i32, i64, vp, vp, vp]),

@@ -55,6 +55,19 @@ __device__ __forceinline__ bool decays(const unsigned char* mask, int64_t n_deca
   return mask ? (mask[i >> 6] != 0) : (i < n_decay);
 }
 
+// One AdamW / Adam-L2 update of one element -- shared by the flat update and
+// the deferred-state replay below, so both produce bit-identical results.
+__device__ __forceinline__ void adam_elem(float g, float gs, bool decay, const AdamArgs& a, float step_size,
+                                          float rbc2, float& w, float& mm, float& vv) {
+  float gk = g * gs;
+  if (!a.adamw && decay) gk += a.wd * w;
+  mm = a.beta1 * mm + (1.f - a.beta1) * gk;
+  vv = a.beta2 * vv + (1.f - a.beta2) * gk * gk;
+  const float denom = sqrtf(vv) * rbc2 + a.eps;
+  if (a.adamw && decay) w -= a.lr * a.wd * w;
+  w -= step_size * mm / denom;
+}
+
 // master == nullptr: the param itself is the fp32 master (P must be float)
 template <typename G, typename P>
 __global__ void __launch_bounds__(256) adam_flat_kernel(P* __restrict__ param, float* __restrict__ master,
@@ -77,13 +90,7 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(P* __restrict__ param, f
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const bool decay = a.decay_mask ? dblk : (i + k) < a.n_decay;
-      float gk = g[k] * gs;
-      if (!a.adamw && decay) gk += a.wd * w[k];
-      mm[k] = a.beta1 * mm[k] + (1.f - a.beta1) * gk;
-      vv[k] = a.beta2 * vv[k] + (1.f - a.beta2) * gk * gk;
-      const float denom = sqrtf(vv[k]) * rbc2 + a.eps;
-      if (a.adamw && decay) w[k] -= a.lr * a.wd * w[k];
-      w[k] -= step_size * mm[k] / denom;
+      adam_elem(g[k], gs, decay, a, step_size, rbc2, w[k], mm[k], vv[k]);
     }
     st8<float>(m, i, mm);
     st8<float>(v, i, vv);
@@ -94,17 +101,88 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(P* __restrict__ param, f
   for (int64_t i = (nvec << 3) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const bool decay = decays(a.decay_mask, a.n_decay, i);
-    float gk = ld<G>(grad, i) * gs;
     float w = master ? master[i] : ld<P>(param, i);
-    if (!a.adamw && decay) gk += a.wd * w;
-    float mk = a.beta1 * m[i] + (1.f - a.beta1) * gk;
-    float vk = a.beta2 * v[i] + (1.f - a.beta2) * gk * gk;
-    if (a.adamw && decay) w -= a.lr * a.wd * w;
-    w -= step_size * mk / (sqrtf(vk) * rbc2 + a.eps);
+    float mk = m[i], vk = v[i];
+    adam_elem(ld<G>(grad, i), gs, decay, a, step_size, rbc2, w, mk, vk);
     m[i] = mk; v[i] = vk;
     if (master) master[i] = w;
     st<P>(param, i, w);
   }
+}
+
+// Deferred optimizer-state write-back (flash-checkpoint ring snapshots,
+// optimizers/fused.py): K consecutive updates of [0, n) from K saved
+// gradients.  write_state = 0: only the parameters are written (the update
+// of an element whose OLD master / exp_avg / exp_avg_sq a pending snapshot
+// has not copied yet -- they stay untouched); write_state = 1: the replay
+// once the snapshot has them -- master, moments and (identical) parameters.
+constexpr int REPLAY_MAX = 8;
+struct AdamReplay {
+  AdamArgs a[REPLAY_MAX];        // per step: lr, bc1, bc2 (+ the shared betas / eps / wd)
+  const void* grad[REPLAY_MAX];  // saved gradients, element 0 = element lo of the flat buffer
+  const float* gscale[REPLAY_MAX];
+  int K, write_state;
+};
+
+template <typename G, typename P>
+__global__ void __launch_bounds__(256) adam_replay_kernel(P* __restrict__ param, float* __restrict__ master,
+                                                          float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                          AdamReplay r) {
+  float gs[REPLAY_MAX], ss[REPLAY_MAX], rb[REPLAY_MAX];
+#pragma unroll
+  for (int k = 0; k < REPLAY_MAX; ++k) {
+    if (k < r.K) {
+      gs[k] = r.gscale[k] ? *r.gscale[k] : 1.f;
+      ss[k] = r.a[k].lr / r.a[k].bc1;
+      rb[k] = rsqrtf(r.a[k].bc2);
+    }
+  }
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float w = master ? master[i] : ld<P>(param, i);
+    float mk = m[i], vk = v[i];
+    const bool decay = decays(r.a[0].decay_mask, r.a[0].n_decay, i);
+    for (int k = 0; k < r.K; ++k)
+      adam_elem(ld<G>((const G*)r.grad[k], i), gs[k], decay, r.a[k], ss[k], rb[k], w, mk, vk);
+    if (r.write_state) {
+      m[i] = mk;
+      v[i] = vk;
+      if (master) master[i] = w;
+    }
+    st<P>(param, i, w);
+  }
+}
+
+// lrs / bc1s / bc2s / grads / gscales: host arrays of K (<= 8) entries.
+extern "C" int dw_adam_replay(void* param, int param_dtype, void* master, void* m, void* v, int64_t n, int K,
+                              const void* const* grads, int grad_dtype, const void* const* gscales, const float* lrs,
+                              const float* bc1s, const float* bc2s, float beta1, float beta2, float eps, float wd,
+                              int adamw, const void* decay_mask, int write_state, void* stream) {
+  if (K < 1 || K > REPLAY_MAX || n < 0) return (int)hipErrorInvalidValue;
+  AdamReplay r{};
+  r.K = K;
+  r.write_state = write_state;
+  for (int k = 0; k < K; ++k) {
+    r.a[k] = AdamArgs{lrs[k], beta1, beta2, eps, wd, bc1s[k], bc2s[k], n, 0, adamw,
+                      (const unsigned char*)decay_mask};
+    r.grad[k] = grads[k];
+    r.gscale[k] = (const float*)gscales[k];
+  }
+  if (n == 0) return 0;
+  const int grid = dw_grid_for(n, 256, 8192);
+  hipStream_t s = (hipStream_t)stream;
+  if (param_dtype == 1 && grad_dtype == 1)
+    hipLaunchKernelGGL((adam_replay_kernel<bf16_t, bf16_t>), dim3(grid), dim3(256), 0, s, (bf16_t*)param,
+                       (float*)master, (float*)m, (float*)v, n, r);
+  else if (param_dtype == 1 && grad_dtype == 0)
+    hipLaunchKernelGGL((adam_replay_kernel<float, bf16_t>), dim3(grid), dim3(256), 0, s, (bf16_t*)param,
+                       (float*)master, (float*)m, (float*)v, n, r);
+  else if (param_dtype == 0 && grad_dtype == 0)
+    hipLaunchKernelGGL((adam_replay_kernel<float, float>), dim3(grid), dim3(256), 0, s, (float*)param,
+                       (float*)master, (float*)m, (float*)v, n, r);
+  else
+    hipLaunchKernelGGL((adam_replay_kernel<bf16_t, float>), dim3(grid), dim3(256), 0, s, (float*)param,
+                       (float*)master, (float*)m, (float*)v, n, r);
+  DW_LAUNCH_RET;
 }
 
 // dtype codes: 0 fp32, 1 bf16

@@ -210,9 +210,25 @@ _OPTIMIZERS = None  # optimizers seen stepping (weak set): their tensors are wri
 
 def _optimizer_step_fence(opt, _args, _kwargs):
     _OPTIMIZERS.add(opt)
+    offer = getattr(opt, "offer_ring_fence", None)
     for c in list(_FENCED):
+        # a pending RING snapshot: an optimizer that can defer the write-back
+        # of its not-yet-copied state (optimizers/fused.py) takes the fence
+        # over instead of stalling its update until the ring has drained
+        if offer is not None and c.ring_pending() and offer(c):
+            continue
         c.fence()
-    _FENCED.clear()
+        _FENCED.discard(c)
+
+
+def _merge(ranges: List[Tuple[int, int]]) -> List[Tuple[int, int]]:
+    out: List[Tuple[int, int]] = []
+    for a, b in sorted(r for r in ranges if r[1] > r[0]):
+        if out and a <= out[-1][1]:
+            out[-1] = (out[-1][0], max(out[-1][1], b))
+        else:
+            out.append((a, b))
+    return out
 
 
 def register_optimizer(opt):
@@ -278,6 +294,15 @@ def _pending_updates(device) -> list:
 
     # ... and optimizer state a restart's restore is still copying in
     return pending_events(device) + deferred_restore.events(device)
+
+
+def _flush_deferred_state():
+    """Optimizers that deferred the write-back of state a ring snapshot was
+    still copying (optimizers/fused.py) complete it before anything
+    snapshots that state again."""
+    from ..optimizers.fused import flush_deferred_state
+
+    flush_deferred_state()
 
 
 def _install_fence_hook():
@@ -528,6 +553,7 @@ class GpuCopier:
         once the snapshot sits complete in the staging buffer, before its
         PCIe flush (HBM-tier stamp: a standby-owned staging buffer survives
         this process, so the step is recoverable from then on)."""
+        _flush_deferred_state()
         if self._use_ring(hi - lo):
             return self._save_slice_ring(layout, shm_payload_addr, lo, hi, on_done, sync)
         snap = self.snapshot(layout, lo, hi, before_copy)
@@ -540,6 +566,7 @@ class GpuCopier:
         shm slot is not needed yet: the engine enqueues this first and picks /
         stamps the slot (gloo vote, metadata pickling) while the copy runs."""
         n = hi - lo
+        _flush_deferred_state()  # a deferred-state optimizer writes its state back before a new snapshot
         self.last_snapshot_mode = "full"
         self._refresh_external(n)
         self._decide_buffers(n)
@@ -685,6 +712,59 @@ class GpuCopier:
             torch.cuda.current_stream(self.device).wait_event(ev)
             self._fence_ev = None
 
+    # ------------------------------- ring progress (deferred-state optimizers)
+    def ring_pending(self) -> bool:
+        """A ring snapshot whose chunk copies may not all have run yet."""
+        return self._ring_gate is not None
+
+    def _ring_wait_enqueued(self):
+        gate = self._ring_gate
+        if gate is not None:
+            gate.wait()  # the flush thread has enqueued every chunk copy (host side, quick)
+
+    def ring_done(self) -> bool:
+        """Every chunk of the pending ring snapshot has been copied (its
+        sources may be written again)."""
+        if self._ring_gate is None:
+            return True
+        self._ring_wait_enqueued()
+        ev = self._ring_last.get("ev")
+        return ev is None or ev.query()
+
+    def ring_sources(self) -> List[Tuple[int, int]]:
+        """Device address ranges the pending ring snapshot reads."""
+        chunks = getattr(self, "_ring_chunks", None)
+        if chunks is None or self._ring_gate is None:
+            return []
+        return _merge([r for srcs in chunks[0] for r in srcs])
+
+    def ring_staged(self) -> List[Tuple[int, int]]:
+        """Source ranges already copied into the ring (chunk events done at
+        the time of the call: a lower bound)."""
+        chunks = getattr(self, "_ring_chunks", None)
+        if chunks is None or self._ring_gate is None:
+            return []
+        self._ring_wait_enqueued()
+        srcs, evs = chunks
+        return _merge([r for j, ev in enumerate(evs) if ev is not None and ev.query() for r in srcs[j]])
+
+    def ring_wait_ranges(self, ranges: List[Tuple[int, int]], stream=None):
+        """Order ``stream`` (default: current) after the chunk copies that
+        read any of ``ranges`` (device-side waits)."""
+        chunks = getattr(self, "_ring_chunks", None)
+        if chunks is None or self._ring_gate is None:
+            return
+        self._ring_wait_enqueued()
+        stream = stream or torch.cuda.current_stream(self.device)
+        srcs, evs = chunks
+        for j, ev in enumerate(evs):
+            if ev is not None and any(a < hi and lo < b for a, b in srcs[j] for lo, hi in ranges):
+                stream.wait_event(ev)
+
+    def ring_last_event(self):
+        self._ring_wait_enqueued()
+        return self._ring_last.get("ev")
+
     # ------------------------------------------------------- staging ring
     def _use_ring(self, n: int) -> bool:
         if n <= 0 or self.staging_mode == "full":
@@ -810,13 +890,18 @@ class GpuCopier:
                         o += c
                     t += 1
                 bounds.append((r0, len(rows), c0, c1))
+            # per chunk: the merged source address ranges it copies (what a
+            # deferred-state optimizer asks about, see ring_staged)
+            chunk_src = [_merge([(r[0], r[0] + r[2]) for r in rows[b0:b1]]) for b0, b1, _c0, _c1 in bounds]
             descs = (torch.from_numpy(np.asarray(rows, dtype=np.uint64).view(np.int64)).to(self.device)
                      if rows else torch.empty(0, 3, dtype=torch.int64, device=self.device))
-            plan = (descs, bounds, build_descs(now_descs, self.device) if now_descs else None)
+            plan = (descs, bounds, build_descs(now_descs, self.device) if now_descs else None, chunk_src)
             if len(self._ring_cache) >= 4:
                 self._ring_cache.pop(next(iter(self._ring_cache)))
             self._ring_cache[key] = plan
-        descs, bounds, now_d = plan
+        descs, bounds, now_d, chunk_src = plan
+        chunk_evs: List[Optional[torch.cuda.Event]] = [None] * len(bounds)
+        self._ring_chunks = (chunk_src, chunk_evs)
         if now_d is not None:
             launch_multi_copy(now_d, cur)  # forward-written storages: copied before returning
         for e, a, b in intersect_extents(layout.cpu_extents(), lo, hi):
@@ -851,6 +936,7 @@ class GpuCopier:
                     launch_multi_copy(descs[r0:r1], cstream)
                     ready = torch.cuda.Event()
                     ready.record(cstream)
+                    chunk_evs[j] = ready
                     self.side_stream.wait_event(ready)
                     dst = shm_payload_addr + lo + c0
                     src = ring_base + (j % K) * C

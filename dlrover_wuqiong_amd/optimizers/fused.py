@@ -22,6 +22,18 @@ from ..ops import _hip
 from ..parallel.flat import FlatParams
 
 
+import weakref
+
+_DEFERRING = weakref.WeakSet()  # optimizers holding a deferred state write-back
+
+
+def flush_deferred_state():
+    """Complete every pending deferred state write-back (device-side waits
+    for the ring snapshots involved, then the replay kernels)."""
+    for opt in list(_DEFERRING):
+        opt.flush_deferred()
+
+
 class _FlatOptimizer(torch.optim.Optimizer):
     def __init__(self, flat: FlatParams, defaults: dict, master_weights: Optional[bool] = None,
                  max_grad_norm: float = 0.0):
@@ -107,9 +119,11 @@ class _FlatOptimizer(torch.optim.Optimizer):
         return self._overlap
 
     def join(self):
-        """Order the current stream after a pending overlapped update."""
+        """Order the current stream after a pending overlapped update (and a
+        deferred state write-back: the state is complete afterwards)."""
         if self._overlap is not None:
             self._overlap.join()
+        self.flush_deferred()
 
     def _run_update(self, launch_range):
         """The update over the whole buffer: one launch, or piecewise on the
@@ -119,6 +133,161 @@ class _FlatOptimizer(torch.optim.Optimizer):
         else:
             launch_range(0, self.flat.numel)
 
+    # ---------------------------- deferred state write-back (ring snapshots)
+    # A flash-checkpoint snapshot through the bounded HBM ring (copier.py
+    # _save_slice_ring) reads parameters and optimizer state while the next
+    # forward / backward run; the next update normally has to wait until the
+    # ring has taken ALL of them -- with a state larger than the ring that is
+    # the PCIe drain of the excess (70B TP=8 shard: 123.5 GB, 64 GB ring,
+    # ~0.7 s stall per save, profiles/r3/tp8_shard_70b_staging_ring64.json).
+    # Instead the update runs at once: the elements whose state the ring has
+    # copied are updated normally; for the others only the NEW PARAMETERS are
+    # written (the next forward needs them) while their master / exp_avg /
+    # exp_avg_sq keep the snapshot's values, and the step's gradient (+ clip
+    # coefficient, lr, bias corrections) is kept.  Once the ring has drained,
+    # one replay kernel applies the K kept steps and writes the state -- the
+    # same per-element math (csrc/kernels/optim.hip adam_elem), so the result
+    # is bit-identical to having waited.  Up to DWAMD_DEFER_STATE_STEPS
+    # (default 4) steps are deferred; the memory cost is one gradient copy of
+    # the deferred elements per step.  ``DWAMD_DEFER_STATE=0`` turns it off.
+    _dsw = None
+    _dsw_offer = None
+
+    def offer_ring_fence(self, copier) -> bool:
+        import os
+
+        if (not self._dsw_supported() or os.environ.get("DWAMD_DEFER_STATE", "1") == "0"
+                or self._overlap is not None or not self.flat.data.is_cuda):
+            return False
+        if self._dsw is not None and self._dsw["copier"] is not copier:
+            return False
+        self._dsw_offer = copier
+        return True
+
+    def _dsw_supported(self) -> bool:
+        return False
+
+    def _dsw_ranges(self, lo: int, hi: int):
+        out = []
+        for t, es in ((self.exp_avg, 4), (self.exp_avg_sq, 4), (self.master, 4)):
+            if t is not None:
+                out.append((t.data_ptr() + es * lo, t.data_ptr() + es * hi))
+        return out
+
+    def _dsw_first_unstaged(self, copier) -> int:
+        """First flat element whose state the ring reads but has not copied
+        yet (flat.numel: none)."""
+        src, staged = copier.ring_sources(), copier.ring_staged()
+        n = self.flat.numel
+        first = n
+        for t in (self.exp_avg, self.exp_avg_sq, self.master):
+            if t is None:
+                continue
+            base, end = t.data_ptr(), t.data_ptr() + 4 * n
+            # the part of the buffer the snapshot covers, minus what it has copied
+            for a, b in src:
+                a, b = max(a, base), min(b, end)
+                if a >= b:
+                    continue
+                cur = a
+                for sa, sb in staged:
+                    if sa <= cur < sb:
+                        cur = sb
+                if cur < b:
+                    first = min(first, (cur - base) // 4)
+                    break
+        return first
+
+    def _dsw_replay(self, write_state: bool, extra=None):
+        """Launch the replay over the deferred elements: the kept steps (+
+        ``extra`` = this step's (grad view, gscale, lr, bc1, bc2))."""
+        import ctypes
+
+        d = self._dsw
+        lo, f = d["lo"], self.flat
+        n = f.numel - lo
+        steps = list(d["steps"]) + ([extra] if extra is not None else [])
+        K = len(steps)
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        arr = ctypes.c_void_p * K
+        farr = ctypes.c_float * K
+        grads = arr(*[ctypes.c_void_p(x[0].data_ptr()) for x in steps])
+        gss = arr(*[ctypes.c_void_p(x[1].data_ptr() if x[1] is not None else 0) for x in steps])
+        ms = self.master
+        _hip.check(_hip.lib().dw_adam_replay(
+            _hip.ptr(f.data[lo:]), _hip.dtype_code(f.data), _hip.ptr(None if ms is None else ms[lo:]),
+            _hip.ptr(self.exp_avg[lo:]), _hip.ptr(self.exp_avg_sq[lo:]), n, K, grads, _hip.dtype_code(f.grad), gss,
+            farr(*[x[2] for x in steps]), farr(*[x[3] for x in steps]), farr(*[x[4] for x in steps]), float(b1),
+            float(b2), float(g["eps"]), float(g["weight_decay"]), int(getattr(self, "adamw", True)),
+            _hip.ptr(f.decay_mask[lo // 64:]), int(write_state), _hip.stream()), "adam_replay")
+
+    def flush_deferred(self):
+        """Write the deferred state back: the current stream waits for the
+        ring snapshot (device side), then the replay runs on it."""
+        d = self._dsw
+        if d is None:
+            return
+        c = d["copier"]
+        c.fence()  # every chunk copied: the old state may be overwritten now
+        from ..flash_checkpoint import copier as _cp
+
+        if _cp._FENCED is not None:
+            _cp._FENCED.discard(c)
+        self._dsw_replay(True)
+        self._dsw = None
+        _DEFERRING.discard(self)
+
+    def _dsw_step(self, launch, gs, lr, bc1, bc2) -> bool:
+        """The update under a pending ring snapshot (see above).  Returns
+        False when no deferral applies (the caller runs the plain update)."""
+        import os
+
+        c = self._dsw_offer
+        self._dsw_offer = None
+        if c is None:
+            return False
+        f = self.flat
+        n = f.numel
+        from ..flash_checkpoint import copier as _cp
+
+        def discard():
+            if _cp._FENCED is not None:
+                _cp._FENCED.discard(c)
+
+        if c.ring_done():
+            # drained: complete any deferral, then the plain update
+            if self._dsw is not None:
+                self.flush_deferred()
+            c.fence()
+            discard()
+            return False
+        if self._dsw is None:
+            lo = self._dsw_first_unstaged(c) // 256 * 256
+            if lo >= n:  # the state is fully copied; only parameters may still be in flight
+                c.ring_wait_ranges([(f.data.data_ptr(), f.data.data_ptr() + f.data.element_size() * n)])
+                return False
+            self._dsw = {"copier": c, "lo": lo, "steps": []}
+            _DEFERRING.add(self)
+        d = self._dsw
+        kmax = max(1, min(7, int(os.environ.get("DWAMD_DEFER_STATE_STEPS", "4"))))
+        if len(d["steps"]) >= kmax:
+            self.flush_deferred()  # waits for the ring (the stall this bounds)
+            c.fence()
+            discard()
+            return False
+        lo = d["lo"]
+        # parameters are written below: their snapshot copies must have run
+        c.ring_wait_ranges([(f.data.data_ptr(), f.data.data_ptr() + f.data.element_size() * n)])
+        if lo > 0:
+            launch(0, lo)  # staged state: the plain update
+        gk = f.grad[lo:].clone()  # this step's gradient of the deferred elements
+        gsk = gs.clone() if gs is not None else None
+        step = (gk, gsk, float(lr), float(bc1), float(bc2))
+        self._dsw_replay(False, extra=step)  # new parameters from the snapshot's state + the kept steps
+        d["steps"].append(step)
+        return True
+
     def checkpoint_safe_tensors(self):
         """Tensors only ``step()`` writes (an overlapped flash-checkpoint
         snapshot may still be reading them after the save call returns)."""
@@ -126,6 +295,7 @@ class _FlatOptimizer(torch.optim.Optimizer):
 
     # -------------------------------------------------------- state dict
     def state_dict(self):
+        self.flush_deferred()
         # The per-parameter views never change: build them once.  All params
         # share one "step" tensor (same value), updated in place.
         if getattr(self, "_sd_views", None) is None:
@@ -147,6 +317,7 @@ class _FlatOptimizer(torch.optim.Optimizer):
         return {"state": state, "param_groups": groups}
 
     def load_state_dict(self, sd):
+        self.flush_deferred()
         st = sd["state"]
         if self.exp_avg.is_cuda:
             # a flash-checkpoint restore may still be landing this state on a
@@ -184,6 +355,9 @@ class FusedAdamW(_FlatOptimizer):
                          max_grad_norm)
         self.adamw = adamw
 
+    def _dsw_supported(self) -> bool:
+        return True
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
@@ -207,6 +381,10 @@ class FusedAdamW(_FlatOptimizer):
                     float(b2), float(g["eps"]), float(g["weight_decay"]), float(bc1), float(bc2), int(self.adamw),
                     _hip.ptr(f.decay_mask[lo // 64:]), _hip.stream()), "adam")
 
+            if self._dsw_offer is not None and self._dsw_step(launch, gs, g["lr"], bc1, bc2):
+                return loss
+            if self._dsw is not None:
+                self.flush_deferred()  # (a fence taken over earlier, no longer offered)
             self._run_update(launch)
             return loss
         # CPU path (reference math)

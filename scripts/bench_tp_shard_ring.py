@@ -42,6 +42,9 @@ def main():
                    help="auto: full-size HBM staging when it fits next to the model, else the bounded ring")
     p.add_argument("--no-prepare", dest="prepare", action="store_false",
                    help="skip Checkpointer.prepare(): the first save creates and pins the shm slots itself")
+    p.add_argument("--optimizer", choices=["flat", "multi"], default="flat",
+                   help="flat: FlatParams + FusedAdamW (flat bf16 params / fp32 master + Adam buffers; defers the "
+                        "state write-back under a ring snapshot, optimizers/fused.py); multi: MultiTensorAdamW")
     p.add_argument("--ring-hbm-gb", type=float, default=0.0,
                    help="HBM the ring may use (DWAMD_RING_HBM_GB; 0 = 4 x 1 GiB when forced, free HBM in auto)")
     a = p.parse_args()
@@ -67,7 +70,17 @@ def main():
         model = Llama(cfg)
     model.to(torch.bfloat16 if cuda else torch.float32)
     nparams = sum(p.numel() for p in model.parameters())
-    opt = MultiTensorAdamW(model.parameters(), lr=1e-5, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0)
+    if a.optimizer == "flat":
+        from dlrover_wuqiong_amd.optimizers.fused import FusedAdamW
+        from dlrover_wuqiong_amd.parallel.flat import FlatParams
+
+        flat = FlatParams(model, dtype=torch.bfloat16 if cuda else torch.float32, device=dev, lazy_zero_grad=True)
+        opt = FusedAdamW(flat, lr=1e-5, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0)
+        exp_avg = lambda: opt.exp_avg  # noqa
+    else:
+        opt = MultiTensorAdamW(model.parameters(), lr=1e-5, betas=(0.9, 0.95), weight_decay=0.1, max_grad_norm=1.0)
+        exp_avg = lambda: opt.flat_state_buffers()[dev]["exp_avg"]  # noqa
+    deferred_steps = []
     data = torch.randint(0, cfg.vocab_size, (2, a.micro_batch, a.seq + 1), device=dev)
     ck = DdpCheckpointer(a.ckpt_dir)
 
@@ -80,6 +93,8 @@ def main():
         loss = model(b[:, :-1], b[:, 1:])
         loss.backward()
         opt.step()
+        if getattr(opt, "_dsw", None) is not None:
+            deferred_steps.append(i)
         opt.zero_grad(set_to_none=True)
         return loss
 
@@ -150,11 +165,12 @@ def main():
     if cuda:
         torch.cuda.synchronize()
     want = [float(t.float().sum()) for t in model.state_dict().values()]
-    want_m = float(opt.flat_state_buffers()[dev]["exp_avg"].sum())
+    opt.join() if hasattr(opt, "join") else None
+    want_m = float(exp_avg().sum())
     with torch.no_grad():
         for t in model.state_dict().values():
             t.zero_()
-        opt.flat_state_buffers()[dev]["exp_avg"].zero_()
+        exp_avg().zero_()
     sync()
     t0 = time.perf_counter()
     ck.load_checkpoint(target=state())
@@ -162,7 +178,7 @@ def main():
         torch.cuda.synchronize()
     load_s = time.perf_counter() - t0
     got = [float(t.float().sum()) for t in model.state_dict().values()]
-    ok = got == want and float(opt.flat_state_buffers()[dev]["exp_avg"].sum()) == want_m
+    ok = got == want and float(exp_avg().sum()) == want_m
     med = statistics.median(steps)
     fence = (statistics.mean(after_save) - med) if after_save else 0.0
     # the ring's save call returns after enqueueing, but the next optimizer
@@ -190,7 +206,8 @@ def main():
         "step_after_save_ms": [round(1000 * x, 1) for x in after_save],
         "fence_cost_ms": round(1000 * fence, 1) if after_save else None,
         "tokens_per_s": round(a.micro_batch * a.seq / med, 1), "load_sec": round(load_s, 3),
-        "load_verified": bool(ok), "losses": [round(x, 3) for x in losses]}), flush=True)
+        "load_verified": bool(ok), "losses": [round(x, 3) for x in losses],
+        "optimizer": type(opt).__name__, "state_writeback_deferred_steps": deferred_steps}), flush=True)
     ck.close()
     prefix = f"dwamd_{os.environ['DWAMD_SHM_PREFIX']}"
     for f in os.listdir("/dev/shm"):  # ~250 GB of host memory: never leave it behind

@@ -604,3 +604,67 @@ def test_gpu_close_right_after_deferred_restore(tmp_path, monkeypatch):
     assert d.complete
     torch.cuda.synchronize()
     assert torch.equal(opt.exp_avg, want[0]) and torch.equal(opt.master, want[1])
+
+
+def _ring_run(tmp_path, monkeypatch, defer: bool, tag: str):
+    """Manual gradients (bit-reproducible), a ring snapshot at step 2 whose
+    PCIe drain is held back by a GPU sleep on the flush stream, 5 more
+    steps; returns the final state, the restored snapshot and whether the
+    optimizer deferred."""
+    from dlrover_wuqiong_amd.flash_checkpoint import copier as cp
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+
+    monkeypatch.setenv("DWAMD_STAGING", "ring")
+    monkeypatch.setenv("DWAMD_RING_SLOTS", "2")
+    monkeypatch.setenv("DWAMD_RING_CHUNK_MB", "1")
+    monkeypatch.setenv("DWAMD_DEFER_STATE", "1" if defer else "0")
+    orig = cp.GpuCopier._save_slice_ring
+
+    def held(self, *a, **k):
+        with torch.cuda.stream(self.side_stream):
+            torch.cuda._sleep(300_000_000)  # the ring's D2H waits ~0.15 s: chunk K+ cannot be copied yet
+        return orig(self, *a, **k)
+
+    monkeypatch.setattr(cp.GpuCopier, "_save_slice_ring", held)
+    model, opt, flat = _model_and_opt()
+    opt.max_grad_norm = 1.0  # the clip coefficient is part of the kept steps
+    ck = DdpCheckpointer(str(tmp_path / tag))
+    state = lambda: {"model": model.state_dict(), "optimizer": opt.state_dict()}  # noqa
+    g = torch.Generator(device="cpu").manual_seed(11)
+    deferred = []
+    snap = None
+    for s in range(7):
+        flat.grad.copy_(torch.randn(flat.numel, generator=g).to("cuda", flat.grad.dtype))
+        opt.step()
+        deferred.append(opt._dsw is not None)
+        if s == 2:
+            torch.cuda.synchronize()
+            snap = (flat.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(), opt.master.clone())
+            assert ck.save_checkpoint(3, state(), storage_type=StorageType.MEMORY)
+    opt.join()
+    torch.cuda.synchronize()
+    final = (flat.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(), opt.master.clone())
+    ck.wait_latest_checkpoint()
+    ck.load_checkpoint(target=state())
+    torch.cuda.synchronize()
+    restored = (flat.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(), opt.master.clone())
+    assert ck.engine._copier.last_snapshot_mode == "ring"
+    ck.close()
+    return final, snap, restored, deferred
+
+
+def test_gpu_ring_snapshot_deferred_state_writeback(tmp_path, monkeypatch):
+    """The update right after a ring snapshot does not wait for the ring:
+    elements whose state was not copied yet get new parameters only, and the
+    kept steps are replayed once the ring drained -- bit-identical to the
+    waiting update, and the snapshot holds the state of the save."""
+    final_w, snap_w, rest_w, def_w = _ring_run(tmp_path, monkeypatch, False, "wait")
+    final_d, snap_d, rest_d, def_d = _ring_run(tmp_path, monkeypatch, True, "defer")
+    assert not any(def_w) and any(def_d), def_d  # the deferral really happened
+    for a, b in zip(final_w, final_d):
+        assert torch.equal(a, b)
+    for s, r in zip(snap_d, rest_d):
+        assert torch.equal(s, r)  # the checkpoint is the state at the save
+    for a, b in zip(snap_w, snap_d):
+        assert torch.equal(a, b)
