@@ -48,6 +48,9 @@
 #ifndef DWAMD_DQ_SPLIT
 #define DWAMD_DQ_SPLIT 1  // A/B: 0 keeps the D=64 mask a runtime branch inside one tile body
 #endif
+#ifndef DWAMD_DQ_MINW
+#define DWAMD_DQ_MINW 1  // A/B: minimum waves per SIMD the dQ kernel is compiled for (3: <= 168 VGPRs)
+#endif
 
 #include "attn_bwd_common.h"
 
@@ -459,7 +462,7 @@ struct DqCfg {
 };
 
 template <int D, bool CAUSAL, bool EXT>
-__global__ void __launch_bounds__(64 * DqCfg<D>::WAVES, 1)
+__global__ void __launch_bounds__(64 * DqCfg<D>::WAVES, (D == 64 && !EXT) ? DWAMD_DQ_MINW : 1)
 attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
                    const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
                    bf16_t* __restrict__ dQ, int S, int H, int HKV, float scale, float scale_log2, AttnStrides st,
