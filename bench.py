@@ -631,14 +631,17 @@ def worker(a) -> int:
     # while parked adopts it here (elastic_agent/pg_preform.py); otherwise
     # this is the cold re-formation the recovery pays
     t_pg0 = time.time()
-    pg_preform.init_process_group(backend, device_id=device if backend == "nccl" else None)
+    pg_world1 = world > 1 or os.environ.get("DWAMD_BENCH_PG_WORLD1", "1") == "1"  # A/B switch
+    if pg_world1:
+        pg_preform.init_process_group(backend, device_id=device if backend == "nccl" else None)
     assert world == a.gpus, f"world {world} != --gpus {a.gpus}"
     ddp = FlatDDP(model, flat, bucket_mb=128)
     opt.grad_scale = 1.0 / max(1, world)
     # the communicator answers (the first collective of an adopted group
     # included) before the restore: part of the measured re-formation
     t = torch.ones(1, device=device if backend == "nccl" else torch.device("cpu"))
-    dist.all_reduce(t)
+    if pg_world1:
+        dist.all_reduce(t)
     if cuda:
         torch.cuda.synchronize()
     assert float(t.item()) == float(world)
@@ -1044,7 +1047,8 @@ def worker(a) -> int:
     ckpt.close()
     if world > 1:
         dist.barrier()
-    dist.destroy_process_group()
+    if dist.is_initialized():
+        dist.destroy_process_group()
     return 0
 
 
