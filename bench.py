@@ -494,6 +494,7 @@ def _fault_summary(a, ev, agent, step_sec, save_sec):
         # staging -> shm) -- a save waits when its buffer's flush lags
         "save_ms_after_restart": [e["save_ms"] for e in steps1 if e.get("save_ms") is not None],
         "flushes_after_restart": done.get("flushes"),
+        "gc_pauses_after_restart": done.get("gc_pauses"),
     }
     # a MODEL, not a measurement: one failure per hour, a checkpoint every
     # ckpt_interval steps (mean loss: half an interval of steps)
@@ -694,6 +695,20 @@ def worker(a) -> int:
         return loss
 
     kill_after = -1
+    import gc
+
+    gc_pauses = []  # Python GC pauses >= 5 ms (diagnosis of save / step outliers)
+    _gc_t = [0.0]
+
+    def _gc_cb(phase, info):
+        if phase == "start":
+            _gc_t[0] = time.perf_counter()
+        elif _gc_t[0]:
+            dt = time.perf_counter() - _gc_t[0]
+            if dt >= 0.005:
+                gc_pauses.append((round(time.time(), 3), info.get("generation"), round(1000 * dt, 1)))
+
+    gc.callbacks.append(_gc_cb)
 
     def _maybe_kill(completed):
         # mid-step: forward + backward enqueued (gradients all-reducing), the
@@ -1038,11 +1053,17 @@ def worker(a) -> int:
     # the window's flushes (HBM staging -> shm): queueing delay and duration
     # per flush, for save-wait diagnosis (a save waits when the previous
     # flush of its staging buffer has not landed)
-    flushes = [{"wait_ms": round(1000 * (t0 - te), 1), "ms": round(1000 * (t1 - t0), 1),
-                "gbps": round(nb / max(t1 - t0, 1e-9) / 1e9, 1)}
-               for te, t0, t1, nb in list(getattr(cp, "flush_log", []) or [])[-12:]] if cp is not None else []
+    flushes = []
+    for rec in (list(getattr(cp, "flush_log", []) or [])[-12:] if cp is not None else []):
+        te, t0, t1, nb = rec[:4]
+        f = {"wait_ms": round(1000 * (t0 - te), 1), "ms": round(1000 * (t1 - t0), 1),
+             "gbps": round(nb / max(t1 - t0, 1e-9) / 1e9, 1)}
+        if len(rec) >= 6:  # queued behind the previous flush / pinned share of the destination
+            f["queued_ms"] = round(1000 * (rec[4] - te), 1)
+            f["pinned_frac"] = round(rec[5] / max(1, nb), 3)
+        flushes.append(f)
     emit({"event": "done", "t": time.time(), "step": step, "start_step": start_step, "incarnation": incarnation,
-          "flushes": flushes, "skipped_saves": ckpt.engine.skipped_saves})
+          "flushes": flushes, "skipped_saves": ckpt.engine.skipped_saves, "gc_pauses": gc_pauses[-20:]})
     sync_all()
     ckpt.close()
     if world > 1:

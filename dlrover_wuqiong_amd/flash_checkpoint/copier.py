@@ -357,7 +357,7 @@ class GpuCopier:
         self.flush_blocks = int(os.environ.get("DWAMD_FLUSH_BLOCKS", "64"))
         self.flush_stats: List[Tuple[int, float]] = []
         # (t_snapshot_enqueued, t_flush_start, t_flush_end, nbytes) per flush
-        self.flush_log: List[Tuple[float, float, float, int]] = []
+        self.flush_log: List[tuple] = []
         self.pinned = PINNED
         # Future of the engine's background shm preparation (prefault +
         # hipHostRegister of this rank's slices): the flush -- never the
@@ -648,6 +648,7 @@ class GpuCopier:
         # drops the GIL); torch's Stream/Event.synchronize would hold the GIL
         # for the whole PCIe transfer and stall the training thread's launches.
         def flush():
+            t_start = time.perf_counter()
             if n > 0:
                 if on_snapshot is not None:
                     _check(_kern().dw_event_sync(ctypes.c_void_p(ev.cuda_event)), "snapshot sync")
@@ -682,7 +683,8 @@ class GpuCopier:
                 _check(_kern().dw_stream_sync(ctypes.c_void_p(self.side_stream.cuda_stream)), "flush sync")
                 t1 = time.perf_counter()
                 self.flush_stats.append((n, t1 - t0))
-                self.flush_log.append((t_enq, t0, t1, n))
+                # (+ when the flush thread took it up, pinned bytes of the destination)
+                self.flush_log.append((t_enq, t0, t1, n, t_start, sum(c for _a, c, p in segs if p)))
             else:
                 with torch.cuda.stream(self.side_stream):
                     self.side_stream.wait_event(ev)
