@@ -59,6 +59,9 @@ __device__ __forceinline__ bool decays(const unsigned char* mask, int64_t n_deca
 // the deferred-state replay below, so both produce bit-identical results.
 __device__ __forceinline__ void adam_elem(float g, float gs, bool decay, const AdamArgs& a, float step_size,
                                           float rbc2, float& w, float& mm, float& vv) {
+  // no FMA contraction: the surrounding kernel (vectorised flat update or
+  // the scalar replay loop) must not change how the products are rounded
+#pragma clang fp contract(off)
   float gk = g * gs;
   if (!a.adamw && decay) gk += a.wd * w;
   mm = a.beta1 * mm + (1.f - a.beta1) * gk;

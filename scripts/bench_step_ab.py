@@ -14,7 +14,32 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(variant, steps, model_name):
+def _init_pg(kind):
+    """A/B: a world-1 process group next to the training loop (none | nccl |
+    nccl_lazy | nccl_destroy | gloo)."""
+    if kind == "none":
+        return
+    import torch
+    import torch.distributed as dist
+
+    for k, v in dict(MASTER_ADDR="127.0.0.1", MASTER_PORT="29611", RANK="0", WORLD_SIZE="1").items():
+        os.environ.setdefault(k, v)
+    if kind == "gloo":
+        dist.init_process_group("gloo")
+        return
+    dev = torch.device("cuda", 0)
+    if kind == "nccl_lazy":
+        dist.init_process_group("nccl")  # no communicator until a collective
+        return
+    dist.init_process_group("nccl", device_id=dev)
+    t = torch.ones(1, device=dev)
+    dist.all_reduce(t)
+    torch.cuda.synchronize()
+    if kind == "nccl_destroy":
+        dist.destroy_process_group()
+
+
+def run(variant, steps, model_name, pg="none"):
     import torch
 
     from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
@@ -22,6 +47,8 @@ def run(variant, steps, model_name):
     from dlrover_wuqiong_amd.parallel.flat import FlatParams
 
     dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    _init_pg(pg)
     torch.manual_seed(0)
     cfg = GPT2Config.named(model_name)
     with torch.device(dev):
@@ -49,7 +76,7 @@ def run(variant, steps, model_name):
         step()
     torch.cuda.synchronize()
     ms = 1000 * (time.perf_counter() - t0) / steps
-    print(json.dumps({"variant": variant, "step_ms": round(ms, 2), "tok_s": round(8 * 1024 / ms * 1000),
+    print(json.dumps({"variant": variant, "pg": pg, "step_ms": round(ms, 2), "tok_s": round(8 * 1024 / ms * 1000),
                       "loss_last": round(float(losses[-1]), 4),
                       "env": {k: v for k, v in os.environ.items() if k.startswith("DWAMD_")}}), flush=True)
 
@@ -60,9 +87,10 @@ def main():
     p.add_argument("--model", default="gpt2-1.5b")
     p.add_argument("--variant", default="", help="off | on (one process); default: both")
     p.add_argument("--env", action="append", default=[], help="KEY=VAL for the child processes")
+    p.add_argument("--pg", default="none", help="world-1 process group: none | nccl | nccl_lazy | nccl_destroy | gloo")
     a = p.parse_args()
     if a.variant:
-        run(a.variant, a.steps, a.model)
+        run(a.variant, a.steps, a.model, a.pg)
         return
     env = dict(os.environ)
     for kv in a.env:
