@@ -71,13 +71,22 @@ def run(variant, steps, model_name, pg="none"):
     for _ in range(3):
         step()
     torch.cuda.synchronize()
+    import resource
+
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
+    c0 = time.thread_time()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
+    c1 = time.thread_time()  # main thread CPU time of issuing the steps
     torch.cuda.synchronize()
     ms = 1000 * (time.perf_counter() - t0) / steps
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    cpu_ms = 1000 * ((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) / steps
     print(json.dumps({"variant": variant, "pg": pg, "step_ms": round(ms, 2), "tok_s": round(8 * 1024 / ms * 1000),
                       "loss_last": round(float(losses[-1]), 4),
+                      "main_thread_cpu_ms_per_step": round(1000 * (c1 - c0) / steps, 2),
+                      "process_cpu_ms_per_step": round(cpu_ms, 2),
                       "env": {k: v for k, v in os.environ.items() if k.startswith("DWAMD_")}}), flush=True)
 
 
