@@ -10,4 +10,10 @@ for pg in none nccl nccl_lazy nccl_destroy gloo; do
   timeout -k 10 200 python -u scripts/bench_step_ab.py --steps 20 --variant off --pg $pg >> gpurun_out/r5/g3_step_pg.log 2>&1 || exit $?
 done
 TORCH_NCCL_ENABLE_MONITORING=0 TORCH_NCCL_ASYNC_ERROR_HANDLING=0 timeout -k 10 200 python -u scripts/bench_step_ab.py --steps 20 --variant off --pg nccl >> gpurun_out/r5/g3_step_pg.log 2>&1 || exit $?
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+for pg in none nccl; do
+  mkdir -p gpurun_out/r5/prof_pg_$pg
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5/prof_pg_$pg -o run -- python3 scripts/bench_step_ab.py --steps 6 --variant off --pg $pg > gpurun_out/r5/prof_pg_$pg/log.txt 2>&1 || exit $?
+  find gpurun_out/r5/prof_pg_$pg -name "*kernel_trace*" -delete
+done
 echo done
