@@ -87,7 +87,8 @@ def run(variant, steps, model_name, pg="none"):
                       "loss_last": round(float(losses[-1]), 4),
                       "main_thread_cpu_ms_per_step": round(1000 * (c1 - c0) / steps, 2),
                       "process_cpu_ms_per_step": round(cpu_ms, 2),
-                      "env": {k: v for k, v in os.environ.items() if k.startswith("DWAMD_")}}), flush=True)
+                      "env": {k: v for k, v in os.environ.items() if k.startswith(("DWAMD_", "TORCH_NCCL", "NCCL_",
+                                                                                       "RCCL_"))}}), flush=True)
 
 
 def main():

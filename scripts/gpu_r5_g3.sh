@@ -10,6 +10,8 @@ for pg in none nccl nccl_lazy nccl_destroy gloo; do
   timeout -k 10 200 python -u scripts/bench_step_ab.py --steps 20 --variant off --pg $pg >> gpurun_out/r5/g3_step_pg.log 2>&1 || exit $?
 done
 TORCH_NCCL_ENABLE_MONITORING=0 TORCH_NCCL_ASYNC_ERROR_HANDLING=0 timeout -k 10 200 python -u scripts/bench_step_ab.py --steps 20 --variant off --pg nccl >> gpurun_out/r5/g3_step_pg.log 2>&1 || exit $?
+TORCH_NCCL_USE_TENSOR_REGISTER_ALLOCATOR_HOOK=0 timeout -k 10 200 python -u scripts/bench_step_ab.py --steps 20 --variant off --pg nccl >> gpurun_out/r5/g3_step_pg.log 2>&1 || exit $?
+NCCL_RUNTIME_CONNECT=0 RCCL_MSCCL_ENABLE=0 timeout -k 10 200 python -u scripts/bench_step_ab.py --steps 20 --variant off --pg nccl >> gpurun_out/r5/g3_step_pg.log 2>&1 || exit $?
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 for pg in none nccl; do
   mkdir -p gpurun_out/r5/prof_pg_$pg
