@@ -2,7 +2,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r5
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_flash_ckpt_gpu.py tests/test_deterministic_gpu.py tests/test_optim_overlap_gpu.py > gpurun_out/r5/g3_pytest.log 2>&1
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_flash_ckpt_gpu.py tests/test_deterministic_gpu.py tests/test_optim_overlap_gpu.py tests/test_ops_gpu.py tests/test_llama.py > gpurun_out/r5/g3_pytest.log 2>&1
 rc=$?; echo pytest_rc=$rc
 [ $rc -le 1 ] || exit $rc
 # which part of a world-1 RCCL process group slows the training step
