@@ -73,3 +73,38 @@ def test_every_optimizer_step_waits_for_pending_restores():
     finally:
         f.done = True
         dr.pending()
+
+
+def test_deferred_state_prefix_from_ring_progress():
+    """The deferred state write-back (optimizers/fused.py) defers exactly the
+    flat elements whose master / exp_avg / exp_avg_sq the ring snapshot reads
+    but has not copied yet (address arithmetic only; CPU tensors)."""
+    from dlrover_wuqiong_amd.optimizers.fused import FusedAdamW
+    from dlrover_wuqiong_amd.parallel.flat import FlatParams
+
+    m = torch.nn.Sequential(torch.nn.Linear(64, 64), torch.nn.Linear(64, 64)).to(torch.bfloat16)
+    flat = FlatParams(m)
+    opt = FusedAdamW(flat, lr=1e-3)
+    n = flat.numel
+    bufs = [opt.exp_avg, opt.exp_avg_sq, opt.master]
+
+    class Ring:
+        def __init__(self, src, staged):
+            self.src, self.stg = src, staged
+
+        def ring_sources(self):
+            return self.src
+
+        def ring_staged(self):
+            return self.stg
+
+    whole = [(b.data_ptr(), b.data_ptr() + 4 * n) for b in bufs]
+    assert opt._dsw_first_unstaged(Ring(whole, [])) == 0  # nothing copied: everything deferred
+    assert opt._dsw_first_unstaged(Ring(whole, whole)) == n  # all copied: nothing deferred
+    # exp_avg fully copied, exp_avg_sq up to element 3000, master up to 5000
+    part = [whole[0], (whole[1][0], whole[1][0] + 4 * 3000), (whole[2][0], whole[2][0] + 4 * 5000)]
+    assert opt._dsw_first_unstaged(Ring(whole, sorted(part))) == 3000
+    # state the snapshot does not read at all never needs protecting
+    assert opt._dsw_first_unstaged(Ring([whole[0]], [])) == 0
+    assert opt._dsw_first_unstaged(Ring([whole[0]], [whole[0]])) == n
+    assert opt._dsw_supported()  # FusedAdamW supports it
