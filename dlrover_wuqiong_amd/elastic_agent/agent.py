@@ -426,7 +426,7 @@ class ElasticTrainingAgent:
         self._preform_gen = getattr(self, "_preform_gen", 0) + 1
         spec = {"store": self._pg_store_addr(), "prefix": f"{self.config.run_id}/standby_pg/{self._preform_gen}/",
                 "world": self.config.nproc_per_node, "backend": os.getenv("DWAMD_STANDBY_PG_BACKEND", "auto"),
-                "timeout": float(os.getenv("DWAMD_STANDBY_PG_TIMEOUT", "120"))}
+                "timeout": float(os.getenv("DWAMD_STANDBY_PG_TIMEOUT", "30"))}
         self._preform_prefix = spec["prefix"]
         for lr, p in self._standby.items():
             try:
