@@ -51,6 +51,13 @@
 #ifndef DWAMD_DQ_MINW
 #define DWAMD_DQ_MINW 1  // A/B: minimum waves per SIMD the dQ kernel is compiled for (3: <= 168 VGPRs)
 #endif
+#ifndef DWAMD_DQ64_O3
+// A/B: the D = 64 dQ kernel at three waves per SIMD -- one tile body with a
+// runtime mask branch (no split), row constants subtracted after the MFMAs
+// instead of held as 32 registers of accumulator init: 166 VGPRs, no spills
+// (238 otherwise, two waves per SIMD)
+#define DWAMD_DQ64_O3 0
+#endif
 
 #include "attn_bwd_common.h"
 
@@ -462,7 +469,7 @@ struct DqCfg {
 };
 
 template <int D, bool CAUSAL, bool EXT>
-__global__ void __launch_bounds__(64 * DqCfg<D>::WAVES, (D == 64 && !EXT) ? DWAMD_DQ_MINW : 1)
+__global__ void __launch_bounds__(64 * DqCfg<D>::WAVES, (D == 64 && !EXT) ? (DWAMD_DQ64_O3 ? 3 : DWAMD_DQ_MINW) : 1)
 attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
                    const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
                    bf16_t* __restrict__ dQ, int S, int H, int HKV, float scale, float scale_log2, AttnStrides st,
@@ -494,7 +501,7 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
   // operand holding -lse2 (resp. -delta) -- a lane's 16 registers all belong
   // to its query -- so P = exp2(S'), dS = P * dP' cost one exp and one mul
   // per element instead of fma + exp + sub + mul.
-  constexpr bool RI = DWAMD_DQ_RI && !EXT;
+  constexpr bool RI = DWAMD_DQ_RI && !EXT && !(D == 64 && DWAMD_DQ64_O3);
   // Q and dO fragments (B operands): lane holds row q, d = 16 kk + 8 hh .. +7
   u32x4 qf[C::KK], dof[C::KK];
 #pragma unroll
@@ -601,7 +608,7 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
       // subtile 0's softmax (a runtime mask branch split them).
       // (D=64 only: at D=128 the overlap needs ~200 more VGPRs than the 256 of
       // two waves per SIMD and spills; there the mask stays a runtime branch.)
-      constexpr bool SPLIT = DWAMD_DQ_SPLIT && D == 64;
+      constexpr bool SPLIT = DWAMD_DQ_SPLIT && D == 64 && !DWAMD_DQ64_O3;
       auto tile = [&](auto mask_c) {
         constexpr bool MASK = decltype(mask_c)::value;
       // one 32-key subtile at a time keeps S^T / dP^T at 32 registers
