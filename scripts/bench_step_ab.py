@@ -39,7 +39,28 @@ def _init_pg(kind):
         dist.destroy_process_group()
 
 
-def run(variant, steps, model_name, pg="none"):
+def _flusher(dev, gb):
+    """A checkpoint-flush stand-in: D2H of ``gb`` GB into pinned host memory
+    on the flash-checkpoint copier's side stream (same stream kind and copy
+    call as ``GpuCopier``), issued every other step."""
+    import torch
+
+    from dlrover_wuqiong_amd.flash_checkpoint.copier import GpuCopier
+
+    c = GpuCopier(dev)
+    n = int(gb * 1e9) // 2
+    src = torch.ones(n, dtype=torch.bfloat16, device=dev)
+    dst = torch.empty(n, dtype=torch.bfloat16, pin_memory=True)
+    s = c.side_stream
+
+    def go():
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            dst.copy_(src, non_blocking=True)
+    return go
+
+
+def run(variant, steps, model_name, pg="none", flush_gb=0.0):
     import torch
 
     from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
@@ -60,8 +81,13 @@ def run(variant, steps, model_name, pg="none"):
         opt.overlap_with_forward(model)
     data = torch.randint(0, cfg.vocab_size, (8, 1025), device=dev)
     losses = []
+    flush = _flusher(dev, flush_gb) if flush_gb else None
+    it = [0]
 
     def step():
+        it[0] += 1
+        if flush is not None and it[0] % 2 == 0:
+            flush()
         loss = model(data[:, :-1], data[:, 1:])
         loss.backward()
         opt.step()
@@ -83,12 +109,12 @@ def run(variant, steps, model_name, pg="none"):
     ms = 1000 * (time.perf_counter() - t0) / steps
     ru1 = resource.getrusage(resource.RUSAGE_SELF)
     cpu_ms = 1000 * ((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) / steps
-    print(json.dumps({"variant": variant, "pg": pg, "step_ms": round(ms, 2), "tok_s": round(8 * 1024 / ms * 1000),
+    print(json.dumps({"variant": variant, "pg": pg, "flush_gb": flush_gb, "step_ms": round(ms, 2), "tok_s": round(8 * 1024 / ms * 1000),
                       "loss_last": round(float(losses[-1]), 4),
                       "main_thread_cpu_ms_per_step": round(1000 * (c1 - c0) / steps, 2),
                       "process_cpu_ms_per_step": round(cpu_ms, 2),
                       "env": {k: v for k, v in os.environ.items() if k.startswith(("DWAMD_", "TORCH_NCCL", "NCCL_",
-                                                                                       "RCCL_"))}}), flush=True)
+                                                                                       "RCCL_", "HSA_", "GPU_", "HIP_"))}}), flush=True)
 
 
 def main():
@@ -98,9 +124,10 @@ def main():
     p.add_argument("--variant", default="", help="off | on (one process); default: both")
     p.add_argument("--env", action="append", default=[], help="KEY=VAL for the child processes")
     p.add_argument("--pg", default="none", help="world-1 process group: none | nccl | nccl_lazy | nccl_destroy | gloo")
+    p.add_argument("--flush-gb", type=float, default=0.0, help="D2H flush of this many GB every other step")
     a = p.parse_args()
     if a.variant:
-        run(a.variant, a.steps, a.model, a.pg)
+        run(a.variant, a.steps, a.model, a.pg, a.flush_gb)
         return
     env = dict(os.environ)
     for kv in a.env:
