@@ -60,7 +60,7 @@ def _flusher(dev, gb):
     return go
 
 
-def run(variant, steps, model_name, pg="none", flush_gb=0.0):
+def run(variant, steps, model_name, pg="none", flush_gb=0.0, flusher_first=False):
     import torch
 
     from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
@@ -69,6 +69,7 @@ def run(variant, steps, model_name, pg="none", flush_gb=0.0):
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    flush = _flusher(dev, flush_gb) if flush_gb and flusher_first else None
     _init_pg(pg)
     torch.manual_seed(0)
     cfg = GPT2Config.named(model_name)
@@ -81,7 +82,8 @@ def run(variant, steps, model_name, pg="none", flush_gb=0.0):
         opt.overlap_with_forward(model)
     data = torch.randint(0, cfg.vocab_size, (8, 1025), device=dev)
     losses = []
-    flush = _flusher(dev, flush_gb) if flush_gb else None
+    if flush is None and flush_gb:
+        flush = _flusher(dev, flush_gb)
     it = [0]
 
     def step():
@@ -109,7 +111,7 @@ def run(variant, steps, model_name, pg="none", flush_gb=0.0):
     ms = 1000 * (time.perf_counter() - t0) / steps
     ru1 = resource.getrusage(resource.RUSAGE_SELF)
     cpu_ms = 1000 * ((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) / steps
-    print(json.dumps({"variant": variant, "pg": pg, "flush_gb": flush_gb, "step_ms": round(ms, 2), "tok_s": round(8 * 1024 / ms * 1000),
+    print(json.dumps({"variant": variant, "pg": pg, "flush_gb": flush_gb, "flusher_first": flusher_first, "step_ms": round(ms, 2), "tok_s": round(8 * 1024 / ms * 1000),
                       "loss_last": round(float(losses[-1]), 4),
                       "main_thread_cpu_ms_per_step": round(1000 * (c1 - c0) / steps, 2),
                       "process_cpu_ms_per_step": round(cpu_ms, 2),
@@ -125,9 +127,10 @@ def main():
     p.add_argument("--env", action="append", default=[], help="KEY=VAL for the child processes")
     p.add_argument("--pg", default="none", help="world-1 process group: none | nccl | nccl_lazy | nccl_destroy | gloo")
     p.add_argument("--flush-gb", type=float, default=0.0, help="D2H flush of this many GB every other step")
+    p.add_argument("--flusher-first", action="store_true", help="create the flush stream before the process group")
     a = p.parse_args()
     if a.variant:
-        run(a.variant, a.steps, a.model, a.pg, a.flush_gb)
+        run(a.variant, a.steps, a.model, a.pg, a.flush_gb, a.flusher_first)
         return
     env = dict(os.environ)
     for kv in a.env:

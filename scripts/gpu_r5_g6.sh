@@ -18,6 +18,7 @@ HSA_ENABLE_SDMA=0 timeout -k 10 200 $AB --pg none >> $L 2>&1 || exit $?
 GPU_MAX_HW_QUEUES=8 timeout -k 10 200 $AB --pg nccl >> $L 2>&1 || exit $?
 TORCH_NCCL_USE_TENSOR_REGISTER_ALLOCATOR_HOOK=0 timeout -k 10 200 $AB --pg nccl >> $L 2>&1 || exit $?
 timeout -k 10 200 $AB --pg nccl_destroy >> $L 2>&1 || exit $?
+timeout -k 10 200 $AB --pg nccl --flusher-first >> $L 2>&1 || exit $?
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 for pg in none nccl; do
   d=gpurun_out/r5/prof_flush_$pg
