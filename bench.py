@@ -191,8 +191,9 @@ def _job(a, n: int, mode: str, run_dir: str, tag: str):
     for flag in ("no_fault", "no_persist", "act_ckpt", "step_overlap"):
         if getattr(a, flag):
             wargs.append("--" + flag.replace("_", "-"))
+    sb_mode = os.environ.get("DWAMD_BENCH_STANDBY", mode)  # A/B only ("off": no standby process)
     cmd = [sys.executable, "-u", "-m", "dlrover_wuqiong_amd.trainer.run", "--nnodes", "1", "--nproc-per-node",
-           str(n), "--max-restarts", "1", "--monitor-interval", "0.05", "--standby-mode", mode,
+           str(n), "--max-restarts", "1", "--monitor-interval", "0.05", "--standby-mode", sb_mode,
            "--standby-delay", "0", "--local-addr", "127.0.0.1", "--event-log", os.path.join(run_dir, "agent.jsonl")
            ] + wargs
     log(f"bench launcher ({mode} standby job):", " ".join(cmd))
@@ -539,6 +540,7 @@ def worker(a) -> int:
     # rehearsal: every rank on cuda:0 (RCCL refuses two ranks per device, so gloo)
     device = torch.device("cuda", 0 if rehearsal else lr) if cuda else torch.device("cpu")
     backend = "nccl" if (cuda and not rehearsal) else "gloo"
+    backend = os.environ.get("DWAMD_BENCH_PG_BACKEND", backend)  # A/B only
     cdev = device if backend == "nccl" else torch.device("cpu")  # small control tensors
     if cuda:
         torch.cuda.set_device(device)

@@ -52,11 +52,13 @@
 #define DWAMD_DQ_MINW 1  // A/B: minimum waves per SIMD the dQ kernel is compiled for (3: <= 168 VGPRs)
 #endif
 #ifndef DWAMD_DQ64_O3
-// A/B: the D = 64 dQ kernel at three waves per SIMD -- one tile body with a
+// The D = 64 dQ kernel at three waves per SIMD -- one tile body with a
 // runtime mask branch (no split), row constants subtracted after the MFMAs
 // instead of held as 32 registers of accumulator init: 166 VGPRs, no spills
-// (238 otherwise, two waves per SIMD)
-#define DWAMD_DQ64_O3 0
+// (238 otherwise, two waves per SIMD).  GPT2 shape backward 366 -> 381 TF/s
+// unpacked, 340 -> 350 packed (profiles/r5/attn_dq64_o3_ab.jsonl); 0: the
+// split two-wave form
+#define DWAMD_DQ64_O3 1
 #endif
 
 #include "attn_bwd_common.h"

@@ -59,16 +59,18 @@ __device__ __forceinline__ bool decays(const unsigned char* mask, int64_t n_deca
 // the deferred-state replay below, so both produce bit-identical results.
 __device__ __forceinline__ void adam_elem(float g, float gs, bool decay, const AdamArgs& a, float step_size,
                                           float rbc2, float& w, float& mm, float& vv) {
-  // no FMA contraction: the surrounding kernel (vectorised flat update or
-  // the scalar replay loop) must not change how the products are rounded
-#pragma clang fp contract(off)
+  // Every multiply-add is an explicit fma and no product feeds an add: the
+  // library builds with -ffp-contract=fast, and the backend contracts the
+  // packed-fp32 code of the vectorised flat update differently from the
+  // scalar replay loop (1-ulp master differences on GPU).  With nothing left
+  // to contract both kernels round identically.
   float gk = g * gs;
-  if (!a.adamw && decay) gk += a.wd * w;
-  mm = a.beta1 * mm + (1.f - a.beta1) * gk;
-  vv = a.beta2 * vv + (1.f - a.beta2) * gk * gk;
-  const float denom = sqrtf(vv) * rbc2 + a.eps;
-  if (a.adamw && decay) w -= a.lr * a.wd * w;
-  w -= step_size * mm / denom;
+  if (!a.adamw && decay) gk = __builtin_fmaf(a.wd, w, gk);
+  mm = __builtin_fmaf(a.beta1, mm, (1.f - a.beta1) * gk);
+  vv = __builtin_fmaf(a.beta2, vv, (1.f - a.beta2) * gk * gk);
+  const float denom = __builtin_fmaf(sqrtf(vv), rbc2, a.eps);
+  if (a.adamw && decay) w = __builtin_fmaf(-(a.lr * a.wd), w, w);
+  w = w - (step_size * mm) / denom;
 }
 
 // master == nullptr: the param itself is the fp32 master (P must be float)
