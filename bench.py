@@ -314,6 +314,7 @@ def framework_rows(a, run_dir) -> dict:
     jobs = {
         "fsdp": ([sys.executable, "-u", os.path.join(REPO, "scripts", "bench_fsdp_llama.py"), "--model", a.model,
                   "--seq", str(a.seq), "--micro-batch", str(a.micro_batch), "--steps", "8", "--ckpt-interval", "4",
+                  "--precision", "amp", "--act-ckpt", "on",
                   "--ckpt-dir", os.path.join(a.ckpt_dir, f"fsdp_{os.getpid()}")],
                  dict(MASTER_PORT=str(29571 + os.getpid() % 1000), DWAMD_SHM_PREFIX=f"bf{os.getpid()}")),
         "megatron": ([sys.executable, "-u", os.path.join(REPO, "scripts", "bench_megatron_tp_shard.py"), "--model",

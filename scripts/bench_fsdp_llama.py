@@ -29,9 +29,12 @@ def main():
     p.add_argument("--steps", type=int, default=8)
     p.add_argument("--ckpt-interval", type=int, default=4)
     p.add_argument("--ckpt-dir", default="/tmp/dwamd_fsdp_ckpt")
-    p.add_argument("--precision", choices=["amp", "half"], default="amp",
+    p.add_argument("--precision", choices=["amp", "half"], default="half",
                    help="amp: fp32 sharded params, FSDP2 casts to bf16 per gather; half: bf16 params + fp32 "
                         "masters inside the fused optimizer")
+    p.add_argument("--act-ckpt", choices=["on", "off"], default="off",
+                   help="activation checkpointing of the decoder layers (off: a 288 GB MI355X holds every "
+                        "activation of Llama-3-8B at S=4096, so the forward is not recomputed)")
     p.add_argument("--torch-optim", action="store_true", help="keep torch.optim.AdamW (no multi-tensor HIP kernel)")
     p.add_argument("--no-ckpt", action="store_true", help="step time only (no flash checkpoints)")
     p.add_argument("--fp8", action="store_true", help="auto_accelerate 'fp8' on the decoder layers' projections")
@@ -76,7 +79,8 @@ def main():
     ok, res, strategy = auto_accelerate(
         model, torch.optim.AdamW, optim_args={"lr": 2e-5, "betas": (0.9, 0.95), "weight_decay": 0.1},
         load_strategy=["module_replace", prec] + ([("fp8", {"include": ("layers", "h.")})] if a.fp8 else []) + [
-                       ("fsdp", {"wrap_cls": (layer_cls,)}), ("checkpoint", {"wrap_cls": (layer_cls,)})],
+                       ("fsdp", {"wrap_cls": (layer_cls,)})]
+        + ([("checkpoint", {"wrap_cls": (layer_cls,)})] if a.act_ckpt == "on" else []),
         fused_optimizer=not a.torch_optim)
     assert ok, "auto_accelerate failed"
     model, opt = res.model, res.optim
@@ -114,7 +118,7 @@ def main():
         if rank == 0:
             print(json.dumps({"metric": "fsdp train step", "n_gpus": world, "model": a.model, "seq_len": a.seq,
                               "precision": a.precision + ("+fp8" if a.fp8 else ""), "optimizer": type(opt).__name__,
-                              "train_step_ms": round(1000 * med, 1),
+                              "act_ckpt": a.act_ckpt, "train_step_ms": round(1000 * med, 1),
                               "tokens_per_s": round(world * a.micro_batch * a.seq / med, 1),
                               "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if cuda else None,
                               "step_ms": [round(1000 * x, 1) for x in steps], "losses": [round(x, 3) for x in losses]}))
