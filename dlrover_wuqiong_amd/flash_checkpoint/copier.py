@@ -776,6 +776,12 @@ class GpuCopier:
         if self._ring_decision is not None and self._ring_decision[0] == n:
             return self._ring_decision[1]
         ring = False
+        # standby-owned staging (this process's own after an activation, or
+        # the current standby's) needs no HBM of this process: adopt it before
+        # judging free memory -- right after a restart the dead worker's HBM
+        # may not be released yet, and a ring decided then (cached per slice
+        # size) would fence every later optimizer step on its PCIe drain
+        self._refresh_external(n)
         if self._ext is None:
             try:
                 free, _total = torch.cuda.mem_get_info(self.device)
