@@ -636,19 +636,22 @@ def worker(a) -> int:
     # this is the cold re-formation the recovery pays
     t_pg0 = time.time()
     pg_world1 = world > 1 or os.environ.get("DWAMD_BENCH_PG_WORLD1", "1") == "1"  # A/B switch
+    lazy = os.environ.get("DWAMD_BENCH_PG_LAZY") == "1"  # A/B only: no eager communicator, no check
     if pg_world1:
-        pg_preform.init_process_group(backend, device_id=device if backend == "nccl" else None)
+        pg_preform.init_process_group(backend, device_id=device if backend == "nccl" and not lazy else None)
     assert world == a.gpus, f"world {world} != --gpus {a.gpus}"
     ddp = FlatDDP(model, flat, bucket_mb=128)
     opt.grad_scale = 1.0 / max(1, world)
     # the communicator answers (the first collective of an adopted group
     # included) before the restore: part of the measured re-formation
     t = torch.ones(1, device=device if backend == "nccl" else torch.device("cpu"))
-    if pg_world1:
+    if pg_world1 and not lazy:
         dist.all_reduce(t)
     if cuda:
         torch.cuda.synchronize()
     assert float(t.item()) == float(world)
+    if pg_world1 and world == 1 and os.environ.get("DWAMD_BENCH_PG_DESTROY") == "1":  # A/B only
+        dist.destroy_process_group()
     t_pg = time.time()
     pg_info = {"adopted": pg_preform.adopted() is not None, "init_sec": round(t_pg - t_pg0, 4),
                "preform_sec": (pg_preform.adopted() or {}).get("sec"),  # paid while parked
