@@ -61,6 +61,17 @@
 #define DWAMD_DQ64_O3 1
 #endif
 
+#ifndef DWAMD_DQ_AUG
+// A/B: the dQ kernel's row constants as one extra MFMA k-step per chain:
+// Q (prescaled by scale * log2 e) and dO get a 17th..18th "column" holding
+// -lse2 resp. -delta split into bf16 hi + lo, K and V a matching column of
+// ones, so S^T arrives as S * scale * log2 e - lse2 and dP^T as dP - delta:
+// P = exp2(S'), dS = P * dP' -- one exp and one multiply per element and no
+// per-subtile accumulator initialisation, for two more MFMAs per 32 keys
+// (the kernel is VALU-bound: 9.7 VALU per MFMA, MFMA busy 14 %)
+#define DWAMD_DQ_AUG 0
+#endif
+
 #include "attn_bwd_common.h"
 
 // delta[b,h,q] = sum_d dO*O.  D/8 lanes per (b, s, h) row (16-byte loads),
@@ -503,14 +514,15 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
   // operand holding -lse2 (resp. -delta) -- a lane's 16 registers all belong
   // to its query -- so P = exp2(S'), dS = P * dP' cost one exp and one mul
   // per element instead of fma + exp + sub + mul.
-  constexpr bool RI = DWAMD_DQ_RI && !EXT && !(D == 64 && DWAMD_DQ64_O3);
+  constexpr bool AUG = DWAMD_DQ_AUG && !EXT;
+  constexpr bool RI = DWAMD_DQ_RI && !EXT && !(D == 64 && DWAMD_DQ64_O3) && !AUG;
   // Q and dO fragments (B operands): lane holds row q, d = 16 kk + 8 hh .. +7
   u32x4 qf[C::KK], dof[C::KK];
 #pragma unroll
   for (int kk = 0; kk < C::KK; ++kk) {
     if (q < SQ) {
       qf[kk] = *(const u32x4*)(Qb + (int64_t)q * st.q_rs + 16 * kk + 8 * hh);
-      if (RI) qf[kk] = scaled8(qf[kk], scale_log2);
+      if (RI || AUG) qf[kk] = scaled8(qf[kk], scale_log2);
       dof[kk] = *(const u32x4*)(dOb + (int64_t)q * st.do_rs + 16 * kk + 8 * hh);
     } else {
       qf[kk] = (u32x4){0, 0, 0, 0};
@@ -534,6 +546,18 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
     s_init[i] = -lse2;
     dp_init[i] = -dl;
   }
+  // AUG: the augmented k-step's operands.  B side (this lane's query row,
+  // k-index 8 hh .. +7): -lse2 and -delta as bf16 hi + lo in k-indices 0, 1;
+  // A side (key rows): ones there.  No visible key (lse2 = inf): -inf + 0.
+  u32x4 qaug = {0, 0, 0, 0}, doaug = {0, 0, 0, 0}, ones = {0, 0, 0, 0};
+  if (AUG && hh == 0) {
+    const float nl = -lse2, nd = -dl;
+    const float nl_hi = bf2f(f2bf(nl)), nd_hi = bf2f(f2bf(nd));
+    qaug[0] = pk2(nl_hi, nl > -INFINITY ? nl - nl_hi : 0.f);
+    doaug[0] = pk2(nd_hi, nd - nd_hi);
+    ones[0] = pk2(1.f, 1.f);
+  }
+  const f32x16 zero16 = {};
 
   int n_tiles = (SK + C::BK - 1) / C::BK;
   int t_begin = 0;
@@ -619,7 +643,10 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
         // dP^T starts at -delta (row constant as the initial accumulator) at
         // D=64; at D=128 that form cost this kernel 40+ spilled VGPRs
         f32x16 s, dp;
-        if (!RI) {
+        if (AUG) {
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(ones), as_bf(qaug), zero16, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(ones), as_bf(doaug), zero16, 0, 0, 0);
+        } else if (!RI) {
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             s[i] = 0.f;
@@ -644,7 +671,7 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
           }
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            if (RI) {
+            if (RI || AUG) {
               s[i] = __builtin_amdgcn_exp2f(s[i]) * dp[i];  // dS^T (scale applied in the epilogue)
             } else {
               const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], scale_log2, -lse2));
