@@ -28,6 +28,7 @@ def _init_pg(kind):
         dist.init_process_group("gloo")
         return
     dev = torch.device("cuda", 0)
+    env0 = dict(os.environ)
     if kind == "nccl_lazy":
         dist.init_process_group("nccl")  # no communicator until a collective
         return
@@ -35,23 +36,51 @@ def _init_pg(kind):
     t = torch.ones(1, device=dev)
     dist.all_reduce(t)
     torch.cuda.synchronize()
+    changed = {k: (env0.get(k), v) for k, v in os.environ.items() if env0.get(k) != v}
+    gone = [k for k in env0 if k not in os.environ]
+    print(json.dumps({"env_changed_by_rccl_init": changed, "env_removed": gone}), flush=True)
     if kind == "nccl_destroy":
         dist.destroy_process_group()
 
 
-def _flusher(dev, gb):
-    """A checkpoint-flush stand-in: D2H of ``gb`` GB into pinned host memory
-    on the flash-checkpoint copier's side stream (same stream kind and copy
-    call as ``GpuCopier``), issued every other step."""
+def _flusher(dev, gb, dst_kind="pinned"):
+    """A checkpoint-flush stand-in: D2H of ``gb`` GB on the flash-checkpoint
+    copier's side stream, issued every other step.  dst_kind "pinned": torch
+    pinned memory (hipHostMalloc); "shm": a /dev/shm file mapping registered
+    with hipHostRegister and copied with the copier's own call (what a real
+    flush writes)."""
+    import ctypes
+    import mmap
+
     import torch
 
-    from dlrover_wuqiong_amd.flash_checkpoint.copier import GpuCopier
+    from dlrover_wuqiong_amd.flash_checkpoint.copier import PinnedRegistry, GpuCopier, _kern
 
     c = GpuCopier(dev)
     n = int(gb * 1e9) // 2
     src = torch.ones(n, dtype=torch.bfloat16, device=dev)
-    dst = torch.empty(n, dtype=torch.bfloat16, pin_memory=True)
     s = c.side_stream
+    if dst_kind == "shm":
+        path = f"/dev/shm/dwamd_step_ab_{os.getpid()}"
+        fd = os.open(path, os.O_CREAT | os.O_RDWR, 0o600)
+        os.ftruncate(fd, 2 * n)
+        mm = mmap.mmap(fd, 2 * n)
+        os.close(fd)
+        os.unlink(path)  # the mapping keeps the pages; nothing left behind
+        addr = ctypes.addressof(ctypes.c_char.from_buffer(mm))
+        reg = PinnedRegistry()
+        assert reg.ensure(addr, 2 * n)
+        segs = reg.split(addr, 2 * n)
+        _flusher.keep = (mm, reg)
+
+        def go():
+            s.wait_stream(torch.cuda.current_stream(dev))
+            sp = ctypes.c_void_p(s.cuda_stream)
+            for a, cnt, pinned in segs:
+                assert _kern().dw_memcpy_async(ctypes.c_void_p(a), ctypes.c_void_p(src.data_ptr() + (a - addr)), cnt,
+                                               1 if pinned else 3, sp) == 0
+        return go
+    dst = torch.empty(n, dtype=torch.bfloat16, pin_memory=True)
 
     def go():
         s.wait_stream(torch.cuda.current_stream(dev))
@@ -60,7 +89,7 @@ def _flusher(dev, gb):
     return go
 
 
-def run(variant, steps, model_name, pg="none", flush_gb=0.0, flusher_first=False):
+def run(variant, steps, model_name, pg="none", flush_gb=0.0, flusher_first=False, flush_dst="pinned"):
     import torch
 
     from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
@@ -69,7 +98,7 @@ def run(variant, steps, model_name, pg="none", flush_gb=0.0, flusher_first=False
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    flush = _flusher(dev, flush_gb) if flush_gb and flusher_first else None
+    flush = _flusher(dev, flush_gb, flush_dst) if flush_gb and flusher_first else None
     _init_pg(pg)
     torch.manual_seed(0)
     cfg = GPT2Config.named(model_name)
@@ -83,7 +112,7 @@ def run(variant, steps, model_name, pg="none", flush_gb=0.0, flusher_first=False
     data = torch.randint(0, cfg.vocab_size, (8, 1025), device=dev)
     losses = []
     if flush is None and flush_gb:
-        flush = _flusher(dev, flush_gb)
+        flush = _flusher(dev, flush_gb, flush_dst)
     it = [0]
 
     def step():
@@ -111,7 +140,7 @@ def run(variant, steps, model_name, pg="none", flush_gb=0.0, flusher_first=False
     ms = 1000 * (time.perf_counter() - t0) / steps
     ru1 = resource.getrusage(resource.RUSAGE_SELF)
     cpu_ms = 1000 * ((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) / steps
-    print(json.dumps({"variant": variant, "pg": pg, "flush_gb": flush_gb, "flusher_first": flusher_first, "step_ms": round(ms, 2), "tok_s": round(8 * 1024 / ms * 1000),
+    print(json.dumps({"variant": variant, "pg": pg, "flush_gb": flush_gb, "flusher_first": flusher_first, "flush_dst": flush_dst, "step_ms": round(ms, 2), "tok_s": round(8 * 1024 / ms * 1000),
                       "loss_last": round(float(losses[-1]), 4),
                       "main_thread_cpu_ms_per_step": round(1000 * (c1 - c0) / steps, 2),
                       "process_cpu_ms_per_step": round(cpu_ms, 2),
@@ -128,9 +157,10 @@ def main():
     p.add_argument("--pg", default="none", help="world-1 process group: none | nccl | nccl_lazy | nccl_destroy | gloo")
     p.add_argument("--flush-gb", type=float, default=0.0, help="D2H flush of this many GB every other step")
     p.add_argument("--flusher-first", action="store_true", help="create the flush stream before the process group")
+    p.add_argument("--flush-dst", default="pinned", choices=["pinned", "shm"])
     a = p.parse_args()
     if a.variant:
-        run(a.variant, a.steps, a.model, a.pg, a.flush_gb, a.flusher_first)
+        run(a.variant, a.steps, a.model, a.pg, a.flush_gb, a.flusher_first, a.flush_dst)
         return
     env = dict(os.environ)
     for kv in a.env:
