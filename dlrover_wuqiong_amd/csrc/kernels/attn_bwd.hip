@@ -68,7 +68,10 @@
 // ones, so S^T arrives as S * scale * log2 e - lse2 and dP^T as dP - delta:
 // P = exp2(S'), dS = P * dP' -- one exp and one multiply per element and no
 // per-subtile accumulator initialisation, for two more MFMAs per 32 keys
-// (the kernel is VALU-bound: 9.7 VALU per MFMA, MFMA busy 14 %)
+// (9.7 VALU per MFMA, MFMA busy 14 %).  Measured: 30 % fewer VALU in the
+// tile body, no gain (GPT2 bwd 389 -> 382 TF/s, D=128 S=8k 737 -> 730;
+// profiles/r5/attn_dq_aug_ab.jsonl): dQ runs beside dK/dV and waits on
+// memory, so it stays off
 #define DWAMD_DQ_AUG 0
 #endif
 
