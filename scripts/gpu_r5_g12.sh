@@ -12,3 +12,6 @@ timeout -k 10 200 $AB --pg nccl --flush-dst shm >> $L 2>&1 || exit $?
 timeout -k 10 200 $AB --pg nccl --flush-dst shm --flusher-first >> $L 2>&1 || exit $?
 timeout -k 10 200 $AB --pg nccl --flush-dst pinned >> $L 2>&1 || exit $?
 echo done
+B="--no-fault --no-frameworks --no-import-fault --out-dir"
+HSA_NO_SCRATCH_RECLAIM=1 timeout -k 10 300 python bench.py $B gpurun_out/r5/e_noreclaim > gpurun_out/r5/e_noreclaim.json 2> gpurun_out/r5/e_noreclaim.err || exit $?
+echo done2
