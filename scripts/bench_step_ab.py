@@ -89,7 +89,8 @@ def _flusher(dev, gb, dst_kind="pinned"):
     return go
 
 
-def run(variant, steps, model_name, pg="none", flush_gb=0.0, flusher_first=False, flush_dst="pinned"):
+def run(variant, steps, model_name, pg="none", flush_gb=0.0, flusher_first=False, flush_dst="pinned",
+        pg_late=False):
     import torch
 
     from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
@@ -99,7 +100,8 @@ def run(variant, steps, model_name, pg="none", flush_gb=0.0, flusher_first=False
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     flush = _flusher(dev, flush_gb, flush_dst) if flush_gb and flusher_first else None
-    _init_pg(pg)
+    if not pg_late:
+        _init_pg(pg)
     torch.manual_seed(0)
     cfg = GPT2Config.named(model_name)
     with torch.device(dev):
@@ -109,6 +111,8 @@ def run(variant, steps, model_name, pg="none", flush_gb=0.0, flusher_first=False
     opt = FusedAdamW(flat, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0)
     if variant == "on":
         opt.overlap_with_forward(model)
+    if pg_late:  # as in bench.py: the group after the model and optimizer exist
+        _init_pg(pg)
     data = torch.randint(0, cfg.vocab_size, (8, 1025), device=dev)
     losses = []
     if flush is None and flush_gb:
@@ -140,7 +144,7 @@ def run(variant, steps, model_name, pg="none", flush_gb=0.0, flusher_first=False
     ms = 1000 * (time.perf_counter() - t0) / steps
     ru1 = resource.getrusage(resource.RUSAGE_SELF)
     cpu_ms = 1000 * ((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) / steps
-    print(json.dumps({"variant": variant, "pg": pg, "flush_gb": flush_gb, "flusher_first": flusher_first, "flush_dst": flush_dst, "step_ms": round(ms, 2), "tok_s": round(8 * 1024 / ms * 1000),
+    print(json.dumps({"variant": variant, "pg": pg, "flush_gb": flush_gb, "flusher_first": flusher_first, "flush_dst": flush_dst, "pg_late": pg_late, "step_ms": round(ms, 2), "tok_s": round(8 * 1024 / ms * 1000),
                       "loss_last": round(float(losses[-1]), 4),
                       "main_thread_cpu_ms_per_step": round(1000 * (c1 - c0) / steps, 2),
                       "process_cpu_ms_per_step": round(cpu_ms, 2),
@@ -158,9 +162,10 @@ def main():
     p.add_argument("--flush-gb", type=float, default=0.0, help="D2H flush of this many GB every other step")
     p.add_argument("--flusher-first", action="store_true", help="create the flush stream before the process group")
     p.add_argument("--flush-dst", default="pinned", choices=["pinned", "shm"])
+    p.add_argument("--pg-late", action="store_true", help="create the process group after the model / optimizer")
     a = p.parse_args()
     if a.variant:
-        run(a.variant, a.steps, a.model, a.pg, a.flush_gb, a.flusher_first, a.flush_dst)
+        run(a.variant, a.steps, a.model, a.pg, a.flush_gb, a.flusher_first, a.flush_dst, a.pg_late)
         return
     env = dict(os.environ)
     for kv in a.env:

@@ -2,6 +2,10 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r5/prof_scratch
 export HSA_ENABLE_IPC_MODE_LEGACY=0
+L=gpurun_out/r5/g13_pg_late.log
+AB="python -u scripts/bench_step_ab.py --steps 20 --variant off --flush-gb 8 --flush-dst shm"
+timeout -k 10 200 $AB --pg nccl --pg-late >> $L 2>&1 || exit $?
+timeout -k 10 200 $AB --pg nccl --pg-late --flusher-first >> $L 2>&1 || exit $?
 B="--no-fault --no-frameworks --no-import-fault --out-dir"
 HSA_NO_SCRATCH_RECLAIM=1 timeout -k 10 300 python bench.py $B gpurun_out/r5/e_noreclaim > gpurun_out/r5/e_noreclaim.json 2> gpurun_out/r5/e_noreclaim.err || exit $?
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
