@@ -90,7 +90,7 @@ def _flusher(dev, gb, dst_kind="pinned"):
 
 
 def run(variant, steps, model_name, pg="none", flush_gb=0.0, flusher_first=False, flush_dst="pinned",
-        pg_late=False):
+        pg_late=False, sync_each=False):
     import torch
 
     from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
@@ -128,6 +128,8 @@ def run(variant, steps, model_name, pg="none", flush_gb=0.0, flusher_first=False
         opt.step()
         flat.zero_grad()
         losses.append(loss.detach())
+        if sync_each:  # as bench.py: the host waits for the compute stream every step
+            torch.cuda.current_stream().synchronize()
 
     for _ in range(3):
         step()
@@ -144,7 +146,7 @@ def run(variant, steps, model_name, pg="none", flush_gb=0.0, flusher_first=False
     ms = 1000 * (time.perf_counter() - t0) / steps
     ru1 = resource.getrusage(resource.RUSAGE_SELF)
     cpu_ms = 1000 * ((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) / steps
-    print(json.dumps({"variant": variant, "pg": pg, "flush_gb": flush_gb, "flusher_first": flusher_first, "flush_dst": flush_dst, "pg_late": pg_late, "step_ms": round(ms, 2), "tok_s": round(8 * 1024 / ms * 1000),
+    print(json.dumps({"variant": variant, "pg": pg, "flush_gb": flush_gb, "flusher_first": flusher_first, "flush_dst": flush_dst, "pg_late": pg_late, "sync_each": sync_each, "step_ms": round(ms, 2), "tok_s": round(8 * 1024 / ms * 1000),
                       "loss_last": round(float(losses[-1]), 4),
                       "main_thread_cpu_ms_per_step": round(1000 * (c1 - c0) / steps, 2),
                       "process_cpu_ms_per_step": round(cpu_ms, 2),
@@ -163,9 +165,10 @@ def main():
     p.add_argument("--flusher-first", action="store_true", help="create the flush stream before the process group")
     p.add_argument("--flush-dst", default="pinned", choices=["pinned", "shm"])
     p.add_argument("--pg-late", action="store_true", help="create the process group after the model / optimizer")
+    p.add_argument("--sync-each", action="store_true", help="compute-stream synchronize after every step")
     a = p.parse_args()
     if a.variant:
-        run(a.variant, a.steps, a.model, a.pg, a.flush_gb, a.flusher_first, a.flush_dst, a.pg_late)
+        run(a.variant, a.steps, a.model, a.pg, a.flush_gb, a.flusher_first, a.flush_dst, a.pg_late, a.sync_each)
         return
     env = dict(os.environ)
     for kv in a.env:
