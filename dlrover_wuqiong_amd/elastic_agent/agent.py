@@ -43,6 +43,25 @@ from ..common.rpc import find_free_port, find_free_port_in_range, find_free_port
 from .master_client import MasterClient
 
 
+
+def _hw_queues(env: Dict[str, str]):
+    """Hardware queues per worker process.  HIP maps streams of one priority
+    onto at most GPU_MAX_HW_QUEUES hardware queues (default 4) and shares
+    them round-robin beyond that.  A worker here has more streams than that
+    (compute, RCCL's own and torch's RCCL stream, the attention backward's
+    dQ stream, the checkpoint snapshot / flush / restore streams); once RCCL
+    has taken its queues, a later stream can land on the compute stream's
+    queue, and a 20 GB checkpoint flush queued there stretched the next three
+    GPT2-1.5B steps from 109 to ~155 ms (profiles/r5/flush_queue_sharing.md).
+    Raised to DWAMD_GPU_MAX_HW_QUEUES (default 8) unless already higher."""
+    want = int(os.getenv("DWAMD_GPU_MAX_HW_QUEUES", "8") or 0)
+    try:
+        cur = int(env.get("GPU_MAX_HW_QUEUES", "4"))
+    except ValueError:
+        cur = 4
+    if want > cur:
+        env["GPU_MAX_HW_QUEUES"] = str(min(want, 32))
+
 class RendezvousTimeoutError(RuntimeError):
     pass
 
@@ -300,6 +319,7 @@ class ElasticTrainingAgent:
         # RCCL watchdog: a collective past DWAMD_COLLECTIVE_TIMEOUT_S tears the
         # process down (the agent then restarts the group) instead of hanging
         env.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "3")
+        _hw_queues(env)
         return env
 
     def _clear_ctl(self):
@@ -475,6 +495,7 @@ class ElasticTrainingAgent:
         env.setdefault("OMP_NUM_THREADS", "1")
         env["DWAMD_AGENT_CTL_DIR"] = self.ctl_dir
         env["DWAMD_STANDBY_LOCAL_RANK"] = str(local_rank)
+        _hw_queues(env)
         if self.config.standby_mode == "deep":
             from .standby import STANDBY_ENV
 
