@@ -330,11 +330,15 @@ class GpuCopier:
         # (every `stride`-th CU) instead.
         stride = flush_cu_stride if flush_cu_stride is not None else int(
             os.environ.get("DWAMD_FLUSH_CU_STRIDE", "8"))
-        # lowprio (default): non-blocking, lowest-priority queue -> the flush
-        # never implicitly serialises with the legacy null stream and loses
-        # dispatch arbitration to training kernels.  cumask: restrict the
-        # flush blit to every `stride`-th CU (blocking stream type).
-        kind = os.environ.get("DWAMD_FLUSH_STREAM", "lowprio")  # lowprio | cumask | highprio | plain
+        # plain (default): a normal-priority torch stream.  lowprio: a
+        # non-blocking lowest-priority stream -- with HIP's default 4 hardware
+        # queues per process, once RCCL's communicator has taken queues, a
+        # low-priority stream created afterwards ended up where the training
+        # stream waits behind the flush (GPT2-1.5B steps after a save 109 ->
+        # 150 ms; plain: 108, at 4 and 8 queues alike --
+        # profiles/r5/flush_queue_sharing.md).  cumask: restrict the flush
+        # blit to every `stride`-th CU (blocking stream type).
+        kind = os.environ.get("DWAMD_FLUSH_STREAM", "plain")  # plain | lowprio | cumask | highprio
         self._cumask_ptr = None
         self.flush_cus = 0
         self.flush_stream_kind = kind
