@@ -530,8 +530,10 @@ def test_gpu_deferred_optimizer_restore_orders_the_first_step(tmp_path, monkeypa
     torch.cuda.synchronize()
     # (embedding backward uses atomics: equal up to summation order; a step
     # that read the corrupted state would be off by O(1))
+    diag = [(n, int(torch.isnan(g.float()).sum()), int(torch.isnan(r.float()).sum()))
+            for n, g, r in zip(("param", "exp_avg", "master"), (flat.data, opt.exp_avg, opt.master), want)]
     for got, ref in zip((flat.data.float(), opt.exp_avg, opt.master), want):
-        torch.testing.assert_close(got, ref.float(), rtol=1e-2, atol=1e-3)
+        torch.testing.assert_close(got, ref.float(), rtol=1e-2, atol=1e-3, msg=lambda m: f"{m}\nNaNs (got, want): {diag}")
     if defer:
         assert d.resident_sec(timeout=30) > 0
     ck.close()
