@@ -519,6 +519,7 @@ def test_gpu_deferred_optimizer_restore_orders_the_first_step(tmp_path, monkeypa
     step()
     torch.cuda.synchronize()
     want = flat.data.clone(), opt.exp_avg.clone(), opt.master.clone()
+    want_step = opt.step_count
     # corrupt, restore (no sync), step at once
     flat.data.zero_()
     opt.exp_avg.fill_(3.0)
@@ -532,6 +533,9 @@ def test_gpu_deferred_optimizer_restore_orders_the_first_step(tmp_path, monkeypa
     # that read the corrupted state would be off by O(1))
     diag = [(n, int(torch.isnan(g.float()).sum()), int(torch.isnan(r.float()).sum()))
             for n, g, r in zip(("param", "exp_avg", "master"), (flat.data, opt.exp_avg, opt.master), want)]
+    diag.append(("step_count", opt.step_count, "dsw", opt._dsw is not None, "fenced",
+                 len(cp._FENCED) if cp._FENCED is not None else None, "want_step", want_step,
+                 "v_nan", int(torch.isnan(opt.exp_avg_sq).sum()), "v_min", float(opt.exp_avg_sq.min())))
     for got, ref in zip((flat.data.float(), opt.exp_avg, opt.master), want):
         torch.testing.assert_close(got, ref.float(), rtol=1e-2, atol=1e-3, msg=lambda m: f"{m}\nNaNs (got, want): {diag}")
     if defer:
@@ -569,6 +573,7 @@ def test_gpu_deferred_restore_then_optimizer_load_state_dict(tmp_path, monkeypat
     ck.wait_latest_checkpoint()
     torch.cuda.synchronize()
     want = flat.data.clone(), opt.exp_avg.clone(), opt.master.clone()
+    want_step = opt.step_count
     flat.data.zero_()
     opt.exp_avg.fill_(3.0)
     opt.master.fill_(-1.0)
