@@ -1103,8 +1103,16 @@ class GpuCopier:
 
     def close(self):
         try:
+            # an optimizer still deferring state behind this copier's ring
+            # writes it back now; then nothing pending may outlive the copier
+            # (a closed copier left in the fence set would be offered to
+            # later optimizers)
+            _flush_deferred_state()
             self.wait()
+            self.fence()
         finally:
+            if _FENCED is not None:
+                _FENCED.discard(self)
             self._executor.shutdown(wait=True)
             self.pinned.release_all()
             self._stagings = [None, None]

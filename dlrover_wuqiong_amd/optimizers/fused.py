@@ -161,11 +161,19 @@ class _FlatOptimizer(torch.optim.Optimizer):
             return False
         if self._dsw is not None and self._dsw["copier"] is not copier:
             return False
+        if self._dsw is None and not self._ring_touches(copier):
+            return False  # the ring reads none of this optimizer's tensors (someone else's snapshot)
         self._dsw_offer = copier
         return True
 
     def _dsw_supported(self) -> bool:
         return False
+
+    def _ring_touches(self, copier) -> bool:
+        f = self.flat
+        mine = [(f.data.data_ptr(), f.data.data_ptr() + f.data.element_size() * f.numel)] + self._dsw_ranges(
+            0, f.numel)
+        return any(a < mb and ma < b for a, b in copier.ring_sources() for ma, mb in mine)
 
     def _dsw_ranges(self, lo: int, hi: int):
         out = []
