@@ -530,6 +530,10 @@ def summarize_import(a, run_dir, wall, mode="import"):
 # =========================================================================
 def worker(a) -> int:
     t_proc = time.time()
+    if os.environ.get("DWAMD_BENCH_STACK_DUMP_S"):  # hang diagnosis: every thread's stack, periodically
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["DWAMD_BENCH_STACK_DUMP_S"]), repeat=True)
     import torch
     import torch.distributed as dist
 
