@@ -55,10 +55,9 @@ def _hw_queues(env: Dict[str, str]):
     GPT2-1.5B steps from 109 to ~155 ms (profiles/r5/flush_queue_sharing.md).
     The copier's flush stream is now a normal-priority stream, which does not
     share that way at 4 queues (107.3 ms at 4 and 107.2 at 8), so the
-    inherited value is kept by default: more queues per process also means
-    more user queues per GPU for the hardware scheduler to map (a worker and a
-    standby per GPU; several workers per GPU in a shared-device rehearsal).
-    DWAMD_GPU_MAX_HW_QUEUES=N raises it to N (at most 32)."""
+    inherited value is kept by default (more queues per process are more user
+    queues per GPU for the hardware scheduler to map, a worker and a standby
+    per GPU).  DWAMD_GPU_MAX_HW_QUEUES=N raises it to N (at most 32)."""
     want = int(os.getenv("DWAMD_GPU_MAX_HW_QUEUES", "0") or 0)
     try:
         cur = int(env.get("GPU_MAX_HW_QUEUES", "4"))
