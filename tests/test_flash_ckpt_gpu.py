@@ -502,10 +502,12 @@ def test_gpu_deferred_optimizer_restore_orders_the_first_step(tmp_path, monkeypa
 
     monkeypatch.setattr(cp.GpuCopier, "_pipelined_h2d", slow)
     model, opt, flat = _model_and_opt()
+    trail = [("built", opt.step_count)]
     ck = DdpCheckpointer(str(tmp_path / "ck"))
     state = lambda: {"model": model.state_dict(), "optimizer": opt.state_dict()}  # noqa
     assert ck.save_checkpoint(5, state(), storage_type=StorageType.MEMORY)
     ck.wait_latest_checkpoint()
+    trail.append(("saved", opt.step_count))
     x = torch.randint(0, model.cfg.vocab_size if hasattr(model, "cfg") else 50257, (2, 65), device="cuda",
                       generator=torch.Generator("cuda").manual_seed(7))
 
@@ -516,8 +518,11 @@ def test_gpu_deferred_optimizer_restore_orders_the_first_step(tmp_path, monkeypa
 
     ck.load_checkpoint(target=state())
     torch.cuda.synchronize()
+    trail.append(("loaded", opt.step_count, ck.engine.last_restore_source, id(opt._step_t),
+                  [id(v["step"]) for v in list(opt.state_dict()["state"].values())[:2]]))
     step()
     torch.cuda.synchronize()
+    trail.append(("stepped", opt.step_count))
     want = flat.data.clone(), opt.exp_avg.clone(), opt.master.clone()
     want_step = opt.step_count
     # corrupt, restore (no sync), step at once
@@ -535,7 +540,7 @@ def test_gpu_deferred_optimizer_restore_orders_the_first_step(tmp_path, monkeypa
             for n, g, r in zip(("param", "exp_avg", "master"), (flat.data, opt.exp_avg, opt.master), want)]
     diag.append(("step_count", opt.step_count, "dsw", opt._dsw is not None, "fenced",
                  len(cp._FENCED) if cp._FENCED is not None else None, "want_step", want_step,
-                 "v_nan", int(torch.isnan(opt.exp_avg_sq).sum()), "v_min", float(opt.exp_avg_sq.min())))
+                 "v_nan", int(torch.isnan(opt.exp_avg_sq).sum()), "v_min", float(opt.exp_avg_sq.min()), trail))
     for got, ref in zip((flat.data.float(), opt.exp_avg, opt.master), want):
         torch.testing.assert_close(got, ref.float(), rtol=1e-2, atol=1e-3, msg=lambda m: f"{m}\nNaNs (got, want): {diag}")
     if defer:
