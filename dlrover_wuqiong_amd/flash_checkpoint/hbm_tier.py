@@ -186,35 +186,15 @@ def find_published(ctl_dir: str, local_rank: int) -> Optional[dict]:
 
 
 def import_published(info: dict) -> Optional[List[HbmBuffer]]:
-    # one importer per device at a time (a node-wide file lock): in a
-    # shared-device rehearsal (two ranks importing their standbys' handles on
-    # the SAME device at once) one hipIpcOpenMemHandle never returned; with
-    # one process per GPU nothing contends here
-    import fcntl
-
-    try:
-        import torch
-
-        dev = torch.cuda.current_device()
-    except Exception:
-        dev = 0
-    import tempfile
-
-    lock = open(os.path.join(tempfile.gettempdir(), f"dwamd_ipc_import_{os.getuid()}_{dev}.lock"), "a")
     out = []
-    try:
-        fcntl.flock(lock, fcntl.LOCK_EX)
-        for hx in info["handles"]:
-            raw = bytes.fromhex(hx)
-            p = ctypes.c_void_p(0)
-            err = _kern().dw_ipc_open_handle(raw, ctypes.byref(p))
-            if err != 0:
-                logger.warning(f"importing the standby's HBM staging failed ({err}); keeping local buffers")
-                for b in out:
-                    b.release()
-                return None
-            out.append(HbmBuffer(int(p.value), int(info["nbytes"]), int(info["pid"]), owned=False))
-        return out
-    finally:
-        fcntl.flock(lock, fcntl.LOCK_UN)
-        lock.close()
+    for hx in info["handles"]:
+        raw = bytes.fromhex(hx)
+        p = ctypes.c_void_p(0)
+        err = _kern().dw_ipc_open_handle(raw, ctypes.byref(p))
+        if err != 0:
+            logger.warning(f"importing the standby's HBM staging failed ({err}); keeping local buffers")
+            for b in out:
+                b.release()
+            return None
+        out.append(HbmBuffer(int(p.value), int(info["nbytes"]), int(info["pid"]), owned=False))
+    return out
