@@ -508,6 +508,28 @@ def test_gpu_deferred_optimizer_restore_orders_the_first_step(tmp_path, monkeypa
     assert ck.save_checkpoint(5, state(), storage_type=StorageType.MEMORY)
     ck.wait_latest_checkpoint()
     trail.append(("saved", opt.step_count))
+
+    def shm_probe(tag):
+        # where the optimizer's step scalar sits in each slot of the segment
+        import numpy as np
+
+        from dlrover_wuqiong_amd.flash_checkpoint.layout import TensorMeta, iter_leaves
+
+        h = ck.engine._shm_handler
+        out = [tag, h.complete_steps(), h.num_slots, h.payload_size]
+        for slot in range(h.num_slots):
+            meta = h.get_meta(slot) or {}
+            tree = meta.get("tree")
+            if not isinstance(tree, dict) or "optimizer" not in tree:
+                out.append((slot, "no optimizer tree", sorted(tree) if isinstance(tree, dict) else type(tree)))
+                continue
+            m = next(iter(tree["optimizer"]["state"].values()))["step"]
+            assert isinstance(m, TensorMeta)
+            raw = np.frombuffer(h.shared_memory.buf, dtype=np.float32, count=1, offset=m.offset + h.payload_offset(slot))
+            out.append((slot, m.offset, str(m.dtype), m.device, float(raw[0])))
+        trail.append(tuple(out))
+
+    shm_probe("after_save")
     x = torch.randint(0, model.cfg.vocab_size if hasattr(model, "cfg") else 50257, (2, 65), device="cuda",
                       generator=torch.Generator("cuda").manual_seed(7))
 
@@ -518,6 +540,7 @@ def test_gpu_deferred_optimizer_restore_orders_the_first_step(tmp_path, monkeypa
 
     ck.load_checkpoint(target=state())
     torch.cuda.synchronize()
+    shm_probe("after_load")
     trail.append(("loaded", opt.step_count, ck.engine.last_restore_source, id(opt._step_t),
                   [id(v["step"]) for v in list(opt.state_dict()["state"].values())[:2]]))
     step()
