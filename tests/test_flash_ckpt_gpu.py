@@ -517,9 +517,16 @@ def test_gpu_deferred_optimizer_restore_orders_the_first_step(tmp_path, monkeypa
 
         h = ck.engine._shm_handler
         out = [tag, h.complete_steps(), h.num_slots, h.payload_size]
+        lay = ck.engine._layout_cache.cached() if hasattr(ck.engine, "_layout_cache") else None
+        if lay is not None:
+            sp = opt._step_t.data_ptr()
+            out.append(("cpu_extents", len(lay.cpu_extents()), [(e.src_ptr == sp, e.offset, e.nbytes)
+                                                               for e in lay.cpu_extents()][:4]))
         for slot in range(h.num_slots):
             meta = h.get_meta(slot) or {}
             tree = meta.get("tree")
+            if isinstance(tree, dict) and "model_states" in tree:
+                tree = tree["model_states"]
             if not isinstance(tree, dict) or "optimizer" not in tree:
                 out.append((slot, "no optimizer tree", sorted(tree) if isinstance(tree, dict) else type(tree)))
                 continue
