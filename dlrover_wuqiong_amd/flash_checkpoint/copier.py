@@ -640,6 +640,10 @@ class GpuCopier:
         of the staged bytes behind the snapshot's event."""
         layout, lo, hi, idx, stg, ev = (snap[k] for k in ("layout", "lo", "hi", "idx", "stg", "ev"))
         n = hi - lo
+        # the PCIe flush writes the device region only: host tensors (below)
+        # sit after it in the payload and must not be overwritten with the
+        # staging buffer's bytes at their offsets
+        n_dev = max(0, min(hi, layout.gpu_end) - lo)
         t_enq = snap["t_enq"]
         if n > 0:
             # CPU tensors go straight to shm (small: counters, rng state...)
@@ -670,15 +674,15 @@ class GpuCopier:
                 with torch.cuda.stream(self.side_stream):
                     self.side_stream.wait_event(ev)  # device-side dependency only
                     t0 = time.perf_counter()
-                    self._flush_t0[idx], self._flush_n[idx] = t0, n
+                    self._flush_t0[idx], self._flush_n[idx] = t0, n_dev
                     dst = shm_payload_addr + lo
                     src = stg.data_ptr()
                     sp = ctypes.c_void_p(self.side_stream.cuda_stream)
-                    segs = self.pinned.split(dst, n) if pinned else [(dst, n, False)]
+                    segs = (self.pinned.split(dst, n_dev) if pinned else [(dst, n_dev, False)]) if n_dev else []
                     dptr = _kern().dw_host_device_ptr(ctypes.c_void_p(dst)) if (
                         pinned and self.flush_mode == "kernel" and len(segs) == 1) else None
-                    if dptr and (n % 16 == 0):
-                        _check(_kern().dw_stream_copy(ctypes.c_void_p(dptr), ctypes.c_void_p(src), n,
+                    if dptr and (n_dev % 16 == 0):
+                        _check(_kern().dw_stream_copy(ctypes.c_void_p(dptr), ctypes.c_void_p(src), n_dev,
                                                       self.flush_blocks, sp), "D2H flush")
                     else:
                         for a, c, p in segs:
@@ -686,9 +690,9 @@ class GpuCopier:
                                                            1 if p else 3, sp), "D2H flush")
                 _check(_kern().dw_stream_sync(ctypes.c_void_p(self.side_stream.cuda_stream)), "flush sync")
                 t1 = time.perf_counter()
-                self.flush_stats.append((n, t1 - t0))
+                self.flush_stats.append((n_dev, t1 - t0))
                 # (+ when the flush thread took it up, pinned bytes of the destination)
-                self.flush_log.append((t_enq, t0, t1, n, t_start, sum(c for _a, c, p in segs if p)))
+                self.flush_log.append((t_enq, t0, t1, n_dev, t_start, sum(c for _a, c, p in segs if p)))
             else:
                 with torch.cuda.stream(self.side_stream):
                     self.side_stream.wait_event(ev)
@@ -844,6 +848,8 @@ class GpuCopier:
         the flush thread (it also waits for the shm registration), so the
         training thread never waits on PCIe unless it reaches the fence."""
         self.last_snapshot_mode = "ring"
+        hi_all = hi
+        hi = max(lo, min(hi, layout.gpu_end))  # the ring carries the device region; host tensors go to shm below
         n = hi - lo
         self.wait()  # one ring: the previous pipeline must have drained
         self.fence()
@@ -916,7 +922,7 @@ class GpuCopier:
         self._ring_chunks = (chunk_src, chunk_evs)
         if now_d is not None:
             launch_multi_copy(now_d, cur)  # forward-written storages: copied before returning
-        for e, a, b in intersect_extents(layout.cpu_extents(), lo, hi):
+        for e, a, b in intersect_extents(layout.cpu_extents(), lo, hi_all):
             runtime().dw_memcpy_parallel(ctypes.c_void_p(shm_payload_addr + a),
                                          ctypes.c_void_p(e.src_ptr + (a - e.offset)), b - a, 4)
         ev_start = torch.cuda.Event()

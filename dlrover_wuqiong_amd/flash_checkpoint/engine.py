@@ -996,7 +996,10 @@ class CheckpointEngine(ABC):
             # every rank reads the whole payload from shm.
             if require_hbm:
                 if hbm_src is not None:
-                    copier.write_back(hbm_src, base + s_lo, s_hi - s_lo)
+                    # the device region of this slice only: host tensors were
+                    # written to shm at save time and lie after it
+                    dev_end = max((m.offset + m.nbytes for m, _t in pairs if m.device == "cuda"), default=0)
+                    copier.write_back(hbm_src, base + s_lo, max(0, min(s_hi, dev_end) - s_lo))
                     h.set_slice_step(slot, self._slice_idx, step)
                 self._ctl_barrier()
                 self.last_restore_source = "hbm->shm"

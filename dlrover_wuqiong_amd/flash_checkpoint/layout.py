@@ -67,6 +67,14 @@ class Layout:
     def cpu_extents(self):
         return [e for e in self.extents if e.device != "cuda"]
 
+    @property
+    def gpu_end(self) -> int:
+        """End of the device region: plan_layout places every device storage
+        before every host one, so [0, gpu_end) is what a staging buffer's
+        PCIe flush may write -- host tensors (copied to shm directly) lie
+        beyond it and are never overwritten by staging bytes."""
+        return max((e.offset + e.nbytes for e in self.extents if e.device == "cuda"), default=0)
+
 
 def traverse(value: Any, visitor: Callable[[Any], Any]) -> Any:
     """Rebuild ``value`` with ``visitor`` applied to every non-container leaf."""
@@ -251,8 +259,10 @@ def plan_layout(state_dict: Any) -> Tuple[Layout, List[torch.Tensor]]:
     extents: List[Extent] = []
     tensor_offset: Dict[int, int] = {}
     cursor = 0
-    # deterministic order: first appearance in the state dict
-    order = sorted(groups.items(), key=lambda kv: min(x[2] for x in kv[1]))
+    # deterministic order: device storages first (the staging buffers' PCIe
+    # flush covers one contiguous device region and must not write over
+    # host tensors), then host ones; each by first appearance in the dict
+    order = sorted(groups.items(), key=lambda kv: (kv[0][0] != "cuda", min(x[2] for x in kv[1])))
     for key, ranges in order:
         ranges.sort()
         merged: List[List[int]] = []  # [start, end, [idx...]]

@@ -754,3 +754,37 @@ def test_gpu_ring_snapshot_deferred_state_writeback(tmp_path, monkeypatch):
         assert torch.equal(s, r)  # the checkpoint is the state at the save
     for a, b in zip(snap_w, snap_d):
         assert torch.equal(a, b)
+
+
+def test_gpu_flush_never_overwrites_host_tensors(tmp_path):
+    """A host (CPU) tensor between device tensors of a state dict (a torch
+    optimizer's per-parameter ``step``): the staging buffer's PCIe flush must
+    not write its stale bytes over the host tensor's slot in shm (the layout
+    puts device storages first; the flush covers that region only)."""
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+    from dlrover_wuqiong_amd.flash_checkpoint.ddp import DdpCheckpointer
+
+    a = torch.randn(1 << 20, device="cuda")
+    b = torch.randn(1 << 20, device="cuda")
+    step = torch.tensor(3.0)
+    ck = DdpCheckpointer(str(tmp_path / "ck"))
+    state = lambda: {"a": a, "step": step, "b": b}  # noqa
+    assert ck.save_checkpoint(1, state(), storage_type=StorageType.MEMORY)
+    ck.wait_latest_checkpoint()
+    lay = ck.engine._layout_cache.cached()
+    assert all(e.offset >= lay.gpu_end for e in lay.cpu_extents())  # host tensors after the device region
+    for t in ck.engine._copier._stagings:
+        if t is not None:
+            t.fill_(0xBF)  # garbage where a host tensor would sit inside the staging image
+    step.fill_(4.0)
+    assert ck.save_checkpoint(2, state(), storage_type=StorageType.MEMORY)
+    ck.wait_latest_checkpoint()
+    want = a.clone(), b.clone()
+    a.zero_()
+    b.zero_()
+    step.fill_(-1.0)
+    ck.load_checkpoint(target=state())
+    torch.cuda.synchronize()
+    assert float(step) == 4.0
+    assert torch.equal(a, want[0]) and torch.equal(b, want[1])
+    ck.close()
