@@ -174,11 +174,7 @@ def _job(a, n: int, mode: str, run_dir: str, tag: str):
     if a.rehearse_shared_device:
         env["DWAMD_REHEARSE_SHARED_DEVICE"] = "1"
         env["DWAMD_STANDBY_PG_BACKEND"] = "gloo"  # the standbys pre-form what the workers will ask for
-        # no HBM tier when several ranks share the card: a worker's
-        # hipIpcOpenMemHandle of its standby's buffers on the shared device
-        # never returned (gpurun_out/r5/rehearsal2b,c stack dumps); one
-        # process per GPU imports fine (every N=1 run)
-        env["DWAMD_HBM_TIER"] = "0"
+
     if mode == "import":
         # the reference's restart semantics: the replacement restores from
         # host shm (the framework default -- job "import_hbm" -- also gives
