@@ -14,8 +14,18 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 @pytest.mark.timeout(600)
 def test_wheel_ships_compat_packages_and_dlrover_run(tmp_path):
-    r = subprocess.run([sys.executable, "-m", "pip", "wheel", "--no-deps", "--no-build-isolation", "-w",
-                        str(tmp_path), REPO], capture_output=True, text=True, timeout=580)
+    import shutil
+
+    # setuptools builds in the source tree: leave no build/ or *.egg-info behind
+    leftovers = [os.path.join(REPO, d) for d in ("build", "dlrover_wuqiong_amd.egg-info")]
+    existed = {d: os.path.exists(d) for d in leftovers}
+    try:
+        r = subprocess.run([sys.executable, "-m", "pip", "wheel", "--no-deps", "--no-build-isolation", "-w",
+                            str(tmp_path), REPO], capture_output=True, text=True, timeout=580)
+    finally:
+        for d, was in existed.items():
+            if not was:
+                shutil.rmtree(d, ignore_errors=True)
     if r.returncode != 0 and "No module named pip" in r.stderr:
         pytest.skip("pip not available")
     assert r.returncode == 0, r.stderr[-4000:]
