@@ -27,6 +27,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_gpu_rehearse_ranks_shared_device(tmp_path, ranks):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    # the rehearsal's 2-4 workers + standbys share this card with the test
+    # process: hand back what earlier tests left in this process's cache
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
     cmd = [sys.executable, "-u", os.path.join(REPO, "bench.py"), "--gpus", str(ranks), "--rehearse-shared-device",
            "--model", "gpt2", "--micro-batch", "2", "--seq", "256", "--steps", "4", "--warmup", "2",
