@@ -221,6 +221,19 @@ def _optimizer_step_fence(opt, _args, _kwargs):
         _FENCED.discard(c)
 
 
+def _snapshot_stream(device) -> torch.cuda.Stream:
+    """The stream of overlapped / ring snapshot copies: HIGH priority.  HIP
+    shares hardware queues among the streams of one priority once a process
+    has more than GPU_MAX_HW_QUEUES of them; a snapshot copy queued behind the
+    previous checkpoint's 0.4 s PCIe flush (normal priority) stalled the next
+    optimizer step's fence by that much (GPT2-1.5B, overlapped snapshots:
+    steps after a save 491 ms).  A different priority is a different queue."""
+    try:
+        return torch.cuda.Stream(device=device, priority=-1)
+    except Exception:
+        return torch.cuda.Stream(device=device)
+
+
 def _merge(ranges: List[Tuple[int, int]]) -> List[Tuple[int, int]]:
     out: List[Tuple[int, int]] = []
     for a, b in sorted(r for r in ranges if r[1] > r[0]):
@@ -589,7 +602,7 @@ class GpuCopier:
         copy_stream = cur
         if self.overlap and n > 0:
             if self._snap_stream is None:
-                self._snap_stream = torch.cuda.Stream(device=self.device)
+                self._snap_stream = _snapshot_stream(self.device)
             copy_stream = self._snap_stream
             copy_stream.wait_stream(cur)  # the state as of this save call
             for e in _pending_updates(self.device):  # ... after an overlapped update
@@ -860,7 +873,7 @@ class GpuCopier:
             self._ring_free = [torch.cuda.Event() for _ in range(K)]
             self._ring_cache.clear()
         if self._snap_stream is None:
-            self._snap_stream = torch.cuda.Stream(device=self.device)
+            self._snap_stream = _snapshot_stream(self.device)
         cur = torch.cuda.current_stream(self.device)
         cstream = self._snap_stream
         ring_base = self._ring.data_ptr()
