@@ -170,6 +170,12 @@ def _job(a, n: int, mode: str, run_dir: str, tag: str):
         # a save whose staging buffer is still flushing WAITS (and the wait is
         # part of the measured pause) instead of being skipped
         "DWAMD_CKPT_BUSY": "wait",
+        # the training loop saves between iterations and writes parameters /
+        # optimizer state only in optimizer.step: the HBM snapshot copy runs
+        # on a side stream under the next forward, fenced by that step
+        # (copier.py; the pause is the host work only).  DWAMD_OVERLAP_SNAPSHOT=0:
+        # the copy on the compute stream inside the pause
+        "DWAMD_OVERLAP_SNAPSHOT": os.environ.get("DWAMD_OVERLAP_SNAPSHOT", "1"),
     })
     if a.rehearse_shared_device:
         env["DWAMD_REHEARSE_SHARED_DEVICE"] = "1"
@@ -396,6 +402,7 @@ def summarize(a, run_dir, n, wall):
         "train_step_ms": round(1000 * step_sec, 2),
         "tokens_per_s": round(a.micro_batch * a.seq * phase0["world"] / step_sec, 1),
         "optimizer_update": phase0.get("optimizer_update"),
+        "snapshot_copy": phase0.get("snapshot_copy"),
         "loss": phase0["loss"],
         "rccl_world": phase0["world"],
         # incarnation 0 forms its world cold: the cost a restart would pay
@@ -901,7 +908,9 @@ def worker(a) -> int:
               "backend": backend, "slices": ckpt.engine._num_slices, "hbm_plan": getattr(ckpt.engine, "hbm_plan", None),
               "host_plan": getattr(ckpt.engine, "host_plan", None),
               "gather": ckpt.engine._gather_group is not None, "pg": pg_info,
-              "optimizer_update": "under next forward" if opt._overlap is not None else "compute stream"})
+              "optimizer_update": "under next forward" if opt._overlap is not None else "compute stream",
+              "snapshot_copy": "overlapped (fenced by the next optimizer step)" if ckpt.engine._copier is not None
+              and ckpt.engine._copier.overlap else "in the pause"})
 
         # ---------------- DISK persist (agent: torch.save archive written from
         # shm with parallel pwrite) while training continues: persist time and
