@@ -502,41 +502,10 @@ def test_gpu_deferred_optimizer_restore_orders_the_first_step(tmp_path, monkeypa
 
     monkeypatch.setattr(cp.GpuCopier, "_pipelined_h2d", slow)
     model, opt, flat = _model_and_opt()
-    trail = [("built", opt.step_count)]
     ck = DdpCheckpointer(str(tmp_path / "ck"))
     state = lambda: {"model": model.state_dict(), "optimizer": opt.state_dict()}  # noqa
     assert ck.save_checkpoint(5, state(), storage_type=StorageType.MEMORY)
     ck.wait_latest_checkpoint()
-    trail.append(("saved", opt.step_count))
-
-    def shm_probe(tag):
-        # where the optimizer's step scalar sits in each slot of the segment
-        import numpy as np
-
-        from dlrover_wuqiong_amd.flash_checkpoint.layout import TensorMeta, iter_leaves
-
-        h = ck.engine._shm_handler
-        out = [tag, h.complete_steps(), h.num_slots, h.payload_size]
-        lay = ck.engine._layout_cache.cached() if hasattr(ck.engine, "_layout_cache") else None
-        if lay is not None:
-            sp = opt._step_t.data_ptr()
-            out.append(("cpu_extents", len(lay.cpu_extents()), [(e.src_ptr == sp, e.offset, e.nbytes)
-                                                               for e in lay.cpu_extents()][:4]))
-        for slot in range(h.num_slots):
-            meta = h.get_meta(slot) or {}
-            tree = meta.get("tree")
-            if isinstance(tree, dict) and "model_states" in tree:
-                tree = tree["model_states"]
-            if not isinstance(tree, dict) or "optimizer" not in tree:
-                out.append((slot, "no optimizer tree", sorted(tree) if isinstance(tree, dict) else type(tree)))
-                continue
-            m = next(iter(tree["optimizer"]["state"].values()))["step"]
-            assert isinstance(m, TensorMeta)
-            raw = np.frombuffer(h.shared_memory.buf, dtype=np.float32, count=1, offset=m.offset + h.payload_offset(slot))
-            out.append((slot, m.offset, str(m.dtype), m.device, float(raw[0])))
-        trail.append(tuple(out))
-
-    shm_probe("after_save")
     x = torch.randint(0, model.cfg.vocab_size if hasattr(model, "cfg") else 50257, (2, 65), device="cuda",
                       generator=torch.Generator("cuda").manual_seed(7))
 
@@ -547,14 +516,10 @@ def test_gpu_deferred_optimizer_restore_orders_the_first_step(tmp_path, monkeypa
 
     ck.load_checkpoint(target=state())
     torch.cuda.synchronize()
-    shm_probe("after_load")
-    trail.append(("loaded", opt.step_count, ck.engine.last_restore_source, id(opt._step_t),
-                  [id(v["step"]) for v in list(opt.state_dict()["state"].values())[:2]]))
+    assert opt.step_count == 1  # the host-side step counter came back too (not staging bytes)
     step()
     torch.cuda.synchronize()
-    trail.append(("stepped", opt.step_count))
     want = flat.data.clone(), opt.exp_avg.clone(), opt.master.clone()
-    want_step = opt.step_count
     # corrupt, restore (no sync), step at once
     flat.data.zero_()
     opt.exp_avg.fill_(3.0)
@@ -568,9 +533,7 @@ def test_gpu_deferred_optimizer_restore_orders_the_first_step(tmp_path, monkeypa
     # that read the corrupted state would be off by O(1))
     diag = [(n, int(torch.isnan(g.float()).sum()), int(torch.isnan(r.float()).sum()))
             for n, g, r in zip(("param", "exp_avg", "master"), (flat.data, opt.exp_avg, opt.master), want)]
-    diag.append(("step_count", opt.step_count, "dsw", opt._dsw is not None, "fenced",
-                 len(cp._FENCED) if cp._FENCED is not None else None, "want_step", want_step,
-                 "v_nan", int(torch.isnan(opt.exp_avg_sq).sum()), "v_min", float(opt.exp_avg_sq.min()), trail))
+    diag.append(("step_count", opt.step_count))
     for got, ref in zip((flat.data.float(), opt.exp_avg, opt.master), want):
         torch.testing.assert_close(got, ref.float(), rtol=1e-2, atol=1e-3, msg=lambda m: f"{m}\nNaNs (got, want): {diag}")
     if defer:
@@ -608,7 +571,6 @@ def test_gpu_deferred_restore_then_optimizer_load_state_dict(tmp_path, monkeypat
     ck.wait_latest_checkpoint()
     torch.cuda.synchronize()
     want = flat.data.clone(), opt.exp_avg.clone(), opt.master.clone()
-    want_step = opt.step_count
     flat.data.zero_()
     opt.exp_avg.fill_(3.0)
     opt.master.fill_(-1.0)
