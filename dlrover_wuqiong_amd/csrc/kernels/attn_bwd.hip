@@ -45,6 +45,9 @@
 // (profiles/r4/attn_dkdv64_w3_ab.jsonl).  -DDWAMD_DKDV64_W3=0: the 2-wave form
 #define DWAMD_DKDV64_W3 1
 #endif
+#ifndef DWAMD_DKDV64_BQT
+#define DWAMD_DKDV64_BQT 64  // A/B: queries per staged tile of the D = 64 dK/dV kernel (32 / 64 / 128)
+#endif
 #ifndef DWAMD_DQ_SPLIT
 #define DWAMD_DQ_SPLIT 1  // A/B: 0 keeps the D=64 mask a runtime branch inside one tile body
 #endif
@@ -118,7 +121,7 @@ struct DkvCfg {
   // ~65 KiB LDS each) share a CU
   static constexpr int WAVES = 4;
   static constexpr int BKB = 32 * WAVES;   // keys per workgroup
-  static constexpr int BQT = D == 64 ? 64 : 32;  // queries per tile
+  static constexpr int BQT = D == 64 ? DWAMD_DKDV64_BQT : 32;  // queries per tile
   static constexpr int NCH = D / 8;
   static constexpr int KK = D / 16;
   static constexpr int DT = D / 32;
