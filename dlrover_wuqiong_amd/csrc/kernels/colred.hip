@@ -400,20 +400,37 @@ __global__ void __launch_bounds__(256) norm_bwd_fused_kernel(
 // are summed by colsum_f32_kernel.
 // DS: also the column sums of dx itself (the bias gradient of the Linear
 // whose output is this add-norm's residual input): partial rows [3H].
+#ifndef DWAMD_NORM_BWD_LDSACC
+// A/B: the block's dgamma / dbeta (/ dx column) sums in LDS (ds_add_f32, the
+// lane-contiguous layout [k][vector]) instead of 2-3 x 32 per-lane registers:
+// the VPL = 4 instance (H 1025..2047, GPT2-1.5B's 1600) then fits more than
+// one wave per SIMD (256 VGPRs + 82-114 AGPRs otherwise).  Sums in LDS are
+// added in arrival order; DWAMD_DETERMINISTIC takes the two-pass path anyway
+#define DWAMD_NORM_BWD_LDSACC 0
+#endif
+
 template <int VPL, bool RMS, bool DS = false>
-__global__ void __launch_bounds__(256) norm_bwd_part_kernel(
+__global__ void __launch_bounds__(256, (DWAMD_NORM_BWD_LDSACC && VPL == 4) ? 2 : 1) norm_bwd_part_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ gamma,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const bf16_t* __restrict__ dres,
     bf16_t* __restrict__ dx, float* __restrict__ part, int64_t rows, int H) {
   static_assert(VPL <= 4, "small-H norm backward");
-  __shared__ float red[2][4][512 + 4];
+  constexpr bool LA = DWAMD_NORM_BWD_LDSACC != 0;
+  constexpr int NVP = 64 * VPL;  // vectors per row, padded
+  __shared__ float red[LA ? 1 : 2][LA ? 1 : 4][LA ? 1 : 512 + 4];
+  __shared__ float lacc[LA ? (DS ? 3 : 2) : 1][LA ? 8 * NVP : 1];  // [array][k * NVP + vector]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nv = H >> 3;
-  float ag[VPL][8], ab[VPL][8], ad[VPL][8];
+  float ag[LA ? 1 : VPL][8], ab[LA ? 1 : VPL][8], ad[LA ? 1 : VPL][8];
+  if constexpr (LA) {
+    for (int i = threadIdx.x; i < (DS ? 3 : 2) * 8 * NVP; i += 256) (&lacc[0][0])[i] = 0.f;
+    __syncthreads();
+  } else {
 #pragma unroll
-  for (int j = 0; j < VPL; ++j)
+    for (int j = 0; j < VPL; ++j)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) ag[j][k] = ab[j][k] = ad[j][k] = 0.f;
+      for (int k = 0; k < 8; ++k) ag[j][k] = ab[j][k] = ad[j][k] = 0.f;
+  }
   u32x4 gv[VPL];
 #pragma unroll
   for (int j = 0; j < VPL; ++j) {
@@ -455,8 +472,13 @@ __global__ void __launch_bounds__(256) norm_bwd_part_kernel(
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float a = (xf[k] - b.mu) * b.rs, g = df[k] * gm[k];
-          ag[j][k] += df[k] * a;
-          if constexpr (!RMS) ab[j][k] += df[k];
+          if constexpr (LA) {
+            atomicAdd(&lacc[0][k * NVP + c], df[k] * a);
+            if constexpr (!RMS) atomicAdd(&lacc[1][k * NVP + c], df[k]);
+          } else {
+            ag[j][k] += df[k] * a;
+            if constexpr (!RMS) ab[j][k] += df[k];
+          }
           s1 += g;
           s2 += g * a;
         }
@@ -482,25 +504,49 @@ __global__ void __launch_bounds__(256) norm_bwd_part_kernel(
         }
         if constexpr (DS) {
 #pragma unroll
-          for (int k = 0; k < 8; ++k) ad[j][k] += o[k];
+          for (int k = 0; k < 8; ++k) {
+            if constexpr (LA)
+              atomicAdd(&lacc[DS ? 2 : 0][k * NVP + c], o[k]);
+            else
+              ad[j][k] += o[k];
+          }
         }
         *(u32x4*)(dx + row * H + c * 8) = pack8(o);
       }
     }
   };
-  Row A, B;
   int64_t row = (int64_t)blockIdx.x * 4 + wid;
-  load(A, row);
-  while (row < rows) {
-    load(B, row + stride);
-    process(A, row);
-    row += stride;
-    if (row >= rows) break;
-    load(A, row + stride);
-    process(B, row);
-    row += stride;
+  if constexpr (LA) {
+    // more waves per SIMD instead of a second register set: one row in flight per wave
+    Row A;
+    for (; row < rows; row += stride) {
+      load(A, row);
+      process(A, row);
+    }
+  } else {
+    Row A, B;
+    load(A, row);
+    while (row < rows) {
+      load(B, row + stride);
+      process(A, row);
+      row += stride;
+      if (row >= rows) break;
+      load(A, row + stride);
+      process(B, row);
+      row += stride;
+    }
   }
   float* prow = part + (int64_t)blockIdx.x * (DS ? 3 : 2) * H;
+  if constexpr (LA) {
+    __syncthreads();
+    for (int col = threadIdx.x; col < H; col += 256) {
+      const int cv = col >> 3, k = col & 7;
+      prow[col] = lacc[0][k * NVP + cv];
+      prow[H + col] = RMS ? 0.f : lacc[1][k * NVP + cv];
+      if constexpr (DS) prow[2 * H + col] = lacc[DS ? 2 : 0][k * NVP + cv];
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < VPL; ++j) {
 #pragma unroll
@@ -653,7 +699,7 @@ extern "C" int64_t dw_colred_det_floats(int64_t rows, int C, int kind) {
   if (kind == 1) return grid_y(2048) * C;
   // norm: the two-pass path (colred_kernel<1>, 2 sums per column) or the
   // small-H partial-rows path (colsum_f32_kernel over <= 3H columns)
-  const int64_t nb = std::min<int64_t>((rows + 3) / 4, C > 1024 ? 256 : 512);
+  const int64_t nb = std::min<int64_t>((rows + 3) / 4, (C > 1024 && !DWAMD_NORM_BWD_LDSACC) ? 256 : 512);
   return std::max<int64_t>(grid_y(norm_colred_blocks()) * 2 * C, colsum_f32_splits(nb) * 3 * C);
 }
 
@@ -745,7 +791,7 @@ extern "C" int dw_norm_bwd3(const void* dy, const void* x, const void* gamma, co
   accumulate &= 1;
   // every workgroup resident at once, each wave striding over rows: H > 1024
   // (VPL 4) needs ~310-370 VGPRs, one workgroup per CU; smaller H two
-  const int64_t nb = std::min<int64_t>((rows + 3) / 4, H > 1024 ? 256 : 512);
+  const int64_t nb = std::min<int64_t>((rows + 3) / 4, (H > 1024 && !DWAMD_NORM_BWD_LDSACC) ? 256 : 512);
   const int pw = dsum ? 3 : 2;
   if (dsum_done) *dsum_done = 0;
   static const bool off = getenv_flag("DWAMD_NORM_BWD_PART_OFF");  // A/B switch
