@@ -405,7 +405,9 @@ __global__ void __launch_bounds__(256) norm_bwd_fused_kernel(
 // lane-contiguous layout [k][vector]) instead of 2-3 x 32 per-lane registers:
 // the VPL = 4 instance (H 1025..2047, GPT2-1.5B's 1600) then fits more than
 // one wave per SIMD (256 VGPRs + 82-114 AGPRs otherwise).  Sums in LDS are
-// added in arrival order; DWAMD_DETERMINISTIC takes the two-pass path anyway
+// added in arrival order; DWAMD_DETERMINISTIC takes the two-pass path anyway.
+// Measured: GPT2-1.5B step 108.4 -> 124.7 ms (the LDS float atomics cost more
+// than the occupancy gains; profiles/r5/norm_bwd_ldsacc_ab.jsonl) -- off
 #define DWAMD_NORM_BWD_LDSACC 0
 #endif
 
