@@ -1126,7 +1126,10 @@ class GpuCopier:
             # writes it back now; then nothing pending may outlive the copier
             # (a closed copier left in the fence set would be offered to
             # later optimizers)
-            _flush_deferred_state()
+            try:
+                _flush_deferred_state()
+            except Exception as e:  # e.g. at interpreter exit, the runtime already torn down
+                logger.warning(f"deferred optimizer-state write-back at close failed: {e}")
             self.wait()
             self.fence()
         finally:
