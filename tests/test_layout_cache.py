@@ -46,3 +46,29 @@ def test_hit_rebuilds_same_tree_and_misses_on_change():
     a, _ = cache.plan(sd4)
     b, _ = cache.plan(sd4)
     assert a.extents is not b.extents
+
+
+def test_device_storages_first_and_gpu_end(monkeypatch):
+    """plan_layout puts every device storage before every host one (the
+    staging flush writes [0, gpu_end) only); the order inside each group is
+    first appearance.  Device tensors are faked by their storage key."""
+    import torch
+
+    from dlrover_wuqiong_amd.flash_checkpoint import layout as L
+
+    a, s, b = torch.zeros(1000), torch.tensor(3.0), torch.zeros(500)
+    fake_dev = {a.untyped_storage().data_ptr(), b.untyped_storage().data_ptr()}
+    orig = L._storage_key
+
+    def key(t):
+        k = orig(t)
+        return ("cuda", 0, k[2]) if k[2] in fake_dev else k
+
+    monkeypatch.setattr(L, "_storage_key", key)
+    lay, _ = L.plan_layout({"a": a, "step": s, "b": b})
+    devs = [e.device for e in lay.extents]
+    assert devs == ["cuda", "cuda", "cpu"], devs  # the host scalar after both device tensors
+    assert lay.gpu_end == max(e.offset + e.nbytes for e in lay.extents if e.device == "cuda")
+    assert all(e.offset >= lay.gpu_end for e in lay.cpu_extents())
+    metas = lay.meta_tree
+    assert metas["a"].offset < metas["b"].offset < metas["step"].offset

@@ -45,3 +45,30 @@ def test_overlap_needs_gpu():
     opt = FusedAdamW(FlatParams(m), lr=1e-3)
     with pytest.raises(ValueError):
         opt.overlap_with_forward(m)
+
+
+def test_ring_fence_taken_over_only_for_own_tensors():
+    """An optimizer defers its state write-back only behind a ring snapshot
+    that reads ITS tensors (a stale or foreign copier is fenced normally)."""
+    import torch
+
+    from dlrover_wuqiong_amd.optimizers.fused import FusedAdamW
+    from dlrover_wuqiong_amd.parallel.flat import FlatParams
+
+    model = torch.nn.Linear(64, 64)
+    opt = FusedAdamW(FlatParams(model), lr=1e-3)
+
+    class Ring:
+        def __init__(self, ranges):
+            self.ranges = ranges
+
+        def ring_sources(self):
+            return self.ranges
+
+    m = opt.exp_avg
+    assert opt._ring_touches(Ring([(m.data_ptr(), m.data_ptr() + 16)]))
+    p = opt.flat.data
+    assert opt._ring_touches(Ring([(p.data_ptr() + 8, p.data_ptr() + 12)]))
+    other = torch.zeros(1 << 16)
+    assert not opt._ring_touches(Ring([(other.data_ptr(), other.data_ptr() + other.numel() * 4)]))
+    assert not opt._ring_touches(Ring([]))
