@@ -410,6 +410,11 @@ __global__ void __launch_bounds__(256) norm_bwd_fused_kernel(
 // than the occupancy gains; profiles/r5/norm_bwd_ldsacc_ab.jsonl) -- off
 #define DWAMD_NORM_BWD_LDSACC 0
 #endif
+#ifndef DWAMD_NORM_BWD_PF
+// A/B: rows prefetched per wave (register sets); 2 = load the next row before
+// computing the current one
+#define DWAMD_NORM_BWD_PF 2
+#endif
 
 template <int VPL, bool RMS, bool DS = false>
 __global__ void __launch_bounds__(256, (DWAMD_NORM_BWD_LDSACC && VPL == 4) ? 2 : 1) norm_bwd_part_kernel(
@@ -524,6 +529,23 @@ __global__ void __launch_bounds__(256, (DWAMD_NORM_BWD_LDSACC && VPL == 4) ? 2 :
     for (; row < rows; row += stride) {
       load(A, row);
       process(A, row);
+    }
+  } else if constexpr (DWAMD_NORM_BWD_PF > 2) {
+    // PF register sets: PF - 1 rows in flight while one is computed (a wave
+    // owns ~rows / 1024 rows, 8 at GPT2's B*S = 8192, so the ramp matters)
+    constexpr int PF = DWAMD_NORM_BWD_PF;
+    Row R[PF];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) load(R[p], row + p * stride);
+    for (; row < rows; row += PF * stride) {
+#pragma unroll
+      for (int p = 0; p < PF; ++p) {
+        const int64_t rr = row + p * stride;
+        if (rr < rows) {
+          process(R[p], rr);
+          load(R[p], rr + PF * stride);
+        }
+      }
     }
   } else {
     Row A, B;
