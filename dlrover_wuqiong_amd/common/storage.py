@@ -25,6 +25,13 @@ from .serialize import ClassMeta
 _BIG_WRITE = 4 << 20  # records at least this large go through the native parallel pwrite
 
 
+def _direct_bit() -> int:
+    """``dw_write_file`` mode bit 2: O_DIRECT for the aligned body of large
+    records (``DWAMD_PERSIST_ODIRECT=0``: buffered + fsync, page-cache
+    write-back)."""
+    return 4 if os.environ.get("DWAMD_PERSIST_ODIRECT", "1") == "1" else 0
+
+
 class _ParallelFileWriter:
     """Sequential-write file object for ``torch.save``.
 
@@ -49,7 +56,8 @@ class _ParallelFileWriter:
             import numpy as np
 
             addr = np.frombuffer(mv, dtype=np.uint8).ctypes.data
-            r = runtime().dw_write_file(self.path.encode(), ctypes.c_void_p(addr), n, self.off, self.threads, 0)
+            r = runtime().dw_write_file(self.path.encode(), ctypes.c_void_p(addr), n, self.off, self.threads,
+                                        _direct_bit())
             if r != 0:
                 raise OSError(f"write {self.path}: {last_error()}")
             self.big_bytes += n
@@ -229,7 +237,7 @@ class PosixDiskStorage(CheckpointStorage):
     def write_bytes(self, addr, nbytes, path, offset=0, truncate=True, fsync=True, threads=8):
         path = str(path)
         os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
-        mode = (1 if truncate else 0) | (2 if fsync else 0)
+        mode = (1 if truncate else 0) | (2 if fsync else 0) | _direct_bit()
         r = runtime().dw_write_file(path.encode(), ctypes.c_void_p(addr), int(nbytes), int(offset),
                                     int(threads), mode)
         if r != 0:
