@@ -35,7 +35,7 @@ def main():
     p.add_argument("--act-ckpt", choices=["on", "off"], default="off",
                    help="activation checkpointing of the decoder layers (off: a 288 GB MI355X holds every "
                         "activation of Llama-3-8B at S=4096, so the forward is not recomputed)")
-    p.add_argument("--reshard", choices=["on", "off"], default="on",
+    p.add_argument("--reshard", choices=["on", "off"], default="off",
                    help="off: FSDP2 reshard_after_forward=False (auto_accelerate 'zero2'): the gathered bf16 "
                         "parameters stay resident from forward to backward (16 GB for 8B on a 288 GB card), "
                         "no second all-gather per layer")
