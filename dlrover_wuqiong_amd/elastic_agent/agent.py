@@ -709,14 +709,14 @@ class ElasticTrainingAgent:
         the 100 ms monitor sleep otherwise adds ~50 ms to every recovery.
         Reads only, never reaps (the main loop's ``poll`` does)."""
         interval = float(os.getenv("DWAMD_EXIT_POLL_S", "0.005"))
-        signaled = set()
+        signaled = set()  # Popen objects (by identity: pids get reused across restarts)
         while not self._stop_hb.wait(interval):
             for w in list(self.workers):
-                pid = w.proc.pid
-                if pid in signaled:
+                p = w.proc
+                if p in signaled:
                     continue
-                if w.proc.returncode not in (None, 0) or _exiting_code(pid) is not None:
-                    signaled.add(pid)
+                if p.returncode not in (None, 0) or _exiting_code(p.pid) is not None:
+                    signaled.add(p)
                     self._exit_evt.set()
 
     def _monitor_workers(self) -> RunResult:
