@@ -648,11 +648,9 @@ class GpuCopier:
                 "t_enq": time.perf_counter()}
 
     def flush_snapshot(self, snap: dict, shm_payload_addr: int, on_done: Callable[[], None], sync: bool = False,
-                       on_snapshot: Optional[Callable[[], None]] = None,
-                       before_flush: Optional[Callable[[], None]] = None):
+                       on_snapshot: Optional[Callable[[], None]] = None):
         """Copy the CPU extents into the shm slot now and queue the PCIe flush
-        of the staged bytes behind the snapshot's event.  ``before_flush``
-        runs first on the flush thread (the slot's metadata, off the pause)."""
+        of the staged bytes behind the snapshot's event."""
         layout, lo, hi, idx, stg, ev = (snap[k] for k in ("layout", "lo", "hi", "idx", "stg", "ev"))
         n = hi - lo
         # the PCIe flush writes the device region only: host tensors (below)
@@ -672,8 +670,6 @@ class GpuCopier:
         # for the whole PCIe transfer and stall the training thread's launches.
         def flush():
             t_start = time.perf_counter()
-            if before_flush is not None:
-                before_flush()
             if n > 0:
                 if on_snapshot is not None:
                     _check(_kern().dw_event_sync(ctypes.c_void_p(ev.cuda_event)), "snapshot sync")

@@ -20,7 +20,6 @@ Replicated vs sharded state:
    rank, each rank moves its own shard.
 """
 
-import copy
 import gc
 import hashlib
 import os
@@ -51,10 +50,6 @@ _PREP_PIECE = max(64, int(os.environ.get("DWAMD_PREP_PIECE_MB", "1024"))) << 20 
 
 # DWAMD_CKPT_SPECULATE=0: walk + verify the state dict before enqueueing the copy
 _SPECULATE = os.environ.get("DWAMD_CKPT_SPECULATE", "1") == "1"
-# DWAMD_CKPT_DEFER_META=0: pickle the slot's metadata inside the save pause;
-# default: the flush thread writes it first thing (~1 ms of pause for a few
-# hundred tensors), before the HBM-tier stamp and the completion words
-_DEFER_META = os.environ.get("DWAMD_CKPT_DEFER_META", "1") == "1"
 
 class CheckpointEventType:
     SAVE = 1
@@ -620,16 +615,8 @@ class CheckpointEngine(ABC):
         conf.num_slices = self._num_slices
         conf.generation = self._generation
         h.set_slice_step(slot, self._slice_idx, 0)  # slot reads incomplete before any byte changes
-        write_meta = None
         if self._is_shard_owner:
-            if snap is not None and _DEFER_META:
-                # the slot stays incomplete (slice step 0) until on_done, which
-                # the flush thread runs after this; a private copy of the config
-                meta_conf = copy.copy(conf)
-                meta_tree = layout.meta_tree
-                write_meta = lambda: h.set_metadata(slot, meta_tree, meta_conf)  # noqa: E731
-            else:
-                h.set_metadata(slot, layout.meta_tree, conf)
+            h.set_metadata(slot, layout.meta_tree, conf)
 
         def on_snapshot():
             if "idx" in stage:
@@ -647,8 +634,7 @@ class CheckpointEngine(ABC):
                 self._release_when_complete(step, slot)
 
         if snap is not None:
-            copier.flush_snapshot(snap, h.payload_addr(slot), on_done, on_snapshot=on_snapshot,
-                                  before_flush=write_meta)
+            copier.flush_snapshot(snap, h.payload_addr(slot), on_done, on_snapshot=on_snapshot)
         elif has_gpu and copier is not None:
             copier.save_slice(layout, h.payload_addr(slot), lo, hi, on_done, before_copy=before_copy,
                               on_snapshot=on_snapshot)
