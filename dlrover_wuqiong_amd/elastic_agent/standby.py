@@ -259,19 +259,6 @@ def _gpu_init(lr: str) -> bool:
         return False
 
 
-def _staging_known() -> bool:
-    """True when the reservation needs no staging term (HBM tier: a standby
-    owns the buffers) or the slice size it is computed from is known."""
-    if os.environ.get("DWAMD_HBM_TIER", "1") == "1":
-        return True
-    try:
-        from ..flash_checkpoint.prewarm import local_slice_bytes
-
-        return local_slice_bytes() > 0
-    except Exception:
-        return True
-
-
 def _reserve_state_memory(reserved: int = 0, prof: Optional[dict] = None) -> int:
     """Fill PyTorch's caching allocator with about the HBM the worker will
     take -- its recorded peak footprint (warm profile: model + optimizer +
@@ -287,14 +274,10 @@ def _reserve_state_memory(reserved: int = 0, prof: Optional[dict] = None) -> int
     try:
         import torch
 
-        from ..flash_checkpoint.prewarm import local_slice_bytes, local_state_bytes
+        from ..flash_checkpoint.prewarm import local_state_bytes
         from .warm_profile import reserve_bytes
 
-        # no HBM tier: the worker this process becomes allocates its own
-        # (double) staging at its first save -- reserve that too
-        staging = 0 if os.environ.get("DWAMD_HBM_TIER", "1") == "1" else 2 * local_slice_bytes()
-        want = reserve_bytes(prof, local_state_bytes(), float(os.environ.get("DWAMD_STANDBY_RESERVE_FACTOR", "1.25")),
-                             staging)
+        want = reserve_bytes(prof, local_state_bytes(), float(os.environ.get("DWAMD_STANDBY_RESERVE_FACTOR", "1.25")))
         if want <= reserved:
             return reserved
         free, _total = torch.cuda.mem_get_info()
@@ -362,7 +345,6 @@ def _wait_command(pin: bool, ctl: str, lr: str, interval: float = 0.25) -> Optio
     pinned_marked = False
     reserved = 0
     prof = None
-    topped = False  # the reservation includes the staging buffers (or needs none)
     cmd = None
     while cmd is None:
         if pin:
@@ -376,13 +358,7 @@ def _wait_command(pin: bool, ctl: str, lr: str, interval: float = 0.25) -> Optio
                 if prof is not None:
                     if reserved >= 0:
                         reserved = _reserve_state_memory(reserved, prof)
-                        topped = _staging_known()
                     _mark(ctl, WARM_PREFIX, lr, f"{reserved}\n")
-            elif not topped and reserved > 0 and _staging_known():
-                # the checkpoint's slice size became known after the profile:
-                # add the worker's staging buffers to the reservation (once)
-                reserved = _reserve_state_memory(reserved, prof)
-                topped = True
             if reserved == 0:
                 reserved = _reserve_state_memory()
             else:

@@ -289,17 +289,12 @@ def load(ctl: str, local_rank) -> Optional[dict]:
         return None
 
 
-def reserve_bytes(prof: Optional[dict], state_bytes: int, factor: float = 1.25, staging_bytes: int = 0) -> int:
+def reserve_bytes(prof: Optional[dict], state_bytes: int, factor: float = 1.25) -> int:
     """Bytes the standby should hold in its caching allocator: the worker's
-    recorded peak footprint, else ~its checkpoint payload (model + optimizer),
-    plus ``staging_bytes``: the flash-checkpoint staging buffers the worker
-    allocates at its first save when no standby owns them (no HBM tier).
-    Without them in the reservation that first save's 2 x slice-size
-    hipMalloc lands right after the restart, next to the killed process's
-    VRAM teardown (measured: 0.6 + 3.2 s stalls in one run)."""
+    recorded peak footprint, else ~its checkpoint payload (model + optimizer)."""
     if prof and prof.get("max_reserved"):
-        return int(prof["max_reserved"]) + int(staging_bytes)
-    return int(state_bytes * factor) + int(staging_bytes)
+        return int(prof["max_reserved"])
+    return int(state_bytes * factor)
 
 
 def summary(prof: Optional[dict]) -> List:

@@ -43,22 +43,3 @@ def test_integer_operands_replay_as_zeros():
     e = wp._enc(torch.tensor([[3, 7]]), "cpu")
     t = wp._dec(e, torch.device("cpu"))
     assert t.dtype == torch.int64 and t.shape == (1, 2) and int(t.abs().sum()) == 0
-
-
-def test_reserve_bytes_adds_worker_staging_without_hbm_tier(monkeypatch):
-    from dlrover_wuqiong_amd.elastic_agent import standby
-    from dlrover_wuqiong_amd.elastic_agent.warm_profile import reserve_bytes
-
-    prof = {"max_reserved": 45 << 30}
-    assert reserve_bytes(prof, 20 << 30) == 45 << 30
-    assert reserve_bytes(prof, 20 << 30, staging_bytes=40 << 30) == 85 << 30
-    assert reserve_bytes(None, 20 << 30, 1.25, 40 << 30) == 25 * (1 << 30) + (40 << 30)
-    monkeypatch.setenv("DWAMD_HBM_TIER", "1")
-    assert standby._staging_known()  # the standby owns the staging: nothing to add
-    monkeypatch.setenv("DWAMD_HBM_TIER", "0")
-    from dlrover_wuqiong_amd.flash_checkpoint import prewarm
-
-    monkeypatch.setattr(prewarm, "local_slice_bytes", lambda: 0)
-    assert not standby._staging_known()
-    monkeypatch.setattr(prewarm, "local_slice_bytes", lambda: 20 << 30)
-    assert standby._staging_known()
