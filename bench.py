@@ -418,7 +418,9 @@ def summarize(a, run_dir, n, wall):
         "launcher_wall_s": round(wall, 1),
     }
     persist = next((e for e in ev if e["event"] == "persisted"), None)
-    if persist is not None:
+    if persist is not None and persist.get("persist_sec") is None:
+        res["persist_sec"] = None  # not durable within DWAMD_BENCH_PERSIST_TIMEOUT_S
+    elif persist is not None:
         res["persist_sec"] = round(persist["persist_sec"], 3)
         res["persist_gbps"] = round(phase0["ckpt_bytes"] / persist["persist_sec"] / 1e9, 2)
         res["persist_step_ms_during"] = persist.get("step_ms_during")
@@ -922,6 +924,9 @@ def worker(a) -> int:
             persist_t0 = time.time()
             ckpt.save_checkpoint(step, state(), storage_type=StorageType.DISK)
             during, persist_done = [], None
+            # a persist that never lands (disk full, storage error) must not
+            # hang the run: give up after DWAMD_BENCH_PERSIST_TIMEOUT_S
+            persist_deadline = time.time() + float(os.environ.get("DWAMD_BENCH_PERSIST_TIMEOUT_S", "300"))
             while persist_done is None:
                 if len(during) < 400:
                     ts = time.perf_counter()
@@ -930,53 +935,59 @@ def worker(a) -> int:
                     during.append(time.perf_counter() - ts)
                 else:
                     time.sleep(0.01)
-                done_here = 0
+                done_here = 0  # rank 0 decides for all: 1 durable, 2 past the deadline
                 if rank == 0:
                     try:
                         with open(tracker) as f:
                             done_here = 1 if f.read().strip() == str(persist_step) else 0
                     except OSError:
                         pass
+                    if not done_here and time.time() > persist_deadline:
+                        done_here = 2
                 if world > 1:
                     t = torch.tensor([done_here], device=cdev)
                     dist.broadcast(t, 0)
                     done_here = int(t.item())
-                if done_here:
+                if done_here == 1:
                     persist_done = time.time() - persist_t0
+                elif done_here == 2:
+                    log(f"[rank {rank}] persist of step {persist_step} not durable after the deadline")
+                    break
             med = mx(statistics.median(during)) if during else None
             emit({"event": "persisted", "persist_sec": persist_done, "steps_during": len(during),
                   "step_ms_during": round(1000 * med, 2) if med else None,
                   "interference_pct": round(100 * (med / step_sec - 1), 2) if med else None})
 
-            # ---------------- storage restore (node replaced: shm gone): the
-            # persisted archive straight into the live tensors, page cache
-            # dropped first and O_DIRECT reads -- the device's read rate
-            from dlrover_wuqiong_amd.flash_checkpoint.storage_loader import drop_file_cache
+            if persist_done is not None:  # (no durable archive: no storage restore to time)
+                # ---------------- storage restore (node replaced: shm gone): the
+                # persisted archive straight into the live tensors, page cache
+                # dropped first and O_DIRECT reads -- the device's read rate
+                from dlrover_wuqiong_amd.flash_checkpoint.storage_loader import drop_file_cache
 
-            path = os.path.join(a.ckpt_dir, str(persist_step), "rank_0.pt")  # DDP: one node copy
-            sync_all()
-            flat.data.zero_()
-            opt.exp_avg.zero_()
-            third.zero_()
-            try:
-                drop_file_cache(path)
-            except OSError:
-                pass
-            sync_all()
-            t0 = time.perf_counter()
-            ckpt.engine._load_from_storage(path, target={CheckpointConstant.MODEL_STATES_NAME: state()})
-            if cuda:
-                torch.cuda.synchronize()
-            sec = mx(time.perf_counter() - t0)
-            from_storage = state_sums()
-            storage_src = getattr(ckpt.engine, "last_restore_source", None)
-            # the same step from memory (the DISK save snapshotted it to shm
-            # first): the two restores must agree bit for bit.  This also puts
-            # the live state back to that checkpoint for the fault window.
-            ckpt.load_checkpoint(target=state())
-            sync_all()
-            emit({"event": "storage_load", "sec": sec, "ok": from_storage == state_sums(),
-                  "source": storage_src, "stats": getattr(ckpt.engine, "last_storage_load_stats", None)})
+                path = os.path.join(a.ckpt_dir, str(persist_step), "rank_0.pt")  # DDP: one node copy
+                sync_all()
+                flat.data.zero_()
+                opt.exp_avg.zero_()
+                third.zero_()
+                try:
+                    drop_file_cache(path)
+                except OSError:
+                    pass
+                sync_all()
+                t0 = time.perf_counter()
+                ckpt.engine._load_from_storage(path, target={CheckpointConstant.MODEL_STATES_NAME: state()})
+                if cuda:
+                    torch.cuda.synchronize()
+                sec = mx(time.perf_counter() - t0)
+                from_storage = state_sums()
+                storage_src = getattr(ckpt.engine, "last_restore_source", None)
+                # the same step from memory (the DISK save snapshotted it to shm
+                # first): the two restores must agree bit for bit.  This also puts
+                # the live state back to that checkpoint for the fault window.
+                ckpt.load_checkpoint(target=state())
+                sync_all()
+                emit({"event": "storage_load", "sec": sec, "ok": from_storage == state_sums(),
+                      "source": storage_src, "stats": getattr(ckpt.engine, "last_storage_load_stats", None)})
         sync_all()
         s0 = step
         emit({"event": "fault_start", "t": time.time(), "s0": s0})

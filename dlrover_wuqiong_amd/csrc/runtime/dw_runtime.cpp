@@ -237,12 +237,9 @@ int dw_write_file(const char* path, const void* buf, uint64_t n, uint64_t file_o
         buf = (const char*)buf + body;
         file_off += body;
         n -= body;
-      } else if (e != EINVAL) {
-        errno = e;
-        set_err("pwrite(O_DIRECT)");
-        close(fd);
-        return -1;
-      }  // EINVAL: O_DIRECT refused mid-way -- everything again, buffered
+      }  // any failure of the direct path (EINVAL: refused mid-way, or a file
+         // system that accepts the flag but fails the writes): everything
+         // again through the buffered path, whose errors are the ones reported
     }
   }
   std::atomic<int> failed{0};  // errno of the first failing worker (errno is per thread)
