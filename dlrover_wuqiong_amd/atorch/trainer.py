@@ -138,8 +138,12 @@ def _count_params(model: nn.Module) -> Tuple[int, int]:
 
 class AtorchTrainer:
     def __init__(self, model: nn.Module, args: AtorchTrainingArgs, data_collator=None, train_dataset=None,
-                 eval_dataset=None, tokenizer=None, compute_metrics=None, callbacks=None, optimizers=(None, None)):
+                 eval_dataset=None, tokenizer=None, compute_metrics=None, callbacks=None, optimizers=(None, None),
+                 preprocess_logits_for_metrics=None):
         self.args = args
+        # (logits, labels) -> what compute_metrics needs, applied per eval
+        # batch on the device (reference atorch_trainer.py:149)
+        self.preprocess_logits_for_metrics = preprocess_logits_for_metrics
         self.data_collator = data_collator
         self.train_dataset = train_dataset
         self.eval_dataset = eval_dataset
@@ -483,70 +487,129 @@ class AtorchTrainer:
     def _comm_device(self):
         return self.device if dist.is_initialized() and dist.get_backend() == "nccl" else torch.device("cpu")
 
+    _DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.float64, torch.int64, torch.int32, torch.int16,
+               torch.int8, torch.uint8, torch.bool)
+    _MAX_DIMS = 8
+
     def _gather(self, t: Optional[torch.Tensor], counts: List[int], pad_index=-100) -> Optional[torch.Tensor]:
         """Rank-ordered concatenation over the data-parallel ranks of each
-        rank's first ``counts[rank]`` rows (the ranks' tensors are padded to
-        a common shape -- trailing dims with ``pad_index`` -- for the
-        all-gather, then trimmed)."""
+        rank's first ``counts[rank]`` rows.  COLLECTIVE: every rank calls it,
+        a rank without rows with ``t=None`` -- the dtype and trailing shape
+        are agreed first (max over ranks), the tensors padded with
+        ``pad_index`` to a common shape for the all-gather, then trimmed.
+        Returns None on every rank when no rank has a tensor."""
         world = self._world()
-        if world == 1 or t is None:
+        if world == 1:
             return t
         dev = self._comm_device()
-        t = t.to(dev)
-        shape = torch.tensor([max(counts)] + list(t.shape[1:]), dtype=torch.int64, device=dev)
-        dist.all_reduce(shape, op=dist.ReduceOp.MAX)
-        want = [int(x) for x in shape.tolist()]
-        if want != list(t.shape):
-            out = t.new_full(want, pad_index)
-            out[tuple(slice(0, n) for n in t.shape)] = t
-            t = out
-        parts = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(parts, t.contiguous())
+        nd = self._MAX_DIMS
+        meta = torch.zeros(2 + nd, dtype=torch.int64, device=dev)
+        if t is not None:
+            if t.dim() > nd or t.dtype not in self._DTYPES:
+                raise ValueError(f"cannot gather a {t.dtype} tensor of {t.dim()} dims")
+            meta[0] = 1 + self._DTYPES.index(t.dtype)
+            meta[1] = t.dim()
+            meta[2:2 + t.dim()] = torch.tensor(list(t.shape), dtype=torch.int64)
+        dist.all_reduce(meta, op=dist.ReduceOp.MAX)
+        m = [int(x) for x in meta.tolist()]
+        if m[0] == 0:
+            return None
+        dtype, ndim = self._DTYPES[m[0] - 1], m[1]
+        want = [max(counts)] + m[3:2 + ndim]
+        out = torch.full(want, pad_index, dtype=dtype, device=dev)
+        if t is not None and t.numel():
+            out[tuple(slice(0, n) for n in t.shape)] = t.to(dev, dtype)
+        parts = [torch.empty_like(out) for _ in range(world)]
+        dist.all_gather(parts, out)
         return torch.cat([p[:c] for p, c in zip(parts, counts)])
 
+    def _counts(self, rows: int) -> List[int]:
+        """Every rank's row count (collective)."""
+        if self._world() == 1:
+            return [rows]
+        c = torch.zeros(self._world(), dtype=torch.int64, device=self._comm_device())
+        c[self._rank()] = rows
+        dist.all_reduce(c)
+        return [int(x) for x in c.tolist()]
+
     def evaluation_loop(self, dataset, metric_key_prefix: str = "eval", want_preds: bool = False):
-        """Loss, predictions and labels over the WHOLE dataset: per-sample
-        losses and logits stay on the device during the loop (no host sync
-        per batch), are gathered across the data-parallel ranks once at the
-        end, and the sampler's padding is cut off (reference
-        ``evaluation_loop`` / ``_nested_gather``,
-        atorch_trainer.py:1659,1857-2043)."""
+        """Loss, predictions and labels over the WHOLE dataset, in dataset
+        order, on every rank (reference ``evaluation_loop`` /
+        ``_nested_gather``, atorch_trainer.py:1857-2043).
+
+        Memory-bounded like the reference (atorch_trainer.py:149,203-207,
+        1903-1961): ``preprocess_logits_for_metrics(logits, labels)`` runs
+        per batch on the device (e.g. vocab logits -> argmax ids), logits
+        keep their own dtype, and with ``eval_accumulation_steps = k`` the
+        device-side accumulation is gathered across the ranks and moved to
+        the host every k batches -- the device holds at most k batches (x
+        world while gathering) whatever the dataset length.  Without it the
+        accumulation stays on the device and is gathered once at the end
+        (no host sync per batch).  Gathers are collectives every rank
+        enters, ranks whose share is only padding batches included."""
         dl = self.get_eval_dataloader(dataset)
         n = len(dl.dataset)
         real_batches = getattr(dl.batch_sampler, "num_real_batches", None)
+        eas = self.args.eval_accumulation_steps or 0
+        world = self._world()
         self.model.eval()
-        losses, preds, labels = [], [], []
+        losses, preds, labels = [], [], []  # device-side, since the last flush
+        host = {"loss": [[] for _ in range(world)], "pred": [[] for _ in range(world)],
+                "label": [[] for _ in range(world)]}
         collect = want_preds or self.compute_metrics is not None
+        pre = self.preprocess_logits_for_metrics
+        peak = 0
+
+        def flush():
+            nonlocal losses, preds, labels
+            counts = self._counts(sum(x.numel() for x in losses))
+            for key, buf in (("loss", losses), ("pred", preds), ("label", labels)):
+                local = _pad_cat(buf) if buf else None
+                g = self._gather(local, counts) if world > 1 else local
+                if g is None:
+                    continue
+                g = g.cpu()
+                o = 0
+                for r, c in enumerate(counts):  # per rank: the final order is rank-major (dataset order)
+                    if c:
+                        host[key][r].append(g[o:o + c])
+                    o += c
+            losses, preds, labels = [], [], []
+
         with torch.no_grad():
             for bi, inputs in enumerate(dl):
                 inputs = self._prepare_inputs(inputs)
                 with self._autocast():
                     loss, out = self.compute_loss(self.model, inputs, return_outputs=True)
-                if real_batches is not None and bi >= real_batches:
-                    continue  # a padding batch (keeps FSDP / DDP collectives matched)
-                bs = self._batch_size(inputs)
-                losses.append(loss.detach().float().reshape(1).expand(bs))
-                if collect:
-                    lg = self._logits(out)
-                    if lg is not None:
-                        preds.append(lg.detach().float())
-                    lb = self._labels(inputs)
-                    if lb is not None:
-                        labels.append(lb.detach())
+                if real_batches is None or bi < real_batches:  # else a padding batch (collectives matched)
+                    bs = self._batch_size(inputs)
+                    losses.append(loss.detach().float().reshape(1).expand(bs))
+                    if collect:
+                        lg = self._logits(out)
+                        lb = self._labels(inputs)
+                        if lg is not None and pre is not None:
+                            lg = pre(lg, lb)
+                        if lg is not None:
+                            preds.append(lg.detach())
+                        if lb is not None:
+                            labels.append(lb.detach())
+                    peak = max(peak, sum(t.numel() * t.element_size() for t in preds + labels))
+                del out
+                if eas and (bi + 1) % eas == 0:
+                    flush()
+        flush()
         self.model.train()
-        counts = [n]
-        if self._world() > 1:
-            mine = sum(x.numel() for x in losses)
-            c = torch.zeros(self._world(), dtype=torch.int64, device=self._comm_device())
-            c[self._rank()] = mine
-            dist.all_reduce(c)
-            counts = [int(x) for x in c.tolist()]
-        loss_all = self._gather(torch.cat(losses) if losses else torch.zeros(0, device=self.device), counts)
-        preds_all = self._gather(_pad_cat(preds), counts) if preds else None
-        labels_all = self._gather(_pad_cat(labels), counts) if labels else None
-        preds_all = preds_all.cpu() if preds_all is not None else None
-        labels_all = labels_all.cpu() if labels_all is not None else None
-        metrics = {f"{metric_key_prefix}_loss": float(loss_all.mean()) if loss_all.numel() else float("nan")}
+        self.eval_peak_accum_bytes = peak  # device bytes of accumulated predictions + labels at most
+
+        def cat(key):
+            parts = [t for r in range(world) for t in host[key][r]]
+            if not parts:
+                return None
+            t = _pad_cat(parts)
+            return t.float() if t.dtype in (torch.bfloat16, torch.float16) else t  # numpy has no bf16
+
+        loss_all, preds_all, labels_all = cat("loss"), cat("pred"), cat("label")
+        metrics = {f"{metric_key_prefix}_loss": float(loss_all.mean()) if loss_all is not None else float("nan")}
         if self.compute_metrics is not None and preds_all is not None:
             from transformers import EvalPrediction
 

@@ -159,6 +159,11 @@ class _FlatOptimizer(torch.optim.Optimizer):
         if (not self._dsw_supported() or os.environ.get("DWAMD_DEFER_STATE", "1") == "0"
                 or self._overlap is not None or not self.flat.data.is_cuda):
             return False
+        if self.master is None:
+            # no fp32 master: the parameters ARE the weights the replay starts
+            # from, and a deferred step overwrites them -- replaying the kept
+            # steps would apply them twice.  Wait for the ring instead.
+            return False
         if self._dsw is not None and self._dsw["copier"] is not copier:
             return False
         if self._dsw is None and not self._ring_touches(copier):

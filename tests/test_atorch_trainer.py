@@ -186,6 +186,151 @@ def test_four_rank_evaluation_equals_single_process(tmp_path):
         assert out[3] == 37 and torch.allclose(torch.tensor(out[2]), want_pred, atol=1e-5)
 
 
+class _LMDS(torch.utils.data.Dataset):
+    """Token sequences for a vocab-sized-logits model."""
+
+    def __init__(self, n, seq=12, vocab=512):
+        g = torch.Generator().manual_seed(5)
+        self.x = torch.randint(0, vocab, (n, seq), generator=g)
+
+    def __len__(self):
+        return len(self.x)
+
+    def __getitem__(self, i):
+        return {"x": self.x[i], "labels": self.x[i]}
+
+
+class _LM(torch.nn.Module):
+    def __init__(self, vocab=512):
+        super().__init__()
+        torch.manual_seed(0)
+        self.emb = torch.nn.Embedding(vocab, 16)
+        self.head = torch.nn.Linear(16, vocab)
+
+    def forward(self, x, labels=None):
+        logits = self.head(self.emb(x))
+        out = {"logits": logits}
+        if labels is not None:
+            out["loss"] = torch.nn.functional.cross_entropy(logits.flatten(0, 1), labels.flatten())
+        return out
+
+
+def _argmax(logits, labels):
+    return logits.argmax(-1)
+
+
+def _tok_metrics(p):
+    import numpy as np
+
+    return {"tok_acc": float((p.predictions == p.label_ids).mean()), "rows": int(len(p.label_ids)),
+            "pred_sum": int(np.sum(p.predictions))}
+
+
+def _lm_eval(rank, world, port, q, out, sizes, eas):
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    import torch.distributed as dist
+
+    try:
+        from dlrover_wuqiong_amd.atorch.trainer import AtorchTrainer
+
+        if world > 1:
+            dist.init_process_group("gloo")
+        res = []
+        for n in sizes:
+            t = AtorchTrainer(_LM(), _cls_args(out, per_device_eval_batch_size=2, eval_accumulation_steps=eas,
+                                               atorch_opt="ddp" if world > 1 else "none"),
+                              train_dataset=_LMDS(8), eval_dataset=_LMDS(n), compute_metrics=_tok_metrics,
+                              preprocess_logits_for_metrics=_argmax)
+            m = t.evaluate()
+            res.append((m, t.eval_peak_accum_bytes))
+            t.close()
+        q.put((rank, ("ok", res)))
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        traceback.print_exc()
+        q.put((rank, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _spawn_eval(world, target, args):
+    import torch.multiprocessing as mp
+
+    from conftest import free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in ps), key=lambda x: x[0])
+    for p in ps:
+        p.join(timeout=60)
+    return res
+
+
+def test_bounded_eval_with_logit_preprocessing_matches_single_process(tmp_path):
+    """Vocab-sized logits reduced to argmax ids per batch, moved to the host
+    every 2 batches on 4 gloo ranks: the metrics equal one process's, and
+    the device-side accumulation is bounded whatever the dataset length."""
+    import queue
+
+    q = queue.Queue()
+    _lm_eval(0, 1, 0, q, str(tmp_path / "s"), (37, 150), None)
+    _r, single = q.get()
+    assert single[0] == "ok", single
+    res = _spawn_eval(4, _lm_eval, (str(tmp_path / "d"), (37, 150), 2))
+    for _r, out in res:
+        assert isinstance(out, tuple) and out[0] == "ok", res
+        for (m, peak), (want, _p) in zip(out[1], single[1]):
+            assert m["eval_rows"] == want["eval_rows"] and m["eval_pred_sum"] == want["eval_pred_sum"]
+            assert abs(m["eval_tok_acc"] - want["eval_tok_acc"]) < 1e-12
+            assert abs(m["eval_loss"] - want["eval_loss"]) < 1e-5
+        (_m37, peak37), (_m150, peak150) = out[1]
+        # at most 2 batches of int64 ids + labels (2 x 12 tokens x 8 B each) on the device
+        assert peak37 == peak150 <= 2 * 2 * (2 * 12 * 8), (peak37, peak150)
+
+
+def _few_batches_eval(rank, world, port, q, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    import torch.distributed as dist
+
+    try:
+        from dlrover_wuqiong_amd.atorch.trainer import AtorchTrainer
+
+        dist.init_process_group("gloo")
+        # 9 samples, eval batch 3: 3 batches on 4 ranks -- rank 3 has only a padding batch
+        t = AtorchTrainer(_Cls(), _cls_args(out), train_dataset=_ClsDS(), eval_dataset=_ClsDS(9),
+                          compute_metrics=_metrics)
+        m = t.evaluate()
+        pr = t.predict(_ClsDS(9))
+        q.put((rank, ("ok", m, pr.num_samples, tuple(pr.predictions.shape))))
+        t.close()
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        traceback.print_exc()
+        q.put((rank, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_eval_with_more_ranks_than_batches(tmp_path):
+    """A rank whose whole share is padding still enters every gather (no
+    deadlock) and the result covers exactly the dataset."""
+    res = _spawn_eval(4, _few_batches_eval, (str(tmp_path / "d"),))
+    for _r, out in res:
+        assert isinstance(out, tuple) and out[0] == "ok", res
+        assert out[1]["eval_n"] == 9 and out[2] == 9 and out[3] == (9, 2)
+
+
 def test_load_best_model_at_end(tmp_path):
     from dlrover_wuqiong_amd.atorch.trainer import AtorchTrainer
 

@@ -16,7 +16,7 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-def _model_and_opt():
+def _model_and_opt(dtype=torch.bfloat16):
     from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
     from dlrover_wuqiong_amd.optimizers.fused import FusedAdamW
     from dlrover_wuqiong_amd.parallel.flat import FlatParams
@@ -25,7 +25,7 @@ def _model_and_opt():
     cfg = GPT2Config.named("gpt2-tiny")
     with torch.device("cuda"):
         model = GPT2(cfg)
-    model.to(torch.bfloat16)
+    model.to(dtype)
     flat = FlatParams(model)
     opt = FusedAdamW(flat, lr=1e-3)
     x = torch.randint(0, cfg.vocab_size, (2, 65), device="cuda")
@@ -610,7 +610,7 @@ def test_gpu_close_right_after_deferred_restore(tmp_path, monkeypatch):
     assert torch.equal(opt.exp_avg, want[0]) and torch.equal(opt.master, want[1])
 
 
-def _ring_run(tmp_path, monkeypatch, defer: bool, tag: str):
+def _ring_run(tmp_path, monkeypatch, defer: bool, tag: str, dtype=torch.bfloat16):
     """Manual gradients (bit-reproducible), a ring snapshot at step 2 whose
     PCIe drain is held back by a GPU sleep on the flush stream, 5 more
     steps; returns the final state, the restored snapshot and whether the
@@ -631,14 +631,15 @@ def _ring_run(tmp_path, monkeypatch, defer: bool, tag: str):
         return orig(self, *a, **k)
 
     monkeypatch.setattr(cp.GpuCopier, "_save_slice_ring", held)
-    model, opt, flat = _model_and_opt()
+    model, opt, flat = _model_and_opt(dtype)
     opt.max_grad_norm = 1.0  # the clip coefficient is part of the kept steps
     g = torch.Generator(device="cpu").manual_seed(11)
+    w = opt.master if opt.master is not None else flat.data  # the fp32 weights the update reads
     # seeded state: _model_and_opt's warm-up backward reduces with float
     # atomics, so its first update differs from run to run in the last bits
     with torch.no_grad():
-        opt.master.copy_(0.02 * torch.randn(flat.numel, generator=g))
-        flat.data.copy_(opt.master.to(flat.data.dtype))
+        w.copy_(0.02 * torch.randn(flat.numel, generator=g))
+        flat.data.copy_(w.to(flat.data.dtype))
         opt.exp_avg.copy_(1e-3 * torch.randn(flat.numel, generator=g))
         opt.exp_avg_sq.copy_(1e-6 * torch.rand(flat.numel, generator=g))
     ck = DdpCheckpointer(str(tmp_path / tag))
@@ -651,15 +652,15 @@ def _ring_run(tmp_path, monkeypatch, defer: bool, tag: str):
         deferred.append(opt._dsw is not None)
         if s == 2:
             torch.cuda.synchronize()
-            snap = (flat.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(), opt.master.clone())
+            snap = (flat.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(), w.clone())
             assert ck.save_checkpoint(3, state(), storage_type=StorageType.MEMORY)
     opt.join()
     torch.cuda.synchronize()
-    final = (flat.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(), opt.master.clone())
+    final = (flat.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(), w.clone())
     ck.wait_latest_checkpoint()
     ck.load_checkpoint(target=state())
     torch.cuda.synchronize()
-    restored = (flat.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(), opt.master.clone())
+    restored = (flat.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone(), w.clone())
     assert ck.engine._copier.last_snapshot_mode == "ring"
     ck.close()
     return final, snap, restored, deferred
@@ -672,8 +673,8 @@ def test_gpu_adam_replay_matches_flat_updates():
     opt.max_grad_norm = 1.0
     g = torch.Generator(device="cpu").manual_seed(3)
     with torch.no_grad():
-        opt.master.copy_(0.02 * torch.randn(flat.numel, generator=g))
-        flat.data.copy_(opt.master.to(flat.data.dtype))
+        w.copy_(0.02 * torch.randn(flat.numel, generator=g))
+        flat.data.copy_(w.to(flat.data.dtype))
         opt.exp_avg.copy_(1e-3 * torch.randn(flat.numel, generator=g))
         opt.exp_avg_sq.copy_(1e-6 * torch.rand(flat.numel, generator=g))
     s0 = [t.clone() for t in (flat.data, opt.exp_avg, opt.exp_avg_sq, opt.master)]
@@ -716,6 +717,19 @@ def test_gpu_ring_snapshot_deferred_state_writeback(tmp_path, monkeypatch):
         assert torch.equal(s, r)  # the checkpoint is the state at the save
     for a, b in zip(snap_w, snap_d):
         assert torch.equal(a, b)
+
+
+def test_gpu_ring_snapshot_fp32_params_without_master(tmp_path, monkeypatch):
+    """fp32 parameters with no master copy: the parameters are the weights a
+    replay would start from, so the optimizer must not defer (a deferred
+    step would be applied twice) -- the result equals the waiting run."""
+    final_w, snap_w, _rest_w, _ = _ring_run(tmp_path, monkeypatch, False, "wait32", torch.float32)
+    final_d, snap_d, rest_d, def_d = _ring_run(tmp_path, monkeypatch, True, "defer32", torch.float32)
+    assert not any(def_d)
+    for name, a, b in zip(("param", "exp_avg", "exp_avg_sq", "weights"), final_w, final_d):
+        assert torch.equal(a, b), (name, float((a - b).abs().max()))
+    for s, r in zip(snap_d, rest_d):
+        assert torch.equal(s, r)
 
 
 def test_gpu_flush_never_overwrites_host_tensors(tmp_path):
