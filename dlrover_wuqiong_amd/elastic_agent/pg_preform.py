@@ -97,6 +97,9 @@ def preform(store_addr: str, prefix: str, rank: int, world: int, backend: str = 
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         ok = float(t.item()) == float(world)
+        # the pre-form limit guarded the rendezvous only: later store waits
+        # (subgroup unique ids after an adoption) get the collective timeout
+        store.set_timeout(collective_timeout())
     except Exception as e:
         _log(f"pre-forming a {backend} group of {world} failed: {e}")
         _destroy()
@@ -147,9 +150,61 @@ def _compatible(backend, world_size: int, rank: int) -> bool:
     return world_size == _state["world"] and rank == _state["rank"]
 
 
+_rebound: list = []  # (namespace dict, name) rebound to the wrapper at arm()
+# big third-party trees that never call init_process_group themselves (the
+# scan is on the restart path; torch's own entry points are patched above)
+_SKIP_MODULES = frozenset(("torch", "numpy", "scipy", "pandas", "pyarrow", "sympy", "encodings", "importlib"))
+
+
+_alias_sites: Optional[list] = None  # (namespace dict, name) found while parked
+
+
+def _find_aliases(orig) -> list:
+    out = []
+    for mname, mod in list(sys.modules.items()):
+        if mod is None or mname.split(".", 1)[0] in _SKIP_MODULES:
+            continue
+        d = getattr(mod, "__dict__", None)
+        if not isinstance(d, dict) or d is globals():  # (this module keeps the original in _orig_init)
+            continue
+        try:
+            out.extend((d, k) for k, v in d.items() if v is orig)
+        except RuntimeError:  # the dict changed under us (another thread importing)
+            continue
+    return out
+
+
+def _rebind_aliases(orig, wrapper) -> int:
+    """Point every module-global name that IS ``orig`` at ``wrapper``: a
+    script that did ``from torch.distributed import init_process_group``
+    before a deep standby parked holds the original function in its own
+    globals (``__main__``, the runpy module of the script, or any of its
+    modules); patching the torch attributes alone would leave it calling
+    the original, which then finds the pre-formed default group and raises
+    "trying to initialize the default process group twice"."""
+    global _alias_sites
+    # a deep standby scanned while parked (the script is blocked in
+    # standby_point, so nothing new binds the name): the restart only rebinds
+    sites = _alias_sites if _alias_sites is not None else _find_aliases(orig)
+    _alias_sites = None
+    n = 0
+    for d, k in sites:
+        if d.get(k) is orig:
+            d[k] = wrapper
+            _rebound.append((d, k))
+            n += 1
+    return n
+
+
 def arm(adopt: bool):
     """Called once at activation.  ``adopt`` (the agent's decision): keep the
-    pre-formed group for the script's ``init_process_group``; else drop it."""
+    pre-formed group for the script's ``init_process_group``; else drop it.
+
+    The first ``init_process_group`` call after this -- through
+    ``torch.distributed``, ``distributed_c10d`` or any module-global alias of
+    the function -- adopts the group when the request matches it (backend,
+    world, rank), else destroys it and forms the world cold; either way the
+    patch and every rebound alias are undone by that call."""
     global _orig_init
     if not _state:
         return
@@ -163,7 +218,7 @@ def arm(adopt: bool):
 
     if _orig_init is not None:
         return
-    _orig_init = c10d.init_process_group
+    _orig_init = orig = c10d.init_process_group
 
     def init_process_group(backend=None, init_method=None, timeout=None, world_size=-1, rank=-1, store=None,
                            group_name="", pg_options=None, device_id=None, **kw):
@@ -171,18 +226,39 @@ def arm(adopt: bool):
         _restore_init()
         if dist.is_initialized() and _state and _compatible(backend, world_size, rank):
             _adopted = dict(_state, adopted_at=time.time())
+            _set_store_timeout(timeout)
             _log(f"adopted the pre-formed {_state['backend']} group (rank {_state['rank']} of {_state['world']})")
             return None
         if _state:
             _log(f"requested backend={backend!r} world={world_size} rank={rank} does not match the pre-formed "
                  f"{_state}: forming the world cold")
             _destroy()
-        return c10d.init_process_group(backend=backend, init_method=init_method, timeout=timeout,
-                                       world_size=world_size, rank=rank, store=store, group_name=group_name,
-                                       pg_options=pg_options, device_id=device_id, **kw)
+        return orig(backend=backend, init_method=init_method, timeout=timeout, world_size=world_size, rank=rank,
+                    store=store, group_name=group_name, pg_options=pg_options, device_id=device_id, **kw)
 
     c10d.init_process_group = init_process_group
     dist.init_process_group = init_process_group
+    _rebound.clear()
+    _rebind_aliases(orig, init_process_group)
+
+
+def disarm():
+    """Undo :func:`arm`'s patch without using it (the script never called
+    ``init_process_group``); the pre-formed group stays the default group."""
+    _restore_init()
+
+
+def _set_store_timeout(timeout=None):
+    """The adopted group keeps the standby's store client: give it the
+    script's (or the collective) timeout instead of the pre-form limit, so
+    store waits of lazily created subgroups time out like a cold world's."""
+    try:
+        import torch.distributed.distributed_c10d as c10d
+
+        t = timeout if timeout is not None else collective_timeout()
+        c10d._get_default_store().set_timeout(t)
+    except Exception as e:  # never fatal
+        _log(f"store timeout not updated: {e}")
 
 
 def _restore_init():
@@ -192,8 +268,13 @@ def _restore_init():
     import torch.distributed as dist
     import torch.distributed.distributed_c10d as c10d
 
+    wrapper = c10d.init_process_group
     c10d.init_process_group = _orig_init
     dist.init_process_group = _orig_init
+    for d, k in _rebound:
+        if d.get(k) is wrapper:
+            d[k] = _orig_init
+    _rebound.clear()
     _orig_init = None
 
 
@@ -203,8 +284,13 @@ def handle_line(obj: dict, ctl: str, lr: str) -> bool:
     spec = obj.get("preform") if isinstance(obj, dict) else None
     if spec is None:
         return False
+    global _alias_sites
     ok = preform(spec["store"], spec["prefix"], int(lr), int(spec["world"]), spec.get("backend", "auto"),
                  timeout=float(spec.get("timeout", 120.0)))
+    if ok:
+        import torch.distributed.distributed_c10d as c10d
+
+        _alias_sites = _find_aliases(c10d.init_process_group)  # off the restart path
     if ok and ctl:
         path = os.path.join(ctl, PG_MARK_PREFIX + lr)
         with open(path + ".tmp", "w") as f:

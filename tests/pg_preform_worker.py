@@ -17,6 +17,8 @@ import time
 
 import torch
 import torch.distributed as dist
+import torch.distributed.distributed_c10d as c10d
+from torch.distributed import init_process_group as imported_init  # bound before a deep standby parks
 
 from dlrover_wuqiong_amd.elastic_agent import pg_preform
 
@@ -26,14 +28,28 @@ def main():
     p.add_argument("--out", required=True)
     p.add_argument("--kill", action="store_true")
     p.add_argument("--first-world", type=int, default=0, help="world size of the incarnation that waits")
+    p.add_argument("--deep", action="store_true", help="deep-standby script: parks in standby_point()")
+    p.add_argument("--backend", default="gloo")
     a = p.parse_args()
+    if a.deep:
+        from dlrover_wuqiong_amd.elastic_agent.standby import standby_point
+
+        standby_point(prepin_shm=False)
     t0 = time.time()
-    dist.init_process_group("gloo")
+    lr = int(os.environ.get("LOCAL_RANK", "0"))
+    if not a.deep:
+        dist.init_process_group(a.backend)
+    elif lr % 2 == 0:
+        imported_init(a.backend)  # the module-global alias taken before the standby parked
+    else:
+        c10d.init_process_group(a.backend)
     rank, world = dist.get_rank(), dist.get_world_size()
     t = torch.tensor([float(rank + 1)])
     dist.all_reduce(t)
     inc = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
     rec = {"inc": inc, "rank": rank, "world": world, "adopted": pg_preform.adopted() is not None,
+           # the patch and every rebound alias are gone after the call
+           "clean": pg_preform._orig_init is None and imported_init is c10d.init_process_group is dist.init_process_group,
            "sum": float(t.item()), "init_sec": round(time.time() - t0, 4), "pid": os.getpid()}
     with open(a.out, "a") as f:
         f.write(json.dumps(rec) + "\n")

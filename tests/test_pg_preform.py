@@ -49,6 +49,25 @@ def test_eight_rank_restart_adopts_preformed_group(tmp_path):
     assert "pre-formed process group adopted" in log
 
 
+def test_deep_standby_script_with_imported_init_adopts(tmp_path):
+    """A deep-standby script that bound ``init_process_group`` before parking
+    (``from torch.distributed import init_process_group`` / a
+    ``distributed_c10d`` module alias): all 8 restarted ranks adopt the
+    pre-formed group, nothing raises "initialize the default process group
+    twice", and the patch is removed afterwards."""
+    out = tmp_path / "out.jsonl"
+    p = _run(["--nnodes", "1", "--nproc-per-node", "8", "--max-restarts", "1", "--monitor-interval", "0.05",
+              "--standby-mode", "deep", WORKER, "--out", str(out), "--kill", "--deep"],
+             {"DWAMD_STANDBY_DELAY": "0", "DWAMD_FAILURE_STOP_TIMEOUT": "0"})
+    log, _ = p.communicate(timeout=300)
+    assert p.returncode == 0, log[-5000:]
+    assert "twice" not in log
+    recs = _records(out)
+    second = [r for r in recs if r["inc"] == 1]
+    assert sorted(r["rank"] for r in second) == list(range(8)), recs
+    assert all(r["adopted"] and r["clean"] and r["sum"] == 36.0 for r in second), second
+
+
 def test_membership_change_falls_back_to_cold_init(tmp_path):
     port = free_port()
     out = tmp_path / "out.jsonl"
@@ -89,6 +108,7 @@ def test_membership_change_falls_back_to_cold_init(tmp_path):
 _UNIT = r"""
 import datetime, os, sys
 import torch, torch.distributed as dist
+ORIG = [dist.init_process_group]  # (a list: module-global aliases are rebound by arm())
 from dlrover_wuqiong_amd.elastic_agent import pg_preform
 port = int(sys.argv[1])
 store = dist.TCPStore("127.0.0.1", port, is_master=True, wait_for_workers=False)
@@ -97,9 +117,14 @@ os.environ.update(RANK="0", WORLD_SIZE="1")
 assert pg_preform.preform(f"127.0.0.1:{port}", "g1/", 0, 1, "gloo")
 assert pg_preform._compatible("gloo", -1, -1) and pg_preform._compatible("cpu:gloo,cuda:nccl", 1, 0)
 assert not pg_preform._compatible("nccl", -1, -1) and not pg_preform._compatible("gloo", 2, -1)
+holder = type(sys)("user_mod"); holder.ipg = ORIG[0]; sys.modules["user_mod"] = holder
 pg_preform.arm(True)
-dist.init_process_group("gloo")
+assert holder.ipg is not ORIG[0]  # module-global aliases are rebound to the adopting wrapper
+holder.ipg("gloo", timeout=datetime.timedelta(seconds=77))
 assert pg_preform.adopted() is not None and dist.is_initialized()
+assert holder.ipg is ORIG[0]  # ... and restored by the call
+from torch.distributed.distributed_c10d import _get_default_store
+assert abs(_get_default_store().timeout.total_seconds() - 77) < 1  # the script's timeout, not the pre-form limit
 assert dist.init_process_group is pg_preform._orig_init or pg_preform._orig_init is None  # patch removed
 dist.destroy_process_group()
 # 2) formed, then a mismatching request: destroyed, the world forms cold
@@ -108,7 +133,8 @@ assert pg_preform.preform(f"127.0.0.1:{port}", "g2/", 0, 1, "gloo")
 pg_preform._state["world"] = 2  # as if formed for another world than the one requested
 pg_preform.arm(True)
 os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port + 1))
-dist.init_process_group("gloo", world_size=1, rank=0, store=dist.PrefixStore("cold/", store))
+holder.ipg("gloo", world_size=1, rank=0, store=dist.PrefixStore("cold/", store))  # through an alias too
+assert holder.ipg is ORIG[0]
 assert pg_preform.adopted() is None and pg_preform.preformed() is None and dist.is_initialized()
 dist.destroy_process_group()
 # 3) the agent says no: dropped at activation
