@@ -170,12 +170,12 @@ def _job(a, n: int, mode: str, run_dir: str, tag: str):
         # a save whose staging buffer is still flushing WAITS (and the wait is
         # part of the measured pause) instead of being skipped
         "DWAMD_CKPT_BUSY": "wait",
-        # the training loop saves between iterations and writes parameters /
-        # optimizer state only in optimizer.step: the HBM snapshot copy runs
-        # on a side stream under the next forward, fenced by that step
-        # (copier.py; the pause is the host work only).  DWAMD_OVERLAP_SNAPSHOT=0:
-        # the copy on the compute stream inside the pause
-        "DWAMD_OVERLAP_SNAPSHOT": os.environ.get("DWAMD_OVERLAP_SNAPSHOT", "1"),
+        # the framework default: the HBM snapshot copy runs on the compute
+        # stream inside the pause.  The opt-in overlapped copy (side stream
+        # under the next forward, fenced by the next optimizer step; only safe
+        # when checkpointed tensors are written in optimizer.step alone) is
+        # measured separately in the deep job (``save_sec_overlapped``)
+        "DWAMD_OVERLAP_SNAPSHOT": os.environ.get("DWAMD_OVERLAP_SNAPSHOT", "0"),
     })
     if a.rehearse_shared_device:
         env["DWAMD_REHEARSE_SHARED_DEVICE"] = "1"
@@ -387,6 +387,15 @@ def summarize(a, run_dir, n, wall):
         "rehearsal": rehearsal,
         "save_sec_mean": round(save_sec, 4),
         "save_sec_max": round(phase0["save_sec_max"], 4),
+        "snapshot_mode": phase0.get("snapshot_copy"),
+        # the training time one save costs, pause + anything it leaves to
+        # the following steps (loop time per step - median step) x interval,
+        # the closing wait for the last PCIe flush excluded
+        "per_save_training_cost_ms": phase0.get("per_save_cost_ms"),
+        # the opt-in overlapped snapshot copy (DWAMD_OVERLAP_SNAPSHOT=1): pause
+        # and the same per-save cost, measured right after the timed loop
+        "save_sec_overlapped": phase0.get("save_sec_overlapped"),
+        "per_save_training_cost_ms_overlapped": phase0.get("per_save_cost_ms_overlapped"),
         "timed_saves": phase0.get("timed_saves"),
         "timed_saves_ok": phase0.get("timed_saves_ok"),
         "skipped_saves_timed": phase0.get("skipped_saves_timed"),
@@ -507,6 +516,10 @@ def _fault_summary(a, ev, agent, step_sec, save_sec):
         "save_ms_after_restart": [e["save_ms"] for e in steps1 if e.get("save_ms") is not None],
         "flushes_after_restart": done.get("flushes"),
         "gc_pauses_after_restart": done.get("gc_pauses"),
+        # device allocations of the caching allocator from activation to the
+        # 4th save after the restart (0: everything came from what the standby
+        # reserved while parked)
+        "device_allocs_after_restart": done.get("device_allocs_after_restart"),
     }
     # a MODEL, not a measurement: one failure per hour, a checkpoint every
     # ckpt_interval steps (mean loss: half an interval of steps)
@@ -636,8 +649,18 @@ def worker(a) -> int:
         if cuda:
             torch.cuda.synchronize()
             torch.cuda.empty_cache()  # the parked standby keeps only model + optimizer (+ HBM staging)
+    def dev_allocs() -> int:
+        """Device allocations the caching allocator made so far (cumulative)."""
+        if not cuda:
+            return 0
+        st = torch.cuda.memory_stats(device)
+        return int(st.get("num_device_alloc", st.get("segment.all.allocated", 0)))
+
+    alloc0 = dev_allocs()  # import standby: this process became the worker just now
     info = standby_point()  # deep standby: parks here until the agent activates it
     t_act = time.time() if info is not None else t_proc
+    if info is not None:
+        alloc0 = dev_allocs()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -803,8 +826,8 @@ def worker(a) -> int:
         # this worker's warm profile -- recorded during the warm-up)
         wait_standbys(["standby_ready.{}"])
         if cuda:
-            wait_standbys(["standby_warm.{}"] + (["hbm_staging.{}.json"] if a.phase == "import_hbm" else []),
-                          timeout=90.0)
+            # ... and hold the staging buffers + restart-path reservations
+            wait_standbys(["standby_warm.{}", "standby_staging.{}"], timeout=90.0)
         dt, _ok = save()
         ckpt.wait_latest_checkpoint()
         sync_all()
@@ -826,7 +849,10 @@ def worker(a) -> int:
         # warm-up): their one-time model build must not land in the timed
         # window.  Parked + (on a GPU) this rank's shm slices registered and
         # the HBM-tier staging buffers published
-        wait_standbys(["standby_ready.{}"] + (["standby_pinned.{}", "hbm_staging.{}.json"] if cuda else []))
+        wait_standbys(["standby_ready.{}"] + (["standby_pinned.{}", "hbm_staging.{}.json", "standby_staging.{}"]
+                                              if cuda else []))
+        if cuda:  # ... and the standbys' restart-path reservations (activation peak, small blocks)
+            wait_standbys(["standby_reserved.{}"], timeout=90.0)
         # one untimed save: the copier switches to the standby-owned staging
         # buffers (waits for in-flight flushes once)
         save()
@@ -850,6 +876,7 @@ def worker(a) -> int:
                 dt, ok = save()
                 save_times.append(dt)
                 oks.append(bool(ok))
+        t_loop = time.perf_counter() - t_start  # every step's compute done; the last flush may still run
         sync_all()
         t_timed = mx(time.perf_counter() - t_start)
         log(f"[rank {rank}] step ms:", [round(1000 * x, 1) for x in step_times], "save ms:",
@@ -863,6 +890,32 @@ def worker(a) -> int:
         save_max = mx(max(ok_times))
         step_sec = mx(statistics.median(step_times))
         loss_v = float(loss.float().item())
+        per_save_cost = mx(1000.0 * (t_loop / a.steps - statistics.median(step_times)) * a.ckpt_interval)
+
+        # ---------------- the opt-in overlapped snapshot copy: the same loop
+        # with the HBM copy on a side stream under the next forward
+        cp = ckpt.engine._copier
+        save_ov, cost_ov = None, None
+        if cuda and cp is not None and not cp.overlap:
+            ckpt.wait_latest_checkpoint()
+            sync_all()
+            cp.overlap = True
+            ov_saves, ov_steps = [], []
+            n_ov = 3 * a.ckpt_interval
+            t1 = time.perf_counter()
+            for i in range(n_ov):
+                ts = time.perf_counter()
+                train_step(False)
+                sync_step()
+                ov_steps.append(time.perf_counter() - ts)
+                if i % a.ckpt_interval == 0:
+                    ov_saves.append(save()[0])
+            t_ov = time.perf_counter() - t1
+            ckpt.wait_latest_checkpoint()
+            sync_all()
+            cp.overlap = False
+            save_ov = round(mx(statistics.mean(ov_saves)), 4)
+            cost_ov = round(mx(1000.0 * (t_ov / n_ov - statistics.median(ov_steps)) * a.ckpt_interval), 2)
 
         # ---------------- time to durable: pause + flush until in shm
         ckpt.wait_latest_checkpoint()
@@ -912,7 +965,9 @@ def worker(a) -> int:
               "gather": ckpt.engine._gather_group is not None, "pg": pg_info,
               "optimizer_update": "under next forward" if opt._overlap is not None else "compute stream",
               "snapshot_copy": "overlapped (fenced by the next optimizer step)" if ckpt.engine._copier is not None
-              and ckpt.engine._copier.overlap else "in the pause"})
+              and ckpt.engine._copier.overlap else "in the pause",
+              "per_save_cost_ms": round(per_save_cost, 2), "save_sec_overlapped": save_ov,
+              "per_save_cost_ms_overlapped": cost_ov})
 
         # ---------------- DISK persist (agent: torch.save archive written from
         # shm with parallel pwrite) while training continues: persist time and
@@ -1052,6 +1107,7 @@ def worker(a) -> int:
     s_end = s0 + a.fault_window
     last_before_kill = kill_after - (kill_after - s0) % a.ckpt_interval if kill_after > 0 else -1
     skipped_w = ckpt.engine.skipped_saves
+    saves_after, allocs_after = 0, None
     while step < s_end:
         train_step(True)
         sync_step()
@@ -1071,6 +1127,10 @@ def worker(a) -> int:
             save_ms = round(1000 * _dt, 2)
             if not ok:
                 emit({"event": "window_skipped", "n": 1, "step": step, "incarnation": incarnation})
+            if incarnation > 0:
+                saves_after += 1
+                if saves_after == 4:
+                    allocs_after = dev_allocs() - alloc0
             if incarnation == 0 and step == last_before_kill:
                 emit({"event": "saved_sums", "step": step, "rank": rank, "sums": state_sums()}, all_ranks=True)
         emit({"event": "step", "step": step, "t": time.time(), "incarnation": incarnation, "save_ms": save_ms})
@@ -1094,7 +1154,9 @@ def worker(a) -> int:
             f["pinned_frac"] = round(rec[5] / max(1, nb), 3)
         flushes.append(f)
     emit({"event": "done", "t": time.time(), "step": step, "start_step": start_step, "incarnation": incarnation,
-          "flushes": flushes, "skipped_saves": ckpt.engine.skipped_saves, "gc_pauses": gc_pauses[-20:]})
+          "flushes": flushes, "skipped_saves": ckpt.engine.skipped_saves, "gc_pauses": gc_pauses[-20:],
+          "device_allocs_after_restart": allocs_after if allocs_after is not None else (
+              dev_allocs() - alloc0 if incarnation > 0 else None)})
     sync_all()
     ckpt.close()
     if world > 1:

@@ -125,20 +125,31 @@ def _pinned_bytes() -> int:
         return 0
 
 
+STAGING_PREFIX = "standby_staging."  # staging buffers held for the worker (value: bytes, tier on/off)
+RESERVED_PREFIX = "standby_reserved."  # restart-path HBM reserved (value: bytes held for the worker)
+
+
 def _publish_hbm_staging(ctl: str, lr: str):
-    """Own the live worker's checkpoint staging buffers (HBM tier): they
-    then survive the worker, and this standby restores from them D2D."""
-    if os.environ.get("DWAMD_HBM_TIER", "1") != "1":
-        return
+    """Hold the worker's checkpoint staging buffers in this standby.  HBM
+    tier on: publish them to the live worker (they outlive it, the standby
+    restores D2D).  Tier off: keep them private -- the worker this standby
+    becomes snapshots into them, so no save after a restart allocates VRAM.
+    Also reserves the replicated restore's all-gather temporary (N > 1)."""
     try:
-        from ..flash_checkpoint.hbm_tier import publish_standby_buffers
-        from ..flash_checkpoint.prewarm import local_slice_bytes
+        from ..flash_checkpoint import hbm_tier
+        from ..flash_checkpoint.prewarm import local_slice_bytes, restore_temp_bytes
 
         n = local_slice_bytes()
-        if n > 0:
-            publish_standby_buffers(ctl, int(lr), n)
+        if n <= 0:
+            return
+        tier = os.environ.get("DWAMD_HBM_TIER", "1") == "1"
+        ok = (hbm_tier.publish_standby_buffers(ctl, int(lr), n) if tier else
+              hbm_tier.reserve_private_staging(n))
+        tmp = hbm_tier.reserve_restore_temp(restore_temp_bytes())
+        if ok and ctl and not os.path.exists(os.path.join(ctl, STAGING_PREFIX + lr)):
+            _mark(ctl, STAGING_PREFIX, lr, f"{2 * n} {int(tier)} {tmp}\n")
     except Exception as e:  # never fatal: the restore falls back to shm
-        print(f"[standby] HBM staging not published: {e}", file=sys.stderr)
+        print(f"[standby] HBM staging not held: {e}", file=sys.stderr)
 
 
 def _mark(ctl: str, prefix: str, lr: str, text: str):
@@ -176,10 +187,13 @@ def standby_point(prepin_shm: bool = True, repin_interval: float = 0.25) -> Opti
     buf = b""
     fd = sys.stdin.fileno()
     cmd = None
+    rsv = _Reservation(ctl, lr, deep=True) if prepin_shm else None
     while cmd is None:
         if not pinned_marked and prepin_shm and _pinned_bytes() > 0:
             _mark(ctl, PINNED_PREFIX, lr, f"{_pinned_bytes()}\n")
             pinned_marked = True
+        if rsv is not None:
+            rsv.tick()
         r, _, _ = select.select([fd], [], [], repin_interval)
         if r:
             chunk = os.read(fd, 1 << 20)
@@ -259,16 +273,18 @@ def _gpu_init(lr: str) -> bool:
         return False
 
 
-def _reserve_state_memory(reserved: int = 0, prof: Optional[dict] = None) -> int:
+def _reserve_state_memory(reserved: int = 0, prof: Optional[dict] = None, held: int = 0) -> int:
     """Fill PyTorch's caching allocator with about the HBM the worker will
     take -- its recorded peak footprint (warm profile: model + optimizer +
     activations), else the checkpoint payload size once a save made it known
     -- and leave it cached: the driver's allocation of fresh VRAM (it clears
     every new buffer) is then paid while waiting, not inside the restart
     (~1.9 s for the 19 GB of GPT2-1.5B Adam state alone).  ``reserved``:
-    bytes already held (only the increment is allocated).  Bounded by the
-    free HBM; DWAMD_STANDBY_RESERVE=0 disables it.  Returns bytes reserved
-    (-1: skipped for good)."""
+    bytes already held (only the increment is allocated); ``held``: bytes
+    of the worker's footprint this process already holds otherwise (a deep
+    standby's built model + optimizer).  Bounded by the free HBM;
+    DWAMD_STANDBY_RESERVE=0 disables it.  Returns bytes reserved (-1:
+    skipped for good)."""
     if os.environ.get("DWAMD_STANDBY_RESERVE", "1") != "1":
         return -1
     try:
@@ -278,6 +294,7 @@ def _reserve_state_memory(reserved: int = 0, prof: Optional[dict] = None) -> int
         from .warm_profile import reserve_bytes
 
         want = reserve_bytes(prof, local_state_bytes(), float(os.environ.get("DWAMD_STANDBY_RESERVE_FACTOR", "1.25")))
+        want -= held
         if want <= reserved:
             return reserved
         free, _total = torch.cuda.mem_get_info()
@@ -290,6 +307,67 @@ def _reserve_state_memory(reserved: int = 0, prof: Optional[dict] = None) -> int
     except Exception as e:  # never fatal
         print(f"[standby] HBM reserve skipped: {e}", file=sys.stderr)
         return reserved or -1
+
+
+class _Reservation:
+    """Everything a restart would otherwise allocate from the driver, held
+    by the standby while it waits (``DWAMD_STANDBY_RESERVE=0``: off):
+
+    * the worker's peak footprint in the caching allocator (import: the
+      whole peak; deep: the peak minus the model + optimizer it already
+      built -- the first steps' activations);
+    * 128 MiB of small-block pool (descriptor tables, scalars, batches);
+    * checkpoint staging + the restore all-gather temporary
+      (:func:`_publish_hbm_staging`).
+
+    The counter the bench reports (``device_allocs_after_restart``) is the
+    allocator's device allocations from activation to the 4th save after
+    the restart; with these held it is 0.  Released under HBM pressure."""
+
+    def __init__(self, ctl: str, lr: str, deep: bool):
+        self.ctl, self.lr, self.deep = ctl, lr, deep
+        self.reserved = 0
+        self.prof = None
+        self.small = False
+        self.marked = False
+        self.held = 0
+
+    def tick(self, replay_profile: bool = False):
+        if os.environ.get("DWAMD_STANDBY_RESERVE", "1") != "1":
+            return
+        if not self.small:
+            try:
+                from ..flash_checkpoint.hbm_tier import reserve_small_pool
+
+                reserve_small_pool()
+            except Exception as e:  # never fatal
+                print(f"[standby] small-pool reserve skipped: {e}", file=sys.stderr)
+            self.small = True
+            if self.deep:
+                import torch
+
+                self.held = int(torch.cuda.memory_allocated())  # the built model + optimizer
+        if self.prof is None:
+            if replay_profile:
+                self.prof = _apply_warm_profile(self.ctl, self.lr)
+            else:
+                from . import warm_profile
+
+                self.prof = warm_profile.load(self.ctl, self.lr) if self.ctl else None
+            if self.prof is not None:
+                if self.reserved >= 0:
+                    self.reserved = _reserve_state_memory(self.reserved, self.prof, self.held)
+                _mark(self.ctl, WARM_PREFIX, self.lr, f"{self.reserved}\n")
+                self._mark_reserved()
+        if self.reserved == 0 and not self.deep:
+            self.reserved = _reserve_state_memory()
+        elif self.reserved > 0:
+            self.reserved = _release_under_pressure(self.reserved)
+
+    def _mark_reserved(self):
+        if not self.marked:
+            _mark(self.ctl, RESERVED_PREFIX, self.lr, f"{max(0, self.reserved)}\n")
+            self.marked = True
 
 
 def _apply_warm_profile(ctl: str, lr: str) -> Optional[dict]:
@@ -343,8 +421,7 @@ def _wait_command(pin: bool, ctl: str, lr: str, interval: float = 0.25) -> Optio
     buf = b""
     fd = sys.stdin.fileno()
     pinned_marked = False
-    reserved = 0
-    prof = None
+    rsv = _Reservation(ctl, lr, deep=False)
     cmd = None
     while cmd is None:
         if pin:
@@ -353,16 +430,7 @@ def _wait_command(pin: bool, ctl: str, lr: str, interval: float = 0.25) -> Optio
             if not pinned_marked and _pinned_bytes() > 0:
                 _mark(ctl, PINNED_PREFIX, lr, f"{_pinned_bytes()}\n")
                 pinned_marked = True
-            if prof is None:
-                prof = _apply_warm_profile(ctl, lr)
-                if prof is not None:
-                    if reserved >= 0:
-                        reserved = _reserve_state_memory(reserved, prof)
-                    _mark(ctl, WARM_PREFIX, lr, f"{reserved}\n")
-            if reserved == 0:
-                reserved = _reserve_state_memory()
-            else:
-                reserved = _release_under_pressure(reserved)
+            rsv.tick(replay_profile=True)
         r, _, _ = select.select([fd], [], [], interval)
         if r:
             chunk = os.read(fd, 1 << 20)

@@ -318,6 +318,18 @@ def _flush_deferred_state():
     flush_deferred_state()
 
 
+def device_free_bytes(device) -> int:
+    """HBM a new allocation of this process can get without growing its
+    footprint: the driver's free memory plus what the caching allocator
+    holds unused (a standby's reservation the worker grows into)."""
+    free, _total = torch.cuda.mem_get_info(device)
+    try:
+        cached = torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device)
+    except Exception:
+        cached = 0
+    return int(free) + max(0, int(cached))
+
+
 def _install_fence_hook():
     global _FENCED, _OPTIMIZERS
     if _FENCED is None:
@@ -445,12 +457,16 @@ class GpuCopier:
         Switching waits for in-flight flushes of the old buffers."""
         from . import hbm_tier
 
-        if os.environ.get("DWAMD_HBM_TIER", "1") != "1" or nbytes <= 0:
+        if nbytes <= 0:
             return
         cand, key = None, None
         own = [b for b in hbm_tier.OWNED if b.ptr and b.nbytes >= nbytes]
+        # tier off: no standby-published buffers, but this process's own
+        # (hbm_tier.reserve_private_staging while it was the standby) are its
+        # staging -- no fresh VRAM on the first saves after a restart
         info = hbm_tier.find_published(os.environ.get("DWAMD_AGENT_CTL_DIR", ""),
-                                       int(os.environ.get("LOCAL_RANK", "0")))
+                                       int(os.environ.get("LOCAL_RANK", "0"))) if (
+            os.environ.get("DWAMD_HBM_TIER", "1") == "1") else None
         if info is not None and int(info["nbytes"]) >= nbytes and len(info["handles"]) >= 2:
             if info["_key"] == self._ext_key:
                 return
@@ -502,7 +518,7 @@ class GpuCopier:
             from .hbm_budget import staging_buffers
 
             try:
-                free, _total = torch.cuda.mem_get_info(self.device)
+                free = device_free_bytes(self.device)
                 have = sum(t.numel() for t in self._stagings if t is not None)
                 nb = staging_buffers(free, have, nbytes, self.staging_reserve)
             except Exception:
@@ -805,7 +821,7 @@ class GpuCopier:
         self._refresh_external(n)
         if self._ext is None:
             try:
-                free, _total = torch.cuda.mem_get_info(self.device)
+                free = device_free_bytes(self.device)
                 have = sum(t.numel() for t in self._stagings if t is not None)
                 from .hbm_budget import use_ring
 
@@ -1029,18 +1045,31 @@ class GpuCopier:
         from .gather import all_gather_slices
         from .hbm_budget import gather_chunk
 
+        from . import hbm_tier
+
         per = hi - lo
         rank = dist.get_rank(gather_group)
-        try:
-            free, _t = torch.cuda.mem_get_info(self.device)
-        except Exception:
-            free = 0
         # the gather's temporary (never the staging buffers: with the HBM tier
         # they hold the checkpoint being restored) is bounded: world x c bytes
         # per round (hbm_budget.gather_chunk), the whole payload in one round
-        # when it fits
-        c = min(per, gather_chunk(per, world, free))
-        tmp = torch.empty(c * world, dtype=torch.uint8, device=self.device)
+        # when it fits.  A standby reserved it while parked
+        # (hbm_tier.reserve_restore_temp): no fresh VRAM on the restart path
+        tmp = hbm_tier.take_restore_temp()
+        want_idx = torch.device(self.device).index
+        if (tmp is not None and tmp.is_cuda and (want_idx is None or tmp.device.index == want_idx)
+                and tmp.numel() >= world * min(per, 64 << 20)):
+            c = min(per, tmp.numel() // world)
+            if c < per:
+                c = max(min(per, 64 << 20), c // (2 << 20) * (2 << 20))
+            self.last_restore_temp = "reserved"
+        else:
+            try:
+                free = device_free_bytes(self.device)
+            except Exception:
+                free = 0
+            c = min(per, gather_chunk(per, world, free))
+            tmp = torch.empty(c * world, dtype=torch.uint8, device=self.device)
+            self.last_restore_temp = "allocated"
         merged = _merge_pieces(pieces_gpu)
         self.last_restore_gather = {"rounds": -(-per // c) if per else 0, "chunk": c, "temp_bytes": c * world}
         for o in range(0, per, c):

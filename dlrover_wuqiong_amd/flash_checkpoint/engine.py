@@ -368,12 +368,19 @@ class CheckpointEngine(ABC):
         try:
             from .hbm_budget import plan
 
+            from . import copier as _cp
+
             dev = torch.cuda.current_device()
             _free, total = torch.cuda.mem_get_info(dev)
             state = int(torch.cuda.memory_allocated(dev))
+            # gradients a deferred optimizer-state write-back would keep (ring)
+            grad_bytes = sum(o.flat.grad.numel() * o.flat.grad.element_size() for o in list(_cp._OPTIMIZERS or ())
+                             if getattr(o, "_dsw_supported", lambda: False)() and getattr(o, "flat", None) is not None
+                             and o.flat.grad is not None)
             p = plan(total, worker_state=state, worker_peak=max(state, int(torch.cuda.max_memory_reserved(dev))),
                      payload=payload, world_local=self._num_slices if self._replicated else self._local_world,
-                     replicated=self._replicated, standby=os.environ.get("DWAMD_STANDBY_MODE", "import"))
+                     replicated=self._replicated, standby=os.environ.get("DWAMD_STANDBY_MODE", "import"),
+                     hbm_tier=os.environ.get("DWAMD_HBM_TIER", "1") == "1", grad_bytes=grad_bytes)
             self.hbm_plan = p.as_dict()
             logger.info(f"rank {self._rank}: HBM budget {self.hbm_plan}")
         except Exception as e:  # a log line must never fail a save

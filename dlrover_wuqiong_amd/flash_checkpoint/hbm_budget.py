@@ -11,11 +11,15 @@ node's local ranks, a sharded one is already per rank):
   ring of K chunks when not even one slice fits next to the worker;
 * the HBM tier (``hbm_tier.py``): the staging buffers are owned by the
   standby and outlive the worker -- no extra bytes, same buffers;
-* a deep standby: its own model + optimizer (it parks fully built);
-  an import standby: only what it reserves in its caching allocator for
-  the worker it will become (released under pressure, ``standby.py``);
+* a deep standby: its own model + optimizer (it parks fully built) plus
+  the rest of the worker's peak (activations) held in its caching
+  allocator; an import standby: the worker's peak in its caching allocator
+  (released under pressure, ``standby.py``).  With the HBM tier off the
+  standby also holds its own staging buffers (``standby_staging``): the
+  worker it becomes then allocates nothing on the restart path;
 * the replicated restore: the slice all-gather's temporary, bounded here
-  to ``world x chunk`` (chunked gather) instead of the whole payload.
+  to ``world x chunk`` (chunked gather) instead of the whole payload, and
+  reserved by the standby while it parks (``gather_temp_bytes``).
 
 Reference: the reference sizes nothing on the device -- its snapshot is a
 synchronous copy into pageable shm (``ckpt_saver.py:197-206``).
@@ -73,6 +77,8 @@ class HbmPlan:
     gather_chunk: int
     gather_temp_bytes: int
     restore_peak: int  # worker + staging + standby + the gather temporary
+    defer_steps: int  # ring staging: optimizer steps whose state write-back may be deferred (0: wait for the ring)
+    defer_bytes: int  # HBM of the kept gradients of those steps
     fits: bool
     notes: Dict[str, str] = field(default_factory=dict)
 
@@ -86,18 +92,26 @@ class HbmPlan:
 
 def plan(total: int, worker_state: int, worker_peak: int, payload: int, world_local: int, replicated: bool,
          standby: str = "import", ring_chunk: int = 1 << 30, ring_slots: int = 4,
-         reserve: Optional[int] = None, import_reserve: bool = True) -> HbmPlan:
+         reserve: Optional[int] = None, import_reserve: bool = True, hbm_tier: bool = True,
+         grad_bytes: int = 0) -> HbmPlan:
     """Decisions for ONE GPU of a node with ``world_local`` ranks.
 
     worker_state: model + optimizer bytes of a rank (what a deep standby
     also holds); worker_peak: the rank's peak footprint (state + activations);
     payload: the rank's checkpoint payload (the whole replicated state, or
-    this rank's shard)."""
+    this rank's shard); grad_bytes: the rank's gradient bytes (ring staging:
+    a deferred optimizer-state write-back keeps one copy of the deferred
+    elements' gradient per deferred step, optimizers/fused.py)."""
     notes = {}
     slice_bytes = -(-payload // world_local) if replicated else payload
     free_for_staging = total - worker_peak
+    world_g = world_local if replicated else 1
+    per = slice_bytes if replicated else payload
+    # the restore all-gather temporary a standby reserves (sized like the
+    # restore itself: copier.restore -> gather_chunk)
+    temp_reserved = gather_chunk(per, world_g, 1 << 62) * world_g if world_g > 1 else 0
     if standby == "deep":
-        sb_bytes = worker_state
+        sb_bytes = worker_peak + temp_reserved  # built state + activation peak + gather temporary
         if free_for_staging - sb_bytes < slice_bytes + (staging_reserve() if reserve is None else reserve):
             notes["standby"] = "deep standby does not fit next to the worker + one staging slice: import"
             standby, sb_bytes = "import", 0
@@ -110,24 +124,37 @@ def plan(total: int, worker_state: int, worker_peak: int, payload: int, world_lo
         staging, st_bytes = "double", 2 * slice_bytes
     else:
         staging, st_bytes = "single", slice_bytes
+    defer_k, defer_b = 0, 0
+    if staging == "ring" and grad_bytes > 0:
+        kcap = max(1, min(7, int(os.environ.get("DWAMD_DEFER_STATE_STEPS", "4"))))
+        # (the same 2 GiB margin as optimizers/fused.py _defer_budget)
+        room = total - worker_peak - st_bytes - (sb_bytes if standby == "deep" else 0) - 2 * GiB
+        defer_k = max(0, min(kcap, room // grad_bytes))
+        defer_b = defer_k * grad_bytes
+        notes["defer"] = (f"ring: state write-back deferred for up to {defer_k} steps ({defer_b / GiB:.1f} GiB of "
+                          f"kept gradients)" if defer_k else "ring: no room for a kept gradient; steps wait for the ring")
     if standby == "import" and import_reserve:
-        # the import standby caches about the worker's peak, bounded by what
-        # is left (it releases it when the worker's own use grows)
-        sb_bytes = max(0, min(worker_peak, total - worker_peak - st_bytes - 8 * GiB))
+        # the import standby caches about the worker's peak (+ the gather
+        # temporary), bounded by what is left (it releases it when the
+        # worker's own use grows); with the tier off it also holds its own
+        # staging buffers next to the live worker's
+        own_staging = 0 if (hbm_tier or staging == "ring") else st_bytes
+        sb_bytes = max(0, min(worker_peak + temp_reserved,
+                              total - worker_peak - st_bytes - own_staging - defer_b - 8 * GiB))
+        sb_bytes += own_staging
     # restore: a NEW worker (after the failure the old one is gone) rebuilds
-    # its state, then gathers; the standby's cache became that worker
-    world_g = world_local if replicated else 1
-    per = slice_bytes if replicated else payload
+    # its state, then gathers into the temporary its standby reserved
     free_at_restore = total - worker_state - st_bytes - (sb_bytes if standby == "deep" else 0)
-    ch = gather_chunk(per, world_g, free_at_restore) if world_g > 1 else per
+    ch = gather_chunk(per, world_g, free_at_restore + temp_reserved) if world_g > 1 else per
     temp = ch * world_g if world_g > 1 else 0
     if world_g > 1 and ch < per:
         notes["gather"] = f"restore gather chunked: {-(-per // ch)} rounds of {world_g} x {ch >> 20} MiB"
-    steady = worker_peak + st_bytes + sb_bytes
-    restore_peak = worker_state + st_bytes + (sb_bytes if standby == "deep" else 0) + temp
+    steady = worker_peak + st_bytes + sb_bytes + defer_b
+    # the recovered worker holds what its standby held (the temporary inside it)
+    restore_peak = max(worker_state + temp, sb_bytes) + st_bytes + (sb_bytes if standby == "deep" else 0)
     return HbmPlan(total=total, worker_peak=worker_peak, slice_bytes=slice_bytes, staging=staging,
                    staging_bytes=st_bytes, standby=standby, standby_bytes=sb_bytes, gather_chunk=ch,
-                   gather_temp_bytes=temp, restore_peak=restore_peak,
+                   gather_temp_bytes=temp, restore_peak=restore_peak, defer_steps=defer_k, defer_bytes=defer_b,
                    fits=steady <= total and restore_peak <= total, notes=notes)
 
 

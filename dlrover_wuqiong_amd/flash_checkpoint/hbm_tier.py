@@ -108,6 +108,26 @@ def _warm_restore_path():
         logger.warning(f"standby: restore-path warm-up failed: {e}")
 
 
+def _alloc_owned(nbytes: int, nbuf: int) -> bool:
+    for _ in range(nbuf):
+        p = ctypes.c_void_p(0)
+        err = _kern().dw_device_malloc(nbytes, ctypes.byref(p))
+        if err != 0:
+            logger.warning(f"standby: hipMalloc({nbytes}) failed ({err})")
+            release_owned()
+            return False
+        OWNED.append(HbmBuffer(int(p.value), nbytes, os.getpid(), owned=True))
+    return True
+
+
+def release_owned():
+    global _published_key
+    for b in OWNED:
+        b.release()
+    OWNED.clear()
+    _published_key = None
+
+
 def publish_standby_buffers(ctl_dir: str, local_rank: int, nbytes: int, nbuf: int = 2,
                             reserve: int = 24 << 30) -> bool:
     """Standby side: (re)allocate ``nbuf`` buffers of ``nbytes`` and publish
@@ -116,36 +136,23 @@ def publish_standby_buffers(ctl_dir: str, local_rank: int, nbytes: int, nbuf: in
     global _published_key
     if not ctl_dir or nbytes <= 0:
         return False
-    key = (nbytes, nbuf)
+    key = (nbytes, nbuf, True)
     if _published_key == key and OWNED:
         return True
-    for b in OWNED:
-        b.release()
-    OWNED.clear()
-    _published_key = None
+    release_owned()
     if _free_hbm() < nbuf * nbytes + reserve:
         logger.info(f"standby: not enough free HBM for {nbuf} x {nbytes} B checkpoint staging")
         return False
     hsz = _kern().dw_ipc_handle_size()
+    if not _alloc_owned(nbytes, nbuf):
+        return False
     handles = []
-    for _ in range(nbuf):
-        p = ctypes.c_void_p(0)
-        err = _kern().dw_device_malloc(nbytes, ctypes.byref(p))
-        if err != 0:
-            logger.warning(f"standby: hipMalloc({nbytes}) failed ({err})")
-            for b in OWNED:
-                b.release()
-            OWNED.clear()
-            return False
-        buf = HbmBuffer(int(p.value), nbytes, os.getpid(), owned=True)
-        OWNED.append(buf)
+    for buf in OWNED:
         h = ctypes.create_string_buffer(hsz)
         err = _kern().dw_ipc_get_handle(ctypes.c_void_p(buf.ptr), h)
         if err != 0:
             logger.warning(f"standby: hipIpcGetMemHandle failed ({err}); HBM tier disabled")
-            for b in OWNED:
-                b.release()
-            OWNED.clear()
+            release_owned()
             return False
         handles.append(h.raw.hex())
     info = {"pid": os.getpid(), "nbytes": nbytes, "handles": handles}
@@ -157,6 +164,73 @@ def publish_standby_buffers(ctl_dir: str, local_rank: int, nbytes: int, nbuf: in
     _warm_restore_path()
     logger.info(f"standby: published {nbuf} x {nbytes / 2**30:.1f} GiB HBM checkpoint staging buffers")
     return True
+
+
+def reserve_private_staging(nbytes: int, nbuf: int = 2, reserve: int = 24 << 30) -> bool:
+    """HBM tier off (``DWAMD_HBM_TIER=0``, the reference's restart
+    semantics): the standby still allocates the staging buffers that the
+    worker it becomes will snapshot into -- privately (no handles
+    published; the live worker keeps its own).  The first saves after a
+    restart then need no fresh VRAM: a hipMalloc of a 20 GB buffer next to a
+    killed process whose VRAM the driver is still tearing down stalled
+    0.5-3 s (BENCH_r05 ``import_mode.save_ms_after_restart`` 515, 491 ms).
+    The copier adopts them as its own staging (``copier._refresh_external``)."""
+    global _published_key
+    if nbytes <= 0:
+        return False
+    key = (nbytes, nbuf, False)
+    if _published_key == key and OWNED:
+        return True
+    release_owned()
+    if _free_hbm() < nbuf * nbytes + reserve:
+        logger.info(f"standby: not enough free HBM for {nbuf} x {nbytes} B private checkpoint staging")
+        return False
+    if not _alloc_owned(nbytes, nbuf):
+        return False
+    _published_key = key
+    _warm_restore_path()
+    logger.info(f"standby: reserved {nbuf} x {nbytes / 2**30:.1f} GiB HBM checkpoint staging (private)")
+    return True
+
+
+# ------------------------------------------------ restore-time reservations
+# The replicated restore's all-gather temporary (copier.restore, N > 1):
+# allocated by the standby while parked, handed to the restore, then freed
+# into the caching allocator (where the first step's activations reuse it).
+_RESTORE_TMP = None
+
+
+def reserve_restore_temp(nbytes: int, reserve: int = 24 << 30) -> int:
+    """Hold ``nbytes`` of HBM for the restore's gather temporary (bytes held)."""
+    global _RESTORE_TMP
+    if nbytes <= 0:
+        return 0
+    if _RESTORE_TMP is not None and _RESTORE_TMP.numel() >= nbytes:
+        return _RESTORE_TMP.numel()
+    import torch
+
+    _RESTORE_TMP = None
+    if _free_hbm() < nbytes + reserve:
+        return 0
+    _RESTORE_TMP = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    return nbytes
+
+
+def take_restore_temp():
+    """The reserved gather temporary (once), or None."""
+    global _RESTORE_TMP
+    t, _RESTORE_TMP = _RESTORE_TMP, None
+    return t
+
+
+def reserve_small_pool(mib: int = 128):
+    """Pre-fill the caching allocator's small-block pool (2 MiB segments for
+    allocations <= 1 MiB: descriptor tables, scalars, the first batch) so
+    the restart path allocates none of them from the driver."""
+    import torch
+
+    ts = [torch.empty(1 << 20, dtype=torch.uint8, device="cuda") for _ in range(max(1, mib))]
+    del ts
 
 
 def _alive(pid: int) -> bool:

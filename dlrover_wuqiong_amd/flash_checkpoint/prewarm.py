@@ -28,9 +28,11 @@ from .shm_handler import (_ADOPTABLE, DLROVER_CKPT_CONFIG_KEY, HEADER_BYTES, MAG
 _PINNED_BYTES: Dict[str, int] = {}
 _SLICE_BYTES: Dict[str, int] = {}  # segment -> this rank's slice bytes (layout known)
 _STATE_BYTES: Dict[str, int] = {}  # segment -> its whole payload (the state the worker rebuilds)
+_NSLICES: Dict[str, int] = {}  # segment -> slices of a replicated checkpoint (1: none)
 
 
-def _slot_ranges(shm: SharedMemory, shard: int, local_rank: int) -> Tuple[List[Tuple[int, int]], bool]:
+def _slot_ranges(shm: SharedMemory, shard: int, local_rank: int,
+                 nslices: Dict[str, int] = None) -> Tuple[List[Tuple[int, int]], bool]:
     """(addr, nbytes) of this rank's slice in every slot, and whether the
     slice layout is known (slot metadata written by a save)."""
     import numpy as np
@@ -49,6 +51,8 @@ def _slot_ranges(shm: SharedMemory, shard: int, local_rank: int) -> Tuple[List[T
         cfg = meta.get(DLROVER_CKPT_CONFIG_KEY)
         known = known or cfg is not None
         nsl = max(1, getattr(cfg, "num_slices", 1)) if cfg is not None else 1
+        if cfg is not None and nslices is not None:
+            nslices["nsl"] = nsl
         base = HEADER_BYTES + s * stride
         if nsl > 1:
             from .layout import split_ranges
@@ -80,6 +84,19 @@ def local_slice_bytes() -> int:
     return max(_SLICE_BYTES.values(), default=0)
 
 
+def restore_temp_bytes() -> int:
+    """HBM of the replicated restore's all-gather temporary on this rank
+    (``copier.restore``: world x per-round chunk; 0 without slices)."""
+    from .hbm_budget import GiB, gather_chunk
+
+    out = 0
+    for name, nsl in _NSLICES.items():
+        per = _SLICE_BYTES.get(name, 0)
+        if nsl > 1 and per > 0:
+            out = max(out, gather_chunk(per, nsl, free=1 << 62) * nsl)
+    return out
+
+
 def prepin_local_checkpoint_shm() -> float:
     """Returns seconds spent.  No-op (0.0) when no segment exists yet."""
     import torch
@@ -101,6 +118,7 @@ def prepin_local_checkpoint_shm() -> float:
             _PINNED_BYTES.pop(name, None)
             _SLICE_BYTES.pop(name, None)
             _STATE_BYTES.pop(name, None)
+            _NSLICES.pop(name, None)
             shm.close()
             shm = None
         if shm is None:
@@ -110,9 +128,11 @@ def prepin_local_checkpoint_shm() -> float:
                 shm = SharedMemory(name, create=False)
             except FileNotFoundError:
                 continue
-        ranges, known = _slot_ranges(shm, shard, lr)
+        info: Dict[str, int] = {}
+        ranges, known = _slot_ranges(shm, shard, lr, info)
         if known and ranges:
             _SLICE_BYTES[name] = ranges[0][1]
+            _NSLICES[name] = info.get("nsl", 1)
             import numpy as np
 
             _STATE_BYTES[name] = int(np.frombuffer(shm.buf, dtype=np.int64, count=2)[1])

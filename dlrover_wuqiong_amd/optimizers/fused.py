@@ -280,10 +280,17 @@ class _FlatOptimizer(torch.optim.Optimizer):
             if lo >= n:  # the state is fully copied; only parameters may still be in flight
                 c.ring_wait_ranges([(f.data.data_ptr(), f.data.data_ptr() + f.data.element_size() * n)])
                 return False
-            self._dsw = {"copier": c, "lo": lo, "steps": []}
+            kmax = self._defer_budget((n - lo) * f.grad.element_size())
+            if kmax < 1:
+                # not even one kept gradient fits next to the next step's
+                # activations: wait for the ring (the stall deferral avoids)
+                c.fence()
+                discard()
+                return False
+            self._dsw = {"copier": c, "lo": lo, "steps": [], "kmax": kmax}
             _DEFERRING.add(self)
         d = self._dsw
-        kmax = max(1, min(7, int(os.environ.get("DWAMD_DEFER_STATE_STEPS", "4"))))
+        kmax = d["kmax"]
         if len(d["steps"]) >= kmax:
             self.flush_deferred()  # waits for the ring (the stall this bounds)
             c.fence()
@@ -300,6 +307,40 @@ class _FlatOptimizer(torch.optim.Optimizer):
         self._dsw_replay(False, extra=step)  # new parameters from the snapshot's state + the kept steps
         d["steps"].append(step)
         return True
+
+    last_defer_plan = None
+
+    def _defer_budget(self, per_step: int) -> int:
+        """Deferred steps (K) whose kept gradients fit in HBM: each deferred
+        step keeps a copy of the deferred elements' gradient until the ring
+        drains.  Budget = free HBM (driver + the allocator's unused cache)
+        minus the next forward/backward's activation growth (this process's
+        peak minus what it holds now, measured at this optimizer step) minus
+        ``DWAMD_DEFER_RESERVE_GB`` (2).  K = min(DWAMD_DEFER_STATE_STEPS, 4
+        by default, budget // per-step bytes); 0 = wait for the ring.  The
+        plan is kept in ``last_defer_plan`` (and counted by
+        ``hbm_budget.plan``'s ``defer_bytes``)."""
+        import os
+
+        from ..flash_checkpoint.copier import device_free_bytes
+
+        kcap = max(1, min(7, int(os.environ.get("DWAMD_DEFER_STATE_STEPS", "4"))))
+        dev = self.flat.device
+        try:
+            free = device_free_bytes(dev)
+            growth = max(0, int(torch.cuda.max_memory_allocated(dev)) - int(torch.cuda.memory_allocated(dev)))
+        except Exception:
+            free, growth = 0, 0
+        margin = int(float(os.environ.get("DWAMD_DEFER_RESERVE_GB", "2")) * (1 << 30))
+        budget = free - growth - margin
+        k = max(0, min(kcap, budget // max(1, per_step + 64)))
+        self.last_defer_plan = {"steps": int(k), "per_step_bytes": int(per_step), "budget_bytes": int(budget),
+                                "free_bytes": int(free), "activation_growth_bytes": int(growth),
+                                "decision": "defer" if k >= 1 else "wait"}
+        from ..common.log import logger
+
+        logger.info(f"deferred optimizer-state write-back plan: {self.last_defer_plan}")
+        return int(k)
 
     def checkpoint_safe_tensors(self):
         """Tensors only ``step()`` writes (an overlapped flash-checkpoint

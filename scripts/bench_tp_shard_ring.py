@@ -207,7 +207,11 @@ def main():
         "fence_cost_ms": round(1000 * fence, 1) if after_save else None,
         "tokens_per_s": round(a.micro_batch * a.seq / med, 1), "load_sec": round(load_s, 3),
         "load_verified": bool(ok), "losses": [round(x, 3) for x in losses],
-        "optimizer": type(opt).__name__, "state_writeback_deferred_steps": deferred_steps}), flush=True)
+        "optimizer": type(opt).__name__, "state_writeback_deferred_steps": deferred_steps,
+        # the deferral's HBM plan (optimizers/fused.py _defer_budget) and the
+        # engine's per-GPU plan with the kept gradients counted (hbm_budget.plan)
+        "defer_plan": getattr(opt, "last_defer_plan", None), "hbm_plan": getattr(ck.engine, "hbm_plan", None),
+        "hbm_reserved_peak_gb": round(torch.cuda.max_memory_reserved() / gb, 1) if cuda else None}), flush=True)
     ck.close()
     prefix = f"dwamd_{os.environ['DWAMD_SHM_PREFIX']}"
     for f in os.listdir("/dev/shm"):  # ~250 GB of host memory: never leave it behind

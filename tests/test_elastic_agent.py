@@ -202,3 +202,33 @@ def test_no_standbys_once_the_restart_budget_is_spent():
     assert not ag._standbys_useful()  # single node, no restart left: a standby could never run
     ag.config = ElasticLaunchConfig(max_nodes=4)
     assert ag._standbys_useful()  # membership changes still restart the workers
+
+
+def test_standby_reserves_the_restart_path(monkeypatch, tmp_path):
+    """Deep standby: once the live worker's warm profile (its peak) exists,
+    the standby caches peak - (the model + optimizer it already built), fills
+    the small-block pool once and marks the reservation; an import standby
+    reserves the whole peak."""
+    import torch
+
+    from dlrover_wuqiong_amd.elastic_agent import standby, warm_profile
+    from dlrover_wuqiong_amd.flash_checkpoint import hbm_tier
+
+    GiB = 1 << 30
+    calls = {"small": 0, "empty": []}
+    monkeypatch.setattr(hbm_tier, "reserve_small_pool", lambda: calls.__setitem__("small", calls["small"] + 1))
+    monkeypatch.setattr(torch.cuda, "memory_allocated", lambda *a: 25 * GiB)
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda *a: (200 * GiB, 288 * GiB))
+    monkeypatch.setattr(torch, "empty", lambda n, **k: calls["empty"].append(n))
+    prof = {"max_reserved": 45 * GiB}
+    monkeypatch.setattr(warm_profile, "load", lambda ctl, lr: prof)
+    r = standby._Reservation(str(tmp_path), "0", deep=True)
+    r.tick()
+    r.tick()
+    assert calls["small"] == 1 and calls["empty"] == [20 * GiB] and r.reserved == 20 * GiB
+    assert (tmp_path / "standby_reserved.0").read_text().strip() == str(20 * GiB)
+    monkeypatch.setattr(standby, "_apply_warm_profile", lambda ctl, lr: prof)
+    calls["empty"].clear()
+    r = standby._Reservation(str(tmp_path), "1", deep=False)
+    r.tick(replay_profile=True)
+    assert calls["empty"] == [45 * GiB]

@@ -88,6 +88,55 @@ def test_copier_decisions_follow_the_budget(monkeypatch):
     assert c._use_ring(30 * GiB) is hb.use_ring(40 * GiB, 0, 30 * GiB, 24 * GiB) is True
 
 
+def test_copier_counts_the_allocator_cache_as_free(monkeypatch):
+    """A recovered import worker holds its standby's reservation in the
+    caching allocator: the driver reports little free HBM, but the staging
+    decision must count the cached blocks (else it picks one buffer or the
+    ring and every later save waits on the flush)."""
+    from dlrover_wuqiong_amd.flash_checkpoint.copier import GpuCopier, device_free_bytes
+
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda *a: (10 * GiB, HBM))
+    monkeypatch.setattr(torch.cuda, "memory_reserved", lambda *a: 130 * GiB)
+    monkeypatch.setattr(torch.cuda, "memory_allocated", lambda *a: 40 * GiB)
+    assert device_free_bytes("cuda") == 100 * GiB
+    c = GpuCopier.__new__(GpuCopier)
+    c.device, c._stagings, c._nbuf, c.staging_reserve = "cuda", [None, None], 0, 24 * GiB
+    c._decide_buffers(30 * GiB)
+    assert c._nbuf == 2
+    c.staging_mode, c._ring_decision, c._ext = "auto", None, None
+    c.ring_slots, c.ring_chunk, c.ring_hbm, c._ring_auto = 4, GiB, 0, 0
+    c.wait = lambda: None
+    c._refresh_external = lambda n: None
+    assert c._use_ring(30 * GiB) is False
+
+
+def test_n8_restart_allocation_plan():
+    """GPT2-1.5B DDP on 8 GPUs (replicated 21.8 GB state, 1/8 slices): every
+    byte the restart path needs is held by the standby -- the gather
+    temporary it reserves equals what copier.restore would allocate, and the
+    plan fits next to the live worker on a 288 GB card, tier on and off."""
+    from dlrover_wuqiong_amd.flash_checkpoint import prewarm
+
+    payload = int(21.8 * GiB)
+    state, peak = int(24.9 * GiB), int(45.5 * GiB)
+    per = -(-payload // 8)
+    for standby in ("deep", "import"):
+        for tier in (True, False):
+            p = hb.plan(HBM, worker_state=state, worker_peak=peak, payload=payload, world_local=8, replicated=True,
+                        standby=standby, hbm_tier=tier)
+            assert p.fits and p.staging == "double", (standby, tier, p)
+            assert p.gather_temp_bytes == hb.gather_chunk(per, 8, 1 << 62) * 8 <= 16 * GiB + 8 * (2 << 20)
+            assert p.standby_bytes >= p.gather_temp_bytes
+            if standby == "import" and not tier:
+                assert p.standby_bytes >= 2 * per  # its own staging buffers
+    # what the parked standby reserves (prewarm.restore_temp_bytes) is that temporary
+    prewarm._SLICE_BYTES["seg"], prewarm._NSLICES["seg"] = per, 8
+    try:
+        assert prewarm.restore_temp_bytes() == p.gather_temp_bytes
+    finally:
+        prewarm._SLICE_BYTES.pop("seg"), prewarm._NSLICES.pop("seg")
+
+
 @pytest.mark.parametrize("per,world,chunk", [(1000, 4, 1000), (1000, 4, 256), (999, 3, 100)])
 def test_chunked_gather_scatter_plan_covers_payload(per, world, chunk):
     """The restore's per-round scatter descriptors (copier.restore) place
@@ -195,3 +244,38 @@ def test_engine_creates_one_slot_segment_when_two_do_not_fit(tmp_path, monkeypat
         ck2.save_checkpoint(5, {"model": big.state_dict(), "step": 5}, storage_type=StorageType.MEMORY)
     ck2.close()
     del eng_mod
+
+
+def test_deferred_write_back_budget_70b_tp8(monkeypatch):
+    """Llama-3-70B TP=8 shard (8.8e9 elements: bf16 params + fp32 master +
+    Adam = 123.5 GB, bf16 gradient 17.6 GB) on a ring: the plan counts the
+    kept gradients of the deferred steps, and the optimizer picks K from the
+    free HBM at ring time -- the full 4 with room, fewer when tight, 0
+    (wait for the ring) when not even one kept gradient fits."""
+    import torch.nn as nn
+
+    from dlrover_wuqiong_amd.flash_checkpoint import copier as cp
+    from dlrover_wuqiong_amd.optimizers.fused import FusedAdamW
+    from dlrover_wuqiong_amd.parallel.flat import FlatParams
+
+    elems = int(8.8e9)
+    grad = 2 * elems
+    state = elems * (2 + 4 + 4 + 4) + grad
+    p = hb.plan(HBM, worker_state=state, worker_peak=state + 30 * GiB, payload=elems * 14, world_local=8,
+                replicated=False, standby="import", grad_bytes=grad, ring_chunk=GiB, ring_slots=64)
+    assert p.staging == "ring" and p.defer_steps >= 1 and p.defer_bytes == p.defer_steps * grad
+    assert "defer" in p.notes
+    tight = hb.plan(HBM, worker_state=state, worker_peak=HBM - 65 * GiB, payload=elems * 14, world_local=8,
+                    replicated=False, standby="import", grad_bytes=grad, ring_chunk=GiB, ring_slots=64)
+    assert tight.staging == "ring" and tight.defer_steps == 0 and "wait" in tight.notes["defer"]
+
+    opt = FusedAdamW(FlatParams(nn.Linear(8, 8)), lr=1e-3)
+    per_step = grad  # the whole shard's gradient still unstaged (worst case)
+    growth = 20 * GiB
+    monkeypatch.setattr(torch.cuda, "max_memory_allocated", lambda *a: 150 * GiB + growth)
+    monkeypatch.setattr(torch.cuda, "memory_allocated", lambda *a: 150 * GiB)
+    for free, want in ((120 * GiB, 4), (60 * GiB, 2), (30 * GiB, 0)):
+        monkeypatch.setattr(cp, "device_free_bytes", lambda d, f=free: f)
+        k = opt._defer_budget(per_step)
+        assert k == want == opt.last_defer_plan["steps"], (free, k, opt.last_defer_plan)
+        assert opt.last_defer_plan["decision"] == ("defer" if want else "wait")
