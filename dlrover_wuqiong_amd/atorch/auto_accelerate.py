@@ -647,6 +647,10 @@ def _apply_fsdp(ctx, cfg, reshard=True):
         mesh = DeviceMesh("cuda" if torch.cuda.is_available() else "cpu", ranks, mesh_dim_names=("data",))
     model = ctx["model"]
     cfgd = dict(cfg) if isinstance(cfg, dict) else {}
+    if cfgd.get("optim_in_backward"):
+        # each unit's optimizer update from its post-backward reduce-scatter,
+        # on a side stream under the rest of the backward (optimizers/in_backward.py)
+        ctx["optim_in_backward"] = True
     # meta-device model (init_empty_weights / torch.device("meta")): shard
     # first, then materialise only this rank's shards (atorch/meta_init.py)
     from . import meta_init
@@ -917,6 +921,11 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
                                  cpu_offload=lcfg.get("outer_optim_cpu_offload", False))
             logger.info(f"fsdp: local SGD over the replicate dimension (sync every "
                         f"{optim.sync_interval} steps after {optim.warmup_steps} warm-up steps)")
+    if ctx.get("optim_in_backward") and optim is not None:
+        from ..optimizers.in_backward import install
+
+        if install(model, optim) is not None:
+            logger.info("fsdp: optimizer update per FSDP unit inside the backward")
     if ctx.get("moe_ddp") is not None and optim is not None:
         ctx["moe_ddp"].attach_optimizer(getattr(optim, "optimizer", optim))
     if ctx.get("fp8") and optim is not None:

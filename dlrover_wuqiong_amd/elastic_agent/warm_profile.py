@@ -143,7 +143,9 @@ def _write(rec, t0: float):
             "gemm_calls": rec.calls, "gemms": list(rec.seen.values()), "ops": list(rec.other.values()),
             "max_reserved": int(torch.cuda.max_memory_reserved(dev)),
             "reserved": int(torch.cuda.memory_reserved(dev)),
-            "max_allocated": int(torch.cuda.max_memory_allocated(dev))}
+            "max_allocated": int(torch.cuda.max_memory_allocated(dev)),
+            # checkpoint staging inside max_reserved (the standby holds its own)
+            "staging_reserved": int(_state.get("staging", 0))}
     path = profile_path(ctl, lr)
     with open(path + ".tmp", "w") as f:
         json.dump(prof, f)
@@ -179,11 +181,14 @@ def _top_mode():
     return _get_current_dispatch_mode()
 
 
-def on_save():
+def on_save(staging_bytes: int = 0):
     """Called by the checkpoint engine after every flash save (training
-    thread): the first save arms the recorder for the next optimizer step."""
+    thread): the first save arms the recorder for the next optimizer step.
+    ``staging_bytes``: snapshot staging the caching allocator holds for the
+    copier (subtracted from the recorded footprint)."""
     if _state["done"] or not _enabled():
         return
+    _state["staging"] = max(int(staging_bytes), int(_state.get("staging", 0)))
     import torch
 
     if not torch.cuda.is_available():
@@ -293,7 +298,7 @@ def reserve_bytes(prof: Optional[dict], state_bytes: int, factor: float = 1.25) 
     """Bytes the standby should hold in its caching allocator: the worker's
     recorded peak footprint, else ~its checkpoint payload (model + optimizer)."""
     if prof and prof.get("max_reserved"):
-        return int(prof["max_reserved"])
+        return max(0, int(prof["max_reserved"]) - int(prof.get("staging_reserved", 0)))
     return int(state_bytes * factor)
 
 

@@ -477,7 +477,11 @@ class CheckpointEngine(ABC):
             # import-mode standby to replay (elastic_agent/warm_profile.py)
             from ..elastic_agent import warm_profile
 
-            warm_profile.on_save()
+            # (the snapshot staging this process allocated is not part of
+            # the footprint a standby reserves: it holds its own staging)
+            c = self._copier
+            warm_profile.on_save(sum(t.numel() for t in c._stagings if isinstance(t, torch.Tensor))
+                                 if c is not None else 0)
 
     def _skip_busy(self) -> bool:
         """Reference semantics (a save is skipped while the previous one is

@@ -91,8 +91,8 @@ class _MultiTensorOptimizer(torch.optim.Optimizer):
         self.last_grad_norm = None
         self._step_t = torch.zeros((), dtype=torch.float32)  # shared by every param's state["step"]
         self._master_weights = master_weights
-        self._cache_key = None
-        self._tables = None
+        self._table_cache = {}  # slot -> (key, tables): the whole step, or per FSDP unit (in_backward.py)
+        self._in_backward = None
         self._build_state()
 
     # ------------------------------------------------------------ state
@@ -192,6 +192,10 @@ class _MultiTensorOptimizer(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        ib = self._in_backward
+        if ib is not None and ib.owns_step():
+            ib.finish()  # the backward ran this step's update per FSDP unit (optimizers/in_backward.py)
+            return loss
         self._step_t += 1
         live = [(gi, p) for gi, g in enumerate(self.param_groups) for p in g["params"] if p.grad is not None]
         if not live:
@@ -203,10 +207,11 @@ class _MultiTensorOptimizer(torch.optim.Optimizer):
         return loss
 
     # ---- GPU: one multi-tensor launch (+ two tiny ones when clipping)
-    def _tables_for(self, live):
+    def _tables_for(self, live, slot=None):
         key = tuple((gi, _local(p.grad).data_ptr(), _local(p).data_ptr()) for gi, p in live)
-        if key == self._cache_key:
-            return self._tables
+        hit = self._table_cache.get(slot)
+        if hit is not None and hit[0] == key:
+            return hit[1]
         L = _hip.lib()
         chunk = int(L.dw_mt_chunk())
         desc = np.zeros(len(live), dtype=_DESC)
@@ -237,13 +242,13 @@ class _MultiTensorOptimizer(torch.optim.Optimizer):
         d_chunks = torch.from_numpy(np.ascontiguousarray(ch).view(np.uint8).reshape(-1)).pin_memory().to(
             dev, non_blocking=True)
         sharded = any(_is_dtensor(p) for _gi, p in live)
-        self._tables = (d_desc, d_chunks, len(ch), sharded)
-        self._cache_key = key
-        return self._tables
+        tables = (d_desc, d_chunks, len(ch), sharded)
+        self._table_cache[slot] = (key, tables)
+        return tables
 
-    def _cuda_step(self, live):
+    def _cuda_step(self, live, slot=None):
         L = _hip.lib()
-        d_desc, d_chunks, nchunks, sharded = self._tables_for(live)
+        d_desc, d_chunks, nchunks, sharded = self._tables_for(live, slot)
         dev = d_desc.device
         gs = None
         if self.max_grad_norm > 0 or self.grad_scale != 1.0:

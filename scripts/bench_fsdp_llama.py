@@ -40,6 +40,9 @@ def main():
                         "parameters stay resident from forward to backward (16 GB for 8B on a 288 GB card), "
                         "no second all-gather per layer")
     p.add_argument("--torch-optim", action="store_true", help="keep torch.optim.AdamW (no multi-tensor HIP kernel)")
+    p.add_argument("--optim-in-backward", action="store_true",
+                   help="each FSDP unit's AdamW update from its post-backward reduce-scatter on a side stream "
+                        "(optimizers/in_backward.py)")
     p.add_argument("--no-ckpt", action="store_true", help="step time only (no flash checkpoints)")
     p.add_argument("--fp8", action="store_true", help="auto_accelerate 'fp8' on the decoder layers' projections")
     p.add_argument("--storage", action="store_true",
@@ -83,7 +86,8 @@ def main():
     ok, res, strategy = auto_accelerate(
         model, torch.optim.AdamW, optim_args={"lr": 2e-5, "betas": (0.9, 0.95), "weight_decay": 0.1},
         load_strategy=["module_replace", prec] + ([("fp8", {"include": ("layers", "h.")})] if a.fp8 else []) + [
-                       ("fsdp" if a.reshard == "on" else "zero2", {"wrap_cls": (layer_cls,)})]
+                       ("fsdp" if a.reshard == "on" else "zero2",
+                        {"wrap_cls": (layer_cls,), "optim_in_backward": a.optim_in_backward})]
         + ([("checkpoint", {"wrap_cls": (layer_cls,)})] if a.act_ckpt == "on" else []),
         fused_optimizer=not a.torch_optim)
     assert ok, "auto_accelerate failed"
@@ -122,6 +126,7 @@ def main():
         if rank == 0:
             print(json.dumps({"metric": "fsdp train step", "n_gpus": world, "model": a.model, "seq_len": a.seq,
                               "precision": a.precision + ("+fp8" if a.fp8 else ""), "optimizer": type(opt).__name__,
+                              "optim_in_backward": getattr(opt, "_in_backward", None) is not None,
                               "act_ckpt": a.act_ckpt, "reshard_after_forward": a.reshard == "on", "train_step_ms": round(1000 * med, 1),
                               "tokens_per_s": round(world * a.micro_batch * a.seq / med, 1),
                               "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if cuda else None,
