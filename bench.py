@@ -560,7 +560,7 @@ def worker(a) -> int:
     import torch
     import torch.distributed as dist
 
-    from dlrover_wuqiong_amd.trainer.elastic import standby_point
+    from dlrover_wuqiong_amd.trainer.elastic import standby_point, training_stream
 
     lr = int(os.environ.get("LOCAL_RANK", "0"))
     cuda = torch.cuda.is_available()
@@ -572,8 +572,9 @@ def worker(a) -> int:
     cdev = device if backend == "nccl" else torch.device("cpu")  # small control tensors
     if cuda:
         torch.cuda.set_device(device)
-        # train on a dedicated non-blocking stream (not the legacy null stream)
-        torch.cuda.set_stream(torch.cuda.Stream(device))
+        # train on a dedicated non-blocking stream (not the legacy null stream);
+        # an import standby's (its HBM reservation is cached for that stream)
+        torch.cuda.set_stream(training_stream(device))
 
     from dlrover_wuqiong_amd.common.constants import CheckpointConstant
     from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType

@@ -415,14 +415,25 @@ __global__ void __launch_bounds__(256) norm_bwd_fused_kernel(
 // computing the current one
 #define DWAMD_NORM_BWD_PF 2
 #endif
+#ifndef DWAMD_NORM_BWD_W2
+// A/B: the VPL = 4 instance (H 1025..2047) with ONE row register set and the
+// per-lane column sums kept in registers, compiled for two waves per SIMD
+// (<= 256 registers): the second wave hides the row loads the prefetch set
+// hid before, and twice the workgroups are resident (512)
+#define DWAMD_NORM_BWD_W2 0
+#endif
 
 template <int VPL, bool RMS, bool DS = false>
-__global__ void __launch_bounds__(256, (DWAMD_NORM_BWD_LDSACC && VPL == 4) ? 2 : 1) norm_bwd_part_kernel(
+__global__ void __launch_bounds__(256, ((DWAMD_NORM_BWD_LDSACC || DWAMD_NORM_BWD_W2) && VPL == 4) ? 2 : 1)
+norm_bwd_part_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ gamma,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const bf16_t* __restrict__ dres,
     bf16_t* __restrict__ dx, float* __restrict__ part, int64_t rows, int H) {
   static_assert(VPL <= 4, "small-H norm backward");
   constexpr bool LA = DWAMD_NORM_BWD_LDSACC != 0;
+  // two waves per SIMD: gamma re-read per row (L1-resident) and the residual
+  // gradient loaded where it is added, not held across the row reductions
+  constexpr bool W2 = DWAMD_NORM_BWD_W2 && VPL == 4 && !LA;
   constexpr int NVP = 64 * VPL;  // vectors per row, padded
   __shared__ float red[LA ? 1 : 2][LA ? 1 : 4][LA ? 1 : 512 + 4];
   __shared__ float lacc[LA ? (DS ? 3 : 2) : 1][LA ? 8 * NVP : 1];  // [array][k * NVP + vector]
@@ -438,18 +449,24 @@ __global__ void __launch_bounds__(256, (DWAMD_NORM_BWD_LDSACC && VPL == 4) ? 2 :
 #pragma unroll
       for (int k = 0; k < 8; ++k) ag[j][k] = ab[j][k] = ad[j][k] = 0.f;
   }
-  u32x4 gv[VPL];
+  u32x4 gv[W2 ? 1 : VPL];
+  if constexpr (!W2) {
 #pragma unroll
-  for (int j = 0; j < VPL; ++j) {
-    const int c = lane + 64 * j;
-    if (c < nv) gv[j] = *(const u32x4*)(gamma + c * 8);
+    for (int j = 0; j < VPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nv) gv[j] = *(const u32x4*)(gamma + c * 8);
+    }
   }
+  auto gam = [&](int j, int c) -> u32x4 {
+    if constexpr (W2) return *(const u32x4*)(gamma + c * 8);
+    else return gv[j];
+  };
   // grid-stride over rows, one row per wave per step, the next row's x / dy
   // / dres (and mean / rstd) loaded before the current one is computed: two
   // named register sets, the loop unrolled by two so nothing is copied
   const int64_t stride = (int64_t)gridDim.x * 4;
   struct Row {
-    u32x4 x[VPL], d[VPL], r[VPL];
+    u32x4 x[VPL], d[VPL], r[W2 ? 1 : VPL];
     float mu, rs;
   };
   auto load = [&](Row& b, int64_t row) {
@@ -460,7 +477,8 @@ __global__ void __launch_bounds__(256, (DWAMD_NORM_BWD_LDSACC && VPL == 4) ? 2 :
       if (c < nv) {
         b.x[j] = *(const u32x4*)(x + row * H + c * 8);
         b.d[j] = *(const u32x4*)(dy + row * H + c * 8);
-        if (dres) b.r[j] = *(const u32x4*)(dres + row * H + c * 8);
+        if constexpr (!W2)
+          if (dres) b.r[j] = *(const u32x4*)(dres + row * H + c * 8);
       }
     }
     b.mu = RMS ? 0.f : mean_in[row];
@@ -475,7 +493,7 @@ __global__ void __launch_bounds__(256, (DWAMD_NORM_BWD_LDSACC && VPL == 4) ? 2 :
         float xf[8], df[8], gm[8];
         unpack8(b.x[j], xf);
         unpack8(b.d[j], df);
-        unpack8(gv[j], gm);
+        unpack8(gam(j, c), gm);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float a = (xf[k] - b.mu) * b.rs, g = df[k] * gm[k];
@@ -498,14 +516,18 @@ __global__ void __launch_bounds__(256, (DWAMD_NORM_BWD_LDSACC && VPL == 4) ? 2 :
       const int c = lane + 64 * j;
       if (c < nv) {
         float xf[8], df[8], gm[8], o[8];
+        u32x4 rv;
+        if constexpr (W2)
+          if (dres) rv = *(const u32x4*)(dres + row * H + c * 8);
         unpack8(b.x[j], xf);  // recomputed: cheaper than 64 more live registers
         unpack8(b.d[j], df);
-        unpack8(gv[j], gm);
+        unpack8(gam(j, c), gm);
 #pragma unroll
         for (int k = 0; k < 8; ++k) o[k] = b.rs * (df[k] * gm[k] - m1 - (xf[k] - b.mu) * b.rs * m2);
         if (dres) {
           float r[8];
-          unpack8(b.r[j], r);
+          if constexpr (W2) unpack8(rv, r);
+          else unpack8(b.r[W2 ? 0 : j], r);
 #pragma unroll
           for (int k = 0; k < 8; ++k) o[k] += r[k];
         }
@@ -523,7 +545,7 @@ __global__ void __launch_bounds__(256, (DWAMD_NORM_BWD_LDSACC && VPL == 4) ? 2 :
     }
   };
   int64_t row = (int64_t)blockIdx.x * 4 + wid;
-  if constexpr (LA) {
+  if constexpr (LA || (DWAMD_NORM_BWD_W2 && VPL == 4)) {
     // more waves per SIMD instead of a second register set: one row in flight per wave
     Row A;
     for (; row < rows; row += stride) {
@@ -815,7 +837,8 @@ extern "C" int dw_norm_bwd3(const void* dy, const void* x, const void* gamma, co
   accumulate &= 1;
   // every workgroup resident at once, each wave striding over rows: H > 1024
   // (VPL 4) needs ~310-370 VGPRs, one workgroup per CU; smaller H two
-  const int64_t nb = std::min<int64_t>((rows + 3) / 4, (H > 1024 && !DWAMD_NORM_BWD_LDSACC) ? 256 : 512);
+  const int64_t nb = std::min<int64_t>((rows + 3) / 4,
+                                       (H > 1024 && !DWAMD_NORM_BWD_LDSACC && !DWAMD_NORM_BWD_W2) ? 256 : 512);
   const int pw = dsum ? 3 : 2;
   if (dsum_done) *dsum_done = 0;
   static const bool off = getenv_flag("DWAMD_NORM_BWD_PART_OFF");  // A/B switch

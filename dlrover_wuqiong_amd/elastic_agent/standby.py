@@ -55,6 +55,7 @@ SPEC_ENV = "DWAMD_STANDBY_SPEC"
 READY_PREFIX = "standby_ready."
 
 _activated: Optional[dict] = None
+_STREAM = None  # import standby: the stream its HBM reservation belongs to (the worker's current stream)
 
 
 def is_standby() -> bool:
@@ -232,6 +233,12 @@ def _control_lines(buf: bytes, ctl: str, lr: str):
     return buf, None
 
 
+def reserved_stream():
+    """The stream an import standby made current (its reservation's stream),
+    else None."""
+    return _STREAM
+
+
 def activation_info() -> Optional[dict]:
     return dict(_activated) if _activated else None
 
@@ -253,6 +260,16 @@ def _gpu_init(lr: str) -> bool:
         if not torch.cuda.is_available():
             return False
         torch.cuda.set_device(int(lr) % max(1, torch.cuda.device_count()))
+        # PyTorch's caching allocator reuses a freed block only for the
+        # stream it was allocated on: everything this standby reserves for the
+        # worker it becomes is allocated on ONE non-blocking stream, which
+        # stays the current stream when the script runs (a script that keeps
+        # the current stream -- or asks dlrover_wuqiong_amd.trainer.elastic.
+        # training_stream() -- allocates from the reservation; one that
+        # switches to a stream of its own allocates from the driver)
+        global _STREAM
+        _STREAM = torch.cuda.Stream()
+        torch.cuda.set_stream(_STREAM)
         x = torch.ones(64, 64, device="cuda", dtype=torch.bfloat16)
         (x @ x).float().sum().item()  # BLAS handle + a first kernel launch
         from .._native import kernels

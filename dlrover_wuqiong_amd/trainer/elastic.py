@@ -65,6 +65,19 @@ def standby_point(prepin_shm: bool = True):
     return _sp(prepin_shm=prepin_shm)
 
 
+def training_stream(device=None) -> "torch.cuda.Stream":
+    """The stream to train on: the current stream when it is not the
+    device's default one (an import standby made the stream its HBM
+    reservation belongs to current -- allocations on it reuse the
+    reservation instead of asking the driver for fresh VRAM right after a
+    restart), else a new non-blocking stream.  Callers set it current."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    cur = torch.cuda.current_stream(dev)
+    if cur != torch.cuda.default_stream(dev):
+        return cur
+    return torch.cuda.Stream(dev)
+
+
 @dataclass
 class GradientState:
     num_steps: int = 0

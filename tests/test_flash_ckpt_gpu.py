@@ -673,8 +673,8 @@ def test_gpu_adam_replay_matches_flat_updates():
     opt.max_grad_norm = 1.0
     g = torch.Generator(device="cpu").manual_seed(3)
     with torch.no_grad():
-        w.copy_(0.02 * torch.randn(flat.numel, generator=g))
-        flat.data.copy_(w.to(flat.data.dtype))
+        opt.master.copy_(0.02 * torch.randn(flat.numel, generator=g))
+        flat.data.copy_(opt.master.to(flat.data.dtype))
         opt.exp_avg.copy_(1e-3 * torch.randn(flat.numel, generator=g))
         opt.exp_avg_sq.copy_(1e-6 * torch.rand(flat.numel, generator=g))
     s0 = [t.clone() for t in (flat.data, opt.exp_avg, opt.exp_avg_sq, opt.master)]
