@@ -380,7 +380,9 @@ class CheckpointEngine(ABC):
             p = plan(total, worker_state=state, worker_peak=max(state, int(torch.cuda.max_memory_reserved(dev))),
                      payload=payload, world_local=self._num_slices if self._replicated else self._local_world,
                      replicated=self._replicated, standby=os.environ.get("DWAMD_STANDBY_MODE", "import"),
-                     hbm_tier=os.environ.get("DWAMD_HBM_TIER", "1") == "1", grad_bytes=grad_bytes)
+                     hbm_tier=os.environ.get("DWAMD_HBM_TIER", "1") == "1", grad_bytes=grad_bytes,
+                     staging_mode=os.environ.get("DWAMD_STAGING", "auto"),
+                     ring_bytes=int(float(os.environ.get("DWAMD_RING_HBM_GB", "0")) * (1 << 30)))
             self.hbm_plan = p.as_dict()
             logger.info(f"rank {self._rank}: HBM budget {self.hbm_plan}")
         except Exception as e:  # a log line must never fail a save

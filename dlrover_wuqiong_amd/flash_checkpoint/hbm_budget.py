@@ -93,7 +93,7 @@ class HbmPlan:
 def plan(total: int, worker_state: int, worker_peak: int, payload: int, world_local: int, replicated: bool,
          standby: str = "import", ring_chunk: int = 1 << 30, ring_slots: int = 4,
          reserve: Optional[int] = None, import_reserve: bool = True, hbm_tier: bool = True,
-         grad_bytes: int = 0) -> HbmPlan:
+         grad_bytes: int = 0, staging_mode: str = "auto", ring_bytes: int = 0) -> HbmPlan:
     """Decisions for ONE GPU of a node with ``world_local`` ranks.
 
     worker_state: model + optimizer bytes of a rank (what a deep standby
@@ -118,8 +118,9 @@ def plan(total: int, worker_state: int, worker_peak: int, payload: int, world_lo
     else:
         sb_bytes = 0
     free_for_staging -= sb_bytes
-    if use_ring(free_for_staging, 0, slice_bytes, reserve):
-        staging, st_bytes = "ring", min(ring_slots * ring_chunk, max(0, free_for_staging))
+    if staging_mode == "ring" or (staging_mode != "full" and use_ring(free_for_staging, 0, slice_bytes, reserve)):
+        # (copier._ring_shape: DWAMD_RING_HBM_GB when set, else K x C)
+        staging, st_bytes = "ring", min(ring_bytes or ring_slots * ring_chunk, max(0, free_for_staging))
     elif staging_buffers(free_for_staging, 0, slice_bytes, reserve) == 2:
         staging, st_bytes = "double", 2 * slice_bytes
     else:
