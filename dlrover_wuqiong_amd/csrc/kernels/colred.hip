@@ -418,9 +418,12 @@ __global__ void __launch_bounds__(256) norm_bwd_fused_kernel(
 #ifndef DWAMD_NORM_BWD_W2
 // A/B: the VPL = 4 instance (H 1025..2047) with ONE row register set and the
 // per-lane column sums kept in registers, compiled for two waves per SIMD
-// (<= 256 registers): the second wave hides the row loads the prefetch set
-// hid before, and twice the workgroups are resident (512)
-#define DWAMD_NORM_BWD_W2 0
+// (<= 256 registers; gamma re-read per row, the residual gradient loaded
+// where it is added): the second wave hides the row loads the prefetch set
+// hid before, and twice the workgroups are resident (512).  GPT2-1.5B's call
+// (H = 1600, dres + dx column sums): 39.0 -> 36.9 us at 8192 rows, 62.0 ->
+// 56.1 us at 16384 (profiles/r6/norm_bwd_w2_ab.jsonl); 0: the prefetch form
+#define DWAMD_NORM_BWD_W2 1
 #endif
 
 template <int VPL, bool RMS, bool DS = false>
