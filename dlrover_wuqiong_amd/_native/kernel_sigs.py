@@ -65,6 +65,7 @@ SIGS = {
     "dw_scale_flat": (i32, [vp, i32, i64, vp, vp]),
     # optim_multi.hip
     "dw_mt_adam": (i32, [vp, vp, i64, vp, vp, i32, vp]),
+    "dw_mt_adam_grid": (i32, [vp, vp, i64, vp, vp, i32, i32, vp]),
     "dw_mt_sumsq": (i32, [vp, vp, i64, vp, vp, vp]),
     "dw_mt_hyper_size": (i32, []),
     "dw_mt_chunk": (i32, []),

@@ -189,18 +189,28 @@ static int mt_grid(int64_t nchunks) {
   return (int)(g < 1 ? 1 : g);
 }
 
-extern "C" int dw_mt_adam(const void* descs, const void* chunks, int64_t nchunks, const void* gscale,
-                          const void* hyper, int agd, void* stream) {
+// max_blocks > 0 caps the grid: an update running beside other work (the
+// optimizer inside the FSDP backward, optimizers/in_backward.py) then holds
+// at most that many workgroups' worth of CUs at a time
+extern "C" int dw_mt_adam_grid(const void* descs, const void* chunks, int64_t nchunks, const void* gscale,
+                               const void* hyper, int agd, int max_blocks, void* stream) {
   if (nchunks <= 0) return 0;
   const MTHyper h = *(const MTHyper*)hyper;
   hipStream_t s = (hipStream_t)stream;
+  int g = mt_grid(nchunks);
+  if (max_blocks > 0 && g > max_blocks) g = max_blocks;
   if (agd)
-    hipLaunchKernelGGL(mt_step_kernel<true>, dim3(mt_grid(nchunks)), dim3(MT_THREADS), 0, s,
-                       (const MTDesc*)descs, (const MTChunk*)chunks, nchunks, (const float*)gscale, h);
+    hipLaunchKernelGGL(mt_step_kernel<true>, dim3(g), dim3(MT_THREADS), 0, s, (const MTDesc*)descs,
+                       (const MTChunk*)chunks, nchunks, (const float*)gscale, h);
   else
-    hipLaunchKernelGGL(mt_step_kernel<false>, dim3(mt_grid(nchunks)), dim3(MT_THREADS), 0, s,
-                       (const MTDesc*)descs, (const MTChunk*)chunks, nchunks, (const float*)gscale, h);
+    hipLaunchKernelGGL(mt_step_kernel<false>, dim3(g), dim3(MT_THREADS), 0, s, (const MTDesc*)descs,
+                       (const MTChunk*)chunks, nchunks, (const float*)gscale, h);
   DW_LAUNCH_RET;
+}
+
+extern "C" int dw_mt_adam(const void* descs, const void* chunks, int64_t nchunks, const void* gscale,
+                          const void* hyper, int agd, void* stream) {
+  return dw_mt_adam_grid(descs, chunks, nchunks, gscale, hyper, agd, 0, stream);
 }
 
 // ws: float[GRID_SUM_MAX + 1] (see grid_sum_finish)

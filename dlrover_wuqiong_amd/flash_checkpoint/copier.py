@@ -1052,22 +1052,18 @@ class GpuCopier:
         # the gather's temporary (never the staging buffers: with the HBM tier
         # they hold the checkpoint being restored) is bounded: world x c bytes
         # per round (hbm_budget.gather_chunk), the whole payload in one round
-        # when it fits.  A standby reserved it while parked
-        # (hbm_tier.reserve_restore_temp): no fresh VRAM on the restart path
+        # when it fits.  c is a COLLECTIVE size: it depends on (per, world,
+        # DWAMD_RESTORE_GATHER_GB) only, never on this rank's free memory, so
+        # every rank runs the same rounds.  A standby reserved the temporary
+        # while parked (hbm_tier.reserve_restore_temp): no fresh VRAM on the
+        # restart path
+        c = min(per, gather_chunk(per, world, 1 << 62))
         tmp = hbm_tier.take_restore_temp()
         want_idx = torch.device(self.device).index
         if (tmp is not None and tmp.is_cuda and (want_idx is None or tmp.device.index == want_idx)
-                and tmp.numel() >= world * min(per, 64 << 20)):
-            c = min(per, tmp.numel() // world)
-            if c < per:
-                c = max(min(per, 64 << 20), c // (2 << 20) * (2 << 20))
+                and tmp.numel() >= c * world):
             self.last_restore_temp = "reserved"
         else:
-            try:
-                free = device_free_bytes(self.device)
-            except Exception:
-                free = 0
-            c = min(per, gather_chunk(per, world, free))
             tmp = torch.empty(c * world, dtype=torch.uint8, device=self.device)
             self.last_restore_temp = "allocated"
         merged = _merge_pieces(pieces_gpu)

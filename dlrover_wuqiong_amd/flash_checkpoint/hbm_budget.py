@@ -54,7 +54,9 @@ def gather_chunk(per: int, world: int, free: int, cap: Optional[int] = None, mar
     """Per-rank bytes per round of the restore all-gather: the whole slice
     (one round, temporary = world x per) when it fits in ``free - margin``
     and under ``cap`` (``DWAMD_RESTORE_GATHER_GB``, default 16 GiB total),
-    else the largest 2 MiB multiple that does."""
+    else the largest 2 MiB multiple that does.  The restore itself passes
+    an unbounded ``free``: the chunk is a collective size every rank must
+    agree on (the standby reserved the temporary; the plan checks it fits)."""
     if per <= 0 or world <= 1:
         return per
     cap = int(float(os.environ.get("DWAMD_RESTORE_GATHER_GB", "16")) * GiB) if cap is None else cap

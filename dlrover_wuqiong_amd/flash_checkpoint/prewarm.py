@@ -87,13 +87,15 @@ def local_slice_bytes() -> int:
 def restore_temp_bytes() -> int:
     """HBM of the replicated restore's all-gather temporary on this rank
     (``copier.restore``: world x per-round chunk; 0 without slices)."""
-    from .hbm_budget import GiB, gather_chunk
+    from .hbm_budget import gather_chunk
+    from .layout import split_ranges
 
     out = 0
     for name, nsl in _NSLICES.items():
-        per = _SLICE_BYTES.get(name, 0)
-        if nsl > 1 and per > 0:
-            out = max(out, gather_chunk(per, nsl, free=1 << 62) * nsl)
+        total = _STATE_BYTES.get(name, 0)
+        if nsl > 1 and total > 0:
+            per = split_ranges(total, nsl)[0][1]  # the padded slice every rank gathers (engine._restore_into)
+            out = max(out, min(per, gather_chunk(per, nsl, free=1 << 62)) * nsl)
     return out
 
 

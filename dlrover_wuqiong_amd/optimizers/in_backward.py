@@ -74,6 +74,11 @@ class OptimizerInBackward:
         self._rest = [(gi, p) for gi, g in enumerate(optimizer.param_groups) for p in g["params"]
                       if id(p) not in covered]
         self.stream = stream
+        # workgroups of each per-unit update (0: the plain step's grid): fewer
+        # CUs taken from the backward GEMMs it runs beside
+        import os
+
+        self.max_blocks = int(os.environ.get("DWAMD_IN_BACKWARD_BLOCKS", "0"))
         self._started = False  # this backward launched updates (the step counter was advanced)
         self._done: set = set()
         self.enabled = True
@@ -99,7 +104,10 @@ class OptimizerInBackward:
 
     def _side(self, device) -> torch.cuda.Stream:
         if self.stream is None:
-            self.stream = torch.cuda.Stream(device=device)
+            # high priority: its own hardware-queue class (a normal-priority
+            # stream created after RCCL's can share the compute stream's queue
+            # at HIP's default 4 queues, serialising the overlap away)
+            self.stream = torch.cuda.Stream(device=device, priority=-1)
         return self.stream
 
     def _after_unit(self, pg, idx: int):
@@ -134,7 +142,7 @@ class OptimizerInBackward:
             side.wait_event(ev)  # this unit's reduce-scattered gradients
         side.wait_stream(cur)  # (and everything the backward queued so far for it)
         with torch.cuda.stream(side):
-            self.opt._cuda_step(live, slot=("unit", idx))
+            self.opt._cuda_step(live, slot=("unit", idx), max_blocks=self.max_blocks)
         for _gi, p in live:
             _local(p.grad).record_stream(side)  # freed by zero_grad on the compute stream
         self._done.add(idx)

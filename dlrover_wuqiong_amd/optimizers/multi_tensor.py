@@ -246,7 +246,7 @@ class _MultiTensorOptimizer(torch.optim.Optimizer):
         self._table_cache[slot] = (key, tables)
         return tables
 
-    def _cuda_step(self, live, slot=None):
+    def _cuda_step(self, live, slot=None, max_blocks: int = 0):
         L = _hip.lib()
         d_desc, d_chunks, nchunks, sharded = self._tables_for(live, slot)
         dev = d_desc.device
@@ -271,8 +271,9 @@ class _MultiTensorOptimizer(torch.optim.Optimizer):
         raw = np.concatenate([h[k] for k in _HYPER_FIELDS] + [np.array([1 if self._adamw_flag() else 0],
                                                                           dtype=np.int32).view(np.float32)])
         assert raw.nbytes == int(L.dw_mt_hyper_size()), "MTHyper layout mismatch"
-        _hip.check(L.dw_mt_adam(_hip.ptr(d_desc), _hip.ptr(d_chunks), nchunks, _hip.ptr(gs),
-                                ctypes.c_void_p(raw.ctypes.data), int(self._agd), _hip.stream()), "mt_step")
+        _hip.check(L.dw_mt_adam_grid(_hip.ptr(d_desc), _hip.ptr(d_chunks), nchunks, _hip.ptr(gs),
+                                     ctypes.c_void_p(raw.ctypes.data), int(self._agd), int(max_blocks),
+                                     _hip.stream()), "mt_step")
 
     def _adamw_flag(self) -> bool:
         return True

@@ -130,11 +130,11 @@ def test_n8_restart_allocation_plan():
             if standby == "import" and not tier:
                 assert p.standby_bytes >= 2 * per  # its own staging buffers
     # what the parked standby reserves (prewarm.restore_temp_bytes) is that temporary
-    prewarm._SLICE_BYTES["seg"], prewarm._NSLICES["seg"] = per, 8
+    prewarm._STATE_BYTES["seg"], prewarm._NSLICES["seg"] = payload, 8
     try:
         assert prewarm.restore_temp_bytes() == p.gather_temp_bytes
     finally:
-        prewarm._SLICE_BYTES.pop("seg"), prewarm._NSLICES.pop("seg")
+        prewarm._STATE_BYTES.pop("seg"), prewarm._NSLICES.pop("seg")
 
 
 @pytest.mark.parametrize("per,world,chunk", [(1000, 4, 1000), (1000, 4, 256), (999, 3, 100)])
