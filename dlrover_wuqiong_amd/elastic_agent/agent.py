@@ -53,16 +53,18 @@ def _hw_queues(env: Dict[str, str]):
     has taken its queues, a later stream can land on the compute stream's
     queue, and a 20 GB checkpoint flush queued there stretched the next three
     GPT2-1.5B steps from 109 to ~155 ms (profiles/r5/flush_queue_sharing.md).
-    The copier's flush stream is a normal-priority stream, which avoided that
-    at 4 queues while the compute stream was created after RCCL's; an import
-    standby creates its compute stream first (its HBM reservation belongs to
-    it, ``standby.py``), and at 4 queues the flush then shared its queue:
-    every step after a save took +385 ms (import-mode goodput 75 -> 47 %,
-    ``profiles/r6/bench_1gpu_import_queue_sharing.json``).  The agent
-    therefore raises the count to DWAMD_GPU_MAX_HW_QUEUES (default 8: a
-    dedicated queue per stream of a worker; r5 measured 8 equal or better at
-    every variant) unless it is already higher; 0 keeps the inherited value."""
-    want = int(os.getenv("DWAMD_GPU_MAX_HW_QUEUES", "8") or 0)
+    The copier's flush stream is a normal-priority stream, which does not
+    share that way at 4 queues (107.3 ms at 4 and 107.2 at 8).  An import
+    standby creates its compute stream before RCCL's (its HBM reservation
+    belongs to it, ``standby.py``) and therefore also creates the flush
+    stream right after it; with the flush created later it shared the
+    compute stream's queue (every step after a save +385 ms,
+    ``profiles/r6/bench_1gpu_import_queue_sharing.json``).  At 8 queues the
+    flush's blit kernels instead run beside every step (deep-standby steps
+    after a save 110 -> 117-124 ms, goodput 93.5 -> 88.9 %,
+    ``profiles/r6/bench_1gpu_8queues.json``), so the inherited value is kept
+    by default.  DWAMD_GPU_MAX_HW_QUEUES=N raises it to N (at most 32)."""
+    want = int(os.getenv("DWAMD_GPU_MAX_HW_QUEUES", "0") or 0)
     try:
         cur = int(env.get("GPU_MAX_HW_QUEUES", "4"))
     except ValueError:

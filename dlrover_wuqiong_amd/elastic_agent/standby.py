@@ -270,6 +270,14 @@ def _gpu_init(lr: str) -> bool:
         global _STREAM
         _STREAM = torch.cuda.Stream()
         torch.cuda.set_stream(_STREAM)
+        # ... and the checkpoint flush stream right after it: HIP maps the
+        # streams of one priority round-robin onto GPU_MAX_HW_QUEUES (4)
+        # hardware queues, and a flush stream created after RCCL's streams
+        # landed on the compute stream's queue (each step after a save waited
+        # for the 0.4 s flush; profiles/r6/bench_1gpu_import_queue_sharing.json)
+        from ..flash_checkpoint.copier import precreate_flush_stream
+
+        precreate_flush_stream(torch.device("cuda", torch.cuda.current_device()))
         x = torch.ones(64, 64, device="cuda", dtype=torch.bfloat16)
         (x @ x).float().sum().item()  # BLAS handle + a first kernel launch
         from .._native import kernels

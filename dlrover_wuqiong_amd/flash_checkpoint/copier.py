@@ -221,6 +221,19 @@ def _optimizer_step_fence(opt, _args, _kwargs):
         _FENCED.discard(c)
 
 
+_FLUSH_STREAMS: dict = {}  # device index -> a flush stream created early (precreate_flush_stream)
+
+
+def precreate_flush_stream(device) -> torch.cuda.Stream:
+    """Create this device's checkpoint flush stream now (the next copier of
+    this process adopts it): hardware queues are assigned in creation order
+    (see elastic_agent/standby.py)."""
+    idx = torch.device(device).index or 0
+    if idx not in _FLUSH_STREAMS:
+        _FLUSH_STREAMS[idx] = torch.cuda.Stream(device=device)
+    return _FLUSH_STREAMS[idx]
+
+
 def _snapshot_stream(device) -> torch.cuda.Stream:
     """The stream of overlapped / ring snapshot copies: HIGH priority.  HIP
     shares hardware queues among the streams of one priority once a process
@@ -378,8 +391,9 @@ class GpuCopier:
             p = _kern().dw_stream_create_prio(0 if kind == "lowprio" else 2, ctypes.byref(pr))
             if p:
                 self._cumask_ptr = p
-        self.side_stream = (torch.cuda.ExternalStream(self._cumask_ptr, device=device)
-                            if self._cumask_ptr else torch.cuda.Stream(device=device))
+        pre = _FLUSH_STREAMS.get(torch.device(device).index or 0) if kind == "plain" else None
+        self.side_stream = (torch.cuda.ExternalStream(self._cumask_ptr, device=device) if self._cumask_ptr
+                            else pre if pre is not None else torch.cuda.Stream(device=device))
         # "memcpy": hipMemcpyAsync (runtime blit); "kernel": our bounded
         # copy kernel storing through the device mapping of the pinned shm
         self.flush_mode = os.environ.get("DWAMD_FLUSH_MODE", "memcpy")

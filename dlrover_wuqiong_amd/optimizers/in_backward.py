@@ -74,8 +74,9 @@ class OptimizerInBackward:
         self._rest = [(gi, p) for gi, g in enumerate(optimizer.param_groups) for p in g["params"]
                       if id(p) not in covered]
         self.stream = stream
-        # workgroups of each per-unit update (0: the plain step's grid): fewer
-        # CUs taken from the backward GEMMs it runs beside
+        # workgroups of each per-unit update (0: the plain step's grid).
+        # Capping it measured slower (256: 312 ms, 64: 331 ms per Llama-3-8B
+        # step, high-priority stream): kept for A/B
         import os
 
         self.max_blocks = int(os.environ.get("DWAMD_IN_BACKWARD_BLOCKS", "0"))
@@ -104,10 +105,10 @@ class OptimizerInBackward:
 
     def _side(self, device) -> torch.cuda.Stream:
         if self.stream is None:
-            # high priority: its own hardware-queue class (a normal-priority
-            # stream created after RCCL's can share the compute stream's queue
-            # at HIP's default 4 queues, serialising the overlap away)
-            self.stream = torch.cuda.Stream(device=device, priority=-1)
+            # normal priority: a high-priority stream let each unit's update
+            # pre-empt the backward GEMMs (Llama-3-8B step 242 -> 283 ms;
+            # profiles/r6/llama3_8b_fsdp_in_backward_ab.jsonl)
+            self.stream = torch.cuda.Stream(device=device)
         return self.stream
 
     def _after_unit(self, pg, idx: int):

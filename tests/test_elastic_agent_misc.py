@@ -3,14 +3,14 @@
 from dlrover_wuqiong_amd.elastic_agent.agent import _hw_queues
 
 
-def test_hw_queues_raised_to_eight_by_default(monkeypatch):
+def test_hw_queues_kept_by_default_raised_on_request(monkeypatch):
     monkeypatch.delenv("DWAMD_GPU_MAX_HW_QUEUES", raising=False)
     env = {"GPU_MAX_HW_QUEUES": "4"}
     _hw_queues(env)
-    assert env["GPU_MAX_HW_QUEUES"] == "8"
+    assert env["GPU_MAX_HW_QUEUES"] == "4"
     env = {}
     _hw_queues(env)
-    assert env["GPU_MAX_HW_QUEUES"] == "8"  # HIP's default is 4
+    assert "GPU_MAX_HW_QUEUES" not in env
     monkeypatch.setenv("DWAMD_GPU_MAX_HW_QUEUES", "0")
     env = {"GPU_MAX_HW_QUEUES": "4"}
     _hw_queues(env)
