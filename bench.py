@@ -111,6 +111,7 @@ def parse(argv=None):
                    help="N ranks share cuda:0 over gloo: rehearses the N>1 fault path on one GPU")
     p.add_argument("--no-frameworks", action="store_true",
                    help="skip the FSDP / Megatron flash-checkpoint rows (N=1, GPT2-1.5B only)")
+    p.add_argument("--only-import", action="store_true", help=argparse.SUPPRESS)  # A/B: the import-mode job alone
     p.add_argument("--step-overlap", action="store_true",
                    help="run the optimizer update under the next forward (optimizers/overlap.py)")
     # worker-only
@@ -241,11 +242,15 @@ def launcher(a) -> int:
     os.makedirs(run_dir, exist_ok=True)
     res, rc = None, 1
     try:
-        rc, wall, prefix, ck = _job(a, n, "deep", run_dir, "")
-        try:
-            res = summarize(a, run_dir, n, wall)
-        finally:
-            _cleanup(prefix, ck)
+        if a.only_import:
+            rc, res = 0, {"metric": METRIC, "only_import": True}
+            a.no_import_hbm, a.no_frameworks = True, True
+        else:
+            rc, wall, prefix, ck = _job(a, n, "deep", run_dir, "")
+            try:
+                res = summarize(a, run_dir, n, wall)
+            finally:
+                _cleanup(prefix, ck)
         jobs = []
         if res is not None and not a.no_fault and not a.no_import_fault:
             jobs.append(("import", "i", "import_mode"))

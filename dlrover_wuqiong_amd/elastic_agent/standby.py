@@ -268,8 +268,9 @@ def _gpu_init(lr: str) -> bool:
         # training_stream() -- allocates from the reservation; one that
         # switches to a stream of its own allocates from the driver)
         global _STREAM
-        _STREAM = torch.cuda.Stream()
-        torch.cuda.set_stream(_STREAM)
+        if os.environ.get("DWAMD_STANDBY_STREAM", "1") == "1":
+            _STREAM = torch.cuda.Stream()
+            torch.cuda.set_stream(_STREAM)
         # ... and the checkpoint flush stream right after it: HIP maps the
         # streams of one priority round-robin onto GPU_MAX_HW_QUEUES (4)
         # hardware queues, and a flush stream created after RCCL's streams
@@ -277,7 +278,8 @@ def _gpu_init(lr: str) -> bool:
         # for the 0.4 s flush; profiles/r6/bench_1gpu_import_queue_sharing.json)
         from ..flash_checkpoint.copier import precreate_flush_stream
 
-        precreate_flush_stream(torch.device("cuda", torch.cuda.current_device()))
+        if os.environ.get("DWAMD_STANDBY_FLUSH_STREAM", "1") == "1":
+            precreate_flush_stream(torch.device("cuda", torch.cuda.current_device()))
         x = torch.ones(64, 64, device="cuda", dtype=torch.bfloat16)
         (x @ x).float().sum().item()  # BLAS handle + a first kernel launch
         from .._native import kernels
