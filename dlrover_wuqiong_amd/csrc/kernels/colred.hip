@@ -421,9 +421,11 @@ __global__ void __launch_bounds__(256) norm_bwd_fused_kernel(
 // (<= 256 registers; gamma re-read per row, the residual gradient loaded
 // where it is added): the second wave hides the row loads the prefetch set
 // hid before, and twice the workgroups are resident (512).  GPT2-1.5B's call
-// (H = 1600, dres + dx column sums): 39.0 -> 36.9 us at 8192 rows, 62.0 ->
-// 56.1 us at 16384 (profiles/r6/norm_bwd_w2_ab.jsonl); 0: the prefetch form
-#define DWAMD_NORM_BWD_W2 1
+// (H = 1600, dres + dx column sums) alone: 39.0 -> 36.9 us at 8192 rows, 62.0
+// -> 56.1 us at 16384 (profiles/r6/norm_bwd_w2_ab.jsonl); inside the step the
+// kernel goes 35.6 -> 34.5 us but the column-sum pass over twice the block
+// partials 7.6 -> 10.4 us (profiles/r6/gpt2_1.5b_step_kernels.md): off
+#define DWAMD_NORM_BWD_W2 0
 #endif
 
 template <int VPL, bool RMS, bool DS = false>
