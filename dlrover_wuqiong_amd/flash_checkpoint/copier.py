@@ -1115,11 +1115,15 @@ class GpuCopier:
         from . import deferred_restore
 
         cur = torch.cuda.current_stream(self.device)
-        if getattr(self, "_restore_stream", None) is None:
-            self._restore_stream = torch.cuda.Stream(device=self.device)
+        # on the flush stream (idle at a restore; the first flush queues
+        # behind these copies): a stream created here, after RCCL's, shared a
+        # hardware queue with an import standby's compute stream at HIP's
+        # default 4 queues, and every step after a save then waited for that
+        # save's 0.4 s flush (import-mode goodput 73 -> 47 %,
+        # profiles/r6/import_stall_ab.jsonl)
         merged = _merge_pieces(pieces_gpu)
         copies = [(shm_payload_addr + off, dst, n) for off, dst, n in merged]
-        d = deferred_restore.DeferredRestore(self.device, self._restore_stream, cur.record_event(),
+        d = deferred_restore.DeferredRestore(self.device, self.side_stream, cur.record_event(),
                                              lambda stream: self._pipelined_h2d(copies, stream), t0)
         deferred_restore.add(d)
         return d
