@@ -313,29 +313,29 @@ class _FlatOptimizer(torch.optim.Optimizer):
     def _defer_budget(self, per_step: int) -> int:
         """Deferred steps (K) whose kept gradients fit in HBM: each deferred
         step keeps a copy of the deferred elements' gradient until the ring
-        drains.  Budget = free HBM (driver + the allocator's unused cache)
-        minus the next forward/backward's activation growth (this process's
-        peak minus what it holds now, measured at this optimizer step) minus
-        ``DWAMD_DEFER_RESERVE_GB`` (2).  K = min(DWAMD_DEFER_STATE_STEPS, 4
-        by default, budget // per-step bytes); 0 = wait for the ring.  The
-        plan is kept in ``last_defer_plan`` (and counted by
-        ``hbm_budget.plan``'s ``defer_bytes``)."""
+        drains.  Budget = the driver's free HBM minus ``DWAMD_DEFER_RESERVE_GB``
+        (2).  The caching allocator's unused cache is NOT counted: at an
+        optimizer step it holds the blocks the freed activations came from,
+        which the next forward takes again (a process-lifetime peak statistic
+        is no measure of that: it keeps earlier, larger workloads).  K =
+        min(DWAMD_DEFER_STATE_STEPS, 4 by default, budget // per-step
+        bytes); 0 = wait for the ring.  The plan is kept in
+        ``last_defer_plan`` (and counted by ``hbm_budget.plan``'s
+        ``defer_bytes``)."""
         import os
-
-        from ..flash_checkpoint.copier import device_free_bytes
 
         kcap = max(1, min(7, int(os.environ.get("DWAMD_DEFER_STATE_STEPS", "4"))))
         dev = self.flat.device
         try:
-            free = device_free_bytes(dev)
-            growth = max(0, int(torch.cuda.max_memory_allocated(dev)) - int(torch.cuda.memory_allocated(dev)))
+            free = int(torch.cuda.mem_get_info(dev)[0])
+            cached = max(0, int(torch.cuda.memory_reserved(dev)) - int(torch.cuda.memory_allocated(dev)))
         except Exception:
-            free, growth = 0, 0
+            free, cached = 0, 0
         margin = int(float(os.environ.get("DWAMD_DEFER_RESERVE_GB", "2")) * (1 << 30))
-        budget = free - growth - margin
+        budget = free - margin
         k = max(0, min(kcap, budget // max(1, per_step + 64)))
         self.last_defer_plan = {"steps": int(k), "per_step_bytes": int(per_step), "budget_bytes": int(budget),
-                                "free_bytes": int(free), "activation_growth_bytes": int(growth),
+                                "driver_free_bytes": int(free), "allocator_cache_bytes": int(cached),
                                 "decision": "defer" if k >= 1 else "wait"}
         from ..common.log import logger
 
