@@ -331,7 +331,9 @@ def framework_rows(a, run_dir) -> dict:
                  dict(MASTER_PORT=str(29571 + os.getpid() % 1000), DWAMD_SHM_PREFIX=f"bf{os.getpid()}")),
         "megatron": ([sys.executable, "-u", os.path.join(REPO, "scripts", "bench_megatron_tp_shard.py"), "--model",
                       "gpt2-1.5b" if a.model == "gpt2-1.5b" else "llama-tiny", "--tp", "1", "--saves", "3",
-                      "--work-gemms", "1200" if a.model == "gpt2-1.5b" else "2", "--ckpt-dir",
+                      # GPT2-1.5B: real training steps between the saves (the state in Megatron's layout is views
+                      # into the live model and optimizer); other models: stand-in GEMMs
+                      *(["--train-steps", "4"] if a.model == "gpt2-1.5b" else ["--work-gemms", "2"]), "--ckpt-dir",
                       os.path.join(a.ckpt_dir, f"meg_{os.getpid()}")],
                      dict(DWAMD_SHM_PREFIX=f"bm{os.getpid()}")),
     }

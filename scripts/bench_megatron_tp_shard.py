@@ -94,6 +94,69 @@ def build_state(shapes, device):
     return {"model": model, "optimizer": optim, "rng_state": [{"random_rng_state": 0}]}
 
 
+def megatron_names_gpt2(n_layer: int):
+    """This framework's GPT2 parameter names -> Megatron-core GPTModel names
+    (same shapes at TP=1; tied embeddings = Megatron's default
+    share_embeddings_and_output_weights, so no output_layer)."""
+    out = {"wte.weight": "embedding.word_embeddings.weight", "wpe.weight": "embedding.position_embeddings.weight",
+           "ln_f.weight": "decoder.final_layernorm.weight", "ln_f.bias": "decoder.final_layernorm.bias"}
+    per = {"ln_1.weight": "self_attention.linear_qkv.layer_norm_weight",
+           "ln_1.bias": "self_attention.linear_qkv.layer_norm_bias",
+           "attn.c_attn.weight": "self_attention.linear_qkv.weight", "attn.c_attn.bias": "self_attention.linear_qkv.bias",
+           "attn.c_proj.weight": "self_attention.linear_proj.weight", "attn.c_proj.bias": "self_attention.linear_proj.bias",
+           "ln_2.weight": "mlp.linear_fc1.layer_norm_weight", "ln_2.bias": "mlp.linear_fc1.layer_norm_bias",
+           "mlp.c_fc.weight": "mlp.linear_fc1.weight", "mlp.c_fc.bias": "mlp.linear_fc1.bias",
+           "mlp.c_proj.weight": "mlp.linear_fc2.weight", "mlp.c_proj.bias": "mlp.linear_fc2.bias"}
+    for i in range(n_layer):
+        for k, v in per.items():
+            out[f"h.{i}.{k}"] = f"decoder.layers.{i}.{v}"
+    return out
+
+
+def build_trained_gpt2(device, micro_batch: int, seq: int):
+    """A real GPT2-1.5B training setup (bf16 params, fp32 masters + Adam in
+    FusedAdamW's flat buffers) whose state dict in Megatron's layout is
+    views into the live tensors: the saves checkpoint what training writes."""
+    from dlrover_wuqiong_amd.models.gpt2 import GPT2, GPT2Config
+    from dlrover_wuqiong_amd.optimizers.fused import FusedAdamW
+    from dlrover_wuqiong_amd.parallel.flat import FlatParams
+
+    cfg = GPT2Config.named("gpt2-1.5b")
+    cfg.n_positions = max(cfg.n_positions, seq)
+    torch.manual_seed(0)
+    with torch.device(device):
+        model = GPT2(cfg)
+    model.to(torch.bfloat16)
+    flat = FlatParams(model, dtype=torch.bfloat16, device=device)
+    opt = FusedAdamW(flat, lr=1.5e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0)
+    names = megatron_names_gpt2(cfg.n_layer)
+    pname = {id(p): n for n, p in model.named_parameters()}
+    msd, main, exp_avg, exp_avg_sq = {}, [], {}, {}
+    for i, (o, c) in enumerate(flat.offsets):
+        p = flat.params[i]
+        msd[names[pname[id(p)]]] = p.data
+        main.append(opt.master[o:o + c].view(p.shape))
+        exp_avg[i] = opt.exp_avg[o:o + c].view(p.shape)
+        exp_avg_sq[i] = opt.exp_avg_sq[o:o + c].view(p.shape)
+    g = opt.param_groups[0]
+    optim = {"optimizer": {"state": {i: {"exp_avg": exp_avg[i], "exp_avg_sq": exp_avg_sq[i], "step": opt._step_t}
+                                     for i in exp_avg},
+                           "param_groups": [{"lr": g["lr"], "betas": g["betas"], "eps": g["eps"],
+                                             "weight_decay": g["weight_decay"], "params": list(exp_avg)}]},
+             "fp32_from_fp16_params": [main]}
+    data = torch.randint(0, cfg.vocab_size, (2, micro_batch, seq + 1), device=device)
+
+    def step(i):
+        b = data[i % 2]
+        loss = model(b[:, :-1], b[:, 1:])
+        loss.backward()
+        opt.step()
+        flat.zero_grad()
+        return loss
+
+    return {"model": msd, "optimizer": optim, "rng_state": [{"random_rng_state": 0}]}, step, model.num_params()
+
+
 def tensors(sd):
     if isinstance(sd, torch.Tensor):
         yield sd
@@ -115,6 +178,9 @@ def main():
     p.add_argument("--tp", type=int, default=8)
     p.add_argument("--saves", type=int, default=3)
     p.add_argument("--work-gemms", type=int, default=4000, help="bf16 8192^3 GEMMs between saves (~3.3 s)")
+    p.add_argument("--train-steps", type=int, default=0,
+                   help="gpt2-1.5b at TP=1: REAL training steps (B=8 x 1024) between saves instead of stand-in "
+                        "GEMMs; the Megatron-layout state is views into the live model / optimizer")
     p.add_argument("--ckpt-dir", default="/tmp/dwamd_megatron_ckpt")
     args = p.parse_args()
     os.environ.setdefault("LOCAL_WORLD_SIZE", "1")
@@ -132,7 +198,12 @@ def main():
     shapes = shard_param_shapes(m, args.tp)
     nparams = sum(int(torch.Size(s).numel()) for s in shapes.values())
     t0 = time.perf_counter()
-    sd = build_state(shapes, device)
+    real = args.train_steps > 0
+    if real:
+        assert args.model == "gpt2-1.5b" and args.tp == 1 and cuda, "real training: gpt2-1.5b, TP=1, on a GPU"
+        sd, train_step, nparams = build_trained_gpt2(device, 8, 1024)
+    else:
+        sd = build_state(shapes, device)
     nbytes = sum(t.numel() * t.element_size() for t in tensors(sd))
     print(f"{args.model} TP={args.tp} rank-0 shard: {nparams / 1e9:.2f} B params, {len(shapes)} tensors, "
           f"{nbytes / 1e9:.1f} GB state, built in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
@@ -141,7 +212,18 @@ def main():
     a = torch.randn(n, n, dtype=torch.bfloat16 if cuda else torch.float32, device=device)
     bmat = torch.randn_like(a)
 
+    step_times = []
+    n_trained = [0]
+
     def work():
+        if real:
+            for _ in range(args.train_steps):
+                ts = time.perf_counter()
+                train_step(n_trained[0])
+                torch.cuda.current_stream().synchronize()
+                step_times.append(time.perf_counter() - ts)
+                n_trained[0] += 1
+            return
         for _ in range(args.work_gemms):
             torch.mm(a, bmat)
         for t in list(tensors(sd["model"]))[:8]:  # the step changes the state
@@ -202,7 +284,9 @@ def main():
     ckpt.close()
     print(json.dumps({
         "metric": "megatron tp-shard flash ckpt pause s", "value": round(sum(pauses) / len(pauses), 4), "unit": "s",
-        "higher_is_better": False, "dtype": "bf16 params + fp32 main/Adam", "data": "synthetic values",
+        "higher_is_better": False, "dtype": "bf16 params + fp32 main/Adam",
+        "data": ("synthetic tokens, random-init weights, trained between saves" if real else "synthetic values"),
+        "train_step_ms": round(1000 * sorted(step_times)[len(step_times) // 2], 1) if step_times else None,
         "config": {"model": f"{args.model} (Megatron-core names)", "parallelism": f"tp{args.tp}: rank 0's shard "
                    "on one GPU", "layout": os.path.relpath(get_checkpoint_name(args.ckpt_dir, it), args.ckpt_dir)},
         "params": nparams, "ckpt_bytes": nbytes, "save_sec": [round(x, 4) for x in pauses],
