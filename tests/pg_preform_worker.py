@@ -66,6 +66,12 @@ def main():
         with open(a.out + f".ready{rank}", "w") as f:
             f.write("1")
         if a.kill and rank == world - 1:
+            # every rank's record is on disk before the kill (the agent stops
+            # the survivors within milliseconds of it)
+            deadline = time.time() + 60
+            while time.time() < deadline and sum(1 for r in range(world)
+                                                 if os.path.exists(a.out + f".ready{r}")) < world:
+                time.sleep(0.05)
             os.kill(os.getpid(), signal.SIGKILL)
         while True:  # stopped by the agent (failure of a peer / membership change)
             time.sleep(0.1)
