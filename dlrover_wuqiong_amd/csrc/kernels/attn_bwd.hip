@@ -208,8 +208,7 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
   const long long bh = vl.cu_q ? (long long)h : (long long)b * H + h;  // dropout hash row
   const float al2 = EXT ? ext_alibi2(ex, b, h) : 0.f;
   u32x4 q_st[C::VPT], do_st[C::VPT];
-  // row constants staged NEGATED: they are the initial accumulators of S' and dP'
-  float lse_st = -INFINITY, del_st = 0.f;
+  float lse_st = -INFINITY, del_st = 0.f;  // the tile's LSE / delta (raw)
   auto issue = [&](int it) {
     const int q0 = q_lo + it * C::BQT;
 #pragma unroll
@@ -227,11 +226,12 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
       }
     }
     if (tid < C::BQT) {
+      // raw values: negated / scaled at write(), after the tile's compute --
+      // arithmetic here waited on the load at once, with the tile barrier
+      // right behind it
       const int q = q0 + tid;
-      const float l = q < SQ ? lse_b[q] : -INFINITY;
-      // a row that saw no key (lse = -inf) contributes nothing: p = 2^-inf
-      lse_st = l > -INFINITY ? -l * 1.4426950408889634f : -INFINITY;
-      del_st = q < SQ ? -del_b[q] : 0.f;
+      lse_st = q < SQ ? lse_b[q] : -INFINITY;
+      del_st = q < SQ ? del_b[q] : 0.f;
     }
   };
   auto write = [&](int buf) {
@@ -247,8 +247,10 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
       *(u32x4*)(dl + img_off<D>(row, c)) = do_st[i];
     }
     if (tid < C::BQT) {
-      stl[tid] = lse_st;
-      stl[C::BQT + tid] = del_st;
+      // row constants NEGATED: they are the initial accumulators of S' and dP';
+      // a row that saw no key (lse = -inf) contributes nothing: p = 2^-inf
+      stl[tid] = lse_st > -INFINITY ? -lse_st * 1.4426950408889634f : -INFINITY;
+      stl[C::BQT + tid] = -del_st;
     }
   };
   if (n_it > 0) {
