@@ -26,6 +26,10 @@ Optimizations (applied in a fixed, dependency-respecting order):
                      "gpipe" | "interleaved", "virtual_stages": v}; train with
                      ``result.model.train_step(ids, targets)`` (``parallel/pipeline.py``)
   fsdp / zero2       FSDP2 ``fully_shard`` per layer (zero2: no reshard after fwd)
+  flat_fsdp /        flat-unit FSDP (``parallel/flat_fsdp.py``): one flat buffer
+  flat_zero2         per layer, collectives in place (no copy-in / copy-out),
+                     the fused optimizer over the rank's shard; flash
+                     checkpoints in ATorch's flat-shard format
   zero1              ZeroRedundancyOptimizer on top of DDP
   ddp                DistributedDataParallel (default when data parallel > 1)
 
@@ -60,7 +64,8 @@ from . import distributed as adist
 
 ORDER = ["parallel_mode", "module_replace", "half", "amp_native", "fp8", "tensor_parallel", "sequence_parallel",
          "context_parallel",
-         "checkpoint", "mixed_parallel", "pipeline_parallel", "fsdp", "zero2", "zero1", "ddp"]
+         "checkpoint", "mixed_parallel", "pipeline_parallel", "fsdp", "zero2", "flat_fsdp", "flat_zero2", "zero1",
+         "ddp"]
 ALIASES = {"amp": "amp_native", "amp_native_bf16": "amp_native", "fsdp2": "fsdp", "zero3": "fsdp",
            "pipe": "pipeline_parallel", "pipeline": "pipeline_parallel", "ds_3d_parallel": "mixed_parallel",
            "deepspeed_3d_parallel": "mixed_parallel", "3d_parallel": "mixed_parallel"}
@@ -712,6 +717,24 @@ def _apply_fsdp(ctx, cfg, reshard=True):
     logger.info(f"fsdp: {n} layers sharded (reshard_after_forward={reshard})")
 
 
+def _apply_flat_fsdp(ctx, cfg, reshard=True):
+    """Flat-unit FSDP over the data-parallel group (every rank at world 1):
+    the optimizer built below is the fused flat one over the rank's shard."""
+    from ..parallel.flat_fsdp import FlatFSDP
+
+    cfgd = dict(cfg) if isinstance(cfg, dict) else {}
+    model = ctx["model"]
+    if _meta_model(model):
+        raise RuntimeError("flat_fsdp: materialise the model first (meta-device init needs fsdp / zero2)")
+    model = model.to(_device())  # the flat buffers are built where the parameters are
+    pg = ctx.get("dp_group") if dist.is_initialized() else None
+    ctx["model"] = FlatFSDP(model, wrap_cls=_wrap_cls(ctx, cfg), process_group=pg,
+                            reshard_after_forward=cfgd.get("reshard_after_forward", reshard),
+                            sync_module_states=cfgd.get("sync_module_states", True))
+    ctx["flat_fsdp"] = ctx["model"]
+    ctx["fsdp"] = True  # no DDP on top; autocast is the caller's (use "half": bf16 parameters)
+
+
 def _apply_ddp(ctx, cfg):
     if not dist.is_initialized() or ctx.get("fsdp"):
         return
@@ -751,7 +774,27 @@ APPLY = {"parallel_mode": _apply_parallel_mode, "module_replace": _apply_module_
          "checkpoint": _apply_checkpoint, "mixed_parallel": _apply_mixed_parallel,
          "pipeline_parallel": _apply_pipeline_parallel,
          "fsdp": _apply_fsdp, "zero2": functools.partial(_apply_fsdp, reshard=False),
+         "flat_fsdp": _apply_flat_fsdp, "flat_zero2": functools.partial(_apply_flat_fsdp, reshard=False),
          "zero1": lambda ctx, cfg: ctx.__setitem__("zero1", True), "ddp": _apply_ddp}
+
+
+def _flat_optimizer(fs, optim_func, args):
+    """The fused flat optimizer over a FlatFSDP shard for torch / ATorch
+    AdamW, Adam and AGD (the shard is one flat buffer: per-parameter groups
+    do not apply)."""
+    from ..optimizers.fused import FusedAdamW, FusedAGD
+
+    name = getattr(optim_func, "__name__", str(optim_func))
+    a = dict(args)
+    if name in ("AdamW", "FusedAdamW", "MultiTensorAdamW", "Adam"):
+        kw = {k: a[k] for k in ("lr", "betas", "eps", "weight_decay") if k in a}
+        if "max_grad_norm" in a:
+            kw["max_grad_norm"] = a["max_grad_norm"]
+        return FusedAdamW(fs.shard_flat, adamw=name != "Adam", **kw)
+    if name in ("AGD", "FusedAGD"):
+        kw = {k: a[k] for k in ("lr", "betas", "delta", "weight_decay") if k in a}
+        return FusedAGD(fs.shard_flat, **kw)
+    raise ValueError(f"flat_fsdp: no fused flat optimizer for {name} (AdamW / Adam / AGD)")
 
 
 _PARTITION: List[int] = []  # [rank, size] of the last auto_accelerate's data partition
@@ -856,7 +899,7 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
         strategy = Strategy.from_spec([("parallel_mode", (dims, None))] + strategy.opts)
     if world > 1 and "parallel_mode" not in strategy.names():
         strategy = Strategy.from_spec([("parallel_mode", None)] + strategy.opts)
-    if world > 1 and not {"ddp", "fsdp", "zero2", "zero1"} & set(strategy.names()):
+    if world > 1 and not {"ddp", "fsdp", "zero2", "zero1", "flat_fsdp", "flat_zero2"} & set(strategy.names()):
         strategy = Strategy.from_spec(strategy.opts + [("ddp", None)])
     if "zero1" in strategy.names() and "ddp" not in strategy.names():
         strategy = Strategy.from_spec(strategy.opts + [("ddp", None)])
@@ -896,14 +939,16 @@ def auto_accelerate(model: nn.Module, optim_func=None, dataset=None, loss_func=N
                 if n_groups <= 16:
                     optim_func, args = fcls, fargs
                     logger.info(f"optimizer: {fcls.__name__} (multi-tensor HIP kernel)")
-        if ctx.get("zero1"):
+        if ctx.get("flat_fsdp") is not None:
+            optim = _flat_optimizer(ctx["flat_fsdp"], optim_func, args)
+        elif ctx.get("zero1"):
             from torch.distributed.optim import ZeroRedundancyOptimizer
 
             optim = ZeroRedundancyOptimizer(params, optimizer_class=optim_func, process_group=ctx.get("dp_group"),
                                             **args)
         else:
             optim = optim_func(params, **args)
-        if ctx.get("local_sgd"):
+        if ctx.get("local_sgd") and optim is not None:
             from .local_sgd import GTAReducer, HSDPLocalSGD, LinearReducer
 
             rg, lcfg = ctx["local_sgd"]

@@ -107,9 +107,29 @@ def _shard_info(p) -> Tuple[torch.Tensor, dict]:
     return p, {"shape": list(p.shape), "dim": 0, "offset": 0, "length": int(p.shape[0]) if p.dim() else 1}
 
 
+def _flat_fsdp(model):
+    """The ``parallel.flat_fsdp.FlatFSDP`` behind ``model`` (or None)."""
+    from ..parallel.flat_fsdp import FlatFSDP
+
+    for m in (model, getattr(model, "module", None)):
+        if isinstance(m, FlatFSDP):
+            return m
+    return None
+
+
 def get_flat_model_param(model) -> Tuple[Dict, Dict, Dict, Dict]:
     """(params {name: local shard}, buffers, param_meta, ckpt_meta)."""
     rank, world = _dp_rank_world()
+    fs = _flat_fsdp(model)
+    if fs is not None:
+        # FlatParameter layout: this rank's element range of every flattened
+        # parameter ("dim": -1), views of the live shard buffer
+        views, fmeta = fs.flat_shard_tensors()
+        meta = {n: dict(m, rank=rank, dtype=str(views[n].dtype).replace("torch.", "")) for n, m in fmeta.items()}
+        buffers = {clean_name(k): v for k, v in fs.module.named_buffers()}
+        ckpt_meta = {"version": CKPT_VERSION, "world_size": world, "layout": "flat",
+                     "wrap_class": [[type(u.module).__module__, type(u.module).__name__] for u in fs.units[:2]]}
+        return views, buffers, meta, ckpt_meta
     params, meta = {}, {}
     for name, p in model.named_parameters():
         local, m = _shard_info(p.detach())
@@ -123,8 +143,40 @@ def get_flat_model_param(model) -> Tuple[Dict, Dict, Dict, Dict]:
     return params, buffers, meta, ckpt_meta
 
 
+_FLAT_STATES = (("exp_avg", "exp_avg"), ("exp_avg_sq", "exp_avg_sq"), ("master_param", "master"))
+
+
+def _flat_optim_views(fs, optimizer) -> Dict[str, torch.Tensor]:
+    """"<param>-<state>" element-range views of a flat optimizer's state over
+    a FlatFSDP shard (FusedAdamW / FusedAGD: exp_avg, exp_avg_sq, fp32
+    master, one step counter)."""
+    out = {}
+    for key, attr in _FLAT_STATES:
+        buf = getattr(optimizer, attr, None)
+        if buf is None:
+            continue
+        views, _m = fs._shard_views(buf)
+        for n, v in views.items():
+            out[f"{n}-{key}"] = v
+    step = getattr(optimizer, "_step_t", None)
+    if step is not None:
+        for n in fs.flat_shard_tensors()[0]:
+            out[f"{n}-step"] = step
+    return out
+
+
 def get_fsdp_optim_param(model, optimizer) -> Tuple[Dict, List]:
     """(optim_states {"<param>-<state>": local tensor}, param_groups with names)."""
+    fs = _flat_fsdp(model)
+    if fs is not None and getattr(optimizer, "flat", None) is fs.shard_flat:
+        names = [n for u in fs.units for n in u.names]
+        groups = []
+        for g in optimizer.param_groups:
+            packed = {k: (list(v) if isinstance(v, tuple) else v) for k, v in g.items() if k != "params"}
+            packed = {k: v for k, v in packed.items() if isinstance(v, (int, float, str, bool, list, type(None)))}
+            packed["params"] = names
+            groups.append(packed)
+        return _flat_optim_views(fs, optimizer), groups
     names = {id(p): clean_name(n) for n, p in model.named_parameters()}
     groups, states = [], {}
     for g in optimizer.param_groups:
@@ -298,11 +350,38 @@ class ShardTensorUtil:
         for v in self.param_meta.values():
             v.sort(key=lambda m: m["offset"])
 
+    def _elements(self, fds, key_fn, name, lo: int, hi: int) -> torch.Tensor:
+        """Elements [lo, hi) of the FLATTENED tensor ``name`` (1-D), whatever
+        the layout it was saved in (element ranges or dim-0 row shards)."""
+        metas = self.param_meta[name]
+        if metas[0]["dim"] == -1:
+            parts = []
+            for m in metas:
+                a, b = max(lo, m["offset"]), min(hi, m["offset"] + m["length"])
+                if a < b:
+                    parts.append(fds[m["rank"]].get_slice(key_fn(name))[a - m["offset"]:b - m["offset"]])
+            if not parts:
+                return torch.empty(0)
+            return torch.cat(parts) if len(parts) > 1 else parts[0]
+        shape = metas[0]["shape"]
+        row = 1
+        for d in shape[1:]:
+            row *= int(d)
+        r0, r1 = lo // row, (hi + row - 1) // row
+        return self._rows(fds, key_fn, name, r0, r1).reshape(-1)[lo - r0 * row:hi - r0 * row]
+
     def _rows(self, fds, key_fn, name, lo: int, hi: int) -> torch.Tensor:
         """Rows [lo, hi) along the sharded dim of ``name`` from the shards
         that overlap them."""
         metas = self.param_meta[name]
         dim = metas[0]["dim"]
+        if dim == -1:  # saved as element ranges: dim-0 rows of the full shape
+            shape = list(metas[0]["shape"])
+            row = 1
+            for d in shape[1:]:
+                row *= int(d)
+            shape[0] = hi - lo
+            return self._elements(fds, key_fn, name, lo * row, hi * row).view(shape)
         parts = []
         for m in metas:
             a, b = max(lo, m["offset"]), min(hi, m["offset"] + m["length"])
@@ -321,6 +400,11 @@ class ShardTensorUtil:
 
     def load_tensor_by_name(self, name: str) -> torch.Tensor:
         m = self.param_meta[name][0]
+        if m["dim"] == -1:
+            n = 1
+            for d in m["shape"]:
+                n *= int(d)
+            return self._elements(self._fds, lambda x: x, name, 0, n).view(m["shape"])
         return self._rows(self._fds, lambda n: n, name, 0, m["shape"][m["dim"]] if m["shape"] else 1)
 
     def load_buffers(self) -> Dict[str, torch.Tensor]:
@@ -336,6 +420,19 @@ class ShardTensorUtil:
 
     def load_into_model(self, model):
         """Copy every parameter's rows for THIS rank's current sharding."""
+        fs = _flat_fsdp(model)
+        if fs is not None:
+            views, meta = fs.flat_shard_tensors()
+            with torch.no_grad():
+                for n, v in views.items():
+                    m = meta[n]
+                    v.copy_(self._elements(self._fds, lambda x: x, n, m["offset"], m["offset"] + m["length"])
+                            .to(v.dtype))
+                bufs = self.load_buffers()
+                for name, b in fs.module.named_buffers():
+                    if clean_name(name) in bufs:
+                        b.copy_(bufs[clean_name(name)])
+            return
         with torch.no_grad():
             for name, p in model.named_parameters():
                 n = clean_name(name)
@@ -351,6 +448,28 @@ class ShardTensorUtil:
         state tensors (creating them as zeros-like first if it has none)."""
         with open(os.path.join(self.path, "optim_meta")) as f:
             groups = json.load(f)
+        fs = _flat_fsdp(model)
+        if fs is not None and getattr(optimizer, "flat", None) is fs.shard_flat:
+            for g, sg in zip(optimizer.param_groups, groups):
+                for k, v in sg.items():
+                    if k != "params":
+                        g[k] = tuple(v) if k == "betas" else v
+            _views, meta = fs.flat_shard_tensors()
+            keys = {r: set(fd.keys()) for r, fd in self._ofds.items()}
+            with torch.no_grad():
+                for key, v in _flat_optim_views(fs, optimizer).items():
+                    name, st = key.rsplit("-", 1)
+                    if not any(key in ks for ks in keys.values()):
+                        continue
+                    if st == "step":
+                        r0 = next(r for r, ks in keys.items() if key in ks)
+                        v.copy_(self._ofds[r0].get_tensor(key).to(v.dtype).view(v.shape))
+                        continue
+                    m = meta[name]
+                    v.copy_(self._elements(self._ofds, lambda x, _s=st: f"{x}-{_s}", name, m["offset"],
+                                           m["offset"] + m["length"]).to(v.dtype))
+            logger.info(f"flat optimizer state resharded from world {self.world} checkpoint {self.path}")
+            return
         names = {clean_name(n): p for n, p in model.named_parameters()}
         for g, sg in zip(optimizer.param_groups, groups):
             for k, v in sg.items():

@@ -53,7 +53,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
         # directly: an in-place (flash checkpoint) restore restores it too
         self._step_t = torch.zeros((), dtype=torch.float32)
         self.max_grad_norm = max_grad_norm
-        self.grad_scale = 1.0  # e.g. 1/world for summed DDP gradients
+        # e.g. 1/world for summed DDP gradients; a FlatFSDP shard brings its own
+        self.grad_scale = float(getattr(flat, "grad_scale", 1.0))
         self._scalars = torch.zeros(4, dtype=torch.float32, device=dev)  # sumsq, coef, norm, pad
         self.last_grad_norm = None
 
@@ -80,6 +81,10 @@ class _FlatOptimizer(torch.optim.Optimizer):
             _hip.check(L.dw_sumsq_flat(_hip.ptr(self.flat.grad), _hip.dtype_code(self.flat.grad), self.flat.numel,
                                        _hip.ptr(s[0:1]), _hip.ptr(_hip.grid_sum_ws(s.device)), _hip.stream()),
                        "sumsq")
+            if getattr(self.flat, "norm_reduce", False):  # a sharded gradient (FlatFSDP): the global norm
+                import torch.distributed as dist
+
+                dist.all_reduce(s[0:1], group=self.flat.norm_group)
             _hip.check(L.dw_clip_coef(_hip.ptr(s[0:1]), float(self.max_grad_norm), float(self.grad_scale),
                                       _hip.ptr(s[1:2]), _hip.ptr(s[2:3]), _hip.stream()), "clip_coef")
             self.last_grad_norm = s[2]
@@ -91,7 +96,12 @@ class _FlatOptimizer(torch.optim.Optimizer):
         g = self.flat.grad.float()
         scale = self.grad_scale
         if self.max_grad_norm > 0:
-            nrm = float(g.norm()) * self.grad_scale
+            sq = (g * g).sum().reshape(1)
+            if getattr(self.flat, "norm_reduce", False):
+                import torch.distributed as dist
+
+                dist.all_reduce(sq, group=self.flat.norm_group)
+            nrm = float(sq.sqrt()) * self.grad_scale
             self.last_grad_norm = torch.tensor(nrm)
             scale *= min(1.0, self.max_grad_norm / (nrm + 1e-6))
         return scale

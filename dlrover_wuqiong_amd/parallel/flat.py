@@ -36,7 +36,8 @@ class FlatParams:
     def __init__(self, module: nn.Module, dtype: Optional[torch.dtype] = None, device=None,
                  no_decay_fn: Callable[[str, torch.Tensor], bool] = default_no_decay,
                  grad_dtype: Optional[torch.dtype] = None, direct_grads: bool = True,
-                 lazy_zero_grad: Optional[bool] = None):
+                 lazy_zero_grad: Optional[bool] = None, named: Optional[List[Tuple[str, nn.Parameter]]] = None,
+                 pad_to: int = ALIGN, data: Optional[torch.Tensor] = None, grad: Optional[torch.Tensor] = None):
         """``direct_grads``: the fused ops (``ops/linear.py``, norms, bias
         activations) accumulate straight into the flat ``.grad`` views
         (``ops/_grad.py``); call ``zero_grad()`` (not ``set_to_none``) once
@@ -46,10 +47,17 @@ class FlatParams:
         next backward's first contributions overwrite -- gradients read
         between ``zero_grad()`` and the end of the next backward are
         undefined, and gradients written by hand after ``zero_grad()`` need
-        the eager default."""
-        named = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
-        # tied weights appear once in named_parameters (dedup by identity)
-        named.reverse()
+        the eager default.
+
+        Flat-unit FSDP (``parallel/flat_fsdp.py``) builds one per unit:
+        ``named`` (an explicit parameter list, in buffer order) instead of
+        the module's, ``pad_to`` (the buffer's numel rounded up to a multiple,
+        world x 64 there) and ``data`` / ``grad`` (caller-owned buffers of
+        that numel, e.g. a slice of the rank's shard buffer at world 1)."""
+        if named is None:
+            named = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
+            # tied weights appear once in named_parameters (dedup by identity)
+            named.reverse()
         first = named[0][1] if named else None
         self.dtype = dtype or (first.dtype if first is not None else torch.float32)
         self.grad_dtype = grad_dtype or self.dtype
@@ -64,9 +72,14 @@ class FlatParams:
             self.params.append(p)
             self.offsets.append((off, p.numel()))
             off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
-        self.numel = off
-        self.data = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
-        self.grad = torch.zeros(self.numel, dtype=self.grad_dtype, device=self.device)
+        self.numel = (off + pad_to - 1) // pad_to * pad_to
+        if data is None:
+            data = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
+        if grad is None:
+            grad = torch.zeros(self.numel, dtype=self.grad_dtype, device=self.device)
+        if data.numel() != self.numel or grad.numel() != self.numel:
+            raise ValueError(f"FlatParams: buffers of {data.numel()} / {grad.numel()} elements, {self.numel} needed")
+        self.data, self.grad = data, grad
         mask = torch.ones(max(1, self.numel // ALIGN), dtype=torch.uint8)
         for n, p, (o, c) in zip(self.names, self.params, self.offsets):
             view = self.data[o:o + c].view_as(p)
