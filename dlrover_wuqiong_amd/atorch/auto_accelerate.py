@@ -197,12 +197,30 @@ def _replace_norms(model: nn.Module):
     return n
 
 
+def _replace_linears(model: nn.Module) -> int:
+    """Plain ``nn.Linear`` -> ``ops.linear.FusedLinear`` (same module, class
+    swapped): once a flat buffer owns the weight (FlatParams / FlatFSDP set
+    ``_dwamd_direct``) the weight gradient GEMM accumulates straight into the
+    flat gradient on a side stream; otherwise it is ``F.linear`` as before.
+    Without it autograd zero-fills and then adds every weight gradient (two
+    extra passes per projection: 10 ms per Llama-3-8B step)."""
+    from ..ops.linear import FusedLinear
+
+    n = 0
+    for m in model.modules():
+        if type(m) is nn.Linear:
+            m.__class__ = FusedLinear
+            n += 1
+    return n
+
+
 def _apply_module_replace(ctx, cfg):
     from .hf_attention import enable_dwamd_attention
 
     n = _replace_norms(ctx["model"])
+    nl = _replace_linears(ctx["model"])
     hf = enable_dwamd_attention(ctx["model"])
-    logger.info(f"module_replace: {n} norm layers -> fused HIP norms"
+    logger.info(f"module_replace: {n} norm layers -> fused HIP norms, {nl} Linear -> FusedLinear"
                 + ("; HF attention -> MFMA flash attention" if hf else ""))
 
 

@@ -239,7 +239,9 @@ class FlatFSDP(nn.Module):
             if self._fwd_order is None:
                 self._recording.append(u.idx)
             self._issue_gather(u)
-            nxt = self._neighbour(u, +1)
+            # (not in an activation-checkpoint recompute inside the backward:
+            # the next unit in forward order has finished its backward there)
+            nxt = None if _in_backward() else self._neighbour(u, +1)
             if nxt is not None:
                 self._issue_gather(nxt)  # overlaps this unit's forward
             self._ensure(u)
@@ -247,7 +249,9 @@ class FlatFSDP(nn.Module):
 
     def _make_post_forward(self, u: _Unit):
         def hook(_m, _args, out):
-            if not torch.is_grad_enabled():
+            if not torch.is_grad_enabled() or _in_backward():
+                # no_grad forward, or the recompute of an activation-checkpointed
+                # unit inside its backward: the parameters stay until its gradients
                 return None
             self._release(u)
             if self.reshard:
@@ -326,6 +330,9 @@ class FlatFSDP(nn.Module):
                 self._fwd_order = list(self._recording)
             self._recording = []
             for u in self.units:
+                if u.work is not None:  # a gather issued before the optimizer step: stale
+                    u.work.wait()
+                    u.work = None
                 u.fresh = False  # the optimizer may have updated the shards
             for u in self.units:
                 if u.is_root:
@@ -374,6 +381,13 @@ class FlatFSDP(nn.Module):
         for h in self._handles:
             h.remove()
         self._handles = []
+
+
+def _in_backward() -> bool:
+    try:
+        return torch._C._current_graph_task_id() != -1
+    except AttributeError:  # pragma: no cover
+        return False
 
 
 def _flatten(x):

@@ -44,6 +44,9 @@ def main():
                    help="each FSDP unit's AdamW update from its post-backward reduce-scatter on a side stream "
                         "(optimizers/in_backward.py)")
     p.add_argument("--no-ckpt", action="store_true", help="step time only (no flash checkpoints)")
+    p.add_argument("--flat", action="store_true",
+                   help="flat-unit FSDP (auto_accelerate flat_zero2 / flat_fsdp, parallel/flat_fsdp.py: in-place "
+                        "collectives, fused optimizer over the rank shard) + flat-shard flash checkpoints")
     p.add_argument("--fp8", action="store_true", help="auto_accelerate 'fp8' on the decoder layers' projections")
     p.add_argument("--storage", action="store_true",
                    help="also persist and time the storage restore (fast O_DIRECT reader vs stock dist_cp.load)")
@@ -83,18 +86,22 @@ def main():
             model = Llama(cfg)
         layer_cls = LlamaDecoderLayer
     prec = ("amp_native", {"dtype": torch.bfloat16}) if a.precision == "amp" else "half"
+    if a.flat and (a.precision != "half" or a.optim_in_backward or a.torch_optim):
+        raise SystemExit("--flat: bf16 parameters (--precision half) and the fused flat optimizer only")
+    shard = ("flat_fsdp" if a.reshard == "on" else "flat_zero2") if a.flat else (
+        "fsdp" if a.reshard == "on" else "zero2")
+    scfg = {"wrap_cls": (layer_cls,)} if a.flat else {"wrap_cls": (layer_cls,), "optim_in_backward": a.optim_in_backward}
     ok, res, strategy = auto_accelerate(
         model, torch.optim.AdamW, optim_args={"lr": 2e-5, "betas": (0.9, 0.95), "weight_decay": 0.1},
         load_strategy=["module_replace", prec] + ([("fp8", {"include": ("layers", "h.")})] if a.fp8 else []) + [
-                       ("fsdp" if a.reshard == "on" else "zero2",
-                        {"wrap_cls": (layer_cls,), "optim_in_backward": a.optim_in_backward})]
+                       (shard, scfg)]
         + ([("checkpoint", {"wrap_cls": (layer_cls,)})] if a.act_ckpt == "on" else []),
         fused_optimizer=not a.torch_optim)
     assert ok, "auto_accelerate failed"
     model, opt = res.model, res.optim
     g = torch.Generator().manual_seed(rank)
     data = torch.randint(0, cfg.vocab_size, (2, a.micro_batch, a.seq + 1), generator=g).to(dev)
-    ck = FsdpShardCheckpointer(a.ckpt_dir)
+    ck = None if a.flat else FsdpShardCheckpointer(a.ckpt_dir)
 
     def sync():
         # the training stream only: a device-wide synchronize would also wait
@@ -127,10 +134,15 @@ def main():
             print(json.dumps({"metric": "fsdp train step", "n_gpus": world, "model": a.model, "seq_len": a.seq,
                               "precision": a.precision + ("+fp8" if a.fp8 else ""), "optimizer": type(opt).__name__,
                               "optim_in_backward": getattr(opt, "_in_backward", None) is not None,
-                              "act_ckpt": a.act_ckpt, "reshard_after_forward": a.reshard == "on", "train_step_ms": round(1000 * med, 1),
+                              "act_ckpt": a.act_ckpt, "reshard_after_forward": a.reshard == "on",
+                              "fsdp": "flat" if a.flat else "fsdp2", "train_step_ms": round(1000 * med, 1),
                               "tokens_per_s": round(world * a.micro_batch * a.seq / med, 1),
                               "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if cuda else None,
                               "step_ms": [round(1000 * x, 1) for x in steps], "losses": [round(x, 3) for x in losses]}))
+        dist.destroy_process_group()
+        return
+    if a.flat:
+        _flat_ckpt_run(a, model, opt, step, sync, rank, world, cuda, strategy)
         dist.destroy_process_group()
         return
     ts = time.perf_counter()
@@ -248,6 +260,76 @@ def main():
             "losses": [round(x, 3) for x in losses]}))
     ck.close()
     dist.destroy_process_group()
+
+
+def _flat_ckpt_run(a, model, opt, step, sync, rank, world, cuda, strategy):
+    """Flash checkpoints of a FlatFSDP model in the flat-shard format
+    (atorch/fsdp_flat_ckpt.py): the live shard + fused-optimizer state
+    buffers are the state, restored in place from memory."""
+    from dlrover_wuqiong_amd.atorch import fsdp_flat_ckpt as ffc
+    from dlrover_wuqiong_amd.flash_checkpoint.checkpointer import StorageType
+
+    eng = ffc._engine(a.ckpt_dir)
+
+    def save(i):
+        return ffc.save_checkpoint(i, model, opt, os.path.join(a.ckpt_dir, f"step-{i}"),
+                                   storage_type=StorageType.MEMORY)
+
+    ts = time.perf_counter()
+    save(0)  # untimed: shm set-up
+    sync()
+    eng.wait_for_memory_save()
+    setup_s = time.perf_counter() - ts
+    pauses, steps, losses, landed = [], [], [], []
+    for i in range(a.steps):
+        t0 = time.perf_counter()
+        losses.append(float(step(i).item()))
+        sync()
+        steps.append(time.perf_counter() - t0)
+        if i % a.ckpt_interval == 0:
+            t0 = time.perf_counter()
+            ok = save(i + 1)
+            sync()
+            pauses.append(time.perf_counter() - t0)
+            landed.append(bool(ok))
+    last = a.steps + 1
+    eng.wait_for_memory_save()
+    save(last)
+    eng.wait_for_memory_save()
+    if cuda:
+        torch.cuda.synchronize()
+    live = (model.shard_flat.data, opt.exp_avg, opt.exp_avg_sq) + ((opt.master,) if opt.master is not None else ())
+
+    def fingerprint(t):  # bit-exact sum of the raw words: no full-size clone next to a 100+ GB state
+        w = t.view(torch.int16 if t.element_size() == 2 else torch.int32)
+        return int(torch.sum(w, dtype=torch.int64)), int(torch.sum(w[1::7], dtype=torch.int64))
+
+    want = [fingerprint(t) for t in live]
+    with torch.no_grad():
+        for t in live:
+            t.zero_()
+    sync()
+    t0 = time.perf_counter()
+    got = ffc.load_checkpoint(model, opt, os.path.join(a.ckpt_dir, f"step-{last}"))
+    if cuda:
+        torch.cuda.synchronize()
+    load_s = time.perf_counter() - t0
+    verified = got == last and [fingerprint(t) for t in live] == want
+    med = sorted(steps)[len(steps) // 2]
+    if rank == 0:
+        ok_p = [p for p, ok in zip(pauses, landed) if ok]
+        print(json.dumps({
+            "metric": "fsdp flash ckpt pause s", "unit": "s", "value": round(sum(ok_p) / max(1, len(ok_p)), 4),
+            "higher_is_better": False, "n_gpus": world, "dtype": "bf16 params, fp32 masters", "fsdp": "flat",
+            "optimizer": type(opt).__name__, "data": "synthetic tokens, random-init weights",
+            "config": {"model": a.model, "seq_len": a.seq, "micro_batch": a.micro_batch, "strategy": str(strategy)[:300]},
+            "save_sec": [round(x, 4) for x in pauses], "setup_save_s": round(setup_s, 2), "saves_landed": landed,
+            "load_sec": round(load_s, 3), "load_verified": bool(verified),
+            "ckpt_bytes_per_rank": int(sum(t.numel() * t.element_size() for t in live)),
+            "train_step_ms": round(1000 * med, 1), "tokens_per_s": round(world * a.micro_batch * a.seq / med, 1),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if cuda else None,
+            "step_ms": [round(1000 * x, 1) for x in steps], "losses": [round(x, 3) for x in losses]}))
+    ffc.close_engines()
 
 
 if __name__ == "__main__":

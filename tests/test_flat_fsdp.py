@@ -55,7 +55,7 @@ def _reference(micro=1):
     return losses, {n: p.detach().clone() for n, p in m.named_parameters()}
 
 
-def _train_worker(rank, world, port, reshard, micro, q):
+def _train_worker(rank, world, port, reshard, micro, act_ckpt, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -64,6 +64,12 @@ def _train_worker(rank, world, port, reshard, micro, q):
         from dlrover_wuqiong_amd.parallel.flat_fsdp import FlatFSDP
 
         m, cfg = _gpt2()
+        if act_ckpt:  # recomputed in the backward, after the unit's storage was released
+            from torch.distributed.algorithms._checkpoint.checkpoint_wrapper import (
+                apply_activation_checkpointing, checkpoint_wrapper)
+
+            apply_activation_checkpointing(m, checkpoint_wrapper_fn=checkpoint_wrapper,
+                                           check_fn=lambda mod: isinstance(mod, Block))
         model = FlatFSDP(m, wrap_cls=(Block,), reshard_after_forward=reshard)
         opt = FusedAdamW(model.shard_flat, lr=1e-2, weight_decay=0.05, max_grad_norm=0.5)
         opt.grad_scale = 1.0 / (world * micro)  # summed over ranks and accumulated micro-batches
@@ -114,15 +120,27 @@ def _spawn(target, world, *args):
     return [r for r in res if r is not None]
 
 
-@pytest.mark.parametrize("world,reshard,micro", [(1, False, 1), (2, False, 1), (2, True, 1), (2, True, 2)])
-def test_flat_fsdp_matches_one_process(world, reshard, micro):
+@pytest.mark.parametrize("world,reshard,micro,act_ckpt", [(1, False, 1, False), (2, False, 1, False),
+                                                         (2, True, 1, False), (2, True, 2, False),
+                                                         (2, True, 1, True), (4, True, 1, False)])
+def test_flat_fsdp_matches_one_process(world, reshard, micro, act_ckpt):
     ref_losses, ref_params = _reference(micro=world * micro)
-    (losses, params, released), = _spawn(_train_worker, world, reshard, micro)
+    (losses, params, released), = _spawn(_train_worker, world, reshard, micro, act_ckpt)
     assert losses == pytest.approx(ref_losses, rel=1e-5, abs=1e-5)
     for n, p in ref_params.items():
-        torch.testing.assert_close(torch.from_numpy(params[n]), p, rtol=2e-4, atol=2e-4, msg=n)
+        torch.testing.assert_close(torch.from_numpy(params[_plain(n, params)]), p, rtol=2e-4, atol=2e-4, msg=n)
     # ZeRO-3: the layers' gathered storage is released between steps
     assert all(released) == (reshard and world > 1)
+
+
+def _plain(name, params):
+    """``name`` as the (possibly activation-checkpoint-wrapped) model spells it."""
+    if name in params:
+        return name
+    for k in params:
+        if k.replace("_checkpoint_wrapped_module.", "") == name:
+            return k
+    raise KeyError(name)
 
 
 def test_flat_fsdp_world1_is_the_shard():
