@@ -809,7 +809,7 @@ def _flat_optimizer(fs, optim_func, args):
         if "max_grad_norm" in a:
             kw["max_grad_norm"] = a["max_grad_norm"]
         return FusedAdamW(fs.shard_flat, adamw=name != "Adam", **kw)
-    if name in ("AGD", "FusedAGD"):
+    if name in ("AGD", "FusedAGD", "MultiTensorAGD"):
         kw = {k: a[k] for k in ("lr", "betas", "delta", "weight_decay") if k in a}
         return FusedAGD(fs.shard_flat, **kw)
     raise ValueError(f"flat_fsdp: no fused flat optimizer for {name} (AdamW / Adam / AGD)")

@@ -62,6 +62,8 @@ def parse_args(argv=None):
     p.add_argument("--optim_grouped_params", action="store_true")
     p.add_argument("--log_interval", type=int, default=10)
     p.add_argument("--use_fsdp", action="store_true")
+    p.add_argument("--use_flat_fsdp", action="store_true",
+                   help="flat-unit FSDP (one flat buffer per layer, in-place collectives, fused optimizer)")
     p.add_argument("--use_amp", action="store_true")
     p.add_argument("--use_fp8", action="store_true")
     p.add_argument("--use_checkpointing", action="store_true")
@@ -96,6 +98,8 @@ def build_strategy(args, model_type):
                                outer_optim_class=torch.optim.SGD if args.outer_optim_class == "sgd" else None,
                                outer_optim_kwargs={"lr": 0.7, "momentum": 0.8, "nesterov": True})
         strategy.append(("fsdp", fsdp_config))
+    if args.use_flat_fsdp:
+        strategy.append(("flat_fsdp", {"wrap_cls": (get_module_type(model_type),), "reshard_after_forward": True}))
     if args.use_amp:
         strategy.append(("amp_native", {"dtype": torch.bfloat16}))
     if args.use_checkpointing:

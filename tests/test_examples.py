@@ -57,6 +57,15 @@ def test_auto_accelerate_example_fsdp_two_ranks():
     _losses(out)
 
 
+def test_auto_accelerate_example_flat_fsdp_two_ranks():
+    out = _run(["train.py", "--model_type", "llama", "--distributed", "--load_strategy", "--use_flat_fsdp",
+                "--max_steps", "4", "--layer_num", "2", "--log_interval", "1"],
+               os.path.join(EX, "auto_accelerate"), nproc=2)
+    assert "strategy: ['parallel_mode', 'flat_fsdp']" in out, out[-2000:]
+    first, last = _losses(out)
+    assert abs(first) < 20 and abs(last) < 20
+
+
 def test_llama2_fsdp_example():
     out = _run(["fsdp_llama2.py", "--max_steps", "3", "--gradient_checkpointing"], os.path.join(EX, "llama2"))
     assert out.count("iter ") == 3
