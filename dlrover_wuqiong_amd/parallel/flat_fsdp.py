@@ -31,8 +31,14 @@ the parameters outside every unit) is ONE flat buffer:
   forward and re-gathered when its backward starts (the storage-resize trick
   of FSDP: saved tensors are views of the same storage); the next unit's
   gather is prefetched (forward order recorded by the first forward, reverse
-  order in backward).  Without it (ZeRO-2) the gathered parameters stay from
-  the forward to the end of the backward.  The root stays gathered.
+  order in backward).  ZeRO-3 also gives a layer's unsharded gradient buffer
+  back once its reduce-scatter has completed and takes it again when the
+  layer's backward starts, so neither full-size buffer outlives its use
+  (``p.grad`` of a wrapped parameter is then only valid inside the backward:
+  the gradient is the shard's, ``shard_flat.grad``; clip through the
+  optimizer's ``max_grad_norm``).  Without resharding (ZeRO-2) the gathered
+  parameters and the unsharded gradients stay, as in DDP.  The root stays
+  gathered.
 
 Readiness of a unit's gradient is counted like ``FlatDDP``'s buckets: the
 first backward records how often each parameter's post-accumulate hook
@@ -63,13 +69,15 @@ from .flat import ALIGN, FlatParams, default_no_decay
 
 class _Unit:
     __slots__ = ("idx", "module", "flat", "full", "gfull", "shard", "shard_grad", "base", "lo", "len", "work",
-                 "fresh", "released", "rs_work", "nbytes", "is_root", "names")
+                 "fresh", "released", "rs_work", "nbytes", "is_root", "names", "reduced", "grad_released")
 
     def __init__(self, idx, module, is_root):
         self.idx, self.module, self.is_root = idx, module, is_root
         self.work = self.rs_work = None
         self.fresh = False  # ``full`` holds the current shards' values
         self.released = False
+        self.reduced = False  # reduce-scatter launched in this backward
+        self.grad_released = False  # ``gfull``'s storage given back (ZeRO-3)
 
 
 class ShardFlat:
@@ -193,6 +201,8 @@ class FlatFSDP(nn.Module):
         self._recording: List[int] = []
         self._expected: Optional[List[int]] = None
         self._calls = [0] * len(self.units)
+        self._inflight: List[_Unit] = []  # reduce-scatters not yet known complete
+        self.free_grads = self.reshard
         self._handles = []
         if self.world > 1:
             for u in self.units:
@@ -254,14 +264,41 @@ class FlatFSDP(nn.Module):
                 # unit inside its backward: the parameters stay until its gradients
                 return None
             self._release(u)
-            if self.reshard:
+            if self.reshard or self.free_grads:
                 ts = [t for t in _flatten(out) if torch.is_tensor(t) and t.requires_grad]
                 if ts:
                     torch.autograd.graph.register_multi_grad_hook(ts, lambda _g: self._pre_backward(u), mode="any")
             return None
         return hook
 
+    def _take_grad(self, u: _Unit):
+        if not u.grad_released:
+            return
+        u.gfull.untyped_storage().resize_(u.nbytes)
+        u.grad_released = False
+        if not u.flat._fresh:  # no gradient generation open (no zero_grad since the last step): start from 0
+            u.gfull.zero_()
+
+    def _give_grad(self, u: _Unit):
+        if self.free_grads and self._sync and not u.is_root and not u.grad_released:
+            u.gfull.untyped_storage().resize_(0)
+            u.grad_released = True
+
+    def _drain(self, block: bool):
+        """Reduce-scatters known complete (all of them with ``block``):
+        their unsharded gradient buffers can be given back."""
+        keep = []
+        for v in self._inflight:
+            if block or v.rs_work.is_completed():
+                v.rs_work.wait()  # orders this stream after the collective
+                v.rs_work = None
+                self._give_grad(v)
+            else:
+                keep.append(v)
+        self._inflight = keep
+
     def _pre_backward(self, u: _Unit):
+        self._take_grad(u)
         self._issue_gather(u)
         prev = self._neighbour(u, -1)
         if prev is not None:
@@ -273,7 +310,7 @@ class FlatFSDP(nn.Module):
         def hook(_p):
             if not self._sync:
                 return
-            if u.rs_work is not None:
+            if u.reduced:
                 raise RuntimeError(f"FlatFSDP: a gradient of unit {u.idx} arrived after its reduce-scatter "
                                    "(a parameter used more often than in the first backward)")
             self._calls[u.idx] += 1
@@ -283,10 +320,14 @@ class FlatFSDP(nn.Module):
         return hook
 
     def _reduce(self, u: _Unit):
+        self._take_grad(u)  # (a unit whose backward never ran: its gradient is zero)
         u.flat.finalize_grads()  # lazily zeroed gradients nobody wrote
         u.rs_work = dist.reduce_scatter_tensor(u.shard_grad, u.gfull, group=self.pg, async_op=True)
+        u.reduced = True
+        self._inflight.append(u)
         if not u.is_root:
             self._release(u)
+        self._drain(block=False)
 
     def finish_gradient_sync(self):
         """Every unit's gradient reduced into the shard gradient (launching
@@ -301,11 +342,11 @@ class FlatFSDP(nn.Module):
         if self._expected is None:
             self._expected = list(self._calls)
         for u in self.units:
-            if u.rs_work is None:
+            if not u.reduced:
                 self._reduce(u)
+        self._drain(block=True)
         for u in self.units:
-            u.rs_work.wait()
-            u.rs_work = None
+            u.reduced = False
         self._calls = [0] * len(self.units)
 
     @contextmanager
@@ -321,6 +362,8 @@ class FlatFSDP(nn.Module):
 
     def zero_grad(self):
         for u in self.units:
+            if u.grad_released and not u.flat.lazy_zero:
+                continue  # no storage: _take_grad zeroes it when the backward takes it again
             u.flat.zero_grad()
 
     # ------------------------------------------------------------- forward

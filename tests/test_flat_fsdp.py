@@ -91,7 +91,8 @@ def _train_worker(rank, world, port, reshard, micro, act_ckpt, q):
             dist.all_reduce(tot)
             losses.append(float(tot) / (world * micro))
         sd = model.full_state_dict()
-        released = [u.released for u in model.units if not u.is_root]
+        released = [u.released and u.grad_released and u.gfull.untyped_storage().size() == 0
+                    for u in model.units if not u.is_root]
         if rank == 0:
             q.put((losses, {k: v.float().numpy() for k, v in sd.items()}, released))
         else:
@@ -129,7 +130,7 @@ def test_flat_fsdp_matches_one_process(world, reshard, micro, act_ckpt):
     assert losses == pytest.approx(ref_losses, rel=1e-5, abs=1e-5)
     for n, p in ref_params.items():
         torch.testing.assert_close(torch.from_numpy(params[_plain(n, params)]), p, rtol=2e-4, atol=2e-4, msg=n)
-    # ZeRO-3: the layers' gathered storage is released between steps
+    # ZeRO-3: the layers' gathered parameters and unsharded gradients are released between steps
     assert all(released) == (reshard and world > 1)
 
 
