@@ -631,6 +631,159 @@ norm_bwd_part_kernel(
   }
 }
 
+// Norm backward for 1024 < H < 2048 with TWO waves per row.  The one-wave
+// form (VPL = 4 above) holds 4 vectors x 3 arrays of a row per lane plus 96
+// per-lane column accumulators: ~310 VGPRs, one wave per SIMD, latency-bound
+// at ~3 TB/s (GPT2-1.5B's H = 1600: 34.5 us per call in the step).  Here a
+// row is split between a wave pair (each wave 2 vectors per lane = half the
+// columns): 48 accumulators, 180-242 VGPRs, two waves per SIMD; the row
+// reductions (sum g, sum g a) combine through LDS with one barrier per row
+// step (parity double-buffered).  One 8-wave workgroup per CU (4 rows in
+// flight, the next row of each pair prefetched) keeps ONE partial row per
+// workgroup, as many as the one-wave form: the column-sum pass is unchanged.
+// Deterministic: a fixed row order per pair and a fixed half-0 + half-1
+// order for the row sums.
+#ifndef DWAMD_NORM_BWD_PAIR_WAVES
+#define DWAMD_NORM_BWD_PAIR_WAVES 8
+#endif
+template <bool RMS, bool DS>
+__global__ void __launch_bounds__(64 * DWAMD_NORM_BWD_PAIR_WAVES, 1)
+norm_bwd_pair_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ gamma,
+                     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+                     const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx, float* __restrict__ part,
+                     int64_t rows, int H) {
+  constexpr int NW = DWAMD_NORM_BWD_PAIR_WAVES, NP = NW / 2;
+  __shared__ float xch[2][NP][2][2];  // [parity][pair][half][sum g, sum g a]
+  __shared__ float red[NW][1024];     // per-wave column partials of one array (final reduction)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int pair = wid >> 1, half = wid & 1;
+  const int nv = H >> 3;
+  float ag[2][8], ab[2][8], ad[2][8];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ag[j][k] = ab[j][k] = ad[j][k] = 0.f;
+  // this lane's vectors: half * 128 + lane + 64 j (j < 2) cover 0 .. 255
+  int vc[2];
+  bool vok[2];
+  u32x4 gv[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    vc[j] = 128 * half + lane + 64 * j;
+    vok[j] = vc[j] < nv;
+    gv[j] = vok[j] ? *(const u32x4*)(gamma + vc[j] * 8) : (u32x4){0, 0, 0, 0};
+  }
+  struct Row {
+    u32x4 x[2], d[2], r[2];
+    float mu, rs;
+  };
+  auto load = [&](Row& b, int64_t row) {
+    if (row >= rows) return;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (vok[j]) {
+        b.x[j] = *(const u32x4*)(x + row * H + vc[j] * 8);
+        b.d[j] = *(const u32x4*)(dy + row * H + vc[j] * 8);
+        if (dres) b.r[j] = *(const u32x4*)(dres + row * H + vc[j] * 8);
+      }
+    }
+    b.mu = RMS ? 0.f : mean_in[row];
+    b.rs = rstd_in[row];
+  };
+  auto process = [&](const Row& b, int64_t row, int it) {
+    const bool ok = row < rows;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (ok && vok[j]) {
+        float xf[8], df[8], gm[8];
+        unpack8(b.x[j], xf);
+        unpack8(b.d[j], df);
+        unpack8(gv[j], gm);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float a = (xf[k] - b.mu) * b.rs, g = df[k] * gm[k];
+          ag[j][k] += df[k] * a;
+          if constexpr (!RMS) ab[j][k] += df[k];
+          s1 += g;
+          s2 += g * a;
+        }
+      }
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    float(*xc)[2][2] = xch[it & 1];
+    if (lane == 0) {
+      xc[pair][half][0] = s1;
+      xc[pair][half][1] = s2;
+    }
+    __syncthreads();  // the only barrier of the row step (the slot of step it-1 stays untouched)
+    const float m1 = RMS ? 0.f : (xc[pair][0][0] + xc[pair][1][0]) / (float)H;
+    const float m2 = (xc[pair][0][1] + xc[pair][1][1]) / (float)H;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (ok && vok[j]) {
+        float xf[8], df[8], gm[8], o[8];
+        unpack8(b.x[j], xf);
+        unpack8(b.d[j], df);
+        unpack8(gv[j], gm);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = b.rs * (df[k] * gm[k] - m1 - (xf[k] - b.mu) * b.rs * m2);
+        if (dres) {
+          float r[8];
+          unpack8(b.r[j], r);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] += r[k];
+        }
+        if constexpr (DS) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) ad[j][k] += o[k];
+        }
+        *(u32x4*)(dx + row * H + vc[j] * 8) = pack8(o);
+      }
+    }
+  };
+  // every wave of the workgroup runs the same number of row steps (barriers)
+  const int64_t stride = (int64_t)gridDim.x * NP;
+  const int64_t first = (int64_t)blockIdx.x * NP;
+  const int n_it = first < rows ? (int)((rows - first + stride - 1) / stride) : 0;
+  int64_t row = first + pair;
+  Row A, B;
+  load(A, row);
+  for (int it = 0; it < n_it; ++it) {
+    if (it & 1) {
+      load(A, row + stride);
+      process(B, row, it);
+    } else {
+      load(B, row + stride);
+      process(A, row, it);
+    }
+    row += stride;
+  }
+  // column partials of the workgroup: the 6 waves of each half summed in a fixed order
+  float* prow = part + (int64_t)blockIdx.x * (DS ? 3 : 2) * H;
+  auto reduce = [&](const float (*acc)[8], int off) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[wid][8 * (lane + 64 * j) + k] = acc[j][k];
+    __syncthreads();
+    for (int c = threadIdx.x; c < H; c += 64 * NW) {
+      const int h = c >> 10, lc = c & 1023;
+      float sum = 0.f;
+#pragma unroll
+      for (int p2 = 0; p2 < NP; ++p2) sum += red[2 * p2 + h][lc];
+      prow[off + c] = sum;
+    }
+    __syncthreads();
+  };
+  reduce(ag, 0);
+  if constexpr (!RMS) reduce(ab, H);
+  else
+    for (int c = threadIdx.x; c < H; c += 64 * NW) prow[H + c] = 0.f;
+  if constexpr (DS) reduce(ad, 2 * H);
+}
+
 // Column sums of fp32 partials [R, 2H] into out0 (columns 0..H-1) and out1
 // (H..2H-1, may be null): thread = column, grid.y splits the rows; one
 // atomic per (column, row-split) into ws, the last row-split block of each
@@ -851,6 +1004,35 @@ extern "C" int dw_norm_bwd3(const void* dy, const void* x, const void* gamma, co
     return dw_norm_bwd2(dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, ws, rows, H, rms, out_fp32, accumulate,
                         stream, det);
   hipStream_t s = (hipStream_t)stream;
+  static const bool pair_on = [] {  // A/B: DWAMD_NORM_BWD_PAIR=0 keeps the one-wave-per-row kernel
+    const char* e = getenv("DWAMD_NORM_BWD_PAIR");
+    return !(e && e[0] == '0');
+  }();
+  if (pair_on && H > 1024 && H < 2048) {
+    constexpr int NP = DWAMD_NORM_BWD_PAIR_WAVES / 2;
+    const int64_t nbp = std::min<int64_t>((rows + NP - 1) / NP, 256);  // one workgroup per CU, resident
+    if (nbp * pw * H <= part_floats) {
+#define NBW(RM, DSV)                                                                                          \
+  hipLaunchKernelGGL((norm_bwd_pair_kernel<RM, DSV>), dim3((unsigned)nbp), dim3(64 * DWAMD_NORM_BWD_PAIR_WAVES), 0, \
+                     s, (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)gamma,                           \
+                     RM ? nullptr : (const float*)mean, (const float*)rstd, (const bf16_t*)dres, (bf16_t*)dx,      \
+                     (float*)part, rows, H)
+      if (rms) {
+        if (dsum) NBW(true, true); else NBW(true, false);
+      } else {
+        if (dsum) NBW(false, true); else NBW(false, false);
+      }
+#undef NBW
+      if (dsum_done) *dsum_done = dsum ? 1 : 0;
+      const int H2 = pw * H;
+      const int splits = (int)colsum_f32_splits(nbp);
+      const int per = (int)((nbp + splits - 1) / splits);
+      dim3 g((H2 + 255) / 256, (unsigned)((nbp + per - 1) / per));
+      hipLaunchKernelGGL(colsum_f32_kernel, g, dim3(256), 0, s, (const float*)part, (int)nbp, H2, per, (float*)ws,
+                         dgamma, rms ? nullptr : dbeta, out_fp32, accumulate, H, dsum, acc2, (float*)det);
+      DW_LAUNCH_RET;
+    }
+  }
 #define NBP(RM, DSV)                                                                                          \
   hipLaunchKernelGGL((norm_bwd_part_kernel<VPL, RM, DSV>), dim3((unsigned)nb), dim3(256), 0, s,              \
                      (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)gamma, RM ? nullptr : (const float*)mean, \
