@@ -742,13 +742,18 @@ def _apply_flat_fsdp(ctx, cfg, reshard=True):
 
     cfgd = dict(cfg) if isinstance(cfg, dict) else {}
     model = ctx["model"]
-    if _meta_model(model):
-        raise RuntimeError("flat_fsdp: materialise the model first (meta-device init needs fsdp / zero2)")
-    model = model.to(_device())  # the flat buffers are built where the parameters are
+    meta = _meta_model(model)
+    if not meta:
+        model = model.to(_device())  # the flat buffers are built where the parameters are
     pg = ctx.get("dp_group") if dist.is_initialized() else None
+    # a meta-device model is materialised per shard (sharding-invariant
+    # counter-based init, atorch/meta_init.py); init_seed / buffer_init_fn as for fsdp
     ctx["model"] = FlatFSDP(model, wrap_cls=_wrap_cls(ctx, cfg), process_group=pg,
                             reshard_after_forward=cfgd.get("reshard_after_forward", reshard),
-                            sync_module_states=cfgd.get("sync_module_states", True))
+                            sync_module_states=cfgd.get("sync_module_states", True), device=_device(),
+                            init_seed=int(cfgd.get("init_seed", 0)), buffer_init_fn=cfgd.get("buffer_init_fn"))
+    if meta:
+        ctx["meta_init"] = "flat_deterministic"
     ctx["flat_fsdp"] = ctx["model"]
     ctx["fsdp"] = True  # no DDP on top; autocast is the caller's (use "half": bf16 parameters)
 

@@ -84,7 +84,8 @@ class FlatParams:
         for n, p, (o, c) in zip(self.names, self.params, self.offsets):
             view = self.data[o:o + c].view_as(p)
             with torch.no_grad():
-                view.copy_(p.data.to(self.device, self.dtype))
+                if not p.is_meta:  # (a meta-device model: the owner fills the buffer, parallel/flat_fsdp.py)
+                    view.copy_(p.data.to(self.device, self.dtype))
             p.data = view
             p.grad = self.grad[o:o + c].view_as(p)
             p._dwamd_direct = bool(direct_grads)

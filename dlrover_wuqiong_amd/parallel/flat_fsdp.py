@@ -112,7 +112,16 @@ class FlatFSDP(nn.Module):
     def __init__(self, module: nn.Module, wrap_cls: Sequence[type] = (), process_group=None,
                  reshard_after_forward: bool = True, prefetch: bool = True,
                  no_decay_fn: Callable[[str, torch.Tensor], bool] = default_no_decay,
-                 sync_module_states: bool = True):
+                 sync_module_states: bool = True, device=None, init_seed: int = 0,
+                 buffer_init_fn: Optional[Callable] = None):
+        """A ``module`` built on the meta device (``torch.device("meta")``)
+        is materialised per shard: each rank allocates only its shard (and,
+        without resharding, the unit buffers it gathers into) on ``device``
+        and fills its element range of every parameter from the sharding-
+        invariant counter-based streams of ``atorch/meta_init.py``
+        (``init_spec`` of the model, else the module type), so a Llama-3-70B
+        job never builds the whole model in fp32 on any rank; meta buffers
+        are rebuilt as ``meta_init`` does (``buffer_init_fn``)."""
         super().__init__()
         self.module = module
         self.pg = process_group
@@ -125,7 +134,12 @@ class FlatFSDP(nn.Module):
         params_all = [p for p in module.parameters()]
         if not params_all:
             raise ValueError("FlatFSDP: the module has no parameters")
+        meta = any(p.is_meta for p in params_all)
         dev = params_all[0].device
+        if meta:
+            dev = torch.device(device) if device is not None else (
+                torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+            self._materialize_buffers(module, dev, buffer_init_fn)
         dtype = params_all[0].dtype
         if any(p.dtype != dtype for p in params_all if p.requires_grad):
             raise ValueError("FlatFSDP: every trainable parameter must have one dtype (cast the model first)")
@@ -179,11 +193,20 @@ class FlatFSDP(nn.Module):
             else:
                 u.full = torch.zeros(n, dtype=dtype, device=dev)
                 u.gfull = torch.zeros(n, dtype=dtype, device=dev)
+            if meta:
+                named = self._rebind_meta(module, named, u.full)
             u.flat = FlatParams(None, named=named, pad_to=pad, data=u.full, grad=u.gfull, no_decay_fn=no_decay_fn,
-                                lazy_zero_grad=True)
+                                lazy_zero_grad=True, device=dev)
             u.names = [nm for nm, _p in named]
             u.nbytes = n * u.full.element_size()
-            if self.world > 1:
+            if meta:
+                self._init_shard(module, u, init_seed)  # gathered into ``full`` by the first forward
+                if self.world > 1:
+                    u.fresh = False
+                    if self.reshard and not is_root:
+                        u.full.untyped_storage().resize_(0)
+                        u.released = True
+            elif self.world > 1:
                 if sync_module_states:
                     dist.broadcast(u.full, src=src, group=process_group)
                 with torch.no_grad():
@@ -213,6 +236,78 @@ class FlatFSDP(nn.Module):
                     self._handles.append(p.register_post_accumulate_grad_hook(self._make_grad_hook(u)))
         logger.info(f"FlatFSDP: {len(self.units)} units, {shard_total} elements per rank shard "
                     f"(world {self.world}, reshard_after_forward={self.reshard})")
+
+    # ------------------------------------------------------ meta-device init
+    @staticmethod
+    @torch.no_grad()
+    def _materialize_buffers(module: nn.Module, dev, buffer_init_fn):
+        from ..atorch.meta_init import _init_meta_buffers
+
+        names = []
+        for mname, m in module.named_modules():
+            for bname, b in list(m._buffers.items()):
+                if b is not None and b.is_meta:
+                    m._buffers[bname] = torch.empty_like(b, device=dev)
+                    names.append(f"{mname}.{bname}" if mname else bname)
+                elif b is not None and b.device != dev:
+                    m._buffers[bname] = b.to(dev)
+        if names:
+            _init_meta_buffers(module, names, dev, buffer_init_fn)
+
+    @staticmethod
+    def _rebind_meta(module: nn.Module, named, full: torch.Tensor):
+        """Replace each meta parameter by a Parameter that IS its view of the
+        unit buffer (FlatParams' layout: 64-element aligned, in order); a meta
+        tensor cannot be re-pointed through ``.data``."""
+        owners = {}
+        for m in module.modules():
+            for pname, p in m._parameters.items():
+                if p is not None:
+                    owners.setdefault(id(p), []).append((m, pname))
+        out, off = [], 0
+        for name, p in named:
+            c = p.numel()
+            if p.is_meta:
+                # a fresh parameter re-pointed through .data: its own version
+                # counter (a Parameter built ON the view would share the unit
+                # buffer's, and every in-place gather would invalidate the
+                # autograd-saved weights)
+                newp = nn.Parameter(torch.empty(0, dtype=full.dtype, device=full.device), requires_grad=p.requires_grad)
+                newp.data = full[off:off + c].view(p.shape)
+                for m, pname in owners.get(id(p), []):
+                    m._parameters[pname] = newp
+                p = newp
+            out.append((name, p))
+            off += (c + ALIGN - 1) // ALIGN * ALIGN
+        return out
+
+    @torch.no_grad()
+    def _init_shard(self, module: nn.Module, u: _Unit, seed: int):
+        """This rank's element range of every parameter of ``u``: the values
+        the unsharded parameter would get from ``meta_init``'s streams."""
+        from ..atorch.meta_init import _fill_counter, _module_spec
+
+        owner = {}
+        for mname, m in module.named_modules():
+            for pname, p in m.named_parameters(recurse=False):
+                owner.setdefault(id(p), (m, pname))
+        spec_fn = getattr(module, "init_spec", None)
+        hi = u.lo + u.len
+        for name, p, (o, c) in zip(u.names, u.flat.params, u.flat.offsets):
+            a, b = max(o, u.lo), min(o + c, hi)
+            if a >= b:
+                continue
+            m, pname = owner[id(p)]
+            spec = spec_fn(name) if callable(spec_fn) else None
+            if spec is None:
+                spec = _module_spec(module, m, pname)
+            piece = u.shard[a - u.lo:b - u.lo]
+            if spec is None:
+                logger.warning(f"FlatFSDP meta init: no init spec for {name} ({type(m).__name__}): zeros")
+                piece.zero_()
+                continue
+            lo_, hi_ = (spec[1], spec[2]) if len(spec) >= 3 else (0.0, 0.0)
+            _fill_counter(piece, a - o, name, seed, spec[0], lo_, hi_)
 
     # ------------------------------------------------------------ gathers
     def _issue_gather(self, u: _Unit):

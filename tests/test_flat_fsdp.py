@@ -290,3 +290,60 @@ def test_flat_fsdp_checkpoint_reshards(tmp_path):
     util.load_into_model(plain)
     for n, p in plain.named_parameters():
         assert torch.equal(p, ref["full"][n]), n
+
+
+def _meta_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dlrover_wuqiong_amd.atorch.auto_accelerate import auto_accelerate
+        from dlrover_wuqiong_amd.models.gpt2 import GPT2, Block, GPT2Config
+
+        cfg = GPT2Config.named("gpt2-tiny")
+        with torch.device("meta"):
+            m = GPT2(cfg)
+        ok, res, _s = auto_accelerate(m, torch.optim.AdamW, optim_args={"lr": 1e-3},
+                                      load_strategy=[("flat_fsdp", {"wrap_cls": (Block,)})])
+        model = res.model
+        # nothing of the whole model was built: each rank holds its shard (+ the root unit gathered)
+        layers = [u for u in model.units if not u.is_root]
+        assert all(u.released for u in layers) and model.shard_flat.numel < sum(u.len for u in model.units) * world
+        x = _data(cfg, 1)[0]
+        loss = model(x[:, :-1], x[:, 1:])  # every rank the whole batch: the loss of the unsharded model
+        loss.backward()
+        res.optim.step()
+        sd = model.full_state_dict()
+        if rank == 0:
+            q.put((float(loss), {k: v.float().numpy() for k, v in sd.items()}))
+        else:
+            q.put(None)
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        traceback.print_exc()
+        q.put(repr(e))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_flat_fsdp_meta_init_materialises_per_shard():
+    """A meta-device model: every rank fills only its element ranges from the
+    sharding-invariant streams -- the gathered model equals the unsharded
+    model under meta_init.deterministic_init_, and it trains the same."""
+    from dlrover_wuqiong_amd.atorch.meta_init import deterministic_init_
+    from dlrover_wuqiong_amd.optimizers.fused import FusedAdamW
+    from dlrover_wuqiong_amd.parallel.flat import FlatParams
+
+    (loss, params), = _spawn(_meta_worker, 2)
+    ref, cfg = _gpt2()
+    deterministic_init_(ref, seed=0)
+    flat = FlatParams(ref)
+    opt = FusedAdamW(flat, lr=1e-3)
+    x = _data(cfg, 1)[0]
+    ref_loss = ref(x[:, :-1], x[:, 1:])
+    ref_loss.backward()
+    opt.step()
+    assert float(ref_loss) == pytest.approx(loss, rel=1e-5)
+    for n, p in ref.named_parameters():
+        torch.testing.assert_close(torch.from_numpy(params[n]), p.detach(), rtol=2e-4, atol=2e-4, msg=n)
