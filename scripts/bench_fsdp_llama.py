@@ -44,6 +44,8 @@ def main():
                    help="each FSDP unit's AdamW update from its post-backward reduce-scatter on a side stream "
                         "(optimizers/in_backward.py)")
     p.add_argument("--no-ckpt", action="store_true", help="step time only (no flash checkpoints)")
+    p.add_argument("--meta", action="store_true",
+                   help="build the model on the meta device (with --flat: each rank materialises only its shard)")
     p.add_argument("--flat", action="store_true",
                    help="flat-unit FSDP (auto_accelerate flat_zero2 / flat_fsdp, parallel/flat_fsdp.py: in-place "
                         "collectives, fused optimizer over the rank shard) + flat-shard flash checkpoints")
@@ -82,7 +84,8 @@ def main():
         from dlrover_wuqiong_amd.models.llama import Llama, LlamaConfig, LlamaDecoderLayer
 
         cfg = LlamaConfig.named(a.model)
-        with torch.device(dev):
+        t_build = time.perf_counter()
+        with torch.device("meta" if a.meta else dev):
             model = Llama(cfg)
         layer_cls = LlamaDecoderLayer
     prec = ("amp_native", {"dtype": torch.bfloat16}) if a.precision == "amp" else "half"
@@ -99,6 +102,10 @@ def main():
         fused_optimizer=not a.torch_optim)
     assert ok, "auto_accelerate failed"
     model, opt = res.model, res.optim
+    if cuda:
+        torch.cuda.synchronize()
+    build_s = time.perf_counter() - t_build if not a.model.startswith("gpt2") else None
+    build_peak_gb = round(torch.cuda.max_memory_allocated() / 2**30, 1) if cuda else None
     g = torch.Generator().manual_seed(rank)
     data = torch.randint(0, cfg.vocab_size, (2, a.micro_batch, a.seq + 1), generator=g).to(dev)
     ck = None if a.flat else FsdpShardCheckpointer(a.ckpt_dir)
@@ -135,7 +142,9 @@ def main():
                               "precision": a.precision + ("+fp8" if a.fp8 else ""), "optimizer": type(opt).__name__,
                               "optim_in_backward": getattr(opt, "_in_backward", None) is not None,
                               "act_ckpt": a.act_ckpt, "reshard_after_forward": a.reshard == "on",
-                              "fsdp": "flat" if a.flat else "fsdp2", "train_step_ms": round(1000 * med, 1),
+                              "fsdp": "flat" if a.flat else "fsdp2", "meta_init": a.meta,
+                              "build_s": round(build_s, 2) if build_s else None, "build_peak_gb": build_peak_gb,
+                              "train_step_ms": round(1000 * med, 1),
                               "tokens_per_s": round(world * a.micro_batch * a.seq / med, 1),
                               "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if cuda else None,
                               "step_ms": [round(1000 * x, 1) for x in steps], "losses": [round(x, 3) for x in losses]}))
