@@ -746,12 +746,19 @@ def _apply_flat_fsdp(ctx, cfg, reshard=True):
     if not meta:
         model = model.to(_device())  # the flat buffers are built where the parameters are
     pg = ctx.get("dp_group") if dist.is_initialized() else None
+    rg = None
+    zg = ctx.get("zero_group") if dist.is_initialized() else None
+    if zg is not None and pg is not None and dist.get_world_size(zg) > 1 and dist.get_world_size(pg) > 1:
+        # parallel_mode ("zero", z) x ("data", d): shard within the zero group,
+        # replicate across the data groups (hybrid sharding, as fsdp's 2-D mesh)
+        pg, rg = zg, pg
     # a meta-device model is materialised per shard (sharding-invariant
     # counter-based init, atorch/meta_init.py); init_seed / buffer_init_fn as for fsdp
     ctx["model"] = FlatFSDP(model, wrap_cls=_wrap_cls(ctx, cfg), process_group=pg,
                             reshard_after_forward=cfgd.get("reshard_after_forward", reshard),
                             sync_module_states=cfgd.get("sync_module_states", True), device=_device(),
-                            init_seed=int(cfgd.get("init_seed", 0)), buffer_init_fn=cfgd.get("buffer_init_fn"))
+                            init_seed=int(cfgd.get("init_seed", 0)), buffer_init_fn=cfgd.get("buffer_init_fn"),
+                            replicate_group=rg)
     if meta:
         ctx["meta_init"] = "flat_deterministic"
     ctx["flat_fsdp"] = ctx["model"]

@@ -347,8 +347,15 @@ class ShardTensorUtil:
             op = os.path.join(path, f"optim_param.{s}")
             if os.path.exists(op):
                 self._ofds[r] = safe_open(op, framework="pt")
-        for v in self.param_meta.values():
-            v.sort(key=lambda m: m["offset"])
+        for name, v in list(self.param_meta.items()):
+            # hybrid sharding: replicas saved the same ranges -- keep one of each
+            seen, uniq = set(), []
+            for m in sorted(v, key=lambda m: (m["offset"], m["rank"])):
+                key = (m["offset"], m["length"])
+                if key not in seen:
+                    seen.add(key)
+                    uniq.append(m)
+            self.param_meta[name] = uniq
 
     def _elements(self, fds, key_fn, name, lo: int, hi: int) -> torch.Tensor:
         """Elements [lo, hi) of the FLATTENED tensor ``name`` (1-D), whatever

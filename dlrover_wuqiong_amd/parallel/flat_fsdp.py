@@ -99,7 +99,7 @@ class ShardFlat:
         self.decay_mask = decay_mask
         self.norm_reduce = owner.world > 1  # over norm_group (None: the default group)
         self.norm_group = owner.pg
-        self.grad_scale = 1.0 / owner.world
+        self.grad_scale = 1.0 / (owner.world * owner.replicas)
 
     def finalize_grads(self):
         self._owner.finish_gradient_sync()
@@ -113,7 +113,7 @@ class FlatFSDP(nn.Module):
                  reshard_after_forward: bool = True, prefetch: bool = True,
                  no_decay_fn: Callable[[str, torch.Tensor], bool] = default_no_decay,
                  sync_module_states: bool = True, device=None, init_seed: int = 0,
-                 buffer_init_fn: Optional[Callable] = None):
+                 buffer_init_fn: Optional[Callable] = None, replicate_group=None):
         """A ``module`` built on the meta device (``torch.device("meta")``)
         is materialised per shard: each rank allocates only its shard (and,
         without resharding, the unit buffers it gathers into) on ``device``
@@ -121,7 +121,13 @@ class FlatFSDP(nn.Module):
         invariant counter-based streams of ``atorch/meta_init.py``
         (``init_spec`` of the model, else the module type), so a Llama-3-70B
         job never builds the whole model in fp32 on any rank; meta buffers
-        are rebuilt as ``meta_init`` does (``buffer_init_fn``)."""
+        are rebuilt as ``meta_init`` does (``buffer_init_fn``).
+
+        ``replicate_group`` (hybrid sharding, HSDP): shards live in
+        ``process_group`` (e.g. a node's xGMI group) and are replicated
+        across ``replicate_group``; after the shard group's reduce-scatters
+        one all-reduce of the rank's whole shard gradient sums the replicas
+        (reference ATorch FSDP HYBRID_SHARD, zero_optimization.py:377-394)."""
         super().__init__()
         self.module = module
         self.pg = process_group
@@ -129,6 +135,8 @@ class FlatFSDP(nn.Module):
         self.world = dist.get_world_size(process_group) if init else 1
         self.rank = dist.get_rank(process_group) if init else 0
         self.reshard = bool(reshard_after_forward) and self.world > 1
+        self.rg = replicate_group
+        self.replicas = dist.get_world_size(replicate_group) if (init and replicate_group is not None) else 1
         self.prefetch = bool(prefetch)
         self._sync = True
         params_all = [p for p in module.parameters()]
@@ -206,9 +214,12 @@ class FlatFSDP(nn.Module):
                     if self.reshard and not is_root:
                         u.full.untyped_storage().resize_(0)
                         u.released = True
-            elif self.world > 1:
+            elif self.world > 1 or self.replicas > 1:
                 if sync_module_states:
-                    dist.broadcast(u.full, src=src, group=process_group)
+                    if self.replicas > 1:  # every replica of every shard: global rank 0's values
+                        dist.broadcast(u.full, src=0)
+                    else:
+                        dist.broadcast(u.full, src=src, group=process_group)
                 with torch.no_grad():
                     u.shard.copy_(u.full[u.lo:u.lo + u.len])
                 u.fresh = True
@@ -227,6 +238,10 @@ class FlatFSDP(nn.Module):
         self._inflight: List[_Unit] = []  # reduce-scatters not yet known complete
         self.free_grads = self.reshard
         self._handles = []
+        if self.world == 1 and self.replicas > 1:
+            for u in self.units:
+                for p in u.flat.params:
+                    self._handles.append(p.register_post_accumulate_grad_hook(self._make_count_hook(u)))
         if self.world > 1:
             for u in self.units:
                 if not u.is_root:
@@ -414,6 +429,15 @@ class FlatFSDP(nn.Module):
                 self._reduce(u)
         return hook
 
+    def _make_count_hook(self, u: _Unit):
+        def hook(_p):
+            if self._sync:
+                self._calls[u.idx] += 1
+        return hook
+
+    def _calls_any(self) -> bool:
+        return any(self._calls)
+
     def _reduce(self, u: _Unit):
         self._take_grad(u)  # (a unit whose backward never ran: its gradient is zero)
         u.flat.finalize_grads()  # lazily zeroed gradients nobody wrote
@@ -430,7 +454,12 @@ class FlatFSDP(nn.Module):
         called by the optimizer before its update."""
         for u in self.units:
             u.flat.finalize_grads()
-        if self.world == 1 or not self._sync:
+        if not self._sync or (self.world == 1 and self.replicas == 1):
+            return
+        if self.world == 1:  # replicas of an unsharded model: the gradient all-reduce only
+            if self._calls_any():
+                dist.all_reduce(self._shard_grad, group=self.rg)
+                self._calls = [0] * len(self.units)
             return
         if not any(self._calls):
             return  # no backward since the last sync
@@ -440,6 +469,8 @@ class FlatFSDP(nn.Module):
             if not u.reduced:
                 self._reduce(u)
         self._drain(block=True)
+        if self.replicas > 1:  # sum the replicas' shard gradients: one collective over the shard
+            dist.all_reduce(self._shard_grad, group=self.rg)
         for u in self.units:
             u.reduced = False
         self._calls = [0] * len(self.units)

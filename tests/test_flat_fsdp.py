@@ -347,3 +347,89 @@ def test_flat_fsdp_meta_init_materialises_per_shard():
     assert float(ref_loss) == pytest.approx(loss, rel=1e-5)
     for n, p in ref.named_parameters():
         torch.testing.assert_close(torch.from_numpy(params[n]), p.detach(), rtol=2e-4, atol=2e-4, msg=n)
+
+
+def _hsdp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dlrover_wuqiong_amd.models.gpt2 import Block
+        from dlrover_wuqiong_amd.optimizers.fused import FusedAdamW
+        from dlrover_wuqiong_amd.parallel.flat_fsdp import FlatFSDP
+
+        # shard groups {0,1} {2,3}, replicate groups {0,2} {1,3}
+        shard = [dist.new_group([0, 1]), dist.new_group([2, 3])][rank // 2]
+        rep = [dist.new_group([0, 2]), dist.new_group([1, 3])][rank % 2]
+        m, cfg = _gpt2()
+        model = FlatFSDP(m, wrap_cls=(Block,), process_group=shard, replicate_group=rep, reshard_after_forward=True)
+        opt = FusedAdamW(model.shard_flat, lr=1e-2, weight_decay=0.05, max_grad_norm=0.5)
+        assert opt.grad_scale == 0.25
+        losses = []
+        for x in _data(cfg):
+            xm = x.chunk(world)[rank]
+            loss = model(xm[:, :-1], xm[:, 1:])
+            loss.backward()
+            opt.step()
+            opt.zero_grad()
+            t = loss.detach().clone()
+            dist.all_reduce(t)
+            losses.append(float(t) / world)
+        sd = model.full_state_dict()
+        if rank == 0:
+            q.put((losses, {k: v.float().numpy() for k, v in sd.items()}))
+        else:
+            q.put(None)
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        traceback.print_exc()
+        q.put(repr(e))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_flat_fsdp_hybrid_sharding_matches_one_process():
+    """HSDP: 2 shard groups x 2 replicas (4 gloo ranks) == one process on
+    the whole batch (global-norm clipping over the shard group)."""
+    ref_losses, ref_params = _reference(micro=4)
+    (losses, params), = _spawn(_hsdp_worker, 4)
+    assert losses == pytest.approx(ref_losses, rel=1e-5, abs=1e-5)
+    for n, p in ref_params.items():
+        torch.testing.assert_close(torch.from_numpy(params[n]), p, rtol=2e-4, atol=2e-4, msg=n)
+
+
+def _auto_hsdp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dlrover_wuqiong_amd.atorch.auto_accelerate import auto_accelerate
+        from dlrover_wuqiong_amd.models.gpt2 import Block
+
+        m, cfg = _gpt2()
+        ok, res, _s = auto_accelerate(m, torch.optim.AdamW, optim_args={"lr": 1e-3},
+                                      load_strategy=[("parallel_mode", ([("zero", 2), ("data", 2)], None)),
+                                                     ("flat_fsdp", {"wrap_cls": (Block,)})])
+        assert ok and res.model.world == 2 and res.model.replicas == 2 and res.optim.grad_scale == 0.25
+        x = _data(cfg, 1)[0].chunk(world)[rank]
+        for _ in range(2):
+            loss = res.model(x[:, :-1], x[:, 1:])
+            loss.backward()
+            res.optim.step()
+            res.optim.zero_grad()
+        # replicas hold identical shards
+        shard = res.model.shard_flat.data.clone()
+        peer = shard.clone()
+        dist.broadcast(peer, src=rank % 2, group=res.model.rg)
+        q.put(bool(torch.equal(shard, peer)))
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        traceback.print_exc()
+        q.put(repr(e))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_auto_accelerate_flat_fsdp_hybrid():
+    assert _spawn(_auto_hsdp_worker, 4) == [True] * 4
