@@ -189,6 +189,7 @@ class FlatFSDP(nn.Module):
         self._shard_grad = torch.zeros(shard_total, dtype=dtype, device=dev)
         masks = []
         self.units: List[_Unit] = []
+        self.free_grads = self.reshard
         base = 0
         src = dist.get_global_rank(process_group, 0) if (init and process_group is not None) else 0
         for i, ((m, named, is_root), n) in enumerate(zip(groups, sizes)):
@@ -209,11 +210,7 @@ class FlatFSDP(nn.Module):
             u.nbytes = n * u.full.element_size()
             if meta:
                 self._init_shard(module, u, init_seed)  # gathered into ``full`` by the first forward
-                if self.world > 1:
-                    u.fresh = False
-                    if self.reshard and not is_root:
-                        u.full.untyped_storage().resize_(0)
-                        u.released = True
+                u.fresh = self.world == 1
             elif self.world > 1 or self.replicas > 1:
                 if sync_module_states:
                     if self.replicas > 1:  # every replica of every shard: global rank 0's values
@@ -223,6 +220,14 @@ class FlatFSDP(nn.Module):
                 with torch.no_grad():
                     u.shard.copy_(u.full[u.lo:u.lo + u.len])
                 u.fresh = True
+            if self.reshard and not is_root:
+                # ZeRO-3: neither full-size buffer outlives the set-up of its
+                # unit (the first forward gathers, the first backward takes the
+                # gradient buffer): no rank ever holds two model-sized copies
+                u.full.untyped_storage().resize_(0)
+                u.released, u.fresh = True, False
+                u.gfull.untyped_storage().resize_(0)
+                u.grad_released = True
             masks.append(u.flat.decay_mask[u.lo // ALIGN:(u.lo + u.len) // ALIGN])
             self.units.append(u)
             base += u.len
@@ -236,7 +241,6 @@ class FlatFSDP(nn.Module):
         self._expected: Optional[List[int]] = None
         self._calls = [0] * len(self.units)
         self._inflight: List[_Unit] = []  # reduce-scatters not yet known complete
-        self.free_grads = self.reshard
         self._handles = []
         if self.world == 1 and self.replicas > 1:
             for u in self.units:
