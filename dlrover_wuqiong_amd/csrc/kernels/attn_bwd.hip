@@ -45,6 +45,15 @@
 // (profiles/r4/attn_dkdv64_w3_ab.jsonl).  -DDWAMD_DKDV64_W3=0: the 2-wave form
 #define DWAMD_DKDV64_W3 1
 #endif
+#ifndef DWAMD_DKDV_DMA
+// The D = 64 dK/dV kernel's Q / dO tiles by LDS-DMA (global_load_lds_dwordx4:
+// each wave one 1-KiB 8-row group per tensor and chunk, the T10 swizzle folded
+// into the per-lane source addresses) instead of register staging + ds_write:
+// 168 VGPRs + 2 spills -> 155, GPT2-shape kernel 105.7 -> 101.0 us alone,
+// backward 171-174 -> 169.5-170 us (profiles/r6/attn_dkdv64_dma_ab.jsonl); 0:
+// register staging
+#define DWAMD_DKDV_DMA 1
+#endif
 #ifndef DWAMD_DKDV64_BQT
 #define DWAMD_DKDV64_BQT 64  // A/B: queries per staged tile of the D = 64 dK/dV kernel (32 / 64 / 128)
 #endif
@@ -207,12 +216,33 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
   const int n_it = max(0, (q_end - q_lo + C::BQT - 1) / C::BQT);
   const long long bh = vl.cu_q ? (long long)h : (long long)b * H + h;  // dropout hash row
   const float al2 = EXT ? ext_alibi2(ex, b, h) : 0.f;
-  u32x4 q_st[C::VPT], do_st[C::VPT];
+  constexpr bool DMA = DWAMD_DKDV_DMA && D == 64 && !EXT && C::BQT == 64 && C::WAVES == 4;
+  u32x4 q_st[DMA ? 1 : C::VPT], do_st[DMA ? 1 : C::VPT];
   float lse_st = -INFINITY, del_st = 0.f;  // the tile's LSE / delta (raw)
+  // LDS-DMA of the tile's Q and dO images: lane L of chunk ci writes LDS bytes
+  // 1024 ci + 16 L = img_off(row, ch) with row = 8 ci + (L & 31) / 4 and
+  // ch = 4 (L >> 5) + ((L & 3) ^ ((row >> 2) & 3)); rows past the sequence
+  // read the last row (their LSE is -inf: p = 0, no contribution)
+  auto dma = [&](int it, int buf) {
+    const int q0 = q_lo + it * C::BQT;
+    char* ql = smem + buf * C::BUF;
+    char* dl = ql + C::TILE;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ci = 2 * wid + j;
+      const int row = 8 * ci + ((lane & 31) >> 2);
+      const int ch = 4 * (lane >> 5) + ((lane & 3) ^ ((row >> 2) & 3));
+      const int q = min(q0 + row, SQ - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(Qb + (int64_t)q * st.q_rs + ch * 8), LDS_PTR(ql + 1024 * ci),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(dOb + (int64_t)q * st.do_rs + ch * 8), LDS_PTR(dl + 1024 * ci),
+                                       16, 0, 0);
+    }
+  };
   auto issue = [&](int it) {
     const int q0 = q_lo + it * C::BQT;
 #pragma unroll
-    for (int i = 0; i < C::VPT; ++i) {
+    for (int i = 0; i < (DMA ? 0 : C::VPT); ++i) {
       const int v = tid + 64 * C::WAVES * i;
       int row, c;
       stage_rc<D>(v, row, c);
@@ -239,7 +269,7 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
     char* dl = ql + C::TILE;
     float* stl = (float*)(dl + C::TILE);
 #pragma unroll
-    for (int i = 0; i < C::VPT; ++i) {
+    for (int i = 0; i < (DMA ? 0 : C::VPT); ++i) {
       const int v = tid + 64 * C::WAVES * i;
       int row, c;
       stage_rc<D>(v, row, c);
@@ -254,11 +284,17 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
     }
   };
   if (n_it > 0) {
+    if constexpr (DMA) dma(0, 0);
     issue(0);
     write(0);
-    if (n_it > 1) issue(1);
+    if (!DMA && n_it > 1) issue(1);
   }
+  if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile's DMA landed
   __syncthreads();
+  if (DMA && n_it > 1) {
+    dma(1, 1);
+    issue(1);
+  }
   // per-lane LDS read offsets; the rest of each address is an immediate
   const int rwl[2] = {row_lane<D>(lane, 0), row_lane<D>(lane, 1)};
   const int trl[2] = {tr_lane<D>(lane, 0), tr_lane<D>(lane, 1)};
@@ -391,9 +427,14 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
     }
     if (it + 1 < n_it) {
       write((it + 1) & 1);  // buffer last read in iteration it-1
-      if (it + 2 < n_it) issue(it + 2);
+      if (!DMA && it + 2 < n_it) issue(it + 2);
     }
+    if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile it+1's DMA landed
     __syncthreads();
+    if (DMA && it + 2 < n_it) {  // buffer it & 1 is free: every wave is past this tile
+      dma(it + 2, it & 1);
+      issue(it + 2);
+    }
   }
   if (key >= SK) return;
   // accumulator rows = d: register i of tile dt is d = 32 dt + 8 (i>>2) + 4 hh + (i&3)
