@@ -54,6 +54,9 @@
 // register staging
 #define DWAMD_DKDV_DMA 1
 #endif
+#ifndef DWAMD_DQ_DMA
+#define DWAMD_DQ_DMA 1  // the D = 64 dQ kernel's K / V tiles by LDS-DMA (0: register staging)
+#endif
 #ifndef DWAMD_DKDV64_BQT
 #define DWAMD_DKDV64_BQT 64  // A/B: queries per staged tile of the D = 64 dK/dV kernel (32 / 64 / 128)
 #endif
@@ -627,10 +630,28 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
   if (EXT && ex.bias && q < SQ)
     brow = ex.bias + (int64_t)b * ex.bias_bs + (int64_t)h * ex.bias_hs + (int64_t)q * ex.bias_qs;
 
-  u32x4 kst[C::VPT], vst[C::VPT];
+  // (D = 64: K / V tiles by LDS-DMA, as the dK/dV kernel's Q / dO; keys past
+  // the sequence read the last key -- masked, p = 0)
+  constexpr bool DMA = DWAMD_DQ_DMA && D == 64 && !EXT && C::BK == 64 && C::WAVES == 4;
+  u32x4 kst[DMA ? 1 : C::VPT], vst[DMA ? 1 : C::VPT];
+  auto dma = [&](int t, int buf) {
+    char* kl = smem + buf * 2 * C::TILE;
+    char* vl = kl + C::TILE;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ci = 2 * wid + j;
+      const int row = 8 * ci + ((lane & 31) >> 2);
+      const int ch = 4 * (lane >> 5) + ((lane & 3) ^ ((row >> 2) & 3));
+      const int key = min(t * C::BK + row, SK - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(Kb + (int64_t)key * st.k_rs + ch * 8), LDS_PTR(kl + 1024 * ci),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(Vb + (int64_t)key * st.v_rs + ch * 8), LDS_PTR(vl + 1024 * ci),
+                                       16, 0, 0);
+    }
+  };
   auto issue_load = [&](int t) {
 #pragma unroll
-    for (int i = 0; i < C::VPT; ++i) {
+    for (int i = 0; i < (DMA ? 0 : C::VPT); ++i) {
       const int v = tid + 64 * C::WAVES * i;
       int row, c;
       stage_rc<D>(v, row, c);
@@ -648,7 +669,7 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
     char* kl = smem + buf * 2 * C::TILE;
     char* vl = kl + C::TILE;
 #pragma unroll
-    for (int i = 0; i < C::VPT; ++i) {
+    for (int i = 0; i < (DMA ? 0 : C::VPT); ++i) {
       const int v = tid + 64 * C::WAVES * i;
       int row, c;
       stage_rc<D>(v, row, c);
@@ -656,10 +677,16 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
       *(u32x4*)(vl + img_off<D>(row, c)) = vst[i];
     }
   };
-  issue_load(t_begin);
-  write_lds(0);
-  if (n_run > 1) issue_load(t_begin + 1);
+  if constexpr (DMA) {
+    if (n_run > 0) dma(t_begin, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    issue_load(t_begin);
+    write_lds(0);
+    if (n_run > 1) issue_load(t_begin + 1);
+  }
   __syncthreads();
+  if (DMA && n_run > 1) dma(t_begin + 1, 1);
   const int rwl[2] = {row_lane<D>(lane, 0), row_lane<D>(lane, 1)};
   const int trl[2] = {tr_lane<D>(lane, 0), tr_lane<D>(lane, 1)};
 
@@ -760,11 +787,13 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
       else
         tile(std::false_type{});
     }
-    if (tt + 1 < n_run) {
+    if (!DMA && tt + 1 < n_run) {
       write_lds((tt + 1) & 1);
       if (tt + 2 < n_run) issue_load(t + 2);
     }
+    if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile tt+1 landed
     __syncthreads();
+    if (DMA && tt + 2 < n_run) dma(t + 2, tt & 1);  // buffer tt & 1 is free
   }
   if (q < SQ) {
     bf16_t* dQq = dQ + (int64_t)b * st.dq_bs + (int64_t)h * D + (int64_t)(sr.q_off + q) * st.dq_rs;
