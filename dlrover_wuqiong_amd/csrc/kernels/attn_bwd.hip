@@ -57,6 +57,11 @@
 #ifndef DWAMD_DQ_DMA
 #define DWAMD_DQ_DMA 1  // the D = 64 dQ kernel's K / V tiles by LDS-DMA (0: register staging)
 #endif
+#ifndef DWAMD_DMA128
+// LDS-DMA staging in the D = 128 dK/dV and dQ kernels too: S=4096 GQA causal
+// dK/dV 1320 -> 1226 us, dQ 1031 -> 996 us (profiles/r6/attn_dma128_ab.jsonl)
+#define DWAMD_DMA128 1
+#endif
 #ifndef DWAMD_DKDV64_BQT
 #define DWAMD_DKDV64_BQT 64  // A/B: queries per staged tile of the D = 64 dK/dV kernel (32 / 64 / 128)
 #endif
@@ -219,22 +224,22 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
   const int n_it = max(0, (q_end - q_lo + C::BQT - 1) / C::BQT);
   const long long bh = vl.cu_q ? (long long)h : (long long)b * H + h;  // dropout hash row
   const float al2 = EXT ? ext_alibi2(ex, b, h) : 0.f;
-  constexpr bool DMA = DWAMD_DKDV_DMA && D == 64 && !EXT && C::BQT == 64 && C::WAVES == 4;
+  constexpr bool DMA = DWAMD_DKDV_DMA && (D == 64 || DWAMD_DMA128) && !EXT && !W1 &&
+                       (C::TILE / 1024) % C::WAVES == 0;
+  constexpr int NG = C::TILE / 1024 / C::WAVES;  // 1 KiB DMA chunks per wave per tensor
   u32x4 q_st[DMA ? 1 : C::VPT], do_st[DMA ? 1 : C::VPT];
   float lse_st = -INFINITY, del_st = 0.f;  // the tile's LSE / delta (raw)
-  // LDS-DMA of the tile's Q and dO images: lane L of chunk ci writes LDS bytes
-  // 1024 ci + 16 L = img_off(row, ch) with row = 8 ci + (L & 31) / 4 and
-  // ch = 4 (L >> 5) + ((L & 3) ^ ((row >> 2) & 3)); rows past the sequence
-  // read the last row (their LSE is -inf: p = 0, no contribution)
+  // LDS-DMA of the tile's Q and dO images (attn_common.h dma_rc); rows past
+  // the sequence read the last row (their LSE is -inf: p = 0, no contribution)
   auto dma = [&](int it, int buf) {
     const int q0 = q_lo + it * C::BQT;
     char* ql = smem + buf * C::BUF;
     char* dl = ql + C::TILE;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int ci = 2 * wid + j;
-      const int row = 8 * ci + ((lane & 31) >> 2);
-      const int ch = 4 * (lane >> 5) + ((lane & 3) ^ ((row >> 2) & 3));
+    for (int j = 0; j < NG; ++j) {
+      const int ci = NG * wid + j;
+      int row, ch;
+      dma_rc<D>(ci, lane, row, ch);
       const int q = min(q0 + row, SQ - 1);
       __builtin_amdgcn_global_load_lds((const void*)(Qb + (int64_t)q * st.q_rs + ch * 8), LDS_PTR(ql + 1024 * ci),
                                        16, 0, 0);
@@ -632,16 +637,17 @@ attn_bwd_dq_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, c
 
   // (D = 64: K / V tiles by LDS-DMA, as the dK/dV kernel's Q / dO; keys past
   // the sequence read the last key -- masked, p = 0)
-  constexpr bool DMA = DWAMD_DQ_DMA && D == 64 && !EXT && C::BK == 64 && C::WAVES == 4;
+  constexpr bool DMA = DWAMD_DQ_DMA && (D == 64 || DWAMD_DMA128) && !EXT && (C::TILE / 1024) % C::WAVES == 0;
+  constexpr int NG = C::TILE / 1024 / C::WAVES;  // 1 KiB DMA chunks per wave per tensor
   u32x4 kst[DMA ? 1 : C::VPT], vst[DMA ? 1 : C::VPT];
   auto dma = [&](int t, int buf) {
     char* kl = smem + buf * 2 * C::TILE;
     char* vl = kl + C::TILE;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int ci = 2 * wid + j;
-      const int row = 8 * ci + ((lane & 31) >> 2);
-      const int ch = 4 * (lane >> 5) + ((lane & 3) ^ ((row >> 2) & 3));
+    for (int j = 0; j < NG; ++j) {
+      const int ci = NG * wid + j;
+      int row, ch;
+      dma_rc<D>(ci, lane, row, ch);
       const int key = min(t * C::BK + row, SK - 1);
       __builtin_amdgcn_global_load_lds((const void*)(Kb + (int64_t)key * st.k_rs + ch * 8), LDS_PTR(kl + 1024 * ci),
                                        16, 0, 0);

@@ -63,6 +63,18 @@ __device__ __forceinline__ void stage_rc(int v, int& row, int& c) {
   c = (rest % CG) * 4 + (v & 3);
 }
 
+// LDS-DMA (global_load_lds_dwordx4) into an img_off tile: one wave
+// instruction writes 1 KiB, lane L to LDS byte 1024 ci + 16 L (the
+// instruction's LDS base is wave-uniform), so a chunk ci covers 8 rows x 64
+// columns and the swizzle moves into the per-lane SOURCE address: lane L
+// fetches (row, ch) with img_off<D>(row, ch) == 1024 ci + 16 L
+template <int D>
+__device__ __forceinline__ void dma_rc(int ci, int lane, int& row, int& ch) {
+  constexpr int HALVES = D / 64;  // 1 KiB chunks per 8-row group
+  row = 8 * (ci / HALVES) + ((lane & 31) >> 2);
+  ch = 4 * (2 * (ci % HALVES) + (lane >> 5)) + ((lane & 3) ^ ((row >> 2) & 3));
+}
+
 // Block coordinates of a 1-D launch over nx * ny * nz workgroups (x fastest).
 // Hardware hands consecutive workgroup ids to the 8 XCDs round-robin, and each
 // XCD has a private L2; the remap gives every XCD a contiguous chunk of the

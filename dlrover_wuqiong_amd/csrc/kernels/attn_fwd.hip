@@ -22,8 +22,8 @@
 //  * One LDS image per tile in the "8-row x 32-column subtile" layout of
 //    guide T10 (a): conflict-free for the K row reads (ds_read_b128, A
 //    operand of S^T) and the V transposed reads.
-//  * Register-staged global loads issued one tile ahead (T14 issue-early /
-//    write-late); exp2 with the softmax scale folded into log2(e); causal:
+//  * K/V tiles fetched one tile ahead: D = 64 by LDS-DMA straight into the
+//    image, D = 128 register-staged (T14 issue-early / write-late); exp2 with the softmax scale folded into log2(e); causal:
 //    tiles above a wave's diagonal are skipped by that wave, the longest
 //    query blocks are dispatched first.
 #include "attn_common.h"
@@ -35,6 +35,20 @@
 // break the interleaved MFMA chains: GPT2 shape fwd 65.5 -> 73.1 us, D=128
 // S=4k 649 -> 702 us (profiles/r4/attn_fwd_diag_skip_ab.jsonl)
 #define DWAMD_FWD_DIAG_SKIP 0
+#endif
+
+#ifndef DWAMD_FWD64_BK
+#define DWAMD_FWD64_BK 128  // keys per K/V tile at D = 64 (launch_fwd)
+#endif
+#ifndef DWAMD_FWD_DMA
+// D = 64 K / V tiles by LDS-DMA (0: register staging).  GPT2 shape (B8 S1024
+// H25 causal) kernel 70.3 -> 65.0 us, S=4096 120.9 -> 111.8 us; with DMA the
+// 64-key form drops to 150 VGPRs (3 waves / SIMD) and wins at S <= 2048
+// (63.5 us), the 128-key form at longer S (profiles/r6/attn_fwd64_dma_ab.jsonl)
+#define DWAMD_FWD_DMA 1
+#endif
+#ifndef DWAMD_FWD64_BK64_MAX_S
+#define DWAMD_FWD64_BK64_MAX_S 2048
 #endif
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -152,10 +166,31 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   if (EXT && ex.bias && q0 + r < SQ)
     brow = ex.bias + (int64_t)b * ex.bias_bs + (int64_t)h * ex.bias_hs + (int64_t)(q0 + r) * ex.bias_qs;
 
-  u32x4 kst[C::VPT], vst[C::VPT];
+  // D = 64: K / V tiles go global -> LDS by DMA (global_load_lds_dwordx4: one
+  // wave instruction fills one 8-row x 64-column group of the T10 image, the
+  // swizzle lives in the per-lane source address); no staging registers, no
+  // ds_write.  Keys past the sequence read the last key: masked, p = 0.
+  constexpr bool DMA = DWAMD_FWD_DMA && D == 64 && !EXT && (C::TILE / 1024) % C::WAVES == 0;
+  constexpr int NG = C::TILE / 1024 / C::WAVES;  // 1 KiB DMA chunks per wave per tensor
+  u32x4 kst[DMA ? 1 : C::VPT], vst[DMA ? 1 : C::VPT];
+  auto dma = [&](int t, int buf) {
+    char* kl = smem + buf * 2 * C::TILE;
+    char* vl = kl + C::TILE;
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+      const int ci = NG * wid + j;
+      int row, ch;
+      dma_rc<D>(ci, lane, row, ch);
+      const int key = min(t * C::BK + row, SK - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(Kb + (int64_t)key * st.k_rs + ch * 8), LDS_PTR(kl + 1024 * ci),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(Vb + (int64_t)key * st.v_rs + ch * 8), LDS_PTR(vl + 1024 * ci),
+                                       16, 0, 0);
+    }
+  };
   auto issue_load = [&](int t) {
 #pragma unroll
-    for (int i = 0; i < C::VPT; ++i) {
+    for (int i = 0; i < (DMA ? 0 : C::VPT); ++i) {
       const int v = tid + 64 * C::WAVES * i;
       int row, c;
       stage_rc<D>(v, row, c);
@@ -173,7 +208,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
     char* kl = smem + buf * 2 * C::TILE;
     char* vl = kl + C::TILE;
 #pragma unroll
-    for (int i = 0; i < C::VPT; ++i) {
+    for (int i = 0; i < (DMA ? 0 : C::VPT); ++i) {
       const int v = tid + 64 * C::WAVES * i;
       int row, c;
       stage_rc<D>(v, row, c);
@@ -182,10 +217,16 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
     }
   };
 
-  issue_load(t_begin);
-  write_lds(0);
-  if (n_run > 1) issue_load(t_begin + 1);
+  if constexpr (DMA) {
+    if (n_run > 0) dma(t_begin, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    issue_load(t_begin);
+    write_lds(0);
+    if (n_run > 1) issue_load(t_begin + 1);
+  }
   __syncthreads();
+  if (DMA && n_run > 1) dma(t_begin + 1, 1);
 
   // per-lane LDS read offsets (attn_common.h row_lane / tr_lane); the rest
   // of every read address is a compile-time immediate
@@ -355,11 +396,13 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
         }
       }
     }
-    if (tt + 1 < n_run) {
+    if (!DMA && tt + 1 < n_run) {
       write_lds((tt + 1) & 1);
       if (tt + 2 < n_run) issue_load(t + 2);
     }
+    if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile tt+1 landed
     __syncthreads();
+    if (DMA && tt + 2 < n_run) dma(t + 2, tt & 1);  // buffer tt & 1 is free
   }
 
   // ---- epilogue: O = O^T / l ; lse
@@ -417,9 +460,10 @@ static void launch_fwd(const void* q, const void* k, const void* v, void* o, voi
   // D=64: 128-key tiles -- twice the MFMAs per barrier and per staging pass,
   // 252 VGPRs: +4-8 % over 64-key tiles (GPT2 shape 354 -> 369 TF/s, S=4096
   // 578 -> 626; profiles/r3/attn_fwd64_bk128_ab.jsonl).  D=128 keeps 64 (128
-  // spills).  flags=1 selects the 64-key form for A/B runs.
-  constexpr int BKT = D == 64 ? 128 : 64;
-  if (D == 64 && variant == 1)
+  // spills).  flags=1 selects the 64-key form for A/B runs; with DMA staging
+  // the 64-key form is the faster one up to S = DWAMD_FWD64_BK64_MAX_S.
+  constexpr int BKT = D == 64 ? DWAMD_FWD64_BK : 64;
+  if (D == 64 && (variant == 1 || (DWAMD_FWD_DMA && S <= DWAMD_FWD64_BK64_MAX_S)))
     return causal ? launch_fwd_v<D, true, false, W, 1, 64>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s)
                   : launch_fwd_v<D, false, false, W, 1, 64>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s);
   return causal ? launch_fwd_v<D, true, false, W, 1, BKT>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s)

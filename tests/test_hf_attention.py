@@ -36,7 +36,7 @@ def test_auto_accelerate_module_replace_switches_hf_attention():
                                  load_strategy=["module_replace"])
     m = res.model
     assert m.config._attn_implementation == NAME
-    ids = torch.randint(0, 128, (2, 16))
+    ids = torch.randint(0, 128, (2, 16), device=next(m.parameters()).device)  # (cuda on a GPU box)
     m(input_ids=ids, labels=ids).loss.backward()
 
 
