@@ -47,6 +47,11 @@
 // (63.5 us), the 128-key form at longer S (profiles/r6/attn_fwd64_dma_ab.jsonl)
 #define DWAMD_FWD_DMA 1
 #endif
+#ifndef DWAMD_FWD_DMA128
+// the D = 128 K / V tiles by LDS-DMA too (214 -> 194 VGPRs): GQA S=4096 forward
+// 652 -> 594 us, S=8192 1006 -> 1077 TF/s (profiles/r6/attn_fwd128_dma_ab.jsonl)
+#define DWAMD_FWD_DMA128 1
+#endif
 #ifndef DWAMD_FWD64_BK64_MAX_S
 #define DWAMD_FWD64_BK64_MAX_S 2048
 #endif
@@ -170,7 +175,7 @@ attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, cons
   // wave instruction fills one 8-row x 64-column group of the T10 image, the
   // swizzle lives in the per-lane source address); no staging registers, no
   // ds_write.  Keys past the sequence read the last key: masked, p = 0.
-  constexpr bool DMA = DWAMD_FWD_DMA && D == 64 && !EXT && (C::TILE / 1024) % C::WAVES == 0;
+  constexpr bool DMA = DWAMD_FWD_DMA && (D == 64 || DWAMD_FWD_DMA128) && !EXT && (C::TILE / 1024) % C::WAVES == 0;
   constexpr int NG = C::TILE / 1024 / C::WAVES;  // 1 KiB DMA chunks per wave per tensor
   u32x4 kst[DMA ? 1 : C::VPT], vst[DMA ? 1 : C::VPT];
   auto dma = [&](int t, int buf) {
