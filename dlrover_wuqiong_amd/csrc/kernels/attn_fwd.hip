@@ -47,6 +47,9 @@
 // (63.5 us), the 128-key form at longer S (profiles/r6/attn_fwd64_dma_ab.jsonl)
 #define DWAMD_FWD_DMA 1
 #endif
+#ifndef DWAMD_FWD128_BK
+#define DWAMD_FWD128_BK 64  // A/B: keys per K/V tile at D = 128 (128: same speed, profiles/r6/attn_fwd128_bk128_ab.jsonl)
+#endif
 #ifndef DWAMD_FWD_DMA128
 // the D = 128 K / V tiles by LDS-DMA too (214 -> 194 VGPRs): GQA S=4096 forward
 // 652 -> 594 us, S=8192 1006 -> 1077 TF/s (profiles/r6/attn_fwd128_dma_ab.jsonl)
@@ -467,7 +470,7 @@ static void launch_fwd(const void* q, const void* k, const void* v, void* o, voi
   // 578 -> 626; profiles/r3/attn_fwd64_bk128_ab.jsonl).  D=128 keeps 64 (128
   // spills).  flags=1 selects the 64-key form for A/B runs; with DMA staging
   // the 64-key form is the faster one up to S = DWAMD_FWD64_BK64_MAX_S.
-  constexpr int BKT = D == 64 ? DWAMD_FWD64_BK : 64;
+  constexpr int BKT = D == 64 ? DWAMD_FWD64_BK : DWAMD_FWD128_BK;
   if (D == 64 && (variant == 1 || (DWAMD_FWD_DMA && S <= DWAMD_FWD64_BK64_MAX_S)))
     return causal ? launch_fwd_v<D, true, false, W, 1, 64>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s)
                   : launch_fwd_v<D, false, false, W, 1, 64>(q, k, v, o, lse, B, S, H, HKV, scale_log2, st, vl, none, s);
