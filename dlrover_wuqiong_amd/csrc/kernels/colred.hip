@@ -646,17 +646,27 @@ norm_bwd_part_kernel(
 #ifndef DWAMD_NORM_BWD_PAIR_WAVES
 #define DWAMD_NORM_BWD_PAIR_WAVES 8
 #endif
-template <bool RMS, bool DS>
+// G = 4 (2048 <= H <= 4096, Llama's 4096): the same with a row split over a
+// wave QUAD -- each wave still 2 vectors per lane (1024 columns), two rows
+// in flight per workgroup.  The one-pass kernel it replaces there
+// (norm_bwd_fused_kernel, 8 vectors per lane, float atomics per block)
+// moved ~2.4 TB/s: Llama-3-8B's call (RMSNorm, 4096 x 4096, residual
+// gradient fused) 43.1 -> 32.5 us, 8192 rows 66.7 -> 56.6 us
+// (profiles/r6/norm_bwd_quad_ab.jsonl); 0: the atomic one-pass kernel
+#ifndef DWAMD_NORM_BWD_QUAD
+#define DWAMD_NORM_BWD_QUAD 1
+#endif
+template <bool RMS, bool DS, int G = 2>
 __global__ void __launch_bounds__(64 * DWAMD_NORM_BWD_PAIR_WAVES, 1)
 norm_bwd_pair_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ gamma,
                      const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                      const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx, float* __restrict__ part,
                      int64_t rows, int H) {
-  constexpr int NW = DWAMD_NORM_BWD_PAIR_WAVES, NP = NW / 2;
-  __shared__ float xch[2][NP][2][2];  // [parity][pair][half][sum g, sum g a]
+  constexpr int NW = DWAMD_NORM_BWD_PAIR_WAVES, NP = NW / G;
+  __shared__ float xch[2][NP][G][2];  // [parity][row group][part][sum g, sum g a]
   __shared__ float red[NW][1024];     // per-wave column partials of one array (final reduction)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int pair = wid >> 1, half = wid & 1;
+  const int pair = wid / G, half = wid % G;  // row group, column part
   const int nv = H >> 3;
   float ag[2][8], ab[2][8], ad[2][8];
 #pragma unroll
@@ -712,14 +722,20 @@ norm_bwd_pair_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x
     }
     s1 = wave_sum(s1);
     s2 = wave_sum(s2);
-    float(*xc)[2][2] = xch[it & 1];
+    float(*xc)[G][2] = xch[it & 1];
     if (lane == 0) {
       xc[pair][half][0] = s1;
       xc[pair][half][1] = s2;
     }
     __syncthreads();  // the only barrier of the row step (the slot of step it-1 stays untouched)
-    const float m1 = RMS ? 0.f : (xc[pair][0][0] + xc[pair][1][0]) / (float)H;
-    const float m2 = (xc[pair][0][1] + xc[pair][1][1]) / (float)H;
+    float t1 = 0.f, t2 = 0.f;  // fixed part order
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      t1 += xc[pair][q][0];
+      t2 += xc[pair][q][1];
+    }
+    const float m1 = RMS ? 0.f : t1 / (float)H;
+    const float m2 = t2 / (float)H;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       if (ok && vok[j]) {
@@ -772,7 +788,7 @@ norm_bwd_pair_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x
       const int h = c >> 10, lc = c & 1023;
       float sum = 0.f;
 #pragma unroll
-      for (int p2 = 0; p2 < NP; ++p2) sum += red[2 * p2 + h][lc];
+      for (int p2 = 0; p2 < NP; ++p2) sum += red[G * p2 + h][lc];
       prow[off + c] = sum;
     }
     __syncthreads();
@@ -1000,7 +1016,8 @@ extern "C" int dw_norm_bwd3(const void* dy, const void* x, const void* gamma, co
   const int pw = dsum ? 3 : 2;
   if (dsum_done) *dsum_done = 0;
   static const bool off = getenv_flag("DWAMD_NORM_BWD_PART_OFF");  // A/B switch
-  if (off || !part || !(dgamma || dbeta) || H % 8 != 0 || H >= 2048 || nb * pw * H > part_floats)
+  const bool quad = DWAMD_NORM_BWD_QUAD && H >= 2048 && H <= 4096;
+  if (off || !part || !(dgamma || dbeta) || H % 8 != 0 || (H >= 2048 && !quad) || (!quad && nb * pw * H > part_floats))
     return dw_norm_bwd2(dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, ws, rows, H, rms, out_fp32, accumulate,
                         stream, det);
   hipStream_t s = (hipStream_t)stream;
@@ -1008,21 +1025,32 @@ extern "C" int dw_norm_bwd3(const void* dy, const void* x, const void* gamma, co
     const char* e = getenv("DWAMD_NORM_BWD_PAIR");
     return !(e && e[0] == '0');
   }();
-  if (pair_on && H > 1024 && H < 2048) {
-    constexpr int NP = DWAMD_NORM_BWD_PAIR_WAVES / 2;
+  if ((pair_on && H > 1024 && H < 2048) || quad) {
+    const int NP = DWAMD_NORM_BWD_PAIR_WAVES / (quad ? 4 : 2);
     const int64_t nbp = std::min<int64_t>((rows + NP - 1) / NP, 256);  // one workgroup per CU, resident
+    if (nbp * pw * H > part_floats && quad)
+      return dw_norm_bwd2(dy, x, gamma, mean, rstd, dres, dx, dgamma, dbeta, ws, rows, H, rms, out_fp32, accumulate,
+                          stream, det);
     if (nbp * pw * H <= part_floats) {
-#define NBW(RM, DSV)                                                                                          \
-  hipLaunchKernelGGL((norm_bwd_pair_kernel<RM, DSV>), dim3((unsigned)nbp), dim3(64 * DWAMD_NORM_BWD_PAIR_WAVES), 0, \
-                     s, (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)gamma,                           \
-                     RM ? nullptr : (const float*)mean, (const float*)rstd, (const bf16_t*)dres, (bf16_t*)dx,      \
+#define NBWG(RM, DSV, G)                                                                                          \
+  hipLaunchKernelGGL((norm_bwd_pair_kernel<RM, DSV, G>), dim3((unsigned)nbp), dim3(64 * DWAMD_NORM_BWD_PAIR_WAVES), 0, \
+                     s, (const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)gamma,                               \
+                     RM ? nullptr : (const float*)mean, (const float*)rstd, (const bf16_t*)dres, (bf16_t*)dx,          \
                      (float*)part, rows, H)
+#define NBW(RM, DSV)        \
+  do {                      \
+    if (quad)               \
+      NBWG(RM, DSV, 4);     \
+    else                    \
+      NBWG(RM, DSV, 2);     \
+  } while (0)
       if (rms) {
         if (dsum) NBW(true, true); else NBW(true, false);
       } else {
         if (dsum) NBW(false, true); else NBW(false, false);
       }
 #undef NBW
+#undef NBWG
       if (dsum_done) *dsum_done = dsum ? 1 : 0;
       const int H2 = pw * H;
       const int splits = (int)colsum_f32_splits(nbp);

@@ -63,8 +63,9 @@ def _norm_backward(ctx, dy, dres):
     dsum = direct_grad(fold[1]) if (fold is not None and direct) else None
     if dsum is not None and dsum.dtype != dgamma.dtype:
         dsum = None
-    # small H: one-pass kernel writes per-block fp32 dgamma/dbeta (/dsum) partials here
-    nparts = min(512, (R + 3) // 4) * (3 if dsum is not None else 2) * H if H < 2048 else 0
+    # H <= 4096: the one-pass kernels write per-block fp32 dgamma/dbeta (/dsum)
+    # partials here (2 rows per block-step at H >= 2048)
+    nparts = min(512, (R + 1) // 2) * (3 if dsum is not None else 2) * H if H <= 4096 else 0
     part = torch.empty(nparts, device=x2.device, dtype=torch.float32) if nparts else None
     done = ctypes.c_int(0)
     # flags: bit 0 accumulate dgamma / dbeta (direct storage already holding
