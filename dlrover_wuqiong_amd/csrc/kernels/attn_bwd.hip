@@ -57,6 +57,9 @@
 #ifndef DWAMD_DQ_DMA
 #define DWAMD_DQ_DMA 1  // the D = 64 dQ kernel's K / V tiles by LDS-DMA (0: register staging)
 #endif
+#ifndef DWAMD_DKDV_VDMA
+#define DWAMD_DKDV_VDMA 0  // A/B: the dK/dV kernel's block V image by LDS-DMA
+#endif
 #ifndef DWAMD_DMA128
 // LDS-DMA staging in the D = 128 dK/dV and dQ kernels too: S=4096 GQA causal
 // dK/dV 1320 -> 1226 us, dQ 1031 -> 996 us (profiles/r6/attn_dma128_ab.jsonl)
@@ -181,7 +184,24 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
   // K[key][16 kk + 8 hh .. +7]; the block's V rows live in LDS (B operand of
   // dP, row-read per k-step) -- registers for 2 waves per SIMD.
   char* v_img = smem + 2 * C::BUF;
-  for (int v = tid; v < C::BKB * C::NCH; v += 64 * C::WAVES) {
+  // (VDMA: the V image by LDS-DMA too, drained by the prologue's vmcnt(0);
+  // keys past the sequence read the last key -- only their own, unwritten,
+  // dK / dV rows see it)
+  constexpr bool VDMA = DWAMD_DKDV_VDMA && DWAMD_DKDV_DMA && (D == 64 || DWAMD_DMA128) && !EXT &&
+                        !(DWAMD_DKDV_W1 && D == 128) && (C::VIMG / 1024) % C::WAVES == 0;
+  if constexpr (VDMA) {
+    constexpr int NGV = C::VIMG / 1024 / C::WAVES;
+#pragma unroll
+    for (int j = 0; j < NGV; ++j) {
+      const int ci = NGV * wid + j;
+      int row, ch;
+      dma_rc<D>(ci, lane, row, ch);
+      const int kv = min(kb0 + row, SK - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(Vb + (int64_t)kv * st.v_rs + ch * 8),
+                                       LDS_PTR(v_img + 1024 * ci), 16, 0, 0);
+    }
+  }
+  for (int v = tid; v < (VDMA ? 0 : C::BKB * C::NCH); v += 64 * C::WAVES) {
     int row, c;
     stage_rc<D>(v, row, c);
     const int kv = kb0 + row;
@@ -227,6 +247,7 @@ attn_bwd_dkdv_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
   constexpr bool DMA = DWAMD_DKDV_DMA && (D == 64 || DWAMD_DMA128) && !EXT && !W1 &&
                        (C::TILE / 1024) % C::WAVES == 0;
   constexpr int NG = C::TILE / 1024 / C::WAVES;  // 1 KiB DMA chunks per wave per tensor
+  static_assert(!VDMA || DMA, "the V image's DMA is drained by the tile DMA's prologue wait");
   u32x4 q_st[DMA ? 1 : C::VPT], do_st[DMA ? 1 : C::VPT];
   float lse_st = -INFINITY, del_st = 0.f;  // the tile's LSE / delta (raw)
   // LDS-DMA of the tile's Q and dO images (attn_common.h dma_rc); rows past
