@@ -58,7 +58,9 @@
 #define DWAMD_DQ_DMA 1  // the D = 64 dQ kernel's K / V tiles by LDS-DMA (0: register staging)
 #endif
 #ifndef DWAMD_DKDV_VDMA
-#define DWAMD_DKDV_VDMA 0  // A/B: the dK/dV kernel's block V image by LDS-DMA
+// the dK/dV kernel's block V image by LDS-DMA: GPT2 shape 101.4 -> 99.2 us,
+// D = 128 neutral (profiles/r6/attn_dkdv_vdma_ab.jsonl)
+#define DWAMD_DKDV_VDMA 1
 #endif
 #ifndef DWAMD_DMA128
 // LDS-DMA staging in the D = 128 dK/dV and dQ kernels too: S=4096 GQA causal
